@@ -1,0 +1,186 @@
+"""Evaluate one golden fixture case with the Python oracle (oracle/refsched).
+
+Result format shared with the GPU-path evaluator (tests/gpu_runner.py):
+    {"scores": {node: int}}  |  {"filter": {node: {"code": c, "reasons": [...]}}}  |
+    {"error": message}       |  {"placements": [...]}
+"""
+from oracle.refsched import framework as F
+from oracle.refsched import nodeinfo as NI
+from oracle.refsched import plugins as P
+
+
+def make_plugin(name, args, handle):
+    a = args or {}
+    if name == "NodeResourcesLeastAllocated":
+        return P.LeastAllocated(handle, [tuple(r) for r in a.get("resources", [["cpu", 1], ["memory", 1]])])
+    if name == "NodeResourcesMostAllocated":
+        return P.MostAllocated(handle, [tuple(r) for r in a.get("resources", [["cpu", 1], ["memory", 1]])])
+    if name == "NodeResourcesBalancedAllocation":
+        return P.BalancedAllocation(handle)
+    if name == "NodeResourcesFit":
+        return P.Fit(a.get("ignored", []))
+    if name == "TaintToleration":
+        return P.TaintToleration(handle)
+    if name == "NodeAffinity":
+        return P.NodeAffinity(handle)
+    if name == "NodeUnschedulable":
+        return P.NodeUnschedulable()
+    if name == "NodeName":
+        return P.NodeName()
+    if name == "NodePorts":
+        return P.NodePorts()
+    if name == "ImageLocality":
+        return P.ImageLocality(handle)
+    if name == "NodePreferAvoidPods":
+        return P.NodePreferAvoidPods(handle)
+    if name == "PodTopologySpread":
+        return P.PodTopologySpread(handle, a.get("default_constraints", []))
+    if name == "DefaultPodTopologySpread":
+        return P.DefaultPodTopologySpread(handle)
+    if name == "InterPodAffinity":
+        return P.InterPodAffinity(handle, a.get("hard_pod_affinity_weight", 1))
+    raise KeyError(name)
+
+
+def _handle(c):
+    snap = NI.Snapshot(c["nodes"], c.get("pods", []), order=c.get("order", "given"))
+    return F.Handle(snap, c.get("services", []), c.get("rcs", []), c.get("rss", []), c.get("sss", []))
+
+
+def oracle_eval(c):
+    kind = c["kind"]
+    if kind in ("score", "filter"):
+        h = _handle(c)
+        try:
+            pl = make_plugin(c["plugin"], c.get("args"), h)
+        except ValueError as e:
+            return {"error": str(e)}
+        state = {}
+        pod = c["pod"]
+        if kind == "filter":
+            if hasattr(pl, "prefilter"):
+                st = pl.prefilter(state, pod)
+                if not P.is_success(st):
+                    return {"error": repr(st)}
+            out = {}
+            for ni in h.snapshot.list:
+                st = pl.filter(state, pod, ni)
+                out[NI.name(ni.node)] = {"code": P.code_of(st), "reasons": [] if st is None else st.reasons}
+            return {"filter": out}
+        nodes = [ni.node for ni in h.snapshot.list]
+        names = c.get("filtered") or [NI.name(n) for n in nodes]
+        fnodes = [h.snapshot.get(n).node for n in names]
+        if hasattr(pl, "prescore"):
+            st = pl.prescore(state, pod, fnodes)
+            if not P.is_success(st):
+                return {"error": repr(st)}
+        scores = []
+        for n in names:
+            s, st = pl.score(state, pod, n)
+            if not P.is_success(st):
+                return {"error": repr(st)}
+            scores.append([n, s])
+        if c.get("normalize") and hasattr(pl, "normalize"):
+            st = pl.normalize(state, pod, scores)
+            if not P.is_success(st):
+                return {"error": repr(st)}
+        return {"scores": {n: s for n, s in scores}}
+    if kind == "schedule":
+        prof = profile_from_case(c)
+        res = F.schedule_sequence(c["nodes"], c.get("pods", []), c["schedule_pods"], prof,
+                                  c.get("services", []), c.get("rcs", []), c.get("rss", []), c.get("sss", []))
+        out = []
+        for r in res:
+            if isinstance(r, F.ScheduleError):
+                out.append({"host": None, "error": type(r).__name__})
+            else:
+                out.append({"host": r.host, "totals": {n: s for n, s in r.totals}, "feasible": r.feasible})
+        return {"placements": out}
+    if kind == "select":
+        idx = {n: i for i, (n, _) in enumerate(c["list"])}
+        prof = F.Profile()
+        hosts = set()
+        try:
+            for seq in range(16):
+                hosts.add(F.select_host(c["list"], idx, prof, seq)[0])
+        except F.ScheduleError as e:
+            return {"error": str(e)}
+        return {"hosts": sorted(hosts)}
+    if kind == "num_feasible":
+        gs = F.GenericScheduler(F.Framework(F.Profile(percentage_of_nodes_to_score=c["pct"], filters=[],
+                                                      prefilters=[], prescores=[], scores=[]),
+                                            F.Handle(NI.Snapshot([]))))
+        return {"num": gs.num_feasible_nodes_to_find(c["num_all_nodes"])}
+    if kind == "normalize":
+        scores = [list(x) for x in c["scores"]]
+        P.default_normalize_score(c["max_priority"], c["reverse"], scores)
+        return {"scores": {str(i): s for i, (_, s) in enumerate(scores)}}
+    if kind == "node_tree":
+        return {"order": NI.node_tree_order(c["nodes"])}
+    raise KeyError(kind)
+
+
+def profile_from_case(c):
+    p = c.get("profile") or {}
+    kw = {}
+    for k in ("filters", "prefilters", "prescores"):
+        if k in p:
+            kw[k] = p[k]
+    if "scores" in p:
+        kw["scores"] = [tuple(s) for s in p["scores"]]
+    for k in ("least_resources", "most_resources"):
+        if k in p:
+            kw[k] = [tuple(r) for r in p[k]]
+    for k in ("hard_pod_affinity_weight", "ignored_resources", "pts_default_constraints",
+              "percentage_of_nodes_to_score", "tie_break_mode", "seed"):
+        if k in p:
+            kw[k] = p[k]
+    if p.get("base") == "cluster_autoscaler":
+        return F.cluster_autoscaler_profile(**kw)
+    return F.Profile(**kw)
+
+
+def check(c, got):
+    """Compare a result against the case's expectations; returns a list of mismatches."""
+    bad = []
+    if "expect_error" in c:
+        if "error" not in got or (c["expect_error"] and c["expect_error"] not in got["error"]):
+            bad.append(("error", c["expect_error"], got))
+        return bad
+    if "error" in got:
+        return [("unexpected error", got["error"])]
+    if "expect_scores" in c:
+        for n, s in c["expect_scores"].items():
+            if got["scores"].get(n) != s:
+                bad.append((n, s, got["scores"].get(n)))
+    if "expect_filter" in c:
+        for n, e in c["expect_filter"].items():
+            g = got["filter"].get(n)
+            if g is None or g["code"] != e["code"]:
+                bad.append((n, e, g))
+            elif "reasons" in e and e["reasons"] is not None and sorted(g["reasons"]) != sorted(e["reasons"]):
+                bad.append((n, e, g))
+    if "expect_possible" in c:
+        if not set(got["hosts"]) <= set(c["expect_possible"]):
+            bad.append(("hosts", c["expect_possible"], got["hosts"]))
+    if "expect_num" in c and got.get("num") != c["expect_num"]:
+        bad.append(("num", c["expect_num"], got.get("num")))
+    if "expect_order" in c and got.get("order") != c["expect_order"]:
+        bad.append(("order", c["expect_order"], got.get("order")))
+    if "expect_hosts" in c:
+        for i, allowed in enumerate(c["expect_hosts"]):
+            h = got["placements"][i]["host"]
+            if allowed is None:
+                if h is not None:
+                    bad.append((i, None, h))
+            elif h not in allowed:
+                bad.append((i, allowed, h))
+    if "expect_totals" in c:
+        for i, tot in enumerate(c["expect_totals"]):
+            if tot is None:
+                continue
+            g = got["placements"][i].get("totals", {})
+            for n, s in tot.items():
+                if g.get(n) != s:
+                    bad.append((i, n, s, g.get(n)))
+    return bad
