@@ -1,0 +1,154 @@
+#!/usr/bin/env python3
+"""Benchmark: kube-scheduler's per-pod node-evaluation loop on MI355X.
+
+Default workload = BASELINE.json configs[1]: 5000 nodes / 10,000 pods, NodeResourcesFit +
+LeastAllocated + BalancedAllocation (synthetic cluster).  A step is one batch of
+pods run through the scheduleOne loop (filter -> score -> selectHost -> assume, every pod in queue
+order) on the device-resident snapshot; K steps x pods-per-step = the config's 10,000 pods.
+
+Prints ONE JSON line (rank 0) with pods/s, node-evals/s, the roofline of the dominant kernel
+(k_eval, timed with HIP events on the engine's stream) and the CPU baseline (the C restatement of
+the reference algorithm, oracle/c, timed on this host's cores on a bounded sample).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for p in (ROOT, os.path.join(ROOT, "kubernetes-1_amd")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md chip table)
+BYTES_PER_NODE_EVAL = {"b": 72, "a": 73, "c": 121}  # SURVEY.md 8(d) algorithmic bytes per node-eval
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def make_workload(cfg, n_nodes, n_pods):
+    from kgpu import cluster
+    if cfg == "b":
+        return cluster.fit_least_balanced(n_nodes=n_nodes, n_pods=n_pods)
+    if cfg == "a":
+        nodes, init, pods, prof = cluster.scheduling_basic(n_nodes=n_nodes, n_init=n_nodes, n_pods=n_pods)
+        return nodes, [], init + pods, prof
+    raise SystemExit("config %r not benchmarked yet" % cfg)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="b")
+    ap.add_argument("--nodes", type=int, default=5000)
+    ap.add_argument("--pods-per-step", type=int, default=1000)
+    ap.add_argument("--cpu-sample", type=int, default=400, help="pods timed for the CPU baseline (0: skip)")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    dist_on = world > 1
+    if dist_on:
+        dist.init_process_group("nccl", rank=rank, world_size=world)
+        torch.cuda.set_device(local)
+
+    from kgpu import abi
+    from kgpu.framework import GpuFramework
+
+    B, K, W = args.pods_per_step, args.steps, args.warmup
+    n_pods = B * K
+    t_gen = time.time()
+    nodes, existing, pods, prof = make_workload(args.config, args.nodes, n_pods)
+    fw = GpuFramework(prof, nodes, existing, pods_hint=pods[:16], device=local)
+    q, pc, pnp, errs = fw.compile_pods(pods)
+    assert not errs, errs
+    log("workload: %d nodes, %d pods, compiled in %.1fs" % (len(nodes), len(pods), time.time() - t_gen))
+    eng = fw.engine
+
+    def reset():
+        eng.upload(fw.snap, fw.arrays)
+
+    # warmup (first launches, code object load) on a fresh snapshot, then reset the cluster state
+    for w in range(W):
+        eng.schedule_batch(q[:B], pc, first_seq=0)
+    reset()
+    torch.cuda.synchronize()
+    if dist_on:
+        dist.barrier()
+    stats = abi.Stats()
+    t0 = time.perf_counter()
+    results = []
+    for k in range(K):
+        res, stats = eng.schedule_batch(q[k * B:(k + 1) * B], pc, first_seq=k * B, stats=stats)
+        results.append(res)
+    torch.cuda.synchronize()
+    if dist_on:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist_on:
+        t = torch.tensor([elapsed], device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    res_all = np.concatenate(results)
+    placed = int((res_all["node"] >= 0).sum())
+    pods_per_s = n_pods / elapsed
+
+    # kernel timing pass (separate: per-launch events perturb the timed loop)
+    reset()
+    eng.set_option(abi.OPT_KERNEL_TIMING, 1)
+    kst = abi.Stats()
+    _, kst = eng.schedule_batch(q[:B], pc, first_seq=0, stats=kst)
+    eng.set_option(abi.OPT_KERNEL_TIMING, 0)
+    avg_kernel_s = kst.eval_kernel_ms / 1e3 / max(kst.eval_launches, 1)
+    bpe = BYTES_PER_NODE_EVAL.get(args.config, 72)
+    n_local = fw.snap.n_nodes
+    achieved = n_local * bpe / avg_kernel_s / 1e9
+
+    # CPU baseline: the C restatement with the reference's 16-worker chunked structure
+    cpu = None
+    if rank == 0 and args.cpu_sample > 0:
+        from oracle.cref import RefEngine
+        S = min(args.cpu_sample, n_pods)
+        ref = RefEngine(fw.config, fw.snap, threads=args.cpu_threads)
+        tc = time.perf_counter()
+        rres = ref.schedule(q[:S], pc)
+        tcpu = time.perf_counter() - tc
+        ok = bool(np.array_equal(rres["node"], res_all["node"][:S]))
+        cpu = {"value": round(S / tcpu, 2), "unit": "pods/s", "cores": args.cpu_threads, "kind": "port",
+               "sample": "first %d pods of the same workload on a fresh snapshot (%.1fs); placements %s the GPU's"
+                         % (S, tcpu, "identical to" if ok else "DIFFERENT from")}
+
+    if rank == 0:
+        line = {
+            "metric": "pods scheduled/sec", "value": round(pods_per_s, 2), "unit": "pods/s", "n_gpus": world,
+            "steps": K, "warmup": W, "ms_per_step": round(1e3 * elapsed / K, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "int64", "data": "synthetic",
+            "config": {"workload": "config(%s): %d nodes / %d pods, %s" % (args.config, len(nodes), n_pods,
+                                                                            "+".join(prof.filters + [s for s, _ in prof.scores])),
+                       "nodes": len(nodes), "pods": n_pods, "pods_per_step": B,
+                       "percentage_of_nodes_to_score": 100},
+            "node_evals_per_s": round(pods_per_s * len(nodes), 1),
+            "placed": placed,
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                         "kernel": "k_eval", "avg_kernel_us": round(avg_kernel_s * 1e6, 3),
+                         "bytes_per_launch": n_local * bpe},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if dist_on:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

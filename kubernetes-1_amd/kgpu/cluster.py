@@ -1,0 +1,132 @@
+"""Synthetic clusters for the BASELINE.json configs.
+
+Deterministic: a splitmix64 stream seeded with 0x5CED0001 drives every choice, so the same
+(config, size) always yields the same objects on every host.  Objects are k8s-v1-shaped dicts, as
+the reference's scheduler_perf fabricates them (nodes are API objects only; no kubelets).
+"""
+from . import compile as _c
+
+CLUSTER_SEED = 0x5CED0001
+M64 = (1 << 64) - 1
+GI, MI = 1 << 30, 1 << 20
+ZONE = "topology.kubernetes.io/zone"
+HOSTNAME = "kubernetes.io/hostname"
+
+
+class Rng:
+    def __init__(self, seed=CLUSTER_SEED):
+        self.s = seed & M64
+
+    def next(self):
+        self.s = (self.s + 0x9E3779B97F4A7C15) & M64
+        z = self.s
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M64
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M64
+        return z ^ (z >> 31)
+
+    def below(self, n):
+        return self.next() % n
+
+    def pick(self, seq):
+        return seq[self.below(len(seq))]
+
+    def chance(self, num, den):
+        return self.below(den) < num
+
+
+def node(name, cpu, mem, pods=110, eph=None, labels=None, taints=None):
+    al = {"cpu": str(cpu), "memory": str(mem), "pods": str(pods)}
+    if eph is not None:
+        al["ephemeral-storage"] = str(eph)
+    n = {"metadata": {"name": name}, "spec": {}, "status": {"allocatable": al, "capacity": dict(al)}}
+    if labels:
+        n["metadata"]["labels"] = dict(labels)
+    if taints:
+        n["spec"]["taints"] = list(taints)
+    return n
+
+
+def pod(name, cpu=None, mem=None, ns="default", labels=None, node_name=None, port=None, **spec):
+    req = {}
+    if cpu is not None:
+        req["cpu"] = cpu
+    if mem is not None:
+        req["memory"] = mem
+    c = {"name": "c", "image": "k8s.gcr.io/pause:3.2", "resources": {"requests": req} if req else {}}
+    if port is not None:
+        c["ports"] = [{"containerPort": port}]
+    s = dict(spec)
+    s["containers"] = [c]
+    if node_name is not None:
+        s["nodeName"] = node_name
+    p = {"metadata": {"name": name, "namespace": ns, "uid": "uid-" + name}, "spec": s}
+    if labels:
+        p["metadata"]["labels"] = dict(labels)
+    return p
+
+
+# ----------------------------------------------------------------------------- (a)
+def scheduling_basic(n_nodes=500, n_init=500, n_pods=1000):
+    """scheduler_perf SchedulingBasic (performance-config.yaml:1-13): node-default.yaml nodes,
+    pod-default.yaml pods (100m / 500Mi, containerPort 80 without hostPort), default profile.
+    Init pods are returned unplaced: the caller schedules them first."""
+    nodes = [node("scheduler-perf-%d" % i, "4", "32Gi", 110) for i in range(n_nodes)]
+    init = [pod("init-%d" % i, "100m", "500Mi", port=80) for i in range(n_init)]
+    pods = [pod("pod-%d" % i, "100m", "500Mi", port=80) for i in range(n_pods)]
+    return nodes, init, pods, _c.Profile()
+
+
+# ----------------------------------------------------------------------------- (b)
+def fit_least_balanced(n_nodes=5000, n_pods=10000, seed=CLUSTER_SEED, zones=0):
+    """Config (b): NodeResourcesFit + LeastAllocated + BalancedAllocation."""
+    r = Rng(seed)
+    nodes = []
+    for i in range(n_nodes):
+        labels = {ZONE: "zone%d" % (i % zones), HOSTNAME: "node%d" % i} if zones else None
+        nodes.append(node("node%d" % i, str(r.pick([4, 8, 16, 32, 64])), "%dGi" % r.pick([16, 32, 64, 128, 256]),
+                          110, "100Gi", labels=labels))
+    pods = []
+    for i in range(n_pods):
+        if r.chance(1, 10):
+            pods.append(pod("p%d" % i))
+        else:
+            pods.append(pod("p%d" % i, "%dm" % (100 * (1 + r.below(40))), "%dMi" % (128 * (1 + r.below(64)))))
+    prof = _c.Profile(filters=["NodeResourcesFit"],
+                      scores=[("NodeResourcesBalancedAllocation", 1), ("NodeResourcesLeastAllocated", 1)])
+    return nodes, [], pods, prof
+
+
+# ----------------------------------------------------------------------------- (c)
+def taints_affinity_spread(n_nodes=5000, n_pods=10000, seed=CLUSTER_SEED, n_zones=10, spread=True):
+    """Config (c): taints (10% dedicated=infra:NoSchedule, 20% spot=true:PreferNoSchedule),
+    required NodeAffinity zone In {zone1,zone2,zone3}, PodTopologySpread on zone (DoNotSchedule)
+    and hostname (ScheduleAnyway), default profile."""
+    r = Rng(seed)
+    nodes = []
+    for i in range(n_nodes):
+        taints = []
+        if r.chance(1, 10):
+            taints.append({"key": "dedicated", "value": "infra", "effect": "NoSchedule"})
+        if r.chance(2, 10):
+            taints.append({"key": "spot", "value": "true", "effect": "PreferNoSchedule"})
+        nodes.append(node("node%d" % i, str(r.pick([4, 8, 16, 32, 64])), "%dGi" % r.pick([16, 32, 64, 128, 256]),
+                          110, "100Gi", labels={ZONE: "zone%d" % (i % n_zones), HOSTNAME: "node%d" % i},
+                          taints=taints))
+    pods = []
+    na = {"nodeAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": {"nodeSelectorTerms": [
+        {"matchExpressions": [{"key": ZONE, "operator": "In", "values": ["zone1", "zone2", "zone3"]}]}]}}}
+    for i in range(n_pods):
+        spec = {"affinity": na}
+        if r.chance(1, 2):
+            spec["tolerations"] = [{"key": "dedicated", "operator": "Equal", "value": "infra", "effect": "NoSchedule"}]
+        if spread:
+            sel = {"matchLabels": {"app": "web"}}
+            spec["topologySpreadConstraints"] = [
+                {"maxSkew": 1, "topologyKey": ZONE, "whenUnsatisfiable": "DoNotSchedule", "labelSelector": sel},
+                {"maxSkew": 1, "topologyKey": HOSTNAME, "whenUnsatisfiable": "ScheduleAnyway", "labelSelector": sel}]
+        pods.append(pod("p%d" % i, "%dm" % (100 * (1 + r.below(40))), "%dMi" % (128 * (1 + r.below(64))),
+                        labels={"app": "web"}, **spec))
+    return nodes, [], pods, _c.Profile()
+
+
+CONFIGS = {"a": scheduling_basic, "b": fit_least_balanced, "c": taints_affinity_spread}

@@ -1,0 +1,152 @@
+"""The plugin-side mirror of the reference framework for the GPU path.
+
+`GpuFramework` plays the role of the out-of-tree plugin set the Go shim registers:
+it holds the compiled, device-resident snapshot (cache.UpdateSnapshot), compiles each pod once
+(the PreFilter-time work), and runs the scheduling cycle on libkgpu:
+
+  cycle(pod)      -> per-node filter statuses (RunFilterPlugins + PluginToStatus.Merge,
+                     framework/v1alpha1/framework.go:477-502) and per-plugin raw / normalized
+                     scores (RunScorePlugins, framework.go:579-656) + the selected host
+  schedule(pods)  -> the scheduleOne loop (scheduler.go:509-593) with on-device assume
+
+Status reasons are rebuilt on the host from the device's status word, exactly as the plugins
+format them (file:line at each message).
+"""
+import numpy as np
+
+from . import abi
+from . import api
+from .compile import CompileError, Compiler, Pools
+from .native import Engine
+
+REASON = {
+    "NodeUnschedulable": "node(s) were unschedulable",             # node_unschedulable.go:39
+    "NodeName": "node(s) didn't match the requested hostname",      # node_name.go:38
+    "NodePorts": "node(s) didn't have free ports for the requested pod ports",  # node_ports.go:41
+    "NodeAffinity": "node(s) didn't match node selector",           # node_affinity.go:44
+    "PodTopologySpread": "node(s) didn't match pod topology spread constraints",  # plugin.go:33
+}
+IPA_REASONS = {1: ["node(s) didn't match pod affinity/anti-affinity", "node(s) didn't match pod affinity rules"],
+               2: ["node(s) didn't match pod affinity/anti-affinity", "node(s) didn't match pod anti-affinity rules"],
+               3: ["node(s) didn't match pod affinity/anti-affinity",
+                   "node(s) didn't satisfy existing pods anti-affinity rules"]}
+
+
+class CycleResult:
+    def __init__(self, host, result, statuses, scores):
+        self.host = host            # node name or None
+        self.result = result        # kgpu_result record
+        self.statuses = statuses    # {node: (code, plugin, reasons)} for infeasible nodes
+        self.scores = scores        # {plugin: {node: (raw, normalized)}} over feasible nodes
+
+
+class GpuFramework:
+    def __init__(self, profile, nodes, existing=(), cluster=None, pods_hint=(), device=0, create_engine=True):
+        self.profile = profile
+        self.compiler = Compiler(profile, cluster)
+        self.compiler.register(nodes, existing, pods_hint)
+        self.snap, self.arrays, self.order = self.compiler.compile_snapshot(nodes, existing)
+        self.config = self.compiler.config(device)
+        self.nodes = {api.name_of(n): n for n in nodes}
+        self.filters = [f for f in profile.filters if f in abi.FILTER_IDS]
+        self.seq = 0
+        self.engine = None
+        if create_engine:
+            self.engine = Engine(self.config)
+            self.engine.upload(self.snap, self.arrays)
+
+    # ------------------------------------------------------------------ compile
+    def compile_pods(self, pods):
+        """Returns (queries, pools_ctypes, pools_np, errors) -- errors: {index: message}."""
+        pools = Pools()
+        qs, errors = [], {}
+        for i, p in enumerate(pods):
+            try:
+                qs.append(self.compiler.compile_pod(p, pools))
+            except CompileError as e:
+                errors[i] = str(e)
+                qs.append(np.zeros((), abi.QUERY))
+        pc, pnp = pools.finalize()
+        q = np.array(qs, dtype=abi.QUERY) if qs else np.zeros(0, abi.QUERY)
+        return q, pc, pnp, errors
+
+    # ------------------------------------------------------------------ reasons
+    def reasons(self, pod, node_name, word):
+        pos = word & 0xFF
+        if pos == 0:
+            return None
+        plugin = self.filters[pos - 1]
+        code = (word >> 8) & 3
+        detail = word >> 16
+        if plugin == "NodeResourcesFit":  # fit.go:159-176, 194-267
+            res = api.PodResources(pod)
+            out = []
+            if detail & 1:
+                out.append("Too many pods")
+            for bit, r in ((2, "cpu"), (4, "memory"), (8, "ephemeral-storage")):
+                if detail & bit:
+                    out.append("Insufficient " + r)
+            for i, r in enumerate(res.scalars):
+                if detail & (16 << min(i, 11)):
+                    out.append("Insufficient " + r)
+            return code, plugin, out
+        if plugin == "TaintToleration":  # taint_toleration.go:54-72
+            from .compile import _tolerates
+            tols = api.spec(pod).get("tolerations") or []
+            for t in api.spec(self.nodes[node_name]).get("taints") or []:
+                if t.get("effect") not in ("NoSchedule", "NoExecute"):
+                    continue
+                k, v, e = t.get("key", "") or "", t.get("value", "") or "", t.get("effect")
+                if not any(_tolerates(x, k, v, e) for x in tols):
+                    return code, plugin, ["node(s) had taint {%s: %s}, that the pod didn't tolerate" % (k, v)]
+            return code, plugin, []
+        if plugin == "InterPodAffinity":
+            return code, plugin, list(IPA_REASONS.get(detail, []))
+        return code, plugin, [REASON[plugin]]
+
+    # ------------------------------------------------------------------ cycles
+    def cycle(self, pod, assume=False, seq=None):
+        """One diagnostic scheduling cycle (kgpu_schedule_one)."""
+        q, pc, pnp, errors = self.compile_pods([pod])
+        if errors:
+            raise CompileError(errors[0])
+        s = self.seq if seq is None else seq
+        res, _ = self.engine.schedule_one(q[0], pc, seq=s, assume=assume)
+        self.seq = s + 1
+        n = self.snap.n_nodes
+        words = self.engine.filter_words(n)
+        statuses = {}
+        for i in np.nonzero(words)[0]:
+            nm = self.order[self.snap.node_base + int(i)]
+            statuses[nm] = self.reasons(pod, nm, int(words[i]))
+        scores = {}
+        feas = np.nonzero(words == 0)[0]
+        for name, w in self.profile.scores:
+            raw, norm = self.engine.scores(abi.SCORE_IDS[name], n)
+            scores[name] = {self.order[self.snap.node_base + int(i)]: (int(raw[i]), int(norm[i])) for i in feas}
+        host = self.order[res["node"]] if res["node"] >= 0 else None
+        return CycleResult(host, res, statuses, scores)
+
+    def schedule(self, pods, first_seq=None, stats=None):
+        """scheduleOne loop over pods; returns kgpu_result records (node index -1: FitError,
+        -2: scoring error, -3: compile error)."""
+        q, pc, pnp, errors = self.compile_pods(pods)
+        s0 = self.seq if first_seq is None else first_seq
+        out = np.zeros(len(pods), abi.RESULT)
+        i = 0
+        while i < len(pods):
+            j = i
+            while j < len(pods) and j not in errors:
+                j += 1
+            if j > i:
+                res, stats = self.engine.schedule_batch(q[i:j], pc, first_seq=s0 + i, stats=stats)
+                out[i:j] = res
+            if j < len(pods):
+                out[j]["node"] = -3
+                j += 1
+            i = j
+        self.seq = s0 + len(pods)
+        return out
+
+    def host_of(self, node_index):
+        return self.order[node_index] if node_index >= 0 else None

@@ -1,0 +1,143 @@
+"""ctypes binding of libkgpu.so (include/kgpu.h).  The product path: no fallback.
+
+If the shared library is missing or fails to load, every entry point raises -- there is no CPU
+path behind this module.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import abi
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libkgpu.so")
+_lib = None
+
+EXPORTS = ["kgpu_abi_version", "kgpu_struct_sizes", "kgpu_create", "kgpu_destroy", "kgpu_last_error",
+           "kgpu_upload_snapshot", "kgpu_generation", "kgpu_schedule_one", "kgpu_schedule_batch",
+           "kgpu_get_filter", "kgpu_get_scores", "kgpu_forget_pod", "kgpu_read_nodes", "kgpu_set_option",
+           "kgpu_comm_unique_id", "kgpu_comm_init"]
+
+
+class KgpuError(RuntimeError):
+    def __init__(self, code, msg=""):
+        super().__init__("%s: %s" % (abi.ERRNAMES.get(code, code), msg))
+        self.code = code
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise KgpuError(abi.E_STATE, "libkgpu.so not built (run __graft_entry__.build()): %s" % LIB_PATH)
+    L = C.CDLL(LIB_PATH)
+    vp, i32, i64 = C.c_void_p, C.c_int32, C.c_int64
+    L.kgpu_abi_version.restype = C.c_int
+    L.kgpu_struct_sizes.argtypes = [vp, i32]
+    L.kgpu_create.argtypes = [C.POINTER(abi.Config), C.POINTER(vp)]
+    L.kgpu_destroy.argtypes = [vp]
+    L.kgpu_last_error.argtypes = [vp]
+    L.kgpu_last_error.restype = C.c_char_p
+    L.kgpu_upload_snapshot.argtypes = [vp, C.POINTER(abi.Snapshot), i64]
+    L.kgpu_generation.argtypes = [vp]
+    L.kgpu_generation.restype = i64
+    L.kgpu_schedule_one.argtypes = [vp, vp, C.POINTER(abi.Pools), i64, i32, vp, C.POINTER(i32)]
+    L.kgpu_schedule_batch.argtypes = [vp, vp, i32, C.POINTER(abi.Pools), i64, vp, C.POINTER(abi.Stats)]
+    L.kgpu_get_filter.argtypes = [vp, vp]
+    L.kgpu_get_scores.argtypes = [vp, i32, vp, vp]
+    L.kgpu_forget_pod.argtypes = [vp, i32]
+    L.kgpu_read_nodes.argtypes = [vp, vp, vp, vp, vp, vp, vp]
+    L.kgpu_set_option.argtypes = [vp, i32, i64]
+    L.kgpu_comm_unique_id.argtypes = [vp]
+    L.kgpu_comm_init.argtypes = [vp, i32, i32, vp]
+    if L.kgpu_abi_version() != abi.ABI_VERSION:
+        raise KgpuError(abi.E_STATE, "ABI version mismatch")
+    _lib = L
+    check_layout(L)
+    return L
+
+
+def check_layout(L=None):
+    L = L or lib()
+    out = np.zeros(64, np.int32)
+    m = L.kgpu_struct_sizes(out.ctypes.data, 64)
+    got = [int(x) for x in out[:m]]
+    want = [s for _, s in abi.STRUCT_SIZES]
+    if got != want:
+        bad = [(n, w, g) for (n, w), g in zip(abi.STRUCT_SIZES, got) if w != g]
+        raise KgpuError(abi.E_STATE, "struct layout mismatch (python, C): %r" % bad)
+    return True
+
+
+class Engine:
+    """One libkgpu context: a profile on one GPU holding one device-resident snapshot."""
+
+    def __init__(self, config):
+        L = lib()
+        self._cfg = config
+        h = C.c_void_p()
+        rc = L.kgpu_create(C.byref(config), C.byref(h))
+        if rc != 0:
+            raise KgpuError(rc, "kgpu_create failed")
+        self.h = h
+        self._keep = None
+
+    def _check(self, rc):
+        if rc != 0:
+            msg = lib().kgpu_last_error(self.h)
+            raise KgpuError(rc, msg.decode() if msg else "")
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().kgpu_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def upload(self, snap, arrays, generation=0):
+        self._keep = (snap, arrays)  # the library copies, but keep buffers alive across the call
+        self._check(lib().kgpu_upload_snapshot(self.h, C.byref(snap), generation))
+
+    def set_option(self, opt, value):
+        self._check(lib().kgpu_set_option(self.h, opt, value))
+
+    def schedule_batch(self, queries, pools, first_seq=0, stats=None):
+        q = np.ascontiguousarray(queries, dtype=abi.QUERY)
+        res = np.zeros(len(q), abi.RESULT)
+        st = stats if stats is not None else abi.Stats()
+        self._check(lib().kgpu_schedule_batch(self.h, q.ctypes.data, len(q), C.byref(pools), first_seq,
+                                              res.ctypes.data, C.byref(st)))
+        return res, st
+
+    def schedule_one(self, query, pools, seq=0, assume=True):
+        q = np.ascontiguousarray(np.atleast_1d(query), dtype=abi.QUERY)
+        res = np.zeros(1, abi.RESULT)
+        slot = C.c_int32(-1)
+        self._check(lib().kgpu_schedule_one(self.h, q.ctypes.data, C.byref(pools), seq, 1 if assume else 0,
+                                            res.ctypes.data, C.byref(slot)))
+        return res[0], slot.value
+
+    def filter_words(self, n):
+        out = np.zeros(n, np.uint32)
+        self._check(lib().kgpu_get_filter(self.h, out.ctypes.data))
+        return out
+
+    def scores(self, plugin, n):
+        raw = np.zeros(n, np.int64)
+        norm = np.zeros(n, np.int64)
+        self._check(lib().kgpu_get_scores(self.h, plugin, raw.ctypes.data, norm.ctypes.data))
+        return raw, norm
+
+    def read_nodes(self, n):
+        cols = [np.zeros(n, np.int64) for _ in range(5)] + [np.zeros(n, np.int32)]
+        self._check(lib().kgpu_read_nodes(self.h, *[c.ctypes.data for c in cols]))
+        return dict(zip(["req_cpu", "req_mem", "req_eph", "nz_cpu", "nz_mem", "num_pods"], cols))
+
+    def forget(self, slot):
+        self._check(lib().kgpu_forget_pod(self.h, slot))

@@ -1,0 +1,572 @@
+/*
+ * ORACLE (test infrastructure only) -- C restatement of the kube-scheduler hot path on the
+ * compiled SoA inputs of include/kgpu.h.
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this library;
+ * the product never does.  It follows the reference's control flow, not the GPU kernels':
+ *
+ *   genericScheduler.Schedule        pkg/scheduler/core/generic_scheduler.go:146-209
+ *   findNodesThatPassFilters         generic_scheduler.go:424-495 (parallelize.Until over nodes,
+ *                                    internal/parallelize/parallelism.go:26-43: 16 workers,
+ *                                    chunk = min(sqrt(n), n/16+1))
+ *   RunFilterPlugins                 framework/v1alpha1/framework.go:477-502 (early exit)
+ *   prioritizeNodes/RunScorePlugins  generic_scheduler.go:622-716, framework.go:579-656
+ *   selectHost                       generic_scheduler.go:217-238 (deterministic tie-break key,
+ *                                    oracle/refsched/tiebreak.py)
+ *   assume                           framework/v1alpha1/types.go:456-480
+ *   plugins                          as cited per function below.
+ *
+ * Feasible nodes are collected in Snapshot.List() order (the reference appends through an
+ * atomic counter; DESIGN.md "Determinism contract").  Build: oracle/c/Makefile.
+ */
+#include <math.h>
+#include <pthread.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../include/kgpu.h"
+
+#define MAXN_SCORE 100
+
+typedef struct {
+  kgpu_config cfg;
+  int N, base, total, S, K, TW, PS, nzones;
+  int64_t *alloc_cpu, *alloc_mem, *alloc_eph, *req_cpu, *req_mem, *req_eph, *nz_cpu, *nz_mem;
+  int32_t *alloc_pods, *num_pods;
+  int64_t *alloc_scalar, *req_scalar;
+  uint8_t* unsched;
+  int32_t* label_val;
+  int32_t* value_off;
+  int64_t* value_int;
+  uint8_t* value_int_ok;
+  uint64_t *taint_nosched, *taint_prefer;
+  int32_t* port_count;
+  kgpu_port* ports;
+  int32_t *image_off, *image_id;
+  int64_t* image_score;
+  int32_t *avoid_off, *avoid_id, *zone_id;
+  int threads;
+} ref_state;
+
+static void* dup_bytes(const void* src, size_t bytes) {
+  void* p = malloc(bytes ? bytes : 1);
+  if (src && bytes) memcpy(p, src, bytes);
+  else memset(p, 0, bytes ? bytes : 1);
+  return p;
+}
+
+int kgpu_ref_create(const kgpu_config* cfg, const kgpu_snapshot* s, int threads, ref_state** out) {
+  ref_state* r = (ref_state*)calloc(1, sizeof(ref_state));
+  size_t N = (size_t)s->n_nodes;
+  r->cfg = *cfg;
+  r->N = s->n_nodes;
+  r->base = s->node_base;
+  r->total = s->n_total_nodes > 0 ? s->n_total_nodes : s->n_nodes;
+  r->S = s->n_scalar;
+  r->K = s->n_label_keys;
+  r->TW = s->taint_words > 0 ? s->taint_words : 1;
+  r->PS = s->port_slots > 8 ? s->port_slots : 8;
+  r->nzones = s->n_zones;
+  r->threads = threads > 0 ? threads : 1;
+#define D(f, src, n, T) r->f = (T*)dup_bytes(src, (n) * sizeof(T))
+  D(alloc_cpu, s->alloc_cpu, N, int64_t);
+  D(alloc_mem, s->alloc_mem, N, int64_t);
+  D(alloc_eph, s->alloc_eph, N, int64_t);
+  D(alloc_pods, s->alloc_pods, N, int32_t);
+  D(req_cpu, s->req_cpu, N, int64_t);
+  D(req_mem, s->req_mem, N, int64_t);
+  D(req_eph, s->req_eph, N, int64_t);
+  D(nz_cpu, s->nz_cpu, N, int64_t);
+  D(nz_mem, s->nz_mem, N, int64_t);
+  D(num_pods, s->num_pods, N, int32_t);
+  D(alloc_scalar, s->alloc_scalar, (size_t)r->S * N, int64_t);
+  D(req_scalar, s->req_scalar, (size_t)r->S * N, int64_t);
+  D(unsched, s->unschedulable, N, uint8_t);
+  D(label_val, s->label_val, (size_t)r->K * N, int32_t);
+  D(value_off, s->value_off, (size_t)r->K + 1, int32_t);
+  {
+    size_t nv = (r->K > 0 && s->value_off) ? (size_t)s->value_off[r->K] : 0;
+    D(value_int, s->value_int, nv, int64_t);
+    D(value_int_ok, s->value_int_ok, nv, uint8_t);
+  }
+  D(taint_nosched, s->taint_words > 0 ? s->taint_nosched : NULL, (size_t)r->TW * N, uint64_t);
+  D(taint_prefer, s->taint_words > 0 ? s->taint_prefer : NULL, (size_t)r->TW * N, uint64_t);
+  D(port_count, s->port_count, N, int32_t);
+  r->ports = (kgpu_port*)calloc((size_t)r->PS * N + 1, sizeof(kgpu_port));
+  for (int sl = 0; sl < s->port_slots; ++sl)
+    memcpy(r->ports + (size_t)sl * N, s->ports + (size_t)sl * N, N * sizeof(kgpu_port));
+  D(image_off, s->image_off, N + 1, int32_t);
+  D(image_id, s->image_id, (size_t)s->image_off[N], int32_t);
+  D(image_score, s->image_score, (size_t)s->image_off[N], int64_t);
+  D(avoid_off, s->avoid_off, N + 1, int32_t);
+  D(avoid_id, s->avoid_id, (size_t)s->avoid_off[N], int32_t);
+  D(zone_id, s->zone_id, N, int32_t);
+#undef D
+  *out = r;
+  return 0;
+}
+
+void kgpu_ref_destroy(ref_state* r) {
+  if (!r) return;
+  void* ptrs[] = {r->alloc_cpu, r->alloc_mem, r->alloc_eph, r->req_cpu, r->req_mem, r->req_eph, r->nz_cpu,
+                  r->nz_mem, r->alloc_pods, r->num_pods, r->alloc_scalar, r->req_scalar, r->unsched,
+                  r->label_val, r->value_off, r->value_int, r->value_int_ok, r->taint_nosched, r->taint_prefer,
+                  r->port_count, r->ports, r->image_off, r->image_id, r->image_score, r->avoid_off, r->avoid_id,
+                  r->zone_id};
+  for (size_t i = 0; i < sizeof(ptrs) / sizeof(ptrs[0]); ++i) free(ptrs[i]);
+  free(r);
+}
+
+/* ------------------------------------------------------------------ labels (selector.go:198-242) */
+static int has_val(const kgpu_pools* p, kgpu_range r, int v) {
+  for (int i = 0; i < r.count; ++i)
+    if (p->ints[r.begin + i] == v) return 1;
+  return 0;
+}
+
+static int req_matches_node(const ref_state* r, const kgpu_pools* p, const kgpu_req* q, int n) {
+  int v = q->key >= 0 ? r->label_val[(size_t)q->key * r->N + n] : -1; /* -1: label key absent */
+  switch (q->op) {
+    case KGPU_OP_IN: return v >= 0 && has_val(p, q->vals, v);
+    case KGPU_OP_NOTIN: return v < 0 || !has_val(p, q->vals, v);
+    case KGPU_OP_EXISTS: return v >= 0;
+    case KGPU_OP_DNE: return v < 0;
+    case KGPU_OP_GT:
+    case KGPU_OP_LT: {
+      if (v < 0) return 0;
+      int idx = r->value_off[q->key] + v;
+      if (!r->value_int_ok[idx]) return 0; /* strconv.ParseInt failed */
+      return q->op == KGPU_OP_GT ? r->value_int[idx] > q->imm : r->value_int[idx] < q->imm;
+    }
+  }
+  return 0;
+}
+
+static int selector_matches_node(const ref_state* r, const kgpu_pools* p, kgpu_range reqs, int n) {
+  for (int i = 0; i < reqs.count; ++i)
+    if (!req_matches_node(r, p, &p->reqs[reqs.begin + i], n)) return 0;
+  return 1;
+}
+
+/* plugins/helper/node_affinity.go:28-78 + core/v1/helper/helpers.go:317-346 */
+static int pod_matches_node_selector_and_affinity(const ref_state* r, const kgpu_pools* p, const kgpu_pod_query* q,
+                                                  int n) {
+  if (q->node_selector.count > 0 && !selector_matches_node(r, p, q->node_selector, n)) return 0;
+  if (!(q->flags & KGPU_Q_REQ_NODE_AFFINITY)) return 1;
+  for (int t = 0; t < q->req_terms.count; ++t) {
+    const kgpu_node_term* term = &p->node_terms[q->req_terms.begin + t];
+    if (term->never_match) continue; /* nil/empty term or invalid requirement selects nothing */
+    if (term->reqs.count && !selector_matches_node(r, p, term->reqs, n)) continue;
+    if (term->field_op == KGPU_OP_IN && r->base + n != term->field_node) continue;
+    if (term->field_op == KGPU_OP_NOTIN && r->base + n == term->field_node) continue;
+    return 1;
+  }
+  return 0;
+}
+
+/* ------------------------------------------------------------------ filters */
+static uint32_t filter_fit(const ref_state* r, const kgpu_pools* p, const kgpu_pod_query* q, int n) {
+  /* noderesources/fit.go:194-267 fitsRequest */
+  uint32_t ins = 0;
+  if (r->num_pods[n] + 1 > r->alloc_pods[n]) ins |= 1;
+  if (q->flags & KGPU_Q_FIT_ALL_ZERO) return ins;
+  if (r->alloc_cpu[n] < q->req[0] + r->req_cpu[n]) ins |= 2;
+  if (r->alloc_mem[n] < q->req[1] + r->req_mem[n]) ins |= 4;
+  if (r->alloc_eph[n] < q->req[2] + r->req_eph[n]) ins |= 8;
+  for (int i = 0; i < q->scalars.count; ++i) {
+    const kgpu_scalar_req* s = &p->scalars[q->scalars.begin + i];
+    if (!s->check) continue;
+    int64_t alloc = s->col >= 0 ? r->alloc_scalar[(size_t)s->col * r->N + n] : 0;
+    int64_t used = s->col >= 0 ? r->req_scalar[(size_t)s->col * r->N + n] : 0;
+    if (alloc < s->value + used) ins |= 16u << (i < 11 ? i : 11);
+  }
+  return ins;
+}
+
+static int filter_ports_ok(const ref_state* r, const kgpu_pools* p, const kgpu_pod_query* q, int n) {
+  /* nodeports/node_ports.go:115-123 + HostPortInfo.CheckConflict types.go:726-756 */
+  for (int i = 0; i < q->ports.count; ++i) {
+    const kgpu_port* w = &p->ports[q->ports.begin + i];
+    for (int s = 0; s < r->port_count[n]; ++s) {
+      const kgpu_port* u = &r->ports[(size_t)s * r->N + n];
+      if (u->proto != w->proto || u->port != w->port) continue;
+      if (w->ip == 0 /* 0.0.0.0: any ip */ || u->ip == 0 || u->ip == w->ip) return 0;
+    }
+  }
+  return 1;
+}
+
+static int filter_taints_ok(const ref_state* r, const kgpu_pools* p, const kgpu_pod_query* q, int n) {
+  /* tainttoleration/taint_toleration.go:54-72: any untolerated NoSchedule/NoExecute taint */
+  for (int w = 0; w < r->TW; ++w) {
+    uint64_t tol = w < q->tol_nosched.count ? p->words[q->tol_nosched.begin + w] : 0;
+    if (r->taint_nosched[(size_t)w * r->N + n] & ~tol) return 0;
+  }
+  return 1;
+}
+
+/* RunFilterPlugins with early exit; returns the status word of include/kgpu.h */
+static uint32_t run_filter_plugins(const ref_state* r, const kgpu_pools* p, const kgpu_pod_query* q, int n) {
+  for (int i = 0; i < r->cfg.n_filters; ++i) {
+    uint32_t pos = (uint32_t)(i + 1);
+    switch (r->cfg.filters[i]) {
+      case KGPU_F_NODE_UNSCHEDULABLE:
+        if (r->unsched[n] && !(q->flags & KGPU_Q_TOLERATES_UNSCHEDULABLE)) return pos | (KGPU_CODE_UNRESOLVABLE << 8);
+        break;
+      case KGPU_F_NODE_RESOURCES_FIT: {
+        uint32_t ins = filter_fit(r, p, q, n);
+        if (ins) return pos | (KGPU_CODE_UNSCHEDULABLE << 8) | (ins << 16);
+        break;
+      }
+      case KGPU_F_NODE_NAME:
+        if (q->node_name != -1 && q->node_name != r->base + n) return pos | (KGPU_CODE_UNRESOLVABLE << 8);
+        break;
+      case KGPU_F_NODE_PORTS:
+        if (!filter_ports_ok(r, p, q, n)) return pos | (KGPU_CODE_UNSCHEDULABLE << 8);
+        break;
+      case KGPU_F_NODE_AFFINITY:
+        if (!pod_matches_node_selector_and_affinity(r, p, q, n)) return pos | (KGPU_CODE_UNRESOLVABLE << 8);
+        break;
+      case KGPU_F_TAINT_TOLERATION:
+        if (!filter_taints_ok(r, p, q, n)) return pos | (KGPU_CODE_UNRESOLVABLE << 8);
+        break;
+      default:
+        break; /* PodTopologySpread / InterPodAffinity: not in this build's tier */
+    }
+  }
+  return 0;
+}
+
+/* ------------------------------------------------------------------ scores */
+static int64_t pod_score_scalar(const kgpu_pools* p, const kgpu_pod_query* q, int col) {
+  for (int i = 0; i < q->scalars.count; ++i)
+    if (p->scalars[q->scalars.begin + i].col == col) return p->scalars[q->scalars.begin + i].score_value;
+  return 0;
+}
+
+/* resource_allocation.go:92-113 */
+static void allocatable_requested(const ref_state* r, const kgpu_pools* p, const kgpu_pod_query* q, int res, int n,
+                                  int64_t* alloc, int64_t* req) {
+  if (res == 0) { *alloc = r->alloc_cpu[n]; *req = r->nz_cpu[n] + q->score_req[0]; }
+  else if (res == 1) { *alloc = r->alloc_mem[n]; *req = r->nz_mem[n] + q->score_req[1]; }
+  else if (res == 2) { *alloc = r->alloc_eph[n]; *req = r->req_eph[n] + q->score_req[2]; }
+  else if (res >= 3) {
+    *alloc = r->alloc_scalar[(size_t)(res - 3) * r->N + n];
+    *req = r->req_scalar[(size_t)(res - 3) * r->N + n] + pod_score_scalar(p, q, res - 3);
+  } else { *alloc = 0; *req = 0; }
+}
+
+static int64_t least_requested_score(int64_t requested, int64_t capacity) { /* least_allocated.go:105-117 */
+  if (capacity == 0) return 0;
+  if (requested > capacity) return 0;
+  return ((capacity - requested) * MAXN_SCORE) / capacity;
+}
+
+static int64_t most_requested_score(int64_t requested, int64_t capacity) { /* most_allocated.go:105-117 */
+  if (capacity == 0) return 0;
+  if (requested > capacity) return 0;
+  return (requested * MAXN_SCORE) / capacity;
+}
+
+static int64_t resource_scorer(const ref_state* r, const kgpu_pools* p, const kgpu_pod_query* q, int n, int most) {
+  int64_t node_score = 0, weight_sum = 0;
+  int cnt = most ? r->cfg.n_most : r->cfg.n_least;
+  const kgpu_resource_weight* rw = most ? r->cfg.most : r->cfg.least;
+  for (int i = 0; i < cnt; ++i) {
+    int64_t a, rq;
+    allocatable_requested(r, p, q, rw[i].resource, n, &a, &rq);
+    int64_t s = most ? most_requested_score(rq, a) : least_requested_score(rq, a);
+    node_score += s * rw[i].weight;
+    weight_sum += rw[i].weight;
+  }
+  return weight_sum ? node_score / weight_sum : 0;
+}
+
+static double fraction_of_capacity(int64_t req, int64_t cap) { return cap == 0 ? 1.0 : (double)req / (double)cap; }
+
+static int64_t balanced_score(const ref_state* r, const kgpu_pools* p, const kgpu_pod_query* q, int n) {
+  /* balanced_allocation.go:83-120 */
+  int64_t ca, cr, ma, mr;
+  allocatable_requested(r, p, q, 0, n, &ca, &cr);
+  allocatable_requested(r, p, q, 1, n, &ma, &mr);
+  double cpu = fraction_of_capacity(cr, ca), mem = fraction_of_capacity(mr, ma);
+  if (cpu >= 1 || mem >= 1) return 0;
+  double diff = fabs(cpu - mem);
+  return (int64_t)((1 - diff) * (double)MAXN_SCORE);
+}
+
+static int64_t taint_raw(const ref_state* r, const kgpu_pools* p, const kgpu_pod_query* q, int n) {
+  /* taint_toleration.go:123-136 countIntolerableTaintsPreferNoSchedule */
+  int64_t c = 0;
+  for (int w = 0; w < r->TW; ++w) {
+    uint64_t tol = w < q->tol_prefer.count ? p->words[q->tol_prefer.begin + w] : 0;
+    c += __builtin_popcountll(r->taint_prefer[(size_t)w * r->N + n] & ~tol);
+  }
+  return c;
+}
+
+static int64_t node_affinity_raw(const ref_state* r, const kgpu_pools* p, const kgpu_pod_query* q, int n) {
+  /* node_affinity.go:80-99 */
+  int64_t count = 0;
+  for (int t = 0; t < q->pref_terms.count; ++t) {
+    const kgpu_pref_term* pt = &p->pref_terms[q->pref_terms.begin + t];
+    if (pt->weight == 0 || pt->sel.kind == KGPU_SEL_NOTHING) continue;
+    if (selector_matches_node(r, p, pt->sel.reqs, n)) count += pt->weight;
+  }
+  return count;
+}
+
+static int64_t image_locality(const ref_state* r, const kgpu_pools* p, const kgpu_pod_query* q, int n) {
+  /* image_locality.go:53-101 */
+  const int64_t mb = 1024 * 1024, min_t = 23 * mb, max_c = 1000 * mb;
+  int64_t sum = 0;
+  for (int i = 0; i < q->images.count; ++i) {
+    int id = p->ints[q->images.begin + i];
+    if (id < 0) continue;
+    for (int k = r->image_off[n]; k < r->image_off[n + 1]; ++k)
+      if (r->image_id[k] == id) { sum += r->image_score[k]; break; }
+  }
+  int64_t max_t = max_c * (int64_t)q->n_containers;
+  if (sum < min_t) sum = min_t;
+  else if (sum > max_t) sum = max_t;
+  return (int64_t)MAXN_SCORE * (sum - min_t) / (max_t - min_t);
+}
+
+static int64_t prefer_avoid(const ref_state* r, const kgpu_pod_query* q, int n) {
+  if (q->avoid_id < 0) return MAXN_SCORE;
+  for (int k = r->avoid_off[n]; k < r->avoid_off[n + 1]; ++k)
+    if (r->avoid_id[k] == q->avoid_id) return 0;
+  return MAXN_SCORE;
+}
+
+/* plugins/helper/normalize_score.go:26-54 */
+static void default_normalize(int64_t* s, int n, int reverse) {
+  int64_t mx = 0;
+  for (int i = 0; i < n; ++i) if (s[i] > mx) mx = s[i];
+  if (mx == 0) {
+    if (reverse) for (int i = 0; i < n; ++i) s[i] = MAXN_SCORE;
+    return;
+  }
+  for (int i = 0; i < n; ++i) {
+    int64_t v = MAXN_SCORE * s[i] / mx;
+    s[i] = reverse ? MAXN_SCORE - v : v;
+  }
+}
+
+/* ------------------------------------------------------------------ tie-break (tiebreak.py) */
+static uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  uint64_t z = x;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+static uint64_t tie_key(const kgpu_config* cfg, int64_t seq, int64_t score, uint64_t idx) {
+  const uint64_t M = (1ull << 40) - 1;
+  uint64_t rank;
+  if (cfg->tie_break_mode == 1) {
+    rank = M - idx;
+  } else {
+    uint64_t k = splitmix64(cfg->seed ^ ((uint64_t)seq * 0x9E3779B97F4A7C15ull));
+    uint64_t x = idx & M;
+    x ^= k & M;
+    x = (x * 0xD6E8FEB865ull) & M;
+    x ^= x >> 19;
+    x = (x * 0x94D049BB13ull) & M;
+    x ^= x >> 23;
+    x ^= (k >> 24) & M;
+    rank = x;
+  }
+  return ((uint64_t)score << 40) | rank;
+}
+
+/* ------------------------------------------------------------------ parallelize.Until */
+typedef struct {
+  const ref_state* r;
+  const kgpu_pools* p;
+  const kgpu_pod_query* q;
+  int phase; /* 0 filter, 1 score */
+  int n, chunk;
+  int next;  /* guarded by mu */
+  pthread_mutex_t mu;
+  uint32_t* status;
+  const int* feasible;
+  int nf;
+  int64_t* scores; /* [n_scores][nf] */
+} work_t;
+
+static void process(work_t* w, int i) {
+  const ref_state* r = w->r;
+  if (w->phase == 0) {
+    w->status[i] = run_filter_plugins(r, w->p, w->q, i);
+    return;
+  }
+  int n = w->feasible[i];
+  for (int k = 0; k < r->cfg.n_scores; ++k) {
+    int64_t v = 0;
+    switch (r->cfg.scores[k]) {
+      case KGPU_S_BALANCED_ALLOCATION: v = balanced_score(r, w->p, w->q, n); break;
+      case KGPU_S_LEAST_ALLOCATED: v = resource_scorer(r, w->p, w->q, n, 0); break;
+      case KGPU_S_MOST_ALLOCATED: v = resource_scorer(r, w->p, w->q, n, 1); break;
+      case KGPU_S_IMAGE_LOCALITY: v = image_locality(r, w->p, w->q, n); break;
+      case KGPU_S_NODE_PREFER_AVOID_PODS: v = prefer_avoid(r, w->q, n); break;
+      case KGPU_S_TAINT_TOLERATION: v = taint_raw(r, w->p, w->q, n); break;
+      case KGPU_S_NODE_AFFINITY: v = node_affinity_raw(r, w->p, w->q, n); break;
+      default: v = 0; break; /* PTS / DPTS / IPA raw scores for pods without terms: 0 */
+    }
+    w->scores[(size_t)k * w->nf + i] = v;
+  }
+}
+
+static void* worker(void* arg) {
+  work_t* w = (work_t*)arg;
+  for (;;) {
+    pthread_mutex_lock(&w->mu);
+    int start = w->next;
+    w->next += w->chunk;
+    pthread_mutex_unlock(&w->mu);
+    if (start >= w->n) return NULL;
+    int end = start + w->chunk < w->n ? start + w->chunk : w->n;
+    for (int i = start; i < end; ++i) process(w, i);
+  }
+}
+
+static void parallel_until(work_t* w, int n, int threads) {
+  /* parallelism.go:26-43: chunk = min(floor(sqrt(n)), n/16 + 1) */
+  int chunk = (int)sqrt((double)n);
+  if (n / 16 + 1 < chunk) chunk = n / 16 + 1;
+  if (chunk < 1) chunk = 1;
+  w->n = n;
+  w->chunk = chunk;
+  w->next = 0;
+  if (threads <= 1 || n < 2) {
+    for (int i = 0; i < n; ++i) process(w, i);
+    return;
+  }
+  pthread_t tid[64];
+  int t = threads > 64 ? 64 : threads;
+  for (int i = 0; i < t; ++i) pthread_create(&tid[i], NULL, worker, w);
+  for (int i = 0; i < t; ++i) pthread_join(tid[i], NULL);
+}
+
+/* ------------------------------------------------------------------ assume (types.go:456-480) */
+static void add_pod(ref_state* r, const kgpu_pools* p, const kgpu_pod_query* q, int n) {
+  r->req_cpu[n] += q->req[0];
+  r->req_mem[n] += q->req[1];
+  r->req_eph[n] += q->req[2];
+  for (int i = 0; i < q->scalars.count; ++i) {
+    const kgpu_scalar_req* s = &p->scalars[q->scalars.begin + i];
+    if (s->col >= 0) r->req_scalar[(size_t)s->col * r->N + n] += s->value;
+  }
+  r->nz_cpu[n] += q->nz[0];
+  r->nz_mem[n] += q->nz[1];
+  r->num_pods[n] += 1;
+  for (int i = 0; i < q->ports.count; ++i) {
+    const kgpu_port* w = &p->ports[q->ports.begin + i];
+    int dup = 0;
+    for (int s = 0; s < r->port_count[n]; ++s) {
+      const kgpu_port* u = &r->ports[(size_t)s * r->N + n];
+      if (u->ip == w->ip && u->proto == w->proto && u->port == w->port) dup = 1;
+    }
+    if (!dup && r->port_count[n] < r->PS) r->ports[(size_t)(r->port_count[n]++) * r->N + n] = *w;
+  }
+}
+
+/* One scheduling cycle per query, in order; placements are assumed before the next pod.
+ * status/raw/norm (optional, for the last pod only) receive the per-node diagnostics. */
+int kgpu_ref_schedule(ref_state* r, const kgpu_pod_query* qs, int nq, const kgpu_pools* p, int64_t first_seq,
+                      kgpu_result* out, uint32_t* status_out, int64_t* raw_out, int64_t* norm_out) {
+  int N = r->N;
+  uint32_t* status = (uint32_t*)malloc(sizeof(uint32_t) * (N ? N : 1));
+  int* feasible = (int*)malloc(sizeof(int) * (N ? N : 1));
+  int64_t* scores = (int64_t*)malloc(sizeof(int64_t) * (size_t)(N ? N : 1) * (r->cfg.n_scores ? r->cfg.n_scores : 1));
+  int64_t* totals = (int64_t*)malloc(sizeof(int64_t) * (N ? N : 1));
+  for (int qi = 0; qi < nq; ++qi) {
+    const kgpu_pod_query* q = &qs[qi];
+    work_t w;
+    memset(&w, 0, sizeof(w));
+    pthread_mutex_init(&w.mu, NULL);
+    w.r = r; w.p = p; w.q = q; w.status = status;
+    w.phase = 0;
+    parallel_until(&w, N, r->threads);
+    int nf = 0;
+    for (int i = 0; i < N; ++i) if (status[i] == 0) feasible[nf++] = i;
+    kgpu_result res;
+    memset(&res, 0, sizeof(res));
+    res.feasible = nf;
+    res.evaluated = r->total;
+    res.node = -1;
+    int last = (qi == nq - 1);
+    if (last && status_out) memcpy(status_out, status, sizeof(uint32_t) * N);
+    if (last && raw_out) memset(raw_out, 0, sizeof(int64_t) * KGPU_NUM_SCORES * N);
+    if (last && norm_out) memset(norm_out, 0, sizeof(int64_t) * KGPU_NUM_SCORES * N);
+    if (nf == 1) {
+      res.node = r->base + feasible[0];
+      add_pod(r, p, q, feasible[0]);
+    } else if (nf > 1) {
+      if (q->flags & KGPU_Q_SCORE_ERROR) {
+        res.node = -2;
+      } else {
+        w.phase = 1;
+        w.feasible = feasible;
+        w.nf = nf;
+        w.scores = scores;
+        parallel_until(&w, nf, r->threads);
+        for (int i = 0; i < nf; ++i) totals[i] = 0;
+        for (int k = 0; k < r->cfg.n_scores; ++k) {
+          int64_t* s = scores + (size_t)k * nf;
+          int plugin = r->cfg.scores[k];
+          if (last && raw_out) for (int i = 0; i < nf; ++i) raw_out[(size_t)plugin * N + feasible[i]] = s[i];
+          if (plugin == KGPU_S_TAINT_TOLERATION) default_normalize(s, nf, 1);
+          else if (plugin == KGPU_S_NODE_AFFINITY) default_normalize(s, nf, 0);
+          else if (plugin == KGPU_S_POD_TOPOLOGY_SPREAD) {
+            /* scoring.go:211-257 with no soft constraints: maxScore == 0 -> MaxNodeScore */
+            for (int i = 0; i < nf; ++i) s[i] = MAXN_SCORE;
+          } else if (plugin == KGPU_S_DEFAULT_POD_TOPOLOGY_SPREAD && !(q->flags & KGPU_Q_HAS_TSC)) {
+            /* default_pod_topology_spread.go:116-163 with all counts 0 */
+            const double zw = 2.0 / 3.0;
+            for (int i = 0; i < nf; ++i) {
+              double f = (double)MAXN_SCORE;
+              if (r->zone_id[feasible[i]] >= 0) f = (f * (1.0 - zw)) + (zw * (double)MAXN_SCORE);
+              s[i] = (int64_t)f;
+            }
+          }
+          if (last && norm_out) for (int i = 0; i < nf; ++i) norm_out[(size_t)plugin * N + feasible[i]] = s[i];
+          int64_t wgt = r->cfg.score_weights[k] > 0 ? r->cfg.score_weights[k] : 1;
+          for (int i = 0; i < nf; ++i) totals[i] += s[i] * wgt;
+        }
+        if (r->cfg.n_scores == 0) for (int i = 0; i < nf; ++i) totals[i] = 1;
+        uint64_t best = 0;
+        int bi = -1;
+        for (int i = 0; i < nf; ++i) {
+          uint64_t k = tie_key(&r->cfg, first_seq + qi, totals[i], (uint64_t)(r->base + feasible[i]));
+          if (bi < 0 || k > best) { best = k; bi = i; }
+        }
+        res.node = r->base + feasible[bi];
+        res.scored = 1;
+        res.score = totals[bi];
+        add_pod(r, p, q, feasible[bi]);
+      }
+    }
+    out[qi] = res;
+    pthread_mutex_destroy(&w.mu);
+  }
+  free(status);
+  free(feasible);
+  free(scores);
+  free(totals);
+  return 0;
+}
+
+int kgpu_ref_read_nodes(const ref_state* r, int64_t* req_cpu, int64_t* req_mem, int64_t* req_eph, int64_t* nz_cpu,
+                        int64_t* nz_mem, int32_t* num_pods) {
+  size_t N = (size_t)r->N;
+  if (req_cpu) memcpy(req_cpu, r->req_cpu, 8 * N);
+  if (req_mem) memcpy(req_mem, r->req_mem, 8 * N);
+  if (req_eph) memcpy(req_eph, r->req_eph, 8 * N);
+  if (nz_cpu) memcpy(nz_cpu, r->nz_cpu, 8 * N);
+  if (nz_mem) memcpy(nz_mem, r->nz_mem, 8 * N);
+  if (num_pods) memcpy(num_pods, r->num_pods, 4 * N);
+  return 0;
+}

@@ -1,0 +1,84 @@
+"""Evaluate golden fixture cases through the product's compile step (kgpu.compile) and either
+the C restatement (oracle/c, CPU) or libkgpu.so (GPU).  Same result format as golden_runner."""
+import numpy as np
+
+from kgpu import abi
+from kgpu.compile import Profile
+from kgpu.framework import GpuFramework
+
+TIER1_SCORES = {"NodeResourcesLeastAllocated", "NodeResourcesMostAllocated", "NodeResourcesBalancedAllocation",
+                "TaintToleration", "NodeAffinity", "ImageLocality", "NodePreferAvoidPods"}
+TIER1_FILTERS = {"NodeResourcesFit", "TaintToleration", "NodeAffinity", "NodeUnschedulable", "NodeName",
+                 "NodePorts"}
+
+
+def supported(c):
+    k = c["kind"]
+    if k == "score":
+        return c["plugin"] in TIER1_SCORES
+    if k == "filter":
+        return c["plugin"] in TIER1_FILTERS
+    if k == "schedule":
+        prof = c.get("profile") or {}
+        return all(n in TIER1_SCORES | {"DefaultPodTopologySpread"} for n, _ in prof.get("scores", []))
+    return False
+
+
+def _profile(c):
+    a = c.get("args") or {}
+    if c["kind"] == "score":
+        kw = dict(filters=[], scores=[(c["plugin"], 1)])
+        if c["plugin"] == "NodeResourcesLeastAllocated":
+            kw["least_resources"] = [tuple(r) for r in a.get("resources", [["cpu", 1], ["memory", 1]])]
+        if c["plugin"] == "NodeResourcesMostAllocated":
+            kw["most_resources"] = [tuple(r) for r in a.get("resources", [["cpu", 1], ["memory", 1]])]
+        return Profile(**kw)
+    if c["kind"] == "filter":
+        return Profile(filters=[c["plugin"]], scores=[], ignored_resources=a.get("ignored", []))
+    p = c.get("profile") or {}
+    return Profile(filters=[f for f in p.get("filters", Profile.DEFAULT_FILTERS) if f in abi.FILTER_IDS],
+                   scores=[tuple(s) for s in p.get("scores", Profile.DEFAULT_SCORES)])
+
+
+def soa_eval(c, backend):
+    try:
+        prof = _profile(c)
+    except ValueError as e:
+        return {"error": str(e)}
+    pods = [c["pod"]] if c["kind"] in ("score", "filter") else c["schedule_pods"]
+    fw = GpuFramework(prof, c["nodes"], c.get("pods", []), pods_hint=pods, create_engine=(backend == "gpu"))
+    pod = pods[0]
+    if backend == "gpu":
+        cr = fw.cycle(pod, assume=False)
+        words = {nm: 0 for nm in fw.order}
+        for nm, st in cr.statuses.items():
+            words[nm] = st
+        statuses, scores = cr.statuses, cr.scores
+    else:
+        from oracle.cref import RefEngine
+        q, pc, pnp, errs = fw.compile_pods([pod])
+        ref = RefEngine(fw.config, fw.snap)
+        res, st, raw, norm = ref.schedule(q, pc, diag=True)
+        statuses = {}
+        for i in np.nonzero(st)[0]:
+            nm = fw.order[int(i)]
+            statuses[nm] = fw.reasons(pod, nm, int(st[i]))
+        scores = {}
+        feas = np.nonzero(st == 0)[0]
+        for name, w in prof.scores:
+            sid = abi.SCORE_IDS[name]
+            scores[name] = {fw.order[int(i)]: (int(raw[sid, i]), int(norm[sid, i])) for i in feas}
+    if c["kind"] == "filter":
+        out = {}
+        for nm in fw.order:
+            s = statuses.get(nm)
+            out[nm] = {"code": 0, "reasons": []} if s is None else {"code": s[0], "reasons": s[2]}
+        return {"filter": out}
+    if c["kind"] == "score":
+        sc = scores[c["plugin"]]
+        return {"scores": {nm: (v[1] if c.get("normalize") else v[0]) if c["plugin"] in ("TaintToleration", "NodeAffinity") else v[1] for nm, v in sc.items()}}
+    totals = {}
+    for name, w in prof.scores:
+        for nm, (r, nv) in scores[name].items():
+            totals[nm] = totals.get(nm, 0) + nv * w
+    return {"placements": [{"host": None, "totals": totals}]}
