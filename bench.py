@@ -114,19 +114,28 @@ def main():
     n_local = fw.snap.n_nodes
     achieved = n_local * bpe / avg_kernel_s / 1e9
 
-    # CPU baseline: the C restatement with the reference's 16-worker chunked structure
+    # CPU baseline: the C restatement of the reference algorithm on this host's cores.  Both the
+    # reference's structure (16 workers, chunk = min(sqrt(n), n/16+1)) and a single thread are
+    # timed; the faster one is reported (the stronger baseline).
     cpu = None
     if rank == 0 and args.cpu_sample > 0:
         from oracle.cref import RefEngine
         S = min(args.cpu_sample, n_pods)
-        ref = RefEngine(fw.config, fw.snap, threads=args.cpu_threads)
-        tc = time.perf_counter()
-        rres = ref.schedule(q[:S], pc)
-        tcpu = time.perf_counter() - tc
-        ok = bool(np.array_equal(rres["node"], res_all["node"][:S]))
-        cpu = {"value": round(S / tcpu, 2), "unit": "pods/s", "cores": args.cpu_threads, "kind": "port",
-               "sample": "first %d pods of the same workload on a fresh snapshot (%.1fs); placements %s the GPU's"
-                         % (S, tcpu, "identical to" if ok else "DIFFERENT from")}
+        best = None
+        for th in sorted({1, args.cpu_threads}):
+            ref = RefEngine(fw.config, fw.snap, threads=th)
+            tc = time.perf_counter()
+            rres = ref.schedule(q[:S], pc)
+            tcpu = time.perf_counter() - tc
+            ok = bool(np.array_equal(rres["node"], res_all["node"][:S]))
+            log("cpu baseline: %d thread(s): %.1f pods/s (placements %s)" % (th, S / tcpu, "match" if ok else "DIFFER"))
+            if best is None or S / tcpu > best[0]:
+                best = (S / tcpu, th, tcpu, ok)
+        rate, th, tcpu, ok = best
+        cpu = {"value": round(rate, 2), "unit": "pods/s", "cores": th, "kind": "port",
+               "sample": "C restatement (oracle/c) of the reference algorithm, first %d pods of the same workload "
+                         "on a fresh snapshot, %.2fs at %d thread(s) (faster of 1 and %d); placements %s the GPU's"
+                         % (S, tcpu, th, args.cpu_threads, "identical to" if ok else "DIFFERENT from")}
 
     if rank == 0:
         line = {

@@ -102,14 +102,33 @@ __device__ bool node_affinity_ok(const DevState& st, const kgpu_pod_query& q, in
   return false;
 }
 
+// ---------------------------------------------------------------- node resource row
+// The 72 bytes of NodeInfo.{Allocatable,Requested,NonZeroRequested,len(Pods)} every resource
+// plugin reads, loaded once per node into registers (8-byte coalesced loads per column).
+struct NodeRes {
+  int64_t ac, am, ae;   // Allocatable milliCPU / memory / ephemeral-storage
+  int64_t rc, rm, re;   // Requested
+  int64_t zc, zm;       // NonZeroRequested
+  int32_t ap, np;       // AllowedPodNumber, len(Pods)
+};
+
+__device__ __forceinline__ NodeRes load_res(const DevState& st, int n) {
+  NodeRes r;
+  r.ac = st.alloc_cpu[n]; r.am = st.alloc_mem[n]; r.ae = st.alloc_eph[n];
+  r.rc = st.req_cpu[n]; r.rm = st.req_mem[n]; r.re = st.req_eph[n];
+  r.zc = st.nz_cpu[n]; r.zm = st.nz_mem[n];
+  r.ap = st.alloc_pods[n]; r.np = st.num_pods[n];
+  return r;
+}
+
 // ---------------------------------------------------------------- plugins
-__device__ __forceinline__ uint32_t fit_detail(const DevState& st, const kgpu_pod_query& q, int n) {
+__device__ __forceinline__ uint32_t fit_detail(const DevState& st, const kgpu_pod_query& q, const NodeRes& r, int n) {
   uint32_t d = 0;
-  if (st.num_pods[n] + 1 > st.alloc_pods[n]) d |= 1u;
+  if (r.np + 1 > r.ap) d |= 1u;
   if (q.flags & KGPU_Q_FIT_ALL_ZERO) return d;
-  if (st.alloc_cpu[n] < q.req[0] + st.req_cpu[n]) d |= 2u;
-  if (st.alloc_mem[n] < q.req[1] + st.req_mem[n]) d |= 4u;
-  if (st.alloc_eph[n] < q.req[2] + st.req_eph[n]) d |= 8u;
+  if (r.ac < q.req[0] + r.rc) d |= 2u;
+  if (r.am < q.req[1] + r.rm) d |= 4u;
+  if (r.ae < q.req[2] + r.re) d |= 8u;
   for (int i = 0; i < q.scalars.count; ++i) {
     const kgpu_scalar_req s = st.qp.scalars[q.scalars.begin + i];
     if (!s.check) continue;
@@ -170,12 +189,12 @@ __device__ __forceinline__ int64_t pod_scalar_score(const DevState& st, const kg
 }
 
 // calculateResourceAllocatableRequest (resource_allocation.go:92-113).
-__device__ __forceinline__ void alloc_req(const DevState& st, const kgpu_pod_query& q, int res, int n,
-                                          int64_t& cap, int64_t& req) {
+__device__ __forceinline__ void alloc_req(const DevState& st, const kgpu_pod_query& q, const NodeRes& nr, int res,
+                                          int n, int64_t& cap, int64_t& req) {
   switch (res) {
-    case 0: cap = st.alloc_cpu[n]; req = st.nz_cpu[n] + q.score_req[0]; break;
-    case 1: cap = st.alloc_mem[n]; req = st.nz_mem[n] + q.score_req[1]; break;
-    case 2: cap = st.alloc_eph[n]; req = st.req_eph[n] + q.score_req[2]; break;
+    case 0: cap = nr.ac; req = nr.zc + q.score_req[0]; break;
+    case 1: cap = nr.am; req = nr.zm + q.score_req[1]; break;
+    case 2: cap = nr.ae; req = nr.re + q.score_req[2]; break;
     default:
       if (res >= 3) {
         const int col = res - 3;
@@ -188,22 +207,24 @@ __device__ __forceinline__ void alloc_req(const DevState& st, const kgpu_pod_que
   }
 }
 
-__device__ __forceinline__ int64_t least_score(const DevState& st, const kgpu_pod_query& q, int n) {
+__device__ __forceinline__ int64_t least_score(const DevState& st, const kgpu_pod_query& q, const NodeRes& nr,
+                                               int n) {
   int64_t s = 0;
   for (int i = 0; i < st.n_least; ++i) {
     int64_t cap, req;
-    alloc_req(st, q, st.least[i].resource, n, cap, req);
+    alloc_req(st, q, nr, st.least[i].resource, n, cap, req);
     const int64_t r = (cap == 0 || req > cap) ? 0 : ((cap - req) * 100) / cap;
     s += r * st.least[i].weight;
   }
   return s / st.least_wsum;
 }
 
-__device__ __forceinline__ int64_t most_score(const DevState& st, const kgpu_pod_query& q, int n) {
+__device__ __forceinline__ int64_t most_score(const DevState& st, const kgpu_pod_query& q, const NodeRes& nr,
+                                              int n) {
   int64_t s = 0;
   for (int i = 0; i < st.n_most; ++i) {
     int64_t cap, req;
-    alloc_req(st, q, st.most[i].resource, n, cap, req);
+    alloc_req(st, q, nr, st.most[i].resource, n, cap, req);
     const int64_t r = (cap == 0 || req > cap) ? 0 : (req * 100) / cap;
     s += r * st.most[i].weight;
   }
@@ -211,9 +232,9 @@ __device__ __forceinline__ int64_t most_score(const DevState& st, const kgpu_pod
 }
 
 // balancedResourceScorer (balanced_allocation.go:83-120): IEEE double, no contraction.
-__device__ __forceinline__ int64_t balanced_score(const DevState& st, const kgpu_pod_query& q, int n) {
-  const int64_t cc = st.alloc_cpu[n], cr = st.nz_cpu[n] + q.score_req[0];
-  const int64_t mc = st.alloc_mem[n], mr = st.nz_mem[n] + q.score_req[1];
+__device__ __forceinline__ int64_t balanced_score(const kgpu_pod_query& q, const NodeRes& nr) {
+  const int64_t cc = nr.ac, cr = nr.zc + q.score_req[0];
+  const int64_t mc = nr.am, mr = nr.zm + q.score_req[1];
   const double cf = cc == 0 ? 1.0 : (double)cr / (double)cc;
   const double mf = mc == 0 ? 1.0 : (double)mr / (double)mc;
   if (cf >= 1.0 || mf >= 1.0) return 0;
@@ -265,7 +286,8 @@ struct NodeEval {
   int32_t na;       // raw NodeAffinity score
 };
 
-__device__ __forceinline__ uint32_t run_filters(const DevState& st, const kgpu_pod_query& q, int n) {
+__device__ __forceinline__ uint32_t run_filters(const DevState& st, const kgpu_pod_query& q, const NodeRes& r,
+                                                int n) {
   for (int i = 0; i < st.n_filters; ++i) {
     const int f = st.filters[i];
     const uint32_t pos = (uint32_t)(i + 1);
@@ -275,7 +297,7 @@ __device__ __forceinline__ uint32_t run_filters(const DevState& st, const kgpu_p
           return pos | (KGPU_CODE_UNRESOLVABLE << 8);
         break;
       case KGPU_F_NODE_RESOURCES_FIT: {
-        const uint32_t d = fit_detail(st, q, n);
+        const uint32_t d = fit_detail(st, q, r, n);
         if (d) return pos | (KGPU_CODE_UNSCHEDULABLE << 8) | (d << 16);
         break;
       }
@@ -298,16 +320,16 @@ __device__ __forceinline__ uint32_t run_filters(const DevState& st, const kgpu_p
   return 0;
 }
 
-__device__ __forceinline__ void run_scores(const DevState& st, const kgpu_pod_query& q, int n, NodeEval& e,
-                                           bool diag) {
+__device__ __forceinline__ void run_scores(const DevState& st, const kgpu_pod_query& q, const NodeRes& r, int n,
+                                           NodeEval& e, bool diag) {
   int64_t part = 0;
   for (int i = 0; i < st.n_scores; ++i) {
     const int s = st.scores[i];
     int64_t v = 0;
     switch (s) {
-      case KGPU_S_BALANCED_ALLOCATION: v = balanced_score(st, q, n); break;
-      case KGPU_S_LEAST_ALLOCATED: v = least_score(st, q, n); break;
-      case KGPU_S_MOST_ALLOCATED: v = most_score(st, q, n); break;
+      case KGPU_S_BALANCED_ALLOCATION: v = balanced_score(q, r); break;
+      case KGPU_S_LEAST_ALLOCATED: v = least_score(st, q, r, n); break;
+      case KGPU_S_MOST_ALLOCATED: v = most_score(st, q, r, n); break;
       case KGPU_S_IMAGE_LOCALITY: v = image_score(st, q, n); break;
       case KGPU_S_NODE_PREFER_AVOID_PODS: v = npap_score(st, q, n); break;
       case KGPU_S_POD_TOPOLOGY_SPREAD: v = 100; break;           // no soft constraints: max == 0
@@ -378,30 +400,71 @@ struct Winner {
   int feasible;
 };
 
-// Reduce the BlkKey partials of a finished launch (every thread of the workgroup participates).
-__device__ Winner reduce_keys(const BlkKey* kb, int nb) {
-  __shared__ uint64_t s_key[kBlock / 64];
-  __shared__ int s_idx[kBlock / 64];
-  __shared__ int s_feas[kBlock / 64];
+// selectHost over the partials of a finished launch, computed by every wave on its own (lanes
+// stride over the <= kMaxBlocks partials, then a 64-lane shuffle reduction): no LDS, no barrier.
+__device__ __forceinline__ Winner wave_winner(const BlkKey* kb, int nb) {
   uint64_t k = 0;
   int idx = -1, f = 0;
-  for (int b = threadIdx.x; b < nb; b += kBlock) {
+  for (int b = threadIdx.x & 63; b < nb; b += 64) {
     const BlkKey p = kb[b];
     key_max(k, idx, p.key, p.idx);
     f += p.feasible;
   }
   wave_reduce_key(k, idx);
   f = wave_reduce_sum(f);
-  const int w = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) { s_key[w] = k; s_idx[w] = idx; s_feas[w] = f; }
-  __syncthreads();
-  Winner out{0, -1, 0};
-  for (int i = 0; i < kBlock / 64; ++i) {
-    key_max(out.key, out.idx, s_key[i], s_idx[i]);
-    out.feasible += s_feas[i];
+  return Winner{k, idx, f};
+}
+
+// NodeInfo.AddPod on the chosen row (types.go:456-480): applied by the thread that owns the row,
+// on its register copy (written back) plus the rarely used scalar and host-port columns.
+__device__ void assume_row(const DevState& st, const kgpu_pod_query& q, NodeRes& r, int n) {
+  r.rc += q.req[0];
+  r.rm += q.req[1];
+  r.re += q.req[2];
+  r.zc += q.nz[0];
+  r.zm += q.nz[1];
+  r.np += 1;
+  st.req_cpu[n] = r.rc;
+  st.req_mem[n] = r.rm;
+  st.req_eph[n] = r.re;
+  st.nz_cpu[n] = r.zc;
+  st.nz_mem[n] = r.zm;
+  st.num_pods[n] = r.np;
+  for (int i = 0; i < q.scalars.count; ++i) {
+    const kgpu_scalar_req s = st.qp.scalars[q.scalars.begin + i];
+    if (s.col >= 0) st.req_scalar[(size_t)s.col * st.N + n] += s.value;
   }
-  __syncthreads();
-  return out;
+  if (q.ports.count) {
+    int pc = st.port_count[n];
+    for (int i = 0; i < q.ports.count && pc < st.PS; ++i) {
+      const kgpu_port w = st.qp.ports[q.ports.begin + i];
+      bool dup = false;
+      for (int s = 0; s < pc; ++s) {
+        const kgpu_port p = st.ports[(size_t)s * st.N + n];
+        if (p.ip == w.ip && p.proto == w.proto && p.port == w.port) dup = true;
+      }
+      if (!dup) st.ports[(size_t)(pc++) * st.N + n] = w;
+    }
+    st.port_count[n] = pc;
+  }
+}
+
+// The pending pod's outcome (generic_scheduler.go:171-208): FitError, the len==1 shortcut, or
+// the scored winner.  placed_idx = local row to assume (-1 none).
+__device__ __forceinline__ int settle_prev(const DevState& st, const PodArgs& a, const Winner& w) {
+  const kgpu_pod_query& q = st.queries[a.prev];
+  const bool error = (q.flags & KGPU_Q_SCORE_ERROR) && w.feasible >= 2;
+  const bool placed = w.feasible > 0 && !error;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    kgpu_result r;
+    r.node = placed ? st.node_base + w.idx : (error ? -2 : -1);
+    r.feasible = w.feasible;
+    r.evaluated = st.n_total;
+    r.scored = (placed && w.feasible >= 2) ? 1 : 0;
+    r.score = r.scored ? (int64_t)(w.key >> 40) : 0;
+    st.results[a.prev] = r;
+  }
+  return (placed && a.assume) ? w.idx : -1;
 }
 
 __device__ __forceinline__ void chunk_of(int N, int& lo, int& hi) {
@@ -410,75 +473,46 @@ __device__ __forceinline__ void chunk_of(int N, int& lo, int& hi) {
   hi = min(N, lo + per);
 }
 
-// NodeInfo.AddPod on the chosen row (types.go:456-480) -- single writer thread.
-__device__ void assume_row(const DevState& st, const kgpu_pod_query& q, int n) {
-  st.req_cpu[n] += q.req[0];
-  st.req_mem[n] += q.req[1];
-  st.req_eph[n] += q.req[2];
-  for (int i = 0; i < q.scalars.count; ++i) {
-    const kgpu_scalar_req s = st.qp.scalars[q.scalars.begin + i];
-    if (s.col >= 0) st.req_scalar[(size_t)s.col * st.N + n] += s.value;
-  }
-  st.nz_cpu[n] += q.nz[0];
-  st.nz_mem[n] += q.nz[1];
-  st.num_pods[n] += 1;
-  int pc = st.port_count[n];
-  for (int i = 0; i < q.ports.count && pc < st.PS; ++i) {
-    const kgpu_port w = st.qp.ports[q.ports.begin + i];
-    bool dup = false;
-    for (int s = 0; s < pc; ++s) {
-      const kgpu_port p = st.ports[(size_t)s * st.N + n];
-      if (p.ip == w.ip && p.proto == w.proto && p.port == w.port) dup = true;
-    }
-    if (!dup) st.ports[(size_t)(pc++) * st.N + n] = w;
-  }
-  st.port_count[n] = pc;
-}
-
-// Resolve the pending pod: selectHost over the previous launch's partials, write its result and
-// (in the owning workgroup) apply the assume.  Must be called by all threads of the workgroup.
-__device__ void resolve_prev(const DevState& st, const PodArgs& a, int lo, int hi) {
-  const Winner w = reduce_keys(st.kbuf + (size_t)a.prev_parity * kMaxBlocks, a.prev_blocks);
-  const kgpu_pod_query& q = st.queries[a.prev];
-  const bool error = (q.flags & KGPU_Q_SCORE_ERROR) && w.feasible >= 2;
-  const bool placed = w.feasible > 0 && !error;
-  if (threadIdx.x == 0) {
-    if (placed && a.assume && w.idx >= lo && w.idx < hi) assume_row(st, q, w.idx);
-    if (blockIdx.x == 0) {
-      kgpu_result r;
-      r.node = placed ? st.node_base + w.idx : (error ? -2 : -1);
-      r.feasible = w.feasible;
-      r.evaluated = st.n_total;
-      r.scored = (placed && w.feasible >= 2) ? 1 : 0;
-      r.score = r.scored ? (int64_t)(w.key >> 40) : 0;
-      st.results[a.prev] = r;
-    }
-  }
-  __syncthreads();
-}
-
 // ---------------------------------------------------------------- kernels
 __global__ __launch_bounds__(kBlock) void k_eval(DevState st, PodArgs a) {
   int lo, hi;
   chunk_of(st.N, lo, hi);
-  if (a.prev >= 0) resolve_prev(st, a, lo, hi);
-  if (a.pod < 0) return;
+  const int n0 = lo + threadIdx.x;
+  // independent loads first: this thread's first node row and the pod query overlap the
+  // previous pod's winner reduction
+  NodeRes r0{};
+  if (n0 < hi) r0 = load_res(st, n0);
+  int assume_idx = -1;
+  if (a.prev >= 0) {
+    const Winner w = wave_winner(st.kbuf + (size_t)a.prev_parity * kMaxBlocks, a.prev_blocks);
+    assume_idx = settle_prev(st, a, w);
+  }
+  if (a.pod < 0) {
+    if (assume_idx >= 0 && assume_idx >= lo && assume_idx < hi && ((assume_idx - lo) % kBlock) == (int)threadIdx.x) {
+      NodeRes r = load_res(st, assume_idx);
+      assume_row(st, st.queries[a.prev], r, assume_idx);
+    }
+    return;
+  }
   const kgpu_pod_query q = st.queries[a.pod];
   const uint64_t tk = pod_tie_key(st.seed, a.seq);
   const bool write_nodes = a.norm || a.diag;
 
   uint64_t best = 0;
   int best_i = -1, feas = 0, maxT = 0, maxNA = 0;
-  for (int n = lo + threadIdx.x; n < hi; n += kBlock) {
+  for (int n = n0; n < hi; n += kBlock) {
+    NodeRes r = (n == n0) ? r0 : load_res(st, n);
+    if (n == assume_idx) assume_row(st, st.queries[a.prev], r, n);
     NodeEval e{0, 0, 0, 0};
-    e.status = run_filters(st, q, n);
+    e.status = run_filters(st, q, r, n);
     if (e.status == 0) {
-      run_scores(st, q, n, e, a.diag);
+      run_scores(st, q, r, n, e, a.diag);
       ++feas;
       maxT = max(maxT, e.taint);
       maxNA = max(maxNA, e.na);
       if (!a.norm) {
-        const int64_t total = st.n_scores ? e.partial : 1;
+        // constant DefaultNormalizeScore maxima: every raw TaintToleration / NodeAffinity score is 0
+        const int64_t total = st.n_scores ? norm_total(st, e.partial, e.taint, e.na, 0, 0) : 1;
         const uint64_t key = ((uint64_t)total << 40) | rank40(tk, (uint64_t)(st.node_base + n), st.tie_mode);
         key_max(best, best_i, key, n);
       }
@@ -490,7 +524,7 @@ __global__ __launch_bounds__(kBlock) void k_eval(DevState st, PodArgs a) {
       st.raw_na[n] = e.na;
     }
   }
-  // workgroup reduction: wave64 shuffles, then 4 wave leaders through LDS
+  // workgroup reduction: wave64 shuffles, then the 4 wave leaders through LDS
   __shared__ uint64_t s_key[kBlock / 64];
   __shared__ int s_idx[kBlock / 64], s_f[kBlock / 64], s_t[kBlock / 64], s_na[kBlock / 64];
   wave_reduce_key(best, best_i);
@@ -581,7 +615,12 @@ __global__ __launch_bounds__(kBlock) void k_final(DevState st, PodArgs a, int st
 __global__ __launch_bounds__(kBlock) void k_resolve(DevState st, PodArgs a) {
   int lo, hi;
   chunk_of(st.N, lo, hi);
-  resolve_prev(st, a, lo, hi);
+  const Winner w = wave_winner(st.kbuf + (size_t)a.prev_parity * kMaxBlocks, a.prev_blocks);
+  const int idx = settle_prev(st, a, w);
+  if (idx >= lo && idx < hi && ((idx - lo) % kBlock) == (int)threadIdx.x) {
+    NodeRes r = load_res(st, idx);
+    assume_row(st, st.queries[a.prev], r, idx);
+  }
 }
 
 int eval_blocks(int N) {

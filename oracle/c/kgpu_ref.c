@@ -29,6 +29,9 @@
 
 #define MAXN_SCORE 100
 
+typedef struct pool_s pool_t;
+static void pool_free(pool_t* p);
+
 typedef struct {
   kgpu_config cfg;
   int N, base, total, S, K, TW, PS, nzones;
@@ -47,6 +50,7 @@ typedef struct {
   int64_t* image_score;
   int32_t *avoid_off, *avoid_id, *zone_id;
   int threads;
+  void* pool;
 } ref_state;
 
 static void* dup_bytes(const void* src, size_t bytes) {
@@ -69,6 +73,7 @@ int kgpu_ref_create(const kgpu_config* cfg, const kgpu_snapshot* s, int threads,
   r->PS = s->port_slots > 8 ? s->port_slots : 8;
   r->nzones = s->n_zones;
   r->threads = threads > 0 ? threads : 1;
+  r->pool = NULL;
 #define D(f, src, n, T) r->f = (T*)dup_bytes(src, (n) * sizeof(T))
   D(alloc_cpu, s->alloc_cpu, N, int64_t);
   D(alloc_mem, s->alloc_mem, N, int64_t);
@@ -115,6 +120,7 @@ void kgpu_ref_destroy(ref_state* r) {
                   r->port_count, r->ports, r->image_off, r->image_id, r->image_score, r->avoid_off, r->avoid_id,
                   r->zone_id};
   for (size_t i = 0; i < sizeof(ptrs) / sizeof(ptrs[0]); ++i) free(ptrs[i]);
+  pool_free((pool_t*)r->pool);
   free(r);
 }
 
@@ -419,35 +425,88 @@ static void process(work_t* w, int i) {
   }
 }
 
-static void* worker(void* arg) {
-  work_t* w = (work_t*)arg;
+/* A persistent pool of (threads - 1) workers plus the calling thread: Go's ParallelizeUntil
+ * starts goroutines per call at negligible cost; creating OS threads per call would not be a
+ * faithful baseline, so the workers are created once and woken per parallel section. */
+struct pool_s {
+  pthread_mutex_t mu;
+  pthread_cond_t go, done;
+  int nthreads, gen, busy, quit;
+  work_t* job;
+  pthread_t tid[64];
+};
+
+static void run_chunks(work_t* w) {
   for (;;) {
     pthread_mutex_lock(&w->mu);
     int start = w->next;
     w->next += w->chunk;
     pthread_mutex_unlock(&w->mu);
-    if (start >= w->n) return NULL;
+    if (start >= w->n) return;
     int end = start + w->chunk < w->n ? start + w->chunk : w->n;
     for (int i = start; i < end; ++i) process(w, i);
   }
 }
 
-static void parallel_until(work_t* w, int n, int threads) {
-  /* parallelism.go:26-43: chunk = min(floor(sqrt(n)), n/16 + 1) */
+static void* pool_worker(void* arg) {
+  pool_t* p = (pool_t*)arg;
+  int seen = 0;
+  for (;;) {
+    pthread_mutex_lock(&p->mu);
+    while (p->gen == seen && !p->quit) pthread_cond_wait(&p->go, &p->mu);
+    if (p->quit) { pthread_mutex_unlock(&p->mu); return NULL; }
+    seen = p->gen;
+    work_t* w = p->job;
+    pthread_mutex_unlock(&p->mu);
+    run_chunks(w);
+    pthread_mutex_lock(&p->mu);
+    if (--p->busy == 0) pthread_cond_signal(&p->done);
+    pthread_mutex_unlock(&p->mu);
+  }
+}
+
+static pool_t* pool_new(int threads) {
+  pool_t* p = (pool_t*)calloc(1, sizeof(pool_t));
+  pthread_mutex_init(&p->mu, NULL);
+  pthread_cond_init(&p->go, NULL);
+  pthread_cond_init(&p->done, NULL);
+  p->nthreads = threads > 64 ? 64 : threads;
+  for (int i = 0; i < p->nthreads - 1; ++i) pthread_create(&p->tid[i], NULL, pool_worker, p);
+  return p;
+}
+
+static void pool_free(pool_t* p) {
+  if (!p) return;
+  pthread_mutex_lock(&p->mu);
+  p->quit = 1;
+  pthread_cond_broadcast(&p->go);
+  pthread_mutex_unlock(&p->mu);
+  for (int i = 0; i < p->nthreads - 1; ++i) pthread_join(p->tid[i], NULL);
+  free(p);
+}
+
+static void parallel_until(pool_t* pool, work_t* w, int n) {
+  /* parallelism.go:26-43: 16 workers, chunk = min(floor(sqrt(n)), n/16 + 1) */
   int chunk = (int)sqrt((double)n);
   if (n / 16 + 1 < chunk) chunk = n / 16 + 1;
   if (chunk < 1) chunk = 1;
   w->n = n;
   w->chunk = chunk;
   w->next = 0;
-  if (threads <= 1 || n < 2) {
+  if (!pool || pool->nthreads <= 1 || n < 2) {
     for (int i = 0; i < n; ++i) process(w, i);
     return;
   }
-  pthread_t tid[64];
-  int t = threads > 64 ? 64 : threads;
-  for (int i = 0; i < t; ++i) pthread_create(&tid[i], NULL, worker, w);
-  for (int i = 0; i < t; ++i) pthread_join(tid[i], NULL);
+  pthread_mutex_lock(&pool->mu);
+  pool->job = w;
+  pool->busy = pool->nthreads - 1;
+  pool->gen++;
+  pthread_cond_broadcast(&pool->go);
+  pthread_mutex_unlock(&pool->mu);
+  run_chunks(w);
+  pthread_mutex_lock(&pool->mu);
+  while (pool->busy > 0) pthread_cond_wait(&pool->done, &pool->mu);
+  pthread_mutex_unlock(&pool->mu);
 }
 
 /* ------------------------------------------------------------------ assume (types.go:456-480) */
@@ -478,6 +537,7 @@ static void add_pod(ref_state* r, const kgpu_pools* p, const kgpu_pod_query* q, 
 int kgpu_ref_schedule(ref_state* r, const kgpu_pod_query* qs, int nq, const kgpu_pools* p, int64_t first_seq,
                       kgpu_result* out, uint32_t* status_out, int64_t* raw_out, int64_t* norm_out) {
   int N = r->N;
+  if (!r->pool && r->threads > 1) r->pool = pool_new(r->threads);
   uint32_t* status = (uint32_t*)malloc(sizeof(uint32_t) * (N ? N : 1));
   int* feasible = (int*)malloc(sizeof(int) * (N ? N : 1));
   int64_t* scores = (int64_t*)malloc(sizeof(int64_t) * (size_t)(N ? N : 1) * (r->cfg.n_scores ? r->cfg.n_scores : 1));
@@ -489,7 +549,7 @@ int kgpu_ref_schedule(ref_state* r, const kgpu_pod_query* qs, int nq, const kgpu
     pthread_mutex_init(&w.mu, NULL);
     w.r = r; w.p = p; w.q = q; w.status = status;
     w.phase = 0;
-    parallel_until(&w, N, r->threads);
+    parallel_until((pool_t*)r->pool, &w, N);
     int nf = 0;
     for (int i = 0; i < N; ++i) if (status[i] == 0) feasible[nf++] = i;
     kgpu_result res;
@@ -512,7 +572,7 @@ int kgpu_ref_schedule(ref_state* r, const kgpu_pod_query* qs, int nq, const kgpu
         w.feasible = feasible;
         w.nf = nf;
         w.scores = scores;
-        parallel_until(&w, nf, r->threads);
+        parallel_until((pool_t*)r->pool, &w, nf);
         for (int i = 0; i < nf; ++i) totals[i] = 0;
         for (int k = 0; k < r->cfg.n_scores; ++k) {
           int64_t* s = scores + (size_t)k * nf;
