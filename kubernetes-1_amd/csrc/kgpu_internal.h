@@ -7,8 +7,8 @@
 
 namespace kgpu {
 
-constexpr int kBlock = 256;        // threads per node-evaluation workgroup (4 waves of 64)
-constexpr int kMaxBlocks = 512;    // cap so that the fused winner resolution stays cheap
+constexpr int kBlock = 64;         // threads per node-evaluation workgroup: one wave64
+constexpr int kMaxBlocks = 1024;   // cap so that the fused winner resolution stays cheap
 constexpr int kSelAnd = 0, kSelNothing = 1, kSelEmpty = 2;
 constexpr uint64_t kMask40 = (1ull << 40) - 1;
 

@@ -188,6 +188,20 @@ __device__ __forceinline__ int64_t pod_scalar_score(const DevState& st, const kg
   return 0;
 }
 
+// Exact int64 floor division for 0 <= a, 0 < b: one IEEE double division (correctly rounded,
+// error < 1/4 for operands < 2^52) plus a one-step remainder correction; the 64-bit integer
+// division sequence is the fallback for larger operands.
+__device__ __forceinline__ int64_t div_nonneg(int64_t a, int64_t b) {
+  if (a < (1ll << 52) && b < (1ll << 52)) {
+    int64_t q = (int64_t)((double)a / (double)b);
+    const int64_t r = a - q * b;
+    if (r < 0) q -= 1;
+    else if (r >= b) q += 1;
+    return q;
+  }
+  return a / b;
+}
+
 // calculateResourceAllocatableRequest (resource_allocation.go:92-113).
 __device__ __forceinline__ void alloc_req(const DevState& st, const kgpu_pod_query& q, const NodeRes& nr, int res,
                                           int n, int64_t& cap, int64_t& req) {
@@ -213,10 +227,10 @@ __device__ __forceinline__ int64_t least_score(const DevState& st, const kgpu_po
   for (int i = 0; i < st.n_least; ++i) {
     int64_t cap, req;
     alloc_req(st, q, nr, st.least[i].resource, n, cap, req);
-    const int64_t r = (cap == 0 || req > cap) ? 0 : ((cap - req) * 100) / cap;
+    const int64_t r = (cap == 0 || req > cap) ? 0 : (cap > 0 ? div_nonneg((cap - req) * 100, cap) : ((cap - req) * 100) / cap);
     s += r * st.least[i].weight;
   }
-  return s / st.least_wsum;
+  return s >= 0 ? div_nonneg(s, st.least_wsum) : s / st.least_wsum;
 }
 
 __device__ __forceinline__ int64_t most_score(const DevState& st, const kgpu_pod_query& q, const NodeRes& nr,
@@ -225,10 +239,10 @@ __device__ __forceinline__ int64_t most_score(const DevState& st, const kgpu_pod
   for (int i = 0; i < st.n_most; ++i) {
     int64_t cap, req;
     alloc_req(st, q, nr, st.most[i].resource, n, cap, req);
-    const int64_t r = (cap == 0 || req > cap) ? 0 : (req * 100) / cap;
+    const int64_t r = (cap == 0 || req > cap) ? 0 : (req >= 0 && cap > 0 ? div_nonneg(req * 100, cap) : (req * 100) / cap);
     s += r * st.most[i].weight;
   }
-  return s / st.most_wsum;
+  return s >= 0 ? div_nonneg(s, st.most_wsum) : s / st.most_wsum;
 }
 
 // balancedResourceScorer (balanced_allocation.go:83-120): IEEE double, no contraction.
@@ -474,27 +488,22 @@ __device__ __forceinline__ void chunk_of(int N, int& lo, int& hi) {
 }
 
 // ---------------------------------------------------------------- kernels
+// One workgroup = one wave64: the workgroup argmax is a pure shuffle reduction (no LDS, no
+// barrier), and every wave resolves the previous pod's winner on its own.
 __global__ __launch_bounds__(kBlock) void k_eval(DevState st, PodArgs a) {
   int lo, hi;
   chunk_of(st.N, lo, hi);
   const int n0 = lo + threadIdx.x;
-  // independent loads first: this thread's first node row and the pod query overlap the
-  // previous pod's winner reduction
+  // Independent loads first -- this lane's first node row, the pod query and the pending pod's
+  // partials -- so that their latencies overlap instead of chaining.
   NodeRes r0{};
   if (n0 < hi) r0 = load_res(st, n0);
+  const kgpu_pod_query q = st.queries[a.pod];
   int assume_idx = -1;
   if (a.prev >= 0) {
     const Winner w = wave_winner(st.kbuf + (size_t)a.prev_parity * kMaxBlocks, a.prev_blocks);
     assume_idx = settle_prev(st, a, w);
   }
-  if (a.pod < 0) {
-    if (assume_idx >= 0 && assume_idx >= lo && assume_idx < hi && ((assume_idx - lo) % kBlock) == (int)threadIdx.x) {
-      NodeRes r = load_res(st, assume_idx);
-      assume_row(st, st.queries[a.prev], r, assume_idx);
-    }
-    return;
-  }
-  const kgpu_pod_query q = st.queries[a.pod];
   const uint64_t tk = pod_tie_key(st.seed, a.seq);
   const bool write_nodes = a.norm || a.diag;
 
@@ -524,55 +533,28 @@ __global__ __launch_bounds__(kBlock) void k_eval(DevState st, PodArgs a) {
       st.raw_na[n] = e.na;
     }
   }
-  // workgroup reduction: wave64 shuffles, then the 4 wave leaders through LDS
-  __shared__ uint64_t s_key[kBlock / 64];
-  __shared__ int s_idx[kBlock / 64], s_f[kBlock / 64], s_t[kBlock / 64], s_na[kBlock / 64];
   wave_reduce_key(best, best_i);
   feas = wave_reduce_sum(feas);
   maxT = wave_reduce_max(maxT);
   maxNA = wave_reduce_max(maxNA);
-  const int w = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) {
-    s_key[w] = best; s_idx[w] = best_i; s_f[w] = feas; s_t[w] = maxT; s_na[w] = maxNA;
-  }
-  __syncthreads();
   if (threadIdx.x == 0) {
-    for (int i = 1; i < kBlock / 64; ++i) {
-      key_max(best, best_i, s_key[i], s_idx[i]);
-      feas += s_f[i];
-      maxT = max(maxT, s_t[i]);
-      maxNA = max(maxNA, s_na[i]);
-    }
-    BlkStat bs{feas, maxT, maxNA, 0};
-    st.sbuf[(size_t)a.parity * kMaxBlocks + blockIdx.x] = bs;
-    if (!a.norm) {
-      BlkKey bk{best, best_i, feas};
-      st.kbuf[(size_t)a.parity * kMaxBlocks + blockIdx.x] = bk;
-    }
+    st.sbuf[(size_t)a.parity * kMaxBlocks + blockIdx.x] = BlkStat{feas, maxT, maxNA, 0};
+    if (!a.norm) st.kbuf[(size_t)a.parity * kMaxBlocks + blockIdx.x] = BlkKey{best, best_i, feas};
   }
 }
 
 // Normalize pass: DefaultNormalizeScore maxima over the feasible set are known only after the
 // evaluation launch; combine them with the stored raw values and take the argmax.
 __global__ __launch_bounds__(kBlock) void k_final(DevState st, PodArgs a, int stat_blocks) {
-  __shared__ int s_t[kBlock / 64], s_na[kBlock / 64], s_f[kBlock / 64];
-  int feas = 0, maxT = 0, maxNA = 0;
+  int maxT = 0, maxNA = 0;
   const BlkStat* sb = st.sbuf + (size_t)a.parity * kMaxBlocks;
   for (int b = threadIdx.x; b < stat_blocks; b += kBlock) {
     const BlkStat p = sb[b];
-    feas += p.feasible;
     maxT = max(maxT, p.max_taint);
     maxNA = max(maxNA, p.max_na);
   }
-  feas = wave_reduce_sum(feas);
   maxT = wave_reduce_max(maxT);
   maxNA = wave_reduce_max(maxNA);
-  const int w = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) { s_t[w] = maxT; s_na[w] = maxNA; s_f[w] = feas; }
-  __syncthreads();
-  maxT = 0; maxNA = 0;
-  for (int i = 0; i < kBlock / 64; ++i) { maxT = max(maxT, s_t[i]); maxNA = max(maxNA, s_na[i]); }
-
   int lo, hi;
   chunk_of(st.N, lo, hi);
   const uint64_t tk = pod_tie_key(st.seed, a.seq);
@@ -594,24 +576,13 @@ __global__ __launch_bounds__(kBlock) void k_final(DevState st, PodArgs a, int st
       }
     }
   }
-  __shared__ uint64_t s_key[kBlock / 64];
-  __shared__ int s_idx[kBlock / 64], s_bf[kBlock / 64];
   wave_reduce_key(best, best_i);
   bf = wave_reduce_sum(bf);
-  if ((threadIdx.x & 63) == 0) { s_key[w] = best; s_idx[w] = best_i; s_bf[w] = bf; }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    for (int i = 1; i < kBlock / 64; ++i) {
-      key_max(best, best_i, s_key[i], s_idx[i]);
-      bf += s_bf[i];
-    }
-    BlkKey bk{best, best_i, bf};
-    st.kbuf[(size_t)a.parity * kMaxBlocks + blockIdx.x] = bk;
-  }
+  if (threadIdx.x == 0) st.kbuf[(size_t)a.parity * kMaxBlocks + blockIdx.x] = BlkKey{best, best_i, bf};
 }
 
-// Resolve-only launch (end of a batch / single cycle): one workgroup per chunk mapping of the
-// evaluation grid so that the owner of the winning row applies the assume.
+// Resolve-only launch (end of a batch / single cycle), with the evaluation grid's chunk mapping
+// so that the lane owning the winning row applies the assume.
 __global__ __launch_bounds__(kBlock) void k_resolve(DevState st, PodArgs a) {
   int lo, hi;
   chunk_of(st.N, lo, hi);
