@@ -37,6 +37,8 @@ struct kgpu_ctx {
   bool uploaded = false;
   // grow-only batch buffers
   DevBuf queries, reqs, ints, words, node_terms, pref_terms, spreads, pod_terms, scalars, ports, results;
+  DevBuf dstate;     // device copy of the DevState used by the kernels of the current batch
+  DevState st_batch{};  // its host source (kept alive for the async copy)
   bool timing = false;
   bool use_graph = true;
   std::vector<uint64_t> prefer_union;  // PreferNoSchedule taint ids present on any node
@@ -191,6 +193,10 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
     HIP_OK(c, hipMemsetAsync(st.diag_raw, 0, sizeof(int64_t) * KGPU_NUM_SCORES * (size_t)st.N, c->stream));
     HIP_OK(c, hipMemsetAsync(st.diag_norm, 0, sizeof(int64_t) * KGPU_NUM_SCORES * (size_t)st.N, c->stream));
   }
+  if ((rc = ensure(c, c->dstate, sizeof(DevState)))) return rc;
+  c->st_batch = st;
+  HIP_OK(c, hipMemcpyAsync(c->dstate.p, &c->st_batch, sizeof(DevState), hipMemcpyHostToDevice, c->stream));
+  const DevState* dst = static_cast<const DevState*>(c->dstate.p);
   const int blocks = kgpu::eval_blocks(st.N);
   hipEvent_t t0 = get_event(c, 0), t1 = get_event(c, 1);
   HIP_OK(c, hipEventRecord(t0, c->stream));
@@ -208,10 +214,10 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
     a.diag = diag ? 1 : 0;
     a.seq = first_seq + i;
     if (c->timing) HIP_OK(c, hipEventRecord(get_event(c, ev), c->stream));
-    if (kgpu::launch_eval(st, a, blocks, c->stream)) return fail(c, KGPU_E_DEVICE, "k_eval launch failed");
+    if (kgpu::launch_eval(dst, a, blocks, c->stream)) return fail(c, KGPU_E_DEVICE, "k_eval launch failed");
     if (c->timing) HIP_OK(c, hipEventRecord(get_event(c, ev + 1), c->stream));
     ev += 2;
-    if (a.norm && kgpu::launch_final(st, a, blocks, blocks, c->stream))
+    if (a.norm && kgpu::launch_final(dst, a, blocks, blocks, c->stream))
       return fail(c, KGPU_E_DEVICE, "k_final launch failed");
     prev = i;
   }
@@ -221,7 +227,7 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
   r.prev_blocks = blocks;
   r.prev_parity = prev & 1;
   r.assume = assume;
-  if (kgpu::launch_resolve(st, r, c->stream)) return fail(c, KGPU_E_DEVICE, "k_resolve launch failed");
+  if (kgpu::launch_resolve(dst, st.N, r, c->stream)) return fail(c, KGPU_E_DEVICE, "k_resolve launch failed");
   HIP_OK(c, hipEventRecord(t1, c->stream));
   HIP_OK(c, hipMemcpyAsync(results, st.results, sizeof(kgpu_result) * (size_t)n, hipMemcpyDeviceToHost, c->stream));
   HIP_OK(c, hipStreamSynchronize(c->stream));
@@ -337,7 +343,7 @@ int kgpu_destroy(kgpu_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   free_all(c->snap_allocs);
   free_all(c->work_allocs);
-  for (DevBuf* b : {&c->queries, &c->reqs, &c->ints, &c->words, &c->node_terms, &c->pref_terms, &c->spreads,
+  for (DevBuf* b : {&c->dstate, &c->queries, &c->reqs, &c->ints, &c->words, &c->node_terms, &c->pref_terms, &c->spreads,
                     &c->pod_terms, &c->scalars, &c->ports, &c->results})
     if (b->p) (void)hipFree(b->p);
   for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);

@@ -108,9 +108,11 @@ struct PodArgs {
 };
 
 // Host-side launchers (kgpu_kernels.hip).
-int launch_eval(const DevState& st, const PodArgs& a, int blocks, void* stream);
-int launch_final(const DevState& st, const PodArgs& a, int blocks, int stat_blocks, void* stream);
-int launch_resolve(const DevState& st, const PodArgs& a, void* stream);
+// The DevState lives in device memory (one copy per batch): kernel arguments stay at 40 bytes,
+// so no launch pulls a kilobyte of kernarg segment through the host-coherent path.
+int launch_eval(const DevState* st, const PodArgs& a, int blocks, void* stream);
+int launch_final(const DevState* st, const PodArgs& a, int blocks, int stat_blocks, void* stream);
+int launch_resolve(const DevState* st, int N, const PodArgs& a, void* stream);
 int eval_blocks(int N);
 
 }  // namespace kgpu

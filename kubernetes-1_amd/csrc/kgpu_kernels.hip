@@ -490,7 +490,8 @@ __device__ __forceinline__ void chunk_of(int N, int& lo, int& hi) {
 // ---------------------------------------------------------------- kernels
 // One workgroup = one wave64: the workgroup argmax is a pure shuffle reduction (no LDS, no
 // barrier), and every wave resolves the previous pod's winner on its own.
-__global__ __launch_bounds__(kBlock) void k_eval(DevState st, PodArgs a) {
+__global__ __launch_bounds__(kBlock) void k_eval(const DevState* __restrict__ stp, PodArgs a) {
+  const DevState& st = *stp;
   int lo, hi;
   chunk_of(st.N, lo, hi);
   const int n0 = lo + threadIdx.x;
@@ -545,7 +546,8 @@ __global__ __launch_bounds__(kBlock) void k_eval(DevState st, PodArgs a) {
 
 // Normalize pass: DefaultNormalizeScore maxima over the feasible set are known only after the
 // evaluation launch; combine them with the stored raw values and take the argmax.
-__global__ __launch_bounds__(kBlock) void k_final(DevState st, PodArgs a, int stat_blocks) {
+__global__ __launch_bounds__(kBlock) void k_final(const DevState* __restrict__ stp, PodArgs a, int stat_blocks) {
+  const DevState& st = *stp;
   int maxT = 0, maxNA = 0;
   const BlkStat* sb = st.sbuf + (size_t)a.parity * kMaxBlocks;
   for (int b = threadIdx.x; b < stat_blocks; b += kBlock) {
@@ -583,7 +585,8 @@ __global__ __launch_bounds__(kBlock) void k_final(DevState st, PodArgs a, int st
 
 // Resolve-only launch (end of a batch / single cycle), with the evaluation grid's chunk mapping
 // so that the lane owning the winning row applies the assume.
-__global__ __launch_bounds__(kBlock) void k_resolve(DevState st, PodArgs a) {
+__global__ __launch_bounds__(kBlock) void k_resolve(const DevState* __restrict__ stp, PodArgs a) {
+  const DevState& st = *stp;
   int lo, hi;
   chunk_of(st.N, lo, hi);
   const Winner w = wave_winner(st.kbuf + (size_t)a.prev_parity * kMaxBlocks, a.prev_blocks);
@@ -601,19 +604,19 @@ int eval_blocks(int N) {
   return b;
 }
 
-int launch_eval(const DevState& st, const PodArgs& a, int blocks, void* stream) {
+int launch_eval(const DevState* st, const PodArgs& a, int blocks, void* stream) {
   hipLaunchKernelGGL(k_eval, dim3(blocks), dim3(kBlock), 0, (hipStream_t)stream, st, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_final(const DevState& st, const PodArgs& a, int blocks, int stat_blocks, void* stream) {
+int launch_final(const DevState* st, const PodArgs& a, int blocks, int stat_blocks, void* stream) {
   hipLaunchKernelGGL(k_final, dim3(blocks), dim3(kBlock), 0, (hipStream_t)stream, st, a, stat_blocks);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_resolve(const DevState& st, const PodArgs& a, void* stream) {
+int launch_resolve(const DevState* st, int N, const PodArgs& a, void* stream) {
   // same grid as the evaluation so that chunk ownership matches
-  hipLaunchKernelGGL(k_resolve, dim3(eval_blocks(st.N)), dim3(kBlock), 0, (hipStream_t)stream, st, a);
+  hipLaunchKernelGGL(k_resolve, dim3(eval_blocks(N)), dim3(kBlock), 0, (hipStream_t)stream, st, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
