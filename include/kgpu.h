@@ -382,11 +382,22 @@ int kgpu_read_nodes(kgpu_ctx* ctx, int64_t* req_cpu, int64_t* req_mem, int64_t* 
 
 /* Options.  KGPU_OPT_KERNEL_TIMING (1): bracket every node-evaluation launch with HIP events and
  * report their summed duration in kgpu_stats.eval_kernel_ms (adds per-launch overhead: use in a
- * separate measurement pass).  KGPU_OPT_USE_GRAPH (2): replay pods of a uniform batch through a
- * captured hipGraph (default 1). */
+ * separate measurement pass).  KGPU_OPT_PERSISTENT (2): schedule runs of pods whose normalize
+ * maxima are constant inside one persistent launch, node rows register-resident (default 1);
+ * 0 = one evaluation launch per pod. */
 #define KGPU_OPT_KERNEL_TIMING 1
-#define KGPU_OPT_USE_GRAPH 2
+#define KGPU_OPT_PERSISTENT 2
+/* KGPU_OPT_PERSIST_GROUPS (3): cap on the persistent kernel's workgroups (0 = one per CU); a
+ * lower cap gives each lane more node rows (tests use it to cover every rows-per-lane variant). */
+#define KGPU_OPT_PERSIST_GROUPS 3
+/* KGPU_OPT_PHASE_TRACE (4): record per-pod phase timestamps of the persistent kernel (diagnostics;
+ * read with kgpu_read_phase_trace). */
+#define KGPU_OPT_PHASE_TRACE 4
 int kgpu_set_option(kgpu_ctx* ctx, int32_t option, int64_t value);
+/* Phase stamps of the last persistent run (100 MHz s_memrealtime ticks), 16 per pipeline
+ * iteration (pods + 1): workgroup 0's {start, evaluated, previous pod resolved, published, end, 0,
+ * 0, 0}, then the last workgroup's.  Returns the number of iterations written (<= max_iters). */
+int kgpu_read_phase_trace(kgpu_ctx* ctx, int64_t* out, int32_t max_iters);
 
 /* Node sharding across GPUs (one process per GPU).  kgpu_comm_unique_id fills 128 bytes on rank
  * 0; the caller broadcasts them; every rank calls kgpu_comm_init with its shard's snapshot

@@ -40,7 +40,15 @@ struct kgpu_ctx {
   DevBuf dstate;     // device copy of the DevState used by the kernels of the current batch
   DevState st_batch{};  // its host source (kept alive for the async copy)
   bool timing = false;
-  bool use_graph = true;
+  bool persistent = true;  // KGPU_OPT_PERSISTENT
+  int n_cus = 0;
+  int max_groups = 0;  // KGPU_OPT_PERSIST_GROUPS (0 = n_cus)
+  DevBuf gran;        // persistent-kernel granules + abort word
+  int32_t abort_host = 0;
+  bool phase_trace = false;
+  DevBuf trace;
+  std::vector<int64_t> trace_host;
+  int spec = 0;      // k_eval instantiation for the profile (kgpu::select_spec)
   std::vector<uint64_t> prefer_union;  // PreferNoSchedule taint ids present on any node
   // pods assumed through this context (slot -> record), for kgpu_forget_pod
   struct Assumed {
@@ -201,36 +209,94 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
   hipEvent_t t0 = get_event(c, 0), t1 = get_event(c, 1);
   HIP_OK(c, hipEventRecord(t0, c->stream));
   size_t ev = 2;
-  int prev = -1;
-  for (int32_t i = 0; i < n; ++i) {
-    PodArgs a{};
-    a.pod = i;
-    a.prev = prev;
-    a.prev_blocks = blocks;
-    a.prev_parity = (i - 1) & 1;
-    a.parity = i & 1;
-    a.norm = (diag || needs_norm(c, qs[i], pools)) ? 1 : 0;
-    a.assume = assume;
-    a.diag = diag ? 1 : 0;
-    a.seq = first_seq + i;
-    if (c->timing) HIP_OK(c, hipEventRecord(get_event(c, ev), c->stream));
-    if (kgpu::launch_eval(dst, a, blocks, c->stream)) return fail(c, KGPU_E_DEVICE, "k_eval launch failed");
-    if (c->timing) HIP_OK(c, hipEventRecord(get_event(c, ev + 1), c->stream));
-    ev += 2;
-    if (a.norm && kgpu::launch_final(dst, a, blocks, blocks, c->stream))
-      return fail(c, KGPU_E_DEVICE, "k_final launch failed");
-    prev = i;
+  int64_t timed_passes = 0;
+  // Persistent geometry: one workgroup per CU at most, K node rows per lane in registers.
+  int per = 0, groups = 0;
+  const int kidx = (c->persistent && !diag) ? kgpu::batch_geometry(st.N, std::min(c->max_groups > 0 ? std::min(c->max_groups, c->n_cus) : c->n_cus, 256), &per, &groups) : -1;
+  std::vector<uint8_t> norm((size_t)n);
+  // pods that need the normalize pass or whose scoring fails take the one-launch-per-pod path
+  for (int32_t i = 0; i < n; ++i)
+    norm[(size_t)i] = (diag || needs_norm(c, qs[i], pools) || (qs[i].flags & KGPU_Q_SCORE_ERROR)) ? 1 : 0;
+  bool used_persistent = false;
+  int32_t i = 0;
+  while (i < n) {
+    int32_t j = i;
+    if (kidx >= 0 && !norm[(size_t)i]) {
+      // a run of pods with constant normalize maxima: one persistent launch
+      while (j < n && !norm[(size_t)j]) ++j;
+      const int32_t cnt = j - i;
+      // layout: abort word (64 B) | granules [cnt][groups] u64 | feasible counts [cnt][groups] i32
+      const size_t cells = (size_t)cnt * (size_t)groups;
+      const size_t gbytes = 64 + sizeof(uint64_t) * cells + sizeof(int32_t) * cells;
+      if ((rc = ensure(c, c->gran, gbytes))) return rc;
+      HIP_OK(c, hipMemsetAsync(c->gran.p, 0, 64 + sizeof(uint64_t) * cells, c->stream));
+      kgpu::BatchArgs ba{};
+      ba.first = i;
+      ba.count = cnt;
+      ba.per = per;
+      ba.assume = assume;
+      ba.seq0 = first_seq + i;
+      ba.gran = static_cast<uint64_t*>(c->gran.p) + 8;
+      ba.feas = reinterpret_cast<int32_t*>(ba.gran + cells);
+      ba.abort = static_cast<int32_t*>(c->gran.p);
+      ba.trace = nullptr;
+      if (c->phase_trace) {
+        if ((rc = ensure(c, c->trace, sizeof(int64_t) * 16 * (size_t)(cnt + 1)))) return rc;
+        HIP_OK(c, hipMemsetAsync(c->trace.p, 0, sizeof(int64_t) * 16 * (size_t)(cnt + 1), c->stream));
+        ba.trace = static_cast<int64_t*>(c->trace.p);
+        c->trace_host.assign((size_t)(cnt + 1) * 16, 0);
+      }
+      if (c->timing) HIP_OK(c, hipEventRecord(get_event(c, ev), c->stream));
+      if (kgpu::launch_batch(dst, ba, groups, kidx, c->spec, c->stream))
+        return fail(c, KGPU_E_DEVICE, "k_batch launch failed");
+      if (c->timing) HIP_OK(c, hipEventRecord(get_event(c, ev + 1), c->stream));
+      ev += 2;
+      timed_passes += cnt;
+      HIP_OK(c, hipMemcpyAsync(&c->abort_host, c->gran.p, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+      if (ba.trace)
+        HIP_OK(c, hipMemcpyAsync(c->trace_host.data(), ba.trace, sizeof(int64_t) * 16 * (size_t)(cnt + 1),
+                                 hipMemcpyDeviceToHost, c->stream));
+      used_persistent = true;
+    } else {
+      // one launch per pod; the next launch resolves (and assumes) the previous pod's winner
+      while (j < n && (kidx < 0 || norm[(size_t)j])) ++j;
+      int prev = -1;
+      for (int32_t k = i; k < j; ++k) {
+        PodArgs a{};
+        a.pod = k;
+        a.prev = prev;
+        a.prev_blocks = blocks;
+        a.prev_parity = (k - 1) & 1;
+        a.parity = k & 1;
+        a.norm = (diag || needs_norm(c, qs[k], pools)) ? 1 : 0;
+        a.assume = assume;
+        a.diag = diag ? 1 : 0;
+        a.seq = first_seq + k;
+        if (c->timing) HIP_OK(c, hipEventRecord(get_event(c, ev), c->stream));
+        if (kgpu::launch_eval(dst, a, blocks, c->spec, c->stream))
+          return fail(c, KGPU_E_DEVICE, "k_eval launch failed");
+        if (c->timing) HIP_OK(c, hipEventRecord(get_event(c, ev + 1), c->stream));
+        ev += 2;
+        ++timed_passes;
+        if (a.norm && kgpu::launch_final(dst, a, blocks, blocks, c->stream))
+          return fail(c, KGPU_E_DEVICE, "k_final launch failed");
+        prev = k;
+      }
+      PodArgs r{};
+      r.pod = -1;
+      r.prev = prev;
+      r.prev_blocks = blocks;
+      r.prev_parity = prev & 1;
+      r.assume = assume;
+      if (kgpu::launch_resolve(dst, st.N, r, c->stream)) return fail(c, KGPU_E_DEVICE, "k_resolve launch failed");
+    }
+    i = j;
   }
-  PodArgs r{};
-  r.pod = -1;
-  r.prev = prev;
-  r.prev_blocks = blocks;
-  r.prev_parity = prev & 1;
-  r.assume = assume;
-  if (kgpu::launch_resolve(dst, st.N, r, c->stream)) return fail(c, KGPU_E_DEVICE, "k_resolve launch failed");
   HIP_OK(c, hipEventRecord(t1, c->stream));
   HIP_OK(c, hipMemcpyAsync(results, st.results, sizeof(kgpu_result) * (size_t)n, hipMemcpyDeviceToHost, c->stream));
   HIP_OK(c, hipStreamSynchronize(c->stream));
+  if (used_persistent && c->abort_host)
+    return fail(c, KGPU_E_DEVICE, "persistent batch kernel lost co-residency (workgroups not all resident)");
   if (stats) {
     float ms = 0.f;
     HIP_OK(c, hipEventElapsedTime(&ms, t0, t1));
@@ -247,7 +313,7 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
         sum += k;
       }
       stats->eval_kernel_ms += sum;
-      stats->eval_launches += n;
+      stats->eval_launches += timed_passes;
     }
   }
   // keep host records of assumed pods for ForgetPod
@@ -300,11 +366,16 @@ int kgpu_create(const kgpu_config* cfg, kgpu_ctx** out) {
   int64_t total = 0;
   for (int i = 0; i < cfg->n_scores; ++i) {
     if (cfg->scores[i] < 0 || cfg->scores[i] >= KGPU_NUM_SCORES) return KGPU_E_INVAL;
+    for (int j = 0; j < i; ++j)
+      if (cfg->scores[j] == cfg->scores[i]) return KGPU_E_INVAL;  // a plugin appears once per extension point
     total += std::max<int64_t>(cfg->score_weights[i], 1) * 100;
   }
-  if (total >= (1ll << 23)) return KGPU_E_UNSUPPORTED;  // packed argmax key holds 23 score bits
-  for (int i = 0; i < cfg->n_filters; ++i)
+  if (total >= (1ll << 23) - 1) return KGPU_E_UNSUPPORTED;  // packed argmax key: 23 bits hold score + 1
+  for (int i = 0; i < cfg->n_filters; ++i) {
     if (cfg->filters[i] < 0 || cfg->filters[i] >= KGPU_NUM_FILTERS) return KGPU_E_INVAL;
+    for (int j = 0; j < i; ++j)
+      if (cfg->filters[j] == cfg->filters[i]) return KGPU_E_INVAL;
+  }
   if (cfg->percentage_of_nodes_to_score > 0 && cfg->percentage_of_nodes_to_score < 100) return KGPU_E_UNSUPPORTED;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return KGPU_E_DEVICE;
@@ -316,12 +387,21 @@ int kgpu_create(const kgpu_config* cfg, kgpu_ctx** out) {
     delete c;
     return KGPU_E_DEVICE;
   }
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, c->device) != hipSuccess) {
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+    return KGPU_E_DEVICE;
+  }
+  c->n_cus = prop.multiProcessorCount;
   DevState& st = c->st;
   st.n_filters = cfg->n_filters;
   std::memcpy(st.filters, cfg->filters, sizeof(st.filters));
   st.n_scores = cfg->n_scores;
   std::memcpy(st.scores, cfg->scores, sizeof(st.scores));
   for (int i = 0; i < KGPU_NUM_SCORES; ++i) st.weights[i] = std::max<int64_t>(cfg->score_weights[i], 1);
+  for (int i = 0; i < KGPU_NUM_SCORES; ++i) st.w_of[i] = 0;
+  for (int i = 0; i < cfg->n_scores; ++i) st.w_of[cfg->scores[i]] = st.weights[i];
   st.n_least = cfg->n_least;
   st.n_most = cfg->n_most;
   std::memcpy(st.least, cfg->least, sizeof(st.least));
@@ -333,6 +413,13 @@ int kgpu_create(const kgpu_config* cfg, kgpu_ctx** out) {
   if (st.most_wsum == 0) st.most_wsum = 1;
   st.tie_mode = cfg->tie_break_mode;
   st.seed = cfg->seed;
+  // default requested-resource specs {cpu: 1, memory: 1} (noderesources/resource_allocation.go:36-39)
+  auto def_spec = [](const kgpu_resource_weight* r, int n) {
+    return n == 2 && r[0].resource == 0 && r[0].weight == 1 && r[1].resource == 1 && r[1].weight == 1;
+  };
+  const bool has_least = has_score(c, KGPU_S_LEAST_ALLOCATED), has_most = has_score(c, KGPU_S_MOST_ALLOCATED);
+  const bool def_res = (!has_least || def_spec(cfg->least, cfg->n_least)) && (!has_most || def_spec(cfg->most, cfg->n_most));
+  c->spec = kgpu::select_spec(cfg->filters, cfg->n_filters, cfg->scores, cfg->n_scores, def_res);
   *out = c;
   return KGPU_OK;
 }
@@ -344,7 +431,7 @@ int kgpu_destroy(kgpu_ctx* c) {
   free_all(c->snap_allocs);
   free_all(c->work_allocs);
   for (DevBuf* b : {&c->dstate, &c->queries, &c->reqs, &c->ints, &c->words, &c->node_terms, &c->pref_terms, &c->spreads,
-                    &c->pod_terms, &c->scalars, &c->ports, &c->results})
+                    &c->pod_terms, &c->scalars, &c->ports, &c->results, &c->gran, &c->trace})
     if (b->p) (void)hipFree(b->p);
   for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -356,10 +443,19 @@ const char* kgpu_last_error(const kgpu_ctx* c) { return c ? c->err.c_str() : "nu
 
 int64_t kgpu_generation(const kgpu_ctx* c) { return c ? c->generation : -1; }
 
+int kgpu_read_phase_trace(kgpu_ctx* c, int64_t* out, int32_t max_pods) {
+  if (!c || !out || max_pods < 0) return KGPU_E_INVAL;
+  const int32_t n = std::min<int32_t>(max_pods, (int32_t)(c->trace_host.size() / 16));
+  std::memcpy(out, c->trace_host.data(), sizeof(int64_t) * 16 * (size_t)n);
+  return n;
+}
+
 int kgpu_set_option(kgpu_ctx* c, int32_t option, int64_t value) {
   if (!c) return KGPU_E_INVAL;
   if (option == KGPU_OPT_KERNEL_TIMING) c->timing = value != 0;
-  else if (option == KGPU_OPT_USE_GRAPH) c->use_graph = value != 0;
+  else if (option == KGPU_OPT_PERSISTENT) c->persistent = value != 0;
+  else if (option == KGPU_OPT_PERSIST_GROUPS) c->max_groups = (int)std::max<int64_t>(value, 0);
+  else if (option == KGPU_OPT_PHASE_TRACE) c->phase_trace = value != 0;
   else return KGPU_E_INVAL;
   return KGPU_OK;
 }

@@ -73,7 +73,8 @@ struct DevState {
   int32_t filters[KGPU_NUM_FILTERS];
   int32_t n_scores;
   int32_t scores[KGPU_NUM_SCORES];
-  int64_t weights[KGPU_NUM_SCORES];
+  int64_t weights[KGPU_NUM_SCORES];     // by profile position
+  int64_t w_of[KGPU_NUM_SCORES];        // by plugin id, 0 = plugin not in the profile
   int32_t n_least, n_most;
   kgpu_resource_weight least[8], most[8];
   int64_t least_wsum, most_wsum;
@@ -107,12 +108,33 @@ struct PodArgs {
   int64_t seq;          // tie-break sequence number of `pod`
 };
 
+// Persistent batch launch: a run of `count` pods (queries first..first+count-1) in one kernel.
+struct BatchArgs {
+  int32_t first;        // first query index of the run
+  int32_t count;        // pods in the run
+  int32_t per;          // nodes owned by one workgroup
+  int32_t assume;
+  int64_t seq0;         // tie-break sequence number of query `first`
+  uint64_t* gran;       // [count][groups] granules, zeroed before the launch
+  int32_t* feas;        // [count][groups] feasible count of each published variant
+  int32_t* abort;       // raised (1) by a workgroup that lost co-residency; zeroed before the launch
+  int64_t* trace;       // null, or [count + 1][16] s_memrealtime stamps, 8 per traced workgroup
+                        // (0 and last): iteration start, evaluated, previous pod resolved,
+                        // granule published, iteration end
+};
+
 // Host-side launchers (kgpu_kernels.hip).
 // The DevState lives in device memory (one copy per batch): kernel arguments stay at 40 bytes,
 // so no launch pulls a kilobyte of kernarg segment through the host-coherent path.
-int launch_eval(const DevState* st, const PodArgs& a, int blocks, void* stream);
+int launch_eval(const DevState* st, const PodArgs& a, int blocks, int spec, void* stream);
+// Kernel instantiation for a profile: 0 = generic list-walking kernel, else a straight-line one.
+int select_spec(const int32_t* filters, int nf, const int32_t* scores, int ns, bool def_res);
 int launch_final(const DevState* st, const PodArgs& a, int blocks, int stat_blocks, void* stream);
 int launch_resolve(const DevState* st, int N, const PodArgs& a, void* stream);
 int eval_blocks(int N);
+// Geometry index (workgroup size x rows per lane) and grid of the persistent kernel, -1 when N
+// does not fit in max_groups workgroups.
+int batch_geometry(int N, int max_groups, int* per, int* groups);
+int launch_batch(const DevState* st, const BatchArgs& a, int groups, int kidx, int spec, void* stream);
 
 }  // namespace kgpu

@@ -2,10 +2,17 @@
 //
 // One thread per node over Snapshot.List()-ordered SoA rows (coalesced 8-byte loads), every
 // filter and score plugin of the profile fused into one pass, workgroup argmax through wave64
-// shuffles + LDS, and the previous pod's selectHost + assume folded into the head of the next
-// pod's launch (each workgroup reduces the <= kMaxBlocks partials of the previous launch
-// redundantly; only the workgroup that owns the winning node row writes it).  No dense
-// contraction exists anywhere on this path: the bound is memory, not MFMA.
+// shuffles, and the previous pod's selectHost + assume folded into the head of the next pod's
+// launch (each wave reduces the <= kMaxBlocks partials of the previous launch redundantly; only
+// the lane that owns the winning node row writes it).  No dense contraction exists anywhere on
+// this path: the bound is memory latency/bandwidth, not MFMA.
+//
+// The evaluation kernel is a template over the profile: FM = enabled filters (profile order =
+// ascending plugin id, the default order), SM = enabled score plugins.  Common profiles get a
+// straight-line instantiation (no per-node plugin dispatch, no dependent loads of the plugin
+// list); any other profile runs the kRuntime instantiation that walks the lists from DevState.
+// Uniform data (DevState, queries, pools) is read through the constant address space (scalar
+// loads); node columns through the global address space (no flat instructions).
 //
 // Reference semantics (file:line in /root/reference):
 //   filters  framework/v1alpha1/framework.go:477-502 (profile order, first failure wins)
@@ -26,7 +33,29 @@
 
 #include "kgpu_internal.h"
 
+// Address spaces exist only in the device pass; the host pass parses the same code unqualified.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define GAS __attribute__((address_space(1)))
+#define CAS __attribute__((address_space(4)))
+#else
+#define GAS
+#define CAS
+#endif
+
 namespace kgpu {
+
+template <class T>
+__device__ __forceinline__ GAS T* gp(T* p) {
+  return (GAS T*)p;
+}
+template <class T>
+__device__ __forceinline__ const CAS T* cp(const T* p) {
+  return (const CAS T*)p;
+}
+
+constexpr uint32_t kRuntime = 0xFFFFFFFFu;  // FM/SM of the list-walking instantiation
+constexpr uint32_t kDefRes = 1u << 31;      // SM flag: Least/Most over {cpu: 1, memory: 1}
+constexpr uint32_t kSMask = (1u << KGPU_NUM_SCORES) - 1;
 
 // ---------------------------------------------------------------- tie-break
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
@@ -54,13 +83,13 @@ __device__ __forceinline__ uint64_t rank40(uint64_t k, uint64_t idx, int mode) {
 // ---------------------------------------------------------------- selectors
 __device__ __forceinline__ bool list_has(const int32_t* v, int n, int x) {
   for (int i = 0; i < n; ++i)
-    if (v[i] == x) return true;
+    if (cp(v)[i] == x) return true;
   return false;
 }
 
 // labels.Requirement.Matches on node labels (selector.go:198-242); v < 0 = key absent.
 __device__ bool node_req(const DevState& st, const kgpu_req& r, int n) {
-  const int v = r.key >= 0 ? st.label_val[(size_t)r.key * st.N + n] : -1;
+  const int v = r.key >= 0 ? gp(st.label_val)[(size_t)r.key * st.N + n] : -1;
   switch (r.op) {
     case KGPU_OP_IN:
       return v >= 0 && list_has(st.qp.ints + r.vals.begin, r.vals.count, v);
@@ -72,9 +101,9 @@ __device__ bool node_req(const DevState& st, const kgpu_req& r, int n) {
       return v < 0;
     default: {
       if (v < 0) return false;
-      const int idx = st.value_off[r.key] + v;
-      if (!st.value_int_ok[idx]) return false;
-      const int64_t lv = st.value_int[idx];
+      const int idx = gp(st.value_off)[r.key] + v;
+      if (!gp(st.value_int_ok)[idx]) return false;
+      const int64_t lv = gp(st.value_int)[idx];
       return r.op == KGPU_OP_GT ? lv > r.imm : lv < r.imm;
     }
   }
@@ -82,7 +111,7 @@ __device__ bool node_req(const DevState& st, const kgpu_req& r, int n) {
 
 __device__ bool node_reqs_all(const DevState& st, kgpu_range rr, int n) {
   for (int i = 0; i < rr.count; ++i)
-    if (!node_req(st, st.qp.reqs[rr.begin + i], n)) return false;
+    if (!node_req(st, cp(st.qp.reqs)[rr.begin + i], n)) return false;
   return true;
 }
 
@@ -92,7 +121,7 @@ __device__ bool node_affinity_ok(const DevState& st, const kgpu_pod_query& q, in
   if (!(q.flags & KGPU_Q_REQ_NODE_AFFINITY)) return true;
   const int g = st.node_base + n;
   for (int t = 0; t < q.req_terms.count; ++t) {
-    const kgpu_node_term term = st.qp.node_terms[q.req_terms.begin + t];
+    const kgpu_node_term term = cp(st.qp.node_terms)[q.req_terms.begin + t];
     if (term.never_match) continue;
     if (!node_reqs_all(st, term.reqs, n)) continue;
     if (term.field_op == KGPU_OP_IN && g != term.field_node) continue;
@@ -110,15 +139,24 @@ struct NodeRes {
   int64_t rc, rm, re;   // Requested
   int64_t zc, zm;       // NonZeroRequested
   int32_t ap, np;       // AllowedPodNumber, len(Pods)
+  double ic, im;        // 1/ac, 1/am where > 0 (persistent rows: Allocatable never changes), else 0
 };
 
 __device__ __forceinline__ NodeRes load_res(const DevState& st, int n) {
   NodeRes r;
-  r.ac = st.alloc_cpu[n]; r.am = st.alloc_mem[n]; r.ae = st.alloc_eph[n];
-  r.rc = st.req_cpu[n]; r.rm = st.req_mem[n]; r.re = st.req_eph[n];
-  r.zc = st.nz_cpu[n]; r.zm = st.nz_mem[n];
-  r.ap = st.alloc_pods[n]; r.np = st.num_pods[n];
+  r.ac = gp(st.alloc_cpu)[n]; r.am = gp(st.alloc_mem)[n]; r.ae = gp(st.alloc_eph)[n];
+  r.rc = gp(st.req_cpu)[n]; r.rm = gp(st.req_mem)[n]; r.re = gp(st.req_eph)[n];
+  r.zc = gp(st.nz_cpu)[n]; r.zm = gp(st.nz_mem)[n];
+  r.ap = gp(st.alloc_pods)[n]; r.np = gp(st.num_pods)[n];
+  r.ic = 0.0;
+  r.im = 0.0;
   return r;
+}
+
+// Reciprocals for register-resident rows, computed once per launch.
+__device__ __forceinline__ void set_recips(NodeRes& r) {
+  r.ic = (r.ac > 0 && r.ac < (1ll << 52)) ? 1.0 / (double)r.ac : 0.0;
+  r.im = (r.am > 0 && r.am < (1ll << 52)) ? 1.0 / (double)r.am : 0.0;
 }
 
 // ---------------------------------------------------------------- plugins
@@ -130,21 +168,21 @@ __device__ __forceinline__ uint32_t fit_detail(const DevState& st, const kgpu_po
   if (r.am < q.req[1] + r.rm) d |= 4u;
   if (r.ae < q.req[2] + r.re) d |= 8u;
   for (int i = 0; i < q.scalars.count; ++i) {
-    const kgpu_scalar_req s = st.qp.scalars[q.scalars.begin + i];
+    const kgpu_scalar_req s = cp(st.qp.scalars)[q.scalars.begin + i];
     if (!s.check) continue;
-    const int64_t alloc = s.col >= 0 ? st.alloc_scalar[(size_t)s.col * st.N + n] : 0;
-    const int64_t used = s.col >= 0 ? st.req_scalar[(size_t)s.col * st.N + n] : 0;
+    const int64_t alloc = s.col >= 0 ? gp(st.alloc_scalar)[(size_t)s.col * st.N + n] : 0;
+    const int64_t used = s.col >= 0 ? gp(st.req_scalar)[(size_t)s.col * st.N + n] : 0;
     if (alloc < s.value + used) d |= 16u << (i < 11 ? i : 11);
   }
   return d;
 }
 
 __device__ __forceinline__ bool ports_conflict(const DevState& st, const kgpu_pod_query& q, int n) {
-  const int have = st.port_count[n];
+  const int have = gp(st.port_count)[n];
   for (int i = 0; i < q.ports.count; ++i) {
-    const kgpu_port w = st.qp.ports[q.ports.begin + i];
+    const kgpu_port w = cp(st.qp.ports)[q.ports.begin + i];
     for (int s = 0; s < have; ++s) {
-      const kgpu_port p = st.ports[(size_t)s * st.N + n];
+      const kgpu_port p = gp(st.ports)[(size_t)s * st.N + n];
       if (p.port == w.port && p.proto == w.proto && (w.ip == 0 || p.ip == 0 || p.ip == w.ip)) return true;
     }
   }
@@ -153,18 +191,19 @@ __device__ __forceinline__ bool ports_conflict(const DevState& st, const kgpu_po
 
 __device__ __forceinline__ bool taints_ok(const DevState& st, const kgpu_pod_query& q, int n) {
   for (int w = 0; w < st.TW; ++w) {
-    const uint64_t t = st.taint_nosched[(size_t)w * st.N + n];
-    const uint64_t tol = w < q.tol_nosched.count ? st.qp.words[q.tol_nosched.begin + w] : 0ull;
+    const uint64_t t = gp(st.taint_nosched)[(size_t)w * st.N + n];
+    const uint64_t tol = w < q.tol_nosched.count ? cp(st.qp.words)[q.tol_nosched.begin + w] : 0ull;
     if (t & ~tol) return false;
   }
   return true;
 }
 
 __device__ __forceinline__ int taint_raw(const DevState& st, const kgpu_pod_query& q, int n) {
+  if (!st.any_prefer_taint) return 0;
   int c = 0;
   for (int w = 0; w < st.TW; ++w) {
-    const uint64_t t = st.taint_prefer[(size_t)w * st.N + n];
-    const uint64_t tol = w < q.tol_prefer.count ? st.qp.words[q.tol_prefer.begin + w] : 0ull;
+    const uint64_t t = gp(st.taint_prefer)[(size_t)w * st.N + n];
+    const uint64_t tol = w < q.tol_prefer.count ? cp(st.qp.words)[q.tol_prefer.begin + w] : 0ull;
     c += __popcll(t & ~tol);
   }
   return c;
@@ -173,7 +212,7 @@ __device__ __forceinline__ int taint_raw(const DevState& st, const kgpu_pod_quer
 __device__ __forceinline__ int na_raw(const DevState& st, const kgpu_pod_query& q, int n) {
   int s = 0;
   for (int t = 0; t < q.pref_terms.count; ++t) {
-    const kgpu_pref_term pt = st.qp.pref_terms[q.pref_terms.begin + t];
+    const kgpu_pref_term pt = cp(st.qp.pref_terms)[q.pref_terms.begin + t];
     if (pt.sel.kind == KGPU_SEL_NOTHING) continue;
     if (node_reqs_all(st, pt.sel.reqs, n)) s += pt.weight;
   }
@@ -182,7 +221,7 @@ __device__ __forceinline__ int na_raw(const DevState& st, const kgpu_pod_query& 
 
 __device__ __forceinline__ int64_t pod_scalar_score(const DevState& st, const kgpu_pod_query& q, int col) {
   for (int i = 0; i < q.scalars.count; ++i) {
-    const kgpu_scalar_req s = st.qp.scalars[q.scalars.begin + i];
+    const kgpu_scalar_req s = cp(st.qp.scalars)[q.scalars.begin + i];
     if (s.col == col) return s.score_value;
   }
   return 0;
@@ -212,8 +251,8 @@ __device__ __forceinline__ void alloc_req(const DevState& st, const kgpu_pod_que
     default:
       if (res >= 3) {
         const int col = res - 3;
-        cap = st.alloc_scalar[(size_t)col * st.N + n];
-        req = st.req_scalar[(size_t)col * st.N + n] + pod_scalar_score(st, q, col);
+        cap = gp(st.alloc_scalar)[(size_t)col * st.N + n];
+        req = gp(st.req_scalar)[(size_t)col * st.N + n] + pod_scalar_score(st, q, col);
       } else {
         cap = 0;
         req = 0;
@@ -221,28 +260,71 @@ __device__ __forceinline__ void alloc_req(const DevState& st, const kgpu_pod_que
   }
 }
 
-__device__ __forceinline__ int64_t least_score(const DevState& st, const kgpu_pod_query& q, const NodeRes& nr,
-                                               int n) {
-  int64_t s = 0;
-  for (int i = 0; i < st.n_least; ++i) {
-    int64_t cap, req;
-    alloc_req(st, q, nr, st.least[i].resource, n, cap, req);
-    const int64_t r = (cap == 0 || req > cap) ? 0 : (cap > 0 ? div_nonneg((cap - req) * 100, cap) : ((cap - req) * 100) / cap);
-    s += r * st.least[i].weight;
-  }
-  return s >= 0 ? div_nonneg(s, st.least_wsum) : s / st.least_wsum;
+// floor(a / b) for 0 <= a < 2^52, 0 < b < 2^52 from a precomputed inv ~ 1/b: the product is within
+// one of the quotient, and the remainder test makes the result exact.
+__device__ __forceinline__ int64_t div_recip(int64_t a, int64_t b, double inv) {
+  int64_t q = (int64_t)((double)a * inv);
+  const int64_t r = a - q * b;
+  if (r < 0) q -= 1;
+  else if (r >= b) q += 1;
+  return q;
 }
 
+// leastResourceScorer / mostResourceScorer per resource (least_allocated.go:93-101,
+// most_allocated.go:93-107), Go's truncating int64 arithmetic.
+__device__ __forceinline__ int64_t least_one(int64_t cap, int64_t req) {
+  if (cap == 0 || req > cap) return 0;
+  return cap > 0 ? div_nonneg((cap - req) * 100, cap) : ((cap - req) * 100) / cap;
+}
+__device__ __forceinline__ int64_t most_one(int64_t cap, int64_t req) {
+  if (cap == 0 || req > cap) return 0;
+  return (req >= 0 && cap > 0) ? div_nonneg(req * 100, cap) : (req * 100) / cap;
+}
+__device__ __forceinline__ int64_t least_one(int64_t cap, int64_t req, double inv) {
+  if (cap == 0 || req > cap) return 0;
+  const int64_t x = (cap - req) * 100;
+  if (inv != 0.0 && x >= 0 && x < (1ll << 52)) return div_recip(x, cap, inv);
+  return least_one(cap, req);
+}
+__device__ __forceinline__ int64_t most_one(int64_t cap, int64_t req, double inv) {
+  if (cap == 0 || req > cap) return 0;
+  const int64_t x = req * 100;
+  if (inv != 0.0 && x >= 0 && x < (1ll << 52)) return div_recip(x, cap, inv);
+  return most_one(cap, req);
+}
+__device__ __forceinline__ int64_t wdiv(int64_t s, int64_t w) { return s >= 0 ? div_nonneg(s, w) : s / w; }
+__device__ __forceinline__ int64_t half(int64_t s) { return s >= 0 ? (s >> 1) : s / 2; }
+
+template <bool kDef>
+__device__ __forceinline__ int64_t least_score(const DevState& st, const kgpu_pod_query& q, const NodeRes& nr,
+                                               int n) {
+  if constexpr (kDef) {
+    return half(least_one(nr.ac, nr.zc + q.score_req[0], nr.ic) + least_one(nr.am, nr.zm + q.score_req[1], nr.im));
+  } else {
+    int64_t s = 0;
+    for (int i = 0; i < st.n_least; ++i) {
+      int64_t cap, req;
+      alloc_req(st, q, nr, st.least[i].resource, n, cap, req);
+      s += least_one(cap, req) * st.least[i].weight;
+    }
+    return wdiv(s, st.least_wsum);
+  }
+}
+
+template <bool kDef>
 __device__ __forceinline__ int64_t most_score(const DevState& st, const kgpu_pod_query& q, const NodeRes& nr,
                                               int n) {
-  int64_t s = 0;
-  for (int i = 0; i < st.n_most; ++i) {
-    int64_t cap, req;
-    alloc_req(st, q, nr, st.most[i].resource, n, cap, req);
-    const int64_t r = (cap == 0 || req > cap) ? 0 : (req >= 0 && cap > 0 ? div_nonneg(req * 100, cap) : (req * 100) / cap);
-    s += r * st.most[i].weight;
+  if constexpr (kDef) {
+    return half(most_one(nr.ac, nr.zc + q.score_req[0], nr.ic) + most_one(nr.am, nr.zm + q.score_req[1], nr.im));
+  } else {
+    int64_t s = 0;
+    for (int i = 0; i < st.n_most; ++i) {
+      int64_t cap, req;
+      alloc_req(st, q, nr, st.most[i].resource, n, cap, req);
+      s += most_one(cap, req) * st.most[i].weight;
+    }
+    return wdiv(s, st.most_wsum);
   }
-  return s >= 0 ? div_nonneg(s, st.most_wsum) : s / st.most_wsum;
 }
 
 // balancedResourceScorer (balanced_allocation.go:83-120): IEEE double, no contraction.
@@ -259,16 +341,18 @@ __device__ __forceinline__ int64_t balanced_score(const kgpu_pod_query& q, const
 __device__ __forceinline__ int64_t image_score(const DevState& st, const kgpu_pod_query& q, int n) {
   constexpr int64_t MB = 1024 * 1024, kMin = 23 * MB, kMaxC = 1000 * MB;
   int64_t sum = 0;
-  const int lo0 = st.image_off[n], hi0 = st.image_off[n + 1];
-  for (int i = 0; i < q.images.count; ++i) {
-    const int id = st.qp.ints[q.images.begin + i];
-    if (id < 0) continue;
-    int lo = lo0, hi = hi0;
-    while (lo < hi) {
-      const int mid = (lo + hi) >> 1;
-      if (st.image_id[mid] < id) lo = mid + 1; else hi = mid;
+  if (q.images.count) {
+    const int lo0 = gp(st.image_off)[n], hi0 = gp(st.image_off)[n + 1];
+    for (int i = 0; i < q.images.count; ++i) {
+      const int id = cp(st.qp.ints)[q.images.begin + i];
+      if (id < 0) continue;
+      int lo = lo0, hi = hi0;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (gp(st.image_id)[mid] < id) lo = mid + 1; else hi = mid;
+      }
+      if (lo < hi0 && gp(st.image_id)[lo] == id) sum += gp(st.image_score)[lo];
     }
-    if (lo < hi0 && st.image_id[lo] == id) sum += st.image_score[lo];
   }
   const int64_t maxT = kMaxC * (int64_t)q.n_containers;
   if (sum < kMin) sum = kMin;
@@ -278,15 +362,15 @@ __device__ __forceinline__ int64_t image_score(const DevState& st, const kgpu_po
 
 __device__ __forceinline__ int64_t npap_score(const DevState& st, const kgpu_pod_query& q, int n) {
   if (q.avoid_id < 0) return 100;
-  for (int i = st.avoid_off[n]; i < st.avoid_off[n + 1]; ++i)
-    if (st.avoid_id[i] == q.avoid_id) return 0;
+  for (int i = gp(st.avoid_off)[n]; i < gp(st.avoid_off)[n + 1]; ++i)
+    if (gp(st.avoid_id)[i] == q.avoid_id) return 0;
   return 100;
 }
 
 // DefaultPodTopologySpread with an empty selector (every count is 0): 100 off-zone; zoned
 // nodes get fScore*(1-zoneWeighting) + zoneWeighting*100 (default_pod_topology_spread.go:136-162).
 __device__ __forceinline__ int64_t dpts_empty_score(const DevState& st, int n) {
-  if (st.zone_id[n] < 0) return 100;
+  if (gp(st.zone_id)[n] < 0) return 100;
   const double zw = 2.0 / 3.0;
   const double f = (100.0 * (1.0 - zw)) + (zw * 100.0);
   return (int64_t)f;
@@ -300,86 +384,120 @@ struct NodeEval {
   int32_t na;       // raw NodeAffinity score
 };
 
-__device__ __forceinline__ uint32_t run_filters(const DevState& st, const kgpu_pod_query& q, const NodeRes& r,
-                                                int n) {
-  for (int i = 0; i < st.n_filters; ++i) {
-    const int f = st.filters[i];
-    const uint32_t pos = (uint32_t)(i + 1);
-    switch (f) {
-      case KGPU_F_NODE_UNSCHEDULABLE:
-        if (st.unsched[n] && !(q.flags & KGPU_Q_TOLERATES_UNSCHEDULABLE))
-          return pos | (KGPU_CODE_UNRESOLVABLE << 8);
-        break;
-      case KGPU_F_NODE_RESOURCES_FIT: {
-        const uint32_t d = fit_detail(st, q, r, n);
-        if (d) return pos | (KGPU_CODE_UNSCHEDULABLE << 8) | (d << 16);
-        break;
-      }
-      case KGPU_F_NODE_NAME:
-        if (q.node_name != -1 && q.node_name != st.node_base + n) return pos | (KGPU_CODE_UNRESOLVABLE << 8);
-        break;
-      case KGPU_F_NODE_PORTS:
-        if (q.ports.count && ports_conflict(st, q, n)) return pos | (KGPU_CODE_UNSCHEDULABLE << 8);
-        break;
-      case KGPU_F_NODE_AFFINITY:
-        if (!node_affinity_ok(st, q, n)) return pos | (KGPU_CODE_UNRESOLVABLE << 8);
-        break;
-      case KGPU_F_TAINT_TOLERATION:
-        if (!taints_ok(st, q, n)) return pos | (KGPU_CODE_UNRESOLVABLE << 8);
-        break;
-      default:  // PodTopologySpread / InterPodAffinity: pass for pods without constraints
-        break;
+// One Filter plugin: 0 = Success, else (code << 8) | (detail << 16) of the status word.
+__device__ __forceinline__ uint32_t filter_one(int f, const DevState& st, const kgpu_pod_query& q, const NodeRes& r,
+                                               int n) {
+  switch (f) {
+    case KGPU_F_NODE_UNSCHEDULABLE:
+      if (gp(st.unsched)[n] && !(q.flags & KGPU_Q_TOLERATES_UNSCHEDULABLE)) return KGPU_CODE_UNRESOLVABLE << 8;
+      return 0;
+    case KGPU_F_NODE_RESOURCES_FIT: {
+      const uint32_t d = fit_detail(st, q, r, n);
+      return d ? (KGPU_CODE_UNSCHEDULABLE << 8) | (d << 16) : 0;
     }
+    case KGPU_F_NODE_NAME:
+      return (q.node_name != -1 && q.node_name != st.node_base + n) ? KGPU_CODE_UNRESOLVABLE << 8 : 0;
+    case KGPU_F_NODE_PORTS:
+      return (q.ports.count && ports_conflict(st, q, n)) ? KGPU_CODE_UNSCHEDULABLE << 8 : 0;
+    case KGPU_F_NODE_AFFINITY:
+      return node_affinity_ok(st, q, n) ? 0 : KGPU_CODE_UNRESOLVABLE << 8;
+    case KGPU_F_TAINT_TOLERATION:
+      return taints_ok(st, q, n) ? 0 : KGPU_CODE_UNRESOLVABLE << 8;
+    default:  // PodTopologySpread / InterPodAffinity: pass for pods without constraints
+      return 0;
   }
-  return 0;
 }
 
+// Filters in profile order; the first failure's 1-based position goes in the low byte.
+template <uint32_t FM, int F = 0>
+__device__ __forceinline__ uint32_t run_filters(const DevState& st, const kgpu_pod_query& q, const NodeRes& r, int n) {
+  if constexpr (FM == kRuntime) {
+    for (int i = 0; i < st.n_filters; ++i) {
+      const uint32_t c = filter_one(cp(st.filters)[i], st, q, r, n);
+      if (c) return c | (uint32_t)(i + 1);
+    }
+    return 0;
+  } else if constexpr (F >= KGPU_NUM_FILTERS) {
+    return 0;
+  } else {
+    if constexpr ((FM >> F) & 1u) {
+      constexpr uint32_t pos = __builtin_popcount(FM & ((2u << F) - 1));
+      const uint32_t c = filter_one(F, st, q, r, n);
+      if (c) return c | pos;
+    }
+    return run_filters<FM, F + 1>(st, q, r, n);
+  }
+}
+
+// One Score plugin's raw value (TaintToleration / NodeAffinity go to e.taint / e.na: they are
+// normalized over the feasible set before weighting).
+template <bool kDef>
+__device__ __forceinline__ int64_t score_one(int s, const DevState& st, const kgpu_pod_query& q, const NodeRes& r,
+                                             int n, NodeEval& e) {
+  switch (s) {
+    case KGPU_S_BALANCED_ALLOCATION: return balanced_score(q, r);
+    case KGPU_S_LEAST_ALLOCATED: return least_score<kDef>(st, q, r, n);
+    case KGPU_S_MOST_ALLOCATED: return most_score<kDef>(st, q, r, n);
+    case KGPU_S_IMAGE_LOCALITY: return image_score(st, q, n);
+    case KGPU_S_NODE_PREFER_AVOID_PODS: return npap_score(st, q, n);
+    case KGPU_S_POD_TOPOLOGY_SPREAD: return 100;  // no soft constraints: max == 0
+    case KGPU_S_DEFAULT_POD_TOPOLOGY_SPREAD: return (q.flags & KGPU_Q_HAS_TSC) ? 0 : dpts_empty_score(st, n);
+    case KGPU_S_INTER_POD_AFFINITY: return 0;     // empty topologyScore
+    case KGPU_S_TAINT_TOLERATION: e.taint = taint_raw(st, q, n); return e.taint;
+    case KGPU_S_NODE_AFFINITY: e.na = na_raw(st, q, n); return e.na;
+    default: return 0;
+  }
+}
+
+__device__ __forceinline__ bool normalized(int s) {
+  return s == KGPU_S_TAINT_TOLERATION || s == KGPU_S_NODE_AFFINITY;
+}
+
+template <uint32_t SM, int S = 0>
 __device__ __forceinline__ void run_scores(const DevState& st, const kgpu_pod_query& q, const NodeRes& r, int n,
                                            NodeEval& e, bool diag) {
-  int64_t part = 0;
-  for (int i = 0; i < st.n_scores; ++i) {
-    const int s = st.scores[i];
-    int64_t v = 0;
-    switch (s) {
-      case KGPU_S_BALANCED_ALLOCATION: v = balanced_score(q, r); break;
-      case KGPU_S_LEAST_ALLOCATED: v = least_score(st, q, r, n); break;
-      case KGPU_S_MOST_ALLOCATED: v = most_score(st, q, r, n); break;
-      case KGPU_S_IMAGE_LOCALITY: v = image_score(st, q, n); break;
-      case KGPU_S_NODE_PREFER_AVOID_PODS: v = npap_score(st, q, n); break;
-      case KGPU_S_POD_TOPOLOGY_SPREAD: v = 100; break;           // no soft constraints: max == 0
-      case KGPU_S_DEFAULT_POD_TOPOLOGY_SPREAD:
-        v = (q.flags & KGPU_Q_HAS_TSC) ? 0 : dpts_empty_score(st, n);
-        break;
-      case KGPU_S_INTER_POD_AFFINITY: v = 0; break;              // empty topologyScore
-      case KGPU_S_TAINT_TOLERATION:
-        e.taint = taint_raw(st, q, n);
-        if (diag) st.diag_raw[(size_t)s * st.N + n] = e.taint;
-        continue;
-      case KGPU_S_NODE_AFFINITY:
-        e.na = na_raw(st, q, n);
-        if (diag) st.diag_raw[(size_t)s * st.N + n] = e.na;
-        continue;
-      default: break;
+  if constexpr (SM == kRuntime) {
+    int64_t part = 0;
+    for (int i = 0; i < st.n_scores; ++i) {
+      const int s = cp(st.scores)[i];
+      const int64_t v = score_one<false>(s, st, q, r, n, e);
+      if (diag) gp(st.diag_raw)[(size_t)s * st.N + n] = v;
+      if (!normalized(s)) part += v * cp(st.w_of)[s];
     }
-    if (diag) st.diag_raw[(size_t)s * st.N + n] = v;
-    part += v * st.weights[i];
+    e.partial = part;
+  } else if constexpr (S >= KGPU_NUM_SCORES) {
+    return;
+  } else {
+    if constexpr ((SM >> S) & 1u) {
+      const int64_t v = score_one<(SM & kDefRes) != 0>(S, st, q, r, n, e);
+      if (diag) gp(st.diag_raw)[(size_t)S * st.N + n] = v;
+      if constexpr (!(S == KGPU_S_TAINT_TOLERATION || S == KGPU_S_NODE_AFFINITY)) e.partial += v * st.w_of[S];
+    }
+    run_scores<SM, S + 1>(st, q, r, n, e, diag);
   }
-  e.partial = part;
 }
 
+// DefaultNormalizeScore of the two normalized plugins (reverse for TaintToleration), weighted.
+// Plugins not in the profile have weight 0 in w_of.
 __device__ __forceinline__ int64_t norm_total(const DevState& st, int64_t partial, int taint, int na, int maxT,
                                               int maxNA) {
-  int64_t t = partial;
-  for (int i = 0; i < st.n_scores; ++i) {
-    if (st.scores[i] == KGPU_S_TAINT_TOLERATION) {
-      const int64_t v = maxT == 0 ? 100 : 100 - (100 * (int64_t)taint) / maxT;
-      t += v * st.weights[i];
-    } else if (st.scores[i] == KGPU_S_NODE_AFFINITY) {
-      const int64_t v = maxNA == 0 ? (int64_t)na : (100 * (int64_t)na) / maxNA;
-      t += v * st.weights[i];
-    }
+  const int64_t vt = maxT == 0 ? 100 : 100 - (100 * (int64_t)taint) / maxT;
+  const int64_t vn = maxNA == 0 ? (int64_t)na : (100 * (int64_t)na) / maxNA;
+  return partial + vt * st.w_of[KGPU_S_TAINT_TOLERATION] + vn * st.w_of[KGPU_S_NODE_AFFINITY];
+}
+
+template <uint32_t SM>
+__device__ __forceinline__ int64_t key_total(const DevState& st, int64_t partial, int taint, int na) {
+  if constexpr (SM == kRuntime) {
+    return st.n_scores ? norm_total(st, partial, taint, na, 0, 0) : 1;
+  } else if constexpr ((SM & kSMask) == 0) {
+    return 1;
+  } else {
+    int64_t t = partial;
+    if constexpr ((SM >> KGPU_S_TAINT_TOLERATION) & 1u) t += 100 * st.w_of[KGPU_S_TAINT_TOLERATION];
+    if constexpr ((SM >> KGPU_S_NODE_AFFINITY) & 1u) t += (int64_t)na * st.w_of[KGPU_S_NODE_AFFINITY];
+    return t;
   }
-  return t;
 }
 
 // ---------------------------------------------------------------- reductions
@@ -415,14 +533,28 @@ struct Winner {
 };
 
 // selectHost over the partials of a finished launch, computed by every wave on its own (lanes
-// stride over the <= kMaxBlocks partials, then a 64-lane shuffle reduction): no LDS, no barrier.
+// stride over the <= kMaxBlocks partials, four loads in flight per lane, then a 64-lane shuffle
+// reduction): no LDS, no barrier.
 __device__ __forceinline__ Winner wave_winner(const BlkKey* kb, int nb) {
   uint64_t k = 0;
   int idx = -1, f = 0;
-  for (int b = threadIdx.x & 63; b < nb; b += 64) {
-    const BlkKey p = kb[b];
-    key_max(k, idx, p.key, p.idx);
-    f += p.feasible;
+  const GAS BlkKey* g = gp(kb);
+  for (int b = threadIdx.x & 63; b < nb; b += 256) {
+    BlkKey p[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      p[j] = BlkKey{0, -1, 0};
+      if (b + 64 * j < nb) {
+        p[j].key = g[b + 64 * j].key;
+        p[j].idx = g[b + 64 * j].idx;
+        p[j].feasible = g[b + 64 * j].feasible;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      key_max(k, idx, p[j].key, p[j].idx);
+      f += p[j].feasible;
+    }
   }
   wave_reduce_key(k, idx);
   f = wave_reduce_sum(f);
@@ -438,36 +570,36 @@ __device__ void assume_row(const DevState& st, const kgpu_pod_query& q, NodeRes&
   r.zc += q.nz[0];
   r.zm += q.nz[1];
   r.np += 1;
-  st.req_cpu[n] = r.rc;
-  st.req_mem[n] = r.rm;
-  st.req_eph[n] = r.re;
-  st.nz_cpu[n] = r.zc;
-  st.nz_mem[n] = r.zm;
-  st.num_pods[n] = r.np;
+  gp(st.req_cpu)[n] = r.rc;
+  gp(st.req_mem)[n] = r.rm;
+  gp(st.req_eph)[n] = r.re;
+  gp(st.nz_cpu)[n] = r.zc;
+  gp(st.nz_mem)[n] = r.zm;
+  gp(st.num_pods)[n] = r.np;
   for (int i = 0; i < q.scalars.count; ++i) {
-    const kgpu_scalar_req s = st.qp.scalars[q.scalars.begin + i];
-    if (s.col >= 0) st.req_scalar[(size_t)s.col * st.N + n] += s.value;
+    const kgpu_scalar_req s = cp(st.qp.scalars)[q.scalars.begin + i];
+    if (s.col >= 0) gp(st.req_scalar)[(size_t)s.col * st.N + n] += s.value;
   }
   if (q.ports.count) {
-    int pc = st.port_count[n];
+    int pc = gp(st.port_count)[n];
     for (int i = 0; i < q.ports.count && pc < st.PS; ++i) {
-      const kgpu_port w = st.qp.ports[q.ports.begin + i];
+      const kgpu_port w = cp(st.qp.ports)[q.ports.begin + i];
       bool dup = false;
       for (int s = 0; s < pc; ++s) {
-        const kgpu_port p = st.ports[(size_t)s * st.N + n];
+        const kgpu_port p = gp(st.ports)[(size_t)s * st.N + n];
         if (p.ip == w.ip && p.proto == w.proto && p.port == w.port) dup = true;
       }
-      if (!dup) st.ports[(size_t)(pc++) * st.N + n] = w;
+      if (!dup) gp(st.ports)[(size_t)(pc++) * st.N + n] = w;
     }
-    st.port_count[n] = pc;
+    gp(st.port_count)[n] = pc;
   }
 }
 
 // The pending pod's outcome (generic_scheduler.go:171-208): FitError, the len==1 shortcut, or
-// the scored winner.  placed_idx = local row to assume (-1 none).
-__device__ __forceinline__ int settle_prev(const DevState& st, const PodArgs& a, const Winner& w) {
-  const kgpu_pod_query& q = st.queries[a.prev];
-  const bool error = (q.flags & KGPU_Q_SCORE_ERROR) && w.feasible >= 2;
+// the scored winner.  Returns the local row to assume (-1 none).
+__device__ __forceinline__ int settle_prev(const DevState& st, const PodArgs& a, const kgpu_pod_query& pq,
+                                           const Winner& w) {
+  const bool error = (pq.flags & KGPU_Q_SCORE_ERROR) && w.feasible >= 2;
   const bool placed = w.feasible > 0 && !error;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     kgpu_result r;
@@ -476,7 +608,7 @@ __device__ __forceinline__ int settle_prev(const DevState& st, const PodArgs& a,
     r.evaluated = st.n_total;
     r.scored = (placed && w.feasible >= 2) ? 1 : 0;
     r.score = r.scored ? (int64_t)(w.key >> 40) : 0;
-    st.results[a.prev] = r;
+    gp(st.results)[a.prev] = r;
   }
   return (placed && a.assume) ? w.idx : -1;
 }
@@ -490,6 +622,7 @@ __device__ __forceinline__ void chunk_of(int N, int& lo, int& hi) {
 // ---------------------------------------------------------------- kernels
 // One workgroup = one wave64: the workgroup argmax is a pure shuffle reduction (no LDS, no
 // barrier), and every wave resolves the previous pod's winner on its own.
+template <uint32_t FM, uint32_t SM>
 __global__ __launch_bounds__(kBlock) void k_eval(const DevState* __restrict__ stp, PodArgs a) {
   const DevState& st = *stp;
   int lo, hi;
@@ -499,11 +632,12 @@ __global__ __launch_bounds__(kBlock) void k_eval(const DevState* __restrict__ st
   // partials -- so that their latencies overlap instead of chaining.
   NodeRes r0{};
   if (n0 < hi) r0 = load_res(st, n0);
-  const kgpu_pod_query q = st.queries[a.pod];
+  const kgpu_pod_query q = *cp(st.queries + a.pod);
   int assume_idx = -1;
+  const kgpu_pod_query* pq = st.queries + (a.prev >= 0 ? a.prev : 0);
   if (a.prev >= 0) {
     const Winner w = wave_winner(st.kbuf + (size_t)a.prev_parity * kMaxBlocks, a.prev_blocks);
-    assume_idx = settle_prev(st, a, w);
+    assume_idx = settle_prev(st, a, *cp(pq), w);
   }
   const uint64_t tk = pod_tie_key(st.seed, a.seq);
   const bool write_nodes = a.norm || a.diag;
@@ -512,26 +646,26 @@ __global__ __launch_bounds__(kBlock) void k_eval(const DevState* __restrict__ st
   int best_i = -1, feas = 0, maxT = 0, maxNA = 0;
   for (int n = n0; n < hi; n += kBlock) {
     NodeRes r = (n == n0) ? r0 : load_res(st, n);
-    if (n == assume_idx) assume_row(st, st.queries[a.prev], r, n);
+    if (n == assume_idx) assume_row(st, *cp(pq), r, n);
     NodeEval e{0, 0, 0, 0};
-    e.status = run_filters(st, q, r, n);
+    e.status = run_filters<FM>(st, q, r, n);
     if (e.status == 0) {
-      run_scores(st, q, r, n, e, a.diag);
+      run_scores<SM>(st, q, r, n, e, a.diag);
       ++feas;
       maxT = max(maxT, e.taint);
       maxNA = max(maxNA, e.na);
       if (!a.norm) {
         // constant DefaultNormalizeScore maxima: every raw TaintToleration / NodeAffinity score is 0
-        const int64_t total = st.n_scores ? norm_total(st, e.partial, e.taint, e.na, 0, 0) : 1;
+        const int64_t total = key_total<SM>(st, e.partial, e.taint, e.na);
         const uint64_t key = ((uint64_t)total << 40) | rank40(tk, (uint64_t)(st.node_base + n), st.tie_mode);
         key_max(best, best_i, key, n);
       }
     }
     if (write_nodes) {
-      st.status[n] = e.status;
-      st.partial[n] = e.partial;
-      st.raw_taint[n] = e.taint;
-      st.raw_na[n] = e.na;
+      gp(st.status)[n] = e.status;
+      gp(st.partial)[n] = e.partial;
+      gp(st.raw_taint)[n] = e.taint;
+      gp(st.raw_na)[n] = e.na;
     }
   }
   wave_reduce_key(best, best_i);
@@ -539,8 +673,8 @@ __global__ __launch_bounds__(kBlock) void k_eval(const DevState* __restrict__ st
   maxT = wave_reduce_max(maxT);
   maxNA = wave_reduce_max(maxNA);
   if (threadIdx.x == 0) {
-    st.sbuf[(size_t)a.parity * kMaxBlocks + blockIdx.x] = BlkStat{feas, maxT, maxNA, 0};
-    if (!a.norm) st.kbuf[(size_t)a.parity * kMaxBlocks + blockIdx.x] = BlkKey{best, best_i, feas};
+    gp(st.sbuf)[(size_t)a.parity * kMaxBlocks + blockIdx.x] = BlkStat{feas, maxT, maxNA, 0};
+    if (!a.norm) gp(st.kbuf)[(size_t)a.parity * kMaxBlocks + blockIdx.x] = BlkKey{best, best_i, feas};
   }
 }
 
@@ -549,7 +683,7 @@ __global__ __launch_bounds__(kBlock) void k_eval(const DevState* __restrict__ st
 __global__ __launch_bounds__(kBlock) void k_final(const DevState* __restrict__ stp, PodArgs a, int stat_blocks) {
   const DevState& st = *stp;
   int maxT = 0, maxNA = 0;
-  const BlkStat* sb = st.sbuf + (size_t)a.parity * kMaxBlocks;
+  const GAS BlkStat* sb = gp(st.sbuf) + (size_t)a.parity * kMaxBlocks;
   for (int b = threadIdx.x; b < stat_blocks; b += kBlock) {
     const BlkStat p = sb[b];
     maxT = max(maxT, p.max_taint);
@@ -563,24 +697,25 @@ __global__ __launch_bounds__(kBlock) void k_final(const DevState* __restrict__ s
   uint64_t best = 0;
   int best_i = -1, bf = 0;
   for (int n = lo + threadIdx.x; n < hi; n += kBlock) {
-    if (st.status[n] != 0) continue;
+    if (gp(st.status)[n] != 0) continue;
     ++bf;
-    const int64_t total = st.n_scores ? norm_total(st, st.partial[n], st.raw_taint[n], st.raw_na[n], maxT, maxNA) : 1;
+    const int64_t total =
+        st.n_scores ? norm_total(st, gp(st.partial)[n], gp(st.raw_taint)[n], gp(st.raw_na)[n], maxT, maxNA) : 1;
     const uint64_t key = ((uint64_t)total << 40) | rank40(tk, (uint64_t)(st.node_base + n), st.tie_mode);
     key_max(best, best_i, key, n);
     if (a.diag) {
       for (int i = 0; i < st.n_scores; ++i) {
         const int s = st.scores[i];
-        int64_t v = st.diag_raw[(size_t)s * st.N + n];
+        int64_t v = gp(st.diag_raw)[(size_t)s * st.N + n];
         if (s == KGPU_S_TAINT_TOLERATION) v = maxT == 0 ? 100 : 100 - (100 * v) / maxT;
         if (s == KGPU_S_NODE_AFFINITY) v = maxNA == 0 ? v : (100 * v) / maxNA;
-        st.diag_norm[(size_t)s * st.N + n] = v;
+        gp(st.diag_norm)[(size_t)s * st.N + n] = v;
       }
     }
   }
   wave_reduce_key(best, best_i);
   bf = wave_reduce_sum(bf);
-  if (threadIdx.x == 0) st.kbuf[(size_t)a.parity * kMaxBlocks + blockIdx.x] = BlkKey{best, best_i, bf};
+  if (threadIdx.x == 0) gp(st.kbuf)[(size_t)a.parity * kMaxBlocks + blockIdx.x] = BlkKey{best, best_i, bf};
 }
 
 // Resolve-only launch (end of a batch / single cycle), with the evaluation grid's chunk mapping
@@ -590,11 +725,450 @@ __global__ __launch_bounds__(kBlock) void k_resolve(const DevState* __restrict__
   int lo, hi;
   chunk_of(st.N, lo, hi);
   const Winner w = wave_winner(st.kbuf + (size_t)a.prev_parity * kMaxBlocks, a.prev_blocks);
-  const int idx = settle_prev(st, a, w);
+  const kgpu_pod_query pq = *cp(st.queries + a.prev);
+  const int idx = settle_prev(st, a, pq, w);
   if (idx >= lo && idx < hi && ((idx - lo) % kBlock) == (int)threadIdx.x) {
     NodeRes r = load_res(st, idx);
-    assume_row(st, st.queries[a.prev], r, idx);
+    assume_row(st, pq, r, idx);
   }
+}
+
+// ---------------------------------------------------------------- persistent batch kernel
+// A run of pods in queue order inside ONE launch.  Workgroup g owns nodes [g*per, (g+1)*per) and
+// keeps their resource rows in registers for the whole run (K rows per lane).  Per pod it
+// publishes one 8-byte granule -- valid bit | ((score+1) << 40 | rank40), 0 key = no feasible
+// node -- with a write-through (sc1) store into the pod's own slot row; wave 0 polls the row with
+// sc1 loads until every workgroup's granule is there, and every workgroup then derives the same
+// winner.  Slots are written once per launch (zeroed by the host), so a granule is its own flag.
+//
+// Software pipeline (one pod in flight): while pod i-1's granules travel, every workgroup already
+// evaluates pod i twice -- variant A on its rows as they are, variant B with pod i-1 assumed on
+// its own candidate for pod i-1 (the only row that changes if this workgroup wins i-1) -- and
+// publishes the right variant as soon as pod i-1 resolves.  Per pod the critical path is one
+// granule hop; the node evaluation overlaps it.  When the previous pod carries extended
+// resources or host ports (their columns live in memory) the winner re-evaluates its one row
+// after the assume instead.
+//
+// The chosen variant's feasible count goes to a side array; k_batch_fixup fills in
+// FeasibleNodes and the scored flag after the launch.  A workgroup that waits longer than
+// kSpinTimeout (lost co-residency) raises the abort word and every workgroup leaves the loop.
+constexpr uint64_t kGValid = 1ull << 63;
+constexpr uint64_t kSpinTimeout = 50000000ull;  // s_memrealtime ticks (100 MHz): 0.5 s
+
+__device__ __forceinline__ void store_sc1(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t load_sc1(const uint64_t* p) {
+  return __hip_atomic_load(const_cast<uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int load_sc1(const int32_t* p) {
+  return __hip_atomic_load(const_cast<int32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// NodeInfo.AddPod on a register copy only (the variant-B row): resource columns and pod count.
+__device__ __forceinline__ void assume_regs(const kgpu_pod_query& q, NodeRes& r) {
+  r.rc += q.req[0];
+  r.rm += q.req[1];
+  r.re += q.req[2];
+  r.zc += q.nz[0];
+  r.zm += q.nz[1];
+  r.np += 1;
+}
+
+// Key of one node for one pod: 0 = infeasible, else ((score+1) << 40) | rank40.
+template <uint32_t FM, uint32_t SM>
+__device__ __forceinline__ uint64_t node_key(const DevState& st, const kgpu_pod_query& q, const NodeRes& r, int n,
+                                             uint64_t tk) {
+  if (run_filters<FM>(st, q, r, n) != 0) return 0;
+  NodeEval e{0, 0, 0, 0};
+  run_scores<SM>(st, q, r, n, e, false);
+  const int64_t total = key_total<SM>(st, e.partial, e.taint, e.na);
+  return ((uint64_t)(total + 1) << 40) | rank40(tk, (uint64_t)(st.node_base + n), st.tie_mode);
+}
+
+struct Cand {
+  uint64_t key;
+  int idx;    // local node index within the workgroup's range
+  int feas;
+};
+
+__device__ __forceinline__ void wave_reduce_cand(Cand& c) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const uint64_t k2 = __shfl_xor(c.key, off);
+    const int i2 = __shfl_xor(c.idx, off);
+    c.feas += __shfl_xor(c.feas, off);
+    if (k2 > c.key) { c.key = k2; c.idx = i2; }
+  }
+}
+
+template <int B>
+struct BatchShared {
+  static constexpr int W = B / 64;
+  uint64_t ka[W], kb[W];
+  int ia[W], ib[W], fa[W], fb[W];
+  uint64_t wkey;   // winning key of the resolved pod
+  int wg;          // its workgroup (-1: no feasible node)
+  int abort;
+  int cand;        // this workgroup's candidate (local index) for the pod just published, -1 none
+};
+
+// Per-lane best over its K rows, then the workgroup's best through shuffles + LDS (variant A, and
+// variant B when `vb`: slot jb of lane `ob` replaced by keyb).  Leaves the wave partials in LDS.
+template <int K, int B>
+__device__ __forceinline__ void wg_partials(BatchShared<B>& sh, const uint64_t (&keys)[K], int lo_tid, bool vb,
+                                            int ob, int jb, uint64_t keyb) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  Cand a{0, -1, 0}, b{0, -1, 0};
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    const int l = j * B + lo_tid;
+    const uint64_t k = keys[j];
+    if (k) {
+      ++a.feas;
+      if (k > a.key) { a.key = k; a.idx = l; }
+    }
+    const uint64_t kv = (vb && tid == ob && j == jb) ? keyb : k;
+    if (kv) {
+      ++b.feas;
+      if (kv > b.key) { b.key = kv; b.idx = l; }
+    }
+  }
+  wave_reduce_cand(a);
+  if (vb) wave_reduce_cand(b);
+  if (lane == 0) {
+    sh.ka[wave] = a.key; sh.ia[wave] = a.idx; sh.fa[wave] = a.feas;
+    sh.kb[wave] = b.key; sh.ib[wave] = b.idx; sh.fb[wave] = b.feas;
+  }
+}
+
+template <int B>
+__device__ __forceinline__ Cand wg_combine(const BatchShared<B>& sh, bool variant_b) {
+  Cand c{0, -1, 0};
+#pragma unroll
+  for (int w = 0; w < B / 64; ++w) {
+    const uint64_t k = variant_b ? sh.kb[w] : sh.ka[w];
+    const int i = variant_b ? sh.ib[w] : sh.ia[w];
+    c.feas += variant_b ? sh.fb[w] : sh.fa[w];
+    if (k > c.key) { c.key = k; c.idx = i; }
+  }
+  return c;
+}
+
+// Wave 0: poll pod `row`'s G (<= 256) granules and return the winning key and workgroup to every
+// lane.  The next sweep's loads are issued before the current sweep is examined, so a granule that
+// lands is seen one load latency later, not up to two; the abort word rides along with every
+// sweep.  Returns false on timeout / abort.
+struct Sweep {
+  uint64_t v[4];
+  int abort;
+};
+__device__ __forceinline__ Sweep sweep(const uint64_t* row, int G, const int32_t* abort_word) {
+  const int lane = threadIdx.x & 63;
+  Sweep s;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) s.v[j] = (lane + 64 * j < G) ? load_sc1(row + lane + 64 * j) : kGValid;
+  s.abort = load_sc1(abort_word);
+  return s;
+}
+
+__device__ __forceinline__ bool poll_row(const uint64_t* row, int G, const int32_t* abort_word, uint64_t& wkey,
+                                         int& wg) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  Sweep cur = sweep(row, G, abort_word);
+  for (;;) {
+    const Sweep nxt = sweep(row, G, abort_word);
+    bool all = true;
+    uint64_t k = 0;
+    int gsel = -1;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint64_t v = cur.v[j];
+      if (!(v & kGValid)) {
+        all = false;
+      } else if ((v & ~kGValid) > k) {
+        k = v & ~kGValid;
+        gsel = lane + 64 * j;
+      }
+    }
+    if (__all(all)) {
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t k2 = __shfl_xor(k, off);
+        const int g2 = __shfl_xor(gsel, off);
+        if (k2 > k) { k = k2; gsel = g2; }
+      }
+      wkey = k;
+      wg = k ? gsel : -1;
+      return true;
+    }
+    if (cur.abort != 0 || __builtin_amdgcn_s_memrealtime() - t0 > kSpinTimeout) return false;
+    cur = nxt;
+  }
+}
+
+template <uint32_t FM, uint32_t SM, int K, int B>
+__global__ __launch_bounds__(B) void k_batch(const DevState* __restrict__ stp, BatchArgs pa) {
+  const DevState& st = *stp;
+  const int tid = threadIdx.x, wave = tid >> 6;
+  const int G = gridDim.x, g = blockIdx.x;
+  const int lo = g * pa.per;
+  __shared__ BatchShared<B> sh;
+
+  // rows stay in registers; assume_row writes every change through to the node columns as well
+  NodeRes r[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    const int n = lo + j * B + tid;
+    r[j] = NodeRes{};
+    if (n < st.N) r[j] = load_res(st, n);
+  }
+  // phase stamps (diagnostics): per iteration i, 8 per traced workgroup (0 and last):
+  // start, evaluated, pod i-1 resolved, pod i published, iteration end
+  const bool tr = pa.trace && tid == 0 && (g == 0 || g == G - 1);
+  int64_t* trow = pa.trace ? pa.trace + (g == 0 ? 0 : 8) : nullptr;
+#define KGPU_STAMP(i, k) \
+  if (tr) trow[(size_t)(i) * 16 + (k)] = (int64_t)__builtin_amdgcn_s_memrealtime()
+
+  kgpu_pod_query qp{};                      // pod i-1 (published, not yet resolved)
+  kgpu_pod_query q = *cp(st.queries + pa.first);
+  int cand = -1;                            // this workgroup's candidate for pod i-1 (uniform)
+  bool aborted = false;
+  for (int i = 0; i <= pa.count; ++i) {
+    KGPU_STAMP(i, 0);
+    const bool have_prev = i > 0;
+    const bool have_cur = i < pa.count;
+    // ---- evaluate pod i: variant A on the rows as they are, variant B with pod i-1 assumed on
+    //      this workgroup's candidate (registers only; not for extended resources / host ports)
+    uint64_t keys[K];
+    const bool fast_b = have_prev && cand >= 0 && qp.scalars.count == 0 && qp.ports.count == 0;
+    const int ob = cand >= 0 ? cand % B : -1, jb = cand >= 0 ? cand / B : -1;
+    uint64_t keyb = 0;
+    if (have_cur) {
+      const uint64_t tk = pod_tie_key(st.seed, pa.seq0 + i);
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        const int n = lo + j * B + tid;
+        keys[j] = n < st.N ? node_key<FM, SM>(st, q, r[j], n, tk) : 0;
+      }
+      if (fast_b && tid == ob) {
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+          if (j == jb) {
+            NodeRes rb = r[j];
+            assume_regs(qp, rb);
+            keyb = node_key<FM, SM>(st, q, rb, lo + cand, tk);
+          }
+      }
+      wg_partials<K, B>(sh, keys, tid, fast_b, ob, jb, keyb);
+    }
+    KGPU_STAMP(i, 1);
+    // the next pod's query: issued now, consumed after the hop
+    kgpu_pod_query qn{};
+    if (i + 1 < pa.count) qn = *cp(st.queries + pa.first + i + 1);
+    __syncthreads();
+    // ---- wave 0: resolve pod i-1, then publish pod i's granule (unless this workgroup won i-1
+    //      without a precomputed variant B: it re-evaluates first)
+    const uint64_t* prow = pa.gran + (size_t)(i - 1) * G;
+    uint64_t* row = pa.gran + (size_t)i * G;
+    if (wave == 0) {
+      // both variants' workgroup results are combined before the poll: after it only a select
+      Cand ca{0, -1, 0}, cb{0, -1, 0};
+      if (have_cur) {
+        ca = wg_combine<B>(sh, false);
+        cb = fast_b ? wg_combine<B>(sh, true) : ca;
+      }
+      uint64_t wkey = 0;
+      int wg = -1;
+      bool ok = true;
+      if (have_prev) ok = poll_row(prow, G, pa.abort, wkey, wg);
+      KGPU_STAMP(i, 2);
+      if (tid == 0) {
+        if (!ok) __hip_atomic_store(pa.abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        sh.abort = ok ? 0 : 1;
+        sh.wkey = wkey;
+        sh.wg = wg;
+        sh.cand = -1;
+        const bool won = have_prev && wg == g;
+        if (ok && have_cur && !(won && !fast_b)) {
+          const Cand c = won ? cb : ca;
+          store_sc1(row + g, kGValid | c.key);
+          pa.feas[(size_t)i * G + g] = c.feas;
+          sh.cand = c.key ? c.idx : -1;
+          KGPU_STAMP(i, 3);
+        }
+      }
+    }
+    __syncthreads();
+    if (sh.abort) {
+      aborted = true;
+      break;
+    }
+    // ---- pod i-1's outcome: result record, assume on the winning row
+    if (have_prev) {
+      const uint64_t wkey = sh.wkey;
+      const int wg = sh.wg;
+      const int pod = pa.first + i - 1;
+      if (tid == 0 && ((wg >= 0 && wg == g) || (wg < 0 && g == 0))) {
+        kgpu_result res;
+        res.node = wg >= 0 ? st.node_base + lo + cand : -1;
+        res.feasible = 0;   // k_batch_fixup
+        res.evaluated = st.n_total;
+        res.scored = 0;     // k_batch_fixup
+        res.score = wg >= 0 ? (int64_t)(wkey >> 40) - 1 : 0;
+        gp(st.results)[pod] = res;
+      }
+      if (wg == g) {
+        if (pa.assume && tid == ob) {
+#pragma unroll
+          for (int j = 0; j < K; ++j)
+            if (j == jb) assume_row(st, qp, r[j], lo + cand);
+        }
+        if (!fast_b && have_cur) {
+          // the winner's row changed in memory-resident columns: evaluate it again, republish
+          if (tid == ob) {
+            const uint64_t tk = pod_tie_key(st.seed, pa.seq0 + i);
+#pragma unroll
+            for (int j = 0; j < K; ++j)
+              if (j == jb) keys[j] = node_key<FM, SM>(st, q, r[j], lo + cand, tk);
+          }
+          wg_partials<K, B>(sh, keys, tid, false, -1, -1, 0);
+          __syncthreads();
+          if (tid == 0) {
+            const Cand c = wg_combine<B>(sh, false);
+            store_sc1(row + g, kGValid | c.key);
+            pa.feas[(size_t)i * G + g] = c.feas;
+            sh.cand = c.key ? c.idx : -1;
+            KGPU_STAMP(i, 3);
+          }
+        }
+      }
+      __syncthreads();
+    }
+    cand = sh.cand;
+    qp = q;
+    q = qn;
+    KGPU_STAMP(i, 4);
+  }
+#undef KGPU_STAMP
+  (void)aborted;
+}
+
+// FeasibleNodes and the scored flag of every pod of a persistent run (generic_scheduler.go:184-191:
+// a single feasible node is returned without scoring).
+__global__ void k_batch_fixup(const DevState* __restrict__ stp, BatchArgs pa, int G) {
+  const DevState& st = *stp;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= pa.count) return;
+  int f = 0;
+  for (int g = 0; g < G; ++g) f += pa.feas[(size_t)i * G + g];
+  kgpu_result& r = gp(st.results)[pa.first + i];
+  r.feasible = f;
+  if (r.node >= 0 && f >= 2) {
+    r.scored = 1;
+  } else {
+    r.scored = 0;
+    r.score = 0;
+  }
+}
+
+// ---------------------------------------------------------------- profile instantiations
+constexpr uint32_t bit(int i) { return 1u << i; }
+// config (b) of BASELINE.json: NodeResourcesFit + BalancedAllocation + LeastAllocated
+constexpr uint32_t kFitFM = bit(KGPU_F_NODE_RESOURCES_FIT);
+constexpr uint32_t kFitSM = bit(KGPU_S_BALANCED_ALLOCATION) | bit(KGPU_S_LEAST_ALLOCATED) | kDefRes;
+// the default provider (algorithmprovider/registry.go:71-155)
+constexpr uint32_t kDefaultFM = (1u << KGPU_NUM_FILTERS) - 1;
+constexpr uint32_t kDefaultSM = (kSMask & ~bit(KGPU_S_MOST_ALLOCATED)) | kDefRes;
+// the ClusterAutoscalerProvider (registry.go:157-165): MostAllocated instead of LeastAllocated
+constexpr uint32_t kAutoscalerSM = (kSMask & ~bit(KGPU_S_LEAST_ALLOCATED)) | kDefRes;
+
+struct SpecEntry {
+  uint32_t fm, sm;
+  void (*fn)(const DevState*, PodArgs);
+};
+static const SpecEntry kSpecs[] = {
+    {kRuntime, kRuntime, k_eval<kRuntime, kRuntime>},
+    {kFitFM, kFitSM, k_eval<kFitFM, kFitSM>},
+    {kDefaultFM, kDefaultSM, k_eval<kDefaultFM, kDefaultSM>},
+    {kDefaultFM, kAutoscalerSM, k_eval<kDefaultFM, kAutoscalerSM>},
+};
+constexpr int kNumSpecs = sizeof(kSpecs) / sizeof(kSpecs[0]);
+
+int select_spec(const int32_t* filters, int nf, const int32_t* scores, int ns, bool def_res) {
+  uint32_t fm = 0, sm = 0;
+  for (int i = 0; i < nf; ++i) {
+    if (i > 0 && filters[i] <= filters[i - 1]) return 0;  // not in ascending (default) order
+    fm |= bit(filters[i]);
+  }
+  for (int i = 0; i < ns; ++i) sm |= bit(scores[i]);
+  const bool uses_res = (sm & (bit(KGPU_S_LEAST_ALLOCATED) | bit(KGPU_S_MOST_ALLOCATED))) != 0;
+  if (uses_res) {
+    if (!def_res) return 0;
+    sm |= kDefRes;
+  }
+  for (int s = 1; s < kNumSpecs; ++s) {
+    const uint32_t want = kSpecs[s].sm & (uses_res ? ~0u : ~kDefRes);
+    if (kSpecs[s].fm == fm && want == sm) return s;
+  }
+  return 0;
+}
+
+// Persistent geometries: (threads per workgroup, rows per lane).  256 x 1 keeps small clusters
+// on few workgroups; 1024 x 1 gives 4 waves per SIMD; 512 x 4 holds up to 524,288 nodes per GPU
+// (256 workgroups x 2048 rows) with every row in registers and no spills.  Larger shards take the
+// one-launch-per-pod path.
+struct Geo {
+  int B, K;
+};
+constexpr Geo kGeo[] = {{256, 1}, {1024, 1}, {512, 4}};
+constexpr int kNumGeo = 3;
+constexpr int kBatchLdsPad = 96 * 1024;
+
+template <uint32_t FM, uint32_t SM>
+struct BatchRow {
+  using Fn = void (*)(const DevState*, BatchArgs);
+  static constexpr Fn fn[kNumGeo] = {k_batch<FM, SM, 1, 256>, k_batch<FM, SM, 1, 1024>, k_batch<FM, SM, 4, 512>};
+};
+using BatchFn = void (*)(const DevState*, BatchArgs);
+static const BatchFn* const kBatch[] = {
+    BatchRow<kRuntime, kRuntime>::fn,
+    BatchRow<kFitFM, kFitSM>::fn,
+    BatchRow<kDefaultFM, kDefaultSM>::fn,
+    BatchRow<kDefaultFM, kAutoscalerSM>::fn,
+};
+static_assert(sizeof(kBatch) / sizeof(kBatch[0]) == kNumSpecs, "one k_batch row per profile instantiation");
+
+int batch_geometry(int N, int max_groups, int* per, int* groups) {
+  for (int gi = 0; gi < kNumGeo; ++gi) {
+    const int p = kGeo[gi].B * kGeo[gi].K;
+    const int g = (N + p - 1) / p;
+    if (g <= max_groups) {
+      *per = p;
+      *groups = g < 1 ? 1 : g;
+      return gi;
+    }
+  }
+  return -1;
+}
+
+int launch_batch(const DevState* st, const BatchArgs& a, int groups, int geo, int spec, void* stream) {
+  if (spec < 0 || spec >= kNumSpecs) spec = 0;
+  if (geo < 0 || geo >= kNumGeo) return -1;
+  // One workgroup per CU: a dynamic LDS reservation above half a CU's 160 KB keeps the dispatcher
+  // from stacking two persistent workgroups on one CU (they would share its SIMDs).
+  static bool attr_set[kNumSpecs][kNumGeo] = {};
+  if (!attr_set[spec][geo]) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(kBatch[spec][geo]),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, kBatchLdsPad) != hipSuccess)
+      return -1;
+    attr_set[spec][geo] = true;
+  }
+  hipLaunchKernelGGL(kBatch[spec][geo], dim3(groups), dim3(kGeo[geo].B), kBatchLdsPad, (hipStream_t)stream, st, a);
+  if (hipGetLastError() != hipSuccess) return -1;
+  hipLaunchKernelGGL(k_batch_fixup, dim3((a.count + 255) / 256), dim3(256), 0, (hipStream_t)stream, st, a, groups);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int eval_blocks(int N) {
@@ -604,8 +1178,9 @@ int eval_blocks(int N) {
   return b;
 }
 
-int launch_eval(const DevState* st, const PodArgs& a, int blocks, void* stream) {
-  hipLaunchKernelGGL(k_eval, dim3(blocks), dim3(kBlock), 0, (hipStream_t)stream, st, a);
+int launch_eval(const DevState* st, const PodArgs& a, int blocks, int spec, void* stream) {
+  if (spec < 0 || spec >= kNumSpecs) spec = 0;
+  hipLaunchKernelGGL(kSpecs[spec].fn, dim3(blocks), dim3(kBlock), 0, (hipStream_t)stream, st, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

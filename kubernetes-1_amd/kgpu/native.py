@@ -17,7 +17,7 @@ _lib = None
 EXPORTS = ["kgpu_abi_version", "kgpu_struct_sizes", "kgpu_create", "kgpu_destroy", "kgpu_last_error",
            "kgpu_upload_snapshot", "kgpu_generation", "kgpu_schedule_one", "kgpu_schedule_batch",
            "kgpu_get_filter", "kgpu_get_scores", "kgpu_forget_pod", "kgpu_read_nodes", "kgpu_set_option",
-           "kgpu_comm_unique_id", "kgpu_comm_init"]
+           "kgpu_read_phase_trace", "kgpu_comm_unique_id", "kgpu_comm_init"]
 
 
 class KgpuError(RuntimeError):
@@ -50,6 +50,7 @@ def lib():
     L.kgpu_forget_pod.argtypes = [vp, i32]
     L.kgpu_read_nodes.argtypes = [vp, vp, vp, vp, vp, vp, vp]
     L.kgpu_set_option.argtypes = [vp, i32, i64]
+    L.kgpu_read_phase_trace.argtypes = [vp, vp, i32]
     L.kgpu_comm_unique_id.argtypes = [vp]
     L.kgpu_comm_init.argtypes = [vp, i32, i32, vp]
     if L.kgpu_abi_version() != abi.ABI_VERSION:
@@ -138,6 +139,15 @@ class Engine:
         cols = [np.zeros(n, np.int64) for _ in range(5)] + [np.zeros(n, np.int32)]
         self._check(lib().kgpu_read_nodes(self.h, *[c.ctypes.data for c in cols]))
         return dict(zip(["req_cpu", "req_mem", "req_eph", "nz_cpu", "nz_mem", "num_pods"], cols))
+
+    def phase_trace(self, max_iters):
+        """[iterations][2][8] s_memrealtime stamps (workgroup 0, last workgroup) of the last
+        persistent run: start, evaluated, previous pod resolved, published, end."""
+        out = np.zeros((max_iters, 16), np.int64)
+        n = lib().kgpu_read_phase_trace(self.h, out.ctypes.data, max_iters)
+        if n < 0:
+            self._check(n)
+        return out[:n].reshape(n, 2, 8)
 
     def forget(self, slot):
         self._check(lib().kgpu_forget_pod(self.h, slot))

@@ -1,0 +1,53 @@
+#!/usr/bin/env python3
+"""Per-pod phase breakdown of the persistent batch kernel (s_memrealtime, 10 ns ticks).
+
+phases per pipeline iteration i: eval = pod i evaluated (variants A and B, wave reductions);
+wait_prev = barrier + poll until pod i-1 resolved; publish = pod i's granule stored; assume =
+barrier + result record + assume of pod i-1 on the winning row; next = loop overhead."""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "kubernetes-1_amd")]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--nodes", type=int, default=5000)
+    ap.add_argument("--pods", type=int, default=1000)
+    ap.add_argument("--config", default="b")
+    args = ap.parse_args()
+    import numpy as np
+    from kgpu import abi, cluster
+    from kgpu.framework import GpuFramework
+    if args.config == "b":
+        nodes, ex, pods, prof = cluster.fit_least_balanced(n_nodes=args.nodes, n_pods=args.pods)
+    else:
+        nodes, init, pods, prof = cluster.scheduling_basic(n_nodes=args.nodes, n_init=args.nodes, n_pods=args.pods)
+        ex, pods = [], init + pods
+    fw = GpuFramework(prof, nodes, ex, pods_hint=pods[:16])
+    q, pc, _, errs = fw.compile_pods(pods)
+    eng = fw.engine
+    eng.schedule_batch(q[:64], pc)
+    eng.upload(fw.snap, fw.arrays)
+    eng.set_option(abi.OPT_PHASE_TRACE, 1)
+    eng.schedule_batch(q, pc)
+    t = eng.phase_trace(len(q) + 1).astype(np.float64) * 10.0  # ns
+    t = t[1:-1]  # steady state: skip the prologue and epilogue iterations
+    for w, name in ((0, "wg0"), (1, "wglast")):
+        a = t[:, w, :]
+        per = np.diff(a[:, 0])
+        ph = {"eval": a[:, 1] - a[:, 0], "wait_prev": a[:, 2] - a[:, 1], "publish": a[:, 3] - a[:, 2],
+              "assume": a[:, 4] - a[:, 3], "next": a[1:, 0] - a[:-1, 4]}
+        print("%s: per-pod %.0f ns | " % (name, np.median(per)) +
+              "  ".join("%s %.0f" % (k, np.median(v)) for k, v in ph.items()) + " (medians, ns)")
+    # hop: latest publish of pod i (of the two traced workgroups) -> pod i seen resolved
+    pub = np.maximum(t[:-1, 0, 3], t[:-1, 1, 3])
+    res0, res1 = t[1:, 0, 2], t[1:, 1, 2]
+    print("publish skew (wg0 - wglast) %.0f ns; hop to wg0 %.0f ns, to wglast %.0f ns (medians)"
+          % (np.median(t[:, 0, 3] - t[:, 1, 3]), np.median(res0 - pub), np.median(res1 - pub)))
+
+
+if __name__ == "__main__":
+    main()
