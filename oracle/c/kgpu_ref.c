@@ -49,8 +49,15 @@ typedef struct {
   int32_t *image_off, *image_id;
   int64_t* image_score;
   int32_t *avoid_off, *avoid_id, *zone_id;
+  int32_t *key_n_values, *key_empty_value;
   int threads;
   void* pool;
+  /* existing pods (snapshot pods, then pods assumed by kgpu_ref_schedule) and their terms */
+  int PK;
+  struct rpod_s* pods;
+  int npods, cap_pods;
+  int** node_pods; /* [N] pod indices per node (NodeInfo.Pods order) */
+  int *node_npods, *node_cap;
 } ref_state;
 
 static void* dup_bytes(const void* src, size_t bytes) {
@@ -58,6 +65,184 @@ static void* dup_bytes(const void* src, size_t bytes) {
   if (src && bytes) memcpy(p, src, bytes);
   else memset(p, 0, bytes ? bytes : 1);
   return p;
+}
+
+/* ------------------------------------------------------------------ existing pods
+ * framework.NodeInfo.Pods / PodInfo (framework/v1alpha1/types.go:79-160, 171-209): every pod
+ * keeps its namespace, labels and (anti-)affinity terms.  Terms are deep-copied so that pods
+ * assumed from one kgpu_ref_schedule call outlive that call's pools. */
+typedef struct {
+  int key, op, nvals;
+  int32_t* vals;
+} oreq;
+typedef struct {
+  int kind; /* KGPU_SEL_* */
+  int nreq;
+  oreq* reqs;
+} osel;
+typedef struct {
+  int kind, weight, topo_key, nns;
+  int32_t* ns;
+  osel sel;
+} oterm;
+typedef struct rpod_s {
+  int node, ns;
+  uint32_t flags;
+  int nlab;
+  int32_t* lab; /* (key id, value id) pairs */
+  int nterms;
+  oterm* terms;
+} rpod;
+
+static osel osel_from(const kgpu_selector* s, const kgpu_pools* p) {
+  osel o;
+  o.kind = s->kind;
+  o.nreq = s->kind == KGPU_SEL_AND ? s->reqs.count : 0;
+  o.reqs = (oreq*)calloc(o.nreq ? o.nreq : 1, sizeof(oreq));
+  for (int i = 0; i < o.nreq; ++i) {
+    const kgpu_req* q = &p->reqs[s->reqs.begin + i];
+    o.reqs[i].key = q->key;
+    o.reqs[i].op = q->op;
+    o.reqs[i].nvals = q->vals.count;
+    o.reqs[i].vals = (int32_t*)dup_bytes(p->ints + q->vals.begin, sizeof(int32_t) * q->vals.count);
+  }
+  return o;
+}
+
+static void osel_free(osel* o) {
+  for (int i = 0; i < o->nreq; ++i) free(o->reqs[i].vals);
+  free(o->reqs);
+}
+
+static oterm oterm_from(int kind, const kgpu_pod_term* t, const kgpu_pools* p) {
+  oterm o;
+  o.kind = kind;
+  o.weight = t->weight;
+  o.topo_key = t->topo_key;
+  o.nns = t->ns.count;
+  o.ns = (int32_t*)dup_bytes(p->ints + t->ns.begin, sizeof(int32_t) * t->ns.count);
+  o.sel = osel_from(&t->sel, p);
+  return o;
+}
+
+static void oterm_free(oterm* o) {
+  free(o->ns);
+  osel_free(&o->sel);
+}
+
+static int pod_label(const rpod* pd, int key) {
+  if (key < 0) return -1;
+  for (int i = 0; i < pd->nlab; ++i)
+    if (pd->lab[2 * i] == key) return pd->lab[2 * i + 1];
+  return -1;
+}
+
+/* labels.Selector.Matches on pod labels (selector.go:198-242, 346-353); Nothing() matches nothing */
+static int sel_matches_pod(const osel* s, const rpod* pd) {
+  if (s->kind != KGPU_SEL_AND) return 0;
+  for (int i = 0; i < s->nreq; ++i) {
+    const oreq* q = &s->reqs[i];
+    int v = pod_label(pd, q->key), in = 0;
+    for (int j = 0; j < q->nvals; ++j) in |= (q->vals[j] == v);
+    switch (q->op) {
+      case KGPU_OP_IN: if (!(v >= 0 && in)) return 0; break;
+      case KGPU_OP_NOTIN: if (v >= 0 && in) return 0; break;
+      case KGPU_OP_EXISTS: if (v < 0) return 0; break;
+      case KGPU_OP_DNE: if (v >= 0) return 0; break;
+      default: return 0;
+    }
+  }
+  return 1;
+}
+
+/* schedutil.PodMatchesTermsNamespaceAndSelector (util/topologies.go:40-49) */
+static int term_matches_pod(const oterm* t, const rpod* pd) {
+  int ok = 0;
+  for (int i = 0; i < t->nns; ++i) ok |= (t->ns[i] == pd->ns);
+  return ok && sel_matches_pod(&t->sel, pd);
+}
+
+static void node_add_pod(ref_state* r, int n, int idx) {
+  if (r->node_npods[n] == r->node_cap[n]) {
+    r->node_cap[n] = r->node_cap[n] ? 2 * r->node_cap[n] : 4;
+    r->node_pods[n] = (int*)realloc(r->node_pods[n], sizeof(int) * r->node_cap[n]);
+  }
+  r->node_pods[n][r->node_npods[n]++] = idx;
+}
+
+static rpod* new_pod(ref_state* r) {
+  if (r->npods == r->cap_pods) {
+    r->cap_pods = r->cap_pods ? 2 * r->cap_pods : 64;
+    r->pods = (rpod*)realloc(r->pods, sizeof(rpod) * r->cap_pods);
+  }
+  rpod* pd = &r->pods[r->npods++];
+  memset(pd, 0, sizeof(*pd));
+  return pd;
+}
+
+static void load_pods(ref_state* r, const kgpu_snapshot* s) {
+  r->PK = s->n_pod_label_keys;
+  r->node_pods = (int**)calloc(r->N ? r->N : 1, sizeof(int*));
+  r->node_npods = (int*)calloc(r->N ? r->N : 1, sizeof(int));
+  r->node_cap = (int*)calloc(r->N ? r->N : 1, sizeof(int));
+  for (int i = 0; i < s->n_pods; ++i) {
+    rpod* pd = new_pod(r);
+    pd->node = s->pod_node[i];
+    pd->ns = s->pod_ns[i];
+    pd->flags = s->pod_flags[i];
+    pd->lab = (int32_t*)calloc(2 * (r->PK ? r->PK : 1), sizeof(int32_t));
+    for (int k = 0; k < r->PK; ++k) {
+      int v = s->pod_label_val[(size_t)k * s->n_pods + i];
+      if (v >= 0) { pd->lab[2 * pd->nlab] = k; pd->lab[2 * pd->nlab + 1] = v; pd->nlab++; }
+    }
+  }
+  for (int t = 0; t < s->n_terms; ++t) {
+    const kgpu_term* tm = &s->terms[t];
+    rpod* pd = &r->pods[tm->pod];
+    pd->terms = (oterm*)realloc(pd->terms, sizeof(oterm) * (pd->nterms + 1));
+    pd->terms[pd->nterms++] = oterm_from(tm->kind, &tm->t, &s->pools);
+  }
+  for (int i = 0; i < r->npods; ++i) {
+    int n = r->pods[i].node - r->base;
+    if (n >= 0 && n < r->N) node_add_pod(r, n, i);
+  }
+}
+
+static void free_pods(ref_state* r) {
+  for (int i = 0; i < r->npods; ++i) {
+    for (int t = 0; t < r->pods[i].nterms; ++t) oterm_free(&r->pods[i].terms[t]);
+    free(r->pods[i].terms);
+    free(r->pods[i].lab);
+  }
+  free(r->pods);
+  for (int n = 0; n < r->N; ++n) free(r->node_pods[n]);
+  free(r->node_pods);
+  free(r->node_npods);
+  free(r->node_cap);
+}
+
+/* The incoming pod as a PodInfo: its labels from the query's (key, value) pairs, its terms. */
+static void incoming_pod(rpod* pd, const kgpu_pod_query* q, const kgpu_pools* p) {
+  memset(pd, 0, sizeof(*pd));
+  pd->node = -1;
+  pd->ns = q->ns;
+  pd->flags = KGPU_PF_ACTIVE | ((q->flags & KGPU_Q_TERMINATING) ? KGPU_PF_TERMINATING : 0) |
+              ((q->flags & (KGPU_Q_HAS_POD_AFFINITY | KGPU_Q_HAS_POD_ANTI)) ? KGPU_PF_WITH_AFFINITY : 0);
+  pd->nlab = q->labels.count / 2;
+  pd->lab = (int32_t*)dup_bytes(p->ints + q->labels.begin, sizeof(int32_t) * 2 * pd->nlab);
+  const kgpu_range rs[4] = {q->ipa_req_aff, q->ipa_req_anti, q->ipa_pref_aff, q->ipa_pref_anti};
+  const int kinds[4] = {KGPU_TERM_REQ_AFF, KGPU_TERM_REQ_ANTI, KGPU_TERM_PREF_AFF, KGPU_TERM_PREF_ANTI};
+  int nt = 0;
+  for (int k = 0; k < 4; ++k) nt += rs[k].count;
+  pd->terms = (oterm*)calloc(nt ? nt : 1, sizeof(oterm));
+  for (int k = 0; k < 4; ++k)
+    for (int i = 0; i < rs[k].count; ++i) pd->terms[pd->nterms++] = oterm_from(kinds[k], &p->pod_terms[rs[k].begin + i], p);
+}
+
+static void free_pod(rpod* pd) {
+  for (int t = 0; t < pd->nterms; ++t) oterm_free(&pd->terms[t]);
+  free(pd->terms);
+  free(pd->lab);
 }
 
 int kgpu_ref_create(const kgpu_config* cfg, const kgpu_snapshot* s, int threads, ref_state** out) {
@@ -107,7 +292,10 @@ int kgpu_ref_create(const kgpu_config* cfg, const kgpu_snapshot* s, int threads,
   D(avoid_off, s->avoid_off, N + 1, int32_t);
   D(avoid_id, s->avoid_id, (size_t)s->avoid_off[N], int32_t);
   D(zone_id, s->zone_id, N, int32_t);
+  D(key_n_values, s->key_n_values, (size_t)r->K, int32_t);
+  D(key_empty_value, s->key_empty_value, (size_t)r->K, int32_t);
 #undef D
+  load_pods(r, s);
   *out = r;
   return 0;
 }
@@ -118,8 +306,9 @@ void kgpu_ref_destroy(ref_state* r) {
                   r->nz_mem, r->alloc_pods, r->num_pods, r->alloc_scalar, r->req_scalar, r->unsched,
                   r->label_val, r->value_off, r->value_int, r->value_int_ok, r->taint_nosched, r->taint_prefer,
                   r->port_count, r->ports, r->image_off, r->image_id, r->image_score, r->avoid_off, r->avoid_id,
-                  r->zone_id};
+                  r->zone_id, r->key_n_values, r->key_empty_value};
   for (size_t i = 0; i < sizeof(ptrs) / sizeof(ptrs[0]); ++i) free(ptrs[i]);
+  free_pods(r);
   pool_free((pool_t*)r->pool);
   free(r);
 }
@@ -171,6 +360,442 @@ static int pod_matches_node_selector_and_affinity(const ref_state* r, const kgpu
   return 0;
 }
 
+/* ------------------------------------------------------------------ math.Log (Go stdlib)
+ * Go's math.Log is the FreeBSD e_log.c algorithm (src/math/log.go, go1.13.9); restated here.
+ * Used by PodTopologySpread topologyNormalizingWeight (podtopologyspread/scoring.go:286-288). */
+static double go_log(double x) {
+  const double ln2hi = 6.93147180369123816490e-01, ln2lo = 1.90821492927058770002e-10;
+  const double l1 = 6.666666666666735130e-01, l2 = 3.999999999940941908e-01, l3 = 2.857142874366239149e-01,
+               l4 = 2.222219843214978396e-01, l5 = 1.818357216161805012e-01, l6 = 1.531383769920937332e-01,
+               l7 = 1.479819860511658591e-01;
+  if (x != x || x == INFINITY) return x;
+  if (x < 0) return NAN;
+  if (x == 0) return -INFINITY;
+  int ki;
+  double f1 = frexp(x, &ki);
+  if (f1 < 0.70710678118654752440 /* Sqrt2/2 */) {
+    f1 *= 2;
+    ki--;
+  }
+  double f = f1 - 1;
+  double k = (double)ki;
+  double s = f / (2 + f);
+  double s2 = s * s;
+  double s4 = s2 * s2;
+  double t1 = s2 * (l1 + s4 * (l3 + s4 * (l5 + s4 * l7)));
+  double t2 = s4 * (l2 + s4 * (l4 + s4 * l6));
+  double R = t1 + t2;
+  double hfsq = 0.5 * f * f;
+  return k * ln2hi - ((hfsq - (s * (hfsq + R) + k * ln2lo)) - f);
+}
+
+/* ------------------------------------------------------------------ per-cycle plugin state
+ * CycleState of PodTopologySpread (preFilterState filtering.go:47-60, preScoreState
+ * scoring.go:39-48), InterPodAffinity (filtering.go:47-60, scoring.go:38-43) and
+ * DefaultPodTopologySpread (the selector, default_pod_topology_spread.go:191-205). Maps keyed by
+ * topologyPair{key, value} are per-key arrays indexed by the value id. */
+typedef struct {
+  rpod self;
+  int64_t** arr[8]; /* per-key arrays, lazily allocated: see A_* */
+  /* PodTopologySpread filter */
+  int pn;
+  const kgpu_spread* hard;
+  osel* hsel;
+  int pany;
+  int64_t* pmin; /* [pn] critical-path minimum of the constraint's key */
+  /* PodTopologySpread score */
+  int sn;
+  const kgpu_spread* soft;
+  osel* ssel;
+  double* sw;
+  uint8_t* ignored; /* [N] */
+  /* InterPodAffinity */
+  int ex_any, aff_any, topo_any;
+  /* DefaultPodTopologySpread */
+  osel dsel;
+} qstate;
+
+enum { A_PREG, A_PCNT, A_SREG, A_SCNT, A_EXANTI, A_AFF, A_ANTI, A_TOPO };
+
+static int64_t* karr(qstate* s, const ref_state* r, int which, int k) {
+  if (!s->arr[which]) s->arr[which] = (int64_t**)calloc(r->K ? r->K : 1, sizeof(int64_t*));
+  if (!s->arr[which][k]) s->arr[which][k] = (int64_t*)calloc(r->key_n_values[k] ? r->key_n_values[k] : 1, sizeof(int64_t));
+  return s->arr[which][k];
+}
+
+/* read-only lookup (filter / score run on the worker threads) */
+static int64_t kget(const qstate* s, int which, int k, int v) {
+  if (k < 0 || v < 0 || !s->arr[which] || !s->arr[which][k]) return 0;
+  return s->arr[which][k][v];
+}
+
+static int nval(const ref_state* r, int k, int n) { return k >= 0 ? r->label_val[(size_t)k * r->N + n] : -1; }
+
+static int node_has_labels(const ref_state* r, int n) {
+  for (int k = 0; k < r->K; ++k)
+    if (r->label_val[(size_t)k * r->N + n] >= 0) return 1;
+  return 0;
+}
+
+/* countPodsMatchSelector (podtopologyspread/common.go:85-99): same namespace, not terminating */
+static int64_t count_match(const ref_state* r, int n, const osel* sel, int ns) {
+  int64_t c = 0;
+  for (int i = 0; i < r->node_npods[n]; ++i) {
+    const rpod* pd = &r->pods[r->node_pods[n][i]];
+    if ((pd->flags & KGPU_PF_TERMINATING) || pd->ns != ns) continue;
+    if (sel_matches_pod(sel, pd)) c++;
+  }
+  return c;
+}
+
+static int all_keys(const ref_state* r, const kgpu_spread* c, int nc, int n) {
+  for (int i = 0; i < nc; ++i)
+    if (nval(r, c[i].key, n) < 0) return 0;
+  return 1;
+}
+
+/* PodTopologySpread PreFilter (filtering.go:198-273) */
+static void pts_prefilter(qstate* s, const ref_state* r, const kgpu_pools* p, const kgpu_pod_query* q) {
+  s->pn = q->pts_hard.count;
+  if (!s->pn) return;
+  s->hard = &p->spreads[q->pts_hard.begin];
+  s->hsel = (osel*)calloc(s->pn, sizeof(osel));
+  s->pmin = (int64_t*)calloc(s->pn, sizeof(int64_t));
+  for (int i = 0; i < s->pn; ++i) s->hsel[i] = osel_from(&s->hard[i].sel, p);
+  for (int n = 0; n < r->N; ++n) {
+    if (!pod_matches_node_selector_and_affinity(r, p, q, n) || !all_keys(r, s->hard, s->pn, n)) continue;
+    for (int i = 0; i < s->pn; ++i) karr(s, r, A_PREG, s->hard[i].key)[nval(r, s->hard[i].key, n)] = 1;
+    s->pany = 1;
+  }
+  for (int n = 0; n < r->N; ++n) {
+    for (int i = 0; i < s->pn; ++i) {
+      int k = s->hard[i].key;
+      if (k < 0) continue;
+      int v = nval(r, k, n);
+      if (v < 0) v = r->key_empty_value[k]; /* node.Labels[key] of a missing key is "" */
+      if (v < 0 || !karr(s, r, A_PREG, k)[v]) continue;
+      karr(s, r, A_PCNT, k)[v] += count_match(r, n, &s->hsel[i], q->ns);
+    }
+  }
+  /* criticalPaths.update (filtering.go:93-121) keeps the minimum over the key's pairs in [0] */
+  for (int i = 0; i < s->pn; ++i) {
+    int k = s->hard[i].key;
+    int64_t mn = 2147483647;
+    if (k >= 0) {
+      const int64_t* reg = karr(s, r, A_PREG, k);
+      const int64_t* cnt = karr(s, r, A_PCNT, k);
+      for (int v = 0; v < r->key_n_values[k]; ++v)
+        if (reg[v] && cnt[v] < mn) mn = cnt[v];
+    }
+    s->pmin[i] = mn;
+  }
+}
+
+/* PodTopologySpread Filter (filtering.go:276-328) */
+static int pts_filter_ok(const qstate* s, const ref_state* r, int n) {
+  if (!s->pn || !s->pany) return 1;
+  for (int i = 0; i < s->pn; ++i) {
+    int k = s->hard[i].key;
+    int v = nval(r, k, n);
+    if (v < 0) return 0;
+    int64_t match = kget(s, A_PREG, k, v) ? kget(s, A_PCNT, k, v) : 0;
+    if (match + s->hard[i].self_match - s->pmin[i] > s->hard[i].max_skew) return 0;
+  }
+  return 1;
+}
+
+/* PodTopologySpread PreScore (scoring.go:59-169) over the feasible nodes F */
+static void pts_prescore(qstate* s, const ref_state* r, const kgpu_pools* p, const kgpu_pod_query* q, const int* F,
+                         int nf) {
+  s->sn = q->pts_soft.count;
+  s->ignored = (uint8_t*)calloc(r->N ? r->N : 1, 1);
+  if (!s->sn || nf == 0) {
+    s->sn = 0;
+    return;
+  }
+  s->soft = &p->spreads[q->pts_soft.begin];
+  s->ssel = (osel*)calloc(s->sn, sizeof(osel));
+  s->sw = (double*)calloc(s->sn, sizeof(double));
+  int64_t* size = (int64_t*)calloc(s->sn, sizeof(int64_t));
+  for (int i = 0; i < s->sn; ++i) s->ssel[i] = osel_from(&s->soft[i].sel, p);
+  int nign = 0;
+  for (int j = 0; j < nf; ++j) {
+    int n = F[j];
+    if (!all_keys(r, s->soft, s->sn, n)) {
+      s->ignored[n] = 1;
+      nign++;
+      continue;
+    }
+    for (int i = 0; i < s->sn; ++i) {
+      if (s->soft[i].is_hostname) continue;
+      int64_t* reg = karr(s, r, A_SREG, s->soft[i].key);
+      int v = nval(r, s->soft[i].key, n);
+      if (!reg[v]) {
+        reg[v] = 1;
+        size[i]++;
+      }
+    }
+  }
+  for (int i = 0; i < s->sn; ++i) {
+    int64_t sz = s->soft[i].is_hostname ? (int64_t)(nf - nign) : size[i];
+    s->sw[i] = go_log((double)(sz + 2)); /* topologyNormalizingWeight */
+  }
+  free(size);
+  for (int n = 0; n < r->N; ++n) {
+    if (!pod_matches_node_selector_and_affinity(r, p, q, n) || !all_keys(r, s->soft, s->sn, n)) continue;
+    for (int i = 0; i < s->sn; ++i) {
+      int k = s->soft[i].key, v = nval(r, k, n);
+      if (s->soft[i].is_hostname || !karr(s, r, A_SREG, k)[v]) continue;
+      karr(s, r, A_SCNT, k)[v] += count_match(r, n, &s->ssel[i], q->ns);
+    }
+  }
+}
+
+/* PodTopologySpread Score (scoring.go:174-208) */
+static int64_t pts_score(const qstate* s, const ref_state* r, const kgpu_pod_query* q, int n) {
+  if (s->ignored[n]) return 0;
+  double score = 0;
+  for (int i = 0; i < s->sn; ++i) {
+    int k = s->soft[i].key, v = nval(r, k, n);
+    if (v < 0) continue;
+    int64_t cnt = s->soft[i].is_hostname ? count_match(r, n, &s->ssel[i], q->ns) : kget(s, A_SCNT, k, v);
+    if (cnt < s->soft[i].max_skew) cnt = s->soft[i].max_skew - 1; /* adjustForMaxSkew */
+    score += (double)cnt * s->sw[i];
+  }
+  return (int64_t)score;
+}
+
+/* PodTopologySpread NormalizeScore (scoring.go:211-257) */
+static void pts_normalize(qstate* s, int64_t* sc, const int* F, int nf) {
+  int64_t mn = INT64_MAX, mx = 0;
+  for (int j = 0; j < nf; ++j) {
+    if (s->ignored[F[j]]) continue;
+    if (sc[j] < mn) mn = sc[j];
+    if (sc[j] > mx) mx = sc[j];
+  }
+  for (int j = 0; j < nf; ++j) {
+    if (s->ignored[F[j]]) sc[j] = 0;
+    else if (mx == 0) sc[j] = MAXN_SCORE;
+    else sc[j] = MAXN_SCORE * (mx + mn - sc[j]) / mx;
+  }
+}
+
+/* DefaultPodTopologySpread Score (default_pod_topology_spread.go:75-106) */
+static int64_t dpts_score(const qstate* s, const ref_state* r, const kgpu_pod_query* q, int n) {
+  if (q->flags & KGPU_Q_HAS_TSC) return 0;
+  if (r->node_npods[n] == 0 || s->dsel.kind == KGPU_SEL_EMPTY) return 0;
+  return count_match(r, n, &s->dsel, q->ns);
+}
+
+/* DefaultPodTopologySpread NormalizeScore (default_pod_topology_spread.go:109-163) */
+static void dpts_normalize(const ref_state* r, const kgpu_pod_query* q, int64_t* sc, const int* F, int nf) {
+  if (q->flags & KGPU_Q_HAS_TSC) return;
+  const double zw = 2.0 / 3.0;
+  int Z = r->nzones > 0 ? r->nzones : 1;
+  int64_t* zc = (int64_t*)calloc(Z, sizeof(int64_t));
+  uint8_t* zh = (uint8_t*)calloc(Z, 1);
+  int64_t max_node = 0, max_zone = 0;
+  int have_zones = 0;
+  for (int j = 0; j < nf; ++j) {
+    if (sc[j] > max_node) max_node = sc[j];
+    int z = r->zone_id[F[j]];
+    if (z < 0) continue;
+    zc[z] += sc[j];
+    zh[z] = 1;
+    have_zones = 1;
+  }
+  for (int z = 0; z < Z; ++z)
+    if (zh[z] && zc[z] > max_zone) max_zone = zc[z];
+  for (int j = 0; j < nf; ++j) {
+    double f = (double)MAXN_SCORE;
+    if (max_node > 0) f = (double)MAXN_SCORE * ((double)(max_node - sc[j]) / (double)max_node);
+    int z = r->zone_id[F[j]];
+    if (have_zones && z >= 0) {
+      double zs = (double)MAXN_SCORE;
+      if (max_zone > 0) zs = (double)MAXN_SCORE * ((double)(max_zone - zc[z]) / (double)max_zone);
+      f = (f * (1.0 - zw)) + (zw * zs);
+    }
+    sc[j] = (int64_t)f;
+  }
+  free(zc);
+  free(zh);
+}
+
+/* podMatchesAllAffinityTerms (interpodaffinity/filtering.go:151-161) */
+static int pod_matches_all(const rpod* self, const rpod* pd) {
+  int any = 0;
+  for (int t = 0; t < self->nterms; ++t) {
+    if (self->terms[t].kind != KGPU_TERM_REQ_AFF) continue;
+    any = 1;
+    if (!term_matches_pod(&self->terms[t], pd)) return 0;
+  }
+  return any;
+}
+
+/* InterPodAffinity PreFilter (filtering.go:166-271) */
+static void ipa_prefilter(qstate* s, const ref_state* r) {
+  const rpod* self = &s->self;
+  for (int i = 0; i < r->npods; ++i) {
+    const rpod* ep = &r->pods[i];
+    int n = ep->node - r->base;
+    if (!(ep->flags & KGPU_PF_WITH_AFFINITY) || n < 0 || n >= r->N) continue;
+    for (int t = 0; t < ep->nterms; ++t) {
+      const oterm* tm = &ep->terms[t];
+      if (tm->kind != KGPU_TERM_REQ_ANTI || !term_matches_pod(tm, self)) continue;
+      int v = nval(r, tm->topo_key, n);
+      if (v < 0) continue;
+      karr(s, r, A_EXANTI, tm->topo_key)[v] += 1;
+      s->ex_any = 1;
+    }
+  }
+  int has_req = 0;
+  for (int t = 0; t < self->nterms; ++t) has_req |= (self->terms[t].kind <= KGPU_TERM_REQ_ANTI);
+  if (!has_req) return;
+  for (int n = 0; n < r->N; ++n) {
+    for (int j = 0; j < r->node_npods[n]; ++j) {
+      const rpod* ep = &r->pods[r->node_pods[n][j]];
+      if (pod_matches_all(self, ep)) {
+        for (int t = 0; t < self->nterms; ++t) {
+          const oterm* tm = &self->terms[t];
+          if (tm->kind != KGPU_TERM_REQ_AFF) continue;
+          int v = nval(r, tm->topo_key, n);
+          if (v < 0) continue;
+          karr(s, r, A_AFF, tm->topo_key)[v] += 1;
+          s->aff_any = 1;
+        }
+      }
+      for (int t = 0; t < self->nterms; ++t) {
+        const oterm* tm = &self->terms[t];
+        if (tm->kind != KGPU_TERM_REQ_ANTI || !term_matches_pod(tm, ep)) continue;
+        int v = nval(r, tm->topo_key, n);
+        if (v < 0) continue;
+        karr(s, r, A_ANTI, tm->topo_key)[v] += 1;
+      }
+    }
+  }
+}
+
+/* InterPodAffinity Filter (filtering.go:314-396); returns 0 or the rule that failed (1..3) */
+static int ipa_filter(const qstate* s, const ref_state* r, const kgpu_pod_query* q, int n) {
+  const rpod* self = &s->self;
+  int exist = 1;
+  for (int t = 0; t < self->nterms; ++t) {
+    const oterm* tm = &self->terms[t];
+    if (tm->kind != KGPU_TERM_REQ_AFF) continue;
+    int v = nval(r, tm->topo_key, n);
+    if (v < 0) return 1;
+    if (kget(s, A_AFF, tm->topo_key, v) <= 0) exist = 0;
+  }
+  if (!exist && !(!s->aff_any && (q->flags & KGPU_Q_SELF_MATCH_ALL_AFF))) return 1;
+  for (int t = 0; t < self->nterms; ++t) {
+    const oterm* tm = &self->terms[t];
+    if (tm->kind != KGPU_TERM_REQ_ANTI) continue;
+    int v = nval(r, tm->topo_key, n);
+    if (v >= 0 && kget(s, A_ANTI, tm->topo_key, v) > 0) return 2;
+  }
+  if (s->ex_any) {
+    for (int k = 0; k < r->K; ++k) {
+      int v = nval(r, k, n);
+      if (v >= 0 && kget(s, A_EXANTI, k, v) > 0) return 3;
+    }
+  }
+  return 0;
+}
+
+/* InterPodAffinity PreScore (scoring.go:47-199): topologyScore[key][value] */
+static void ipa_prescore(qstate* s, const ref_state* r, int hard_weight) {
+  const rpod* self = &s->self;
+  const int self_aff = (self->flags & KGPU_PF_WITH_AFFINITY) != 0;
+  for (int n = 0; n < r->N; ++n) {
+    if (!node_has_labels(r, n)) continue; /* processTerm: len(fixedNode.Labels) == 0 */
+    for (int j = 0; j < r->node_npods[n]; ++j) {
+      const rpod* ep = &r->pods[r->node_pods[n][j]];
+      if (!self_aff && !(ep->flags & KGPU_PF_WITH_AFFINITY)) continue; /* PodsWithAffinity only */
+      for (int t = 0; t < self->nterms; ++t) {
+        const oterm* tm = &self->terms[t];
+        if (tm->kind < KGPU_TERM_PREF_AFF) continue;
+        int v = nval(r, tm->topo_key, n);
+        if (v < 0 || !term_matches_pod(tm, ep)) continue;
+        karr(s, r, A_TOPO, tm->topo_key)[v] += (int64_t)tm->weight * (tm->kind == KGPU_TERM_PREF_AFF ? 1 : -1);
+        s->topo_any = 1;
+      }
+      for (int t = 0; t < ep->nterms; ++t) {
+        const oterm* tm = &ep->terms[t];
+        int64_t w;
+        if (tm->kind == KGPU_TERM_REQ_AFF) {
+          if (hard_weight <= 0) continue;
+          w = hard_weight;
+        } else if (tm->kind == KGPU_TERM_PREF_AFF) {
+          w = tm->weight;
+        } else if (tm->kind == KGPU_TERM_PREF_ANTI) {
+          w = -(int64_t)tm->weight;
+        } else {
+          continue;
+        }
+        int v = nval(r, tm->topo_key, n);
+        if (v < 0 || !term_matches_pod(tm, self)) continue;
+        karr(s, r, A_TOPO, tm->topo_key)[v] += w;
+        s->topo_any = 1;
+      }
+    }
+  }
+}
+
+/* InterPodAffinity Score (scoring.go:217-236) */
+static int64_t ipa_score(const qstate* s, const ref_state* r, int n) {
+  if (!s->topo_any) return 0;
+  int64_t sc = 0;
+  for (int k = 0; k < r->K; ++k) {
+    if (!s->arr[A_TOPO] || !s->arr[A_TOPO][k]) continue;
+    int v = nval(r, k, n);
+    if (v >= 0) sc += s->arr[A_TOPO][k][v];
+  }
+  return sc;
+}
+
+/* InterPodAffinity NormalizeScore (scoring.go:241-272) */
+static void ipa_normalize(qstate* s, int64_t* sc, int nf) {
+  if (!s->topo_any) return;
+  int64_t mx = 0, mn = 0;
+  for (int j = 0; j < nf; ++j) {
+    if (sc[j] > mx) mx = sc[j];
+    if (sc[j] < mn) mn = sc[j];
+  }
+  int64_t diff = mx - mn;
+  for (int j = 0; j < nf; ++j) {
+    double f = 0;
+    if (diff > 0) f = (double)MAXN_SCORE * ((double)(sc[j] - mn) / (double)diff);
+    sc[j] = (int64_t)f;
+  }
+}
+
+static void qstate_free(qstate* s, const ref_state* r) {
+  for (int a = 0; a < 8; ++a) {
+    if (!s->arr[a]) continue;
+    for (int k = 0; k < r->K; ++k) free(s->arr[a][k]);
+    free(s->arr[a]);
+  }
+  for (int i = 0; i < s->pn; ++i) osel_free(&s->hsel[i]);
+  for (int i = 0; i < s->sn; ++i) osel_free(&s->ssel[i]);
+  free(s->hsel);
+  free(s->ssel);
+  free(s->pmin);
+  free(s->sw);
+  free(s->ignored);
+  osel_free(&s->dsel);
+  free_pod(&s->self);
+}
+
+/* NodeInfo.AddPod's pod-list side (types.go:456-480): the assumed pod becomes an existing pod */
+static void add_pod_record(ref_state* r, const kgpu_pod_query* q, const kgpu_pools* p, int n) {
+  rpod tmp;
+  incoming_pod(&tmp, q, p);
+  tmp.node = r->base + n;
+  rpod* pd = new_pod(r);
+  *pd = tmp;
+  node_add_pod(r, n, r->npods - 1);
+}
+
 /* ------------------------------------------------------------------ filters */
 static uint32_t filter_fit(const ref_state* r, const kgpu_pools* p, const kgpu_pod_query* q, int n) {
   /* noderesources/fit.go:194-267 fitsRequest */
@@ -212,8 +837,21 @@ static int filter_taints_ok(const ref_state* r, const kgpu_pools* p, const kgpu_
   return 1;
 }
 
+static int has_filter(const ref_state* r, int f) {
+  for (int i = 0; i < r->cfg.n_filters; ++i)
+    if (r->cfg.filters[i] == f) return 1;
+  return 0;
+}
+
+static int has_score(const ref_state* r, int sc) {
+  for (int i = 0; i < r->cfg.n_scores; ++i)
+    if (r->cfg.scores[i] == sc) return 1;
+  return 0;
+}
+
 /* RunFilterPlugins with early exit; returns the status word of include/kgpu.h */
-static uint32_t run_filter_plugins(const ref_state* r, const kgpu_pools* p, const kgpu_pod_query* q, int n) {
+static uint32_t run_filter_plugins(const ref_state* r, const kgpu_pools* p, const kgpu_pod_query* q, qstate* qs,
+                                   int n) {
   for (int i = 0; i < r->cfg.n_filters; ++i) {
     uint32_t pos = (uint32_t)(i + 1);
     switch (r->cfg.filters[i]) {
@@ -237,8 +875,16 @@ static uint32_t run_filter_plugins(const ref_state* r, const kgpu_pools* p, cons
       case KGPU_F_TAINT_TOLERATION:
         if (!filter_taints_ok(r, p, q, n)) return pos | (KGPU_CODE_UNRESOLVABLE << 8);
         break;
+      case KGPU_F_POD_TOPOLOGY_SPREAD:
+        if (!pts_filter_ok(qs, r, n)) return pos | (KGPU_CODE_UNSCHEDULABLE << 8);
+        break;
+      case KGPU_F_INTER_POD_AFFINITY: {
+        int rule = ipa_filter(qs, r, q, n);
+        if (rule) return pos | ((rule == 1 ? KGPU_CODE_UNRESOLVABLE : KGPU_CODE_UNSCHEDULABLE) << 8) | ((uint32_t)rule << 16);
+        break;
+      }
       default:
-        break; /* PodTopologySpread / InterPodAffinity: not in this build's tier */
+        break;
     }
   }
   return 0;
@@ -400,12 +1046,13 @@ typedef struct {
   const int* feasible;
   int nf;
   int64_t* scores; /* [n_scores][nf] */
+  qstate* qs;
 } work_t;
 
 static void process(work_t* w, int i) {
   const ref_state* r = w->r;
   if (w->phase == 0) {
-    w->status[i] = run_filter_plugins(r, w->p, w->q, i);
+    w->status[i] = run_filter_plugins(r, w->p, w->q, w->qs, i);
     return;
   }
   int n = w->feasible[i];
@@ -419,7 +1066,10 @@ static void process(work_t* w, int i) {
       case KGPU_S_NODE_PREFER_AVOID_PODS: v = prefer_avoid(r, w->q, n); break;
       case KGPU_S_TAINT_TOLERATION: v = taint_raw(r, w->p, w->q, n); break;
       case KGPU_S_NODE_AFFINITY: v = node_affinity_raw(r, w->p, w->q, n); break;
-      default: v = 0; break; /* PTS / DPTS / IPA raw scores for pods without terms: 0 */
+      case KGPU_S_POD_TOPOLOGY_SPREAD: v = pts_score(w->qs, r, w->q, n); break;
+      case KGPU_S_DEFAULT_POD_TOPOLOGY_SPREAD: v = dpts_score(w->qs, r, w->q, n); break;
+      case KGPU_S_INTER_POD_AFFINITY: v = ipa_score(w->qs, r, n); break;
+      default: v = 0; break;
     }
     w->scores[(size_t)k * w->nf + i] = v;
   }
@@ -549,6 +1199,14 @@ int kgpu_ref_schedule(ref_state* r, const kgpu_pod_query* qs, int nq, const kgpu
     pthread_mutex_init(&w.mu, NULL);
     w.r = r; w.p = p; w.q = q; w.status = status;
     w.phase = 0;
+    /* PreFilter (framework.go:369-389) */
+    qstate qst;
+    memset(&qst, 0, sizeof(qst));
+    incoming_pod(&qst.self, q, p);
+    qst.dsel = osel_from(&q->dpts, p);
+    if (has_filter(r, KGPU_F_POD_TOPOLOGY_SPREAD)) pts_prefilter(&qst, r, p, q);
+    if (has_filter(r, KGPU_F_INTER_POD_AFFINITY)) ipa_prefilter(&qst, r);
+    w.qs = &qst;
     parallel_until((pool_t*)r->pool, &w, N);
     int nf = 0;
     for (int i = 0; i < N; ++i) if (status[i] == 0) feasible[nf++] = i;
@@ -564,10 +1222,14 @@ int kgpu_ref_schedule(ref_state* r, const kgpu_pod_query* qs, int nq, const kgpu
     if (nf == 1) {
       res.node = r->base + feasible[0];
       add_pod(r, p, q, feasible[0]);
+      add_pod_record(r, q, p, feasible[0]);
     } else if (nf > 1) {
       if (q->flags & KGPU_Q_SCORE_ERROR) {
         res.node = -2;
       } else {
+        /* PreScore (framework.go:543-563) */
+        if (has_score(r, KGPU_S_POD_TOPOLOGY_SPREAD)) pts_prescore(&qst, r, p, q, feasible, nf);
+        if (has_score(r, KGPU_S_INTER_POD_AFFINITY)) ipa_prescore(&qst, r, r->cfg.hard_pod_affinity_weight);
         w.phase = 1;
         w.feasible = feasible;
         w.nf = nf;
@@ -580,18 +1242,9 @@ int kgpu_ref_schedule(ref_state* r, const kgpu_pod_query* qs, int nq, const kgpu
           if (last && raw_out) for (int i = 0; i < nf; ++i) raw_out[(size_t)plugin * N + feasible[i]] = s[i];
           if (plugin == KGPU_S_TAINT_TOLERATION) default_normalize(s, nf, 1);
           else if (plugin == KGPU_S_NODE_AFFINITY) default_normalize(s, nf, 0);
-          else if (plugin == KGPU_S_POD_TOPOLOGY_SPREAD) {
-            /* scoring.go:211-257 with no soft constraints: maxScore == 0 -> MaxNodeScore */
-            for (int i = 0; i < nf; ++i) s[i] = MAXN_SCORE;
-          } else if (plugin == KGPU_S_DEFAULT_POD_TOPOLOGY_SPREAD && !(q->flags & KGPU_Q_HAS_TSC)) {
-            /* default_pod_topology_spread.go:116-163 with all counts 0 */
-            const double zw = 2.0 / 3.0;
-            for (int i = 0; i < nf; ++i) {
-              double f = (double)MAXN_SCORE;
-              if (r->zone_id[feasible[i]] >= 0) f = (f * (1.0 - zw)) + (zw * (double)MAXN_SCORE);
-              s[i] = (int64_t)f;
-            }
-          }
+          else if (plugin == KGPU_S_POD_TOPOLOGY_SPREAD) pts_normalize(&qst, s, feasible, nf);
+          else if (plugin == KGPU_S_DEFAULT_POD_TOPOLOGY_SPREAD) dpts_normalize(r, q, s, feasible, nf);
+          else if (plugin == KGPU_S_INTER_POD_AFFINITY) ipa_normalize(&qst, s, nf);
           if (last && norm_out) for (int i = 0; i < nf; ++i) norm_out[(size_t)plugin * N + feasible[i]] = s[i];
           int64_t wgt = r->cfg.score_weights[k] > 0 ? r->cfg.score_weights[k] : 1;
           for (int i = 0; i < nf; ++i) totals[i] += s[i] * wgt;
@@ -607,8 +1260,10 @@ int kgpu_ref_schedule(ref_state* r, const kgpu_pod_query* qs, int nq, const kgpu
         res.scored = 1;
         res.score = totals[bi];
         add_pod(r, p, q, feasible[bi]);
+        add_pod_record(r, q, p, feasible[bi]);
       }
     }
+    qstate_free(&qst, r);
     out[qi] = res;
     pthread_mutex_destroy(&w.mu);
   }

@@ -125,3 +125,85 @@ def cluster(seed, n_nodes=20, n_existing=15, n_pods=30):
         existing.append(p)
     pods = [rpod(r, i, names) for i in range(n_pods)]
     return nodes, existing, pods
+
+
+# ---------------------------------------------------------------- topology workloads (PTS / IPA / DPTS)
+APPS = ["web", "db", "cache"]
+
+
+def _lsel(r):
+    kind = r.random()
+    if kind < 0.5:
+        return {"matchLabels": {"app": r.choice(APPS)}}
+    if kind < 0.7:
+        return {"matchExpressions": [{"key": "app", "operator": "In", "values": r.sample(APPS, 2)}]}
+    if kind < 0.85:
+        return {"matchExpressions": [{"key": r.choice(["tier", "app"]), "operator": "Exists"}]}
+    if kind < 0.95:
+        return {"matchExpressions": [{"key": "app", "operator": "NotIn", "values": [r.choice(APPS)]}]}
+    return {"matchExpressions": [{"key": "tier", "operator": "DoesNotExist"}]}
+
+
+def _pod_term(r):
+    t = {"labelSelector": _lsel(r), "topologyKey": r.choice([ZONE, HOST, REGION, "nokey"])}
+    if r.random() < 0.15:
+        t["namespaces"] = r.sample(["default", "other"], r.choice([1, 2]))
+    return t
+
+
+def _topo_spec(r, spec, md, p_tsc=0.5, p_aff=0.5):
+    if r.random() < p_tsc:
+        tsc = []
+        for _ in range(r.choice([1, 1, 2])):
+            tsc.append({"maxSkew": r.choice([1, 1, 2, 3]), "topologyKey": r.choice([ZONE, HOST, REGION, ZONE]),
+                        "whenUnsatisfiable": r.choice(["DoNotSchedule", "ScheduleAnyway"]),
+                        "labelSelector": _lsel(r)})
+        spec["topologySpreadConstraints"] = tsc
+    if r.random() < p_aff:
+        a = spec.setdefault("affinity", {})
+        for field in ("podAffinity", "podAntiAffinity"):
+            if r.random() < 0.5:
+                continue
+            sub = {}
+            if r.random() < 0.5:
+                sub["requiredDuringSchedulingIgnoredDuringExecution"] = [_pod_term(r) for _ in range(r.choice([1, 2]))]
+            if r.random() < 0.6:
+                sub["preferredDuringSchedulingIgnoredDuringExecution"] = [
+                    {"weight": r.choice([1, 10, 50, 100]), "podAffinityTerm": _pod_term(r)}
+                    for _ in range(r.choice([1, 2]))]
+            a[field] = sub
+        if not a:
+            del spec["affinity"]
+    labels = {"app": r.choice(APPS)}
+    if r.random() < 0.3:
+        labels["tier"] = r.choice(["fe", "be"])
+    md["labels"] = labels
+    if r.random() < 0.2:
+        md["namespace"] = "other"
+    if r.random() < 0.05:
+        md["deletionTimestamp"] = "2020-01-01T00:00:00Z"
+
+
+def topo_cluster(seed, n_nodes=16, n_existing=24, n_pods=30):
+    """Nodes over 3 zones / 2 regions (some unlabeled), existing pods with terms, incoming pods with
+    spread constraints and (anti-)affinity, plus services / replica sets for DefaultPodTopologySpread."""
+    r = random.Random(1000 + seed)
+    nodes = [rnode(r, i) for i in range(n_nodes)]
+    for n in nodes:  # generous capacity: topology plugins decide, not Fit
+        n["status"]["allocatable"].update({"cpu": "64", "memory": "256Gi", "pods": "110"})
+    names = [n["metadata"]["name"] for n in nodes]
+    existing = []
+    for i in range(n_existing):
+        p = rpod(r, 1000 + i, names, allow_node_name=False)
+        p["spec"]["nodeName"] = r.choice(names)
+        _topo_spec(r, p["spec"], p["metadata"], p_tsc=0.0, p_aff=0.4)
+        existing.append(p)
+    pods = []
+    for i in range(n_pods):
+        p = rpod(r, i, names, allow_node_name=False)
+        _topo_spec(r, p["spec"], p["metadata"])
+        pods.append(p)
+    services = [{"metadata": {"name": "svc-web", "namespace": "default"}, "spec": {"selector": {"app": "web"}}}]
+    rss = [{"metadata": {"name": "rs-db", "namespace": "default"},
+            "spec": {"selector": {"matchLabels": {"app": "db"}}}}]
+    return nodes, existing, pods, services, rss

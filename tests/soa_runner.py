@@ -1,20 +1,27 @@
 """Evaluate golden fixture cases through the product's compile step (kgpu.compile) and either
 the C restatement (oracle/c, CPU) or libkgpu.so (GPU).  Same result format as golden_runner."""
+import copy
+
 import numpy as np
 
 from kgpu import abi
-from kgpu.compile import Profile
+from kgpu.compile import Cluster, Profile
 from kgpu.framework import GpuFramework
 
 TIER1_SCORES = {"NodeResourcesLeastAllocated", "NodeResourcesMostAllocated", "NodeResourcesBalancedAllocation",
-                "TaintToleration", "NodeAffinity", "ImageLocality", "NodePreferAvoidPods"}
+                "TaintToleration", "NodeAffinity", "ImageLocality", "NodePreferAvoidPods", "PodTopologySpread",
+                "DefaultPodTopologySpread", "InterPodAffinity"}
 TIER1_FILTERS = {"NodeResourcesFit", "TaintToleration", "NodeAffinity", "NodeUnschedulable", "NodeName",
-                 "NodePorts"}
+                 "NodePorts", "PodTopologySpread", "InterPodAffinity"}
 
 
 def supported(c):
     k = c["kind"]
     if k == "score":
+        # a cycle with one feasible node returns it unscored (generic_scheduler.go:184-191): plugin-level
+        # tables over a single candidate are checked on the oracle only
+        if c.get("filtered") is not None and len(c["filtered"]) < 2:
+            return False
         return c["plugin"] in TIER1_SCORES
     if k == "filter":
         return c["plugin"] in TIER1_FILTERS
@@ -27,14 +34,18 @@ def supported(c):
 def _profile(c):
     a = c.get("args") or {}
     if c["kind"] == "score":
-        kw = dict(filters=[], scores=[(c["plugin"], 1)])
+        # nodes outside the case's "filtered" list are made infeasible through NodeUnschedulable
+        kw = dict(filters=["NodeUnschedulable"] if c.get("filtered") is not None else [], scores=[(c["plugin"], 1)])
+        if c["plugin"] == "InterPodAffinity":
+            kw["hard_pod_affinity_weight"] = a.get("hard_pod_affinity_weight", 1)
         if c["plugin"] == "NodeResourcesLeastAllocated":
             kw["least_resources"] = [tuple(r) for r in a.get("resources", [["cpu", 1], ["memory", 1]])]
         if c["plugin"] == "NodeResourcesMostAllocated":
             kw["most_resources"] = [tuple(r) for r in a.get("resources", [["cpu", 1], ["memory", 1]])]
         return Profile(**kw)
     if c["kind"] == "filter":
-        return Profile(filters=[c["plugin"]], scores=[], ignored_resources=a.get("ignored", []))
+        return Profile(filters=[c["plugin"]], scores=[], ignored_resources=a.get("ignored", []),
+                       pts_default_constraints=a.get("default_constraints", []))
     p = c.get("profile") or {}
     return Profile(filters=[f for f in p.get("filters", Profile.DEFAULT_FILTERS) if f in abi.FILTER_IDS],
                    scores=[tuple(s) for s in p.get("scores", Profile.DEFAULT_SCORES)])
@@ -46,7 +57,16 @@ def soa_eval(c, backend):
     except ValueError as e:
         return {"error": str(e)}
     pods = [c["pod"]] if c["kind"] in ("score", "filter") else c["schedule_pods"]
-    fw = GpuFramework(prof, c["nodes"], c.get("pods", []), pods_hint=pods, create_engine=(backend == "gpu"))
+    nodes = c["nodes"]
+    if c["kind"] == "score" and c.get("filtered") is not None:
+        keep = set(c["filtered"])
+        nodes = copy.deepcopy(nodes)
+        for n in nodes:
+            if n["metadata"]["name"] not in keep:
+                n.setdefault("spec", {})["unschedulable"] = True
+    cluster = Cluster(c.get("services", []), c.get("rcs", []), c.get("rss", []), c.get("sss", []))
+    fw = GpuFramework(prof, nodes, c.get("pods", []), cluster=cluster, pods_hint=pods,
+                      create_engine=(backend == "gpu"))
     pod = pods[0]
     if backend == "gpu":
         cr = fw.cycle(pod, assume=False)

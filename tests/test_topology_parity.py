@@ -1,0 +1,81 @@
+"""Seeded random clusters with PodTopologySpread / InterPodAffinity / DefaultPodTopologySpread
+constraints on the default profile: the Python oracle (objects) == the product's compile step + the
+C restatement (oracle/c) == libkgpu.so on the GPU.  Every placement of the scheduleOne loop is
+compared (node, feasible count, winner's total), so each pod also sees the previous pods' assumes
+in its PTS counts and IPA terms."""
+import numpy as np
+import pytest
+
+import gen_random
+from kgpu.compile import Cluster, Profile
+from kgpu.framework import GpuFramework
+from oracle.refsched import framework as F
+
+SEEDS = list(range(16))
+
+
+def oracle_run(nodes, existing, pods, services, rss):
+    res = F.schedule_sequence(nodes, existing, pods, F.Profile(), services=services, rss=rss)
+    out = []
+    for r in res:
+        if isinstance(r, F.FitError):
+            out.append((None, 0, None))
+        elif isinstance(r, F.ScheduleError):
+            out.append(("error", None, None))
+        else:
+            tot = dict((n, s) for n, s in r.totals)
+            out.append((r.host, r.feasible, tot.get(r.host) if len(r.totals) > 0 else None))
+    return out
+
+
+def product_run(nodes, existing, pods, services, rss, backend, threads=2):
+    fw = GpuFramework(Profile(), nodes, existing, cluster=Cluster(services=services, rss=rss), pods_hint=pods,
+                      create_engine=(backend == "gpu"))
+    if backend == "gpu":
+        res = fw.schedule(pods, first_seq=0)
+        rows = fw.engine.read_nodes(fw.snap.n_nodes)
+    else:
+        from oracle.cref import RefEngine
+        q, pc, pnp, errs = fw.compile_pods(pods)
+        assert not errs
+        ref = RefEngine(fw.config, fw.snap, threads=threads)
+        res = ref.schedule(q, pc)
+        rows = ref.read_nodes()
+    out = []
+    for r in res:
+        if r["node"] == -1:
+            out.append((None, 0, None))
+        elif r["node"] < -1:
+            out.append(("error", None, None))
+        else:
+            out.append((fw.order[r["node"]], int(r["feasible"]), int(r["score"]) if r["scored"] else None))
+    return out, rows
+
+
+def _cmp(want, got):
+    for i, (w, g) in enumerate(zip(want, got)):
+        assert w[0] == g[0], "pod %d: oracle %r, product %r" % (i, w, g)
+        if w[0] not in (None, "error"):
+            assert w[1] == g[1], "pod %d feasible %r vs %r" % (i, w, g)
+            if w[1] > 1:
+                assert w[2] == g[2], "pod %d score %r vs %r" % (i, w, g)
+
+
+@pytest.mark.parametrize("seed", SEEDS)
+def test_c_restatement_matches_python_oracle_topology(seed):
+    args = gen_random.topo_cluster(seed)
+    want = oracle_run(*args)
+    got, _ = product_run(*args, backend="ref")
+    _cmp(want, got)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", SEEDS)
+def test_gpu_matches_oracle_topology(seed):
+    args = gen_random.topo_cluster(seed)
+    want = oracle_run(*args)
+    got, rows = product_run(*args, backend="gpu")
+    _cmp(want, got)
+    _, rows_c = product_run(*args, backend="ref")
+    for k in rows:
+        np.testing.assert_array_equal(rows[k], rows_c[k], err_msg=k)
