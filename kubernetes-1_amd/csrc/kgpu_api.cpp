@@ -8,8 +8,10 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -62,6 +64,28 @@ struct kgpu_ctx {
   int32_t n_snapshot_pods = 0;
   bool last_diag = false;
   std::vector<hipEvent_t> ev_pool;
+  // ---- topology state (kgpu_internal.h "topology plugins")
+  std::map<std::vector<int64_t>, int> class_ids, tclass_ids;
+  std::vector<kgpu::ClassRec> classes;
+  std::vector<kgpu::ClassItem> citems;
+  std::vector<kgpu::TermClassRec> tclasses;
+  std::vector<kgpu_req> creqs;
+  std::vector<int32_t> cints;
+  int classes_init = 0;          // classes whose mcnt column is initialized on the device
+  int Ccap = 0, TCcap = 0;
+  DevBuf d_classes, d_citems, d_tclasses, d_creqs, d_cints, d_plans, d_aux, d_aux_terms, scratch, d_pods;
+  std::vector<int32_t> tcnt_host_init;  // unused placeholder for symmetry
+  // host mirror of the pod table (snapshot pods, then assumed pods in slot order)
+  struct PodRow {
+    int32_t node, ns;
+    uint32_t flags;
+    std::vector<int32_t> pairs;  // (pod label key id, value id)
+    std::vector<int32_t> own_tcls;
+  };
+  std::vector<PodRow> pod_rows;
+  int pod_rows_dev = -1;         // rows present in the device pod table (-1: table never uploaded)
+  std::vector<int32_t> key_n_values, key_empty;
+  int64_t max_key_values = 1;
 };
 
 namespace {
@@ -159,14 +183,391 @@ bool needs_norm(const kgpu_ctx* c, const kgpu_pod_query& q, const kgpu_pools* p)
   return false;
 }
 
-// Tier check: features whose kernels are not in this build (the pod falls back to the caller).
-const char* unsupported(const kgpu_ctx* c, const kgpu_pod_query& q) {
-  if (q.pts_hard.count || q.pts_soft.count) return "PodTopologySpread constraints";
-  if (q.dpts.kind != kgpu::kSelEmpty && !(q.flags & KGPU_Q_HAS_TSC) && has_score(c, KGPU_S_DEFAULT_POD_TOPOLOGY_SPREAD))
-    return "DefaultPodTopologySpread selector";
-  if (q.ipa_req_aff.count || q.ipa_req_anti.count || q.ipa_pref_aff.count || q.ipa_pref_anti.count)
-    return "InterPodAffinity terms";
-  return nullptr;
+
+// ---------------------------------------------------------------- topology: pod classes
+// Classes are interned by content, so every pod with the same spread selector / term shares one
+// match-count column.  Selector requirements and namespace sets are copied into the class pool.
+bool topo_profile(const kgpu_ctx* c) {
+  for (int i = 0; i < c->cfg.n_filters; ++i)
+    if (c->cfg.filters[i] == KGPU_F_POD_TOPOLOGY_SPREAD || c->cfg.filters[i] == KGPU_F_INTER_POD_AFFINITY) return true;
+  return has_score(c, KGPU_S_POD_TOPOLOGY_SPREAD) || has_score(c, KGPU_S_INTER_POD_AFFINITY) ||
+         has_score(c, KGPU_S_DEFAULT_POD_TOPOLOGY_SPREAD);
+}
+
+bool has_filter(const kgpu_ctx* c, int f) {
+  for (int i = 0; i < c->cfg.n_filters; ++i)
+    if (c->cfg.filters[i] == f) return true;
+  return false;
+}
+
+struct ItemSrc {
+  std::vector<int32_t> ns;
+  kgpu_selector sel;
+  const kgpu_pools* p;
+};
+
+void key_push_item(std::vector<int64_t>& k, const ItemSrc& it) {
+  std::vector<int32_t> ns = it.ns;
+  std::sort(ns.begin(), ns.end());
+  k.push_back((int64_t)ns.size());
+  for (int32_t x : ns) k.push_back(x);
+  k.push_back(it.sel.kind);
+  const int nr = it.sel.kind == KGPU_SEL_AND ? it.sel.reqs.count : 0;
+  k.push_back(nr);
+  for (int i = 0; i < nr; ++i) {
+    const kgpu_req& r = it.p->reqs[it.sel.reqs.begin + i];
+    std::vector<int32_t> v(it.p->ints + r.vals.begin, it.p->ints + r.vals.begin + r.vals.count);
+    std::sort(v.begin(), v.end());
+    k.push_back(r.key);
+    k.push_back(r.op);
+    k.push_back(r.imm);
+    k.push_back((int64_t)v.size());
+    for (int32_t x : v) k.push_back(x);
+  }
+}
+
+kgpu::ClassItem store_item(kgpu_ctx* c, const ItemSrc& it) {
+  kgpu::ClassItem o{};
+  o.ns.begin = (int32_t)c->cints.size();
+  o.ns.count = (int32_t)it.ns.size();
+  c->cints.insert(c->cints.end(), it.ns.begin(), it.ns.end());
+  o.sel.kind = it.sel.kind;
+  const int nr = it.sel.kind == KGPU_SEL_AND ? it.sel.reqs.count : 0;
+  std::vector<kgpu_req> reqs;
+  for (int i = 0; i < nr; ++i) {
+    kgpu_req r = it.p->reqs[it.sel.reqs.begin + i];
+    const int32_t b = (int32_t)c->cints.size();
+    c->cints.insert(c->cints.end(), it.p->ints + r.vals.begin, it.p->ints + r.vals.begin + r.vals.count);
+    r.vals.begin = b;
+    reqs.push_back(r);
+  }
+  o.sel.reqs.begin = (int32_t)c->creqs.size();
+  o.sel.reqs.count = nr;
+  c->creqs.insert(c->creqs.end(), reqs.begin(), reqs.end());
+  return o;
+}
+
+int intern_class(kgpu_ctx* c, int excl, const std::vector<ItemSrc>& items) {
+  std::vector<int64_t> k{0, excl, (int64_t)items.size()};
+  for (const ItemSrc& it : items) key_push_item(k, it);
+  auto f = c->class_ids.find(k);
+  if (f != c->class_ids.end()) return f->second;
+  kgpu::ClassRec cr{};
+  cr.item0 = (int32_t)c->citems.size();
+  cr.n_items = (int32_t)items.size();
+  cr.excl_terminating = excl;
+  for (const ItemSrc& it : items) c->citems.push_back(store_item(c, it));
+  const int id = (int)c->classes.size();
+  c->classes.push_back(cr);
+  c->class_ids[k] = id;
+  return id;
+}
+
+int intern_tclass(kgpu_ctx* c, int kind, int weight, int topo_key, const ItemSrc& it) {
+  std::vector<int64_t> k{1, kind, weight, topo_key};
+  key_push_item(k, it);
+  auto f = c->tclass_ids.find(k);
+  if (f != c->tclass_ids.end()) return f->second;
+  kgpu::TermClassRec t{};
+  t.kind = kind;
+  t.weight = weight;
+  t.topo_key = topo_key;
+  t.item = store_item(c, it);
+  const int id = (int)c->tclasses.size();
+  c->tclasses.push_back(t);
+  c->tclass_ids[k] = id;
+  return id;
+}
+
+ItemSrc term_item(const kgpu_pod_term& t, const kgpu_pools* p) {
+  ItemSrc it;
+  it.ns.assign(p->ints + t.ns.begin, p->ints + t.ns.begin + t.ns.count);
+  it.sel = t.sel;
+  it.p = p;
+  return it;
+}
+
+// labels.Selector.Matches of a class item against a pod given as (key, value) pairs
+// (selector.go:198-242; util/topologies.go:40-49).
+bool item_matches(const kgpu_ctx* c, const kgpu::ClassItem& it, int32_t ns, const int32_t* pairs, int np) {
+  bool in_ns = false;
+  for (int i = 0; i < it.ns.count; ++i) in_ns |= c->cints[it.ns.begin + i] == ns;
+  if (!in_ns || it.sel.kind != KGPU_SEL_AND) return false;
+  for (int i = 0; i < it.sel.reqs.count; ++i) {
+    const kgpu_req& r = c->creqs[it.sel.reqs.begin + i];
+    int v = -1;
+    for (int j = 0; j < np; ++j)
+      if (pairs[2 * j] == r.key) v = pairs[2 * j + 1];
+    if (r.key < 0) v = -1;
+    bool in = false;
+    for (int j = 0; j < r.vals.count; ++j) in |= c->cints[r.vals.begin + j] == v;
+    switch (r.op) {
+      case KGPU_OP_IN: if (!(v >= 0 && in)) return false; break;
+      case KGPU_OP_NOTIN: if (v >= 0 && in) return false; break;
+      case KGPU_OP_EXISTS: if (v < 0) return false; break;
+      case KGPU_OP_DNE: if (v >= 0) return false; break;
+      default: return false;
+    }
+  }
+  return true;
+}
+
+bool class_matches(const kgpu_ctx* c, int cls, int32_t ns, uint32_t flags, const int32_t* pairs, int np) {
+  const kgpu::ClassRec& cr = c->classes[cls];
+  if (cr.excl_terminating && (flags & KGPU_PF_TERMINATING)) return false;
+  if (cr.n_items == 0) return false;
+  for (int i = 0; i < cr.n_items; ++i)
+    if (!item_matches(c, c->citems[cr.item0 + i], ns, pairs, np)) return false;
+  return true;
+}
+
+uint32_t query_pod_flags(const kgpu_pod_query& q) {
+  return KGPU_PF_ACTIVE | ((q.flags & KGPU_Q_TERMINATING) ? KGPU_PF_TERMINATING : 0u) |
+         ((q.flags & (KGPU_Q_HAS_POD_AFFINITY | KGPU_Q_HAS_POD_ANTI)) ? KGPU_PF_WITH_AFFINITY : 0u);
+}
+
+struct SlotAlloc {
+  kgpu::QPlan* pl;
+  const kgpu_ctx* c;
+  int64_t off;
+  int get(int kind, int key) {
+    for (int s = 0; s < pl->n_slots; ++s)
+      if (pl->slot_kind[s] == kind && pl->slot_key[s] == key) return s;
+    if (pl->n_slots == kgpu::kMaxSlots) return -1;
+    const int s = pl->n_slots++;
+    pl->slot_kind[s] = kind;
+    pl->slot_key[s] = key;
+    pl->slot_off[s] = off;
+    off += key >= 0 ? std::max<int64_t>(1, c->key_n_values[key]) : 1;
+    return s;
+  }
+};
+
+// Per-query plans of a batch: pass 1 interns every class / term class the batch needs, pass 2
+// matches each pod against all of them (its assume increments and the existing terms it meets).
+int build_plans(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools* p,
+                std::vector<kgpu::QPlan>& plans, std::vector<int32_t>& aux, std::vector<kgpu::TTerm>& aux_terms,
+                int64_t* max_scratch) {
+  const bool fp = has_filter(c, KGPU_F_POD_TOPOLOGY_SPREAD), fi = has_filter(c, KGPU_F_INTER_POD_AFFINITY);
+  const bool sp = has_score(c, KGPU_S_POD_TOPOLOGY_SPREAD), si = has_score(c, KGPU_S_INTER_POD_AFFINITY);
+  const bool sd = has_score(c, KGPU_S_DEFAULT_POD_TOPOLOGY_SPREAD);
+  const int hw = c->cfg.hard_pod_affinity_weight;
+  plans.assign((size_t)n, kgpu::QPlan{});
+  std::vector<std::vector<int32_t>> own((size_t)n);
+  for (int32_t i = 0; i < n; ++i) {
+    const kgpu_pod_query& q = qs[i];
+    kgpu::QPlan& pl = plans[(size_t)i];
+    SlotAlloc sa{&pl, c, (int64_t)kgpu::kHdrWords + std::max(c->st.n_zones, 1)};
+    auto spread = [&](const kgpu_spread& sp0, bool hard, kgpu::TSpread& o, int idx, const kgpu_spread* all) {
+      ItemSrc it{{q.ns}, sp0.sel, p};
+      o.cls = intern_class(c, 1, {it});
+      o.key = sp0.key;
+      o.max_skew = sp0.max_skew;
+      o.self_match = sp0.self_match;
+      o.is_hostname = sp0.is_hostname;
+      o.first_of_key = 1;
+      for (int j = 0; j < idx; ++j)
+        if (all[j].key == sp0.key) o.first_of_key = 0;
+      o.rslot = sa.get(hard ? kgpu::kSlotPReg : kgpu::kSlotSReg, sp0.key);
+      o.cslot = sa.get(hard ? kgpu::kSlotPCnt : kgpu::kSlotSCnt, sp0.key);
+      return o.rslot >= 0 && o.cslot >= 0;
+    };
+    if (fp && q.pts_hard.count) {
+      if (q.pts_hard.count > kgpu::kMaxSpread) return fail(c, KGPU_E_UNSUPPORTED, "more than 4 DoNotSchedule constraints");
+      pl.n_hard = q.pts_hard.count;
+      for (int j = 0; j < pl.n_hard; ++j)
+        if (!spread(p->spreads[q.pts_hard.begin + j], true, pl.hard[j], j, p->spreads + q.pts_hard.begin))
+          return fail(c, KGPU_E_UNSUPPORTED, "too many topology histograms");
+    }
+    if (sp && q.pts_soft.count) {
+      if (q.pts_soft.count > kgpu::kMaxSpread) return fail(c, KGPU_E_UNSUPPORTED, "more than 4 ScheduleAnyway constraints");
+      pl.n_soft = q.pts_soft.count;
+      for (int j = 0; j < pl.n_soft; ++j)
+        if (!spread(p->spreads[q.pts_soft.begin + j], false, pl.soft[j], j, p->spreads + q.pts_soft.begin))
+          return fail(c, KGPU_E_UNSUPPORTED, "too many topology histograms");
+    }
+    pl.dpts_cls = -1;
+    if (sd) {
+      if (q.flags & KGPU_Q_HAS_TSC) pl.dpts_cls = -2;
+      else if (q.dpts.kind != kgpu::kSelEmpty) pl.dpts_cls = intern_class(c, 1, {ItemSrc{{q.ns}, q.dpts, p}});
+    }
+    if (fi) {
+      if (q.ipa_req_aff.count > kgpu::kMaxIpa || q.ipa_req_anti.count > kgpu::kMaxIpa)
+        return fail(c, KGPU_E_UNSUPPORTED, "more than 4 required (anti-)affinity terms");
+      if (q.ipa_req_aff.count) {
+        std::vector<ItemSrc> items;
+        for (int j = 0; j < q.ipa_req_aff.count; ++j) items.push_back(term_item(p->pod_terms[q.ipa_req_aff.begin + j], p));
+        pl.conj_cls = intern_class(c, 0, items);
+        pl.n_aff = q.ipa_req_aff.count;
+        for (int j = 0; j < pl.n_aff; ++j) {
+          const kgpu_pod_term& t = p->pod_terms[q.ipa_req_aff.begin + j];
+          pl.aff[j] = kgpu::TTerm{pl.conj_cls, t.topo_key, sa.get(kgpu::kSlotAff, t.topo_key), 0};
+          if (pl.aff[j].slot < 0) return fail(c, KGPU_E_UNSUPPORTED, "too many topology histograms");
+        }
+      }
+      pl.n_anti = q.ipa_req_anti.count;
+      for (int j = 0; j < pl.n_anti; ++j) {
+        const kgpu_pod_term& t = p->pod_terms[q.ipa_req_anti.begin + j];
+        pl.anti[j] = kgpu::TTerm{intern_class(c, 0, {term_item(t, p)}), t.topo_key, sa.get(kgpu::kSlotAnti, t.topo_key), 0};
+        if (pl.anti[j].slot < 0) return fail(c, KGPU_E_UNSUPPORTED, "too many topology histograms");
+      }
+      pl.self_all = (q.flags & KGPU_Q_SELF_MATCH_ALL_AFF) ? 1 : 0;
+    }
+    if (si) {
+      for (int kind = 0; kind < 2; ++kind) {
+        const kgpu_range r = kind == 0 ? q.ipa_pref_aff : q.ipa_pref_anti;
+        for (int j = 0; j < r.count; ++j) {
+          const kgpu_pod_term& t = p->pod_terms[r.begin + j];
+          if (t.topo_key < 0) continue;
+          if (pl.n_pref == kgpu::kMaxPref) return fail(c, KGPU_E_UNSUPPORTED, "more than 8 preferred pod terms");
+          pl.pref[pl.n_pref++] = kgpu::TTerm{intern_class(c, 0, {term_item(t, p)}), t.topo_key,
+                                             sa.get(kgpu::kSlotTopo, t.topo_key), kind == 0 ? t.weight : -t.weight};
+          if (pl.pref[pl.n_pref - 1].slot < 0) return fail(c, KGPU_E_UNSUPPORTED, "too many topology histograms");
+        }
+      }
+    }
+    // the pod's own terms (PodInfo, types.go:92-160): term classes it adds on assume
+    const kgpu_range tr[4] = {q.ipa_req_aff, q.ipa_req_anti, q.ipa_pref_aff, q.ipa_pref_anti};
+    const int tk[4] = {KGPU_TERM_REQ_AFF, KGPU_TERM_REQ_ANTI, KGPU_TERM_PREF_AFF, KGPU_TERM_PREF_ANTI};
+    for (int k = 0; k < 4; ++k)
+      for (int j = 0; j < tr[k].count; ++j) {
+        const kgpu_pod_term& t = p->pod_terms[tr[k].begin + j];
+        own[(size_t)i].push_back(intern_tclass(c, tk[k], t.weight, t.topo_key, term_item(t, p)));
+      }
+    pl.scratch_len = sa.off;
+  }
+  // pass 2: matches against every class / term class
+  for (int32_t i = 0; i < n; ++i) {
+    const kgpu_pod_query& q = qs[i];
+    kgpu::QPlan& pl = plans[(size_t)i];
+    SlotAlloc sa{&pl, c, pl.scratch_len};
+    const int32_t* pairs = q.labels.count ? p->ints + q.labels.begin : nullptr;
+    const int np = q.labels.count / 2;
+    const uint32_t fl = query_pod_flags(q);
+    pl.assume_cls.begin = (int32_t)aux.size();
+    for (int cl = 0; cl < (int)c->classes.size(); ++cl)
+      if (class_matches(c, cl, q.ns, fl, pairs, np)) aux.push_back(cl);
+    pl.assume_cls.count = (int32_t)aux.size() - pl.assume_cls.begin;
+    pl.own_tcls.begin = (int32_t)aux.size();
+    aux.insert(aux.end(), own[(size_t)i].begin(), own[(size_t)i].end());
+    pl.own_tcls.count = (int32_t)own[(size_t)i].size();
+    // existing pods' terms that match this pod: required anti-affinity first (filter), then the
+    // score terms (scoring.go:109-124)
+    pl.ex.begin = (int32_t)aux_terms.size();
+    for (int pass = 0; pass < 2; ++pass) {
+      for (int t = 0; t < (int)c->tclasses.size(); ++t) {
+        const kgpu::TermClassRec& tc = c->tclasses[t];
+        if (tc.topo_key < 0) continue;
+        int w;
+        if (pass == 0) {
+          if (!fi || tc.kind != KGPU_TERM_REQ_ANTI) continue;
+          w = 0;
+        } else {
+          if (!si) continue;
+          if (tc.kind == KGPU_TERM_REQ_AFF) {
+            if (hw <= 0) continue;
+            w = hw;
+          } else if (tc.kind == KGPU_TERM_PREF_AFF) {
+            w = tc.weight;
+          } else if (tc.kind == KGPU_TERM_PREF_ANTI) {
+            w = -tc.weight;
+          } else {
+            continue;
+          }
+        }
+        if (!item_matches(c, tc.item, q.ns, pairs, np)) continue;
+        const int slot = sa.get(pass == 0 ? kgpu::kSlotExA : kgpu::kSlotTopo, tc.topo_key);
+        if (slot < 0) return fail(c, KGPU_E_UNSUPPORTED, "too many topology histograms");
+        aux_terms.push_back(kgpu::TTerm{t, tc.topo_key, slot, w});
+      }
+      if (pass == 0) pl.n_ex_anti = (int32_t)aux_terms.size() - pl.ex.begin;
+    }
+    pl.ex.count = (int32_t)aux_terms.size() - pl.ex.begin;
+    pl.scratch_len = sa.off;
+    pl.topo = (pl.n_hard || pl.n_soft || pl.dpts_cls >= 0 || pl.n_aff || pl.n_anti || pl.n_pref || pl.ex.count) ? 1 : 0;
+    *max_scratch = std::max(*max_scratch, pl.scratch_len);
+  }
+  return KGPU_OK;
+}
+
+// Grow an int32 [cap][N] column table to hold `need` columns (existing columns kept).
+int grow_columns(kgpu_ctx* c, int32_t** tab, int* cap, int need) {
+  if (need <= *cap && *tab) return KGPU_OK;
+  int nc = std::max(16, *cap);
+  while (nc < need) nc *= 2;
+  const size_t N = (size_t)std::max(c->st.N, 1);
+  int32_t* t = nullptr;
+  HIP_OK(c, hipMalloc(&t, sizeof(int32_t) * N * nc));
+  HIP_OK(c, hipMemsetAsync(t, 0, sizeof(int32_t) * N * nc, c->stream));
+  if (*tab && *cap) HIP_OK(c, hipMemcpyAsync(t, *tab, sizeof(int32_t) * N * (*cap), hipMemcpyDeviceToDevice, c->stream));
+  HIP_OK(c, hipStreamSynchronize(c->stream));
+  if (*tab) (void)hipFree(*tab);
+  *tab = t;
+  *cap = nc;
+  return KGPU_OK;
+}
+
+// Upload the host pod table (node, ns, flags, dense labels) for k_class_init.
+int upload_pod_table(kgpu_ctx* c) {
+  const int rows = (int)c->pod_rows.size();
+  int pk = 0;
+  for (const auto& r : c->pod_rows)
+    for (size_t j = 0; j + 1 < r.pairs.size(); j += 2) pk = std::max(pk, r.pairs[j] + 1);
+  pk = std::max(pk, 1);
+  const size_t R = (size_t)std::max(rows, 1);
+  std::vector<int32_t> buf(R * (3 + (size_t)pk), -1);
+  for (int i = 0; i < rows; ++i) {
+    const auto& r = c->pod_rows[(size_t)i];
+    buf[(size_t)i] = r.node;
+    buf[R + i] = r.ns;
+    buf[2 * R + i] = (int32_t)r.flags;
+    for (size_t j = 0; j + 1 < r.pairs.size(); j += 2) buf[(3 + (size_t)r.pairs[j]) * R + i] = r.pairs[j + 1];
+  }
+  int rc;
+  if ((rc = ensure(c, c->d_pods, sizeof(int32_t) * buf.size()))) return rc;
+  HIP_OK(c, hipMemcpyAsync(c->d_pods.p, buf.data(), sizeof(int32_t) * buf.size(), hipMemcpyHostToDevice, c->stream));
+  HIP_OK(c, hipStreamSynchronize(c->stream));
+  int32_t* b = static_cast<int32_t*>(c->d_pods.p);
+  c->st.pod_node = b;
+  c->st.pod_ns = b + R;
+  c->st.pod_flags = reinterpret_cast<uint32_t*>(b + 2 * R);
+  c->st.pod_lab = b + 3 * R;
+  c->st.Pcap = (int32_t)R;
+  c->st.PKcap = pk;
+  c->pod_rows_dev = rows;
+  return KGPU_OK;
+}
+
+template <class T>
+int upload_vec(kgpu_ctx* c, DevBuf& b, const std::vector<T>& v, const T** dst) {
+  int rc = ensure(c, b, sizeof(T) * std::max<size_t>(v.size(), 1));
+  if (rc) return rc;
+  if (!v.empty()) HIP_OK(c, hipMemcpyAsync(b.p, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice, c->stream));
+  *dst = static_cast<const T*>(b.p);
+  return KGPU_OK;
+}
+
+// Go's math.Log (FreeBSD e_log.c, src/math/log.go) for the PodTopologySpread weight table.
+double go_log(double x) {
+  const double ln2hi = 6.93147180369123816490e-01, ln2lo = 1.90821492927058770002e-10;
+  const double L1 = 6.666666666666735130e-01, L2 = 3.999999999940941908e-01, L3 = 2.857142874366239149e-01,
+               L4 = 2.222219843214978396e-01, L5 = 1.818357216161805012e-01, L6 = 1.531383769920937332e-01,
+               L7 = 1.479819860511658591e-01;
+  if (std::isnan(x) || std::isinf(x)) return x;
+  if (x < 0) return NAN;
+  if (x == 0) return -INFINITY;
+  int ki;
+  double f1 = std::frexp(x, &ki);
+  if (f1 < 0.70710678118654752440) {
+    f1 *= 2;
+    ki--;
+  }
+  const double f = f1 - 1, k = (double)ki;
+  const double s = f / (2 + f), s2 = s * s, s4 = s2 * s2;
+  const double t1 = s2 * (L1 + s4 * (L3 + s4 * (L5 + s4 * L7)));
+  const double t2 = s4 * (L2 + s4 * (L4 + s4 * L6));
+  const double R = t1 + t2, hfsq = 0.5 * f * f;
+  return k * ln2hi - ((hfsq - (s * (hfsq + R) + k * ln2lo)) - f);
 }
 
 hipEvent_t get_event(kgpu_ctx* c, size_t i) {
@@ -182,11 +583,58 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
               kgpu_result* results, kgpu_stats* stats, bool diag, int32_t assume) {
   if (!c->uploaded) return fail(c, KGPU_E_STATE, "no snapshot uploaded");
   if (n <= 0) return KGPU_OK;
-  for (int32_t i = 0; i < n; ++i) {
-    const char* why = unsupported(c, qs[i]);
-    if (why) return fail(c, KGPU_E_UNSUPPORTED, std::string("pod ") + std::to_string(i) + ": " + why);
-  }
   int rc;
+  // topology plugins: plans, class columns, pools (kgpu_internal.h "topology plugins")
+  std::vector<kgpu::QPlan> plans;
+  std::vector<int32_t> aux;
+  std::vector<kgpu::TTerm> aux_terms;
+  int64_t max_scratch = 0;
+  const bool topo_on = topo_profile(c);
+  if (topo_on) {
+    kgpu_pools empty{};
+    if ((rc = build_plans(c, qs, n, pools ? pools : &empty, plans, aux, aux_terms, &max_scratch))) return rc;
+    if ((rc = grow_columns(c, &c->st.mcnt, &c->Ccap, (int)c->classes.size()))) return rc;
+    if ((rc = grow_columns(c, &c->st.tcnt, &c->TCcap, (int)c->tclasses.size()))) return rc;
+    const kgpu::ClassRec* dcl;
+    const kgpu::ClassItem* dci;
+    const kgpu::TermClassRec* dtc;
+    const kgpu_req* dcr;
+    const int32_t* dcint;
+    if ((rc = upload_vec(c, c->d_classes, c->classes, &dcl)) || (rc = upload_vec(c, c->d_citems, c->citems, &dci)) ||
+        (rc = upload_vec(c, c->d_tclasses, c->tclasses, &dtc)) || (rc = upload_vec(c, c->d_creqs, c->creqs, &dcr)) ||
+        (rc = upload_vec(c, c->d_cints, c->cints, &dcint)))
+      return rc;
+    c->st.classes = dcl;
+    c->st.class_items = dci;
+    c->st.tclasses = dtc;
+    c->st.creqs = dcr;
+    c->st.cints = dcint;
+    if (c->classes_init < (int)c->classes.size()) {
+      // fresh mcnt columns: counted on the device over the pod table (snapshot + assumed pods)
+      if (c->pod_rows_dev != (int)c->pod_rows.size() && (rc = upload_pod_table(c))) return rc;
+      if ((rc = ensure(c, c->dstate, sizeof(DevState)))) return rc;
+      c->st_batch = c->st;
+      HIP_OK(c, hipMemcpyAsync(c->dstate.p, &c->st_batch, sizeof(DevState), hipMemcpyHostToDevice, c->stream));
+      if (kgpu::launch_class_init(static_cast<const DevState*>(c->dstate.p), c->classes_init,
+                                  (int)c->classes.size() - c->classes_init, (int)c->pod_rows.size(), c->stream))
+        return fail(c, KGPU_E_DEVICE, "k_class_init launch failed");
+      HIP_OK(c, hipStreamSynchronize(c->stream));
+      c->classes_init = (int)c->classes.size();
+    }
+    const kgpu::QPlan* dpl;
+    const int32_t* dax;
+    const kgpu::TTerm* dat;
+    if ((rc = upload_vec(c, c->d_plans, plans, &dpl)) || (rc = upload_vec(c, c->d_aux, aux, &dax)) ||
+        (rc = upload_vec(c, c->d_aux_terms, aux_terms, &dat)))
+      return rc;
+    c->st.plans = dpl;
+    c->st.aux = dax;
+    c->st.aux_terms = dat;
+    if ((rc = ensure(c, c->scratch, sizeof(int64_t) * (size_t)std::max<int64_t>(max_scratch, 1)))) return rc;
+    c->st.scratch = static_cast<int64_t*>(c->scratch.p);
+  } else {
+    c->st.plans = nullptr;
+  }
   if ((rc = upload_pools(c, pools))) return rc;
   if ((rc = ensure(c, c->queries, sizeof(kgpu_pod_query) * (size_t)n))) return rc;
   HIP_OK(c, hipMemcpyAsync(c->queries.p, qs, sizeof(kgpu_pod_query) * (size_t)n, hipMemcpyHostToDevice, c->stream));
@@ -213,17 +661,45 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
   // Persistent geometry: one workgroup per CU at most, K node rows per lane in registers.
   int per = 0, groups = 0;
   const int kidx = (c->persistent && !diag) ? kgpu::batch_geometry(st.N, std::min(c->max_groups > 0 ? std::min(c->max_groups, c->n_cus) : c->n_cus, 256), &per, &groups) : -1;
-  std::vector<uint8_t> norm((size_t)n);
-  // pods that need the normalize pass or whose scoring fails take the one-launch-per-pod path
-  for (int32_t i = 0; i < n; ++i)
+  std::vector<uint8_t> norm((size_t)n), topo((size_t)n, 0);
+  // pods that need the normalize pass or whose scoring fails take the one-launch-per-pod path;
+  // pods with topology state take the topology pipeline
+  for (int32_t i = 0; i < n; ++i) {
     norm[(size_t)i] = (diag || needs_norm(c, qs[i], pools) || (qs[i].flags & KGPU_Q_SCORE_ERROR)) ? 1 : 0;
+    if (topo_on) topo[(size_t)i] = plans[(size_t)i].topo ? 1 : 0;
+  }
   bool used_persistent = false;
   int32_t i = 0;
   while (i < n) {
     int32_t j = i;
+    if (topo[(size_t)i]) {
+      const kgpu::QPlan& pl = plans[(size_t)i];
+      if (i == 0 || !topo[(size_t)i - 1])
+        HIP_OK(c, hipMemsetAsync(c->st.scratch, 0, sizeof(int64_t) * (size_t)pl.scratch_len, c->stream));
+      int64_t min_values = 0;
+      for (int k = 0; k < pl.n_hard; ++k)
+        if (pl.hard[k].key >= 0) min_values = std::max<int64_t>(min_values, c->key_n_values[pl.hard[k].key]);
+      const int64_t next = (i + 1 < n && topo[(size_t)i + 1]) ? plans[(size_t)i + 1].scratch_len : 0;
+      PodArgs a{};
+      a.pod = i;
+      a.prev = -1;
+      a.parity = i & 1;
+      a.norm = 1;
+      a.assume = assume;
+      a.diag = diag ? 1 : 0;
+      a.seq = first_seq + i;
+      if (c->timing) HIP_OK(c, hipEventRecord(get_event(c, ev), c->stream));
+      if (kgpu::launch_topo(dst, a, blocks, min_values, next, c->stream))
+        return fail(c, KGPU_E_DEVICE, "topology pipeline launch failed");
+      if (c->timing) HIP_OK(c, hipEventRecord(get_event(c, ev + 1), c->stream));
+      ev += 2;
+      ++timed_passes;
+      i = i + 1;
+      continue;
+    }
     if (kidx >= 0 && !norm[(size_t)i]) {
       // a run of pods with constant normalize maxima: one persistent launch
-      while (j < n && !norm[(size_t)j]) ++j;
+      while (j < n && !norm[(size_t)j] && !topo[(size_t)j]) ++j;
       const int32_t cnt = j - i;
       // layout: abort word (64 B) | granules [cnt][groups] u64 | feasible counts [cnt][groups] i32
       const size_t cells = (size_t)cnt * (size_t)groups;
@@ -259,7 +735,7 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
       used_persistent = true;
     } else {
       // one launch per pod; the next launch resolves (and assumes) the previous pod's winner
-      while (j < n && (kidx < 0 || norm[(size_t)j])) ++j;
+      while (j < n && (kidx < 0 || norm[(size_t)j]) && !topo[(size_t)j]) ++j;
       int prev = -1;
       for (int32_t k = i; k < j; ++k) {
         PodArgs a{};
@@ -316,10 +792,23 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
       stats->eval_launches += timed_passes;
     }
   }
-  // keep host records of assumed pods for ForgetPod
+  // keep host records of assumed pods for ForgetPod (and the pod table for later classes)
   if (assume) {
     for (int32_t i = 0; i < n; ++i) {
       if (results[i].node < 0) continue;
+      {
+        kgpu_ctx::PodRow row;
+        row.node = results[i].node;
+        row.ns = qs[i].ns;
+        row.flags = query_pod_flags(qs[i]);
+        if (pools && qs[i].labels.count)
+          row.pairs.assign(pools->ints + qs[i].labels.begin, pools->ints + qs[i].labels.begin + qs[i].labels.count);
+        if (topo_on) {
+          const kgpu_range ot = plans[(size_t)i].own_tcls;
+          row.own_tcls.assign(aux.begin() + ot.begin, aux.begin() + ot.begin + ot.count);
+        }
+        c->pod_rows.push_back(std::move(row));
+      }
       kgpu_ctx::Assumed a;
       a.node = results[i].node - c->st.node_base;
       a.q = qs[i];
@@ -431,8 +920,12 @@ int kgpu_destroy(kgpu_ctx* c) {
   free_all(c->snap_allocs);
   free_all(c->work_allocs);
   for (DevBuf* b : {&c->dstate, &c->queries, &c->reqs, &c->ints, &c->words, &c->node_terms, &c->pref_terms, &c->spreads,
-                    &c->pod_terms, &c->scalars, &c->ports, &c->results, &c->gran, &c->trace})
+                    &c->pod_terms, &c->scalars, &c->ports, &c->results, &c->gran, &c->trace, &c->d_classes,
+                    &c->d_citems, &c->d_tclasses, &c->d_creqs, &c->d_cints, &c->d_plans, &c->d_aux,
+                    &c->d_aux_terms, &c->scratch, &c->d_pods})
     if (b->p) (void)hipFree(b->p);
+  if (c->st.mcnt) (void)hipFree(c->st.mcnt);
+  if (c->st.tcnt) (void)hipFree(c->st.tcnt);
   for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -544,6 +1037,65 @@ int kgpu_upload_snapshot(kgpu_ctx* c, const kgpu_snapshot* s, int64_t generation
   if ((rc = dalloc(c, W, &st.diag_raw, (size_t)KGPU_NUM_SCORES * N))) return rc;
   if ((rc = dalloc(c, W, &st.diag_norm, (size_t)KGPU_NUM_SCORES * N))) return rc;
   HIP_OK(c, hipMemset(st.status, 0, sizeof(uint32_t) * std::max<size_t>(N, 1)));
+  if ((rc = dalloc(c, W, &st.raw_pts, N))) return rc;
+  if ((rc = dalloc(c, W, &st.raw_ipa, N))) return rc;
+  if ((rc = dalloc(c, W, &st.raw_dpts, N))) return rc;
+  st.key_empty = st.key_empty_value;
+  st.hard_pod_affinity_weight = c->cfg.hard_pod_affinity_weight;
+  {
+    // math.Log(x) for x = 0 .. n_total + 2 (PodTopologySpread weights, scoring.go:286-288)
+    std::vector<double> lt((size_t)st.n_total + 3);
+    for (size_t x = 0; x < lt.size(); ++x) lt[x] = go_log((double)x);
+    if ((rc = dcopy(c, R, &st.log_table, lt.data(), lt.size()))) return rc;
+  }
+  // topology state: host copies of the key metadata, the pod table, existing pods' term classes
+  c->key_n_values.assign(s->key_n_values ? s->key_n_values : nullptr, s->key_n_values ? s->key_n_values + st.K : nullptr);
+  c->key_empty.assign(s->key_empty_value ? s->key_empty_value : nullptr,
+                      s->key_empty_value ? s->key_empty_value + st.K : nullptr);
+  c->class_ids.clear();
+  c->tclass_ids.clear();
+  c->classes.clear();
+  c->citems.clear();
+  c->tclasses.clear();
+  c->creqs.clear();
+  c->cints.clear();
+  c->classes_init = 0;
+  c->pod_rows.clear();
+  c->pod_rows_dev = -1;
+  for (int i = 0; i < s->n_pods; ++i) {
+    kgpu_ctx::PodRow row;
+    row.node = s->pod_node[i];
+    row.ns = s->pod_ns[i];
+    row.flags = s->pod_flags[i];
+    for (int k = 0; k < s->n_pod_label_keys; ++k) {
+      const int32_t v = s->pod_label_val[(size_t)k * s->n_pods + i];
+      if (v >= 0) {
+        row.pairs.push_back(k);
+        row.pairs.push_back(v);
+      }
+    }
+    c->pod_rows.push_back(std::move(row));
+  }
+  if (c->st.mcnt) (void)hipFree(c->st.mcnt);
+  if (c->st.tcnt) (void)hipFree(c->st.tcnt);
+  st.mcnt = nullptr;
+  st.tcnt = nullptr;
+  c->Ccap = c->TCcap = 0;
+  std::vector<std::pair<int, int>> term_cells;  // (term class, local node)
+  for (int t = 0; t < s->n_terms; ++t) {
+    const kgpu_term& tm = s->terms[t];
+    const int tc = intern_tclass(c, tm.kind, tm.t.weight, tm.t.topo_key, term_item(tm.t, &s->pools));
+    if (tm.pod < 0 || tm.pod >= s->n_pods || !(s->pod_flags[tm.pod] & KGPU_PF_ACTIVE)) continue;
+    const int ln = s->pod_node[tm.pod] - st.node_base;
+    if (ln >= 0 && ln < st.N) term_cells.emplace_back(tc, ln);
+  }
+  if ((rc = grow_columns(c, &st.mcnt, &c->Ccap, 1))) return rc;
+  if ((rc = grow_columns(c, &st.tcnt, &c->TCcap, (int)c->tclasses.size()))) return rc;
+  if (!term_cells.empty()) {
+    std::vector<int32_t> tc_host((size_t)c->TCcap * N, 0);
+    for (auto& cell : term_cells) tc_host[(size_t)cell.first * N + cell.second] += 1;
+    HIP_OK(c, hipMemcpy(st.tcnt, tc_host.data(), sizeof(int32_t) * tc_host.size(), hipMemcpyHostToDevice));
+  }
   int anyp = 0;
   for (uint64_t w : c->prefer_union) anyp |= (w != 0);
   st.any_prefer_taint = anyp;
@@ -648,6 +1200,26 @@ int kgpu_forget_pod(kgpu_ctx* c, int32_t slot) {
       HIP_OK(c, hipMemcpy(c->st.ports + sl * N + n, &keep[sl], sizeof(kgpu_port), hipMemcpyHostToDevice));
     int32_t kc = (int32_t)keep.size();
     HIP_OK(c, hipMemcpy(c->st.port_count + n, &kc, 4, hipMemcpyHostToDevice));
+  }
+  // topology state: the pod leaves the match-count columns of its classes and term classes
+  const size_t slot_row = (size_t)c->n_snapshot_pods + (size_t)i;
+  if (slot_row < c->pod_rows.size() && c->st.mcnt) {
+    kgpu_ctx::PodRow& row = c->pod_rows[slot_row];
+    auto dec32 = [&](int32_t* col) -> int {
+      int32_t v;
+      HIP_OK(c, hipMemcpy(&v, col + n, 4, hipMemcpyDeviceToHost));
+      v -= 1;
+      HIP_OK(c, hipMemcpy(col + n, &v, 4, hipMemcpyHostToDevice));
+      return KGPU_OK;
+    };
+    const int np = (int)row.pairs.size() / 2;
+    for (int cl = 0; cl < c->classes_init; ++cl)
+      if (class_matches(c, cl, row.ns, row.flags, row.pairs.data(), np) && (rc = dec32(c->st.mcnt + (size_t)cl * N)))
+        return rc;
+    for (int32_t tc : row.own_tcls)
+      if ((rc = dec32(c->st.tcnt + (size_t)tc * N))) return rc;
+    row.flags &= ~KGPU_PF_ACTIVE;
+    c->pod_rows_dev = -1;
   }
   a.active = false;
   return KGPU_OK;

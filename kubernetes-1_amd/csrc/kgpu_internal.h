@@ -37,6 +37,82 @@ struct DevPools {
   const kgpu_port* ports;
 };
 
+// ---------------------------------------------------------------- topology plugins
+// PodTopologySpread / InterPodAffinity / DefaultPodTopologySpread run on device-resident
+// per-node match counts instead of re-walking every existing pod per incoming pod:
+//   mcnt[c][n]  = existing pods on node n matching pod class c (namespace set + label selector(s),
+//                 optionally excluding terminating pods) -- one class per distinct spread
+//                 selector / incoming pod term / DefaultPodTopologySpread selector;
+//   tcnt[t][n]  = existing pods on node n carrying term class t (kind, weight, topology key,
+//                 namespaces, selector) -- the existing pods' (anti-)affinity terms.
+// The host interns classes by content (kgpu_api.cpp), initializes new columns on the device from
+// the pod table (k_class_init), and every assume increments the columns of the classes the pod
+// matches and of the term classes it owns.  Per incoming pod the domain histograms
+// (topologyPair -> count) are rebuilt from these columns in one pass over the nodes.
+constexpr int kMaxSpread = 4;   // spread constraints per kind (DoNotSchedule / ScheduleAnyway)
+constexpr int kMaxIpa = 4;      // required (anti-)affinity terms per kind
+constexpr int kMaxPref = 8;     // preferred terms (affinity + anti-affinity)
+constexpr int kMaxSlots = 24;   // domain histograms per pod
+
+// A pod class item: pod in `ns` (int32 ids in the class pool) and matching `sel` (class pool reqs).
+struct ClassItem {
+  kgpu_range ns;
+  kgpu_selector sel;
+};
+struct ClassRec {
+  int32_t item0, n_items;  // ANDed items (podMatchesAllAffinityTerms uses several)
+  int32_t excl_terminating;
+  int32_t pad;
+};
+struct TermClassRec {
+  int32_t kind, weight, topo_key, pad;
+  ClassItem item;
+};
+
+struct TSpread {
+  int32_t cls, key, rslot, cslot;        // class, node label key, registration / count histogram slots
+  int32_t max_skew, self_match, is_hostname, first_of_key;
+};
+struct TTerm {
+  int32_t cls, key, slot, weight;        // class (or term class), node label key, histogram slot, weight
+};
+
+// Per-query plan built by the host at batch start (not part of the ABI).
+struct QPlan {
+  int32_t topo;              // 1: the pod takes the topology pipeline
+  int32_t n_hard, n_soft;
+  int32_t dpts_cls;          // -1: no DefaultPodTopologySpread counts (empty selector), -2: pod has TSC
+  TSpread hard[kMaxSpread];
+  TSpread soft[kMaxSpread];
+  int32_t n_aff, conj_cls, n_anti, n_pref;
+  int32_t self_all;          // podMatchesAllAffinityTerms(pod, RequiredAffinityTerms)
+  int32_t pad0;
+  TTerm aff[kMaxIpa];
+  TTerm anti[kMaxIpa];
+  TTerm pref[kMaxPref];
+  kgpu_range ex;             // TTerm aux pool: existing term classes matching this pod
+  int32_t n_ex_anti;         // the first n_ex_anti of ex are required anti-affinity (EXA slots)
+  int32_t n_slots;
+  kgpu_range assume_cls;     // int aux pool: classes this pod matches (mcnt increments on assume)
+  kgpu_range own_tcls;       // int aux pool: term classes this pod owns (tcnt increments on assume)
+  int32_t slot_key[kMaxSlots];
+  int32_t slot_kind[kMaxSlots];
+  int64_t slot_off[kMaxSlots];  // int64 offsets into the pod's scratch
+  int64_t scratch_len;       // int64 words (header + zone sums + slots)
+};
+enum SlotKind { kSlotPReg = 0, kSlotPCnt, kSlotSReg, kSlotSCnt, kSlotExA, kSlotAff, kSlotAnti, kSlotTopo };
+
+// Scratch header of one topology pod (zeroed before its first kernel).
+struct TopoHdr {
+  int64_t pmin[kMaxSpread];   // critical-path minimum per hard constraint
+  int64_t ssize[kMaxSpread];  // topology size per soft constraint (first constraint of its key)
+  int64_t pts_min, pts_max, ipa_min, ipa_max, dpts_max;
+  int32_t pany, aff_any, ex_any, topo_any;
+  int32_t feas_nonign, have_zones, done1, done2;
+  int32_t pmin_set, pad[3];
+};
+constexpr int kHdrWords = (int)(sizeof(TopoHdr) / 8);
+
 // Everything a kernel needs, passed by value (well under the 4 KiB kernel-argument limit).
 struct DevState {
   // ---- geometry
@@ -93,6 +169,31 @@ struct DevState {
   kgpu_result* results;                 // [batch capacity]
   int64_t* diag_raw;                    // [KGPU_NUM_SCORES][N] or null
   int64_t* diag_norm;                   // [KGPU_NUM_SCORES][N] or null
+  // ---- topology plugins
+  const QPlan* plans;                   // [batch] per-query plans (null: no topology state)
+  const int32_t* aux;                   // int aux pool of the plans
+  const TTerm* aux_terms;               // TTerm aux pool of the plans
+  int32_t* mcnt;                        // [Ccap][N]
+  int32_t* tcnt;                        // [TCcap][N]
+  const ClassRec* classes;
+  const ClassItem* class_items;
+  const TermClassRec* tclasses;
+  const kgpu_req* creqs;                // class pool
+  const int32_t* cints;
+  int32_t* key_empty;                   // == key_empty_value
+  double* log_table;                    // [n_total + 3] math.Log(x) for x = 0..n_total+2
+  int64_t* scratch;                     // per-pod topology scratch
+  int64_t* raw_pts;                     // [N] (INT64_MIN = ignored node)
+  int64_t* raw_ipa;                     // [N]
+  int64_t* raw_dpts;                    // [N]
+  int32_t hard_pod_affinity_weight;
+  int32_t pad2;
+  // pod table (existing + assumed pods) for class initialization
+  int32_t* pod_node;                    // [Pcap] global node index
+  int32_t* pod_ns;
+  uint32_t* pod_flags;
+  int32_t* pod_lab;                     // [PKcap][Pcap]
+  int32_t Pcap, PKcap;
 };
 
 // Per-launch parameters.
@@ -136,5 +237,12 @@ int eval_blocks(int N);
 // does not fit in max_groups workgroups.
 int batch_geometry(int N, int max_groups, int* per, int* groups);
 int launch_batch(const DevState* st, const BatchArgs& a, int groups, int kidx, int spec, void* stream);
+// Topology pipeline for one pod (PodArgs.pod): domain histograms, critical-path minima, filters,
+// scores, normalize + argmax, resolve + assume.  next_scratch: words of the next topology pod's
+// scratch to zero in the resolve launch (0 none).
+int launch_topo(const DevState* st, const PodArgs& a, int blocks, int64_t min_values, int64_t next_scratch,
+                void* stream);
+// Initialize mcnt columns [c0, c0 + nc) from the pod table (n_pods rows).
+int launch_class_init(const DevState* st, int c0, int nc, int n_pods, void* stream);
 
 }  // namespace kgpu

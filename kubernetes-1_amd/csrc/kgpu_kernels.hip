@@ -384,9 +384,11 @@ struct NodeEval {
   int32_t na;       // raw NodeAffinity score
 };
 
+__device__ uint32_t topo_filter(int f, const DevState& st, const QPlan& pl, int n);
+
 // One Filter plugin: 0 = Success, else (code << 8) | (detail << 16) of the status word.
 __device__ __forceinline__ uint32_t filter_one(int f, const DevState& st, const kgpu_pod_query& q, const NodeRes& r,
-                                               int n) {
+                                               int n, const QPlan* pl = nullptr) {
   switch (f) {
     case KGPU_F_NODE_UNSCHEDULABLE:
       if (gp(st.unsched)[n] && !(q.flags & KGPU_Q_TOLERATES_UNSCHEDULABLE)) return KGPU_CODE_UNRESOLVABLE << 8;
@@ -403,17 +405,18 @@ __device__ __forceinline__ uint32_t filter_one(int f, const DevState& st, const 
       return node_affinity_ok(st, q, n) ? 0 : KGPU_CODE_UNRESOLVABLE << 8;
     case KGPU_F_TAINT_TOLERATION:
       return taints_ok(st, q, n) ? 0 : KGPU_CODE_UNRESOLVABLE << 8;
-    default:  // PodTopologySpread / InterPodAffinity: pass for pods without constraints
-      return 0;
+    default:  // PodTopologySpread / InterPodAffinity: pass for pods outside the topology pipeline
+      return pl ? topo_filter(f, st, *pl, n) : 0;
   }
 }
 
 // Filters in profile order; the first failure's 1-based position goes in the low byte.
 template <uint32_t FM, int F = 0>
-__device__ __forceinline__ uint32_t run_filters(const DevState& st, const kgpu_pod_query& q, const NodeRes& r, int n) {
+__device__ __forceinline__ uint32_t run_filters(const DevState& st, const kgpu_pod_query& q, const NodeRes& r, int n,
+                                                const QPlan* pl = nullptr) {
   if constexpr (FM == kRuntime) {
     for (int i = 0; i < st.n_filters; ++i) {
-      const uint32_t c = filter_one(cp(st.filters)[i], st, q, r, n);
+      const uint32_t c = filter_one(cp(st.filters)[i], st, q, r, n, pl);
       if (c) return c | (uint32_t)(i + 1);
     }
     return 0;
@@ -595,6 +598,16 @@ __device__ void assume_row(const DevState& st, const kgpu_pod_query& q, NodeRes&
   }
 }
 
+// The assumed pod's side of the topology state: the match-count columns of the pod classes it
+// matches and of the term classes it carries (NodeInfo.AddPod -> Pods / PodsWithAffinity).
+__device__ __forceinline__ void assume_counts(const DevState& st, int pod, int n) {
+  if (!st.plans) return;
+  const QPlan* pl = st.plans + pod;
+  const kgpu_range ac = pl->assume_cls, ot = pl->own_tcls;
+  for (int i = 0; i < ac.count; ++i) gp(st.mcnt)[(size_t)st.aux[ac.begin + i] * st.N + n] += 1;
+  for (int i = 0; i < ot.count; ++i) gp(st.tcnt)[(size_t)st.aux[ot.begin + i] * st.N + n] += 1;
+}
+
 // The pending pod's outcome (generic_scheduler.go:171-208): FitError, the len==1 shortcut, or
 // the scored winner.  Returns the local row to assume (-1 none).
 __device__ __forceinline__ int settle_prev(const DevState& st, const PodArgs& a, const kgpu_pod_query& pq,
@@ -646,7 +659,10 @@ __global__ __launch_bounds__(kBlock) void k_eval(const DevState* __restrict__ st
   int best_i = -1, feas = 0, maxT = 0, maxNA = 0;
   for (int n = n0; n < hi; n += kBlock) {
     NodeRes r = (n == n0) ? r0 : load_res(st, n);
-    if (n == assume_idx) assume_row(st, *cp(pq), r, n);
+    if (n == assume_idx) {
+      assume_row(st, *cp(pq), r, n);
+      assume_counts(st, a.prev, n);
+    }
     NodeEval e{0, 0, 0, 0};
     e.status = run_filters<FM>(st, q, r, n);
     if (e.status == 0) {
@@ -730,6 +746,7 @@ __global__ __launch_bounds__(kBlock) void k_resolve(const DevState* __restrict__
   if (idx >= lo && idx < hi && ((idx - lo) % kBlock) == (int)threadIdx.x) {
     NodeRes r = load_res(st, idx);
     assume_row(st, pq, r, idx);
+    assume_counts(st, a.prev, idx);
   }
 }
 
@@ -1023,7 +1040,10 @@ __global__ __launch_bounds__(B) void k_batch(const DevState* __restrict__ stp, B
         if (pa.assume && tid == ob) {
 #pragma unroll
           for (int j = 0; j < K; ++j)
-            if (j == jb) assume_row(st, qp, r[j], lo + cand);
+            if (j == jb) {
+              assume_row(st, qp, r[j], lo + cand);
+              assume_counts(st, pa.first + i - 1, lo + cand);
+            }
         }
         if (!fast_b && have_cur) {
           // the winner's row changed in memory-resident columns: evaluate it again, republish
@@ -1071,6 +1091,497 @@ __global__ void k_batch_fixup(const DevState* __restrict__ stp, BatchArgs pa, in
     r.scored = 0;
     r.score = 0;
   }
+}
+
+// ---------------------------------------------------------------- topology pipeline
+// PodTopologySpread (podtopologyspread/{filtering,scoring}.go), InterPodAffinity
+// (interpodaffinity/{filtering,scoring}.go) and DefaultPodTopologySpread
+// (default_pod_topology_spread.go) for one pod, as a chain of launches over the eval grid:
+//   k_topo_pre      one pass over the nodes: topologyPair -> count histograms built from the
+//                   match-count columns (the PreFilter maps and the PreScore counts), global
+//                   atomics into the pod's scratch
+//   k_topo_min      criticalPaths minimum per DoNotSchedule constraint (filtering.go:93-121)
+//   k_topo_filter   every Filter plugin in profile order (PTS / IPA read the histograms), the
+//                   non-topology scores, ScheduleAnyway pair registration (scoring.go:83-102)
+//   k_topo_score    PTS / IPA / DPTS raw scores of the feasible nodes, their min / max / zone sums
+//   k_topo_final    NormalizeScore of every plugin, weights, packed-key argmax per workgroup
+//   k_topo_resolve  selectHost over the partials, assume (node row + match counts), zero the next
+//                   pod's scratch
+__device__ __forceinline__ int nval(const DevState& st, int k, int n) {
+  return k >= 0 ? gp(st.label_val)[(size_t)k * st.N + n] : -1;
+}
+__device__ __forceinline__ int64_t* slot_ptr(const DevState& st, const QPlan& pl, int slot) {
+  return st.scratch + pl.slot_off[slot];
+}
+__device__ __forceinline__ TopoHdr* hdr(const DevState& st) { return reinterpret_cast<TopoHdr*>(st.scratch); }
+__device__ __forceinline__ int64_t* zone_sums(const DevState& st) { return st.scratch + kHdrWords; }
+__device__ __forceinline__ void add64(int64_t* p, int64_t v) {
+  atomicAdd(reinterpret_cast<unsigned long long*>(p), (unsigned long long)v);
+}
+// order-preserving encodings for atomicMax on zero-initialized words
+__device__ __forceinline__ unsigned long long enc_max(int64_t x) { return (unsigned long long)x ^ (1ull << 63); }
+__device__ __forceinline__ void amax64(int64_t* p, int64_t x) {
+  atomicMax(reinterpret_cast<unsigned long long*>(p), enc_max(x));
+}
+__device__ __forceinline__ void amin64(int64_t* p, int64_t x) {
+  atomicMax(reinterpret_cast<unsigned long long*>(p), ~enc_max(x));
+}
+__device__ __forceinline__ int64_t read_max(const int64_t* p) {  // INT64_MIN when never set
+  const unsigned long long u = *reinterpret_cast<const unsigned long long*>(p);
+  return u ? (int64_t)(u ^ (1ull << 63)) : INT64_MIN;
+}
+__device__ __forceinline__ int64_t read_min(const int64_t* p) {  // INT64_MAX when never set
+  const unsigned long long u = *reinterpret_cast<const unsigned long long*>(p);
+  return u ? (int64_t)(~u ^ (1ull << 63)) : INT64_MAX;
+}
+
+__device__ __forceinline__ bool all_keys(const DevState& st, const TSpread* c, int nc, int n) {
+  for (int i = 0; i < nc; ++i)
+    if (nval(st, c[i].key, n) < 0) return false;
+  return true;
+}
+
+// PodTopologySpread / InterPodAffinity Filter on the histograms of k_topo_pre / k_topo_min.
+__device__ uint32_t topo_filter(int f, const DevState& st, const QPlan& pl, int n) {
+  const TopoHdr* h = hdr(st);
+  if (f == KGPU_F_POD_TOPOLOGY_SPREAD) {  // filtering.go:276-328
+    if (pl.n_hard == 0 || !h->pany) return 0;
+    for (int i = 0; i < pl.n_hard; ++i) {
+      const TSpread& c = pl.hard[i];
+      const int v = nval(st, c.key, n);
+      if (v < 0) return KGPU_CODE_UNSCHEDULABLE << 8;
+      const int64_t match = slot_ptr(st, pl, c.rslot)[v] ? slot_ptr(st, pl, c.cslot)[v] : 0;
+      int64_t mn = read_min(&h->pmin[i]);
+      if (mn == INT64_MAX) mn = 2147483647;  // criticalPaths initial MatchNum (math.MaxInt32)
+      if (match + c.self_match - mn > c.max_skew) return KGPU_CODE_UNSCHEDULABLE << 8;
+    }
+    return 0;
+  }
+  if (f == KGPU_F_INTER_POD_AFFINITY) {  // filtering.go:314-396
+    bool exist = true;
+    for (int i = 0; i < pl.n_aff; ++i) {  // satisfyPodAffinity
+      const int v = nval(st, pl.aff[i].key, n);
+      if (v < 0) return (KGPU_CODE_UNRESOLVABLE << 8) | (1u << 16);
+      if (slot_ptr(st, pl, pl.aff[i].slot)[v] <= 0) exist = false;
+    }
+    if (!exist && !(!h->aff_any && pl.self_all)) return (KGPU_CODE_UNRESOLVABLE << 8) | (1u << 16);
+    for (int i = 0; i < pl.n_anti; ++i) {  // satisfyPodAntiAffinity
+      const int v = nval(st, pl.anti[i].key, n);
+      if (v >= 0 && slot_ptr(st, pl, pl.anti[i].slot)[v] > 0) return (KGPU_CODE_UNSCHEDULABLE << 8) | (2u << 16);
+    }
+    if (h->ex_any) {  // satisfyExistingPodsAntiAffinity: every node label pair
+      for (int s = 0; s < pl.n_slots; ++s) {
+        if (pl.slot_kind[s] != kSlotExA) continue;
+        const int v = nval(st, pl.slot_key[s], n);
+        if (v >= 0 && slot_ptr(st, pl, s)[v] > 0) return (KGPU_CODE_UNSCHEDULABLE << 8) | (3u << 16);
+      }
+    }
+    return 0;
+  }
+  return 0;
+}
+
+__global__ __launch_bounds__(kBlock) void k_topo_pre(const DevState* __restrict__ stp, PodArgs a) {
+  const DevState& st = *stp;
+  const QPlan& pl = st.plans[a.pod];
+  const kgpu_pod_query q = *cp(st.queries + a.pod);
+  TopoHdr* h = hdr(st);
+  int lo, hi;
+  chunk_of(st.N, lo, hi);
+  bool pany = false, ex_any = false, aff_any = false;
+  for (int n = lo + threadIdx.x; n < hi; n += kBlock) {
+    const bool aff_ok = (pl.n_hard || pl.n_soft) ? node_affinity_ok(st, q, n) : false;
+    // PreFilter TpPairToMatchNum (filtering.go:198-273): eligible pairs, then counts over all nodes
+    if (pl.n_hard) {
+      if (aff_ok && all_keys(st, pl.hard, pl.n_hard, n)) {
+        for (int i = 0; i < pl.n_hard; ++i) slot_ptr(st, pl, pl.hard[i].rslot)[nval(st, pl.hard[i].key, n)] = 1;
+        pany = true;
+      }
+      for (int i = 0; i < pl.n_hard; ++i) {
+        const TSpread& c = pl.hard[i];
+        if (c.key < 0) continue;
+        int v = nval(st, c.key, n);
+        if (v < 0) v = gp(st.key_empty)[c.key];  // node.Labels[key] of a missing key is ""
+        const int cnt = gp(st.mcnt)[(size_t)c.cls * st.N + n];
+        if (v >= 0 && cnt) add64(slot_ptr(st, pl, c.cslot) + v, cnt);
+      }
+    }
+    // PreScore counts (scoring.go:145-167): nodes matching affinity and carrying every key
+    if (pl.n_soft && aff_ok && all_keys(st, pl.soft, pl.n_soft, n)) {
+      for (int i = 0; i < pl.n_soft; ++i) {
+        const TSpread& c = pl.soft[i];
+        if (c.is_hostname) continue;
+        const int cnt = gp(st.mcnt)[(size_t)c.cls * st.N + n];
+        if (cnt) add64(slot_ptr(st, pl, c.cslot) + nval(st, c.key, n), cnt);
+      }
+    }
+    // InterPodAffinity PreFilter maps (filtering.go:166-271) and PreScore topologyScore (scoring.go:47-199)
+    for (int j = 0; j < pl.ex.count; ++j) {
+      const TTerm t = st.aux_terms[pl.ex.begin + j];
+      const int v = nval(st, t.key, n);
+      if (v < 0) continue;
+      const int cnt = gp(st.tcnt)[(size_t)t.cls * st.N + n];
+      if (!cnt) continue;
+      if (j < pl.n_ex_anti) {
+        add64(slot_ptr(st, pl, t.slot) + v, cnt);
+        ex_any = true;
+      } else {
+        add64(slot_ptr(st, pl, t.slot) + v, (int64_t)t.weight * cnt);
+      }
+    }
+    if (pl.n_aff) {
+      const int cnt = gp(st.mcnt)[(size_t)pl.conj_cls * st.N + n];
+      if (cnt) {
+        for (int i = 0; i < pl.n_aff; ++i) {
+          const int v = nval(st, pl.aff[i].key, n);
+          if (v < 0) continue;
+          add64(slot_ptr(st, pl, pl.aff[i].slot) + v, cnt);
+          aff_any = true;
+        }
+      }
+    }
+    for (int i = 0; i < pl.n_anti; ++i) {
+      const int v = nval(st, pl.anti[i].key, n);
+      const int cnt = gp(st.mcnt)[(size_t)pl.anti[i].cls * st.N + n];
+      if (v >= 0 && cnt) add64(slot_ptr(st, pl, pl.anti[i].slot) + v, cnt);
+    }
+    for (int i = 0; i < pl.n_pref; ++i) {
+      const int v = nval(st, pl.pref[i].key, n);
+      const int cnt = gp(st.mcnt)[(size_t)pl.pref[i].cls * st.N + n];
+      if (v >= 0 && cnt) add64(slot_ptr(st, pl, pl.pref[i].slot) + v, (int64_t)pl.pref[i].weight * cnt);
+    }
+  }
+  if (__any(pany) && threadIdx.x == 0) h->pany = 1;
+  if (__any(ex_any) && threadIdx.x == 0) h->ex_any = 1;
+  if (__any(aff_any) && threadIdx.x == 0) h->aff_any = 1;
+}
+
+// criticalPaths[0].MatchNum per DoNotSchedule constraint: minimum count over the registered pairs
+// of its key (MaxInt32 when none), grid-stride over the key's values.
+__global__ __launch_bounds__(kBlock) void k_topo_min(const DevState* __restrict__ stp, PodArgs a) {
+  const DevState& st = *stp;
+  const QPlan& pl = st.plans[a.pod];
+  TopoHdr* h = hdr(st);
+  for (int i = 0; i < pl.n_hard; ++i) {
+    const TSpread& c = pl.hard[i];
+    const int nv = c.key >= 0 ? gp(st.key_n_values)[c.key] : 0;
+    int64_t mn = INT64_MAX;
+    const int64_t* reg = slot_ptr(st, pl, c.rslot);
+    const int64_t* cnt = slot_ptr(st, pl, c.cslot);
+    for (int v = blockIdx.x * kBlock + threadIdx.x; v < nv; v += gridDim.x * kBlock)
+      if (reg[v] && cnt[v] < mn) mn = cnt[v];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) mn = min(mn, (int64_t)__shfl_xor(mn, off));
+    if (threadIdx.x == 0 && mn != INT64_MAX) amin64(&h->pmin[i], mn);
+  }
+}
+
+// Filters + the non-topology scores; the feasible set's ScheduleAnyway pairs and sizes.
+__global__ __launch_bounds__(kBlock) void k_topo_filter(const DevState* __restrict__ stp, PodArgs a) {
+  const DevState& st = *stp;
+  const QPlan& pl = st.plans[a.pod];
+  const kgpu_pod_query q = *cp(st.queries + a.pod);
+  TopoHdr* h = hdr(st);
+  QPlan const* plp = &pl;
+  int lo, hi;
+  chunk_of(st.N, lo, hi);
+  int feas = 0, maxT = 0, maxNA = 0, nonign = 0;
+  for (int n = lo + threadIdx.x; n < hi; n += kBlock) {
+    NodeRes r = load_res(st, n);
+    NodeEval e{0, 0, 0, 0};
+    e.status = run_filters<kRuntime>(st, q, r, n, plp);
+    if (e.status == 0) {
+      int64_t part = 0;
+      for (int i = 0; i < st.n_scores; ++i) {
+        const int s = cp(st.scores)[i];
+        if (s == KGPU_S_POD_TOPOLOGY_SPREAD || s == KGPU_S_INTER_POD_AFFINITY ||
+            s == KGPU_S_DEFAULT_POD_TOPOLOGY_SPREAD)
+          continue;  // k_topo_score / k_topo_final
+        const int64_t v = score_one<false>(s, st, q, r, n, e);
+        if (a.diag) gp(st.diag_raw)[(size_t)s * st.N + n] = v;
+        if (!normalized(s)) part += v * cp(st.w_of)[s];
+      }
+      e.partial = part;
+      ++feas;
+      maxT = max(maxT, e.taint);
+      maxNA = max(maxNA, e.na);
+      // PTS PreScore over the filtered nodes (scoring.go:83-102): pairs, sizes, ignored nodes
+      if (pl.n_soft && all_keys(st, pl.soft, pl.n_soft, n)) {
+        ++nonign;
+        for (int i = 0; i < pl.n_soft; ++i) {
+          const TSpread& c = pl.soft[i];
+          if (c.is_hostname) continue;
+          int64_t* reg = slot_ptr(st, pl, c.rslot) + nval(st, c.key, n);
+          const unsigned long long old = atomicExch(reinterpret_cast<unsigned long long*>(reg), 1ull);
+          if (old == 0 && c.first_of_key) add64(&h->ssize[i], 1);
+        }
+      }
+    }
+    gp(st.status)[n] = e.status;
+    gp(st.partial)[n] = e.partial;
+    gp(st.raw_taint)[n] = e.taint;
+    gp(st.raw_na)[n] = e.na;
+  }
+  feas = wave_reduce_sum(feas);
+  maxT = wave_reduce_max(maxT);
+  maxNA = wave_reduce_max(maxNA);
+  nonign = wave_reduce_sum(nonign);
+  if (threadIdx.x == 0) {
+    gp(st.sbuf)[(size_t)a.parity * kMaxBlocks + blockIdx.x] = BlkStat{feas, maxT, maxNA, 0};
+    if (nonign) atomicAdd(&h->feas_nonign, nonign);
+  }
+}
+
+// Raw PodTopologySpread (scoring.go:174-208), InterPodAffinity (scoring.go:217-236) and
+// DefaultPodTopologySpread (default_pod_topology_spread.go:75-106) scores of the feasible nodes.
+__global__ __launch_bounds__(kBlock) void k_topo_score(const DevState* __restrict__ stp, PodArgs a) {
+  const DevState& st = *stp;
+  const QPlan& pl = st.plans[a.pod];
+  TopoHdr* h = hdr(st);
+  int lo, hi;
+  chunk_of(st.N, lo, hi);
+  double w[kMaxSpread];
+  for (int i = 0; i < pl.n_soft; ++i) {  // topologyNormalizingWeight (scoring.go:286-288)
+    const int64_t sz = pl.soft[i].is_hostname ? (int64_t)h->feas_nonign : (pl.soft[i].first_of_key ? h->ssize[i] : 0);
+    w[i] = st.log_table[sz + 2];
+  }
+  int64_t pmn = INT64_MAX, pmx = INT64_MIN, imn = INT64_MAX, imx = INT64_MIN, dmx = 0;
+  bool zoned = false;
+  for (int n = lo + threadIdx.x; n < hi; n += kBlock) {
+    if (gp(st.status)[n] != 0) continue;
+    // PodTopologySpread
+    int64_t ps = 0;
+    if (pl.n_soft && !all_keys(st, pl.soft, pl.n_soft, n)) {
+      ps = INT64_MIN;  // ignored node
+    } else {
+      double score = 0;
+      for (int i = 0; i < pl.n_soft; ++i) {
+        const TSpread& c = pl.soft[i];
+        const int v = nval(st, c.key, n);
+        int64_t cnt = c.is_hostname ? (int64_t)gp(st.mcnt)[(size_t)c.cls * st.N + n] : slot_ptr(st, pl, c.cslot)[v];
+        if (cnt < c.max_skew) cnt = c.max_skew - 1;  // adjustForMaxSkew
+        score += (double)cnt * w[i];
+      }
+      ps = (int64_t)score;
+      pmn = min(pmn, ps);
+      pmx = max(pmx, ps);
+    }
+    // InterPodAffinity: sum over the topologyScore keys the node carries
+    int64_t is = 0;
+    for (int s = 0; s < pl.n_slots; ++s) {
+      if (pl.slot_kind[s] != kSlotTopo) continue;
+      const int v = nval(st, pl.slot_key[s], n);
+      if (v >= 0) is += slot_ptr(st, pl, s)[v];
+    }
+    imn = min(imn, is);
+    imx = max(imx, is);
+    // DefaultPodTopologySpread
+    int64_t ds = 0;
+    if (pl.dpts_cls >= 0) ds = gp(st.mcnt)[(size_t)pl.dpts_cls * st.N + n];
+    dmx = max(dmx, ds);
+    const int z = gp(st.zone_id)[n];
+    if (z >= 0) {
+      zoned = true;
+      if (ds) add64(zone_sums(st) + z, ds);
+    }
+    gp(st.raw_pts)[n] = ps;
+    gp(st.raw_ipa)[n] = is;
+    gp(st.raw_dpts)[n] = ds;
+    if (a.diag) {
+      gp(st.diag_raw)[(size_t)KGPU_S_POD_TOPOLOGY_SPREAD * st.N + n] = ps == INT64_MIN ? 0 : ps;
+      gp(st.diag_raw)[(size_t)KGPU_S_INTER_POD_AFFINITY * st.N + n] = is;
+      gp(st.diag_raw)[(size_t)KGPU_S_DEFAULT_POD_TOPOLOGY_SPREAD * st.N + n] = pl.dpts_cls == -2 ? 0 : ds;
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    pmn = min(pmn, (int64_t)__shfl_xor(pmn, off));
+    pmx = max(pmx, (int64_t)__shfl_xor(pmx, off));
+    imn = min(imn, (int64_t)__shfl_xor(imn, off));
+    imx = max(imx, (int64_t)__shfl_xor(imx, off));
+    dmx = max(dmx, (int64_t)__shfl_xor(dmx, off));
+  }
+  const bool zw = __any(zoned);
+  if (threadIdx.x == 0) {
+    if (pmx != INT64_MIN) {
+      amin64(&h->pts_min, pmn);
+      amax64(&h->pts_max, pmx);
+    }
+    if (imx != INT64_MIN) {
+      amin64(&h->ipa_min, imn);
+      amax64(&h->ipa_max, imx);
+    }
+    if (dmx) amax64(&h->dpts_max, dmx);
+    if (zw) h->have_zones = 1;
+  }
+}
+
+// NormalizeScore of every plugin (framework.go:613-648), total, packed-key argmax per workgroup.
+__global__ __launch_bounds__(kBlock) void k_topo_final(const DevState* __restrict__ stp, PodArgs a, int stat_blocks) {
+  const DevState& st = *stp;
+  const QPlan& pl = st.plans[a.pod];
+  const TopoHdr* h = hdr(st);
+  int maxT = 0, maxNA = 0;
+  const GAS BlkStat* sb = gp(st.sbuf) + (size_t)a.parity * kMaxBlocks;
+  for (int b = threadIdx.x; b < stat_blocks; b += kBlock) {
+    const BlkStat p = sb[b];
+    maxT = max(maxT, p.max_taint);
+    maxNA = max(maxNA, p.max_na);
+  }
+  maxT = wave_reduce_max(maxT);
+  maxNA = wave_reduce_max(maxNA);
+  // PTS (scoring.go:211-257): min / max over the non-ignored nodes
+  const int64_t pmx0 = read_max(&h->pts_max), pmn0 = read_min(&h->pts_min);
+  const int64_t pmx = pmx0 == INT64_MIN ? 0 : max(pmx0, (int64_t)0);
+  const int64_t pmn = pmn0;
+  // IPA (scoring.go:241-272): min and max start at 0
+  const int64_t imx = max(read_max(&h->ipa_max), (int64_t)0), imn = min(read_min(&h->ipa_min), (int64_t)0);
+  const int64_t idiff = imx - imn;
+  // DPTS (default_pod_topology_spread.go:109-163)
+  const int64_t dmax_node = max(read_max(&h->dpts_max), (int64_t)0);
+  int64_t dmax_zone = 0;
+  if (pl.dpts_cls >= 0 && h->have_zones)
+    for (int z = threadIdx.x; z < st.n_zones; z += kBlock) dmax_zone = max(dmax_zone, zone_sums(st)[z]);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) dmax_zone = max(dmax_zone, (int64_t)__shfl_xor(dmax_zone, off));
+  const double M = 100.0, zwt = 2.0 / 3.0;
+  int lo, hi;
+  chunk_of(st.N, lo, hi);
+  const uint64_t tk = pod_tie_key(st.seed, a.seq);
+  uint64_t best = 0;
+  int best_i = -1, bf = 0;
+  for (int n = lo + threadIdx.x; n < hi; n += kBlock) {
+    if (gp(st.status)[n] != 0) continue;
+    ++bf;
+    const int taint = gp(st.raw_taint)[n], na = gp(st.raw_na)[n];
+    const int64_t vt = maxT == 0 ? 100 : 100 - (100 * (int64_t)taint) / maxT;
+    const int64_t vn = maxNA == 0 ? (int64_t)na : (100 * (int64_t)na) / maxNA;
+    const int64_t ps = gp(st.raw_pts)[n];
+    int64_t vp;
+    if (ps == INT64_MIN) vp = 0;
+    else if (pmx == 0) vp = 100;
+    else vp = 100 * (pmx + pmn - ps) / pmx;
+    const int64_t is = gp(st.raw_ipa)[n];
+    const int64_t vi = idiff > 0 ? (int64_t)(M * ((double)(is - imn) / (double)idiff)) : 0;
+    int64_t vd = 0;
+    if (pl.dpts_cls != -2) {
+      const int64_t ds = gp(st.raw_dpts)[n];
+      double f = M;
+      if (dmax_node > 0) f = M * ((double)(dmax_node - ds) / (double)dmax_node);
+      const int z = gp(st.zone_id)[n];
+      if (h->have_zones && z >= 0) {
+        double zs = M;
+        if (dmax_zone > 0) zs = M * ((double)(dmax_zone - zone_sums(st)[z]) / (double)dmax_zone);
+        f = (f * (1.0 - zwt)) + (zwt * zs);
+      }
+      vd = (int64_t)f;
+    }
+    int64_t total = gp(st.partial)[n] + vt * st.w_of[KGPU_S_TAINT_TOLERATION] + vn * st.w_of[KGPU_S_NODE_AFFINITY] +
+                    vp * st.w_of[KGPU_S_POD_TOPOLOGY_SPREAD] + vi * st.w_of[KGPU_S_INTER_POD_AFFINITY] +
+                    vd * st.w_of[KGPU_S_DEFAULT_POD_TOPOLOGY_SPREAD];
+    if (st.n_scores == 0) total = 1;
+    const uint64_t key = ((uint64_t)total << 40) | rank40(tk, (uint64_t)(st.node_base + n), st.tie_mode);
+    key_max(best, best_i, key, n);
+    if (a.diag) {
+      for (int i = 0; i < st.n_scores; ++i) {
+        const int s = st.scores[i];
+        int64_t v = gp(st.diag_raw)[(size_t)s * st.N + n];
+        if (s == KGPU_S_TAINT_TOLERATION) v = vt;
+        if (s == KGPU_S_NODE_AFFINITY) v = vn;
+        if (s == KGPU_S_POD_TOPOLOGY_SPREAD) v = vp;
+        if (s == KGPU_S_INTER_POD_AFFINITY) v = vi;
+        if (s == KGPU_S_DEFAULT_POD_TOPOLOGY_SPREAD) v = vd;
+        gp(st.diag_norm)[(size_t)s * st.N + n] = v;
+      }
+    }
+  }
+  wave_reduce_key(best, best_i);
+  bf = wave_reduce_sum(bf);
+  if (threadIdx.x == 0) gp(st.kbuf)[(size_t)a.parity * kMaxBlocks + blockIdx.x] = BlkKey{best, best_i, bf};
+}
+
+// selectHost + assume of the topology pod, then zero the next topology pod's scratch.
+__global__ __launch_bounds__(kBlock) void k_topo_resolve(const DevState* __restrict__ stp, PodArgs a,
+                                                         int64_t next_scratch) {
+  const DevState& st = *stp;
+  int lo, hi;
+  chunk_of(st.N, lo, hi);
+  const Winner w = wave_winner(st.kbuf + (size_t)a.prev_parity * kMaxBlocks, a.prev_blocks);
+  const kgpu_pod_query pq = *cp(st.queries + a.prev);
+  const int idx = settle_prev(st, a, pq, w);
+  if (idx >= lo && idx < hi && ((idx - lo) % kBlock) == (int)threadIdx.x) {
+    NodeRes r = load_res(st, idx);
+    assume_row(st, pq, r, idx);
+    assume_counts(st, a.prev, idx);
+  }
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < next_scratch; i += (int64_t)gridDim.x * kBlock)
+    st.scratch[i] = 0;
+}
+
+// Pod class membership of the pod-table rows (labels.Selector.Matches, selector.go:198-242;
+// util/topologies.go:40-49), accumulated into fresh mcnt columns.
+__device__ bool pod_item_match(const DevState& st, const ClassItem& it, int p) {
+  const int ns = gp(st.pod_ns)[p];
+  bool in_ns = false;
+  for (int i = 0; i < it.ns.count; ++i) in_ns |= (st.cints[it.ns.begin + i] == ns);
+  if (!in_ns || it.sel.kind != KGPU_SEL_AND) return false;
+  for (int i = 0; i < it.sel.reqs.count; ++i) {
+    const kgpu_req rq = st.creqs[it.sel.reqs.begin + i];
+    const int v = (rq.key >= 0 && rq.key < st.PKcap) ? gp(st.pod_lab)[(size_t)rq.key * st.Pcap + p] : -1;
+    bool in = false;
+    for (int j = 0; j < rq.vals.count; ++j) in |= (st.cints[rq.vals.begin + j] == v);
+    switch (rq.op) {
+      case KGPU_OP_IN: if (!(v >= 0 && in)) return false; break;
+      case KGPU_OP_NOTIN: if (v >= 0 && in) return false; break;
+      case KGPU_OP_EXISTS: if (v < 0) return false; break;
+      case KGPU_OP_DNE: if (v >= 0) return false; break;
+      default: return false;
+    }
+  }
+  return true;
+}
+
+__global__ void k_class_init(const DevState* __restrict__ stp, int c0, int nc, int n_pods) {
+  const DevState& st = *stp;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n_pods) return;
+  const uint32_t fl = gp(st.pod_flags)[p];
+  if (!(fl & KGPU_PF_ACTIVE)) return;
+  const int n = gp(st.pod_node)[p] - st.node_base;
+  if (n < 0 || n >= st.N) return;
+  for (int c = c0; c < c0 + nc; ++c) {
+    const ClassRec cr = st.classes[c];
+    if (cr.excl_terminating && (fl & KGPU_PF_TERMINATING)) continue;
+    bool ok = cr.n_items > 0;
+    for (int i = 0; i < cr.n_items && ok; ++i) ok = pod_item_match(st, st.class_items[cr.item0 + i], p);
+    if (ok) atomicAdd(gp(st.mcnt) + (size_t)c * st.N + n, 1);
+  }
+}
+
+int launch_topo(const DevState* st, const PodArgs& a, int blocks, int64_t min_values, int64_t next_scratch,
+                void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_topo_pre, dim3(blocks), dim3(kBlock), 0, s, st, a);
+  if (min_values > 0) {
+    int64_t mb = (min_values + kBlock - 1) / kBlock;
+    if (mb > kMaxBlocks) mb = kMaxBlocks;
+    hipLaunchKernelGGL(k_topo_min, dim3((int)mb), dim3(kBlock), 0, s, st, a);
+  }
+  hipLaunchKernelGGL(k_topo_filter, dim3(blocks), dim3(kBlock), 0, s, st, a);
+  hipLaunchKernelGGL(k_topo_score, dim3(blocks), dim3(kBlock), 0, s, st, a);
+  hipLaunchKernelGGL(k_topo_final, dim3(blocks), dim3(kBlock), 0, s, st, a, blocks);
+  PodArgs r = a;
+  r.prev = a.pod;
+  r.prev_blocks = blocks;
+  r.prev_parity = a.parity;
+  hipLaunchKernelGGL(k_topo_resolve, dim3(blocks), dim3(kBlock), 0, s, st, r, next_scratch);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_class_init(const DevState* st, int c0, int nc, int n_pods, void* stream) {
+  if (n_pods <= 0 || nc <= 0) return 0;
+  hipLaunchKernelGGL(k_class_init, dim3((n_pods + 255) / 256), dim3(256), 0, (hipStream_t)stream, st, c0, nc, n_pods);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 // ---------------------------------------------------------------- profile instantiations
