@@ -22,7 +22,8 @@ for p in (ROOT, os.path.join(ROOT, "kubernetes-1_amd")):
         sys.path.insert(0, p)
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md chip table)
-BYTES_PER_NODE_EVAL = {"b": 72, "a": 73, "c": 121}  # SURVEY.md 8(d) algorithmic bytes per node-eval
+BYTES_PER_NODE_EVAL = {"b": 72, "a": 73, "c": 121, "d": 84}  # SURVEY.md 8(d) algorithmic bytes per node-eval
+BYTES_PER_EXISTING_POD = {"d": 24}  # IPA reads {node, ns, label bitset} per existing pod per pod
 
 
 def log(*a):
@@ -36,6 +37,10 @@ def make_workload(cfg, n_nodes, n_pods):
     if cfg == "a":
         nodes, init, pods, prof = cluster.scheduling_basic(n_nodes=n_nodes, n_init=n_nodes, n_pods=n_pods)
         return nodes, [], init + pods, prof
+    if cfg == "c":
+        return cluster.taints_affinity_spread(n_nodes=n_nodes, n_pods=n_pods)
+    if cfg == "d":
+        return cluster.pod_affinity(n_nodes=n_nodes, n_existing=n_nodes, n_pods=n_pods)
     raise SystemExit("config %r not benchmarked yet" % cfg)
 
 
@@ -117,8 +122,10 @@ def main():
     per_pod_s = kst.eval_kernel_ms / 1e3 / max(kst.eval_launches, 1)
     bpe = BYTES_PER_NODE_EVAL.get(args.config, 72)
     n_local = fw.snap.n_nodes
-    achieved = n_local * bpe / per_pod_s / 1e9
-    persistent = not args.no_persistent
+    pod_bytes = n_local * bpe + BYTES_PER_EXISTING_POD.get(args.config, 0) * len(existing)
+    achieved = pod_bytes / per_pod_s / 1e9
+    topo = args.config in ("c", "d")
+    persistent = not args.no_persistent and not topo
     launch_pods = B if persistent else 1
 
     # CPU baseline: the C restatement of the reference algorithm on this host's cores.  Both the
@@ -157,10 +164,10 @@ def main():
             "placed": placed,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-                         "kernel": "k_batch" if persistent else "k_eval",
+                         "kernel": "k_batch" if persistent else ("k_topo_* pipeline" if topo else "k_eval"),
                          "avg_kernel_us": round(per_pod_s * launch_pods * 1e6, 3), "pods_per_launch": launch_pods,
                          "us_per_pod": round(per_pod_s * 1e6, 4),
-                         "bytes_per_launch": n_local * bpe * launch_pods},
+                         "bytes_per_launch": pod_bytes * launch_pods},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

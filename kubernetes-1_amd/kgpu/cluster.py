@@ -129,4 +129,54 @@ def taints_affinity_spread(n_nodes=5000, n_pods=10000, seed=CLUSTER_SEED, n_zone
     return nodes, [], pods, _c.Profile()
 
 
-CONFIGS = {"a": scheduling_basic, "b": fit_least_balanced, "c": taints_affinity_spread}
+# ----------------------------------------------------------------------------- (d)
+_AFF_KINDS = ["nil", "req", "pref", "req_pref"]
+
+
+def _pod_terms(label, topo_key, kind):
+    """PodAffinityExists / PodAntiAffinityExists terms (testing/wrappers.go:260-336)."""
+    term = {"labelSelector": {"matchExpressions": [{"key": label, "operator": "Exists"}]}, "topologyKey": topo_key}
+    out = {}
+    if kind in ("req", "req_pref"):
+        out["requiredDuringSchedulingIgnoredDuringExecution"] = [dict(term)]
+    if kind in ("pref", "req_pref"):
+        out["preferredDuringSchedulingIgnoredDuringExecution"] = [{"weight": 1, "podAffinityTerm": dict(term)}]
+    return out
+
+
+def _affinity_combo(i, labels, tp_keys):
+    label, tp = labels[i % len(labels)], tp_keys[i % len(tp_keys)]
+    idx = i % 16
+    aff, anti = _AFF_KINDS[idx // 4], _AFF_KINDS[idx % 4]
+    a = {}
+    if aff != "nil":
+        a["podAffinity"] = _pod_terms(label, tp, aff)
+    if anti != "nil":
+        a["podAntiAffinity"] = _pod_terms(label, tp, anti)
+    return a
+
+
+def pod_affinity(n_nodes=5000, n_existing=5000, n_pods=10000):
+    """Config (d): testing.MakeNodesAndPodsForPodAffinity (workload_prep.go:63-121): nodes labelled
+    region i%3 / zone i%10 / node i, existing pods on node i%N carrying the 16 combinations of
+    PodAffinityExists x PodAntiAffinityExists over labels foo/bar/baz and topology keys
+    region/zone/node.  Nodes get node-default.yaml capacity (4 cpu, 32Gi, 110 pods); incoming pods
+    (pod-default.yaml requests) carry label foo/bar/baz and cycle through the same 16 combinations."""
+    labels, tp_keys = ["foo", "bar", "baz"], ["region", "zone", "node"]
+    nodes = [node("node%d" % i, "4", "32Gi", 110,
+                  labels={"region": "region%d" % (i % 3), "zone": "zone%d" % (i % 10), "node": "node%d" % i})
+             for i in range(n_nodes)]
+    existing = []
+    for i in range(n_existing):
+        a = _affinity_combo(i, labels, tp_keys)
+        spec = {"affinity": a} if a else {}
+        existing.append(pod("pod%d" % i, node_name="node%d" % (i % n_nodes), **spec))
+    pods = []
+    for i in range(n_pods):
+        a = _affinity_combo(i, labels, tp_keys)
+        spec = {"affinity": a} if a else {}
+        pods.append(pod("p%d" % i, "100m", "500Mi", labels={labels[(i // 16) % 3]: ""}, **spec))
+    return nodes, existing, pods, _c.Profile()
+
+
+CONFIGS = {"a": scheduling_basic, "b": fit_least_balanced, "c": taints_affinity_spread, "d": pod_affinity}

@@ -53,6 +53,12 @@ class KeySpace:
     def key(self, k):
         return self.keys.get(k)
 
+    def add_key(self, k):
+        ki = self.keys.add(k)
+        if ki == len(self.vals):
+            self.vals.append(StrDict())
+        return ki
+
     def val(self, ki, v):
         return -1 if ki < 0 else self.vals[ki].get(v)
 
@@ -122,8 +128,16 @@ def _validate_req(key, op, vals):
             raise CompileError("invalid label value %r" % v)
 
 
-def _req_rec(ks, pools, key, op, vals):
-    ki = ks.key(key)
+def _req_rec(ks, pools, key, op, vals, register=False):
+    """register: pod label selectors add their key and values to the pod key space, so that a pod
+    compiled later with that label gets the ids the selector already holds (node selectors run
+    against the fixed node set of the snapshot and drop unknown values instead)."""
+    if register:
+        ki = ks.add_key(key)
+        for v in vals if op in (abi.OP_IN, abi.OP_NOTIN) else ():
+            ks.add(key, v)
+    else:
+        ki = ks.key(key)
     vids = []
     if op in (abi.OP_IN, abi.OP_NOTIN) and ki >= 0:
         vids = sorted({ks.val(ki, v) for v in vals} - {-1})
@@ -140,14 +154,14 @@ def compile_label_selector(ks, pools, ps):
     recs = []
     for k in sorted(ml):
         _validate_req(k, abi.OP_IN, [ml[k]])
-        recs.append(_req_rec(ks, pools, k, abi.OP_IN, [ml[k]]))
+        recs.append(_req_rec(ks, pools, k, abi.OP_IN, [ml[k]], register=True))
     for e in me:
         op = _LSEL.get(e.get("operator"))
         if op is None:
             raise CompileError("invalid pod selector operator %r" % e.get("operator"))
         vals = list(e.get("values") or [])
         _validate_req(e.get("key", ""), op, vals)
-        recs.append(_req_rec(ks, pools, e.get("key", ""), op, vals))
+        recs.append(_req_rec(ks, pools, e.get("key", ""), op, vals, register=True))
     b = len(pools.reqs)
     pools.reqs.extend(recs)
     return (abi.SEL_AND, 0, (b, len(recs)))
@@ -483,7 +497,7 @@ class Compiler:
         snap.port_slots = A["port_slots"]
         snap.n_zones = len(self.zones)
         snap.n_pods = len(A["pod_node"])
-        snap.n_pod_label_keys = len(self.pkeys.keys)
+        snap.n_pod_label_keys = A["pod_label_val"].shape[0]  # keys registered later have no snapshot pod
         snap.n_terms = len(A["terms"])
         snap.pools, A["_pools_np"] = A["_pools"].finalize()
         A["_snap"] = snap

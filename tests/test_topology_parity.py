@@ -79,3 +79,42 @@ def test_gpu_matches_oracle_topology(seed):
     _, rows_c = product_run(*args, backend="ref")
     for k in rows:
         np.testing.assert_array_equal(rows[k], rows_c[k], err_msg=k)
+
+
+def _config_case(name):
+    from kgpu import cluster
+    if name == "c":
+        nodes, ex, pods, _ = cluster.taints_affinity_spread(n_nodes=60, n_pods=80)
+    else:
+        nodes, ex, pods, _ = cluster.pod_affinity(n_nodes=60, n_existing=60, n_pods=48)
+    return nodes, ex, pods, [], []
+
+
+@pytest.mark.parametrize("cfg", ["c", "d"])
+def test_c_restatement_matches_python_oracle_bench_configs(cfg):
+    args = _config_case(cfg)
+    _cmp(oracle_run(*args), product_run(*args, backend="ref")[0])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", ["c", "d"])
+def test_gpu_matches_oracle_bench_configs(cfg):
+    args = _config_case(cfg)
+    _cmp(oracle_run(*args), product_run(*args, backend="gpu")[0])
+
+
+@pytest.mark.parametrize("hint", [0, 4])
+def test_compile_order_independent(hint):
+    """Selectors compiled before any pod carries their label keys / values still match pods
+    compiled later (the snapshot is compiled with only `hint` incoming pods registered)."""
+    from kgpu import cluster
+    from oracle.cref import RefEngine
+    nodes, ex, pods, _ = cluster.pod_affinity(n_nodes=40, n_existing=40, n_pods=48)
+    want = oracle_run(nodes, ex, pods, [], [])
+    fw = GpuFramework(Profile(), nodes, ex, pods_hint=pods[:hint], create_engine=False)
+    q, pc, _, errs = fw.compile_pods(pods)
+    assert not errs
+    res = RefEngine(fw.config, fw.snap).schedule(q, pc)
+    got = [(None, 0, None) if r["node"] == -1 else (fw.order[r["node"]], int(r["feasible"]),
+                                                    int(r["score"]) if r["scored"] else None) for r in res]
+    _cmp(want, got)
