@@ -1,0 +1,248 @@
+"""Golden vectors transcribed from pkg/scheduler/framework/plugins/interpodaffinity/
+{scoring_test.go (TestPreferredAffinity, TestPreferredAffinityWithHardPodAffinitySymmetricWeight),
+filtering_test.go (TestRequiredAffinitySingleNode, TestRequiredAffinityMultipleNodes)}."""
+from gen_common import case
+
+SSRC = "pkg/scheduler/framework/plugins/interpodaffinity/scoring_test.go"
+FSRC = "pkg/scheduler/framework/plugins/interpodaffinity/filtering_test.go"
+
+
+def req(key, op, vals=None):
+    e = {"key": key, "operator": op}
+    if vals is not None:
+        e["values"] = list(vals)
+    return e
+
+
+def term(exprs, topo, ns=None, match_labels=None):
+    sel = {}
+    if exprs is not None:
+        sel["matchExpressions"] = list(exprs)
+    if match_labels is not None:
+        sel["matchLabels"] = dict(match_labels)
+    t = {"labelSelector": sel, "topologyKey": topo}
+    if ns is not None:
+        t["namespaces"] = list(ns)
+    return t
+
+
+def wterm(w, exprs, topo):
+    return {"weight": w, "podAffinityTerm": term(exprs, topo)}
+
+
+def pod(labels=None, node=None, affinity=None, name="", ns=""):
+    m = {"name": name, "namespace": ns}
+    if labels is not None:
+        m["labels"] = dict(labels)
+    s = {}
+    if node:
+        s["nodeName"] = node
+    if affinity is not None:
+        s["affinity"] = affinity
+    return {"metadata": m, "spec": s}
+
+
+def node(name, labels=None):
+    m = {"name": name}
+    if labels is not None:
+        m["labels"] = dict(labels)
+    return {"metadata": m, "spec": {}, "status": {"allocatable": {}}}
+
+
+CHINA, INDIA = {"region": "China"}, {"region": "India"}
+AZ1, AZ2 = {"az": "az1"}, {"az": "az2"}
+CHINA_AZ1 = {"region": "China", "az": "az1"}
+S1, S2 = {"security": "S1"}, {"security": "S2"}
+
+STAY_S1_REGION = {"podAffinity": {"preferredDuringSchedulingIgnoredDuringExecution": [
+    wterm(5, [req("security", "In", ["S1"])], "region")]}}
+STAY_S2_REGION = {"podAffinity": {"preferredDuringSchedulingIgnoredDuringExecution": [
+    wterm(6, [req("security", "In", ["S2"])], "region")]}}
+AFFINITY3 = {"podAffinity": {"preferredDuringSchedulingIgnoredDuringExecution": [
+    wterm(8, [req("security", "NotIn", ["S1"]), req("security", "In", ["S2"])], "region"),
+    wterm(2, [req("security", "Exists"), req("wrongkey", "DoesNotExist")], "region")]}}
+HARD_AFFINITY = {"podAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
+    term([req("security", "In", ["S1", "value2"])], "region"),
+    term([req("security", "Exists"), req("wrongkey", "DoesNotExist")], "region")]}}
+AWAY_S1_AZ = {"podAntiAffinity": {"preferredDuringSchedulingIgnoredDuringExecution": [
+    wterm(5, [req("security", "In", ["S1"])], "az")]}}
+AWAY_S2_AZ = {"podAntiAffinity": {"preferredDuringSchedulingIgnoredDuringExecution": [
+    wterm(5, [req("security", "In", ["S2"])], "az")]}}
+STAY_S1_AWAY_S2 = {"podAffinity": {"preferredDuringSchedulingIgnoredDuringExecution": [
+    wterm(8, [req("security", "In", ["S1"])], "region")]},
+    "podAntiAffinity": {"preferredDuringSchedulingIgnoredDuringExecution": [
+        wterm(5, [req("security", "In", ["S2"])], "az")]}}
+
+
+def score_cases():
+    out = []
+
+    def sc(name, line, p, existing, nodes, want, hard_weight=1):
+        out.append(case(name, SSRC + ":%d" % line, kind="score", plugin="InterPodAffinity",
+                        args={"hard_pod_affinity_weight": hard_weight}, pod=p, pods=existing, nodes=nodes,
+                        normalize=True, expect_scores=want))
+
+    m = ["machine%d" % i for i in range(6)]
+    sc("all machines are same priority as Affinity is nil", 262, pod(S1), [],
+       [node(m[1], CHINA), node(m[2], INDIA), node(m[3], AZ1)], {m[1]: 0, m[2]: 0, m[3]: 0})
+    sc("Affinity: pod that matches topology key & pods in nodes will get high score comparing to others"
+       "which doesn't match either pods in nodes or in topology key", 275, pod(S1, affinity=STAY_S1_REGION),
+       [pod(S1, m[1]), pod(S2, m[2]), pod(S1, m[3])], [node(m[1], CHINA), node(m[2], INDIA), node(m[3], AZ1)],
+       {m[1]: 100, m[2]: 0, m[3]: 0})
+    sc("All the nodes that have the same topology key & label value with one of them has an existing pod that "
+       "match the affinity rules, have the same score", 295, pod(None, affinity=STAY_S1_REGION), [pod(S1, m[1])],
+       [node(m[1], CHINA), node(m[2], CHINA_AZ1), node(m[3], INDIA)], {m[1]: 100, m[2]: 100, m[3]: 0})
+    sc("Affinity: nodes in one region has more matching pods comparing to other reqion, so the region which has "
+       "more macthes will get high score", 312, pod(S1, affinity=STAY_S2_REGION),
+       [pod(S2, m[1]), pod(S2, m[1]), pod(S2, m[2]), pod(S2, m[3]), pod(S2, m[4]), pod(S2, m[5])],
+       [node(m[1], CHINA), node(m[2], INDIA), node(m[3], CHINA), node(m[4], CHINA), node(m[5], INDIA)],
+       {m[1]: 100, m[2]: 50, m[3]: 100, m[4]: 100, m[5]: 50})
+    sc("Affinity: different Label operators and values for pod affinity scheduling preference, including some "
+       "match failures ", 333, pod(S1, affinity=AFFINITY3), [pod(S1, m[1]), pod(S2, m[2]), pod(S1, m[3])],
+       [node(m[1], CHINA), node(m[2], INDIA), node(m[3], AZ1)], {m[1]: 20, m[2]: 100, m[3]: 0})
+    sc("Affinity symmetry: considered only the preferredDuringSchedulingIgnoredDuringExecution in pod affinity "
+       "symmetry", 350, pod(S2), [pod(S1, m[1], STAY_S1_REGION), pod(S2, m[2], STAY_S2_REGION)],
+       [node(m[1], CHINA), node(m[2], INDIA), node(m[3], AZ1)], {m[1]: 0, m[2]: 100, m[3]: 0})
+    sc("Affinity symmetry: considered RequiredDuringSchedulingIgnoredDuringExecution in pod affinity symmetry", 364,
+       pod(S1), [pod(S1, m[1], HARD_AFFINITY), pod(S2, m[2], HARD_AFFINITY)],
+       [node(m[1], CHINA), node(m[2], INDIA), node(m[3], AZ1)], {m[1]: 100, m[2]: 100, m[3]: 0})
+    sc("Anti Affinity: pod that doesnot match existing pods in node will get high score ", 385,
+       pod(S1, affinity=AWAY_S1_AZ), [pod(S1, m[1]), pod(S2, m[2])], [node(m[1], AZ1), node(m[2], CHINA)],
+       {m[1]: 0, m[2]: 100})
+    sc("Anti Affinity: pod that does not matches topology key & matches the pods in nodes will get higher score "
+       "comparing to others ", 398, pod(S1, affinity=AWAY_S1_AZ), [pod(S1, m[1]), pod(S1, m[2])],
+       [node(m[1], AZ1), node(m[2], CHINA)], {m[1]: 0, m[2]: 100})
+    sc("Anti Affinity: one node has more matching pods comparing to other node, so the node which has more "
+       "unmacthes will get high score", 411, pod(S1, affinity=AWAY_S1_AZ),
+       [pod(S1, m[1]), pod(S1, m[1]), pod(S2, m[2])], [node(m[1], AZ1), node(m[2], INDIA)], {m[1]: 0, m[2]: 100})
+    sc("Anti Affinity symmetry: the existing pods in node which has anti affinity match will get high score", 426,
+       pod(S2), [pod(S1, m[1], AWAY_S2_AZ), pod(S2, m[2], AWAY_S1_AZ)], [node(m[1], AZ1), node(m[2], AZ2)],
+       {m[1]: 0, m[2]: 100})
+    sc("Affinity and Anti Affinity: considered only preferredDuringSchedulingIgnoredDuringExecution in both pod "
+       "affinity & anti affinity", 440, pod(S1, affinity=STAY_S1_AWAY_S2), [pod(S1, m[1]), pod(S1, m[2])],
+       [node(m[1], CHINA), node(m[2], AZ1)], {m[1]: 100, m[2]: 0})
+    sc("Affinity and Anti Affinity: considering both affinity and anti-affinity, the pod to schedule and existing "
+       "pods have the same labels", 457, pod(S1, affinity=STAY_S1_AWAY_S2),
+       [pod(S1, m[1]), pod(S1, m[1]), pod(S1, m[2]), pod(S1, m[3]), pod(S1, m[3]), pod(S1, m[4]), pod(S1, m[5])],
+       [node(m[1], CHINA_AZ1), node(m[2], INDIA), node(m[3], CHINA), node(m[4], CHINA), node(m[5], INDIA)],
+       {m[1]: 100, m[2]: 40, m[3]: 100, m[4]: 100, m[5]: 40})
+    sc("Affinity and Anti Affinity and symmetry: considered only preferredDuringSchedulingIgnoredDuringExecution in "
+       "both pod affinity & anti affinity & symmetry", 483, pod(S1, affinity=STAY_S1_AWAY_S2),
+       [pod(S1, m[1]), pod(S2, m[2]), pod(None, m[3], STAY_S1_AWAY_S2), pod(None, m[4], AWAY_S1_AZ)],
+       [node(m[1], CHINA), node(m[2], AZ1), node(m[3], INDIA), node(m[4], AZ2)],
+       {m[1]: 100, m[2]: 0, m[3]: 100, m[4]: 0})
+    sc("Avoid panic when partial nodes in a topology don't have pods with affinity", 503, pod(S1),
+       [pod(S1, m[1]), pod(None, m[2], STAY_S1_AWAY_S2)], [node(m[1], CHINA), node(m[2], CHINA)],
+       {m[1]: 100, m[2]: 100})
+    # ---- TestPreferredAffinityWithHardPodAffinitySymmetricWeight
+    hard = {"podAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
+        term([req("service", "In", ["S1"])], "region")]}}
+    svc = {"service": "S1"}
+    sc("Hard Pod Affinity symmetry: hard pod affinity symmetry weights 1 by default, then nodes that match the hard "
+       "pod affinity symmetry rules, get a high score", 594, pod(svc),
+       [pod(None, m[1], hard), pod(None, m[2], hard)], [node(m[1], CHINA), node(m[2], INDIA), node(m[3], AZ1)],
+       {m[1]: 100, m[2]: 100, m[3]: 0}, hard_weight=1)
+    sc("Hard Pod Affinity symmetry: hard pod affinity symmetry is closed(weights 0), then nodes that match the hard "
+       "pod affinity symmetry rules, get same score with those not match", 609, pod(svc),
+       [pod(None, m[1], hard), pod(None, m[2], hard)], [node(m[1], CHINA), node(m[2], INDIA), node(m[3], AZ1)],
+       {m[1]: 0, m[2]: 0, m[3]: 0}, hard_weight=0)
+    return out
+
+
+
+
+def cpwat(ns, node_name, labels, aff, anti):
+    """createPodWithAffinityTerms (filtering_test.go:34-53): both PodAffinity and PodAntiAffinity
+    are non-nil, holding the given required terms."""
+    a = {"podAffinity": {}, "podAntiAffinity": {}}
+    if aff is not None:
+        a["podAffinity"]["requiredDuringSchedulingIgnoredDuringExecution"] = list(aff)
+    if anti is not None:
+        a["podAntiAffinity"]["requiredDuringSchedulingIgnoredDuringExecution"] = list(anti)
+    return pod(labels, node_name or None, a, ns=ns)
+
+
+R_AFF = ["node(s) didn't match pod affinity/anti-affinity", "node(s) didn't match pod affinity rules"]
+R_ANTI = ["node(s) didn't match pod affinity/anti-affinity", "node(s) didn't match pod anti-affinity rules"]
+R_EXIST = ["node(s) didn't match pod affinity/anti-affinity", "node(s) didn't satisfy existing pods anti-affinity rules"]
+U, UR = 2, 3
+
+
+def single_node_cases():
+    out = []
+    SVC = {"service": "securityscan"}
+    SEC = {"security": "S1"}
+    n1 = node("machine1", {"region": "r1", "zone": "z11"})
+
+    def fc(name, line, p, existing, code=0, reasons=()):
+        out.append(case(name, FSRC + ":%d" % line, kind="filter", plugin="InterPodAffinity", args={}, pod=p,
+                        pods=existing, nodes=[n1],
+                        expect_filter={"machine1": {"code": code, "reasons": list(reasons)}}))
+
+    in_ss = [req("service", "In", ["securityscan", "value2"])]
+    in_av = [req("service", "In", ["antivirusscan", "value2"])]
+    fc("A pod that has no required pod affinity scheduling rules can schedule onto a node with no existing pods", 71,
+       pod(), [])
+    fc("satisfies with requiredDuringSchedulingIgnoredDuringExecution in PodAffinity using In operator that matches "
+       "the existing pod", 76, cpwat("", "", SEC, [term(in_ss, "region")], None), [pod(SVC, "machine1")])
+    fc("satisfies the pod with requiredDuringSchedulingIgnoredDuringExecution in PodAffinity using not in operator "
+       "in labelSelector that matches the existing pod", 96,
+       cpwat("", "", SEC, [term([req("service", "NotIn", ["securityscan3", "value3"])], "region")], None),
+       [pod(SVC, "machine1")])
+    fc("Does not satisfy the PodAffinity with labelSelector because of diff Namespace", 116,
+       cpwat("", "", SEC, [term(in_ss, "", ns=["DiffNameSpace"])], None), [pod(SVC, "machine1", ns="ns")], UR, R_AFF)
+    fc("Doesn't satisfy the PodAffinity because of unmatching labelSelector with the existing pod", 141,
+       cpwat("", "", SVC, [term(in_av, "")], None), [pod(SVC, "machine1")], UR, R_AFF)
+    fc("satisfies the PodAffinity with different label Operators in multiple RequiredDuringSchedulingIgnoredDuring"
+       "Execution ", 165,
+       cpwat("", "", SEC, [term([req("service", "Exists"), req("wrongkey", "DoesNotExist")], "region"),
+                           term([req("service", "In", ["securityscan"]), req("service", "NotIn", ["WrongValue"])],
+                                "region")], None), [pod(SVC, "machine1")])
+    fc("The labelSelector requirements(items of matchExpressions) are ANDed, the pod cannot schedule onto the node "
+       "because one of the matchExpression item don't match.", 202,
+       cpwat("", "", SEC, [term([req("service", "Exists"), req("wrongkey", "DoesNotExist")], "region"),
+                           term([req("service", "In", ["securityscan2"]), req("service", "NotIn", ["WrongValue"])],
+                                "region")], None), [pod(SVC, "machine1")], UR, R_AFF)
+    fc("satisfies the PodAffinity and PodAntiAffinity with the existing pod", 244,
+       cpwat("", "", SEC, [term(in_ss, "region")], [term(in_av, "node")]), [pod(SVC, "machine1")])
+    fc("satisfies the PodAffinity and PodAntiAffinity and PodAntiAffinity symmetry with the existing pod", 278,
+       cpwat("", "", SEC, [term(in_ss, "region")], [term(in_av, "node")]),
+       [cpwat("", "machine1", SVC, None, [term(in_av, "node")])])
+    fc("satisfies the PodAffinity but doesn't satisfy the PodAntiAffinity with the existing pod", 328,
+       cpwat("", "", SEC, [term(in_ss, "region")], [term(in_ss, "zone")]), [pod(SVC, "machine1")], U, R_ANTI)
+    fc("satisfies the PodAffinity and PodAntiAffinity but doesn't satisfy PodAntiAffinity symmetry with the existing "
+       "pod", 367, cpwat("", "", SVC, [term(in_ss, "region")], [term(in_av, "node")]),
+       [cpwat("", "machine1", SVC, None, [term(in_ss, "zone")])], U, R_EXIST)
+    fc("pod matches its own Label in PodAffinity and that matches the existing pod Labels", 422,
+       cpwat("", "", SVC, [term([req("service", "NotIn", ["securityscan", "value2"])], "region")], None),
+       [pod(SVC, "machine2")], UR, R_AFF)
+    fc("verify that PodAntiAffinity from existing pod is respected when pod has no AntiAffinity constraints. doesn't "
+       "satisfy PodAntiAffinity symmetry with the existing pod", 447, pod(SVC),
+       [cpwat("", "machine1", SVC, None, [term(in_ss, "zone")])], U, R_EXIST)
+    fc("verify that PodAntiAffinity from existing pod is respected when pod has no AntiAffinity constraints. satisfy "
+       "PodAntiAffinity symmetry with the existing pod", 478, pod(SVC),
+       [cpwat("", "machine1", SVC, None, [term([req("service", "NotIn", ["securityscan", "value2"])], "zone")])])
+    fc("satisfies the PodAntiAffinity with existing pod but doesn't satisfy PodAntiAffinity symmetry with incoming "
+       "pod", 504, cpwat("", "", SVC, None, [term([req("service", "Exists")], "region"),
+                                             term([req("security", "Exists")], "region")]),
+       [cpwat("", "machine1", SEC, None, [term([req("security", "Exists")], "zone")])], U, R_ANTI)
+    fc("PodAntiAffinity symmetry check a1: incoming pod and existing pod partially match each other on AffinityTerms",
+       554, cpwat("", "", SVC, None, [term([req("service", "Exists")], "zone"),
+                                      term([req("security", "Exists")], "zone")]),
+       [cpwat("", "machine1", SEC, None, [term([req("security", "Exists")], "zone")])], U, R_ANTI)
+    fc("PodAntiAffinity symmetry check a2: incoming pod and existing pod partially match each other on AffinityTerms",
+       604, cpwat("", "", SEC, None, [term([req("security", "Exists")], "zone")]),
+       [cpwat("", "machine1", SVC, None, [term([req("service", "Exists")], "zone"),
+                                           term([req("security", "Exists")], "zone")])], U, R_EXIST)
+    ab = [term([req("abc", "Exists")], "zone"), term([req("def", "Exists")], "zone")]
+    fc("PodAntiAffinity symmetry check b1: incoming pod and existing pod partially match each other on AffinityTerms",
+       654, cpwat("", "", {"abc": "", "xyz": ""}, None, ab),
+       [cpwat("", "machine1", {"def": "", "xyz": ""}, None, ab)], U, R_ANTI)
+    fc("PodAntiAffinity symmetry check b2: incoming pod and existing pod partially match each other on AffinityTerms",
+       715, cpwat("", "", {"def": "", "xyz": ""}, None, ab),
+       [cpwat("", "machine1", {"abc": "", "xyz": ""}, None, ab)], U, R_ANTI)
+    return out
+
+
+def all_cases():
+    return score_cases() + single_node_cases()
