@@ -55,6 +55,8 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=400, help="pods timed for the CPU baseline (0: skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-persistent", action="store_true", help="one evaluation launch per pod")
+    ap.add_argument("--shard", action="store_true",
+                    help="at N=1: run the node-sharded path on a one-rank RCCL communicator (exchange overhead)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -74,11 +76,24 @@ def main():
     B, K, W = args.pods_per_step, args.steps, args.warmup
     n_pods = B * K
     t_gen = time.time()
-    nodes, existing, pods, prof = make_workload(args.config, args.nodes, n_pods)
-    fw = GpuFramework(prof, nodes, existing, pods_hint=pods[:16], device=local)
+    # N > 1: the cluster is sharded by node across the ranks; each GPU holds a
+    # --nodes-sized contiguous shard of Snapshot.List() (weak scaling in nodes: the cluster grows
+    # with N), and every pod's shard winners are all-gathered over RCCL.
+    n_cluster = args.nodes * world
+    nodes, existing, pods, prof = make_workload(args.config, n_cluster, n_pods)
+    sharded = dist_on or args.shard
+    fw = GpuFramework(prof, nodes, existing, pods_hint=pods[:16], device=local,
+                      shard=(rank, world) if sharded else None)
+    if sharded:
+        from kgpu import native
+        uid = [native.comm_unique_id() if rank == 0 else None]
+        if dist_on:
+            dist.broadcast_object_list(uid, src=0)
+        fw.init_comm(rank, world, uid[0])
     q, pc, pnp, errs = fw.compile_pods(pods)
     assert not errs, errs
-    log("workload: %d nodes, %d pods, compiled in %.1fs" % (len(nodes), len(pods), time.time() - t_gen))
+    log("workload: %d nodes (%d on this rank), %d pods, compiled in %.1fs"
+        % (len(nodes), fw.snap.n_nodes, len(pods), time.time() - t_gen))
     eng = fw.engine
     if args.no_persistent:
         eng.set_option(abi.OPT_PERSISTENT, 0)
@@ -125,14 +140,14 @@ def main():
     pod_bytes = n_local * bpe + BYTES_PER_EXISTING_POD.get(args.config, 0) * len(existing)
     achieved = pod_bytes / per_pod_s / 1e9
     topo = args.config in ("c", "d")
-    persistent = not args.no_persistent and not topo
+    persistent = not args.no_persistent and not topo and not sharded
     launch_pods = B if persistent else 1
 
     # CPU baseline: the C restatement of the reference algorithm on this host's cores.  Both the
     # reference's structure (16 workers, chunk = min(sqrt(n), n/16+1)) and a single thread are
     # timed; the faster one is reported (the stronger baseline).
     cpu = None
-    if rank == 0 and args.cpu_sample > 0:
+    if rank == 0 and world == 1 and args.cpu_sample > 0:
         from oracle.cref import RefEngine
         S = min(args.cpu_sample, n_pods)
         best = None
@@ -158,13 +173,15 @@ def main():
             "scaling": "weak", "vs_baseline": None, "dtype": "int64", "data": "synthetic",
             "config": {"workload": "config(%s): %d nodes / %d pods, %s" % (args.config, len(nodes), n_pods,
                                                                             "+".join(prof.filters + [s for s, _ in prof.scores])),
-                       "nodes": len(nodes), "pods": n_pods, "pods_per_step": B,
-                       "percentage_of_nodes_to_score": 100},
+                       "nodes": len(nodes), "nodes_per_gpu": fw.snap.n_nodes, "pods": n_pods, "pods_per_step": B,
+                       "percentage_of_nodes_to_score": 100,
+                       "parallelism": ("node shards x%d, RCCL all-gather per pod" % world) if sharded else "1 GPU"},
             "node_evals_per_s": round(pods_per_s * len(nodes), 1),
             "placed": placed,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
                          "kernel": "k_batch" if persistent else ("k_topo_* pipeline" if topo else "k_eval"),
+                         "bytes_per_node_eval": bpe,
                          "avg_kernel_us": round(per_pod_s * launch_pods * 1e6, 3), "pods_per_launch": launch_pods,
                          "us_per_pod": round(per_pod_s * 1e6, 4),
                          "bytes_per_launch": pod_bytes * launch_pods},

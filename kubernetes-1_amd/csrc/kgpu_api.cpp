@@ -6,6 +6,7 @@
 // maximum is needed) on a single stream, with the previous pod's selectHost + assume folded
 // into the head of the next launch (kgpu_kernels.hip).  The host never waits between pods.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cmath>
@@ -86,6 +87,11 @@ struct kgpu_ctx {
   int pod_rows_dev = -1;         // rows present in the device pod table (-1: table never uploaded)
   std::vector<int32_t> key_n_values, key_empty;
   int64_t max_key_values = 1;
+  // ---- node sharding (kgpu_comm_init): this context holds one contiguous slice of the
+  // snapshot; per pod the shard winners (and normalize maxima) are all-gathered over RCCL
+  ncclComm_t comm = nullptr;
+  int32_t nranks = 1, rank = 0;
+  DevBuf shard;   // send key | send stat | keys [2][kMaxRanks] | stats [2][kMaxRanks]
 };
 
 namespace {
@@ -660,14 +666,31 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
   int64_t timed_passes = 0;
   // Persistent geometry: one workgroup per CU at most, K node rows per lane in registers.
   int per = 0, groups = 0;
-  const int kidx = (c->persistent && !diag) ? kgpu::batch_geometry(st.N, std::min(c->max_groups > 0 ? std::min(c->max_groups, c->n_cus) : c->n_cus, 256), &per, &groups) : -1;
+  const bool sharded = c->comm != nullptr;
+  const int kidx = (c->persistent && !diag && !sharded) ? kgpu::batch_geometry(st.N, std::min(c->max_groups > 0 ? std::min(c->max_groups, c->n_cus) : c->n_cus, 256), &per, &groups) : -1;
   std::vector<uint8_t> norm((size_t)n), topo((size_t)n, 0);
   // pods that need the normalize pass or whose scoring fails take the one-launch-per-pod path;
   // pods with topology state take the topology pipeline
   for (int32_t i = 0; i < n; ++i) {
     norm[(size_t)i] = (diag || needs_norm(c, qs[i], pools) || (qs[i].flags & KGPU_Q_SCORE_ERROR)) ? 1 : 0;
     if (topo_on) topo[(size_t)i] = plans[(size_t)i].topo ? 1 : 0;
+    if (sharded && topo[(size_t)i])
+      return fail(c, KGPU_E_UNSUPPORTED, "node sharding: pods with PodTopologySpread / InterPodAffinity state are "
+                                         "not sharded yet (schedule them on an unsharded context)");
   }
+  // Sharded: after the evaluation (and normalize) of pod k, pack this shard's record and
+  // all-gather it on the same stream; the next launch resolves pod k over every rank's record.
+  auto exchange = [&](int parity, int what) -> int {
+    if (kgpu::launch_shard_pack(dst, parity, blocks, what, c->stream))
+      return fail(c, KGPU_E_DEVICE, "k_shard_pack launch failed");
+    const ncclResult_t r =
+        what == 0 ? ncclAllGather(c->st.shard_send_key, c->st.shard_keys + (size_t)parity * kgpu::kMaxRanks,
+                                  sizeof(BlkKey) / 8, ncclUint64, c->comm, c->stream)
+                  : ncclAllGather(c->st.shard_send_stat, c->st.shard_stats + (size_t)parity * kgpu::kMaxRanks,
+                                  sizeof(BlkStat) / 4, ncclInt32, c->comm, c->stream);
+    if (r != ncclSuccess) return fail(c, KGPU_E_DEVICE, std::string("ncclAllGather: ") + ncclGetErrorString(r));
+    return KGPU_OK;
+  };
   bool used_persistent = false;
   int32_t i = 0;
   while (i < n) {
@@ -754,8 +777,10 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
         if (c->timing) HIP_OK(c, hipEventRecord(get_event(c, ev + 1), c->stream));
         ev += 2;
         ++timed_passes;
+        if (sharded && a.norm && (rc = exchange(a.parity, 1))) return rc;
         if (a.norm && kgpu::launch_final(dst, a, blocks, blocks, c->stream))
           return fail(c, KGPU_E_DEVICE, "k_final launch failed");
+        if (sharded && (rc = exchange(a.parity, 0))) return rc;
         prev = k;
       }
       PodArgs r{};
@@ -810,7 +835,9 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
         c->pod_rows.push_back(std::move(row));
       }
       kgpu_ctx::Assumed a;
+      // the row lives on this shard, or (-1) on another rank, which owns its forget
       a.node = results[i].node - c->st.node_base;
+      if (a.node < 0 || a.node >= c->st.N) a.node = -1;
       a.q = qs[i];
       a.active = true;
       if (pools) {
@@ -926,6 +953,8 @@ int kgpu_destroy(kgpu_ctx* c) {
     if (b->p) (void)hipFree(b->p);
   if (c->st.mcnt) (void)hipFree(c->st.mcnt);
   if (c->st.tcnt) (void)hipFree(c->st.tcnt);
+  if (c->shard.p) (void)hipFree(c->shard.p);
+  if (c->comm) (void)ncclCommDestroy(c->comm);
   for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -1162,6 +1191,10 @@ int kgpu_forget_pod(kgpu_ctx* c, int32_t slot) {
   if (i < 0) return fail(c, KGPU_E_UNSUPPORTED, "forget of a snapshot pod: re-upload the snapshot");
   if (i >= (int32_t)c->assumed.size() || !c->assumed[i].active) return fail(c, KGPU_E_INVAL, "no such assumed pod");
   kgpu_ctx::Assumed& a = c->assumed[i];
+  if (a.node < 0) {  // sharded: assumed on another rank's node
+    a.active = false;
+    return KGPU_OK;
+  }
   HIP_OK(c, hipStreamSynchronize(c->stream));
   // NodeInfo.RemovePod (types.go:484-533): read-modify-write of one row (rare path).
   const size_t n = (size_t)a.node, N = (size_t)c->st.N;
@@ -1226,15 +1259,43 @@ int kgpu_forget_pod(kgpu_ctx* c, int32_t slot) {
 }
 
 int kgpu_comm_unique_id(uint8_t id[128]) {
-  (void)id;
-  return KGPU_E_UNSUPPORTED;
+  if (!id) return KGPU_E_INVAL;
+  static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId is 128 bytes");
+  ncclUniqueId u;
+  if (ncclGetUniqueId(&u) != ncclSuccess) return KGPU_E_DEVICE;
+  std::memcpy(id, &u, 128);
+  return KGPU_OK;
 }
 
 int kgpu_comm_init(kgpu_ctx* c, int32_t nranks, int32_t rank, const uint8_t id[128]) {
-  (void)nranks;
-  (void)rank;
-  (void)id;
-  return fail(c, KGPU_E_UNSUPPORTED, "sharded mode not built yet");
+  if (!c || !id) return KGPU_E_INVAL;
+  if (nranks < 1 || nranks > kgpu::kMaxRanks || rank < 0 || rank >= nranks)
+    return fail(c, KGPU_E_INVAL, "nranks must be in [1, 64] and 0 <= rank < nranks");
+  if (c->comm) return fail(c, KGPU_E_STATE, "communicator already initialized");
+  if (!c->uploaded) return fail(c, KGPU_E_STATE, "upload this rank's shard of the snapshot first");
+  HIP_OK(c, hipSetDevice(c->device));
+  ncclUniqueId u;
+  std::memcpy(&u, id, 128);
+  ncclComm_t comm = nullptr;
+  const ncclResult_t r = ncclCommInitRank(&comm, nranks, u, rank);
+  if (r != ncclSuccess) return fail(c, KGPU_E_DEVICE, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+  const size_t bytes = sizeof(BlkKey) + sizeof(BlkStat) + 2 * kgpu::kMaxRanks * (sizeof(BlkKey) + sizeof(BlkStat));
+  int rc;
+  if ((rc = ensure(c, c->shard, bytes))) {
+    (void)ncclCommDestroy(comm);
+    return rc;
+  }
+  HIP_OK(c, hipMemset(c->shard.p, 0, bytes));
+  char* b = static_cast<char*>(c->shard.p);
+  c->st.shard_send_key = reinterpret_cast<BlkKey*>(b);
+  c->st.shard_send_stat = reinterpret_cast<BlkStat*>(b + sizeof(BlkKey));
+  c->st.shard_keys = reinterpret_cast<BlkKey*>(b + sizeof(BlkKey) + sizeof(BlkStat));
+  c->st.shard_stats = reinterpret_cast<BlkStat*>(c->st.shard_keys + 2 * kgpu::kMaxRanks);
+  c->st.nranks = nranks;
+  c->comm = comm;
+  c->nranks = nranks;
+  c->rank = rank;
+  return KGPU_OK;
 }
 
 }  // extern "C"

@@ -11,6 +11,7 @@ constexpr int kBlock = 64;         // threads per node-evaluation workgroup: one
 constexpr int kMaxBlocks = 1024;   // cap so that the fused winner resolution stays cheap
 constexpr int kSelAnd = 0, kSelNothing = 1, kSelEmpty = 2;
 constexpr uint64_t kMask40 = (1ull << 40) - 1;
+constexpr int kMaxRanks = 64;      // node shards (one per GPU) combined per pod
 
 // Per-workgroup partial of the node-evaluation kernel for one pod.
 struct BlkStat {
@@ -194,6 +195,16 @@ struct DevState {
   uint32_t* pod_flags;
   int32_t* pod_lab;                     // [PKcap][Pcap]
   int32_t Pcap, PKcap;
+  // ---- node sharding (null / 0 when unsharded).  Per pod every rank packs its shard's winner
+  // (BlkKey with a GLOBAL node index) and its normalize maxima (BlkStat) into shard_send; an RCCL
+  // all-gather fills shard_keys / shard_stats [2 parities][kMaxRanks], which the next launch
+  // resolves exactly like the per-workgroup partials of an unsharded launch.
+  BlkKey* shard_send_key;
+  BlkStat* shard_send_stat;
+  BlkKey* shard_keys;
+  BlkStat* shard_stats;
+  int32_t nranks;
+  int32_t pad3;
 };
 
 // Per-launch parameters.
@@ -233,6 +244,9 @@ int select_spec(const int32_t* filters, int nf, const int32_t* scores, int ns, b
 int launch_final(const DevState* st, const PodArgs& a, int blocks, int stat_blocks, void* stream);
 int launch_resolve(const DevState* st, int N, const PodArgs& a, void* stream);
 int eval_blocks(int N);
+// Node sharding: reduce this shard's `blocks` partials of buffer half `parity` to one record in
+// shard_send_key (what = 0, global node index) or shard_send_stat (what = 1).
+int launch_shard_pack(const DevState* st, int parity, int blocks, int what, void* stream);
 // Geometry index (workgroup size x rows per lane) and grid of the persistent kernel, -1 when N
 // does not fit in max_groups workgroups.
 int batch_geometry(int N, int max_groups, int* per, int* groups);

@@ -608,15 +608,31 @@ __device__ __forceinline__ void assume_counts(const DevState& st, int pod, int n
   for (int i = 0; i < ot.count; ++i) gp(st.tcnt)[(size_t)st.aux[ot.begin + i] * st.N + n] += 1;
 }
 
+// The pending pod's winner: over the partials of this shard's previous launch or -- when nodes
+// are sharded across GPUs -- over every rank's packed shard winner (all-gathered by RCCL, global
+// node index).  w.idx comes back LOCAL (-1: the row lives on another rank); *gidx is global.
+__device__ __forceinline__ Winner prev_winner(const DevState& st, const PodArgs& a, int* gidx) {
+  if (st.shard_keys) {
+    Winner w = wave_winner(st.shard_keys + (size_t)a.prev_parity * kMaxRanks, st.nranks);
+    *gidx = w.idx;
+    const int l = w.idx - st.node_base;
+    w.idx = (w.idx >= 0 && l >= 0 && l < st.N) ? l : -1;
+    return w;
+  }
+  const Winner w = wave_winner(st.kbuf + (size_t)a.prev_parity * kMaxBlocks, a.prev_blocks);
+  *gidx = w.idx >= 0 ? st.node_base + w.idx : -1;
+  return w;
+}
+
 // The pending pod's outcome (generic_scheduler.go:171-208): FitError, the len==1 shortcut, or
 // the scored winner.  Returns the local row to assume (-1 none).
 __device__ __forceinline__ int settle_prev(const DevState& st, const PodArgs& a, const kgpu_pod_query& pq,
-                                           const Winner& w) {
+                                           const Winner& w, int gidx) {
   const bool error = (pq.flags & KGPU_Q_SCORE_ERROR) && w.feasible >= 2;
   const bool placed = w.feasible > 0 && !error;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     kgpu_result r;
-    r.node = placed ? st.node_base + w.idx : (error ? -2 : -1);
+    r.node = placed ? gidx : (error ? -2 : -1);
     r.feasible = w.feasible;
     r.evaluated = st.n_total;
     r.scored = (placed && w.feasible >= 2) ? 1 : 0;
@@ -649,8 +665,9 @@ __global__ __launch_bounds__(kBlock) void k_eval(const DevState* __restrict__ st
   int assume_idx = -1;
   const kgpu_pod_query* pq = st.queries + (a.prev >= 0 ? a.prev : 0);
   if (a.prev >= 0) {
-    const Winner w = wave_winner(st.kbuf + (size_t)a.prev_parity * kMaxBlocks, a.prev_blocks);
-    assume_idx = settle_prev(st, a, *cp(pq), w);
+    int gidx;
+    const Winner w = prev_winner(st, a, &gidx);
+    assume_idx = settle_prev(st, a, *cp(pq), w, gidx);
   }
   const uint64_t tk = pod_tie_key(st.seed, a.seq);
   const bool write_nodes = a.norm || a.diag;
@@ -699,7 +716,10 @@ __global__ __launch_bounds__(kBlock) void k_eval(const DevState* __restrict__ st
 __global__ __launch_bounds__(kBlock) void k_final(const DevState* __restrict__ stp, PodArgs a, int stat_blocks) {
   const DevState& st = *stp;
   int maxT = 0, maxNA = 0;
-  const GAS BlkStat* sb = gp(st.sbuf) + (size_t)a.parity * kMaxBlocks;
+  // sharded: the maxima over the whole cluster's feasible set, one all-gathered record per rank
+  const GAS BlkStat* sb = st.shard_stats ? gp(st.shard_stats) + (size_t)a.parity * kMaxRanks
+                                         : gp(st.sbuf) + (size_t)a.parity * kMaxBlocks;
+  if (st.shard_stats) stat_blocks = st.nranks;
   for (int b = threadIdx.x; b < stat_blocks; b += kBlock) {
     const BlkStat p = sb[b];
     maxT = max(maxT, p.max_taint);
@@ -740,14 +760,42 @@ __global__ __launch_bounds__(kBlock) void k_resolve(const DevState* __restrict__
   const DevState& st = *stp;
   int lo, hi;
   chunk_of(st.N, lo, hi);
-  const Winner w = wave_winner(st.kbuf + (size_t)a.prev_parity * kMaxBlocks, a.prev_blocks);
+  int gidx;
+  const Winner w = prev_winner(st, a, &gidx);
   const kgpu_pod_query pq = *cp(st.queries + a.prev);
-  const int idx = settle_prev(st, a, pq, w);
+  const int idx = settle_prev(st, a, pq, w, gidx);
   if (idx >= lo && idx < hi && ((idx - lo) % kBlock) == (int)threadIdx.x) {
     NodeRes r = load_res(st, idx);
     assume_row(st, pq, r, idx);
     assume_counts(st, a.prev, idx);
   }
+}
+
+// Node sharding: this shard's contribution to the pod's cluster-wide selectHost (what = 0: the
+// best packed key with its GLOBAL node index and the shard's feasible count) or to the
+// DefaultNormalizeScore maxima (what = 1).  One wave; the RCCL all-gather that follows on the same
+// stream makes every rank's record visible to the next launch (prev_winner / k_final).
+__global__ __launch_bounds__(kBlock) void k_shard_pack(const DevState* __restrict__ stp, int parity, int blocks,
+                                                       int what) {
+  const DevState& st = *stp;
+  if (what == 0) {
+    const Winner w = wave_winner(st.kbuf + (size_t)parity * kMaxBlocks, blocks);
+    if (threadIdx.x == 0)
+      *gp(st.shard_send_key) = BlkKey{w.key, (w.key && w.idx >= 0) ? st.node_base + w.idx : -1, w.feasible};
+    return;
+  }
+  int f = 0, mt = 0, mn = 0;
+  const GAS BlkStat* sb = gp(st.sbuf) + (size_t)parity * kMaxBlocks;
+  for (int b = threadIdx.x; b < blocks; b += kBlock) {
+    const BlkStat p = sb[b];
+    f += p.feasible;
+    mt = max(mt, p.max_taint);
+    mn = max(mn, p.max_na);
+  }
+  f = wave_reduce_sum(f);
+  mt = wave_reduce_max(mt);
+  mn = wave_reduce_max(mn);
+  if (threadIdx.x == 0) *gp(st.shard_send_stat) = BlkStat{f, mt, mn, 0};
 }
 
 // ---------------------------------------------------------------- persistent batch kernel
@@ -1422,7 +1470,10 @@ __global__ __launch_bounds__(kBlock) void k_topo_final(const DevState* __restric
   const QPlan& pl = st.plans[a.pod];
   const TopoHdr* h = hdr(st);
   int maxT = 0, maxNA = 0;
-  const GAS BlkStat* sb = gp(st.sbuf) + (size_t)a.parity * kMaxBlocks;
+  // sharded: the maxima over the whole cluster's feasible set, one all-gathered record per rank
+  const GAS BlkStat* sb = st.shard_stats ? gp(st.shard_stats) + (size_t)a.parity * kMaxRanks
+                                         : gp(st.sbuf) + (size_t)a.parity * kMaxBlocks;
+  if (st.shard_stats) stat_blocks = st.nranks;
   for (int b = threadIdx.x; b < stat_blocks; b += kBlock) {
     const BlkStat p = sb[b];
     maxT = max(maxT, p.max_taint);
@@ -1506,9 +1557,10 @@ __global__ __launch_bounds__(kBlock) void k_topo_resolve(const DevState* __restr
   const DevState& st = *stp;
   int lo, hi;
   chunk_of(st.N, lo, hi);
-  const Winner w = wave_winner(st.kbuf + (size_t)a.prev_parity * kMaxBlocks, a.prev_blocks);
+  int gidx;
+  const Winner w = prev_winner(st, a, &gidx);
   const kgpu_pod_query pq = *cp(st.queries + a.prev);
-  const int idx = settle_prev(st, a, pq, w);
+  const int idx = settle_prev(st, a, pq, w, gidx);
   if (idx >= lo && idx < hi && ((idx - lo) % kBlock) == (int)threadIdx.x) {
     NodeRes r = load_res(st, idx);
     assume_row(st, pq, r, idx);
@@ -1703,6 +1755,11 @@ int launch_final(const DevState* st, const PodArgs& a, int blocks, int stat_bloc
 int launch_resolve(const DevState* st, int N, const PodArgs& a, void* stream) {
   // same grid as the evaluation so that chunk ownership matches
   hipLaunchKernelGGL(k_resolve, dim3(eval_blocks(N)), dim3(kBlock), 0, (hipStream_t)stream, st, a);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_shard_pack(const DevState* st, int parity, int blocks, int what, void* stream) {
+  hipLaunchKernelGGL(k_shard_pack, dim3(1), dim3(kBlock), 0, (hipStream_t)stream, st, parity, blocks, what);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -17,6 +17,7 @@ import numpy as np
 from . import abi
 from . import api
 from .compile import CompileError, Compiler, Pools
+from . import native
 from .native import Engine
 
 REASON = {
@@ -41,11 +42,15 @@ class CycleResult:
 
 
 class GpuFramework:
-    def __init__(self, profile, nodes, existing=(), cluster=None, pods_hint=(), device=0, create_engine=True):
+    def __init__(self, profile, nodes, existing=(), cluster=None, pods_hint=(), device=0, create_engine=True,
+                 shard=None):
+        """shard=(rank, world): keep only this rank's contiguous slice of Snapshot.List() on the
+        device (native.shard_range); join the communicator with init_comm before scheduling."""
         self.profile = profile
         self.compiler = Compiler(profile, cluster)
         self.compiler.register(nodes, existing, pods_hint)
-        self.snap, self.arrays, self.order = self.compiler.compile_snapshot(nodes, existing)
+        self.shard = None if shard is None else native.shard_range(len(nodes), shard[1], shard[0])
+        self.snap, self.arrays, self.order = self.compiler.compile_snapshot(nodes, existing, shard=self.shard)
         self.config = self.compiler.config(device)
         self.nodes = {api.name_of(n): n for n in nodes}
         self.filters = [f for f in profile.filters if f in abi.FILTER_IDS]
@@ -54,6 +59,10 @@ class GpuFramework:
         if create_engine:
             self.engine = Engine(self.config)
             self.engine.upload(self.snap, self.arrays)
+
+    def init_comm(self, rank, world, uid):
+        """Node sharding over RCCL (kgpu_comm_init): uid from native.comm_unique_id() on rank 0."""
+        self.engine.comm_init(world, rank, uid)
 
     # ------------------------------------------------------------------ compile
     def compile_pods(self, pods):

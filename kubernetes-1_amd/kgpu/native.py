@@ -151,3 +151,24 @@ class Engine:
 
     def forget(self, slot):
         self._check(lib().kgpu_forget_pod(self.h, slot))
+
+    def comm_init(self, nranks, rank, uid):
+        """Join the node-sharding communicator (RCCL): this engine holds one contiguous shard of the
+        snapshot; every rank must then issue the same schedule calls with the same queries."""
+        buf = (C.c_uint8 * 128).from_buffer_copy(bytes(uid))
+        self._check(lib().kgpu_comm_init(self.h, nranks, rank, buf))
+
+
+def comm_unique_id():
+    """128-byte RCCL unique id (rank 0 creates it, the caller broadcasts it)."""
+    buf = (C.c_uint8 * 128)()
+    rc = lib().kgpu_comm_unique_id(buf)
+    if rc != 0:
+        raise KgpuError(rc, "kgpu_comm_unique_id failed")
+    return bytes(buf)
+
+
+def shard_range(n_nodes, world, rank):
+    """Contiguous shard of Snapshot.List() owned by `rank`: (node_base, count)."""
+    base = rank * n_nodes // world
+    return base, (rank + 1) * n_nodes // world - base
