@@ -166,6 +166,17 @@ def main():
                          "on a fresh snapshot, %.2fs at %d thread(s) (faster of 1 and %d); placements %s the GPU's"
                          % (S, tcpu, th, args.cpu_threads, "identical to" if ok else "DIFFERENT from")}
 
+    # HBM traffic of the dominant kernel per launch, from the committed rocprofv3 --pmc passes of
+    # this exact workload (profiles/r01_pmc_traffic.json, tools/gpu_pmc.sh); null when none exist
+    traffic = None
+    try:
+        with open(os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")) as fh:
+            pmc = json.load(fh).get("%s:%d:%d" % (args.config, n_local, launch_pods))
+        if pmc and pmc["kernel"] == ("k_batch" if persistent else "k_eval"):
+            traffic = pmc["traffic_bytes_per_launch"]
+    except (OSError, ValueError):
+        pass
+
     if rank == 0:
         line = {
             "metric": "pods scheduled/sec", "value": round(pods_per_s, 2), "unit": "pods/s", "n_gpus": world,
@@ -179,7 +190,7 @@ def main():
             "node_evals_per_s": round(pods_per_s * len(nodes), 1),
             "placed": placed,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                          "kernel": "k_batch" if persistent else ("k_topo_* pipeline" if topo else "k_eval"),
                          "bytes_per_node_eval": bpe,
                          "avg_kernel_us": round(per_pod_s * launch_pods * 1e6, 3), "pods_per_launch": launch_pods,
