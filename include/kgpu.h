@@ -393,6 +393,10 @@ int kgpu_read_nodes(kgpu_ctx* ctx, int64_t* req_cpu, int64_t* req_mem, int64_t* 
 /* KGPU_OPT_PHASE_TRACE (4): record per-pod phase timestamps of the persistent kernel (diagnostics;
  * read with kgpu_read_phase_trace). */
 #define KGPU_OPT_PHASE_TRACE 4
+/* KGPU_OPT_TOPO_FUSED (5): 1 = run a topology pod's six phases (histograms, critical-path minima,
+ * filters, scores, normalize + argmax, resolve + assume) in one cooperative launch with grid
+ * barriers; 0 (default) = one launch per phase, which measured faster on MI355X. */
+#define KGPU_OPT_TOPO_FUSED 5
 int kgpu_set_option(kgpu_ctx* ctx, int32_t option, int64_t value);
 /* Phase stamps of the last persistent run (100 MHz s_memrealtime ticks), 16 per pipeline
  * iteration (pods + 1): workgroup 0's {start, evaluated, previous pod resolved, published, end, 0,

@@ -44,6 +44,7 @@ struct kgpu_ctx {
   DevState st_batch{};  // its host source (kept alive for the async copy)
   bool timing = false;
   bool persistent = true;  // KGPU_OPT_PERSISTENT
+  bool topo_fused = false;  // KGPU_OPT_TOPO_FUSED (measured slower: DESIGN.md 4)
   int n_cus = 0;
   int max_groups = 0;  // KGPU_OPT_PERSIST_GROUPS (0 = n_cus)
   DevBuf gran;        // persistent-kernel granules + abort word
@@ -712,7 +713,7 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
       a.diag = diag ? 1 : 0;
       a.seq = first_seq + i;
       if (c->timing) HIP_OK(c, hipEventRecord(get_event(c, ev), c->stream));
-      if (kgpu::launch_topo(dst, a, blocks, min_values, next, c->stream))
+      if (kgpu::launch_topo(dst, a, blocks, min_values, next, c->topo_fused, c->stream))
         return fail(c, KGPU_E_DEVICE, "topology pipeline launch failed");
       if (c->timing) HIP_OK(c, hipEventRecord(get_event(c, ev + 1), c->stream));
       ev += 2;
@@ -978,6 +979,7 @@ int kgpu_set_option(kgpu_ctx* c, int32_t option, int64_t value) {
   else if (option == KGPU_OPT_PERSISTENT) c->persistent = value != 0;
   else if (option == KGPU_OPT_PERSIST_GROUPS) c->max_groups = (int)std::max<int64_t>(value, 0);
   else if (option == KGPU_OPT_PHASE_TRACE) c->phase_trace = value != 0;
+  else if (option == KGPU_OPT_TOPO_FUSED) c->topo_fused = value != 0;
   else return KGPU_E_INVAL;
   return KGPU_OK;
 }

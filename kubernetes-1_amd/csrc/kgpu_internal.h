@@ -254,8 +254,9 @@ int launch_batch(const DevState* st, const BatchArgs& a, int groups, int kidx, i
 // Topology pipeline for one pod (PodArgs.pod): domain histograms, critical-path minima, filters,
 // scores, normalize + argmax, resolve + assume.  next_scratch: words of the next topology pod's
 // scratch to zero in the resolve launch (0 none).
-int launch_topo(const DevState* st, const PodArgs& a, int blocks, int64_t min_values, int64_t next_scratch,
-                void* stream);
+// fused = one cooperative launch with grid barriers between the phases (default), else six launches.
+int launch_topo(const DevState* st, PodArgs a, int blocks, int64_t min_values, int64_t next_scratch,
+                bool fused, void* stream);
 // Initialize mcnt columns [c0, c0 + nc) from the pod table (n_pods rows).
 int launch_class_init(const DevState* st, int c0, int nc, int n_pods, void* stream);
 

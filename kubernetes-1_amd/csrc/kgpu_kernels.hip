@@ -29,7 +29,10 @@
 //   weights + sum framework.go:633-648, core/generic_scheduler.go:660-668
 //   selectHost core/generic_scheduler.go:217-238 (deterministic tie-break)
 //   assume   framework/v1alpha1/types.go:456-480 (NodeInfo.AddPod)
+#include <hip/hip_cooperative_groups.h>
 #include <hip/hip_runtime.h>
+
+namespace cg = cooperative_groups;
 
 #include "kgpu_internal.h"
 
@@ -1229,7 +1232,7 @@ __device__ uint32_t topo_filter(int f, const DevState& st, const QPlan& pl, int 
   return 0;
 }
 
-__global__ __launch_bounds__(kBlock) void k_topo_pre(const DevState* __restrict__ stp, PodArgs a) {
+__device__ __forceinline__ void topo_pre(const DevState* __restrict__ stp, PodArgs a) {
   const DevState& st = *stp;
   const QPlan& pl = st.plans[a.pod];
   const kgpu_pod_query q = *cp(st.queries + a.pod);
@@ -1306,7 +1309,7 @@ __global__ __launch_bounds__(kBlock) void k_topo_pre(const DevState* __restrict_
 
 // criticalPaths[0].MatchNum per DoNotSchedule constraint: minimum count over the registered pairs
 // of its key (MaxInt32 when none), grid-stride over the key's values.
-__global__ __launch_bounds__(kBlock) void k_topo_min(const DevState* __restrict__ stp, PodArgs a) {
+__device__ __forceinline__ void topo_min(const DevState* __restrict__ stp, PodArgs a) {
   const DevState& st = *stp;
   const QPlan& pl = st.plans[a.pod];
   TopoHdr* h = hdr(st);
@@ -1325,7 +1328,7 @@ __global__ __launch_bounds__(kBlock) void k_topo_min(const DevState* __restrict_
 }
 
 // Filters + the non-topology scores; the feasible set's ScheduleAnyway pairs and sizes.
-__global__ __launch_bounds__(kBlock) void k_topo_filter(const DevState* __restrict__ stp, PodArgs a) {
+__device__ __forceinline__ void topo_filter(const DevState* __restrict__ stp, PodArgs a) {
   const DevState& st = *stp;
   const QPlan& pl = st.plans[a.pod];
   const kgpu_pod_query q = *cp(st.queries + a.pod);
@@ -1382,7 +1385,7 @@ __global__ __launch_bounds__(kBlock) void k_topo_filter(const DevState* __restri
 
 // Raw PodTopologySpread (scoring.go:174-208), InterPodAffinity (scoring.go:217-236) and
 // DefaultPodTopologySpread (default_pod_topology_spread.go:75-106) scores of the feasible nodes.
-__global__ __launch_bounds__(kBlock) void k_topo_score(const DevState* __restrict__ stp, PodArgs a) {
+__device__ __forceinline__ void topo_score(const DevState* __restrict__ stp, PodArgs a) {
   const DevState& st = *stp;
   const QPlan& pl = st.plans[a.pod];
   TopoHdr* h = hdr(st);
@@ -1465,7 +1468,7 @@ __global__ __launch_bounds__(kBlock) void k_topo_score(const DevState* __restric
 }
 
 // NormalizeScore of every plugin (framework.go:613-648), total, packed-key argmax per workgroup.
-__global__ __launch_bounds__(kBlock) void k_topo_final(const DevState* __restrict__ stp, PodArgs a, int stat_blocks) {
+__device__ __forceinline__ void topo_final(const DevState* __restrict__ stp, PodArgs a, int stat_blocks) {
   const DevState& st = *stp;
   const QPlan& pl = st.plans[a.pod];
   const TopoHdr* h = hdr(st);
@@ -1552,7 +1555,7 @@ __global__ __launch_bounds__(kBlock) void k_topo_final(const DevState* __restric
 }
 
 // selectHost + assume of the topology pod, then zero the next topology pod's scratch.
-__global__ __launch_bounds__(kBlock) void k_topo_resolve(const DevState* __restrict__ stp, PodArgs a,
+__device__ __forceinline__ void topo_resolve(const DevState* __restrict__ stp, PodArgs a,
                                                          int64_t next_scratch) {
   const DevState& st = *stp;
   int lo, hi;
@@ -1568,6 +1571,43 @@ __global__ __launch_bounds__(kBlock) void k_topo_resolve(const DevState* __restr
   }
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < next_scratch; i += (int64_t)gridDim.x * kBlock)
     st.scratch[i] = 0;
+}
+
+__global__ __launch_bounds__(kBlock) void k_topo_pre(const DevState* __restrict__ stp, PodArgs a) { topo_pre(stp, a); }
+__global__ __launch_bounds__(kBlock) void k_topo_min(const DevState* __restrict__ stp, PodArgs a) { topo_min(stp, a); }
+__global__ __launch_bounds__(kBlock) void k_topo_filter(const DevState* __restrict__ stp, PodArgs a) { topo_filter(stp, a); }
+__global__ __launch_bounds__(kBlock) void k_topo_score(const DevState* __restrict__ stp, PodArgs a) { topo_score(stp, a); }
+__global__ __launch_bounds__(kBlock) void k_topo_final(const DevState* __restrict__ stp, PodArgs a, int stat_blocks) { topo_final(stp, a, stat_blocks); }
+__global__ __launch_bounds__(kBlock) void k_topo_resolve(const DevState* __restrict__ stp, PodArgs a,
+                                                         int64_t next_scratch) {
+  topo_resolve(stp, a, next_scratch);
+}
+
+// The whole per-pod topology pipeline in ONE cooperative launch: the six phases above separated
+// by grid-wide barriers instead of kernel boundaries (the grid is <= kMaxBlocks one-wave
+// workgroups, co-resident by construction of hipLaunchCooperativeKernel).  The barrier's
+// agent-scope release/acquire makes each phase's histogram atomics, header words and
+// per-workgroup partials visible to the next phase on every XCD.
+__global__ __launch_bounds__(kBlock) void k_topo_fused(const DevState* __restrict__ stp, PodArgs a, int do_min,
+                                                       int64_t next_scratch) {
+  cg::grid_group grid = cg::this_grid();
+  topo_pre(stp, a);
+  grid.sync();
+  if (do_min) {
+    topo_min(stp, a);
+    grid.sync();
+  }
+  topo_filter(stp, a);
+  grid.sync();
+  topo_score(stp, a);
+  grid.sync();
+  topo_final(stp, a, (int)gridDim.x);
+  grid.sync();
+  PodArgs r = a;
+  r.prev = a.pod;
+  r.prev_blocks = (int)gridDim.x;
+  r.prev_parity = a.parity;
+  topo_resolve(stp, r, next_scratch);
 }
 
 // Pod class membership of the pod-table rows (labels.Selector.Matches, selector.go:198-242;
@@ -1610,9 +1650,15 @@ __global__ void k_class_init(const DevState* __restrict__ stp, int c0, int nc, i
   }
 }
 
-int launch_topo(const DevState* st, const PodArgs& a, int blocks, int64_t min_values, int64_t next_scratch,
-                void* stream) {
+int launch_topo(const DevState* st, PodArgs a, int blocks, int64_t min_values, int64_t next_scratch,
+                bool fused, void* stream) {
   hipStream_t s = (hipStream_t)stream;
+  if (fused) {
+    int do_min = min_values > 0 ? 1 : 0;
+    void* args[] = {(void*)&st, (void*)&a, (void*)&do_min, (void*)&next_scratch};
+    return hipLaunchCooperativeKernel((const void*)k_topo_fused, dim3(blocks), dim3(kBlock), args, 0, s) == hipSuccess
+               ? 0 : -1;
+  }
   hipLaunchKernelGGL(k_topo_pre, dim3(blocks), dim3(kBlock), 0, s, st, a);
   if (min_values > 0) {
     int64_t mb = (min_values + kBlock - 1) / kBlock;

@@ -8,7 +8,7 @@ OK, E_INVAL, E_NOMEM, E_DEVICE, E_CAPACITY, E_STATE, E_UNSUPPORTED = 0, -1, -2, 
 ERRNAMES = {0: "OK", -1: "KGPU_E_INVAL", -2: "KGPU_E_NOMEM", -3: "KGPU_E_DEVICE", -4: "KGPU_E_CAPACITY",
             -5: "KGPU_E_STATE", -6: "KGPU_E_UNSUPPORTED"}
 
-OPT_KERNEL_TIMING, OPT_PERSISTENT, OPT_PERSIST_GROUPS, OPT_PHASE_TRACE = 1, 2, 3, 4
+OPT_KERNEL_TIMING, OPT_PERSISTENT, OPT_PERSIST_GROUPS, OPT_PHASE_TRACE, OPT_TOPO_FUSED = 1, 2, 3, 4, 5
 CODE_SUCCESS, CODE_ERROR, CODE_UNSCHEDULABLE, CODE_UNRESOLVABLE = 0, 1, 2, 3
 
 F_NODE_UNSCHEDULABLE, F_FIT, F_NODE_NAME, F_NODE_PORTS, F_NODE_AFFINITY, F_TAINT, F_PTS, F_IPA = range(8)

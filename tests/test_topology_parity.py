@@ -118,3 +118,29 @@ def test_compile_order_independent(hint):
     got = [(None, 0, None) if r["node"] == -1 else (fw.order[r["node"]], int(r["feasible"]),
                                                     int(r["score"]) if r["scored"] else None) for r in res]
     _cmp(want, got)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", ["c", "d"])
+@pytest.mark.parametrize("fused", [1, 0])
+def test_gpu_topology_multiblock_fused_and_unfused(cfg, fused):
+    # 3000 nodes = 47 one-wave workgroups: the fused kernel's grid barriers order phases across
+    # workgroups (and XCDs); the six-launch variant is the reference schedule of the same phases
+    from kgpu import abi, cluster
+    from oracle.cref import RefEngine
+    if cfg == "c":
+        nodes, ex, pods, prof = cluster.taints_affinity_spread(n_nodes=3000, n_pods=120)
+    else:
+        nodes, ex, pods, prof = cluster.pod_affinity(n_nodes=3000, n_existing=3000, n_pods=96)
+    fw = GpuFramework(prof, nodes, ex, pods_hint=pods)
+    q, pc, _, errs = fw.compile_pods(pods)
+    assert not errs
+    ref = RefEngine(fw.config, fw.snap, threads=4)
+    want = ref.schedule(q, pc)
+    fw.engine.set_option(abi.OPT_TOPO_FUSED, fused)
+    got, _ = fw.engine.schedule_batch(q, pc)
+    for f in ("node", "feasible", "scored", "score"):
+        np.testing.assert_array_equal(want[f], got[f], err_msg=f)
+    rows, rows_c = fw.engine.read_nodes(fw.snap.n_nodes), ref.read_nodes()
+    for k in rows:
+        np.testing.assert_array_equal(rows[k], rows_c[k], err_msg=k)
