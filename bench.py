@@ -172,7 +172,7 @@ def main():
     try:
         with open(os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")) as fh:
             pmc = json.load(fh).get("%s:%d:%d" % (args.config, n_local, launch_pods))
-        if pmc and pmc["kernel"] == ("k_batch" if persistent else "k_eval"):
+        if pmc and pmc["kernel"] == ("k_batch" if persistent else ("k_topo_* pipeline" if topo else "k_eval")):
             traffic = pmc["traffic_bytes_per_launch"]
     except (OSError, ValueError):
         pass
