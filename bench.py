@@ -55,6 +55,7 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=400, help="pods timed for the CPU baseline (0: skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-persistent", action="store_true", help="one evaluation launch per pod")
+    ap.add_argument("--topo-fused", type=int, default=None, help="KGPU_OPT_TOPO_FUSED (default: the library's)")
     ap.add_argument("--shard", action="store_true",
                     help="at N=1: run the node-sharded path on a one-rank RCCL communicator (exchange overhead)")
     args = ap.parse_args()
@@ -97,6 +98,8 @@ def main():
     eng = fw.engine
     if args.no_persistent:
         eng.set_option(abi.OPT_PERSISTENT, 0)
+    if args.topo_fused is not None:
+        eng.set_option(abi.OPT_TOPO_FUSED, args.topo_fused)
 
     def reset():
         eng.upload(fw.snap, fw.arrays)

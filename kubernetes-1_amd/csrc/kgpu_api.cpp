@@ -45,6 +45,8 @@ struct kgpu_ctx {
   bool timing = false;
   bool persistent = true;  // KGPU_OPT_PERSISTENT
   bool topo_fused = false;  // KGPU_OPT_TOPO_FUSED (measured slower: DESIGN.md 4)
+  DevBuf gbar;              // fused topology kernel: grid-barrier arrival counter
+  unsigned long long bar_base = 0;
   int n_cus = 0;
   int max_groups = 0;  // KGPU_OPT_PERSIST_GROUPS (0 = n_cus)
   DevBuf gran;        // persistent-kernel granules + abort word
@@ -713,8 +715,15 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
       a.diag = diag ? 1 : 0;
       a.seq = first_seq + i;
       if (c->timing) HIP_OK(c, hipEventRecord(get_event(c, ev), c->stream));
-      if (kgpu::launch_topo(dst, a, blocks, min_values, next, c->topo_fused, c->stream))
+      if (c->topo_fused && !c->gbar.p) {
+        if ((rc = ensure(c, c->gbar, 64))) return rc;
+        HIP_OK(c, hipMemsetAsync(c->gbar.p, 0, 64, c->stream));
+        c->bar_base = 0;
+      }
+      if (kgpu::launch_topo(dst, a, blocks, min_values, next, c->topo_fused,
+                            static_cast<unsigned long long*>(c->gbar.p), c->bar_base, c->stream))
         return fail(c, KGPU_E_DEVICE, "topology pipeline launch failed");
+      if (c->topo_fused) c->bar_base += (unsigned long long)kgpu::topo_barriers(min_values) * (unsigned long long)blocks;
       if (c->timing) HIP_OK(c, hipEventRecord(get_event(c, ev + 1), c->stream));
       ev += 2;
       ++timed_passes;
@@ -950,7 +959,7 @@ int kgpu_destroy(kgpu_ctx* c) {
   for (DevBuf* b : {&c->dstate, &c->queries, &c->reqs, &c->ints, &c->words, &c->node_terms, &c->pref_terms, &c->spreads,
                     &c->pod_terms, &c->scalars, &c->ports, &c->results, &c->gran, &c->trace, &c->d_classes,
                     &c->d_citems, &c->d_tclasses, &c->d_creqs, &c->d_cints, &c->d_plans, &c->d_aux,
-                    &c->d_aux_terms, &c->scratch, &c->d_pods})
+                    &c->d_aux_terms, &c->scratch, &c->d_pods, &c->gbar})
     if (b->p) (void)hipFree(b->p);
   if (c->st.mcnt) (void)hipFree(c->st.mcnt);
   if (c->st.tcnt) (void)hipFree(c->st.tcnt);

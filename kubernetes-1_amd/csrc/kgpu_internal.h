@@ -255,8 +255,11 @@ int launch_batch(const DevState* st, const BatchArgs& a, int groups, int kidx, i
 // scores, normalize + argmax, resolve + assume.  next_scratch: words of the next topology pod's
 // scratch to zero in the resolve launch (0 none).
 // fused = one cooperative launch with grid barriers between the phases (default), else six launches.
+// bar: the fused kernel's grid-barrier counter (grows monotonically); bar_base: its value before
+// this launch.  A fused launch adds topo_barriers(min_values) * blocks arrivals.
 int launch_topo(const DevState* st, PodArgs a, int blocks, int64_t min_values, int64_t next_scratch,
-                bool fused, void* stream);
+                bool fused, unsigned long long* bar, unsigned long long bar_base, void* stream);
+inline int topo_barriers(int64_t min_values) { return min_values > 0 ? 5 : 4; }
 // Initialize mcnt columns [c0, c0 + nc) from the pod table (n_pods rows).
 int launch_class_init(const DevState* st, int c0, int nc, int n_pods, void* stream);
 

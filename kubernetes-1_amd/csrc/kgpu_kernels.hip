@@ -29,10 +29,7 @@
 //   weights + sum framework.go:633-648, core/generic_scheduler.go:660-668
 //   selectHost core/generic_scheduler.go:217-238 (deterministic tie-break)
 //   assume   framework/v1alpha1/types.go:456-480 (NodeInfo.AddPod)
-#include <hip/hip_cooperative_groups.h>
 #include <hip/hip_runtime.h>
-
-namespace cg = cooperative_groups;
 
 #include "kgpu_internal.h"
 
@@ -1585,24 +1582,38 @@ __global__ __launch_bounds__(kBlock) void k_topo_resolve(const DevState* __restr
 
 // The whole per-pod topology pipeline in ONE cooperative launch: the six phases above separated
 // by grid-wide barriers instead of kernel boundaries (the grid is <= kMaxBlocks one-wave
-// workgroups, co-resident by construction of hipLaunchCooperativeKernel).  The barrier's
-// agent-scope release/acquire makes each phase's histogram atomics, header words and
-// per-workgroup partials visible to the next phase on every XCD.
+// workgroups; hipLaunchCooperativeKernel refuses a grid that cannot be co-resident).
+// Grid barrier on a counter that only ever grows: the host passes the number of arrivals before
+// this launch (`base`), so barrier i of the launch waits for base + i * gridDim.x.  Agent-scope
+// fences publish / acquire the phase's writes across XCDs; the polling load is an agent-scope
+// atomic, so it is served coherently and never from a stale cache line.
+__device__ __forceinline__ void grid_barrier(unsigned long long* ctr, unsigned long long target) {
+  __threadfence();
+  if (threadIdx.x == 0) {
+    __hip_atomic_fetch_add(ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) __builtin_amdgcn_s_sleep(1);
+  }
+  __syncthreads();
+  __threadfence();
+}
+
 __global__ __launch_bounds__(kBlock) void k_topo_fused(const DevState* __restrict__ stp, PodArgs a, int do_min,
-                                                       int64_t next_scratch) {
-  cg::grid_group grid = cg::this_grid();
+                                                       int64_t next_scratch, unsigned long long* bar,
+                                                       unsigned long long base) {
+  const unsigned long long g = gridDim.x;
+  unsigned long long t = base;
   topo_pre(stp, a);
-  grid.sync();
+  grid_barrier(bar, t += g);
   if (do_min) {
     topo_min(stp, a);
-    grid.sync();
+    grid_barrier(bar, t += g);
   }
   topo_filter(stp, a);
-  grid.sync();
+  grid_barrier(bar, t += g);
   topo_score(stp, a);
-  grid.sync();
+  grid_barrier(bar, t += g);
   topo_final(stp, a, (int)gridDim.x);
-  grid.sync();
+  grid_barrier(bar, t += g);
   PodArgs r = a;
   r.prev = a.pod;
   r.prev_blocks = (int)gridDim.x;
@@ -1651,11 +1662,11 @@ __global__ void k_class_init(const DevState* __restrict__ stp, int c0, int nc, i
 }
 
 int launch_topo(const DevState* st, PodArgs a, int blocks, int64_t min_values, int64_t next_scratch,
-                bool fused, void* stream) {
+                bool fused, unsigned long long* bar, unsigned long long bar_base, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (fused) {
     int do_min = min_values > 0 ? 1 : 0;
-    void* args[] = {(void*)&st, (void*)&a, (void*)&do_min, (void*)&next_scratch};
+    void* args[] = {(void*)&st, (void*)&a, (void*)&do_min, (void*)&next_scratch, (void*)&bar, (void*)&bar_base};
     return hipLaunchCooperativeKernel((const void*)k_topo_fused, dim3(blocks), dim3(kBlock), args, 0, s) == hipSuccess
                ? 0 : -1;
   }
