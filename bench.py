@@ -52,7 +52,8 @@ def main():
     ap.add_argument("--config", default="b")
     ap.add_argument("--nodes", type=int, default=5000)
     ap.add_argument("--pods-per-step", type=int, default=1000)
-    ap.add_argument("--cpu-sample", type=int, default=400, help="pods timed for the CPU baseline (0: skip)")
+    ap.add_argument("--cpu-sample", type=int, default=-1,
+                    help="pods timed for the CPU baseline (-1: the whole workload, 0: skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-persistent", action="store_true", help="one evaluation launch per pod")
     ap.add_argument("--topo-fused", type=int, default=None, help="KGPU_OPT_TOPO_FUSED (default: the library's)")
@@ -150,9 +151,9 @@ def main():
     # reference's structure (16 workers, chunk = min(sqrt(n), n/16+1)) and a single thread are
     # timed; the faster one is reported (the stronger baseline).
     cpu = None
-    if rank == 0 and world == 1 and args.cpu_sample > 0:
+    if rank == 0 and world == 1 and args.cpu_sample != 0:
         from oracle.cref import RefEngine
-        S = min(args.cpu_sample, n_pods)
+        S = n_pods if args.cpu_sample < 0 else min(args.cpu_sample, n_pods)
         best = None
         for th in sorted({1, args.cpu_threads}):
             ref = RefEngine(fw.config, fw.snap, threads=th)
@@ -165,7 +166,7 @@ def main():
                 best = (S / tcpu, th, tcpu, ok)
         rate, th, tcpu, ok = best
         cpu = {"value": round(rate, 2), "unit": "pods/s", "cores": th, "kind": "port",
-               "sample": "C restatement (oracle/c) of the reference algorithm, first %d pods of the same workload "
+               "sample": "C restatement (oracle/c) of the reference algorithm, the first %d pods of the same workload "
                          "on a fresh snapshot, %.2fs at %d thread(s) (faster of 1 and %d); placements %s the GPU's"
                          % (S, tcpu, th, args.cpu_threads, "identical to" if ok else "DIFFERENT from")}
 
