@@ -30,17 +30,42 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def host_info():
+    """Host cores and CPU model for the cpu_baseline record (SURVEY.md 8(d) 'report nproc, CPU model')."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    # the GPU box shares its host among GPUs: OMP_NUM_THREADS states this job's CPU share there
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return {"nproc": os.cpu_count() or 1, "affinity_cpus": min(aff, share) if share > 0 else aff, "cpu_model": model}
+
+
 def make_workload(cfg, n_nodes, n_pods):
     from kgpu import cluster
+    """(nodes, existing pods, init pods, measured pods, profile).  Init pods (config a: the
+    scheduler_perf initPods, performance-config.yaml:1-13) are scheduled before the timed region."""
     if cfg == "b":
-        return cluster.fit_least_balanced(n_nodes=n_nodes, n_pods=n_pods)
+        nodes, ex, pods, prof = cluster.fit_least_balanced(n_nodes=n_nodes, n_pods=n_pods)
+        return nodes, ex, [], pods, prof
     if cfg == "a":
         nodes, init, pods, prof = cluster.scheduling_basic(n_nodes=n_nodes, n_init=n_nodes, n_pods=n_pods)
-        return nodes, [], init + pods, prof
+        return nodes, [], init, pods, prof
     if cfg == "c":
-        return cluster.taints_affinity_spread(n_nodes=n_nodes, n_pods=n_pods)
+        nodes, ex, pods, prof = cluster.taints_affinity_spread(n_nodes=n_nodes, n_pods=n_pods)
+        return nodes, ex, [], pods, prof
     if cfg == "d":
-        return cluster.pod_affinity(n_nodes=n_nodes, n_existing=n_nodes, n_pods=n_pods)
+        nodes, ex, pods, prof = cluster.pod_affinity(n_nodes=n_nodes, n_existing=n_nodes, n_pods=n_pods)
+        return nodes, ex, [], pods, prof
     raise SystemExit("config %r not benchmarked yet" % cfg)
 
 
@@ -55,6 +80,7 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=-1,
                     help="pods timed for the CPU baseline (-1: the whole workload, 0: skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--latency-pods", type=int, default=200, help="pods timed one at a time through kgpu_schedule_one")
     ap.add_argument("--no-persistent", action="store_true", help="one evaluation launch per pod")
     ap.add_argument("--topo-fused", type=int, default=None, help="KGPU_OPT_TOPO_FUSED (default: the library's)")
     ap.add_argument("--shard", action="store_true",
@@ -82,9 +108,9 @@ def main():
     # --nodes-sized contiguous shard of Snapshot.List() (weak scaling in nodes: the cluster grows
     # with N), and every pod's shard winners are all-gathered over RCCL.
     n_cluster = args.nodes * world
-    nodes, existing, pods, prof = make_workload(args.config, n_cluster, n_pods)
+    nodes, existing, init, pods, prof = make_workload(args.config, n_cluster, n_pods)
     sharded = dist_on or args.shard
-    fw = GpuFramework(prof, nodes, existing, pods_hint=pods[:16], device=local,
+    fw = GpuFramework(prof, nodes, existing, pods_hint=init[:16] + pods[:16], device=local,
                       shard=(rank, world) if sharded else None)
     if sharded:
         from kgpu import native
@@ -92,8 +118,9 @@ def main():
         if dist_on:
             dist.broadcast_object_list(uid, src=0)
         fw.init_comm(rank, world, uid[0])
-    q, pc, pnp, errs = fw.compile_pods(pods)
+    q_all, pc, pnp, errs = fw.compile_pods(init + pods)
     assert not errs, errs
+    q_init, q = q_all[:len(init)], q_all[len(init):]
     log("workload: %d nodes (%d on this rank), %d pods, compiled in %.1fs"
         % (len(nodes), fw.snap.n_nodes, len(pods), time.time() - t_gen))
     eng = fw.engine
@@ -104,10 +131,13 @@ def main():
 
     def reset():
         eng.upload(fw.snap, fw.arrays)
+        if len(q_init):
+            eng.schedule_batch(q_init, pc, first_seq=0)   # untimed: the cluster's initial state
 
     # warmup (first launches, code object load) on a fresh snapshot, then reset the cluster state
+    reset()
     for w in range(W):
-        eng.schedule_batch(q[:B], pc, first_seq=0)
+        eng.schedule_batch(q[:B], pc, first_seq=len(q_init))
     reset()
     torch.cuda.synchronize()
     if dist_on:
@@ -116,7 +146,7 @@ def main():
     t0 = time.perf_counter()
     results = []
     for k in range(K):
-        res, stats = eng.schedule_batch(q[k * B:(k + 1) * B], pc, first_seq=k * B, stats=stats)
+        res, stats = eng.schedule_batch(q[k * B:(k + 1) * B], pc, first_seq=len(q_init) + k * B, stats=stats)
         results.append(res)
     torch.cuda.synchronize()
     if dist_on:
@@ -134,8 +164,22 @@ def main():
     reset()
     eng.set_option(abi.OPT_KERNEL_TIMING, 1)
     kst = abi.Stats()
-    _, kst = eng.schedule_batch(q[:B], pc, first_seq=0, stats=kst)
+    _, kst = eng.schedule_batch(q[:B], pc, first_seq=len(q_init), stats=kst)
     eng.set_option(abi.OPT_KERNEL_TIMING, 0)
+    # per-pod latency of the drop-in step: kgpu_schedule_one (one cycle with assume and the per-node
+    # filter / score diagnostics the Go shim's Filter/Score lookups read), wall clock per call
+    lat = []
+    if args.latency_pods > 0:
+        reset()
+        for i in range(min(args.latency_pods, len(q))):
+            t1 = time.perf_counter()
+            eng.schedule_one(q[i], pc, seq=len(q_init) + i, assume=True)
+            lat.append((time.perf_counter() - t1) * 1e6)
+    lat_rec = None
+    if lat:
+        la = np.array(lat)
+        lat_rec = {"call": "kgpu_schedule_one", "pods": len(lat), "p50_us": round(float(np.percentile(la, 50)), 2),
+                   "p99_us": round(float(np.percentile(la, 99)), 2), "mean_us": round(float(la.mean()), 2)}
     # eval_launches counts node-evaluation passes (one per pod); with the persistent kernel one
     # launch covers the whole batch, so the per-launch duration is kernel_ms / launches_made
     per_pod_s = kst.eval_kernel_ms / 1e3 / max(kst.eval_launches, 1)
@@ -147,28 +191,38 @@ def main():
     persistent = not args.no_persistent and not topo and not sharded
     launch_pods = B if persistent else 1
 
-    # CPU baseline: the C restatement of the reference algorithm on this host's cores.  Both the
-    # reference's structure (16 workers, chunk = min(sqrt(n), n/16+1)) and a single thread are
-    # timed; the faster one is reported (the stronger baseline).
+    # CPU baseline: the C restatement of the reference algorithm on this host's cores.  Three
+    # worker counts are timed -- 1, the reference's parallelism (16 goroutines,
+    # internal/parallelize/parallelism.go:26), and every core this process may run on -- and the
+    # fastest is reported (the strongest baseline); each one's rate is listed beside it.
     cpu = None
     if rank == 0 and world == 1 and args.cpu_sample != 0:
         from oracle.cref import RefEngine
         S = n_pods if args.cpu_sample < 0 else min(args.cpu_sample, n_pods)
+        host = host_info()
+        rates = {}
         best = None
-        for th in sorted({1, args.cpu_threads}):
+        for th in sorted({1, args.cpu_threads, host["affinity_cpus"]}):
             ref = RefEngine(fw.config, fw.snap, threads=th)
+            if len(q_init):
+                ref.schedule(q_init, pc)   # untimed, like the GPU's
             tc = time.perf_counter()
-            rres = ref.schedule(q[:S], pc)
+            rres = ref.schedule(q[:S], pc, first_seq=len(q_init))
             tcpu = time.perf_counter() - tc
+            ref.close()
             ok = bool(np.array_equal(rres["node"], res_all["node"][:S]))
+            rates[str(th)] = round(S / tcpu, 2)
             log("cpu baseline: %d thread(s): %.1f pods/s (placements %s)" % (th, S / tcpu, "match" if ok else "DIFFER"))
             if best is None or S / tcpu > best[0]:
                 best = (S / tcpu, th, tcpu, ok)
         rate, th, tcpu, ok = best
         cpu = {"value": round(rate, 2), "unit": "pods/s", "cores": th, "kind": "port",
-               "sample": "C restatement (oracle/c) of the reference algorithm, the first %d pods of the same workload "
-                         "on a fresh snapshot, %.2fs at %d thread(s) (faster of 1 and %d); placements %s the GPU's"
-                         % (S, tcpu, th, args.cpu_threads, "identical to" if ok else "DIFFERENT from")}
+               "nproc": host["nproc"], "affinity_cpus": host["affinity_cpus"], "cpu_model": host["cpu_model"],
+               "rates_by_threads": rates,
+               "sample": "C restatement (oracle/c) of the reference algorithm over %s (%d pods) of the same workload "
+                         "on a fresh snapshot, %.2fs at %d thread(s) (fastest of %s workers); placements %s the GPU's"
+                         % ("the whole workload" if S == n_pods else "the first %d pods" % S, S, tcpu, th,
+                            "/".join(sorted(rates, key=int)), "identical to" if ok else "DIFFERENT from")}
 
     # HBM traffic of the dominant kernel per launch, from the committed rocprofv3 --pmc passes of
     # this exact workload (profiles/r01_pmc_traffic.json, tools/gpu_pmc.sh); null when none exist
@@ -201,6 +255,7 @@ def main():
                          "us_per_pod": round(per_pod_s * 1e6, 4),
                          "bytes_per_launch": pod_bytes * launch_pods},
             "cpu_baseline": cpu,
+            "latency": lat_rec,
         }
         print(json.dumps(line), flush=True)
     if dist_on:

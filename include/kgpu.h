@@ -84,6 +84,10 @@ extern "C" {
  *              bit3 ephemeral-storage, bit4+s scalar request s); InterPodAffinity rule
  *              (1 affinity, 2 anti-affinity, 3 existing pods' anti-affinity) */
 #define KGPU_FS_FEASIBLE 0u
+/* percentageOfNodesToScore < 100: a node findNodesThatPassFilters never examined, or the feasible
+ * node whose discovery cancelled the search (generic_scheduler.go:451-471): in neither `filtered`
+ * nor the statuses map */
+#define KGPU_FS_NOT_EVALUATED 0xFFu
 
 /* ---- selector requirement operators (labels/selector.go:198-242) */
 #define KGPU_OP_IN 0
@@ -263,7 +267,9 @@ typedef struct kgpu_config {
   int32_t n_most;
   kgpu_resource_weight most[8];             /* NodeResourcesMostAllocatedArgs.Resources */
   int32_t hard_pod_affinity_weight;         /* InterPodAffinityArgs (v1beta1/defaults.go:165-167) */
-  int32_t percentage_of_nodes_to_score;     /* 100 in every BASELINE config */
+  int32_t percentage_of_nodes_to_score;     /* 0 = adaptive (the reference default), 1-100; 100 in every
+                                               BASELINE config.  < 100: numFeasibleNodesToFind +
+                                               nextStartNodeIndex (generic_scheduler.go:379-495) */
   int32_t tie_break_mode;                   /* 0 hashed rank, 1 first maximum in snapshot order */
   int32_t pad0;
   uint64_t seed;                            /* tie-break seed */
@@ -333,7 +339,7 @@ typedef struct kgpu_snapshot {
 typedef struct kgpu_result {
   int32_t node;        /* chosen node (global index), -1 = FitError (no feasible node) */
   int32_t feasible;    /* ScheduleResult.FeasibleNodes */
-  int32_t evaluated;   /* ScheduleResult.EvaluatedNodes */
+  int32_t evaluated;   /* ScheduleResult.EvaluatedNodes = len(filtered) + len(statuses) */
   int32_t scored;      /* 0 when prioritizeNodes was skipped (generic_scheduler.go:184-191) */
   int64_t score;       /* total weighted score of the chosen node */
 } kgpu_result;

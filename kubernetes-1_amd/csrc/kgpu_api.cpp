@@ -95,6 +95,8 @@ struct kgpu_ctx {
   ncclComm_t comm = nullptr;
   int32_t nranks = 1, rank = 0;
   DevBuf shard;   // send key | send stat | keys [2][kMaxRanks] | stats [2][kMaxRanks]
+  DevBuf cut_buf;  // DevState::cut_state (nextStartNodeIndex, last EvaluatedNodes)
+  bool cut_init = false;
 };
 
 namespace {
@@ -579,6 +581,20 @@ double go_log(double x) {
   return k * ln2hi - ((hfsq - (s * (hfsq + R) + k * ln2lo)) - f);
 }
 
+// numFeasibleNodesToFind (generic_scheduler.go:379-399): minFeasibleNodesToFind = 100,
+// minFeasibleNodesPercentageToFind = 5, adaptive 50 - N/125 when the percentage is 0 (the default,
+// apis/config/types.go:251).
+int32_t num_feasible_nodes_to_find(int32_t n, int32_t pct) {
+  if (n < 100 || pct >= 100) return n;
+  int32_t adaptive = pct;
+  if (adaptive <= 0) {
+    adaptive = 50 - n / 125;
+    if (adaptive < 5) adaptive = 5;
+  }
+  const int32_t k = (int32_t)((int64_t)n * adaptive / 100);
+  return k < 100 ? 100 : k;
+}
+
 hipEvent_t get_event(kgpu_ctx* c, size_t i) {
   while (c->ev_pool.size() <= i) {
     hipEvent_t e;
@@ -670,7 +686,11 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
   // Persistent geometry: one workgroup per CU at most, K node rows per lane in registers.
   int per = 0, groups = 0;
   const bool sharded = c->comm != nullptr;
-  const int kidx = (c->persistent && !diag && !sharded) ? kgpu::batch_geometry(st.N, std::min(c->max_groups > 0 ? std::min(c->max_groups, c->n_cus) : c->n_cus, 256), &per, &groups) : -1;
+  const bool cut = c->st.cut_state != nullptr;  // percentageOfNodesToScore trims the feasible set
+  if (cut && sharded)
+    return fail(c, KGPU_E_UNSUPPORTED, "percentageOfNodesToScore < 100 on a node-sharded engine (nextStartNodeIndex "
+                                       "rotates over the whole cluster): use 100 when sharding");
+  const int kidx = (c->persistent && !diag && !sharded && !cut) ? kgpu::batch_geometry(st.N, std::min(c->max_groups > 0 ? std::min(c->max_groups, c->n_cus) : c->n_cus, 256), &per, &groups) : -1;
   std::vector<uint8_t> norm((size_t)n), topo((size_t)n, 0);
   // pods that need the normalize pass or whose scoring fails take the one-launch-per-pod path;
   // pods with topology state take the topology pipeline
@@ -713,6 +733,7 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
       a.norm = 1;
       a.assume = assume;
       a.diag = diag ? 1 : 0;
+      a.cut = cut ? 1 : 0;
       a.seq = first_seq + i;
       if (c->timing) HIP_OK(c, hipEventRecord(get_event(c, ev), c->stream));
       if (c->topo_fused && !c->gbar.p) {
@@ -721,9 +742,9 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
         c->bar_base = 0;
       }
       if (kgpu::launch_topo(dst, a, blocks, min_values, next, c->topo_fused,
-                            static_cast<unsigned long long*>(c->gbar.p), c->bar_base, c->stream))
+                            static_cast<unsigned long long*>(c->gbar.p), c->bar_base, c->cfg.n_filters, c->stream))
         return fail(c, KGPU_E_DEVICE, "topology pipeline launch failed");
-      if (c->topo_fused) c->bar_base += (unsigned long long)kgpu::topo_barriers(min_values) * (unsigned long long)blocks;
+      if (c->topo_fused && !cut) c->bar_base += (unsigned long long)kgpu::topo_barriers(min_values) * (unsigned long long)blocks;
       if (c->timing) HIP_OK(c, hipEventRecord(get_event(c, ev + 1), c->stream));
       ev += 2;
       ++timed_passes;
@@ -777,13 +798,16 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
         a.prev_blocks = blocks;
         a.prev_parity = (k - 1) & 1;
         a.parity = k & 1;
-        a.norm = (diag || needs_norm(c, qs[k], pools)) ? 1 : 0;
+        a.norm = (diag || cut || needs_norm(c, qs[k], pools)) ? 1 : 0;
         a.assume = assume;
         a.diag = diag ? 1 : 0;
+        a.cut = cut ? 1 : 0;
         a.seq = first_seq + k;
         if (c->timing) HIP_OK(c, hipEventRecord(get_event(c, ev), c->stream));
         if (kgpu::launch_eval(dst, a, blocks, c->spec, c->stream))
           return fail(c, KGPU_E_DEVICE, "k_eval launch failed");
+        if (cut && kgpu::launch_cut(dst, a, blocks, c->cfg.n_filters, c->stream))
+          return fail(c, KGPU_E_DEVICE, "k_cut launch failed");
         if (c->timing) HIP_OK(c, hipEventRecord(get_event(c, ev + 1), c->stream));
         ev += 2;
         ++timed_passes;
@@ -799,6 +823,7 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
       r.prev_blocks = blocks;
       r.prev_parity = prev & 1;
       r.assume = assume;
+      r.cut = cut ? 1 : 0;
       if (kgpu::launch_resolve(dst, st.N, r, c->stream)) return fail(c, KGPU_E_DEVICE, "k_resolve launch failed");
     }
     i = j;
@@ -902,7 +927,7 @@ int kgpu_create(const kgpu_config* cfg, kgpu_ctx** out) {
     for (int j = 0; j < i; ++j)
       if (cfg->filters[j] == cfg->filters[i]) return KGPU_E_INVAL;
   }
-  if (cfg->percentage_of_nodes_to_score > 0 && cfg->percentage_of_nodes_to_score < 100) return KGPU_E_UNSUPPORTED;
+  if (cfg->percentage_of_nodes_to_score < 0 || cfg->percentage_of_nodes_to_score > 100) return KGPU_E_INVAL;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return KGPU_E_DEVICE;
   if (cfg->device < 0 || cfg->device >= ndev) return KGPU_E_INVAL;
@@ -959,7 +984,7 @@ int kgpu_destroy(kgpu_ctx* c) {
   for (DevBuf* b : {&c->dstate, &c->queries, &c->reqs, &c->ints, &c->words, &c->node_terms, &c->pref_terms, &c->spreads,
                     &c->pod_terms, &c->scalars, &c->ports, &c->results, &c->gran, &c->trace, &c->d_classes,
                     &c->d_citems, &c->d_tclasses, &c->d_creqs, &c->d_cints, &c->d_plans, &c->d_aux,
-                    &c->d_aux_terms, &c->scratch, &c->d_pods, &c->gbar})
+                    &c->d_aux_terms, &c->scratch, &c->d_pods, &c->gbar, &c->cut_buf})
     if (b->p) (void)hipFree(b->p);
   if (c->st.mcnt) (void)hipFree(c->st.mcnt);
   if (c->st.tcnt) (void)hipFree(c->st.tcnt);
@@ -1082,6 +1107,19 @@ int kgpu_upload_snapshot(kgpu_ctx* c, const kgpu_snapshot* s, int64_t generation
   if ((rc = dalloc(c, W, &st.raw_dpts, N))) return rc;
   st.key_empty = st.key_empty_value;
   st.hard_pod_affinity_weight = c->cfg.hard_pod_affinity_weight;
+  // percentageOfNodesToScore: nextStartNodeIndex lives with the generic scheduler, not the snapshot
+  // (generic_scheduler.go:451,487), so it carries over a re-upload (taken mod N on use)
+  st.to_find = num_feasible_nodes_to_find(st.n_total, c->cfg.percentage_of_nodes_to_score);
+  if (st.to_find < st.n_total) {
+    if ((rc = ensure(c, c->cut_buf, 16))) return rc;
+    if (!c->cut_init) {
+      HIP_OK(c, hipMemset(c->cut_buf.p, 0, 16));
+      c->cut_init = true;
+    }
+    st.cut_state = static_cast<int32_t*>(c->cut_buf.p);
+  } else {
+    st.cut_state = nullptr;
+  }
   {
     // math.Log(x) for x = 0 .. n_total + 2 (PodTopologySpread weights, scoring.go:286-288)
     std::vector<double> lt((size_t)st.n_total + 3);

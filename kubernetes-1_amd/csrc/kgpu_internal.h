@@ -204,8 +204,16 @@ struct DevState {
   BlkKey* shard_keys;
   BlkStat* shard_stats;
   int32_t nranks;
-  int32_t pad3;
+  // ---- percentageOfNodesToScore (generic_scheduler.go:379-399,424-495): to_find =
+  // numFeasibleNodesToFind(n_total); cut_state[0] = nextStartNodeIndex, cut_state[1] = the last cut
+  // pod's EvaluatedNodes (len(filtered) + len(statuses)).  cut_state is null when to_find == N.
+  int32_t to_find;
+  int32_t* cut_state;
 };
+// Filter status word of a node the cycle never examined (findNodesThatPassFilters stopped before
+// it), or of the feasible node whose discovery cancelled the search: not in `filtered` and not in
+// the statuses map.
+constexpr uint32_t kStatusNotEvaluated = 0xFFu;
 
 // Per-launch parameters.
 struct PodArgs {
@@ -217,6 +225,8 @@ struct PodArgs {
   int32_t norm;         // 1: this pod needs the normalize pass (keys come from k_final)
   int32_t assume;       // apply NodeInfo.AddPod for resolved winners
   int32_t diag;         // write per-plugin raw/normalized scores
+  int32_t cut;          // 1: numFeasibleNodesToFind < N -- k_cut trims the feasible set (R2)
+  int32_t pad;
   int64_t seq;          // tie-break sequence number of `pod`
 };
 
@@ -242,6 +252,11 @@ int launch_eval(const DevState* st, const PodArgs& a, int blocks, int spec, void
 // Kernel instantiation for a profile: 0 = generic list-walking kernel, else a straight-line one.
 int select_spec(const int32_t* filters, int nf, const int32_t* scores, int ns, bool def_res);
 int launch_final(const DevState* st, const PodArgs& a, int blocks, int stat_blocks, void* stream);
+// findNodesThatPassFilters' stopping rule over the evaluated status words: keep the first
+// to_find feasible nodes from nextStartNodeIndex on (rotated order), mark the rest
+// kStatusNotEvaluated, advance nextStartNodeIndex, write the kept set's normalize stats into
+// sbuf[parity] (slot 0; slots 1..blocks-1 zeroed).  One workgroup.
+int launch_cut(const DevState* st, const PodArgs& a, int blocks, int n_filters, void* stream);
 int launch_resolve(const DevState* st, int N, const PodArgs& a, void* stream);
 int eval_blocks(int N);
 // Node sharding: reduce this shard's `blocks` partials of buffer half `parity` to one record in
@@ -254,11 +269,13 @@ int launch_batch(const DevState* st, const BatchArgs& a, int groups, int kidx, i
 // Topology pipeline for one pod (PodArgs.pod): domain histograms, critical-path minima, filters,
 // scores, normalize + argmax, resolve + assume.  next_scratch: words of the next topology pod's
 // scratch to zero in the resolve launch (0 none).
-// fused = one cooperative launch with grid barriers between the phases (default), else six launches.
+// fused = one cooperative launch with grid barriers between the phases, else six launches (the
+// default: measured faster).  A pod with a.cut (percentageOfNodesToScore < 100) always
+// takes the separate launches, with k_cut + k_topo_reg between the filter and score phases.
 // bar: the fused kernel's grid-barrier counter (grows monotonically); bar_base: its value before
 // this launch.  A fused launch adds topo_barriers(min_values) * blocks arrivals.
 int launch_topo(const DevState* st, PodArgs a, int blocks, int64_t min_values, int64_t next_scratch,
-                bool fused, unsigned long long* bar, unsigned long long bar_base, void* stream);
+                bool fused, unsigned long long* bar, unsigned long long bar_base, int n_filters, void* stream);
 inline int topo_barriers(int64_t min_values) { return min_values > 0 ? 5 : 4; }
 // Initialize mcnt columns [c0, c0 + nc) from the pod table (n_pods rows).
 int launch_class_init(const DevState* st, int c0, int nc, int n_pods, void* stream);

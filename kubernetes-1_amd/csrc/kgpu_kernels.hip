@@ -634,7 +634,7 @@ __device__ __forceinline__ int settle_prev(const DevState& st, const PodArgs& a,
     kgpu_result r;
     r.node = placed ? gidx : (error ? -2 : -1);
     r.feasible = w.feasible;
-    r.evaluated = st.n_total;
+    r.evaluated = (a.cut && st.cut_state) ? gp(st.cut_state)[1] : st.n_total;
     r.scored = (placed && w.feasible >= 2) ? 1 : 0;
     r.score = r.scored ? (int64_t)(w.key >> 40) : 0;
     gp(st.results)[a.prev] = r;
@@ -768,6 +768,98 @@ __global__ __launch_bounds__(kBlock) void k_resolve(const DevState* __restrict__
     NodeRes r = load_res(st, idx);
     assume_row(st, pq, r, idx);
     assume_counts(st, a.prev, idx);
+  }
+}
+
+// percentageOfNodesToScore < 100 (generic_scheduler.go:379-399 numFeasibleNodesToFind, :424-495
+// findNodesThatPassFilters): the reference checks nodes from nextStartNodeIndex on, in rotated
+// Snapshot.List() order, and cancels the search when one more node fits after `to_find` already
+// did.  Under the determinism contract (a one-worker run of parallelize.Until) that is:
+//   kept    = the first to_find feasible nodes in rotated order;
+//   p       = rotated position of feasible node to_find + 1 (N if there is none);
+//   statuses = the failing nodes at positions < p; nodes at positions >= p were never examined;
+//   EvaluatedNodes = len(filtered) + len(statuses) = p; nextStartNodeIndex += p (mod N).
+// A profile without filter plugins keeps the first to_find nodes in NON-rotated order and advances
+// by to_find (generic_scheduler.go:438-444).  One 1024-thread workgroup: each thread owns a
+// contiguous run of rotated positions; a block scan of the feasible counts locates the cut.
+constexpr int kCutThreads = 1024;
+__global__ __launch_bounds__(kCutThreads) void k_cut(const DevState* __restrict__ stp, PodArgs a, int blocks,
+                                                     int n_filters) {
+  const DevState& st = *stp;
+  const int N = st.N, K = st.to_find, tid = threadIdx.x;
+  __shared__ int scan[kCutThreads];
+  __shared__ int red[3][kCutThreads / 64];
+  const int start = N > 0 ? gp(st.cut_state)[0] % N : 0;
+  const int per = (N + kCutThreads - 1) / kCutThreads;
+  const int r0 = min(N, tid * per), r1 = min(N, r0 + per);
+  auto node_at = [&](int r) { return n_filters ? (start + r) % N : r; };
+  int cnt = 0;
+  for (int r = r0; r < r1; ++r) cnt += gp(st.status)[node_at(r)] == 0;
+  // inclusive block scan of the per-thread feasible counts
+  scan[tid] = cnt;
+  __syncthreads();
+  for (int off = 1; off < kCutThreads; off <<= 1) {
+    const int v = tid >= off ? scan[tid - off] : 0;
+    __syncthreads();
+    scan[tid] += v;
+    __syncthreads();
+  }
+  const int before = scan[tid] - cnt;  // feasible nodes at positions < r0
+  const int total = scan[kCutThreads - 1];
+  // p: position of feasible node K + 1 (the one that cancels the search), N if none
+  __shared__ int p_sh;
+  if (tid == 0) p_sh = N;
+  __syncthreads();
+  if (n_filters && total > K && before <= K && before + cnt > K) {
+    int seen = before;
+    for (int r = r0; r < r1; ++r)
+      if (gp(st.status)[node_at(r)] == 0 && ++seen == K + 1) {
+        p_sh = r;
+        break;
+      }
+  }
+  __syncthreads();
+  const int p = n_filters ? p_sh : K;
+  int feas = 0, maxT = 0, maxNA = 0;
+  int seen = before;
+  for (int r = r0; r < r1; ++r) {
+    const int n = node_at(r);
+    const uint32_t w = gp(st.status)[n];
+    if (w == 0) {
+      if (++seen <= K) {
+        ++feas;
+        maxT = max(maxT, gp(st.raw_taint)[n]);
+        maxNA = max(maxNA, gp(st.raw_na)[n]);
+        continue;
+      }
+      gp(st.status)[n] = kStatusNotEvaluated;  // feasible but beyond the cut
+    } else if (r >= p) {
+      gp(st.status)[n] = kStatusNotEvaluated;  // never examined
+    }
+  }
+  feas = wave_reduce_sum(feas);
+  maxT = wave_reduce_max(maxT);
+  maxNA = wave_reduce_max(maxNA);
+  if ((tid & 63) == 0) {
+    red[0][tid >> 6] = feas;
+    red[1][tid >> 6] = maxT;
+    red[2][tid >> 6] = maxNA;
+  }
+  __syncthreads();
+  for (int b = tid; b < blocks; b += kCutThreads) {
+    BlkStat o{0, 0, 0, 0};
+    if (b == 0) {
+      for (int w = 0; w < kCutThreads / 64; ++w) {
+        o.feasible += red[0][w];
+        o.max_taint = max(o.max_taint, red[1][w]);
+        o.max_na = max(o.max_na, red[2][w]);
+      }
+    }
+    gp(st.sbuf)[(size_t)a.parity * kMaxBlocks + b] = o;
+  }
+  if (tid == 0) {
+    gp(st.cut_state)[0] = N > 0 ? (start + p) % N : 0;
+    gp(st.cut_state)[1] = p;
   }
 }
 
@@ -1324,6 +1416,35 @@ __device__ __forceinline__ void topo_min(const DevState* __restrict__ stp, PodAr
   }
 }
 
+// initPreScoreState for one filtered node (scoring.go:83-102): ignored when a soft key is missing,
+// else register its ScheduleAnyway pairs (topoSize counts first registrations).  Returns 1 if the
+// node is not ignored.
+__device__ __forceinline__ int soft_register(const DevState& st, const QPlan& pl, int n) {
+  if (!pl.n_soft || !all_keys(st, pl.soft, pl.n_soft, n)) return 0;
+  TopoHdr* h = hdr(st);
+  for (int i = 0; i < pl.n_soft; ++i) {
+    const TSpread& c = pl.soft[i];
+    if (c.is_hostname) continue;
+    int64_t* reg = slot_ptr(st, pl, c.rslot) + nval(st, c.key, n);
+    const unsigned long long old = atomicExch(reinterpret_cast<unsigned long long*>(reg), 1ull);
+    if (old == 0 && c.first_of_key) add64(&h->ssize[i], 1);
+  }
+  return 1;
+}
+
+// ScheduleAnyway registration over the feasible set kept by k_cut.
+__device__ __forceinline__ void topo_reg(const DevState* __restrict__ stp, PodArgs a) {
+  const DevState& st = *stp;
+  const QPlan& pl = st.plans[a.pod];
+  int lo, hi;
+  chunk_of(st.N, lo, hi);
+  int nonign = 0;
+  for (int n = lo + threadIdx.x; n < hi; n += kBlock)
+    if (gp(st.status)[n] == 0) nonign += soft_register(st, pl, n);
+  nonign = wave_reduce_sum(nonign);
+  if (threadIdx.x == 0 && nonign) atomicAdd(&hdr(st)->feas_nonign, nonign);
+}
+
 // Filters + the non-topology scores; the feasible set's ScheduleAnyway pairs and sizes.
 __device__ __forceinline__ void topo_filter(const DevState* __restrict__ stp, PodArgs a) {
   const DevState& st = *stp;
@@ -1354,16 +1475,8 @@ __device__ __forceinline__ void topo_filter(const DevState* __restrict__ stp, Po
       maxT = max(maxT, e.taint);
       maxNA = max(maxNA, e.na);
       // PTS PreScore over the filtered nodes (scoring.go:83-102): pairs, sizes, ignored nodes
-      if (pl.n_soft && all_keys(st, pl.soft, pl.n_soft, n)) {
-        ++nonign;
-        for (int i = 0; i < pl.n_soft; ++i) {
-          const TSpread& c = pl.soft[i];
-          if (c.is_hostname) continue;
-          int64_t* reg = slot_ptr(st, pl, c.rslot) + nval(st, c.key, n);
-          const unsigned long long old = atomicExch(reinterpret_cast<unsigned long long*>(reg), 1ull);
-          if (old == 0 && c.first_of_key) add64(&h->ssize[i], 1);
-        }
-      }
+      // (after k_cut when the feasible set is trimmed: k_topo_reg)
+      if (!a.cut) nonign += soft_register(st, pl, n);
     }
     gp(st.status)[n] = e.status;
     gp(st.partial)[n] = e.partial;
@@ -1574,6 +1687,7 @@ __global__ __launch_bounds__(kBlock) void k_topo_pre(const DevState* __restrict_
 __global__ __launch_bounds__(kBlock) void k_topo_min(const DevState* __restrict__ stp, PodArgs a) { topo_min(stp, a); }
 __global__ __launch_bounds__(kBlock) void k_topo_filter(const DevState* __restrict__ stp, PodArgs a) { topo_filter(stp, a); }
 __global__ __launch_bounds__(kBlock) void k_topo_score(const DevState* __restrict__ stp, PodArgs a) { topo_score(stp, a); }
+__global__ __launch_bounds__(kBlock) void k_topo_reg(const DevState* __restrict__ stp, PodArgs a) { topo_reg(stp, a); }
 __global__ __launch_bounds__(kBlock) void k_topo_final(const DevState* __restrict__ stp, PodArgs a, int stat_blocks) { topo_final(stp, a, stat_blocks); }
 __global__ __launch_bounds__(kBlock) void k_topo_resolve(const DevState* __restrict__ stp, PodArgs a,
                                                          int64_t next_scratch) {
@@ -1662,9 +1776,9 @@ __global__ void k_class_init(const DevState* __restrict__ stp, int c0, int nc, i
 }
 
 int launch_topo(const DevState* st, PodArgs a, int blocks, int64_t min_values, int64_t next_scratch,
-                bool fused, unsigned long long* bar, unsigned long long bar_base, void* stream) {
+                bool fused, unsigned long long* bar, unsigned long long bar_base, int n_filters, void* stream) {
   hipStream_t s = (hipStream_t)stream;
-  if (fused) {
+  if (fused && !a.cut) {
     int do_min = min_values > 0 ? 1 : 0;
     void* args[] = {(void*)&st, (void*)&a, (void*)&do_min, (void*)&next_scratch, (void*)&bar, (void*)&bar_base};
     return hipLaunchCooperativeKernel((const void*)k_topo_fused, dim3(blocks), dim3(kBlock), args, 0, s) == hipSuccess
@@ -1677,6 +1791,10 @@ int launch_topo(const DevState* st, PodArgs a, int blocks, int64_t min_values, i
     hipLaunchKernelGGL(k_topo_min, dim3((int)mb), dim3(kBlock), 0, s, st, a);
   }
   hipLaunchKernelGGL(k_topo_filter, dim3(blocks), dim3(kBlock), 0, s, st, a);
+  if (a.cut) {
+    hipLaunchKernelGGL(k_cut, dim3(1), dim3(kCutThreads), 0, s, st, a, blocks, n_filters);
+    hipLaunchKernelGGL(k_topo_reg, dim3(blocks), dim3(kBlock), 0, s, st, a);
+  }
   hipLaunchKernelGGL(k_topo_score, dim3(blocks), dim3(kBlock), 0, s, st, a);
   hipLaunchKernelGGL(k_topo_final, dim3(blocks), dim3(kBlock), 0, s, st, a, blocks);
   PodArgs r = a;
@@ -1806,6 +1924,11 @@ int launch_eval(const DevState* st, const PodArgs& a, int blocks, int spec, void
 
 int launch_final(const DevState* st, const PodArgs& a, int blocks, int stat_blocks, void* stream) {
   hipLaunchKernelGGL(k_final, dim3(blocks), dim3(kBlock), 0, (hipStream_t)stream, st, a, stat_blocks);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_cut(const DevState* st, const PodArgs& a, int blocks, int n_filters, void* stream) {
+  hipLaunchKernelGGL(k_cut, dim3(1), dim3(kCutThreads), 0, (hipStream_t)stream, st, a, blocks, n_filters);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

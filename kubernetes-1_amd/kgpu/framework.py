@@ -126,6 +126,8 @@ class GpuFramework:
         words = self.engine.filter_words(n)
         statuses = {}
         for i in np.nonzero(words)[0]:
+            if int(words[i]) == abi.STATUS_NOT_EVALUATED:
+                continue  # never examined: percentageOfNodesToScore stopped the search before it
             nm = self.order[self.snap.node_base + int(i)]
             statuses[nm] = self.reasons(pod, nm, int(words[i]))
         scores = {}

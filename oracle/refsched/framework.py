@@ -218,17 +218,24 @@ class GenericScheduler:
         index = {NI.name(ni.node): i for i, ni in enumerate(all_nodes)}
         to_find = self.num_feasible_nodes_to_find(len(all_nodes))
         feasible, statuses = [], {}
-        for i in range(len(all_nodes)):
-            ni = all_nodes[(self.next_start + i) % len(all_nodes)]
-            plugin, fst = self.fw.run_filters(state, pod, ni)
-            if fst is not None and fst.code == P.ERROR:
-                raise ScheduleError(repr(fst))
-            if fst is None:
-                feasible.append(ni.node)
-                if len(feasible) >= to_find:
-                    break
-            else:
-                statuses[NI.name(ni.node)] = (plugin, fst)
+        if not self.fw.filters:
+            # no filter plugins: the first numNodesToFind nodes, not rotated (generic_scheduler.go:438-444)
+            feasible = [ni.node for ni in all_nodes[:to_find]]
+        else:
+            # checkNode (generic_scheduler.go:451-471) run by one worker: after to_find nodes fit, the
+            # next node that fits cancels the search and is dropped (length > numNodesToFind); failures
+            # seen before it are recorded
+            for i in range(len(all_nodes)):
+                ni = all_nodes[(self.next_start + i) % len(all_nodes)]
+                plugin, fst = self.fw.run_filters(state, pod, ni)
+                if fst is not None and fst.code == P.ERROR:
+                    raise ScheduleError(repr(fst))
+                if fst is None:
+                    if len(feasible) >= to_find:
+                        break
+                    feasible.append(ni.node)
+                else:
+                    statuses[NI.name(ni.node)] = (plugin, fst)
         processed = len(feasible) + len(statuses)
         self.next_start = (self.next_start + processed) % len(all_nodes)
         if not feasible:
