@@ -83,6 +83,8 @@ def main():
     ap.add_argument("--latency-pods", type=int, default=200, help="pods timed one at a time through kgpu_schedule_one")
     ap.add_argument("--no-persistent", action="store_true", help="one evaluation launch per pod")
     ap.add_argument("--topo-fused", type=int, default=None, help="KGPU_OPT_TOPO_FUSED (default: the library's)")
+    ap.add_argument("--no-topo-persistent", action="store_true",
+                    help="topology pods through the per-pod topology launches instead of k_tbatch")
     ap.add_argument("--shard", action="store_true",
                     help="at N=1: run the node-sharded path on a one-rank RCCL communicator (exchange overhead)")
     args = ap.parse_args()
@@ -128,6 +130,8 @@ def main():
         eng.set_option(abi.OPT_PERSISTENT, 0)
     if args.topo_fused is not None:
         eng.set_option(abi.OPT_TOPO_FUSED, args.topo_fused)
+    if args.no_topo_persistent:
+        eng.set_option(abi.OPT_TOPO_PERSISTENT, 0)
 
     def reset():
         eng.upload(fw.snap, fw.arrays)
@@ -188,8 +192,9 @@ def main():
     pod_bytes = n_local * bpe + BYTES_PER_EXISTING_POD.get(args.config, 0) * len(existing)
     achieved = pod_bytes / per_pod_s / 1e9
     topo = args.config in ("c", "d")
-    persistent = not args.no_persistent and not topo and not sharded
+    persistent = not args.no_persistent and not sharded and not (topo and args.no_topo_persistent)
     launch_pods = B if persistent else 1
+    kname = ("k_tbatch" if topo else "k_batch") if persistent else ("k_topo_* pipeline" if topo else "k_eval")
 
     # CPU baseline: the C restatement of the reference algorithm on this host's cores.  Three
     # worker counts are timed -- 1, the reference's parallelism (16 goroutines,
@@ -230,7 +235,7 @@ def main():
     try:
         with open(os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")) as fh:
             pmc = json.load(fh).get("%s:%d:%d" % (args.config, n_local, launch_pods))
-        if pmc and pmc["kernel"] == ("k_batch" if persistent else ("k_topo_* pipeline" if topo else "k_eval")):
+        if pmc and pmc["kernel"] == kname:
             traffic = pmc["traffic_bytes_per_launch"]
     except (OSError, ValueError):
         pass
@@ -249,7 +254,7 @@ def main():
             "placed": placed,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                         "kernel": "k_batch" if persistent else ("k_topo_* pipeline" if topo else "k_eval"),
+                         "kernel": kname,
                          "bytes_per_node_eval": bpe,
                          "avg_kernel_us": round(per_pod_s * launch_pods * 1e6, 3), "pods_per_launch": launch_pods,
                          "us_per_pod": round(per_pod_s * 1e6, 4),

@@ -403,6 +403,10 @@ int kgpu_read_nodes(kgpu_ctx* ctx, int64_t* req_cpu, int64_t* req_mem, int64_t* 
  * filters, scores, normalize + argmax, resolve + assume) in one cooperative launch with grid
  * barriers; 0 (default) = one launch per phase, which measured faster on MI355X. */
 #define KGPU_OPT_TOPO_FUSED 5
+/* KGPU_OPT_TOPO_PERSISTENT (6): 1 (default) = runs of PodTopologySpread / InterPodAffinity /
+ * DefaultPodTopologySpread pods go through one persistent launch with device-resident domain
+ * histograms; 0 = one topology pipeline per pod. */
+#define KGPU_OPT_TOPO_PERSISTENT 6
 int kgpu_set_option(kgpu_ctx* ctx, int32_t option, int64_t value);
 /* Phase stamps of the last persistent run (100 MHz s_memrealtime ticks), 16 per pipeline
  * iteration (pods + 1): workgroup 0's {start, evaluated, previous pod resolved, published, end, 0,

@@ -9,9 +9,12 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <array>
+#include <iterator>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <deque>
 #include <map>
 #include <string>
 #include <vector>
@@ -89,7 +92,11 @@ struct kgpu_ctx {
   std::vector<PodRow> pod_rows;
   int pod_rows_dev = -1;         // rows present in the device pod table (-1: table never uploaded)
   std::vector<int32_t> key_n_values, key_empty;
+  std::vector<uint8_t> key_unique;  // every value of the key sits on at most one node (hostname-like)
   int64_t max_key_values = 1;
+  // persistent topology runs (k_tbatch)
+  bool tfast = true;                // KGPU_OPT_TOPO_PERSISTENT
+  DevBuf t_plans, t_plan_of, t_aux, t_looks, t_tabs, t_deltas, t_hists, t_sigs, t_regs, t_zero, abort_buf;
   // ---- node sharding (kgpu_comm_init): this context holds one contiguous slice of the
   // snapshot; per pod the shard winners (and normalize maxima) are all-gathered over RCCL
   ncclComm_t comm = nullptr;
@@ -604,6 +611,479 @@ hipEvent_t get_event(kgpu_ctx* c, size_t i) {
   return c->ev_pool[i];
 }
 
+// ---------------------------------------------------------------- persistent topology runs
+// A run of consecutive topology pods is planned against ONE set of domain histograms
+// (kgpu_internal.h "persistent topology kernel"): every (column, key, signature) the run's pods
+// read becomes a THist, every nodeSelector / required-NodeAffinity program + key set a TSig.
+// A pool whose ranges are interned by content: pods of one template share their records, so the
+// persistent kernel reads cache-hot lines instead of fresh ones per pod.
+template <class T>
+struct RangePool {
+  std::vector<T> v;
+  std::map<std::string, kgpu_range> m;
+  kgpu_range add(const std::vector<T>& items) {
+    if (items.empty()) return kgpu_range{0, 0};
+    std::string k(reinterpret_cast<const char*>(items.data()), items.size() * sizeof(T));
+    auto f = m.find(k);
+    if (f != m.end()) return f->second;
+    const kgpu_range r{(int32_t)v.size(), (int32_t)items.size()};
+    v.insert(v.end(), items.begin(), items.end());
+    m[k] = r;
+    return r;
+  }
+  void truncate(size_t n) {
+    v.resize(n);
+    for (auto it = m.begin(); it != m.end();)
+      it = (size_t)(it->second.begin + it->second.count) > n ? m.erase(it) : std::next(it);
+  }
+};
+
+struct TRun {
+  std::vector<kgpu::THist> hists;
+  std::map<std::array<int32_t, 4>, int> hist_ids;
+  std::vector<kgpu::TSig> sigs;
+  std::map<std::vector<int64_t>, int> sig_ids;
+  std::vector<kgpu::TReg> regs;
+  std::map<std::pair<int, int>, int> reg_ids;
+  std::vector<kgpu::TPlan> plans;   // one per pod while planning; distinct ones after t_finish
+  std::vector<int32_t> plan_of;     // plan index of each pod of the run (after t_finish)
+  RangePool<int32_t> aux;
+  RangePool<kgpu::TLook> looks;
+  RangePool<kgpu::TTab> tabs;
+  RangePool<kgpu::TDelta> deltas;
+  std::vector<int32_t> pods;  // query index of each plan
+  int lds_bins = 0, reg_words = 0, soft_words = 0, zones = 0, pt_max = 0;
+};
+
+void push_reqs(std::vector<int64_t>& k, const kgpu_pools* p, kgpu_range rr) {
+  k.push_back(rr.count);
+  for (int i = 0; i < rr.count; ++i) {
+    const kgpu_req& r = p->reqs[rr.begin + i];
+    std::vector<int32_t> v(p->ints + r.vals.begin, p->ints + r.vals.begin + r.vals.count);
+    std::sort(v.begin(), v.end());
+    k.push_back(r.key);
+    k.push_back(r.op);
+    k.push_back(r.imm);
+    k.push_back((int64_t)v.size());
+    for (int32_t x : v) k.push_back(x);
+  }
+}
+
+// signature = PodMatchesNodeSelectorAndAffinityTerms program + the keys a node must carry
+int t_sig(TRun& tr, const kgpu_pod_query& q, const kgpu_pools* p, int qi, const int32_t* keys, int nk) {
+  std::vector<int64_t> k;
+  push_reqs(k, p, q.node_selector);
+  const bool req = (q.flags & KGPU_Q_REQ_NODE_AFFINITY) != 0;
+  k.push_back(req ? 1 : 0);
+  if (req) {
+    k.push_back(q.req_terms.count);
+    for (int t = 0; t < q.req_terms.count; ++t) {
+      const kgpu_node_term& nt = p->node_terms[q.req_terms.begin + t];
+      k.push_back(nt.never_match);
+      k.push_back(nt.field_op);
+      k.push_back(nt.field_node);
+      push_reqs(k, p, nt.reqs);
+    }
+  }
+  std::vector<int32_t> ks(keys, keys + std::max(nk, 0));
+  std::sort(ks.begin(), ks.end());
+  ks.erase(std::unique(ks.begin(), ks.end()), ks.end());
+  k.push_back(nk < 0 ? -8 : -7);
+  for (int32_t x : ks) k.push_back(x);
+  auto f = tr.sig_ids.find(k);
+  if (f != tr.sig_ids.end()) return f->second;
+  kgpu::TSig sg{};
+  sg.rep = qi;
+  sg.n_keys = nk < 0 ? -1 : (int32_t)ks.size();  // -1: a key no node carries, nothing is eligible
+  for (size_t i = 0; i < ks.size() && i < (size_t)kgpu::kMaxSpread; ++i) sg.keys[i] = ks[i];
+  const int id = (int)tr.sigs.size();
+  tr.sigs.push_back(sg);
+  tr.sig_ids[k] = id;
+  return id;
+}
+
+// histogram of (column, key, signature); off = -1 for a node-unique key (no LDS bins)
+int t_hist(TRun& tr, const kgpu_ctx* c, int kind, int col, int key, int sig) {
+  const std::array<int32_t, 4> k{kind, col, key, sig};
+  auto f = tr.hist_ids.find(k);
+  if (f != tr.hist_ids.end()) return f->second;
+  kgpu::THist h{};
+  h.col_kind = kind;
+  h.col = col;
+  h.key = key;
+  h.sig = sig;
+  h.D = key >= 0 ? c->key_n_values[(size_t)key] : 0;
+  const bool uniq = key >= 0 && c->key_unique[(size_t)key];
+  h.off = uniq ? -1 : tr.lds_bins;
+  if (!uniq) tr.lds_bins += h.D + 1;
+  const int id = (int)tr.hists.size();
+  tr.hists.push_back(h);
+  tr.hist_ids[k] = id;
+  return id;
+}
+
+int t_reg(TRun& tr, const kgpu_ctx* c, int sig, int key) {
+  auto f = tr.reg_ids.find({sig, key});
+  if (f != tr.reg_ids.end()) return f->second;
+  kgpu::TReg r{sig, key, c->key_n_values[(size_t)key], tr.reg_words};
+  tr.reg_words += (r.D + 31) / 32;
+  const int id = (int)tr.regs.size();
+  tr.regs.push_back(r);
+  tr.reg_ids[{sig, key}] = id;
+  return id;
+}
+
+size_t a16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+constexpr size_t kTMiscBytes = 1024;
+
+// LDS layout of a run (byte offsets into the dynamic region); returns the total
+size_t t_layout(const TRun& tr, kgpu::TBatchArgs* a, int B) {
+  size_t o = a16((size_t)tr.lds_bins * 4);
+  const size_t o_reg = o;
+  o = a16(o + (size_t)tr.reg_words * 4);
+  const size_t o_tot = o;
+  o = a16(o + tr.hists.size() * 4);
+  const size_t o_sany = o;
+  o = a16(o + tr.sigs.size() * 4);
+  const int R = kgpu::kTFixed + tr.soft_words + tr.zones;
+  const size_t o_stat = o;
+  o = a16(o + (size_t)R * 8);
+  const size_t o_smask = o;
+  o = a16(o + (size_t)kgpu::kTMaxSoftWords * 4);
+  const size_t o_zsum = o;
+  o = a16(o + (size_t)std::max(tr.zones, 1) * 4);
+  const size_t o_wred = o;
+  o = a16(o + (size_t)(B / 64) * kgpu::kTFixed * 8);
+  const size_t o_pt = o;
+  o = a16(o + (size_t)std::max(tr.pt_max, 1) * 8);
+  const size_t o_misc = o;
+  o = a16(o + kTMiscBytes);
+  if (a) {
+    a->o_reg = (int32_t)o_reg;
+    a->o_tot = (int32_t)o_tot;
+    a->o_sany = (int32_t)o_sany;
+    a->o_stat = (int32_t)o_stat;
+    a->o_smask = (int32_t)o_smask;
+    a->o_zsum = (int32_t)o_zsum;
+    a->o_wred = (int32_t)o_wred;
+    a->o_pt = (int32_t)o_pt;
+    a->o_misc = (int32_t)o_misc;
+    a->R = R;
+  }
+  return o;
+}
+
+struct TRunMark {
+  size_t hists, sigs, regs, plans, aux, looks, tabs;
+  int lds_bins, reg_words, soft_words, zones, pt_max;
+};
+
+void t_rollback(TRun& tr, const TRunMark& m) {
+  for (auto it = tr.hist_ids.begin(); it != tr.hist_ids.end();)
+    it = it->second >= (int)m.hists ? tr.hist_ids.erase(it) : std::next(it);
+  for (auto it = tr.sig_ids.begin(); it != tr.sig_ids.end();)
+    it = it->second >= (int)m.sigs ? tr.sig_ids.erase(it) : std::next(it);
+  for (auto it = tr.reg_ids.begin(); it != tr.reg_ids.end();)
+    it = it->second >= (int)m.regs ? tr.reg_ids.erase(it) : std::next(it);
+  tr.hists.resize(m.hists);
+  tr.sigs.resize(m.sigs);
+  tr.regs.resize(m.regs);
+  tr.plans.resize(m.plans);
+  tr.aux.truncate(m.aux);
+  tr.looks.truncate(m.looks);
+  tr.tabs.truncate(m.tabs);
+  tr.lds_bins = m.lds_bins;
+  tr.reg_words = m.reg_words;
+  tr.soft_words = m.soft_words;
+  tr.zones = m.zones;
+  tr.pt_max = m.pt_max;
+}
+
+kgpu::TLook t_look(TRun& tr, const kgpu_ctx* c, int kind, int col, int key, int weight) {
+  kgpu::TLook l{};
+  l.key = key;
+  l.weight = weight;
+  l.col_kind = kind;
+  l.col = col;
+  l.off = -1;
+  l.D = 0;
+  if (key >= 0) {
+    const kgpu::THist& h = tr.hists[(size_t)t_hist(tr, c, kind, col, key, -1)];
+    l.off = h.off;
+    l.D = h.D;
+  }
+  return l;
+}
+
+// Plan pod qi for the persistent topology kernel; false (run left unchanged) when the pod needs
+// what the kernel does not carry: more than one ScheduleAnyway constraint, a DoNotSchedule
+// constraint on a node-unique key (its criticalPaths minimum is a cluster-wide reduction per
+// pod), a shared ScheduleAnyway key with more than 256 values, more than 32 zones for
+// DefaultPodTopologySpread, more than 64 signatures, or tables beyond the LDS budget.
+bool t_add(TRun& tr, const kgpu_ctx* c, const kgpu_pod_query& q, const kgpu::QPlan& pl, const kgpu_pools* p,
+           const std::vector<int32_t>& aux, const std::vector<kgpu::TTerm>& aux_terms, int qi) {
+  const TRunMark m{tr.hists.size(), tr.sigs.size(), tr.regs.size(), tr.plans.size(), tr.aux.v.size(),
+                   tr.looks.v.size(), tr.tabs.v.size(), tr.lds_bins, tr.reg_words, tr.soft_words, tr.zones, tr.pt_max};
+  auto fail_ = [&]() {
+    t_rollback(tr, m);
+    return false;
+  };
+  if (pl.n_soft > 1) return fail_();
+  kgpu::TPlan tp;
+  std::memset(&tp, 0, sizeof(tp));  // plans are interned by their bytes
+  // the pod's tables: [kind 0 per DoNotSchedule key][kind 2 per score key][kind 1 per anti key],
+  // each with its term list (shared-key histograms)
+  struct Tab {
+    kgpu::TTab t;
+    std::vector<kgpu::TLook> terms;
+  };
+  std::vector<Tab> t0, t1, t2;
+  auto tab_for = [&](std::vector<Tab>& v, int kind, int key) -> int {
+    for (size_t i = 0; i < v.size(); ++i)
+      if (v[i].t.key == key) return (int)i;
+    Tab t{};
+    t.t.kind = kind;
+    t.t.key = key;
+    t.t.D = c->key_n_values[(size_t)key];
+    t.t.reg = -1;
+    t.t.empty_v = -1;
+    v.push_back(t);
+    return (int)v.size() - 1;
+  };
+  tp.aff_sig = t_sig(tr, q, p, qi, nullptr, 0);
+  tp.n_hard = pl.n_hard;
+  if (pl.n_hard) {
+    int32_t keys[kgpu::kMaxSpread];
+    bool missing = false;
+    for (int h = 0; h < pl.n_hard; ++h) {
+      keys[h] = pl.hard[h].key;
+      missing |= keys[h] < 0;
+    }
+    tp.hard_sig = t_sig(tr, q, p, qi, keys, missing ? -1 : pl.n_hard);
+    for (int h = 0; h < pl.n_hard; ++h) {
+      const kgpu::TSpread& sp = pl.hard[h];
+      kgpu::THard& th = tp.hard[h];
+      th.key = sp.key;
+      th.max_skew = sp.max_skew;
+      th.self_match = sp.self_match;
+      th.tab = -1;
+      if (sp.key < 0) continue;  // nothing registers: the filter passes every node (pany == 0)
+      if (c->key_unique[(size_t)sp.key]) return fail_();
+      const int ti = tab_for(t0, 0, sp.key);
+      t0[(size_t)ti].t.reg = t_reg(tr, c, tp.hard_sig, sp.key);
+      t0[(size_t)ti].t.empty_v = c->key_empty[(size_t)sp.key];
+      t0[(size_t)ti].terms.push_back(t_look(tr, c, 0, sp.cls, sp.key, 1));
+      th.tab = ti;
+    }
+  }
+  tp.n_soft = pl.n_soft;
+  if (pl.n_soft) {
+    const kgpu::TSpread& sp = pl.soft[0];
+    tp.soft_key = sp.key;
+    tp.soft_max_skew = sp.max_skew;
+    tp.soft_col = sp.cls;
+    tp.soft_off = -1;
+    tp.soft_sig = -1;
+    if (sp.is_hostname) {
+      tp.soft_mode = 1;
+    } else if (sp.key >= 0 && c->key_unique[(size_t)sp.key]) {
+      tp.soft_mode = 2;
+      int32_t k1 = sp.key;
+      tp.soft_sig = t_sig(tr, q, p, qi, &k1, 1);
+    } else {
+      tp.soft_mode = 0;
+      if (sp.key >= 0) {
+        const int D = c->key_n_values[(size_t)sp.key];
+        if (D > 32 * kgpu::kTMaxSoftWords) return fail_();
+        int32_t k1 = sp.key;
+        tp.soft_sig = t_sig(tr, q, p, qi, &k1, 1);
+        tp.soft_off = tr.hists[(size_t)t_hist(tr, c, 0, sp.cls, sp.key, tp.soft_sig)].off;
+        tp.soft_words = (D + 31) / 32;
+        tr.soft_words = std::max(tr.soft_words, tp.soft_words);
+      }
+    }
+  }
+  tp.n_aff = pl.n_aff;
+  tp.self_all = pl.self_all;
+  for (int a = 0; a < pl.n_aff; ++a) {
+    tp.aff[a] = t_look(tr, c, 0, pl.aff[a].cls, pl.aff[a].key, 0);
+    tp.aff_hist[a] = pl.aff[a].key >= 0 ? t_hist(tr, c, 0, pl.aff[a].cls, pl.aff[a].key, -1) : -1;
+  }
+  tp.n_anti = pl.n_anti;
+  for (int a = 0; a < pl.n_anti; ++a) tp.anti[a] = t_look(tr, c, 0, pl.anti[a].cls, pl.anti[a].key, 0);
+  std::vector<kgpu::TLook> exa_u, score_u;
+  auto add_term = [&](std::vector<Tab>& tabs, std::vector<kgpu::TLook>& uniq, int kind_tab, int col_kind, int col, int key,
+                      int w) {
+    if (key < 0) return;
+    const kgpu::TLook l = t_look(tr, c, col_kind, col, key, w);
+    if (l.off < 0) uniq.push_back(l);
+    else tabs[(size_t)tab_for(tabs, kind_tab, key)].terms.push_back(l);
+  };
+  for (int e = 0; e < pl.n_ex_anti; ++e) {
+    const kgpu::TTerm& t = aux_terms[(size_t)pl.ex.begin + e];
+    add_term(t1, exa_u, 1, 1, t.cls, t.key, 1);
+  }
+  for (int e = 0; e < pl.n_pref; ++e) add_term(t2, score_u, 2, 0, pl.pref[e].cls, pl.pref[e].key, pl.pref[e].weight);
+  for (int e = pl.n_ex_anti; e < pl.ex.count; ++e) {
+    const kgpu::TTerm& t = aux_terms[(size_t)pl.ex.begin + e];
+    add_term(t2, score_u, 2, 1, t.cls, t.key, t.weight);
+  }
+  tp.need_ipa = (!t2.empty() || !score_u.empty()) ? 1 : 0;
+  tp.exa_u = tr.looks.add(exa_u);
+  tp.score_u = tr.looks.add(score_u);
+  // tables: kind 0, kind 2, kind 1 (the last n_exa_tabs)
+  int pt = 0;
+  std::vector<kgpu::TTab> tabs;
+  for (std::vector<Tab>* v : {&t0, &t2, &t1})
+    for (Tab& t : *v) {
+      t.t.off = pt;
+      pt += t.t.D;
+      t.t.terms = tr.looks.add(t.terms);
+      tabs.push_back(t.t);
+    }
+  tp.tabs = tr.tabs.add(tabs);
+  tp.n_exa_tabs = (int32_t)t1.size();
+  if (tp.tabs.count > kgpu::kTMaxTabs) return fail_();
+  tp.pt_words = pt;
+  tr.pt_max = std::max(tr.pt_max, pt);
+  tp.dpts_cls = pl.dpts_cls;
+  if (pl.dpts_cls >= 0) {
+    if (c->st.n_zones > kgpu::kTMaxZones) return fail_();
+    tr.zones = c->st.n_zones;
+  }
+  tp.assume_cls = tr.aux.add(std::vector<int32_t>(aux.begin() + pl.assume_cls.begin,
+                                                   aux.begin() + pl.assume_cls.begin + pl.assume_cls.count));
+  tp.own_tcls = tr.aux.add(std::vector<int32_t>(aux.begin() + pl.own_tcls.begin,
+                                                aux.begin() + pl.own_tcls.begin + pl.own_tcls.count));
+  if (tr.sigs.size() > 64 || t_layout(tr, nullptr, 512) > (size_t)kgpu::kTLdsBudget) return fail_();
+  tr.plans.push_back(tp);
+  tr.pods.push_back(qi);
+  return true;
+}
+
+// Histogram deltas of every planned pod (the run's histograms over the columns it increments),
+// then the distinct plans: pods of one template share one plan record.
+void t_finish(TRun& tr) {
+  std::map<std::string, int> ids;
+  std::vector<kgpu::TPlan> uniq;
+  tr.plan_of.clear();
+  for (kgpu::TPlan& tp : tr.plans) {
+    std::vector<kgpu::TDelta> ds;
+    for (int h = 0; h < (int)tr.hists.size(); ++h) {
+      const kgpu::THist& hh = tr.hists[(size_t)h];
+      const kgpu_range rr = hh.col_kind == 0 ? tp.assume_cls : tp.own_tcls;
+      for (int i = 0; i < rr.count; ++i)
+        if (tr.aux.v[(size_t)rr.begin + i] == hh.col) {
+          kgpu::TDelta d;
+          std::memset(&d, 0, sizeof(d));
+          d.hist = h;
+          d.off = hh.off;
+          d.D = hh.D;
+          d.key = hh.key;
+          d.sig = hh.sig;
+          ds.push_back(d);
+          break;
+        }
+    }
+    tp.deltas = tr.deltas.add(ds);
+    const std::string k(reinterpret_cast<const char*>(&tp), sizeof(tp));
+    auto f = ids.find(k);
+    if (f == ids.end()) {
+      f = ids.emplace(k, (int)uniq.size()).first;
+      uniq.push_back(tp);
+    }
+    tr.plan_of.push_back(f->second);
+  }
+  tr.plans.swap(uniq);
+}
+
+// Upload a planned run and launch k_sig_init + k_hist_init + k_tbatch on the engine's stream.
+int run_tbatch(kgpu_ctx* c, TRun& tr, int first, int count, int64_t first_seq, int32_t assume, int per, int groups,
+               int geo, int32_t* abort_word) {
+  t_finish(tr);
+  int rc;
+  kgpu::TBatchArgs a{};
+  a.first = first;
+  a.count = count;
+  a.per = per;
+  a.assume = assume;
+  a.seq0 = first_seq + first;
+  a.n_hists = (int32_t)tr.hists.size();
+  a.n_sigs = (int32_t)tr.sigs.size();
+  a.n_regs = (int32_t)tr.regs.size();
+  a.lds_bins = tr.lds_bins;
+  a.reg_words = tr.reg_words;
+  a.soft_words = tr.soft_words;
+  a.zones = tr.zones;
+  a.pt_words = tr.pt_max;
+  a.n_keys = c->st.K;
+  a.def_res = c->spec != 0 || (c->cfg.n_least == 2 && c->cfg.least[0].resource == 0 && c->cfg.least[0].weight == 1 &&
+                                c->cfg.least[1].resource == 1 && c->cfg.least[1].weight == 1 && c->cfg.n_most == 2 &&
+                                c->cfg.most[0].resource == 0 && c->cfg.most[0].weight == 1 &&
+                                c->cfg.most[1].resource == 1 && c->cfg.most[1].weight == 1)
+                  ? 1 : 0;
+  size_t lds = t_layout(tr, &a, 512);
+  // at least half a CU's LDS: one persistent workgroup per CU (two would share its SIMDs)
+  a.lds_bytes = (int32_t)std::max<size_t>(lds, 96 * 1024);
+  const size_t N = (size_t)c->st.N;
+  const size_t ew = (N + 31) / 32;
+  for (size_t s = 0; s < tr.sigs.size(); ++s) tr.sigs[s].elig_word = (int32_t)(s * ew);
+  const kgpu::TPlan* dpl;
+  const int32_t* dax;
+  const kgpu::TLook* dlk;
+  const kgpu::TTab* dtb;
+  const kgpu::TDelta* ddl;
+  const kgpu::THist* dh;
+  const kgpu::TSig* dsg;
+  const kgpu::TReg* drg;
+  const int32_t* dpo;
+  if ((rc = upload_vec(c, c->t_plans, tr.plans, &dpl)) || (rc = upload_vec(c, c->t_aux, tr.aux.v, &dax)) ||
+      (rc = upload_vec(c, c->t_plan_of, tr.plan_of, &dpo)) ||
+      (rc = upload_vec(c, c->t_looks, tr.looks.v, &dlk)) || (rc = upload_vec(c, c->t_hists, tr.hists, &dh)) ||
+      (rc = upload_vec(c, c->t_tabs, tr.tabs.v, &dtb)) || (rc = upload_vec(c, c->t_deltas, tr.deltas.v, &ddl)) ||
+      (rc = upload_vec(c, c->t_sigs, tr.sigs, &dsg)) || (rc = upload_vec(c, c->t_regs, tr.regs, &drg)))
+    return rc;
+  a.plans = dpl;
+  a.plan_of = dpo;
+  a.aux = dax;
+  a.looks = dlk;
+  a.tabs = dtb;
+  a.deltas = ddl;
+  a.hists = dh;
+  a.sigs = dsg;
+  a.regs = drg;
+  // zeroed region: hist_init | tot_init | reg_init | sig_any | elig | granules
+  const size_t b_hist = a16((size_t)std::max(tr.lds_bins, 1) * 4), b_tot = a16(std::max<size_t>(tr.hists.size(), 1) * 4);
+  const size_t b_reg = a16((size_t)std::max(tr.reg_words, 1) * 4), b_sany = a16(std::max<size_t>(tr.sigs.size(), 1) * 4);
+  const size_t b_elig = a16(std::max<size_t>(tr.sigs.size() * ew, 1) * 4);
+  const size_t b_gran = (size_t)count * (size_t)(a.R + 1) * (size_t)groups * 8;
+  const size_t total = b_hist + b_tot + b_reg + b_sany + b_elig + b_gran;
+  if ((rc = ensure(c, c->t_zero, total))) return rc;
+  HIP_OK(c, hipMemsetAsync(c->t_zero.p, 0, total, c->stream));
+  char* z = static_cast<char*>(c->t_zero.p);
+  a.hist_init = reinterpret_cast<int32_t*>(z);
+  a.tot_init = reinterpret_cast<int32_t*>(z + b_hist);
+  a.reg_init = reinterpret_cast<uint32_t*>(z + b_hist + b_tot);
+  a.sig_any = reinterpret_cast<int32_t*>(z + b_hist + b_tot + b_reg);
+  a.elig = reinterpret_cast<uint32_t*>(z + b_hist + b_tot + b_reg + b_sany);
+  a.gran = reinterpret_cast<uint64_t*>(z + b_hist + b_tot + b_reg + b_sany + b_elig);
+  a.abort = abort_word;
+  a.trace = nullptr;
+  if (c->phase_trace) {
+    if ((rc = ensure(c, c->trace, sizeof(int64_t) * 16 * (size_t)(count + 1)))) return rc;
+    HIP_OK(c, hipMemsetAsync(c->trace.p, 0, sizeof(int64_t) * 16 * (size_t)(count + 1), c->stream));
+    a.trace = static_cast<int64_t*>(c->trace.p);
+    c->trace_host.assign((size_t)(count + 1) * 16, 0);
+  }
+  if (kgpu::launch_tbatch(static_cast<const DevState*>(c->dstate.p), a, groups, geo, c->spec, c->stream))
+    return fail(c, KGPU_E_DEVICE, std::string("k_tbatch launch failed: ") + hipGetErrorString(hipGetLastError()));
+  if (a.trace)
+    HIP_OK(c, hipMemcpyAsync(c->trace_host.data(), a.trace, sizeof(int64_t) * 16 * (size_t)(count + 1),
+                             hipMemcpyDeviceToHost, c->stream));
+  return KGPU_OK;
+}
+
 int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools* pools, int64_t first_seq,
               kgpu_result* results, kgpu_stats* stats, bool diag, int32_t assume) {
   if (!c->uploaded) return fail(c, KGPU_E_STATE, "no snapshot uploaded");
@@ -715,12 +1195,43 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
     return KGPU_OK;
   };
   bool used_persistent = false;
+  // one abort word for every persistent run of this batch (OR-ed on the device)
+  int rc_abort = ensure(c, c->abort_buf, 64);
+  if (rc_abort) return rc_abort;
+  HIP_OK(c, hipMemsetAsync(c->abort_buf.p, 0, 64, c->stream));
+  int32_t* abort_word = static_cast<int32_t*>(c->abort_buf.p);
+  int tper = 0, tgroups = 0;
+  const int tgeo = (topo_on && c->tfast && !diag && !sharded && !cut && st.K <= 64)
+                       ? kgpu::tbatch_geometry(st.N, std::min(c->max_groups > 0 ? std::min(c->max_groups, c->n_cus) : c->n_cus, 256),
+                                               &tper, &tgroups)
+                       : -1;
+  std::deque<TRun> runs;
+  int32_t scratch_zeroed_for = -1;
   int32_t i = 0;
   while (i < n) {
     int32_t j = i;
+    if (topo[(size_t)i] && tgeo >= 0) {
+      runs.emplace_back();  // kept until the stream is synchronized (async copies read its vectors)
+      TRun& tr = runs.back();
+      kgpu_pools empty{};
+      const kgpu_pools* pp = pools ? pools : &empty;
+      while (j < n && topo[(size_t)j] && t_add(tr, c, qs[j], plans[(size_t)j], pp, aux, aux_terms, j)) ++j;
+      if (j > i) {
+        if (c->timing) HIP_OK(c, hipEventRecord(get_event(c, ev), c->stream));
+        if ((rc = run_tbatch(c, tr, i, j - i, first_seq, assume, tper, tgroups, tgeo, abort_word))) return rc;
+        if (c->timing) HIP_OK(c, hipEventRecord(get_event(c, ev + 1), c->stream));
+        ev += 2;
+        timed_passes += j - i;
+        used_persistent = true;
+        i = j;
+        continue;
+      }
+    }
     if (topo[(size_t)i]) {
       const kgpu::QPlan& pl = plans[(size_t)i];
-      if (i == 0 || !topo[(size_t)i - 1])
+      // the previous pod's resolve launch zeroes this pod's scratch only when it went through this
+      // pipeline too (a persistent topology run in between leaves it dirty)
+      if (scratch_zeroed_for != i)
         HIP_OK(c, hipMemsetAsync(c->st.scratch, 0, sizeof(int64_t) * (size_t)pl.scratch_len, c->stream));
       int64_t min_values = 0;
       for (int k = 0; k < pl.n_hard; ++k)
@@ -745,6 +1256,7 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
                             static_cast<unsigned long long*>(c->gbar.p), c->bar_base, c->cfg.n_filters, c->stream))
         return fail(c, KGPU_E_DEVICE, "topology pipeline launch failed");
       if (c->topo_fused && !cut) c->bar_base += (unsigned long long)kgpu::topo_barriers(min_values) * (unsigned long long)blocks;
+      scratch_zeroed_for = next > 0 ? i + 1 : -1;
       if (c->timing) HIP_OK(c, hipEventRecord(get_event(c, ev + 1), c->stream));
       ev += 2;
       ++timed_passes;
@@ -755,20 +1267,20 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
       // a run of pods with constant normalize maxima: one persistent launch
       while (j < n && !norm[(size_t)j] && !topo[(size_t)j]) ++j;
       const int32_t cnt = j - i;
-      // layout: abort word (64 B) | granules [cnt][groups] u64 | feasible counts [cnt][groups] i32
+      // layout: granules [cnt][groups] u64 | feasible counts [cnt][groups] i32
       const size_t cells = (size_t)cnt * (size_t)groups;
-      const size_t gbytes = 64 + sizeof(uint64_t) * cells + sizeof(int32_t) * cells;
+      const size_t gbytes = sizeof(uint64_t) * cells + sizeof(int32_t) * cells;
       if ((rc = ensure(c, c->gran, gbytes))) return rc;
-      HIP_OK(c, hipMemsetAsync(c->gran.p, 0, 64 + sizeof(uint64_t) * cells, c->stream));
+      HIP_OK(c, hipMemsetAsync(c->gran.p, 0, sizeof(uint64_t) * cells, c->stream));
       kgpu::BatchArgs ba{};
       ba.first = i;
       ba.count = cnt;
       ba.per = per;
       ba.assume = assume;
       ba.seq0 = first_seq + i;
-      ba.gran = static_cast<uint64_t*>(c->gran.p) + 8;
+      ba.gran = static_cast<uint64_t*>(c->gran.p);
       ba.feas = reinterpret_cast<int32_t*>(ba.gran + cells);
-      ba.abort = static_cast<int32_t*>(c->gran.p);
+      ba.abort = abort_word;
       ba.trace = nullptr;
       if (c->phase_trace) {
         if ((rc = ensure(c, c->trace, sizeof(int64_t) * 16 * (size_t)(cnt + 1)))) return rc;
@@ -782,7 +1294,6 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
       if (c->timing) HIP_OK(c, hipEventRecord(get_event(c, ev + 1), c->stream));
       ev += 2;
       timed_passes += cnt;
-      HIP_OK(c, hipMemcpyAsync(&c->abort_host, c->gran.p, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
       if (ba.trace)
         HIP_OK(c, hipMemcpyAsync(c->trace_host.data(), ba.trace, sizeof(int64_t) * 16 * (size_t)(cnt + 1),
                                  hipMemcpyDeviceToHost, c->stream));
@@ -830,9 +1341,17 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
   }
   HIP_OK(c, hipEventRecord(t1, c->stream));
   HIP_OK(c, hipMemcpyAsync(results, st.results, sizeof(kgpu_result) * (size_t)n, hipMemcpyDeviceToHost, c->stream));
+  if (used_persistent)
+    HIP_OK(c, hipMemcpyAsync(&c->abort_host, abort_word, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
   HIP_OK(c, hipStreamSynchronize(c->stream));
-  if (used_persistent && c->abort_host)
-    return fail(c, KGPU_E_DEVICE, "persistent batch kernel lost co-residency (workgroups not all resident)");
+  if (used_persistent && c->abort_host) {
+    // Pods resolved before the abort have already been assumed on the device, but their results
+    // were never returned: the mirror no longer matches the caller's records.  Refuse further
+    // cycles until the snapshot is uploaded again.
+    c->uploaded = false;
+    return fail(c, KGPU_E_DEVICE, "persistent kernel gave up waiting for a workgroup (lost co-residency); the device "
+                                  "mirror is invalid: re-upload the snapshot");
+  }
   if (stats) {
     float ms = 0.f;
     HIP_OK(c, hipEventElapsedTime(&ms, t0, t1));
@@ -984,7 +1503,9 @@ int kgpu_destroy(kgpu_ctx* c) {
   for (DevBuf* b : {&c->dstate, &c->queries, &c->reqs, &c->ints, &c->words, &c->node_terms, &c->pref_terms, &c->spreads,
                     &c->pod_terms, &c->scalars, &c->ports, &c->results, &c->gran, &c->trace, &c->d_classes,
                     &c->d_citems, &c->d_tclasses, &c->d_creqs, &c->d_cints, &c->d_plans, &c->d_aux,
-                    &c->d_aux_terms, &c->scratch, &c->d_pods, &c->gbar, &c->cut_buf})
+                    &c->d_aux_terms, &c->scratch, &c->d_pods, &c->gbar, &c->cut_buf, &c->t_plans, &c->t_aux,
+                    &c->t_looks, &c->t_tabs, &c->t_deltas, &c->t_hists, &c->t_sigs, &c->t_regs, &c->t_zero,
+                    &c->abort_buf, &c->t_plan_of})
     if (b->p) (void)hipFree(b->p);
   if (c->st.mcnt) (void)hipFree(c->st.mcnt);
   if (c->st.tcnt) (void)hipFree(c->st.tcnt);
@@ -1014,6 +1535,7 @@ int kgpu_set_option(kgpu_ctx* c, int32_t option, int64_t value) {
   else if (option == KGPU_OPT_PERSIST_GROUPS) c->max_groups = (int)std::max<int64_t>(value, 0);
   else if (option == KGPU_OPT_PHASE_TRACE) c->phase_trace = value != 0;
   else if (option == KGPU_OPT_TOPO_FUSED) c->topo_fused = value != 0;
+  else if (option == KGPU_OPT_TOPO_PERSISTENT) c->tfast = value != 0;
   else return KGPU_E_INVAL;
   return KGPU_OK;
 }
@@ -1130,6 +1652,21 @@ int kgpu_upload_snapshot(kgpu_ctx* c, const kgpu_snapshot* s, int64_t generation
   c->key_n_values.assign(s->key_n_values ? s->key_n_values : nullptr, s->key_n_values ? s->key_n_values + st.K : nullptr);
   c->key_empty.assign(s->key_empty_value ? s->key_empty_value : nullptr,
                       s->key_empty_value ? s->key_empty_value + st.K : nullptr);
+  c->key_unique.assign((size_t)st.K, 0);
+  for (int k = 0; k < st.K; ++k) {
+    // a key is node-unique when no value labels two nodes (and no node's value is "", which a node
+    // missing the key also stands for in PodTopologySpread's counts)
+    if (c->key_empty[(size_t)k] >= 0) continue;
+    std::vector<uint8_t> seen((size_t)std::max(c->key_n_values[(size_t)k], 1), 0);
+    bool uniq = true;
+    for (size_t i = 0; i < N && uniq; ++i) {
+      const int32_t v = s->label_val[(size_t)k * N + i];
+      if (v < 0) continue;
+      if (v >= (int32_t)seen.size() || seen[(size_t)v]) uniq = false;
+      else seen[(size_t)v] = 1;
+    }
+    c->key_unique[(size_t)k] = uniq ? 1 : 0;
+  }
   c->class_ids.clear();
   c->tclass_ids.clear();
   c->classes.clear();

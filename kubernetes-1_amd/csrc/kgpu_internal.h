@@ -245,6 +245,123 @@ struct BatchArgs {
                         // granule published, iteration end
 };
 
+// ---------------------------------------------------------------- persistent topology kernel
+// k_tbatch schedules a run of PodTopologySpread / InterPodAffinity / DefaultPodTopologySpread pods
+// inside ONE launch.  Every topologyPair -> count map those plugins build per cycle is a
+// pod-independent DOMAIN HISTOGRAM of a match-count column: H[col][key][v] = sum over the nodes
+// whose label `key` has value v of col[n] (col = a pod class of mcnt or a term class of tcnt;
+// bin D = nodes without the key), optionally restricted to the nodes a pod's NodeAffinity admits
+// (PodTopologySpread's ScheduleAnyway counts).  Histograms over keys with few values live in LDS,
+// one replica per workgroup, and every workgroup applies the same +1 deltas after each winner;
+// keys whose every value sits on at most one node (hostname-like) need no histogram: the owner
+// lane reads the node's own column.  Per pod: one pass over the register-resident node rows
+// (filters + raw scores), one granule round for the normalize statistics, one for selectHost.
+constexpr int kTMaxSoftWords = 8;   // shared ScheduleAnyway key: <= 256 domains (OR-ed bitmask)
+constexpr int kTMaxZones = 32;      // DefaultPodTopologySpread zone sums carried in the stats round
+constexpr int kTLdsBudget = 144 * 1024;
+
+struct THist {
+  int32_t col_kind;  // 0: mcnt pod class, 1: tcnt term class
+  int32_t col;
+  int32_t key;       // node label key
+  int32_t sig;       // -1: all nodes; else eligibility signature (TSig) the counted nodes must pass
+  int32_t D;         // distinct values of key (bins 0..D-1, bin D = key missing)
+  int32_t off;       // first LDS bin, -1: node-unique key (lookups read the node's own column)
+};
+struct TSig {
+  int32_t rep;       // query index whose nodeSelector / required NodeAffinity defines the signature
+  int32_t n_keys;
+  int32_t keys[kMaxSpread];
+  int32_t elig_word; // first uint32 word of this signature's node bitmap in TBatchArgs::elig
+  int32_t pad;
+};
+struct TReg {        // registered topology pairs of (signature, key): D-bit mask in LDS
+  int32_t sig, key, D, word;
+};
+struct TLook {       // one lookup H[col][key][label(key, n)]: LDS bins at `off`, or (off < 0, node-unique
+                     // key) the node's own column col of mcnt (col_kind 0) / tcnt (1)
+  int32_t key, weight, off, D;
+  int32_t col_kind, col, pad0, pad1;
+};
+// A per-pod lookup table over the values of one key, built in LDS before the pod's node pass
+// (int64 entries at `off`): kind 0 = TpPairToMatchNum of a DoNotSchedule key (sum over the
+// constraints on the key, 0 for unregistered pairs; `reg` = TReg), 1 = existing pods' required
+// anti-affinity counts of the key, 2 = InterPodAffinity topologyScore[key][*].
+struct TTab {
+  int32_t kind, key, D, off;
+  int32_t reg, empty_v;
+  kgpu_range terms;  // TLook aux (shared-key histograms only)
+};
+struct THard {
+  int32_t key, max_skew, self_match, tab;  // tab: index of the key's kind-0 table in the pod's tabs
+};
+struct TDelta {      // one histogram a pod increments when assumed
+  int32_t hist, off, D, key;
+  int32_t sig, pad0, pad1, pad2;
+};
+struct TPlan {
+  int32_t n_hard, hard_sig;
+  THard hard[kMaxSpread];
+  int32_t n_soft;     // 0 or 1
+  int32_t soft_mode;  // 0 shared key (LDS histogram, topoSize = registered domains),
+                      // 1 kubernetes.io/hostname (count = the node's own column, topoSize = nodes),
+                      // 2 node-unique key (own column if the node is eligible, topoSize = nodes)
+  int32_t soft_off, soft_col, soft_key, soft_max_skew, soft_sig, soft_words;
+  int32_t n_aff, self_all;
+  TLook aff[kMaxIpa];
+  int32_t n_anti, dpts_cls;
+  TLook anti[kMaxIpa];
+  int32_t aff_hist[kMaxIpa];  // THist index of each affinity term (TOT: the map is non-empty)
+  kgpu_range tabs;    // TTab aux
+  int32_t pt_words, n_exa_tabs;  // int64 words of the pod's tables; order: kind 0, kind 2, then the
+                                 // n_exa_tabs kind-1 tables
+  kgpu_range exa_u;   // TLook aux: required anti-affinity terms of existing pods on node-unique keys
+  kgpu_range score_u; // TLook aux: InterPodAffinity score terms on node-unique keys
+  kgpu_range deltas;  // TDelta aux: histograms this pod increments when assumed
+  kgpu_range assume_cls, own_tcls;  // int aux: mcnt / tcnt columns this pod increments
+  int32_t need_ipa;
+  int32_t aff_sig;    // TSig of PodMatchesNodeSelectorAndAffinityTerms alone: the NodeAffinity filter
+};
+// statistics slots of the normalize round (values are 63-bit encoded, see k_tbatch)
+enum TStat { kTFeas = 0, kTMaxT, kTMaxNA, kTNonIgn, kTAdjMin, kTAdjMax, kTIpaMin, kTIpaMax, kTDptsMax, kTZoned, kTFixed };
+constexpr int kTMaxTabs = 16;  // per-pod lookup tables
+struct TBatchArgs {
+  int32_t first, count;   // query range of the run
+  int32_t per;            // nodes owned by one workgroup
+  int32_t assume;
+  int64_t seq0;
+  const TPlan* plans;     // distinct plans of the run
+  const int32_t* plan_of; // [count] plan of each pod
+  const int32_t* aux;
+  const TLook* looks;
+  const TTab* tabs;
+  const TDelta* deltas;
+  const THist* hists;
+  int32_t n_hists, n_sigs, n_regs;
+  int32_t lds_bins;       // LDS histogram bins
+  int32_t reg_words;
+  int32_t R;              // stats slots per pod (kTFixed + soft words + zones)
+  int32_t soft_words, zones;
+  const TSig* sigs;
+  const TReg* regs;
+  int32_t* hist_init;     // [lds_bins] zeroed, filled by k_hist_init
+  int32_t* tot_init;      // [n_hists]
+  uint32_t* reg_init;     // [reg_words]
+  int32_t* sig_any;       // [n_sigs]
+  uint32_t* elig;         // [n_sigs][ceil(N/32)]
+  uint64_t* gran;         // [count][R + 1][groups] granules, zeroed before the launch
+  int32_t* abort;
+  int32_t lds_bytes;
+  int32_t def_res;        // Least/Most over {cpu: 1, memory: 1}
+  int32_t pt_words;       // largest per-pod table area of the run (int64 words)
+  int32_t n_keys;         // node label keys the run's deltas read (winner's labels staged in LDS)
+  // byte offsets of the LDS regions (histogram bins start at 0)
+  int32_t o_reg, o_tot, o_sany, o_stat, o_smask, o_zsum, o_wred, o_misc, o_pt;
+  int64_t* trace;         // null, or [count + 1][16] s_memrealtime stamps (KGPU_OPT_PHASE_TRACE): per pod
+                          // and traced workgroup (0, last): start, PreFilter minima, rows evaluated,
+                          // stats published, stats resolved, key published, winner resolved, end
+};
+
 // Host-side launchers (kgpu_kernels.hip).
 // The DevState lives in device memory (one copy per batch): kernel arguments stay at 40 bytes,
 // so no launch pulls a kilobyte of kernarg segment through the host-coherent path.
@@ -279,5 +396,9 @@ int launch_topo(const DevState* st, PodArgs a, int blocks, int64_t min_values, i
 inline int topo_barriers(int64_t min_values) { return min_values > 0 ? 5 : 4; }
 // Initialize mcnt columns [c0, c0 + nc) from the pod table (n_pods rows).
 int launch_class_init(const DevState* st, int c0, int nc, int n_pods, void* stream);
+// Persistent topology run: signature bitmaps + pair registrations (k_sig_init), histogram
+// initialization from the match-count columns (k_hist_init), then k_tbatch.  kidx: geometry.
+int tbatch_geometry(int N, int max_groups, int* per, int* groups);
+int launch_tbatch(const DevState* st, const TBatchArgs& a, int groups, int geo, int spec, void* stream);
 
 }  // namespace kgpu

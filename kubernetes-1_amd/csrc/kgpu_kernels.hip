@@ -508,26 +508,83 @@ __device__ __forceinline__ void key_max(uint64_t& k, int& i, uint64_t k2, int i2
   if (k2 > k) { k = k2; i = i2; }
 }
 
-__device__ __forceinline__ void wave_reduce_key(uint64_t& k, int& i) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    const uint64_t k2 = __shfl_xor(k, off);
-    const int i2 = __shfl_xor(i, off);
-    key_max(k, i, k2, i2);
-  }
+// Wave64 reductions on the VALU through DPP (no LDS round trip per step, unlike __shfl_xor's
+// ds_bpermute): quad_perm xor 1 and xor 2, row_half_mirror, row_mirror (every lane of a 16-lane row
+// then holds the row's result), row_bcast:15 into rows 1 and 3, row_bcast:31 into rows 2 and 3;
+// lane 63 ends with the wave's result and readlane broadcasts it.  Masked-off or out-of-row lanes
+// read 0, the identity of max (unsigned) and sum.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint32_t dpp32(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROWS, 0xF, true);
+}
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint64_t dpp64(uint64_t x) {
+  return (uint64_t)dpp32<CTRL, ROWS>((uint32_t)x) | ((uint64_t)dpp32<CTRL, ROWS>((uint32_t)(x >> 32)) << 32);
+}
+__device__ __forceinline__ uint64_t readlane64(uint64_t x, int lane) {
+  return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, lane) |
+         ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), lane) << 32);
+}
+struct OpMaxU64 {
+  __device__ __forceinline__ uint64_t operator()(uint64_t a, uint64_t b) const { return a > b ? a : b; }
+};
+struct OpSumU64 {
+  __device__ __forceinline__ uint64_t operator()(uint64_t a, uint64_t b) const { return a + b; }
+};
+template <class Op>
+__device__ __forceinline__ uint64_t wave_red64(uint64_t x, Op op) {
+  x = op(x, dpp64<0xB1, 0xF>(x));
+  x = op(x, dpp64<0x4E, 0xF>(x));
+  x = op(x, dpp64<0x141, 0xF>(x));
+  x = op(x, dpp64<0x140, 0xF>(x));
+  x = op(x, dpp64<0x142, 0xA>(x));
+  x = op(x, dpp64<0x143, 0xC>(x));
+  return readlane64(x, 63);
+}
+__device__ __forceinline__ uint32_t wave_sum32(uint32_t x) {
+  x += dpp32<0xB1, 0xF>(x);
+  x += dpp32<0x4E, 0xF>(x);
+  x += dpp32<0x141, 0xF>(x);
+  x += dpp32<0x140, 0xF>(x);
+  x += dpp32<0x142, 0xA>(x);
+  x += dpp32<0x143, 0xC>(x);
+  return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+}
+__device__ __forceinline__ uint32_t wave_max32u(uint32_t x) {
+  x = max(x, dpp32<0xB1, 0xF>(x));
+  x = max(x, dpp32<0x4E, 0xF>(x));
+  x = max(x, dpp32<0x141, 0xF>(x));
+  x = max(x, dpp32<0x140, 0xF>(x));
+  x = max(x, dpp32<0x142, 0xA>(x));
+  x = max(x, dpp32<0x143, 0xC>(x));
+  return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+}
+// signed 64-bit max / min through the order-preserving unsigned map
+__device__ __forceinline__ int64_t wave_max_i64(int64_t x) {
+  return (int64_t)(wave_red64((uint64_t)x ^ (1ull << 63), OpMaxU64{}) ^ (1ull << 63));
+}
+__device__ __forceinline__ int64_t wave_min_i64(int64_t x) {
+  return (int64_t)(~wave_red64(~((uint64_t)x ^ (1ull << 63)), OpMaxU64{}) ^ (1ull << 63));
+}
+__device__ __forceinline__ int64_t wave_sum_i64(int64_t x) { return (int64_t)wave_red64((uint64_t)x, OpSumU64{}); }
+struct OpOrU64 {
+  __device__ __forceinline__ uint64_t operator()(uint64_t a, uint64_t b) const { return a | b; }
+};
+// argmax of unique keys: the maximum, then the one lane holding it
+__device__ __forceinline__ void wave_argmax(uint64_t& k, int& i) {
+  const uint64_t m = wave_red64(k, OpMaxU64{});
+  const uint64_t b = __ballot(k == m && m != 0);
+  i = b ? __builtin_amdgcn_readlane(i, (int)__builtin_ctzll(b)) : -1;
+  k = m;
 }
 
-__device__ __forceinline__ int wave_reduce_sum(int v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-  return v;
-}
+// keys are unique per node (rank40 is a bijection), so a max + ballot finds the argmax
+__device__ __forceinline__ void wave_reduce_key(uint64_t& k, int& i) { wave_argmax(k, i); }
 
-__device__ __forceinline__ int wave_reduce_max(int v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v = max(v, __shfl_xor(v, off));
-  return v;
-}
+__device__ __forceinline__ int wave_reduce_sum(int v) { return (int)wave_sum32((uint32_t)v); }
+
+// non-negative values only (raw TaintToleration / NodeAffinity scores, counts)
+__device__ __forceinline__ int wave_reduce_max(int v) { return (int)wave_max32u((uint32_t)max(v, 0)); }
 
 struct Winner {
   uint64_t key;
@@ -950,13 +1007,8 @@ struct Cand {
 };
 
 __device__ __forceinline__ void wave_reduce_cand(Cand& c) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    const uint64_t k2 = __shfl_xor(c.key, off);
-    const int i2 = __shfl_xor(c.idx, off);
-    c.feas += __shfl_xor(c.feas, off);
-    if (k2 > c.key) { c.key = k2; c.idx = i2; }
-  }
+  c.feas = wave_reduce_sum(c.feas);
+  wave_argmax(c.key, c.idx);
 }
 
 template <int B>
@@ -1050,12 +1102,7 @@ __device__ __forceinline__ bool poll_row(const uint64_t* row, int G, const int32
       }
     }
     if (__all(all)) {
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) {
-        const uint64_t k2 = __shfl_xor(k, off);
-        const int g2 = __shfl_xor(gsel, off);
-        if (k2 > k) { k = k2; gsel = g2; }
-      }
+      wave_argmax(k, gsel);
       wkey = k;
       wg = k ? gsel : -1;
       return true;
@@ -1079,7 +1126,12 @@ __global__ __launch_bounds__(B) void k_batch(const DevState* __restrict__ stp, B
   for (int j = 0; j < K; ++j) {
     const int n = lo + j * B + tid;
     r[j] = NodeRes{};
-    if (n < st.N) r[j] = load_res(st, n);
+    if (n < st.N) {
+      r[j] = load_res(st, n);
+      // Allocatable never changes inside the run: LeastAllocated / MostAllocated divide through
+      // exact reciprocal-plus-remainder-correction division (div_recip)
+      if constexpr ((SM & kDefRes) != 0 && SM != kRuntime) set_recips(r[j]);
+    }
   }
   // phase stamps (diagnostics): per iteration i, 8 per traced workgroup (0 and last):
   // start, evaluated, pod i-1 resolved, pod i published, iteration end
@@ -1109,6 +1161,7 @@ __global__ __launch_bounds__(B) void k_batch(const DevState* __restrict__ stp, B
         const int n = lo + j * B + tid;
         keys[j] = n < st.N ? node_key<FM, SM>(st, q, r[j], n, tk) : 0;
       }
+      KGPU_STAMP(i, 5);
       if (fast_b && tid == ob) {
 #pragma unroll
         for (int j = 0; j < K; ++j)
@@ -1118,6 +1171,7 @@ __global__ __launch_bounds__(B) void k_batch(const DevState* __restrict__ stp, B
             keyb = node_key<FM, SM>(st, q, rb, lo + cand, tk);
           }
       }
+      KGPU_STAMP(i, 6);
       wg_partials<K, B>(sh, keys, tid, fast_b, ob, jb, keyb);
     }
     KGPU_STAMP(i, 1);
@@ -1410,8 +1464,7 @@ __device__ __forceinline__ void topo_min(const DevState* __restrict__ stp, PodAr
     const int64_t* cnt = slot_ptr(st, pl, c.cslot);
     for (int v = blockIdx.x * kBlock + threadIdx.x; v < nv; v += gridDim.x * kBlock)
       if (reg[v] && cnt[v] < mn) mn = cnt[v];
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) mn = min(mn, (int64_t)__shfl_xor(mn, off));
+    mn = wave_min_i64(mn);
     if (threadIdx.x == 0 && mn != INT64_MAX) amin64(&h->pmin[i], mn);
   }
 }
@@ -1554,14 +1607,11 @@ __device__ __forceinline__ void topo_score(const DevState* __restrict__ stp, Pod
       gp(st.diag_raw)[(size_t)KGPU_S_DEFAULT_POD_TOPOLOGY_SPREAD * st.N + n] = pl.dpts_cls == -2 ? 0 : ds;
     }
   }
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    pmn = min(pmn, (int64_t)__shfl_xor(pmn, off));
-    pmx = max(pmx, (int64_t)__shfl_xor(pmx, off));
-    imn = min(imn, (int64_t)__shfl_xor(imn, off));
-    imx = max(imx, (int64_t)__shfl_xor(imx, off));
-    dmx = max(dmx, (int64_t)__shfl_xor(dmx, off));
-  }
+  pmn = wave_min_i64(pmn);
+  pmx = wave_max_i64(pmx);
+  imn = wave_min_i64(imn);
+  imx = wave_max_i64(imx);
+  dmx = wave_max_i64(dmx);
   const bool zw = __any(zoned);
   if (threadIdx.x == 0) {
     if (pmx != INT64_MIN) {
@@ -1606,8 +1656,7 @@ __device__ __forceinline__ void topo_final(const DevState* __restrict__ stp, Pod
   int64_t dmax_zone = 0;
   if (pl.dpts_cls >= 0 && h->have_zones)
     for (int z = threadIdx.x; z < st.n_zones; z += kBlock) dmax_zone = max(dmax_zone, zone_sums(st)[z]);
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) dmax_zone = max(dmax_zone, (int64_t)__shfl_xor(dmax_zone, off));
+  dmax_zone = wave_max_i64(dmax_zone);
   const double M = 100.0, zwt = 2.0 / 3.0;
   int lo, hi;
   chunk_of(st.N, lo, hi);
@@ -1811,6 +1860,604 @@ int launch_class_init(const DevState* st, int c0, int nc, int n_pods, void* stre
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// ---------------------------------------------------------------- persistent topology kernel
+// (kgpu_internal.h "persistent topology kernel").  Reference semantics, per plugin:
+//   PodTopologySpread  PreFilter/Filter podtopologyspread/filtering.go:146-328 (TpPairToMatchNum,
+//                      criticalPaths, skew), PreScore/Score/Normalize scoring.go:59-257
+//   InterPodAffinity   PreFilter/Filter interpodaffinity/filtering.go:166-396,
+//                      PreScore/Score/Normalize scoring.go:47-272
+//   DefaultPodTopologySpread default_pod_topology_spread.go:75-163
+// Every per-cycle map of those plugins is read from a domain histogram (THist) instead of being
+// rebuilt: TpPairToMatchNum[(k, v)] = sum over the pod's DoNotSchedule constraints on k of
+// H[v] (+ the key-missing bin when v is "", since node.Labels[k] of a missing key is ""), the
+// affinity maps are H[...] > 0, topologyScore[k][v] = sum of weight * H[v].
+__device__ __forceinline__ uint64_t rank40_inv(uint64_t k, uint64_t x, int mode) {
+  // inverse of rank40 (every step is a bijection on 40 bits)
+  if (mode == 1) return kMask40 - x;
+  x ^= (k >> 24) & kMask40;
+  x ^= x >> 23;                                      // 2 * 23 > 40
+  x = (x * 0x38E12D471Bull) & kMask40;               // 0x94D049BB13^-1 mod 2^40
+  x ^= (x >> 19) ^ (x >> 38);
+  x = (x * 0xB38E39396Dull) & kMask40;               // 0xD6E8FEB865^-1 mod 2^40
+  x ^= k & kMask40;
+  return x;
+}
+
+__device__ __forceinline__ bool tb_elig(const TBatchArgs& ta, int sig, int n) {
+  const TSig sg = cp(ta.sigs)[sig];
+  return (gp(ta.elig)[sg.elig_word + (n >> 5)] >> (n & 31)) & 1u;
+}
+
+// signature bitmaps (nodes a pod's nodeSelector / required NodeAffinity admits that carry every
+// key of the signature: filtering.go:229-238, scoring.go:143-150) and the DoNotSchedule pair
+// registrations of each (signature, key) (filtering.go:239-243).
+__global__ void k_sig_init(const DevState* __restrict__ stp, TBatchArgs ta) {
+  const DevState& st = *stp;
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= st.N) return;
+  for (int s = 0; s < ta.n_sigs; ++s) {
+    const TSig sg = cp(ta.sigs)[s];
+    bool ok = sg.n_keys >= 0 && node_affinity_ok(st, *cp(st.queries + sg.rep), n);
+    for (int k = 0; k < sg.n_keys && ok; ++k) ok = sg.keys[k] >= 0 && gp(st.label_val)[(size_t)sg.keys[k] * st.N + n] >= 0;
+    if (!ok) continue;
+    atomicOr(gp(ta.elig) + sg.elig_word + (n >> 5), 1u << (n & 31));
+    __hip_atomic_store(gp(ta.sig_any) + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int r = 0; r < ta.n_regs; ++r) {
+      const TReg rg = cp(ta.regs)[r];
+      if (rg.sig != s) continue;
+      const int v = gp(st.label_val)[(size_t)rg.key * st.N + n];
+      atomicOr(gp(ta.reg_init) + rg.word + (v >> 5), 1u << (v & 31));
+    }
+  }
+}
+
+__device__ __forceinline__ const int32_t* tb_col(const DevState& st, const THist& h) {
+  return (h.col_kind == 0 ? st.mcnt : st.tcnt) + (size_t)h.col * st.N;
+}
+
+// domain histograms (and their totals over the nodes carrying the key) from the columns
+__global__ void k_hist_init(const DevState* __restrict__ stp, TBatchArgs ta) {
+  const DevState& st = *stp;
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= st.N) return;
+  for (int i = 0; i < ta.n_hists; ++i) {
+    const THist h = cp(ta.hists)[i];
+    const int c = gp(tb_col(st, h))[n];
+    if (!c) continue;
+    if (h.sig >= 0 && !tb_elig(ta, h.sig, n)) continue;
+    const int v = h.key >= 0 ? gp(st.label_val)[(size_t)h.key * st.N + n] : -1;
+    if (h.off >= 0) atomicAdd(gp(ta.hist_init) + h.off + (v >= 0 ? v : h.D), c);
+    if (v >= 0) atomicAdd(gp(ta.tot_init) + i, c);
+  }
+}
+
+// 63-bit order-preserving payloads of the statistics granules
+constexpr int64_t kEncBias = 1ll << 62;
+__device__ __forceinline__ uint64_t enc_stat(int64_t x) { return kGValid | (uint64_t)(x + kEncBias); }
+__device__ __forceinline__ int64_t dec_stat(uint64_t g) { return (int64_t)(g & ~kGValid) - kEncBias; }
+enum { kOpSum = 0, kOpMax, kOpMin, kOpOr };
+__device__ __forceinline__ int tstat_op(int r) {
+  switch (r) {
+    case kTMaxT: case kTMaxNA: case kTAdjMax: case kTIpaMax: case kTDptsMax: case kTZoned: return kOpMax;
+    case kTAdjMin: case kTIpaMin: return kOpMin;
+    case kTFeas: case kTNonIgn: return kOpSum;
+    default: return r < kTFixed + kTMaxSoftWords ? kOpOr : kOpSum;  // resolved by the caller's layout
+  }
+}
+__device__ __forceinline__ int64_t tcombine(int op, int64_t a, int64_t b) {
+  switch (op) {
+    case kOpSum: return a + b;
+    case kOpMax: return a > b ? a : b;
+    case kOpMin: return a < b ? a : b;
+    default: return a | b;
+  }
+}
+__device__ __forceinline__ int64_t wave_op_i64(int op, int64_t x) {
+  switch (op) {
+    case kOpSum: return wave_sum_i64(x);
+    case kOpMax: return wave_max_i64(x);
+    case kOpMin: return wave_min_i64(x);
+    default: return (int64_t)wave_red64((uint64_t)x, OpOrU64{});
+  }
+}
+__device__ __forceinline__ int64_t tident(int op) {
+  return op == kOpMax ? INT64_MIN / 4 : (op == kOpMin ? INT64_MAX / 4 : 0);
+}
+
+struct TMisc {
+  int64_t pmin[kTMaxTabs];   // criticalPaths[0].MatchNum per kind-0 table (MaxInt32 when none)
+  uint64_t wkey;             // winning key of the pod (0: no feasible node)
+  int32_t wg, wnode;         // its workgroup, its global node index
+  int32_t abort, pad;
+  uint64_t akey[16];         // per-wave argmax partials
+  int32_t aidx[16];
+  int32_t wlab[64];          // the winner's value of each key the run's deltas read (-1 absent)
+  int32_t welig[64];         // the winner's eligibility under each signature
+  // statistics accumulated across the waves (LDS atomics), kTFixed slots
+  int32_t acc32[8];          // kTFeas, kTMaxT, kTMaxNA, kTNonIgn, kTAdjMin (as ~min), kTAdjMax, kTDptsMax, kTZoned
+  int64_t acc64[2];          // kTIpaMin, kTIpaMax
+};
+
+// Wave `w` polls statistics slots w, w + waves, ... of pod row `row`: every workgroup's granule
+// of the slot, combined with the slot's operation.  False on timeout / abort.
+__device__ __forceinline__ bool tpoll_slot(const uint64_t* row, int G, const int32_t* abort_word, int op,
+                                           int64_t& out) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  for (;;) {
+    bool all = true;
+    int64_t acc = tident(op);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int g = lane + 64 * j;
+      if (g < G) {
+        const uint64_t v = load_sc1(row + g);
+        if (!(v & kGValid)) all = false;
+        else acc = tcombine(op, acc, dec_stat(v));
+      }
+    }
+    if (__all(all)) {
+      out = wave_op_i64(op, acc);
+      return true;
+    }
+    if (load_sc1(abort_word) != 0 || __builtin_amdgcn_s_memrealtime() - t0 > kSpinTimeout) return false;
+  }
+}
+
+__device__ __forceinline__ int64_t tcol(const DevState& st, const TLook& t, int n) {
+  return gp((t.col_kind == 0 ? st.mcnt : st.tcnt) + (size_t)t.col * st.N)[n];
+}
+
+// H[col][key][v] of one lookup at node n (v = label(key, n) >= 0)
+__device__ __forceinline__ int64_t tval(const DevState& st, const int32_t* H, const TLook& t, int v, int n) {
+  return t.off >= 0 ? (int64_t)H[t.off + v] : tcol(st, t, n);
+}
+
+// Score plugins of the pod outside the topology three (which k_tbatch normalizes itself).
+constexpr uint32_t kTopoSM = (1u << KGPU_S_POD_TOPOLOGY_SPREAD) | (1u << KGPU_S_INTER_POD_AFFINITY) |
+                             (1u << KGPU_S_DEFAULT_POD_TOPOLOGY_SPREAD);
+template <uint32_t SM, bool kDef>
+__device__ __forceinline__ void tscores(const DevState& st, const kgpu_pod_query& q, const NodeRes& r, int n, NodeEval& e) {
+  if constexpr (SM == kRuntime) {
+    int64_t p = 0;
+    for (int si = 0; si < st.n_scores; ++si) {
+      const int s = cp(st.scores)[si];
+      if ((kTopoSM >> s) & 1u) continue;
+      const int64_t v = score_one<kDef>(s, st, q, r, n, e);
+      if (!normalized(s)) p += v * cp(st.w_of)[s];
+    }
+    e.partial = p;
+  } else {
+    run_scores<SM & ~kTopoSM>(st, q, r, n, e, false);
+  }
+}
+
+// One node of the pod: filters in profile order (PodTopologySpread / InterPodAffinity read the
+// pod's LDS tables) and the raw scores.  Returns the status word.
+struct TRow {
+  int64_t part, adj, ipa;
+  int32_t taint, na, ds, pad;
+};
+template <uint32_t FM, uint32_t SM, bool kDef>
+__device__ __forceinline__ uint32_t trow_eval(const DevState& st, const TBatchArgs& ta, const kgpu_pod_query& q,
+                                         const TPlan& tp, const NodeRes& r, int n, const int32_t* H,
+                                         const int64_t* PT, const TMisc& M, bool pany, bool aff_any, TRow& o) {
+  auto pts = [&]() -> uint32_t {  // filtering.go:276-328
+    if (!pany) return 0;
+    for (int c = 0; c < tp.n_hard; ++c) {
+      const THard hc = tp.hard[c];
+      const int v = nval(st, hc.key, n);
+      if (v < 0) return KGPU_CODE_UNSCHEDULABLE << 8;
+      const TTab tb = cp(ta.tabs)[tp.tabs.begin + hc.tab];
+      if (PT[tb.off + v] + hc.self_match - M.pmin[hc.tab] > hc.max_skew) return KGPU_CODE_UNSCHEDULABLE << 8;
+    }
+    return 0;
+  };
+  auto ipa = [&]() -> uint32_t {  // filtering.go:314-396
+    bool exist = true;
+    for (int a = 0; a < tp.n_aff; ++a) {
+      const TLook t = tp.aff[a];
+      const int v = nval(st, t.key, n);
+      if (v < 0) return (KGPU_CODE_UNRESOLVABLE << 8) | (1u << 16);
+      if (tval(st, H, t, v, n) <= 0) exist = false;
+    }
+    if (!exist && !(!aff_any && tp.self_all)) return (KGPU_CODE_UNRESOLVABLE << 8) | (1u << 16);
+    for (int a = 0; a < tp.n_anti; ++a) {
+      const TLook t = tp.anti[a];
+      const int v = nval(st, t.key, n);
+      if (v >= 0 && tval(st, H, t, v, n) > 0) return (KGPU_CODE_UNSCHEDULABLE << 8) | (2u << 16);
+    }
+    for (int k = 0; k < tp.n_exa_tabs; ++k) {
+      const TTab tb = cp(ta.tabs)[tp.tabs.begin + tp.tabs.count - tp.n_exa_tabs + k];
+      const int v = nval(st, tb.key, n);
+      if (v >= 0 && PT[tb.off + v] > 0) return (KGPU_CODE_UNSCHEDULABLE << 8) | (3u << 16);
+    }
+    for (int e = 0; e < tp.exa_u.count; ++e) {
+      const TLook t = cp(ta.looks)[tp.exa_u.begin + e];
+      if (nval(st, t.key, n) >= 0 && tcol(st, t, n) > 0) return (KGPU_CODE_UNSCHEDULABLE << 8) | (3u << 16);
+    }
+    return 0;
+  };
+  // NodeAffinity (node_affinity.go:53-62): the pod's selector program was evaluated once per run for
+  // every node (k_sig_init); here it is one bit
+  auto one = [&](int f) -> uint32_t {
+    if (f == KGPU_F_POD_TOPOLOGY_SPREAD) return pts();
+    if (f == KGPU_F_INTER_POD_AFFINITY) return ipa();
+    if (f == KGPU_F_NODE_AFFINITY) return tb_elig(ta, tp.aff_sig, n) ? 0 : KGPU_CODE_UNRESOLVABLE << 8;
+    return filter_one(f, st, q, r, n);
+  };
+  uint32_t status = 0;
+  if constexpr (FM == kRuntime) {
+    for (int fi = 0; fi < st.n_filters && !status; ++fi) {
+      status = one(cp(st.filters)[fi]);
+      if (status) status |= (uint32_t)(fi + 1);
+    }
+  } else {
+    // the default order: ascending plugin id (select_spec picks this instantiation only then)
+    uint32_t pos = 0;
+#pragma unroll
+    for (int f = 0; f < KGPU_NUM_FILTERS; ++f) {
+      if (!((FM >> f) & 1u)) continue;
+      ++pos;
+      if (status) continue;
+      status = one(f);
+      if (status) status |= pos;
+    }
+  }
+  if (status) return status;
+  NodeEval e{0, 0, 0, 0};
+  tscores<SM, kDef>(st, q, r, n, e);
+  o.part = e.partial;
+  o.taint = e.taint;
+  o.na = e.na;
+  // PodTopologySpread ScheduleAnyway (scoring.go:75-102,174-208): INT64_MIN = ignored node
+  o.adj = 0;
+  if (tp.n_soft) {
+    const int v = nval(st, tp.soft_key, n);
+    if (v < 0) {
+      o.adj = INT64_MIN;
+    } else {
+      int64_t cnt;
+      if (tp.soft_mode == 0) cnt = H[tp.soft_off + v];
+      else if (tp.soft_mode == 1) cnt = gp(st.mcnt)[(size_t)tp.soft_col * st.N + n];
+      else cnt = tb_elig(ta, tp.soft_sig, n) ? gp(st.mcnt)[(size_t)tp.soft_col * st.N + n] : 0;
+      o.adj = cnt < tp.soft_max_skew ? tp.soft_max_skew - 1 : cnt;  // adjustForMaxSkew
+    }
+  }
+  // InterPodAffinity topologyScore (scoring.go:217-236)
+  int64_t is = 0;
+  if (tp.need_ipa) {
+    for (int k = 0; k < tp.tabs.count - tp.n_exa_tabs; ++k) {
+      const TTab tb = cp(ta.tabs)[tp.tabs.begin + k];
+      if (tb.kind != 2) continue;
+      const int v = nval(st, tb.key, n);
+      if (v >= 0) is += PT[tb.off + v];
+    }
+    for (int e2 = 0; e2 < tp.score_u.count; ++e2) {
+      const TLook t = cp(ta.looks)[tp.score_u.begin + e2];
+      if (nval(st, t.key, n) >= 0) is += (int64_t)t.weight * tcol(st, t, n);
+    }
+  }
+  o.ipa = is;
+  o.ds = tp.dpts_cls >= 0 ? gp(st.mcnt)[(size_t)tp.dpts_cls * st.N + n] : 0;
+  return 0;
+}
+
+template <int B, int K, uint32_t FM, uint32_t SM, bool kDef>
+__global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, TBatchArgs ta) {
+  const DevState& st = *stp;
+  extern __shared__ __attribute__((aligned(16))) char lds_raw[];
+  int32_t* H = reinterpret_cast<int32_t*>(lds_raw);
+  uint32_t* REG = reinterpret_cast<uint32_t*>(lds_raw + ta.o_reg);
+  int32_t* TOT = reinterpret_cast<int32_t*>(lds_raw + ta.o_tot);
+  int32_t* SANY = reinterpret_cast<int32_t*>(lds_raw + ta.o_sany);
+  int64_t* STAT = reinterpret_cast<int64_t*>(lds_raw + ta.o_stat);
+  uint32_t* SMASK = reinterpret_cast<uint32_t*>(lds_raw + ta.o_smask);
+  int32_t* ZSUM = reinterpret_cast<int32_t*>(lds_raw + ta.o_zsum);
+  int64_t* PT = reinterpret_cast<int64_t*>(lds_raw + ta.o_pt);
+  TMisc& M = *reinterpret_cast<TMisc*>(lds_raw + ta.o_misc);
+  constexpr int W = B / 64;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int G = gridDim.x, g = blockIdx.x;
+  const int lo = g * ta.per;
+
+  for (int i = tid; i < ta.lds_bins; i += B) H[i] = gp(ta.hist_init)[i];
+  for (int i = tid; i < ta.reg_words; i += B) REG[i] = gp(ta.reg_init)[i];
+  for (int i = tid; i < ta.n_hists; i += B) TOT[i] = gp(ta.tot_init)[i];
+  for (int i = tid; i < ta.n_sigs; i += B) SANY[i] = gp(ta.sig_any)[i];
+  if (tid == 0) M.abort = 0;
+  NodeRes r[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    const int n = lo + j * B + tid;
+    r[j] = NodeRes{};
+    if (n < st.N) {
+      r[j] = load_res(st, n);
+      if constexpr (kDef) set_recips(r[j]);
+    }
+  }
+  const int R = ta.R;
+  const bool trc = ta.trace && tid == 0 && (g == 0 || g == G - 1);
+  int64_t* trow = ta.trace ? ta.trace + (g == 0 ? 0 : 8) : nullptr;
+#define KGPU_TSTAMP(k) \
+  if (trc) trow[(size_t)i * 16 + (k)] = (int64_t)__builtin_amdgcn_s_memrealtime()
+  for (int i = 0; i < ta.count; ++i) {
+    KGPU_TSTAMP(0);
+    const int pod = ta.first + i;
+    const kgpu_pod_query q = *cp(st.queries + pod);
+    const TPlan& tp = *cp(ta.plans + cp(ta.plan_of)[i]);
+    const uint64_t tk = pod_tie_key(st.seed, ta.seq0 + i);
+    // ---- the pod's lookup tables and PreFilter state (every workgroup, from its LDS replicas)
+    for (int w = tid; w < ta.soft_words; w += B) SMASK[w] = 0;
+    for (int z = tid; z < ta.zones; z += B) ZSUM[z] = 0;
+    if (tid < kTMaxTabs) M.pmin[tid] = INT64_MAX;
+    if (tid < 8) M.acc32[tid] = 0;
+    if (tid < 2) M.acc64[tid] = tid == 0 ? INT64_MAX : INT64_MIN;
+    __syncthreads();
+    for (int k = 0; k < tp.tabs.count; ++k) {
+      const TTab tb = cp(ta.tabs)[tp.tabs.begin + k];
+      for (int v = tid; v < tb.D; v += B) {
+        int64_t x = 0;
+        for (int t = 0; t < tb.terms.count; ++t) {
+          const TLook lk = cp(ta.looks)[tb.terms.begin + t];
+          x += (int64_t)(tb.kind == 2 ? lk.weight : 1) * H[lk.off + v];
+          if (tb.kind == 0 && v == tb.empty_v) x += H[lk.off + lk.D];  // node.Labels[key] of a missing key is ""
+        }
+        if (tb.kind == 0) {
+          const TReg rg = cp(ta.regs)[tb.reg];
+          if ((REG[rg.word + (v >> 5)] >> (v & 31)) & 1u) atomicMin(reinterpret_cast<long long*>(&M.pmin[k]), (long long)x);
+          else x = 0;  // an unregistered pair has no TpPairToMatchNum entry
+        }
+        PT[tb.off + v] = x;
+      }
+    }
+    const bool pany = tp.n_hard > 0 && SANY[tp.hard_sig] != 0;
+    bool aff_any = false;
+    for (int a = 0; a < tp.n_aff; ++a) aff_any |= tp.aff_hist[a] >= 0 && TOT[tp.aff_hist[a]] > 0;
+    __syncthreads();
+    if (tid < kTMaxTabs && M.pmin[tid] == INT64_MAX) M.pmin[tid] = 2147483647;  // criticalPaths init MaxInt32
+    __syncthreads();
+    KGPU_TSTAMP(1);
+    // ---- Filter + raw scores of this workgroup's rows
+    bool feas[K];
+    TRow o[K];
+    uint32_t sf = 0, smaxT = 0, smaxNA = 0, snon = 0, sadjmin = 0xFFFFFFFFu, sadjmax = 0, sdmax = 0, szoned = 0;
+    int64_t simin = INT64_MAX, simax = INT64_MIN;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      const int n = lo + j * B + tid;
+      feas[j] = false;
+      if (n >= st.N) continue;
+      if (trow_eval<FM, SM, kDef>(st, ta, q, tp, r[j], n, H, PT, M, pany, aff_any, o[j])) continue;
+      feas[j] = true;
+      ++sf;
+      smaxT = max(smaxT, (uint32_t)o[j].taint);
+      smaxNA = max(smaxNA, (uint32_t)o[j].na);
+      if (o[j].adj != INT64_MIN && tp.n_soft) {
+        ++snon;
+        sadjmin = min(sadjmin, (uint32_t)o[j].adj);
+        sadjmax = max(sadjmax, (uint32_t)o[j].adj);
+        if (tp.soft_mode == 0) {
+          const int v = nval(st, tp.soft_key, n);
+          atomicOr(SMASK + (v >> 5), 1u << (v & 31));
+        }
+      }
+      simin = min(simin, o[j].ipa);
+      simax = max(simax, o[j].ipa);
+      sdmax = max(sdmax, (uint32_t)o[j].ds);
+      const int z = gp(st.zone_id)[n];
+      if (z >= 0) {
+        szoned = 1;
+        if (o[j].ds && z < ta.zones) atomicAdd(ZSUM + z, o[j].ds);
+      }
+    }
+    KGPU_TSTAMP(2);
+    // ---- statistics round: wave reductions (DPP), workgroup (LDS atomics), granules, every workgroup
+    sf = wave_sum32(sf);
+    smaxT = wave_max32u(smaxT);
+    smaxNA = wave_max32u(smaxNA);
+    if (tp.n_soft) {
+      snon = wave_sum32(snon);
+      sadjmin = ~wave_max32u(~sadjmin);
+      sadjmax = wave_max32u(sadjmax);
+    }
+    if (tp.need_ipa) {
+      simin = wave_min_i64(simin);
+      simax = wave_max_i64(simax);
+    }
+    if (tp.dpts_cls >= 0) {
+      sdmax = wave_max32u(sdmax);
+      szoned = wave_max32u(szoned);
+    }
+    if (lane == 0) {
+      atomicAdd(&M.acc32[0], (int)sf);
+      atomicMax(reinterpret_cast<unsigned*>(&M.acc32[1]), smaxT);
+      atomicMax(reinterpret_cast<unsigned*>(&M.acc32[2]), smaxNA);
+      if (tp.n_soft) {
+        atomicAdd(&M.acc32[3], (int)snon);
+        atomicMax(reinterpret_cast<unsigned*>(&M.acc32[4]), ~sadjmin);
+        atomicMax(reinterpret_cast<unsigned*>(&M.acc32[5]), sadjmax);
+      }
+      if (tp.need_ipa) {
+        atomicMin(reinterpret_cast<long long*>(&M.acc64[0]), (long long)simin);
+        atomicMax(reinterpret_cast<long long*>(&M.acc64[1]), (long long)simax);
+      }
+      if (tp.dpts_cls >= 0) {
+        atomicMax(reinterpret_cast<unsigned*>(&M.acc32[6]), sdmax);
+        atomicMax(reinterpret_cast<unsigned*>(&M.acc32[7]), szoned);
+      }
+    }
+    __syncthreads();
+    uint64_t* srow = ta.gran + (size_t)i * (R + 1) * G;
+    if (tid < R) {
+      int64_t x;
+      switch (tid) {
+        case kTFeas: x = M.acc32[0]; break;
+        case kTMaxT: x = (uint32_t)M.acc32[1]; break;
+        case kTMaxNA: x = (uint32_t)M.acc32[2]; break;
+        case kTNonIgn: x = M.acc32[3]; break;
+        case kTAdjMin: x = tp.n_soft ? (int64_t)(uint32_t)~(uint32_t)M.acc32[4] : tident(kOpMin); break;
+        case kTAdjMax: x = tp.n_soft ? (int64_t)(uint32_t)M.acc32[5] : tident(kOpMax); break;
+        case kTIpaMin: x = M.acc64[0] == INT64_MAX ? tident(kOpMin) : M.acc64[0]; break;
+        case kTIpaMax: x = M.acc64[1] == INT64_MIN ? tident(kOpMax) : M.acc64[1]; break;
+        case kTDptsMax: x = (uint32_t)M.acc32[6]; break;
+        case kTZoned: x = (uint32_t)M.acc32[7]; break;
+        default: x = tid < kTFixed + ta.soft_words ? (int64_t)SMASK[tid - kTFixed] : (int64_t)ZSUM[tid - kTFixed - ta.soft_words];
+      }
+      store_sc1(srow + (size_t)tid * G + g, enc_stat(x));
+    }
+    KGPU_TSTAMP(3);
+    bool ok = true;
+    for (int rr = wave; rr < R; rr += W) {
+      const int op = rr < kTFixed ? tstat_op(rr) : (rr < kTFixed + ta.soft_words ? kOpOr : kOpSum);
+      int64_t x;
+      if (!tpoll_slot(srow + (size_t)rr * G, G, ta.abort, op, x)) { ok = false; break; }
+      if (lane == 0) STAT[rr] = x;
+    }
+    if (!ok && lane == 0) {
+      __hip_atomic_store(ta.abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      M.abort = 1;
+    }
+    __syncthreads();
+    if (M.abort) break;
+    KGPU_TSTAMP(4);
+    // ---- NormalizeScore of every plugin, weights, packed-key argmax
+    const int64_t feas_total = STAT[kTFeas];
+    const int maxT = (int)STAT[kTMaxT], maxNA = (int)STAT[kTMaxNA];
+    int64_t pmx = 0, pmn = INT64_MAX;
+    double wsoft = 0.0;
+    if (tp.n_soft) {
+      int64_t size = STAT[kTNonIgn];
+      if (tp.soft_mode == 0) {
+        size = 0;
+        for (int w = 0; w < tp.soft_words; ++w) size += __popc((uint32_t)STAT[kTFixed + w]);
+      }
+      wsoft = st.log_table[size + 2];  // topologyNormalizingWeight (scoring.go:286-288)
+      if (STAT[kTNonIgn] > 0) {
+        // int64(cnt * w) does not decrease with cnt: the extremes come from the extreme counts
+        pmn = (int64_t)((double)STAT[kTAdjMin] * wsoft);
+        pmx = max((int64_t)((double)STAT[kTAdjMax] * wsoft), (int64_t)0);
+      }
+    }
+    const int64_t imx = max(STAT[kTIpaMax], (int64_t)0), imn = min(STAT[kTIpaMin], (int64_t)0);
+    const int64_t idiff = imx - imn;
+    const int64_t dmax_node = max(STAT[kTDptsMax], (int64_t)0);
+    int64_t dmax_zone = 0;
+    for (int z = 0; z < ta.zones; ++z) dmax_zone = max(dmax_zone, STAT[kTFixed + ta.soft_words + z]);
+    const bool have_zones = STAT[kTZoned] != 0;
+    const double Mx = 100.0, zwt = 2.0 / 3.0;
+    uint64_t bkey = 0;
+    int bidx = -1;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      if (!feas[j]) continue;
+      const int n = lo + j * B + tid;
+      // DefaultNormalizeScore (helper/normalize_score.go:26-54): non-negative operands, exact
+      // through div_nonneg
+      const int64_t vt = maxT == 0 ? 100 : 100 - div_nonneg(100 * (int64_t)o[j].taint, maxT);
+      const int64_t vn = maxNA == 0 ? (int64_t)o[j].na : div_nonneg(100 * (int64_t)o[j].na, maxNA);
+      int64_t vp;
+      if (o[j].adj == INT64_MIN) {
+        vp = 0;
+      } else {
+        // scoring.go:248-256; pmn <= ps <= pmx, so the dividend is non-negative
+        const int64_t ps = tp.n_soft ? (int64_t)((double)o[j].adj * wsoft) : 0;
+        vp = pmx == 0 ? 100 : div_nonneg(100 * (pmx + pmn - ps), pmx);
+      }
+      const int64_t vi = idiff > 0 ? (int64_t)(Mx * ((double)(o[j].ipa - imn) / (double)idiff)) : 0;
+      int64_t vd = 0;
+      if (tp.dpts_cls != -2) {
+        double f = Mx;
+        if (dmax_node > 0) f = Mx * ((double)(dmax_node - o[j].ds) / (double)dmax_node);
+        const int z = gp(st.zone_id)[n];
+        if (have_zones && z >= 0) {
+          double zs = Mx;
+          if (dmax_zone > 0) zs = Mx * ((double)(dmax_zone - STAT[kTFixed + ta.soft_words + z]) / (double)dmax_zone);
+          f = (f * (1.0 - zwt)) + (zwt * zs);
+        }
+        vd = (int64_t)f;
+      }
+      int64_t total = o[j].part + vt * st.w_of[KGPU_S_TAINT_TOLERATION] + vn * st.w_of[KGPU_S_NODE_AFFINITY] +
+                      vp * st.w_of[KGPU_S_POD_TOPOLOGY_SPREAD] + vi * st.w_of[KGPU_S_INTER_POD_AFFINITY] +
+                      vd * st.w_of[KGPU_S_DEFAULT_POD_TOPOLOGY_SPREAD];
+      if (st.n_scores == 0) total = 1;
+      const uint64_t key = ((uint64_t)(total + 1) << 40) | rank40(tk, (uint64_t)(st.node_base + n), st.tie_mode);
+      if (key > bkey) { bkey = key; bidx = j * B + tid; }
+    }
+    wave_argmax(bkey, bidx);
+    if (lane == 0) {
+      M.akey[wave] = bkey;
+      M.aidx[wave] = bidx;
+    }
+    __syncthreads();
+    uint64_t* arow = srow + (size_t)R * G;
+    if (wave == 0) {
+      uint64_t bk = lane < W ? M.akey[lane] : 0;
+      int bi = lane < W ? M.aidx[lane] : -1;
+      wave_argmax(bk, bi);
+      if (lane == 0) store_sc1(arow + g, kGValid | bk);
+      KGPU_TSTAMP(5);
+      uint64_t wkey = 0;
+      int wg = -1;
+      const bool pok = poll_row(arow, G, ta.abort, wkey, wg);
+      if (lane == 0) {
+        if (!pok) {
+          __hip_atomic_store(ta.abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          M.abort = 1;
+        }
+        M.wkey = wkey;
+        M.wg = wg;
+        M.wnode = wkey ? (int)rank40_inv(tk, wkey & kMask40, st.tie_mode) : -1;
+      }
+    }
+    __syncthreads();
+    if (M.abort) break;
+    KGPU_TSTAMP(6);
+    // ---- outcome (generic_scheduler.go:171-208) and assume (types.go:456-480)
+    const int wnode = M.wnode;  // global index
+    const bool error = (q.flags & KGPU_Q_SCORE_ERROR) && feas_total >= 2;
+    const bool placed = feas_total > 0 && !error;
+    if (tid == 0 && ((M.wg >= 0 && M.wg == g) || (M.wg < 0 && g == 0))) {
+      kgpu_result res;
+      res.node = placed ? wnode : (error ? -2 : -1);
+      res.feasible = (int32_t)feas_total;
+      res.evaluated = st.n_total;
+      res.scored = (placed && feas_total >= 2) ? 1 : 0;
+      res.score = res.scored ? (int64_t)(M.wkey >> 40) - 1 : 0;
+      gp(st.results)[pod] = res;
+    }
+    if (placed && ta.assume) {
+      const int wl = wnode - st.node_base;
+      // the winner's label values and signature bits, staged once for every delta
+      if (tid < ta.n_keys) M.wlab[tid] = gp(st.label_val)[(size_t)tid * st.N + wl];
+      else if (tid >= 64 && tid - 64 < ta.n_sigs) M.welig[tid - 64] = tb_elig(ta, tid - 64, wl) ? 1 : 0;
+      __syncthreads();
+      for (int d = tid; d < tp.deltas.count; d += B) {
+        const TDelta dl = cp(ta.deltas)[tp.deltas.begin + d];
+        if (dl.sig >= 0 && !M.welig[dl.sig]) continue;
+        const int v = dl.key >= 0 ? M.wlab[dl.key] : -1;
+        if (dl.off >= 0) H[dl.off + (v >= 0 ? v : dl.D)] += 1;
+        if (v >= 0) TOT[dl.hist] += 1;
+      }
+      if (M.wg == g) {
+        const int local = wl - lo;
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+          if (local == j * B + tid) {
+            assume_row(st, q, r[j], wl);
+            for (int a = 0; a < tp.assume_cls.count; ++a)
+              gp(st.mcnt)[(size_t)cp(ta.aux)[tp.assume_cls.begin + a] * st.N + wl] += 1;
+            for (int a = 0; a < tp.own_tcls.count; ++a)
+              gp(st.tcnt)[(size_t)cp(ta.aux)[tp.own_tcls.begin + a] * st.N + wl] += 1;
+          }
+      }
+    }
+    __syncthreads();
+    KGPU_TSTAMP(7);
+  }
+#undef KGPU_TSTAMP
+}
+
 // ---------------------------------------------------------------- profile instantiations
 constexpr uint32_t bit(int i) { return 1u << i; }
 // config (b) of BASELINE.json: NodeResourcesFit + BalancedAllocation + LeastAllocated
@@ -1821,6 +2468,66 @@ constexpr uint32_t kDefaultFM = (1u << KGPU_NUM_FILTERS) - 1;
 constexpr uint32_t kDefaultSM = (kSMask & ~bit(KGPU_S_MOST_ALLOCATED)) | kDefRes;
 // the ClusterAutoscalerProvider (registry.go:157-165): MostAllocated instead of LeastAllocated
 constexpr uint32_t kAutoscalerSM = (kSMask & ~bit(KGPU_S_LEAST_ALLOCATED)) | kDefRes;
+
+// persistent topology kernel instantiations: [profile spec][geometry] (kgpu_internal.h)
+struct TGeo {
+  int B, K;
+};
+// 512 threads x 1 or 2 rows per lane (two waves per SIMD, no VGPR spills): up to 262,144 nodes per
+// GPU in 256 workgroups; larger shards take the per-pod topology launches.
+constexpr TGeo kTGeo[] = {{512, 1}, {512, 2}};
+constexpr int kNumTGeo = 2;
+using TBatchFn = void (*)(const DevState*, TBatchArgs);
+template <uint32_t FM, uint32_t SM, bool kDef>
+struct TBatchRow {
+  static constexpr TBatchFn fn[kNumTGeo] = {k_tbatch<512, 1, FM, SM, kDef>, k_tbatch<512, 2, FM, SM, kDef>};
+};
+// rows: 0 generic, 1 generic with Least/Most over {cpu:1, memory:1}, 2 default provider,
+// 3 ClusterAutoscaler provider
+static const TBatchFn* const kTBatch[] = {
+    TBatchRow<kRuntime, kRuntime, false>::fn, TBatchRow<kRuntime, kRuntime, true>::fn,
+    TBatchRow<kDefaultFM, kDefaultSM, true>::fn, TBatchRow<kDefaultFM, kAutoscalerSM, true>::fn};
+
+int tbatch_geometry(int N, int max_groups, int* per, int* groups) {
+  for (int gi = 0; gi < kNumTGeo; ++gi) {
+    const int p = kTGeo[gi].B * kTGeo[gi].K;
+    const int g = (N + p - 1) / p;
+    if (g <= max_groups) {
+      *per = p;
+      *groups = g < 1 ? 1 : g;
+      return gi;
+    }
+  }
+  return -1;
+}
+
+// spec: the k_eval profile instantiation (select_spec), def_res from the TBatchArgs
+int launch_tbatch(const DevState* st, const TBatchArgs& a, int groups, int geo, int spec, void* stream) {
+  if (geo < 0 || geo >= kNumTGeo) return -1;
+  hipStream_t s = (hipStream_t)stream;
+  const int N = a.per * groups;  // >= st->N
+  const int nb = (N + 255) / 256;
+  hipLaunchKernelGGL(k_sig_init, dim3(nb), dim3(256), 0, s, st, a);
+  hipLaunchKernelGGL(k_hist_init, dim3(nb), dim3(256), 0, s, st, a);
+  if (hipGetLastError() != hipSuccess) return -1;
+  const int row = spec == 2 ? 2 : (spec == 3 ? 3 : (a.def_res ? 1 : 0));
+  const TBatchFn fn = kTBatch[row][geo];
+  static bool attr[4][kNumTGeo] = {};
+  if (!attr[row][geo]) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            kTLdsBudget) != hipSuccess)
+      return -1;
+    attr[row][geo] = true;
+  }
+  // one workgroup per CU (>= 80 KB of LDS each); the cooperative launch checks co-residency
+  TBatchArgs arg = a;
+  const DevState* sp = st;
+  void* args[] = {(void*)&sp, (void*)&arg};
+  return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(fn), dim3(groups), dim3(kTGeo[geo].B), args,
+                                    (unsigned)a.lds_bytes, s) == hipSuccess
+             ? 0
+             : -1;
+}
 
 struct SpecEntry {
   uint32_t fm, sm;

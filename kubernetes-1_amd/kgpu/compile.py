@@ -68,19 +68,34 @@ class CompileError(Exception):
 
 
 class Pools:
-    """Growable pools referenced by kgpu_range fields."""
+    """Growable pools referenced by kgpu_range fields.
+
+    Ranges are interned by content: pods compiled from one template (a Deployment's replicas)
+    share every record, so the device reads one cache-hot copy instead of a fresh line per pod."""
 
     def __init__(self):
         self.reqs, self.ints, self.words = [], [], []
         self.node_terms, self.pref_terms, self.spreads, self.pod_terms = [], [], [], []
         self.scalars, self.ports = [], []
+        self._cache = {}
         self._np = None
 
-    @staticmethod
-    def _rng(lst, items):
-        b = len(lst)
-        lst.extend(items)
-        return (b, len(items))
+    def _rng(self, lst, items):
+        items = list(items)
+        if not items:
+            return (0, 0)
+        key = (id(lst), tuple(items))
+        r = self._cache.get(key)
+        if r is None:
+            r = self._cache[key] = (len(lst), len(items))
+            lst.extend(items)
+        return r
+
+    def truncate(self, lst, n):
+        """Drop records appended after position n (a compile step that failed half-way)."""
+        del lst[n:]
+        for k in [k for k, v in self._cache.items() if k[0] == id(lst) and v[0] + v[1] > n]:
+            del self._cache[k]
 
     def ints_range(self, xs):
         return self._rng(self.ints, [int(x) for x in xs])
@@ -162,9 +177,7 @@ def compile_label_selector(ks, pools, ps):
         vals = list(e.get("values") or [])
         _validate_req(e.get("key", ""), op, vals)
         recs.append(_req_rec(ks, pools, e.get("key", ""), op, vals, register=True))
-    b = len(pools.reqs)
-    pools.reqs.extend(recs)
-    return (abi.SEL_AND, 0, (b, len(recs)))
+    return (abi.SEL_AND, 0, pools._rng(pools.reqs, recs))
 
 
 def compile_node_reqs(ks, pools, nsm, validate=True):
@@ -178,9 +191,7 @@ def compile_node_reqs(ks, pools, nsm, validate=True):
         if validate:
             _validate_req(e.get("key", ""), op, vals)
         recs.append(_req_rec(ks, pools, e.get("key", ""), op, vals))
-    b = len(pools.reqs)
-    pools.reqs.extend(recs)
-    return (b, len(recs))
+    return pools._rng(pools.reqs, recs)
 
 
 def label_selector_matches(ps, labels):
@@ -613,8 +624,8 @@ class Compiler:
                 else:
                     out.append(self._pod_term(pod, t, pools))
         except CompileError:
-            del pools.reqs[save[0]:]
-            del pools.ints[save[1]:]
+            pools.truncate(pools.reqs, save[0])
+            pools.truncate(pools.ints, save[1])
             return []
         return out
 
@@ -660,7 +671,7 @@ class Compiler:
             if r not in ("cpu", "memory", "ephemeral-storage") and r not in seen and api.is_scalar(r):
                 sc.append((self.scalars.get(r), 0, 0, api.PodResources._score(res, r, pod)))
                 seen.add(r)
-        q["scalars"] = Pools._rng(pools.scalars, sc)
+        q["scalars"] = pools._rng(pools.scalars, sc)
         nn = api.spec(pod).get("nodeName", "") or ""
         q["node_name"] = -1 if nn == "" else self.node_index.get(nn, -2)
         q["n_containers"] = len(api.containers(pod))
@@ -671,7 +682,7 @@ class Compiler:
                 if port > 0:
                     want.append((self.ips.add(pt.get("hostIP", "") or "0.0.0.0"),
                                  self.protos.add(pt.get("protocol", "") or "TCP"), port, 0))
-        q["ports"] = Pools._rng(pools.ports, want)
+        q["ports"] = pools._rng(pools.ports, want)
         tols = api.spec(pod).get("tolerations") or []
         TW = max(1, (len(self.taints) + 63) // 64)
         m_ns = [0] * TW
@@ -698,7 +709,7 @@ class Compiler:
             flags |= abi.Q_REQ_NODE_AFFINITY
             terms = (na["requiredDuringSchedulingIgnoredDuringExecution"].get("nodeSelectorTerms")) or []
             recs = [self._node_term(t, pools) for t in terms]
-            q["req_terms"] = Pools._rng(pools.node_terms, recs)
+            q["req_terms"] = pools._rng(pools.node_terms, recs)
         prefs = []
         if na is not None and na.get("preferredDuringSchedulingIgnoredDuringExecution") is not None:
             for t in na["preferredDuringSchedulingIgnoredDuringExecution"]:
@@ -715,7 +726,7 @@ class Compiler:
                     flags |= abi.Q_SCORE_ERROR
                     continue
                 prefs.append((w, 0, (abi.SEL_AND, 0, r)))
-        q["pref_terms"] = Pools._rng(pools.pref_terms, prefs)
+        q["pref_terms"] = pools._rng(pools.pref_terms, prefs)
         imgs = [self.images.get(api.normalized_image_name(c.get("image", "") or "")) for c in api.containers(pod)]
         q["images"] = pools.ints_range(imgs)
         ref = api.controller_ref(pod)
@@ -742,10 +753,10 @@ class Compiler:
         byk = {abi.TERM_REQ_AFF: [], abi.TERM_REQ_ANTI: [], abi.TERM_PREF_AFF: [], abi.TERM_PREF_ANTI: []}
         for kind, t in self.pod_terms(pod, pools):
             byk[kind].append(t)
-        q["ipa_req_aff"] = Pools._rng(pools.pod_terms, byk[abi.TERM_REQ_AFF])
-        q["ipa_req_anti"] = Pools._rng(pools.pod_terms, byk[abi.TERM_REQ_ANTI])
-        q["ipa_pref_aff"] = Pools._rng(pools.pod_terms, byk[abi.TERM_PREF_AFF])
-        q["ipa_pref_anti"] = Pools._rng(pools.pod_terms, byk[abi.TERM_PREF_ANTI])
+        q["ipa_req_aff"] = pools._rng(pools.pod_terms, byk[abi.TERM_REQ_AFF])
+        q["ipa_req_anti"] = pools._rng(pools.pod_terms, byk[abi.TERM_REQ_ANTI])
+        q["ipa_pref_aff"] = pools._rng(pools.pod_terms, byk[abi.TERM_PREF_AFF])
+        q["ipa_pref_anti"] = pools._rng(pools.pod_terms, byk[abi.TERM_PREF_ANTI])
         if byk[abi.TERM_REQ_AFF] and self._self_match_all(pod):
             flags |= abi.Q_SELF_MATCH_ALL_AFF
         pairs = []
@@ -827,7 +838,7 @@ class Compiler:
             sel = compile_label_selector(self.pkeys, pools, ps)
             recs.append((ms, self.nkeys.key(key), 1 if key == HOSTNAME else 0,
                          1 if label_selector_matches(ps, pl) else 0, sel))
-        return Pools._rng(pools.spreads, recs)
+        return pools._rng(pools.spreads, recs)
 
     # -------------------------------------------------- config
     def config(self, device=0, node_capacity=0, pod_capacity=0, term_capacity=0):

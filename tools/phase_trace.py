@@ -17,6 +17,7 @@ def main():
     ap.add_argument("--nodes", type=int, default=5000)
     ap.add_argument("--pods", type=int, default=1000)
     ap.add_argument("--config", default="b")
+    ap.add_argument("--groups", type=int, default=0, help="KGPU_OPT_PERSIST_GROUPS cap (0: one per CU)")
     args = ap.parse_args()
     import numpy as np
     from kgpu import abi, cluster
@@ -32,15 +33,18 @@ def main():
     eng.schedule_batch(q[:64], pc)
     eng.upload(fw.snap, fw.arrays)
     eng.set_option(abi.OPT_PHASE_TRACE, 1)
+    if args.groups:
+        eng.set_option(abi.OPT_PERSIST_GROUPS, args.groups)
     eng.schedule_batch(q, pc)
     t = eng.phase_trace(len(q) + 1).astype(np.float64) * 10.0  # ns
     t = t[1:-1]  # steady state: skip the prologue and epilogue iterations
     for w, name in ((0, "wg0"), (1, "wglast")):
         a = t[:, w, :]
         per = np.diff(a[:, 0])
-        ph = {"eval": a[:, 1] - a[:, 0], "wait_prev": a[:, 2] - a[:, 1], "publish": a[:, 3] - a[:, 2],
+        ph = {"evalA": a[:, 5] - a[:, 0], "evalB": a[:, 6] - a[:, 5], "partials": a[:, 1] - a[:, 6],
+              "wait_prev": a[:, 2] - a[:, 1], "publish": a[:, 3] - a[:, 2],
               "assume": a[:, 4] - a[:, 3], "next": a[1:, 0] - a[:-1, 4]}
-        print("%s: per-pod %.0f ns | " % (name, np.median(per)) +
+        print("groups<=%d %s: per-pod %.0f ns | " % (args.groups, name, np.median(per)) +
               "  ".join("%s %.0f" % (k, np.median(v)) for k, v in ph.items()) + " (medians, ns)")
     # hop: latest publish of pod i (of the two traced workgroups) -> pod i seen resolved
     pub = np.maximum(t[:-1, 0, 3], t[:-1, 1, 3])

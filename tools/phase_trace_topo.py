@@ -1,0 +1,52 @@
+#!/usr/bin/env python3
+"""Per-pod phase breakdown of the persistent topology kernel k_tbatch (s_memrealtime, 10 ns ticks).
+
+phases: prefilter (criticalPaths minima from the LDS histograms), rows (filters + raw scores of the
+workgroup's node rows), stats_pub (wave + workgroup reduction, statistics granules stored),
+stats_wait (until every workgroup's statistics arrived), score_pub (normalize, weights, argmax,
+key granule stored), key_wait (until every key arrived), assume (result, histogram deltas, row)."""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "kubernetes-1_amd")]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--nodes", type=int, default=5000)
+    ap.add_argument("--pods", type=int, default=1000)
+    ap.add_argument("--config", default="c")
+    ap.add_argument("--groups", type=int, default=0)
+    args = ap.parse_args()
+    import numpy as np
+    from kgpu import abi, cluster
+    from kgpu.framework import GpuFramework
+    if args.config == "c":
+        nodes, ex, pods, prof = cluster.taints_affinity_spread(n_nodes=args.nodes, n_pods=args.pods)
+    else:
+        nodes, ex, pods, prof = cluster.pod_affinity(n_nodes=args.nodes, n_existing=args.nodes, n_pods=args.pods)
+    fw = GpuFramework(prof, nodes, ex, pods_hint=pods[:16])
+    q, pc, _, errs = fw.compile_pods(pods)
+    eng = fw.engine
+    if args.groups:
+        eng.set_option(abi.OPT_PERSIST_GROUPS, args.groups)
+    eng.schedule_batch(q[:32], pc)
+    eng.upload(fw.snap, fw.arrays)
+    eng.set_option(abi.OPT_PHASE_TRACE, 1)
+    eng.schedule_batch(q, pc)
+    t = eng.phase_trace(len(q) + 1).astype(np.float64) * 10.0  # ns
+    t = t[1:len(q) - 1]
+    names = ["prefilter", "rows", "stats_pub", "stats_wait", "score_pub", "key_wait", "assume"]
+    for w, name in ((0, "wg0"), (1, "wglast")):
+        a = t[:, w, :]
+        per = np.diff(a[:, 0])
+        ph = {names[k]: a[:, k + 1] - a[:, k] for k in range(7)}
+        print("config %s %d nodes groups<=%d %s: per-pod %.0f ns | " % (args.config, args.nodes, args.groups, name,
+                                                                       np.median(per)) +
+              "  ".join("%s %.0f" % (k, np.median(v)) for k, v in ph.items()) + " (medians, ns)")
+
+
+if __name__ == "__main__":
+    main()
