@@ -263,6 +263,9 @@ def main():
             "latency": lat_rec,
         }
         print(json.dumps(line), flush=True)
+    # release the device context before interpreter teardown (under rocprofv3 the HIP runtime may
+    # be finalized before a garbage-collected engine would be)
+    eng.close()
     if dist_on:
         dist.destroy_process_group()
 

@@ -124,6 +124,7 @@ extern "C" {
 #define KGPU_Q_REQ_NODE_AFFINITY 128u      /* RequiredDuringScheduling != nil: terms apply */
 #define KGPU_Q_SCORE_ERROR 256u            /* a Score plugin returns Error (invalid preferred term):
                                               the cycle fails whenever scoring runs */
+#define KGPU_Q_NO_KNOWN_IMAGE 512u         /* no container image is on any node: ImageLocality is 0 */
 
 typedef struct kgpu_range {
   int32_t begin;

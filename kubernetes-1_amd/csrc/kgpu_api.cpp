@@ -738,7 +738,7 @@ size_t a16(size_t x) { return (x + 15) & ~(size_t)15; }
 constexpr size_t kTMiscBytes = 1024;
 
 // LDS layout of a run (byte offsets into the dynamic region); returns the total
-size_t t_layout(const TRun& tr, kgpu::TBatchArgs* a, int B) {
+size_t t_layout(const TRun& tr, kgpu::TBatchArgs* a, int B, int lab_keys = 0, int per = 0) {
   size_t o = a16((size_t)tr.lds_bins * 4);
   const size_t o_reg = o;
   o = a16(o + (size_t)tr.reg_words * 4);
@@ -759,7 +759,11 @@ size_t t_layout(const TRun& tr, kgpu::TBatchArgs* a, int B) {
   o = a16(o + (size_t)std::max(tr.pt_max, 1) * 8);
   const size_t o_misc = o;
   o = a16(o + kTMiscBytes);
+  const size_t o_lab = o;
+  o = a16(o + (size_t)lab_keys * (size_t)per * 4);
   if (a) {
+    a->o_lab = (int32_t)o_lab;
+    a->lab_keys = lab_keys;
     a->o_reg = (int32_t)o_reg;
     a->o_tot = (int32_t)o_tot;
     a->o_sany = (int32_t)o_sany;
@@ -944,6 +948,8 @@ bool t_add(TRun& tr, const kgpu_ctx* c, const kgpu_pod_query& q, const kgpu::QPl
     }
   tp.tabs = tr.tabs.add(tabs);
   tp.n_exa_tabs = (int32_t)t1.size();
+  for (int h = 0; h < pl.n_hard; ++h)
+    if (tp.hard[h].tab >= 0) tp.hard[h].pt_off = t0[(size_t)tp.hard[h].tab].t.off;
   if (tp.tabs.count > kgpu::kTMaxTabs) return fail_();
   tp.pt_words = pt;
   tr.pt_max = std::max(tr.pt_max, pt);
@@ -1023,7 +1029,10 @@ int run_tbatch(kgpu_ctx* c, TRun& tr, int first, int count, int64_t first_seq, i
                                 c->cfg.most[0].resource == 0 && c->cfg.most[0].weight == 1 &&
                                 c->cfg.most[1].resource == 1 && c->cfg.most[1].weight == 1)
                   ? 1 : 0;
-  size_t lds = t_layout(tr, &a, 512);
+  // node labels of the workgroup's rows in LDS when they fit beside the histograms
+  int lab_keys = std::min(c->st.K, 16);
+  while (lab_keys > 0 && t_layout(tr, nullptr, 512, lab_keys, per) > (size_t)kgpu::kTLdsBudget) --lab_keys;
+  size_t lds = t_layout(tr, &a, 512, lab_keys, per);
   // at least half a CU's LDS: one persistent workgroup per CU (two would share its SIMDs)
   a.lds_bytes = (int32_t)std::max<size_t>(lds, 96 * 1024);
   const size_t N = (size_t)c->st.N;

@@ -294,6 +294,7 @@ struct TTab {
 };
 struct THard {
   int32_t key, max_skew, self_match, tab;  // tab: index of the key's kind-0 table in the pod's tabs
+  int32_t pt_off, pad0;                    // that table's first entry
 };
 struct TDelta {      // one histogram a pod increments when assumed
   int32_t hist, off, D, key;
@@ -356,7 +357,9 @@ struct TBatchArgs {
   int32_t pt_words;       // largest per-pod table area of the run (int64 words)
   int32_t n_keys;         // node label keys the run's deltas read (winner's labels staged in LDS)
   // byte offsets of the LDS regions (histogram bins start at 0)
-  int32_t o_reg, o_tot, o_sany, o_stat, o_smask, o_zsum, o_wred, o_misc, o_pt;
+  int32_t o_reg, o_tot, o_sany, o_stat, o_smask, o_zsum, o_wred, o_misc, o_pt, o_lab;
+  int32_t lab_keys;       // node label keys cached in LDS per workgroup ([lab_keys][per] value ids)
+  int32_t pad_l;
   int64_t* trace;         // null, or [count + 1][16] s_memrealtime stamps (KGPU_OPT_PHASE_TRACE): per pod
                           // and traced workgroup (0, last): start, PreFilter minima, rows evaluated,
                           // stats published, stats resolved, key published, winner resolved, end

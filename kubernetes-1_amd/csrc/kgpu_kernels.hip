@@ -340,6 +340,7 @@ __device__ __forceinline__ int64_t balanced_score(const kgpu_pod_query& q, const
 
 __device__ __forceinline__ int64_t image_score(const DevState& st, const kgpu_pod_query& q, int n) {
   constexpr int64_t MB = 1024 * 1024, kMin = 23 * MB, kMaxC = 1000 * MB;
+  if (q.flags & KGPU_Q_NO_KNOWN_IMAGE) return 0;  // sum stays below minThreshold on every node
   int64_t sum = 0;
   if (q.images.count) {
     const int lo0 = gp(st.image_off)[n], hi0 = gp(st.image_off)[n + 1];
@@ -357,7 +358,8 @@ __device__ __forceinline__ int64_t image_score(const DevState& st, const kgpu_po
   const int64_t maxT = kMaxC * (int64_t)q.n_containers;
   if (sum < kMin) sum = kMin;
   else if (sum > maxT) sum = maxT;
-  return (100 * (sum - kMin)) / (maxT - kMin);
+  const int64_t den = maxT - kMin;  // > 0 unless the pod has no containers
+  return den > 0 ? div_nonneg(100 * (sum - kMin), den) : (100 * (sum - kMin)) / den;
 }
 
 __device__ __forceinline__ int64_t npap_score(const DevState& st, const kgpu_pod_query& q, int n) {
@@ -2016,19 +2018,24 @@ __device__ __forceinline__ int64_t tval(const DevState& st, const int32_t* H, co
 // Score plugins of the pod outside the topology three (which k_tbatch normalizes itself).
 constexpr uint32_t kTopoSM = (1u << KGPU_S_POD_TOPOLOGY_SPREAD) | (1u << KGPU_S_INTER_POD_AFFINITY) |
                              (1u << KGPU_S_DEFAULT_POD_TOPOLOGY_SPREAD);
+// reg_taint: the raw TaintToleration score comes from the register-resident taint words (the
+// caller adds it), not from the columns.
 template <uint32_t SM, bool kDef>
-__device__ __forceinline__ void tscores(const DevState& st, const kgpu_pod_query& q, const NodeRes& r, int n, NodeEval& e) {
+__device__ __forceinline__ void tscores(const DevState& st, const kgpu_pod_query& q, const NodeRes& r, int n, NodeEval& e,
+                                        bool reg_taint) {
   if constexpr (SM == kRuntime) {
     int64_t p = 0;
     for (int si = 0; si < st.n_scores; ++si) {
       const int s = cp(st.scores)[si];
       if ((kTopoSM >> s) & 1u) continue;
+      if (s == KGPU_S_TAINT_TOLERATION && reg_taint) continue;
       const int64_t v = score_one<kDef>(s, st, q, r, n, e);
       if (!normalized(s)) p += v * cp(st.w_of)[s];
     }
     e.partial = p;
   } else {
-    run_scores<SM & ~kTopoSM>(st, q, r, n, e, false);
+    if (reg_taint) run_scores<SM & ~kTopoSM & ~(1u << KGPU_S_TAINT_TOLERATION)>(st, q, r, n, e, false);
+    else run_scores<SM & ~kTopoSM>(st, q, r, n, e, false);
   }
 }
 
@@ -2038,18 +2045,30 @@ struct TRow {
   int64_t part, adj, ipa;
   int32_t taint, na, ds, pad;
 };
+// Per-node data that never changes inside a run, loaded once with the resource row: the
+// NodeUnschedulable flag, the taint bitsets (up to two words) and the zone.
+struct TStatic {
+  uint64_t tns[2], tpr[2];
+  int32_t unsched, zone;
+};
+
 template <uint32_t FM, uint32_t SM, bool kDef>
 __device__ __forceinline__ uint32_t trow_eval(const DevState& st, const TBatchArgs& ta, const kgpu_pod_query& q,
                                          const TPlan& tp, const NodeRes& r, int n, const int32_t* H,
-                                         const int64_t* PT, const TMisc& M, bool pany, bool aff_any, TRow& o) {
+                                         const int64_t* PT, const TMisc& M, bool pany, bool aff_any,
+                                         const int32_t* LAB, int li, const TStatic& sr, TRow& o) {
+  // node label value ids from the workgroup's LDS copy (keys < lab_keys), else from the column
+  auto nval = [&](int key) -> int {
+    if (key < 0) return -1;
+    return key < ta.lab_keys ? LAB[key * ta.per + li] : gp(st.label_val)[(size_t)key * st.N + n];
+  };
   auto pts = [&]() -> uint32_t {  // filtering.go:276-328
     if (!pany) return 0;
     for (int c = 0; c < tp.n_hard; ++c) {
       const THard hc = tp.hard[c];
-      const int v = nval(st, hc.key, n);
+      const int v = nval(hc.key);
       if (v < 0) return KGPU_CODE_UNSCHEDULABLE << 8;
-      const TTab tb = cp(ta.tabs)[tp.tabs.begin + hc.tab];
-      if (PT[tb.off + v] + hc.self_match - M.pmin[hc.tab] > hc.max_skew) return KGPU_CODE_UNSCHEDULABLE << 8;
+      if (PT[hc.pt_off + v] + hc.self_match - M.pmin[hc.tab] > hc.max_skew) return KGPU_CODE_UNSCHEDULABLE << 8;
     }
     return 0;
   };
@@ -2057,24 +2076,24 @@ __device__ __forceinline__ uint32_t trow_eval(const DevState& st, const TBatchAr
     bool exist = true;
     for (int a = 0; a < tp.n_aff; ++a) {
       const TLook t = tp.aff[a];
-      const int v = nval(st, t.key, n);
+      const int v = nval(t.key);
       if (v < 0) return (KGPU_CODE_UNRESOLVABLE << 8) | (1u << 16);
       if (tval(st, H, t, v, n) <= 0) exist = false;
     }
     if (!exist && !(!aff_any && tp.self_all)) return (KGPU_CODE_UNRESOLVABLE << 8) | (1u << 16);
     for (int a = 0; a < tp.n_anti; ++a) {
       const TLook t = tp.anti[a];
-      const int v = nval(st, t.key, n);
+      const int v = nval(t.key);
       if (v >= 0 && tval(st, H, t, v, n) > 0) return (KGPU_CODE_UNSCHEDULABLE << 8) | (2u << 16);
     }
     for (int k = 0; k < tp.n_exa_tabs; ++k) {
       const TTab tb = cp(ta.tabs)[tp.tabs.begin + tp.tabs.count - tp.n_exa_tabs + k];
-      const int v = nval(st, tb.key, n);
+      const int v = nval(tb.key);
       if (v >= 0 && PT[tb.off + v] > 0) return (KGPU_CODE_UNSCHEDULABLE << 8) | (3u << 16);
     }
     for (int e = 0; e < tp.exa_u.count; ++e) {
       const TLook t = cp(ta.looks)[tp.exa_u.begin + e];
-      if (nval(st, t.key, n) >= 0 && tcol(st, t, n) > 0) return (KGPU_CODE_UNSCHEDULABLE << 8) | (3u << 16);
+      if (nval(t.key) >= 0 && tcol(st, t, n) > 0) return (KGPU_CODE_UNSCHEDULABLE << 8) | (3u << 16);
     }
     return 0;
   };
@@ -2084,6 +2103,15 @@ __device__ __forceinline__ uint32_t trow_eval(const DevState& st, const TBatchAr
     if (f == KGPU_F_POD_TOPOLOGY_SPREAD) return pts();
     if (f == KGPU_F_INTER_POD_AFFINITY) return ipa();
     if (f == KGPU_F_NODE_AFFINITY) return tb_elig(ta, tp.aff_sig, n) ? 0 : KGPU_CODE_UNRESOLVABLE << 8;
+    if (f == KGPU_F_NODE_UNSCHEDULABLE)  // node_unschedulable.go:51-65
+      return (sr.unsched && !(q.flags & KGPU_Q_TOLERATES_UNSCHEDULABLE)) ? KGPU_CODE_UNRESOLVABLE << 8 : 0;
+    if (f == KGPU_F_TAINT_TOLERATION && st.TW <= 2) {  // taint_toleration.go:54-72
+      for (int w = 0; w < st.TW; ++w) {
+        const uint64_t tol = w < q.tol_nosched.count ? cp(st.qp.words)[q.tol_nosched.begin + w] : 0ull;
+        if (sr.tns[w] & ~tol) return KGPU_CODE_UNRESOLVABLE << 8;
+      }
+      return 0;
+    }
     return filter_one(f, st, q, r, n);
   };
   uint32_t status = 0;
@@ -2106,14 +2134,20 @@ __device__ __forceinline__ uint32_t trow_eval(const DevState& st, const TBatchAr
   }
   if (status) return status;
   NodeEval e{0, 0, 0, 0};
-  tscores<SM, kDef>(st, q, r, n, e);
+  tscores<SM, kDef>(st, q, r, n, e, st.TW <= 2);
+  if (st.TW <= 2 && st.w_of[KGPU_S_TAINT_TOLERATION] && st.any_prefer_taint) {  // taint_toleration.go:123-152
+    for (int w = 0; w < st.TW; ++w) {
+      const uint64_t tol = w < q.tol_prefer.count ? cp(st.qp.words)[q.tol_prefer.begin + w] : 0ull;
+      e.taint += __popcll(sr.tpr[w] & ~tol);
+    }
+  }
   o.part = e.partial;
   o.taint = e.taint;
   o.na = e.na;
   // PodTopologySpread ScheduleAnyway (scoring.go:75-102,174-208): INT64_MIN = ignored node
   o.adj = 0;
   if (tp.n_soft) {
-    const int v = nval(st, tp.soft_key, n);
+    const int v = nval(tp.soft_key);
     if (v < 0) {
       o.adj = INT64_MIN;
     } else {
@@ -2130,12 +2164,12 @@ __device__ __forceinline__ uint32_t trow_eval(const DevState& st, const TBatchAr
     for (int k = 0; k < tp.tabs.count - tp.n_exa_tabs; ++k) {
       const TTab tb = cp(ta.tabs)[tp.tabs.begin + k];
       if (tb.kind != 2) continue;
-      const int v = nval(st, tb.key, n);
+      const int v = nval(tb.key);
       if (v >= 0) is += PT[tb.off + v];
     }
     for (int e2 = 0; e2 < tp.score_u.count; ++e2) {
       const TLook t = cp(ta.looks)[tp.score_u.begin + e2];
-      if (nval(st, t.key, n) >= 0) is += (int64_t)t.weight * tcol(st, t, n);
+      if (nval(t.key) >= 0) is += (int64_t)t.weight * tcol(st, t, n);
     }
   }
   o.ipa = is;
@@ -2155,6 +2189,7 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
   uint32_t* SMASK = reinterpret_cast<uint32_t*>(lds_raw + ta.o_smask);
   int32_t* ZSUM = reinterpret_cast<int32_t*>(lds_raw + ta.o_zsum);
   int64_t* PT = reinterpret_cast<int64_t*>(lds_raw + ta.o_pt);
+  int32_t* LAB = reinterpret_cast<int32_t*>(lds_raw + ta.o_lab);  // [lab_keys][per] label value ids
   TMisc& M = *reinterpret_cast<TMisc*>(lds_raw + ta.o_misc);
   constexpr int W = B / 64;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -2165,15 +2200,27 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
   for (int i = tid; i < ta.reg_words; i += B) REG[i] = gp(ta.reg_init)[i];
   for (int i = tid; i < ta.n_hists; i += B) TOT[i] = gp(ta.tot_init)[i];
   for (int i = tid; i < ta.n_sigs; i += B) SANY[i] = gp(ta.sig_any)[i];
+  for (int i = tid; i < ta.lab_keys * ta.per; i += B) {
+    const int k = i / ta.per, n = lo + i % ta.per;
+    LAB[i] = n < st.N ? gp(st.label_val)[(size_t)k * st.N + n] : -1;
+  }
   if (tid == 0) M.abort = 0;
   NodeRes r[K];
+  TStatic sr[K];
 #pragma unroll
   for (int j = 0; j < K; ++j) {
     const int n = lo + j * B + tid;
     r[j] = NodeRes{};
+    sr[j] = TStatic{{0, 0}, {0, 0}, 0, -1};
     if (n < st.N) {
       r[j] = load_res(st, n);
       if constexpr (kDef) set_recips(r[j]);
+      sr[j].unsched = gp(st.unsched)[n];
+      sr[j].zone = gp(st.zone_id)[n];
+      for (int w = 0; w < st.TW && w < 2; ++w) {
+        sr[j].tns[w] = gp(st.taint_nosched)[(size_t)w * st.N + n];
+        sr[j].tpr[w] = gp(st.taint_prefer)[(size_t)w * st.N + n];
+      }
     }
   }
   const int R = ta.R;
@@ -2184,7 +2231,13 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
   for (int i = 0; i < ta.count; ++i) {
     KGPU_TSTAMP(0);
     const int pod = ta.first + i;
-    const kgpu_pod_query q = *cp(st.queries + pod);
+    if (wave == W - 1 && i + 1 < ta.count && lane < (int)(sizeof(kgpu_pod_query) / 16)) {
+      // warm the next pod's query record (its first touch would otherwise put a memory round
+      // trip at the head of the next pod)
+      const uint4 x = reinterpret_cast<const GAS uint4*>(gp(st.queries + pod + 1))[lane];
+      asm volatile("" ::"v"(x.x));
+    }
+    const kgpu_pod_query& q = *cp(st.queries + pod);
     const TPlan& tp = *cp(ta.plans + cp(ta.plan_of)[i]);
     const uint64_t tk = pod_tie_key(st.seed, ta.seq0 + i);
     // ---- the pod's lookup tables and PreFilter state (every workgroup, from its LDS replicas)
@@ -2228,7 +2281,8 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
       const int n = lo + j * B + tid;
       feas[j] = false;
       if (n >= st.N) continue;
-      if (trow_eval<FM, SM, kDef>(st, ta, q, tp, r[j], n, H, PT, M, pany, aff_any, o[j])) continue;
+      if (trow_eval<FM, SM, kDef>(st, ta, q, tp, r[j], n, H, PT, M, pany, aff_any, LAB, j * B + tid, sr[j], o[j]))
+        continue;
       feas[j] = true;
       ++sf;
       smaxT = max(smaxT, (uint32_t)o[j].taint);
@@ -2238,14 +2292,14 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
         sadjmin = min(sadjmin, (uint32_t)o[j].adj);
         sadjmax = max(sadjmax, (uint32_t)o[j].adj);
         if (tp.soft_mode == 0) {
-          const int v = nval(st, tp.soft_key, n);
+          const int v = tp.soft_key < ta.lab_keys ? LAB[tp.soft_key * ta.per + j * B + tid] : nval(st, tp.soft_key, n);
           atomicOr(SMASK + (v >> 5), 1u << (v & 31));
         }
       }
       simin = min(simin, o[j].ipa);
       simax = max(simax, o[j].ipa);
       sdmax = max(sdmax, (uint32_t)o[j].ds);
-      const int z = gp(st.zone_id)[n];
+      const int z = sr[j].zone;
       if (z >= 0) {
         szoned = 1;
         if (o[j].ds && z < ta.zones) atomicAdd(ZSUM + z, o[j].ds);
@@ -2369,7 +2423,7 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
       if (tp.dpts_cls != -2) {
         double f = Mx;
         if (dmax_node > 0) f = Mx * ((double)(dmax_node - o[j].ds) / (double)dmax_node);
-        const int z = gp(st.zone_id)[n];
+        const int z = sr[j].zone;
         if (have_zones && z >= 0) {
           double zs = Mx;
           if (dmax_zone > 0) zs = Mx * ((double)(dmax_zone - STAT[kTFixed + ta.soft_words + z]) / (double)dmax_zone);

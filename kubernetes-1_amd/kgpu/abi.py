@@ -33,6 +33,7 @@ TERM_REQ_AFF, TERM_REQ_ANTI, TERM_PREF_AFF, TERM_PREF_ANTI = range(4)
 PF_TERMINATING, PF_WITH_AFFINITY, PF_ACTIVE = 1, 2, 4
 (Q_TOLERATES_UNSCHED, Q_FIT_ALL_ZERO, Q_HAS_TSC, Q_HAS_POD_AFFINITY, Q_HAS_POD_ANTI, Q_SELF_MATCH_ALL_AFF,
  Q_TERMINATING, Q_REQ_NODE_AFFINITY, Q_SCORE_ERROR) = (1, 2, 4, 8, 16, 32, 64, 128, 256)
+Q_NO_KNOWN_IMAGE = 512
 
 RANGE = np.dtype([("begin", "<i4"), ("count", "<i4")], align=True)
 REQ = np.dtype([("key", "<i4"), ("op", "<i4"), ("vals", RANGE), ("imm", "<i8")], align=True)

@@ -729,6 +729,8 @@ class Compiler:
         q["pref_terms"] = pools._rng(pools.pref_terms, prefs)
         imgs = [self.images.get(api.normalized_image_name(c.get("image", "") or "")) for c in api.containers(pod)]
         q["images"] = pools.ints_range(imgs)
+        if all(i < 0 for i in imgs):
+            flags |= abi.Q_NO_KNOWN_IMAGE  # image_locality.go:53-79: sumScores 0 -> score 0
         ref = api.controller_ref(pod)
         q["avoid_id"] = -1
         if ref is not None and ref.get("kind") in ("ReplicationController", "ReplicaSet"):
