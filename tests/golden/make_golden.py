@@ -14,7 +14,8 @@ sys.path.insert(0, HERE)
 REF = "/root/reference"
 
 GROUPS = ["noderesources", "tainttoleration", "nodeaffinity", "normalize", "generic", "node_tree",
-          "podtopologyspread", "interpodaffinity", "misc"]
+          "podtopologyspread", "interpodaffinity", "defaultpodtopologyspread", "imagelocality",
+          "nodepreferavoidpods", "nodeports", "nodename", "nodeunschedulable", "misc"]
 
 
 def resolve(cases):
