@@ -268,3 +268,42 @@ def controller_ref(pod):
         if o.get("controller"):
             return o
     return None
+
+
+PREFER_AVOID_PODS_ANNOTATION = "scheduler.alpha.kubernetes.io/preferAvoidPods"
+
+
+def _ci(d, key):
+    """encoding/json matches struct field names case-insensitively."""
+    if not isinstance(d, dict):
+        return None
+    if key in d:
+        return d[key]
+    for k, v in d.items():
+        if k.lower() == key.lower():
+            return v
+    return None
+
+
+def avoid_pods(node):
+    """(kind, uid) of every preferAvoidPods entry with a podController.
+
+    pkg/apis/core/v1/helper/helpers.go:500-509 GetAvoidPodsFromNodeAnnotations decodes the JSON
+    annotation; node_prefer_avoid_pods.go:68-72 treats a decode error as "no entries".  The
+    already-decoded shorthand annotations["preferAvoidPods"] = [{"kind", "uid"}] is accepted too."""
+    ann = meta(node).get("annotations") or {}
+    out = []
+    raw = ann.get(PREFER_AVOID_PODS_ANNOTATION)
+    if isinstance(raw, str) and raw != "":
+        import json
+        try:
+            doc = json.loads(raw)
+            for a in _ci(doc, "preferAvoidPods") or []:
+                pc = _ci(_ci(a, "podSignature"), "podController")
+                if pc is not None:
+                    out.append((_ci(pc, "kind") or "", _ci(pc, "uid") or ""))
+        except (ValueError, TypeError, AttributeError):
+            return []
+    for a in ann.get("preferAvoidPods") or []:
+        out.append((a.get("kind"), a.get("uid")))
+    return out

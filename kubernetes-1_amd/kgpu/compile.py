@@ -367,8 +367,8 @@ class Compiler:
         for im in (n.get("status") or {}).get("images") or []:
             for nm in im.get("names") or []:
                 self.images.add(nm)
-        for a in ((api.meta(n).get("annotations") or {}).get("preferAvoidPods")) or []:
-            self.controllers.add((a.get("kind"), a.get("uid")))
+        for a in api.avoid_pods(n):
+            self.controllers.add(a)
         z = api.zone_key(n)
         if z:
             self.zones.add(z)
@@ -465,8 +465,8 @@ class Compiler:
                     ims[self.images.get(nm)] = int(float(int(im.get("sizeBytes", 0))) * spread)
             img_lists.append(sorted(ims.items()))
             av = set()
-            for a in ((api.meta(n).get("annotations") or {}).get("preferAvoidPods")) or []:
-                av.add(self.controllers.get((a.get("kind"), a.get("uid"))))
+            for a in api.avoid_pods(n):
+                av.add(self.controllers.get(a))
             avoid_lists.append(sorted(av))
         # existing pods -> node rows + pod table
         A.update(self._compile_existing(existing, A))

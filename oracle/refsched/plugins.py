@@ -6,6 +6,7 @@ that a reader can check them side by side.  All int64 arithmetic is exact Python
 (Go int64 does not overflow for any in-range input); float64 islands are Python floats
 (IEEE double, no FMA contraction) evaluated in the reference's operation order.
 """
+import json
 import math
 
 from . import labels as L
@@ -434,9 +435,9 @@ def controller_ref(pod):
 class NodePreferAvoidPods:
     """nodepreferavoidpods/node_prefer_avoid_pods.go:47-82.
 
-    The node annotation scheduler.alpha.kubernetes.io/preferAvoidPods is modelled as the
-    already-decoded list node.metadata.annotations["preferAvoidPods"] =
-    [{"kind": ..., "uid": ...}]; an undecodable annotation is modelled as absent.
+    The node annotation scheduler.alpha.kubernetes.io/preferAvoidPods (JSON, as in the reference)
+    is decoded by _avoids; the already-decoded shorthand node.metadata.annotations["preferAvoidPods"]
+    = [{"kind": ..., "uid": ...}] is accepted beside it.
     """
     name = "NodePreferAvoidPods"
 
@@ -450,11 +451,39 @@ class NodePreferAvoidPods:
             ref = None
         if ref is None:
             return MAX_NODE_SCORE, None
-        avoids = ((ni.node.get("metadata") or {}).get("annotations") or {}).get("preferAvoidPods") or []
-        for a in avoids:
-            if a.get("kind") == ref.get("kind") and a.get("uid") == ref.get("uid"):
+        for kind, uid in _avoids(ni.node):
+            if kind == ref.get("kind") and uid == ref.get("uid"):
                 return 0, None
         return MAX_NODE_SCORE, None
+
+
+def _json_field(d, key):
+    # encoding/json: exact field name first, then a case-insensitive match
+    if not isinstance(d, dict):
+        return None
+    if key in d:
+        return d[key]
+    return next((v for k, v in d.items() if k.lower() == key.lower()), None)
+
+
+def _avoids(node):
+    """v1helper.GetAvoidPodsFromNodeAnnotations (pkg/apis/core/v1/helper/helpers.go:500-509); a
+    decode error reads as no entries (node_prefer_avoid_pods.go:68-72), entries without a
+    podController are skipped (:73-78)."""
+    ann = (node.get("metadata") or {}).get("annotations") or {}
+    out = []
+    raw = ann.get("scheduler.alpha.kubernetes.io/preferAvoidPods") or ""
+    if raw:
+        try:
+            entries = _json_field(json.loads(raw), "preferAvoidPods") or []
+            for a in entries:
+                pc = _json_field(_json_field(a, "podSignature"), "podController")
+                if pc is not None:
+                    out.append((_json_field(pc, "kind") or "", _json_field(pc, "uid") or ""))
+        except (ValueError, TypeError, AttributeError):
+            out = []
+    out += [(a.get("kind"), a.get("uid")) for a in ann.get("preferAvoidPods") or []]
+    return out
 
 
 # ============================================================ DefaultSelector (helper/spread.go:29-72)

@@ -117,6 +117,8 @@ def oracle_eval(c):
         return {"scores": {str(i): s for i, (_, s) in enumerate(scores)}}
     if kind == "node_tree":
         return {"order": NI.node_tree_order(c["nodes"])}
+    if kind == "image_name":
+        return {"name": P.normalized_image_name(c["input"])}
     raise KeyError(kind)
 
 
@@ -165,6 +167,8 @@ def check(c, got):
             bad.append(("hosts", c["expect_possible"], got["hosts"]))
     if "expect_num" in c and got.get("num") != c["expect_num"]:
         bad.append(("num", c["expect_num"], got.get("num")))
+    if "expect_name" in c and got.get("name") != c["expect_name"]:
+        bad.append(("name", c["expect_name"], got.get("name")))
     if "expect_order" in c and got.get("order") != c["expect_order"]:
         bad.append(("order", c["expect_order"], got.get("order")))
     if "expect_hosts" in c:

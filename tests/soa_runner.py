@@ -4,7 +4,7 @@ import copy
 
 import numpy as np
 
-from kgpu import abi
+from kgpu import abi, api
 from kgpu.compile import Cluster, Profile
 from kgpu.framework import GpuFramework
 
@@ -25,6 +25,8 @@ def supported(c):
         return c["plugin"] in TIER1_SCORES
     if k == "filter":
         return c["plugin"] in TIER1_FILTERS
+    if k == "image_name":
+        return True
     if k == "schedule":
         prof = c.get("profile") or {}
         return all(n in TIER1_SCORES | {"DefaultPodTopologySpread"} for n, _ in prof.get("scores", []))
@@ -52,6 +54,9 @@ def _profile(c):
 
 
 def soa_eval(c, backend):
+    if c["kind"] == "image_name":
+        # host-side: kgpu/compile.py interns normalized names before any image id reaches the device
+        return {"name": api.normalized_image_name(c["input"])}
     try:
         prof = _profile(c)
     except ValueError as e:
