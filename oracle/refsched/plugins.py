@@ -637,6 +637,28 @@ class PodTopologySpread:
         state["PreFilterPodTopologySpread"] = {"constraints": cons, "pairs": pairs, "paths": paths}
         return None
 
+    # ---- filtering.go:123-143, 161-180 (AddPod / RemovePod, used by the nominated-pod pass)
+    def update_with_pod(self, state, updated_pod, preemptor, node, delta):
+        s = state.get("PreFilterPodTopologySpread")
+        if s is None or NI.namespace(updated_pod) != NI.namespace(preemptor) or node is None:
+            return
+        nl = NI.labels_of(node)
+        if not node_labels_match_spread(nl, s["constraints"]):
+            return
+        plabels = NI.labels_of(updated_pod)
+        for _, key, sel in s["constraints"]:
+            if not sel.matches(plabels):
+                continue
+            pair = (key, nl[key])
+            s["pairs"][pair] += delta
+            s["paths"][key].update(nl[key], s["pairs"][pair])
+
+    def add_pod(self, state, pod, pod_to_add, ni):
+        self.update_with_pod(state, pod_to_add, pod, ni.node, 1)
+
+    def remove_pod(self, state, pod, pod_to_remove, ni):
+        self.update_with_pod(state, pod_to_remove, pod, ni.node, -1)
+
     def filter(self, state, pod, ni):
         s = state.get("PreFilterPodTopologySpread")
         if s is None:

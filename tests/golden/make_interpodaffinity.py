@@ -244,5 +244,113 @@ def single_node_cases():
     return out
 
 
+def multi_node_cases():
+    """TestRequiredAffinityMultipleNodes (filtering_test.go:797-1683): every node of the table is
+    filtered, and each has its own expected status."""
+    out = []
+    CN, CN_AZ1, IN = {"region": "China"}, {"region": "China", "az": "az1"}, {"region": "India"}
+
+    def nd(name, **labels):
+        return node(name, labels)
+
+    def rzh(name, zone):
+        return nd(name, region="r1", zone=zone, hostname=name)
+
+    def fc(name, line, p, existing, nodes, want):
+        exp = {}
+        for n, w in zip(nodes, want):
+            exp[n["metadata"]["name"]] = {"code": 0, "reasons": []} if w is None else {"code": w[0], "reasons": list(w[1])}
+        out.append(case(name, FSRC + ":%d" % line, kind="filter", plugin="InterPodAffinity", args={}, pod=p,
+                        pods=existing, nodes=nodes, expect_filter=exp))
+
+    ex = lambda k: req(k, "Exists")
+    aff_fail, anti_fail, exist_fail = (UR, R_AFF), (U, R_ANTI), (U, R_EXIST)
+    fc("A pod can be scheduled onto all the nodes that have the same topology key & label value with one of them has "
+       "an existing pod that matches the affinity rules", 852,
+       cpwat("", "", None, [term([req("foo", "In", ["bar"])], "region")], None),
+       [pod({"foo": "bar"}, "machine1", name="p1")],
+       [node("machine1", CN), node("machine2", CN_AZ1), node("machine3", IN)], [None, None, aff_fail])
+    two_zone = [term([req("foo", "In", ["bar"])], "zone"), term([req("service", "In", ["securityscan"])], "zone")]
+    fc("The affinity rule is to schedule all of the pods of this collection to the same zone. The first pod of the "
+       "collection should not be blocked from being scheduled onto any node, even there's no existing pod that "
+       "matches the rule anywhere.", 888, cpwat("", "", {"foo": "bar", "service": "securityscan"}, two_zone, None),
+       [pod({"foo": "bar"}, "nodeA", name="p1")],
+       [nd("nodeA", zone="az1", hostname="h1"), nd("nodeB", zone="az2", hostname="h2")], [None, None])
+    fc("The first pod of the collection can only be scheduled on nodes labelled with the requested topology keys", 936,
+       cpwat("", "", {"foo": "bar", "service": "securityscan"}, two_zone, None),
+       [pod({"foo": "bar"}, "nodeA", name="p1")],
+       [nd("nodeA", zoneLabel="az1", hostname="h1"), nd("nodeB", zoneLabel="az2", hostname="h2")],
+       [aff_fail, aff_fail])
+    abc_region = [term([req("foo", "In", ["abc"])], "region")]
+    fc("NodeA and nodeB have same topologyKey and label value. NodeA has an existing pod that matches the inter pod "
+       "affinity rule. The pod can not be scheduled onto nodeA and nodeB.", 973,
+       cpwat("", "", None, None, abc_region), [pod({"foo": "abc"}, "nodeA")],
+       [nd("nodeA", region="r1", hostname="nodeA"), nd("nodeB", region="r1", hostname="nodeB")],
+       [anti_fail, anti_fail])
+    fc("This test ensures that anti-affinity matches a pod when any term of the anti-affinity rule matches a pod.",
+       1022, cpwat("", "", None, None, [term([req("foo", "In", ["abc"])], "region"),
+                                        term([req("service", "In", ["securityscan"])], "zone")]),
+       [pod({"foo": "abc", "service": "securityscan"}, "nodeA")], [rzh("nodeA", "z1"), rzh("nodeB", "z2")],
+       [anti_fail, anti_fail])
+    fc("NodeA and nodeB have same topologyKey and label value. NodeA has an existing pod that matches the inter pod "
+       "affinity rule. The pod can not be scheduled onto nodeA and nodeB but can be scheduled onto nodeC", 1061,
+       cpwat("", "", None, None, abc_region), [pod({"foo": "abc"}, "nodeA")],
+       [node("nodeA", CN), node("nodeB", CN_AZ1), node("nodeC", IN)], [anti_fail, anti_fail, None])
+    fc("NodeA and nodeB have same topologyKey and label value. NodeA has an existing pod that matches the inter pod "
+       "affinity rule. The pod can not be scheduled onto nodeA, nodeB, but can be scheduled onto nodeC (NodeC has an "
+       "existing pod that match the inter pod affinity rule but in different namespace)", 1121,
+       cpwat("NS1", "", {"foo": "123"}, None, [term([req("foo", "In", ["bar"])], "region")]),
+       [pod({"foo": "bar"}, "nodeA", ns="NS1"),
+        cpwat("NS2", "nodeC", None, None, [term([req("foo", "In", ["123"])], "region")])],
+       [node("nodeA", CN), node("nodeB", CN_AZ1), node("nodeC", IN)], [anti_fail, anti_fail, None])
+    z1 = [rzh("nodeA", "z1"), rzh("nodeB", "z1")]
+    z12 = [rzh("nodeA", "z1"), rzh("nodeB", "z2")]
+    fc("Test existing pod's anti-affinity: if an existing pod has a term with invalid topologyKey, labelSelector of "
+       "the term is firstly checked, and then topologyKey of the term is also checked", 1148,
+       pod({"foo": ""}), [cpwat("", "nodeA", None, None, [term([ex("foo")], "invalid-node-label")])], z1,
+       [None, None])
+    fc("Test incoming pod's anti-affinity: even if labelSelector matches, we still check if topologyKey matches", 1178,
+       cpwat("", "", None, None, [term([ex("foo")], "invalid-node-label")]), [pod({"foo": ""}, "nodeA")], z1,
+       [None, None])
+    fc("Test existing pod's anti-affinity: incoming pod wouldn't considered as a fit as it violates each existingPod's "
+       "terms on all nodes", 1230, pod({"foo": "", "bar": ""}),
+       [cpwat("", "nodeA", None, None, [term([ex("foo")], "zone")]),
+        cpwat("", "nodeA", None, None, [term([ex("bar")], "region")])], z12, [exist_fail, exist_fail])
+    fc("Test incoming pod's anti-affinity: incoming pod wouldn't considered as a fit as it at least violates one "
+       "anti-affinity rule of existingPod", 1288,
+       cpwat("", "", None, None, [term([ex("foo")], "zone"), term([ex("bar")], "region")]),
+       [pod({"foo": ""}, "nodeA"), pod({"bar": ""}, "nodeB")], z12, [anti_fail, anti_fail])
+    fc("Test existing pod's anti-affinity: only when labelSelector and topologyKey both match, it's counted as a "
+       "single term match - case when one term has invalid topologyKey", 1333, pod({"foo": "", "bar": ""}),
+       [cpwat("", "nodeA", None, None, [term([ex("foo")], "invalid-node-label"), term([ex("bar")], "zone")])], z12,
+       [exist_fail, None])
+    fc("Test incoming pod's anti-affinity: only when labelSelector and topologyKey both match, it's counted as a "
+       "single term match - case when one term has invalid topologyKey", 1381,
+       cpwat("", "", None, None, [term([ex("foo")], "invalid-node-label"), term([ex("bar")], "zone")]),
+       [pod({"foo": "", "bar": ""}, "nodeA", name="podA")], z12, [anti_fail, None])
+    fc("Test existing pod's anti-affinity: only when labelSelector and topologyKey both match, it's counted as a "
+       "single term match - case when all terms have valid topologyKey", 1430, pod({"foo": "", "bar": ""}),
+       [cpwat("", "nodeA", None, None, [term([ex("foo")], "region"), term([ex("bar")], "zone")])], z12,
+       [exist_fail, exist_fail])
+    fc("Test incoming pod's anti-affinity: only when labelSelector and topologyKey both match, it's counted as a "
+       "single term match - case when all terms have valid topologyKey", 1482,
+       cpwat("", "", None, None, [term([ex("foo")], "region"), term([ex("bar")], "zone")]),
+       [pod({"foo": "", "bar": ""}, "nodeA")], z12, [anti_fail, anti_fail])
+    fc("Test existing pod's anti-affinity: existingPod on nodeA and nodeB has at least one anti-affinity term matches "
+       "incoming pod, so incoming pod can only be scheduled to nodeC", 1558, pod({"foo": "", "bar": ""}),
+       [cpwat("", "nodeA", None, None, [term([ex("foo")], "zone"), term([ex("labelA")], "zone")]),
+        cpwat("", "nodeB", None, None, [term([ex("bar")], "zone"), term([ex("labelB")], "zone")])],
+       [rzh("nodeA", "z1"), rzh("nodeB", "z2"), rzh("nodeC", "z3")], [exist_fail, exist_fail, None])
+    fc("Test incoming pod's affinity: firstly check if all affinityTerms match, and then check if all topologyKeys "
+       "match", 1599, cpwat("", "", None, [term([ex("foo")], "region"), term([ex("bar")], "zone")], None),
+       [pod({"foo": "", "bar": ""}, "nodeA", name="pod1")], z1, [None, None])
+    fc("Test incoming pod's affinity: firstly check if all affinityTerms match, and then check if all topologyKeys "
+       "match, and the match logic should be satisfied on the same pod", 1657,
+       cpwat("", "", None, [term([ex("foo")], "region"), term([ex("bar")], "zone")], None),
+       [pod({"foo": ""}, "nodeA", name="pod1"), pod({"bar": ""}, "nodeB", name="pod2")], z12,
+       [aff_fail, aff_fail])
+    return out
+
+
 def all_cases():
-    return score_cases() + single_node_cases()
+    return score_cases() + single_node_cases() + multi_node_cases()

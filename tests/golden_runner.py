@@ -117,9 +117,50 @@ def oracle_eval(c):
         return {"scores": {str(i): s for i, (_, s) in enumerate(scores)}}
     if kind == "node_tree":
         return {"order": NI.node_tree_order(c["nodes"])}
+    if kind == "pts_state":
+        return pts_state(c)
     if kind == "image_name":
         return {"name": P.normalized_image_name(c["input"])}
     raise KeyError(kind)
+
+
+def _canon_selector(sel):
+    """A selector as sorted (key, op, values) triples; "=" and "==" read as one operator."""
+    if sel.nothing:
+        return "nothing"
+    return sorted([r.key, {"==": "="}.get(r.op, r.op), sorted(r.vals)] for r in sel.reqs)
+
+
+def pts_state(c):
+    """PodTopologySpread cycle state after PreFilter (+ AddPod/RemovePod) or PreScore."""
+    h = _handle(c)
+    pl = make_plugin("PodTopologySpread", c.get("args"), h)
+    state, pod = {}, c["pod"]
+    if c["op"] == "prescore":
+        st = pl.prescore(state, pod, [ni.node for ni in h.snapshot.list])
+        if not P.is_success(st):
+            return {"error": repr(st)}
+        s = state["PreScorePodTopologySpread"]
+        return {"state": {"constraints": [[m, k, _canon_selector(sel)] for m, k, sel in s["constraints"]],
+                          "ignored": sorted(s["ignored"]),
+                          "pairs": sorted([k, v, n] for (k, v), n in s["counts"].items()),
+                          "weights": list(s["weights"])}}
+    st = pl.prefilter(state, pod)
+    if not P.is_success(st):
+        return {"error": repr(st)}
+    if c["op"] in ("add", "remove"):
+        ni = h.snapshot.get(c["op_node"])
+        (pl.add_pod if c["op"] == "add" else pl.remove_pod)(state, pod, c["op_pod"], ni)
+    s = state["PreFilterPodTopologySpread"]
+    paths = {}
+    for k, cp in s["paths"].items():
+        p = [list(cp.p[0]), list(cp.p[1])]
+        # filtering_test.go:50-55 criticalPaths.sort: equal counts compare alphabetically
+        if p[0][1] == p[1][1] and p[0][0] > p[1][0]:
+            p[0][0], p[1][0] = p[1][0], p[0][0]
+        paths[k] = p
+    return {"state": {"constraints": [[m, k, _canon_selector(sel)] for m, k, sel in s["constraints"]],
+                      "paths": paths, "pairs": sorted([k, v, n] for (k, v), n in s["pairs"].items())}}
 
 
 def profile_from_case(c):
@@ -167,6 +208,8 @@ def check(c, got):
             bad.append(("hosts", c["expect_possible"], got["hosts"]))
     if "expect_num" in c and got.get("num") != c["expect_num"]:
         bad.append(("num", c["expect_num"], got.get("num")))
+    if "expect_state" in c:
+        bad += _check_state(c["expect_state"], got.get("state") or {})
     if "expect_name" in c and got.get("name") != c["expect_name"]:
         bad.append(("name", c["expect_name"], got.get("name")))
     if "expect_order" in c and got.get("order") != c["expect_order"]:
@@ -187,4 +230,25 @@ def check(c, got):
             for n, s in tot.items():
                 if g.get(n) != s:
                     bad.append((i, n, s, g.get(n)))
+    return bad
+
+
+def _check_state(want, got):
+    import math
+    from oracle.refsched import labels as L
+    bad = []
+    wc = [[m, k, _canon_selector(L.label_selector_as_selector(sel))] for m, k, sel in want.get("constraints", [])]
+    if wc != got.get("constraints"):
+        bad.append(("constraints", wc, got.get("constraints")))
+    for f in ("paths", "ignored"):
+        if f in want and want[f] != got.get(f):
+            bad.append((f, want[f], got.get(f)))
+    if sorted(map(list, want.get("pairs", []))) != got.get("pairs"):
+        bad.append(("pairs", want.get("pairs"), got.get("pairs")))
+    if "weight_sizes" in want:
+        # scoring.go:260 topologyNormalizingWeight(size) = math.Log(float64(size + 2))
+        w = [math.log(n + 2) for n in want["weight_sizes"]]
+        g = got.get("weights") or []
+        if len(w) != len(g) or any(abs(a - b) > 1e-15 * abs(a) for a, b in zip(w, g)):
+            bad.append(("weights", w, g))
     return bad
