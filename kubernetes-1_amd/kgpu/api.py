@@ -236,25 +236,90 @@ def zone_key(node):
     return region + ":\x00:" + zone
 
 
+class NodeTree:
+    """The scheduler cache's nodeTree (internal/cache/node_tree.go:31-196).
+
+    Zones (GetZoneKey) in first-insertion order, each an array of node names with a cursor.  The
+    cursors and the zone index persist across snapshots: Snapshot.List() after a node event is the
+    next numNodes outputs of next() (cache.go:278-301), which need not restart at zone 0."""
+
+    def __init__(self, nodes=()):
+        self.zones = []      # zone keys, first-insertion order
+        self.arrays = {}     # zone -> [names, cursor]
+        self.zone_index = 0
+        self.num_nodes = 0
+        for n in nodes:
+            self.add_node(n)
+
+    def add_node(self, n):
+        z, nm = zone_key(n), name_of(n)
+        arr = self.arrays.get(z)
+        if arr is None:
+            self.zones.append(z)
+            self.arrays[z] = [[nm], 0]
+        elif nm in arr[0]:
+            return                          # node_tree.go:72-77: already present, no change
+        else:
+            arr[0].append(nm)
+        self.num_nodes += 1
+
+    def remove_node(self, n):
+        """Returns False when the node is not in its zone's array (node_tree.go:106-107)."""
+        z, nm = zone_key(n), name_of(n)
+        arr = self.arrays.get(z)
+        if arr is None or nm not in arr[0]:
+            return False
+        arr[0].remove(nm)
+        if not arr[0]:
+            del self.arrays[z]
+            self.zones.remove(z)
+        self.num_nodes -= 1
+        return True
+
+    def update_node(self, old, new):
+        if old is not None and zone_key(old) == zone_key(new):
+            return
+        if old is None and zone_key(new) == "":
+            return
+        if old is not None:
+            self.remove_node(old)
+        self.add_node(new)
+
+    def _reset(self):
+        for arr in self.arrays.values():
+            arr[1] = 0
+        self.zone_index = 0
+
+    def next(self):
+        if not self.zones:
+            return ""
+        exhausted = 0
+        while True:
+            if self.zone_index >= len(self.zones):
+                self.zone_index = 0
+            arr = self.arrays[self.zones[self.zone_index]]
+            self.zone_index += 1
+            if arr[1] < len(arr[0]):
+                arr[1] += 1
+                return arr[0][arr[1] - 1]
+            exhausted += 1
+            if exhausted >= len(self.zones):
+                self._reset()
+
+    def list(self):
+        """One Snapshot.List() pass: numNodes calls of next()."""
+        return [self.next() for _ in range(self.num_nodes)]
+
+    def tree(self):
+        return {z: list(self.arrays[z][0]) for z in self.zones}
+
+
 def snapshot_order(nodes):
-    """nodeTree zone round-robin over insertion order (internal/cache/node_tree.go:147-170)."""
-    zones, groups = [], {}
+    """Snapshot.List() order of a freshly built cache: node objects in nodeTree order."""
+    by_name = {}
     for n in nodes:
-        z = zone_key(n)
-        if z not in groups:
-            zones.append(z)
-            groups[z] = []
-        groups[z].append(n)
-    out = []
-    if not zones:
-        return out
-    depth = max(len(g) for g in groups.values())
-    for i in range(depth):
-        for z in zones:
-            g = groups[z]
-            if i < len(g):
-                out.append(g[i])
-    return out
+        by_name.setdefault(name_of(n), n)
+    return [by_name[nm] for nm in NodeTree(nodes).list()]
 
 
 def normalized_image_name(n):

@@ -44,7 +44,8 @@ class Profile:
     def __init__(self, filters=None, prefilters=None, prescores=None, scores=None,
                  least_resources=(("cpu", 1), ("memory", 1)), most_resources=(("cpu", 1), ("memory", 1)),
                  hard_pod_affinity_weight=1, ignored_resources=(), pts_default_constraints=(),
-                 percentage_of_nodes_to_score=100, tie_break_mode=tiebreak.MODE_HASH, seed=0x7B):
+                 percentage_of_nodes_to_score=100, tie_break_mode=tiebreak.MODE_HASH, seed=0x7B,
+                 plugin_factories=None):
         self.filters = list(DEFAULT_FILTERS if filters is None else filters)
         self.prefilters = list(DEFAULT_PREFILTERS if prefilters is None else prefilters)
         self.prescores = list(DEFAULT_PRESCORES if prescores is None else prescores)
@@ -57,6 +58,9 @@ class Profile:
         self.percentage_of_nodes_to_score = percentage_of_nodes_to_score
         self.tie_break_mode = tie_break_mode
         self.seed = seed
+        # extra plugin constructors, name -> factory(handle): the fake plugins of the reference's
+        # generic_scheduler_test.go (tests/fake_plugins.py)
+        self.plugin_factories = dict(plugin_factories or {})
 
 
 def cluster_autoscaler_profile(**kw):
@@ -68,9 +72,10 @@ def cluster_autoscaler_profile(**kw):
 class Handle:
     """FrameworkHandle: snapshot lister + informer-backed listers used by DefaultSelector."""
 
-    def __init__(self, snapshot, services=(), rcs=(), rss=(), sss=()):
+    def __init__(self, snapshot, services=(), rcs=(), rss=(), sss=(), pvcs=()):
         self.snapshot = snapshot
         self.services, self.rcs, self.rss, self.sss = list(services), list(rcs), list(rss), list(sss)
+        self.pvcs = list(pvcs)
 
 
 class ScheduleError(Exception):
@@ -104,6 +109,8 @@ class Framework:
             "DefaultPodTopologySpread": lambda: P.DefaultPodTopologySpread(h),
             "InterPodAffinity": lambda: P.InterPodAffinity(h, profile.hard_pod_affinity_weight),
         }
+        for n, f in profile.plugin_factories.items():
+            reg[n] = (lambda f: lambda: f(h))(f)
         self.plugins = {}
 
         def get(n):
@@ -158,7 +165,9 @@ class Framework:
             for n in nodes:
                 s, st = pl.score(state, pod, NI.name(n))
                 if not P.is_success(st):
-                    raise ScheduleError("score plugin %s: %r" % (pl.name, st))
+                    # framework.go:603-607 -> generic_scheduler.go:640-642
+                    raise ScheduleError('error while running score plugin for pod "%s": %s'
+                                        % (NI.name(pod), "; ".join(st.reasons)))
                 lst.append([NI.name(n), s])
             out[pl.name] = lst
         for pl, w in self.scores:
@@ -207,6 +216,7 @@ class GenericScheduler:
         return num
 
     def schedule(self, pod, pod_seq):
+        pod_passes_basic_checks(pod, self.fw.handle.pvcs)
         snap = self.fw.handle.snapshot
         state = {}
         all_nodes = snap.list
@@ -259,6 +269,21 @@ class GenericScheduler:
                       [NI.name(n) for n in feasible])
 
 
+def pod_passes_basic_checks(pod, pvcs):
+    """generic_scheduler.go:1084-1107: every PVC volume must exist in the pod's namespace and not
+    be terminating."""
+    ns = NI.namespace(pod)
+    for v in (pod.get("spec") or {}).get("volumes") or []:
+        claim = (v.get("persistentVolumeClaim") or {}).get("claimName") if v.get("persistentVolumeClaim") else None
+        if claim is None:
+            continue
+        pvc = next((c for c in pvcs if NI.name(c) == claim and NI.namespace(c) == ns), None)
+        if pvc is None:
+            raise ScheduleError('persistentvolumeclaim "%s" not found' % claim)
+        if (pvc.get("metadata") or {}).get("deletionTimestamp") is not None:
+            raise ScheduleError('persistentvolumeclaim "%s" is being deleted' % claim)
+
+
 def select_host(totals, index, profile, pod_seq):
     """selectHost (generic_scheduler.go:217-238) with the deterministic packed-key tie-break."""
     if not totals:
@@ -272,12 +297,12 @@ def select_host(totals, index, profile, pod_seq):
 
 
 def schedule_sequence(nodes, existing_pods, pods, profile, services=(), rcs=(), rss=(), sss=(),
-                      first_seq=0):
+                      first_seq=0, pvcs=(), order="tree"):
     """scheduleOne loop: each placed pod is assumed (NodeInfo.AddPod) before the next one.
 
     Returns a list of Result (or FitError/ScheduleError instances for unschedulable pods)."""
-    snap = NI.Snapshot(nodes, existing_pods)
-    fw = Framework(profile, Handle(snap, services, rcs, rss, sss))
+    snap = NI.Snapshot(nodes, existing_pods, order=order)
+    fw = Framework(profile, Handle(snap, services, rcs, rss, sss, pvcs))
     gs = GenericScheduler(fw)
     out = []
     for i, pod in enumerate(pods):

@@ -388,6 +388,70 @@ def get_zone_key(node):
     return region + ":\x00:" + zone
 
 
+class NodeTreeRef:
+    """node_tree.go:31-196 step by step: tree map + zones list + zoneIndex + per-array lastIndex."""
+
+    def __init__(self, nodes=()):
+        self.tree = {}
+        self.zones = []
+        self.zone_index = 0
+        self.num_nodes = 0
+        for n in nodes or ():
+            self.add_node(n)
+
+    def add_node(self, n):                          # node_tree.go:69-86
+        zone = get_zone_key(n)
+        na = self.tree.get(zone)
+        if na is not None:
+            if name(n) in na["nodes"]:
+                return
+            na["nodes"].append(name(n))
+        else:
+            self.zones.append(zone)
+            self.tree[zone] = {"nodes": [name(n)], "last": 0}
+        self.num_nodes += 1
+
+    def remove_node(self, n):                       # node_tree.go:88-108; returns the error or None
+        zone = get_zone_key(n)
+        na = self.tree.get(zone)
+        if na is not None:
+            for i, nm in enumerate(na["nodes"]):
+                if nm == name(n):
+                    del na["nodes"][i]
+                    if not na["nodes"]:
+                        del self.tree[zone]
+                        self.zones.remove(zone)
+                    self.num_nodes -= 1
+                    return None
+        return "node %r in group %r was not found" % (name(n), zone)
+
+    def update_node(self, old, new):                # node_tree.go:120-132
+        old_zone = get_zone_key(old) if old is not None else ""
+        if old_zone == get_zone_key(new):
+            return
+        self.remove_node(old)
+        self.add_node(new)
+
+    def next(self):                                 # node_tree.go:144-170
+        if not self.zones:
+            return ""
+        num_exhausted = 0
+        while True:
+            if self.zone_index >= len(self.zones):
+                self.zone_index = 0
+            na = self.tree[self.zones[self.zone_index]]
+            self.zone_index += 1
+            if na["last"] >= len(na["nodes"]):
+                num_exhausted += 1
+                if num_exhausted >= len(self.zones):
+                    for a in self.tree.values():
+                        a["last"] = 0
+                    self.zone_index = 0
+                continue
+            na["last"] += 1
+            return na["nodes"][na["last"] - 1]
+
+
 def node_tree_order(nodes):
     """nodeTree: zone groups in first-insertion order, then round-robin (node_tree.go:147-170)."""
     zones, tree = [], {}

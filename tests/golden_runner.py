@@ -88,13 +88,18 @@ def oracle_eval(c):
     if kind == "schedule":
         prof = profile_from_case(c)
         res = F.schedule_sequence(c["nodes"], c.get("pods", []), c["schedule_pods"], prof,
-                                  c.get("services", []), c.get("rcs", []), c.get("rss", []), c.get("sss", []))
+                                  c.get("services", []), c.get("rcs", []), c.get("rss", []), c.get("sss", []),
+                                  pvcs=c.get("pvcs", []), order=c.get("order", "tree"))
         out = []
         for r in res:
             if isinstance(r, F.ScheduleError):
-                out.append({"host": None, "error": type(r).__name__})
+                e = {"host": None, "error": type(r).__name__, "message": str(r)}
+                if isinstance(r, F.FitError):
+                    e["fit"] = {n: [st.code, list(st.reasons)] for n, (_, st) in r.statuses.items()}
+                out.append(e)
             else:
-                out.append({"host": r.host, "totals": {n: s for n, s in r.totals}, "feasible": r.feasible})
+                out.append({"host": r.host, "totals": {n: s for n, s in r.totals}, "feasible": r.feasible,
+                            "evaluated": r.evaluated})
         return {"placements": out}
     if kind == "select":
         idx = {n: i for i, (n, _) in enumerate(c["list"])}
@@ -117,11 +122,31 @@ def oracle_eval(c):
         return {"scores": {str(i): s for i, (_, s) in enumerate(scores)}}
     if kind == "node_tree":
         return {"order": NI.node_tree_order(c["nodes"])}
+    if kind == "node_tree_ops":
+        return replay_node_tree(NI.NodeTreeRef(c["initial"]), c["ops"],
+                                lambda t, r: t.remove_node(r) is not None)
     if kind == "pts_state":
         return pts_state(c)
     if kind == "image_name":
         return {"name": P.normalized_image_name(c["input"])}
     raise KeyError(kind)
+
+
+def replay_node_tree(t, ops, remove_failed):
+    """Apply a node_tree_ops sequence to a nodeTree implementation; shared by the oracle and the
+    product's kgpu.api.NodeTree (tests/soa_runner.py)."""
+    output, errors = [], []
+    for op in ops:
+        if op[0] == "add":
+            t.add_node(op[1])
+        elif op[0] == "remove":
+            errors.append(bool(remove_failed(t, op[1])))
+        elif op[0] == "update":
+            t.update_node(op[1], op[2])
+        else:
+            output.append(t.next())
+    tree = {z: list(t.tree[z]["nodes"]) for z in t.zones} if isinstance(t, NI.NodeTreeRef) else t.tree()
+    return {"output": output, "tree": tree, "remove_errors": errors}
 
 
 def _canon_selector(sel):
@@ -178,6 +203,9 @@ def profile_from_case(c):
               "percentage_of_nodes_to_score", "tie_break_mode", "seed"):
         if k in p:
             kw[k] = p[k]
+    if "fake" in p:
+        import fake_plugins
+        kw["plugin_factories"] = fake_plugins.factories(p["fake"])
     if p.get("base") == "cluster_autoscaler":
         return F.cluster_autoscaler_profile(**kw)
     return F.Profile(**kw)
@@ -210,6 +238,9 @@ def check(c, got):
         bad.append(("num", c["expect_num"], got.get("num")))
     if "expect_state" in c:
         bad += _check_state(c["expect_state"], got.get("state") or {})
+    for f in ("output", "tree", "remove_errors"):
+        if "expect_" + f in c and got.get(f) != c["expect_" + f]:
+            bad.append((f, c["expect_" + f], got.get(f)))
     if "expect_name" in c and got.get("name") != c["expect_name"]:
         bad.append(("name", c["expect_name"], got.get("name")))
     if "expect_order" in c and got.get("order") != c["expect_order"]:
@@ -222,6 +253,15 @@ def check(c, got):
                     bad.append((i, None, h))
             elif h not in allowed:
                 bad.append((i, allowed, h))
+    for i, want in enumerate(c.get("expect_messages") or []):
+        if want is not None and want != got["placements"][i].get("message"):
+            bad.append((i, "message", want, got["placements"][i].get("message")))
+    for i, want in enumerate(c.get("expect_fit") or []):
+        if want is not None and want != got["placements"][i].get("fit"):
+            bad.append((i, "fit", want, got["placements"][i].get("fit")))
+    for i, want in enumerate(c.get("expect_evaluated") or []):
+        if want is not None and want != got["placements"][i].get("evaluated"):
+            bad.append((i, "evaluated", want, got["placements"][i].get("evaluated")))
     if "expect_totals" in c:
         for i, tot in enumerate(c["expect_totals"]):
             if tot is None:

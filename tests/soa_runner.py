@@ -25,10 +25,14 @@ def supported(c):
         return c["plugin"] in TIER1_SCORES
     if k == "filter":
         return c["plugin"] in TIER1_FILTERS
-    if k == "image_name":
+    if k in ("image_name", "node_tree", "node_tree_ops"):
         return True
     if k == "schedule":
         prof = c.get("profile") or {}
+        # the fake plugins of generic_scheduler_test.go and the PVC basic checks are oracle-only
+        if any(f not in TIER1_FILTERS for f in prof.get("filters", [])) or c.get("pvcs") or \
+                any((p.get("spec") or {}).get("volumes") for p in c["schedule_pods"]):
+            return False
         return all(n in TIER1_SCORES | {"DefaultPodTopologySpread"} for n, _ in prof.get("scores", []))
     return False
 
@@ -54,6 +58,11 @@ def _profile(c):
 
 
 def soa_eval(c, backend):
+    if c["kind"] == "node_tree":
+        return {"order": [api.name_of(n) for n in api.snapshot_order(c["nodes"])]}
+    if c["kind"] == "node_tree_ops":
+        from golden_runner import replay_node_tree
+        return replay_node_tree(api.NodeTree(c["initial"]), c["ops"], lambda t, r: not t.remove_node(r))
     if c["kind"] == "image_name":
         # host-side: kgpu/compile.py interns normalized names before any image id reaches the device
         return {"name": api.normalized_image_name(c["input"])}
@@ -75,6 +84,7 @@ def soa_eval(c, backend):
     pod = pods[0]
     if backend == "gpu":
         cr = fw.cycle(pod, assume=False)
+        res0 = cr.result
         words = {nm: 0 for nm in fw.order}
         for nm, st in cr.statuses.items():
             words[nm] = st
@@ -84,6 +94,7 @@ def soa_eval(c, backend):
         q, pc, pnp, errs = fw.compile_pods([pod])
         ref = RefEngine(fw.config, fw.snap)
         res, st, raw, norm = ref.schedule(q, pc, diag=True)
+        res0 = res[0]
         statuses = {}
         for i in np.nonzero(st)[0]:
             nm = fw.order[int(i)]
@@ -106,4 +117,6 @@ def soa_eval(c, backend):
     for name, w in prof.scores:
         for nm, (r, nv) in scores[name].items():
             totals[nm] = totals.get(nm, 0) + nv * w
-    return {"placements": [{"host": None, "totals": totals}]}
+    node = int(res0["node"])
+    return {"placements": [{"host": fw.order[node] if node >= 0 else None, "totals": totals,
+                            "evaluated": int(res0["evaluated"]), "feasible": int(res0["feasible"])}]}
