@@ -17,6 +17,11 @@
  *   kgpu_get_filter                 per-node PluginToStatus.Merge code (framework.go:477-502)
  *   kgpu_get_scores                 PluginToNodeScores (framework.go:579-656), raw and normalized
  *   kgpu_forget_pod                 cache.ForgetPod (cache.go:383-410) -> NodeInfo.RemovePod (types.go:484)
+ *   kgpu_apply_delta                the NodeInfo side of the informer / cache event stream between two
+ *                                   UpdateSnapshot calls (cache.go:202-301, 338-523, 581-647):
+ *                                   NodeInfo.AddPod / RemovePod (types.go:456-533) by pod UID,
+ *                                   NodeInfo.SetNode (types.go:587-600), and the Snapshot.List()
+ *                                   rebuild after a node add / remove (cache.go:278-301)
  *   kgpu_comm_*                     node sharding over RCCL/xGMI (no reference counterpart: the
  *                                   reference parallelises over 16 goroutines only,
  *                                   internal/parallelize/parallelism.go:26-43)
@@ -335,6 +340,8 @@ typedef struct kgpu_snapshot {
   const int32_t* pod_label_val; /* [n_pod_label_keys][n_pods] value id, -1 absent */
   const kgpu_term* terms;       /* existing pods' affinity terms */
   kgpu_pools pools;             /* pools referenced by terms */
+  const int64_t* pod_uid;       /* [n_pods] caller id of each pod's types.UID (kgpu_apply_delta); NULL:
+                                   the snapshot pods cannot be addressed by deltas */
 } kgpu_snapshot;
 
 typedef struct kgpu_result {
@@ -382,6 +389,80 @@ int kgpu_get_scores(kgpu_ctx* ctx, int32_t plugin, int64_t* raw, int64_t* normal
 
 /* Mirror coherence: ForgetPod / RemovePod of an existing pod slot (cache.go:383-410). */
 int kgpu_forget_pod(kgpu_ctx* ctx, int32_t pod_slot);
+
+/* ---- delta stream (kgpu_apply_delta).  The caller keeps the scheduler cache's bookkeeping
+ * (podStates / assumedPods / nodeTree, cache.go) and sends the NodeInfo changes it implies; the
+ * engine applies them to the device mirror in one launch and de-duplicates pods by UID. */
+#define KGPU_D_ADD_POD 1     /* NodeInfo.AddPod (types.go:456-480) on `node`: item = the pod (query).
+                                AssumePod, AddPod of a new or expired pod, the add half of UpdatePod or
+                                of a confirmed pod bound elsewhere.  E_STATE if `uid` is already on a node. */
+#define KGPU_D_REMOVE_POD 2  /* NodeInfo.RemovePod (types.go:484-533): item = the pod being removed (its
+                                requests are subtracted, as RemovePod recomputes them from the object);
+                                E_STATE if `uid` is not on `node`.  ForgetPod, RemovePod, the remove half
+                                of UpdatePod. */
+#define KGPU_D_SET_NODE 3    /* NodeInfo.SetNode (types.go:587-600) with the node's list position
+                                unchanged: item = node row.  cache.UpdateNode; a zone change does not
+                                move the node until the next list rebuild (cache.go:278-301). */
+
+typedef struct kgpu_delta {
+  int32_t op;         /* KGPU_D_* */
+  int32_t node;       /* global node index in Snapshot.List() after this batch's reorder */
+  int64_t uid;        /* pod ops: the caller's id for the pod's types.UID */
+  int32_t item;       /* pod ops: index into kgpu_delta_batch.pods; SET_NODE: into .rows */
+  int32_t pad;
+} kgpu_delta;
+
+/* A node's own attributes (everything NodeInfo derives from the v1.Node, not from its pods). */
+typedef struct kgpu_node_row {
+  int64_t alloc_cpu, alloc_mem, alloc_eph;
+  int32_t alloc_pods;
+  int32_t unschedulable;
+  int32_t zone_id;            /* GetZoneKey id, -1 none (may exceed n_zones: the count grows) */
+  int32_t pad;
+  kgpu_range labels;          /* int32 pool: (node label key id, value id) pairs; other keys absent */
+  kgpu_range taints;          /* u64 word pool: taint_words NoSchedule|NoExecute words, then
+                                 taint_words PreferNoSchedule words (empty range: no taints) */
+  kgpu_range alloc_scalar;    /* u64 word pool: n_scalar int64 allocatable values (empty: all 0) */
+} kgpu_node_row;
+
+typedef struct kgpu_delta_batch {
+  int32_t n_deltas;
+  int32_t n_pods;
+  const kgpu_delta* deltas;          /* applied in order, after the reorder below */
+  const kgpu_pod_query* pods;        /* pod records referenced by pod deltas */
+  int32_t n_rows;
+  int32_t n_order;                   /* 0: the node list is unchanged */
+  const kgpu_node_row* rows;         /* rows referenced by SET_NODE deltas (and new nodes) */
+  /* Node add / remove: the new Snapshot.List() (nodeTree.next() x numNodes, cache.go:278-301) as,
+   * per new position, the old index or -1 - r for a node with no old row (its attributes come from
+   * a SET_NODE delta on it in this batch; it starts with no pods).  Pods of dropped nodes leave the
+   * device (cache.RemoveNode drops the NodeInfo, cache.go:626-640). */
+  const int32_t* order;
+  /* label dictionary growth (new values of existing keys); NULL: unchanged.  Same layout as
+   * kgpu_snapshot: key_n_values[K], value_off[K+1], value_int / value_int_ok[value_off[K]],
+   * key_empty_value[K]. */
+  const int32_t* key_n_values;
+  const int32_t* value_off;
+  const int64_t* value_int;
+  const uint8_t* value_int_ok;
+  const int32_t* key_empty_value;
+  /* ImageLocality / NodePreferAvoidPods CSR over the (new) node list; NULL: unchanged.  Required
+   * with a reorder (scaledImageScore depends on len(NodeInfos().List()), image_locality.go:110). */
+  const int32_t* image_off;
+  const int32_t* image_id;
+  const int64_t* image_score;
+  const int32_t* avoid_off;
+  const int32_t* avoid_id;
+  int32_t n_zones;                   /* zone ids in use (0: unchanged) */
+  int32_t pad;
+  kgpu_pools pools;                  /* pools of `pods` and `rows` */
+} kgpu_delta_batch;
+
+/* Apply one batch of cache deltas to the device mirror and stamp it with `generation`
+ * (Snapshot.generation, cache.go:248-251).  slots (may be NULL) receives, per delta, the pod-table
+ * slot the pod occupies after an ADD_POD (-1 otherwise).  On any error the mirror is marked invalid
+ * (KGPU_E_STATE on later cycles) and the snapshot must be uploaded again. */
+int kgpu_apply_delta(kgpu_ctx* ctx, const kgpu_delta_batch* batch, int64_t generation, int32_t* slots);
 
 /* Read back node rows (requested / nonzero / pod count) for coherence checks. */
 int kgpu_read_nodes(kgpu_ctx* ctx, int64_t* req_cpu, int64_t* req_mem, int64_t* req_eph, int64_t* nz_cpu,

@@ -17,6 +17,7 @@
 #include <deque>
 #include <map>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "kgpu_internal.h"
@@ -59,16 +60,38 @@ struct kgpu_ctx {
   std::vector<int64_t> trace_host;
   int spec = 0;      // k_eval instantiation for the profile (kgpu::select_spec)
   std::vector<uint64_t> prefer_union;  // PreferNoSchedule taint ids present on any node
-  // pods assumed through this context (slot -> record), for kgpu_forget_pod
-  struct Assumed {
-    int node;
-    kgpu_pod_query q;
+  // Every pod on a device row, by pod-table slot (parallel to pod_rows): snapshot pods first, then
+  // pods assumed by a schedule call or added by kgpu_apply_delta.  The resource record is what
+  // NodeInfo.RemovePod subtracts for kgpu_forget_pod; snapshot pods have none (their removal goes
+  // through a REMOVE_POD delta, which carries the pod).
+  struct PodRec {
+    int64_t uid = 0;
+    bool has_uid = false;
+    bool active = false;
+    bool has_res = false;
+    int32_t node = -1;  // global node index, -1: on no listed node (node removed)
+    kgpu_pod_query q{};
     std::vector<kgpu_scalar_req> sc;
     std::vector<kgpu_port> ports;
-    bool active;
   };
-  std::vector<Assumed> assumed;
+  std::vector<PodRec> recs;
+  std::unordered_map<int64_t, int32_t> uid_slot;  // active pods with a UID
   int32_t n_snapshot_pods = 0;
+  // host copies for incremental bookkeeping under SET_NODE deltas
+  std::vector<int32_t> label_host;                 // [K][N] value ids
+  std::vector<std::vector<int32_t>> val_nodes;     // [K][values] nodes carrying the value
+  std::vector<int32_t> multi_values;               // [K] values carried by >= 2 nodes
+  std::vector<uint64_t> prefer_host;               // [TW][N]
+  std::vector<int32_t> prefer_cnt;                 // [TW * 64] nodes carrying PreferNoSchedule taint t
+  int64_t port_bound = 0;                          // upper bound of any node's UsedPorts entries
+  // Snapshot.List() may hold one NodeInfo at several positions: cache.go:283-291 takes numNodes
+  // nodeTree.next() outputs, and after a node add the tree can restart its round-robin half way
+  // through a pass.  Such rows are aliases: every change to the node is applied to all of them.
+  std::vector<int32_t> row_canon;                  // [N] first row of the row's node (local index)
+  std::unordered_map<int32_t, std::vector<int32_t>> alias_rows;  // canonical row -> all its rows
+  bool has_alias = false;
+  DevBuf flags_buf;                                // DevState::port_overflow
+  DevBuf d_ops, d_dpods, d_drows, d_dints, d_dwords, d_dscalars, d_dports, d_daux, d_remap, d_from;
   bool last_diag = false;
   std::vector<hipEvent_t> ev_pool;
   // ---- topology state (kgpu_internal.h "topology plugins")
@@ -562,6 +585,37 @@ int upload_vec(kgpu_ctx* c, DevBuf& b, const std::vector<T>& v, const T** dst) {
   if (rc) return rc;
   if (!v.empty()) HIP_OK(c, hipMemcpyAsync(b.p, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice, c->stream));
   *dst = static_cast<const T*>(b.p);
+  return KGPU_OK;
+}
+
+// Swap a registered device allocation for a new one (the old one is freed).
+void swap_alloc(std::vector<void*>& reg, void* old_p, void* new_p) {
+  for (void*& q : reg)
+    if (q == old_p) {
+      q = new_p;
+      (void)hipFree(old_p);
+      return;
+    }
+  reg.push_back(new_p);
+  if (old_p) (void)hipFree(old_p);
+}
+
+// NodeInfo.UsedPorts has no cap (HostPortInfo.Add): before a batch that may add `extra` entries
+// to one node, grow the [PS][N] slot table so that no entry can be lost.
+int reserve_ports(kgpu_ctx* c, int64_t extra) {
+  const int64_t need = c->port_bound + extra;
+  DevState& st = c->st;
+  if (need <= st.PS) return KGPU_OK;
+  const int ps = (int)std::max<int64_t>(need, 2 * (int64_t)st.PS);
+  const size_t N = (size_t)st.N;
+  kgpu_port* np = nullptr;
+  HIP_OK(c, hipMalloc(&np, sizeof(kgpu_port) * std::max<size_t>((size_t)ps * N, 1)));
+  HIP_OK(c, hipMemsetAsync(np, 0, sizeof(kgpu_port) * (size_t)ps * N, c->stream));
+  if (N) HIP_OK(c, hipMemcpyAsync(np, st.ports, sizeof(kgpu_port) * (size_t)st.PS * N, hipMemcpyDeviceToDevice, c->stream));
+  HIP_OK(c, hipStreamSynchronize(c->stream));
+  swap_alloc(c->snap_allocs, st.ports, np);
+  st.ports = np;
+  st.PS = ps;
   return KGPU_OK;
 }
 
@@ -1093,11 +1147,23 @@ int run_tbatch(kgpu_ctx* c, TRun& tr, int first, int count, int64_t first_seq, i
   return KGPU_OK;
 }
 
+int copy_to_aliases(kgpu_ctx* c, int32_t* cols, int ncols);
+int assume_via_delta(kgpu_ctx* c, const kgpu_pod_query& q, const kgpu_pools* pools, int32_t gnode);
+
 int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools* pools, int64_t first_seq,
               kgpu_result* results, kgpu_stats* stats, bool diag, int32_t assume) {
   if (!c->uploaded) return fail(c, KGPU_E_STATE, "no snapshot uploaded");
   if (n <= 0) return KGPU_OK;
   int rc;
+  if (c->has_alias && assume) {
+    // A node listed twice: the device assume updates one row only, so place pods one at a time
+    // and apply NodeInfo.AddPod to every row of the chosen node through k_delta.
+    for (int32_t i = 0; i < n; ++i) {
+      if ((rc = run_batch(c, qs + i, 1, pools, first_seq + i, results + i, stats, diag, 0))) return rc;
+      if (results[i].node >= 0 && (rc = assume_via_delta(c, qs[i], pools, results[i].node))) return rc;
+    }
+    return KGPU_OK;
+  }
   // topology plugins: plans, class columns, pools (kgpu_internal.h "topology plugins")
   std::vector<kgpu::QPlan> plans;
   std::vector<int32_t> aux;
@@ -1132,6 +1198,9 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
       if (kgpu::launch_class_init(static_cast<const DevState*>(c->dstate.p), c->classes_init,
                                   (int)c->classes.size() - c->classes_init, (int)c->pod_rows.size(), c->stream))
         return fail(c, KGPU_E_DEVICE, "k_class_init launch failed");
+      if (c->has_alias && (rc = copy_to_aliases(c, c->st.mcnt + (size_t)c->classes_init * c->st.N,
+                                                (int)c->classes.size() - c->classes_init)))
+        return rc;
       HIP_OK(c, hipStreamSynchronize(c->stream));
       c->classes_init = (int)c->classes.size();
     }
@@ -1149,6 +1218,10 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
   } else {
     c->st.plans = nullptr;
   }
+  int64_t batch_ports = 0;
+  if (assume)
+    for (int32_t i = 0; i < n; ++i) batch_ports += qs[i].ports.count;
+  if ((rc = reserve_ports(c, batch_ports))) return rc;
   if ((rc = upload_pools(c, pools))) return rc;
   if ((rc = ensure(c, c->queries, sizeof(kgpu_pod_query) * (size_t)n))) return rc;
   HIP_OK(c, hipMemcpyAsync(c->queries.p, qs, sizeof(kgpu_pod_query) * (size_t)n, hipMemcpyHostToDevice, c->stream));
@@ -1352,7 +1425,14 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
   HIP_OK(c, hipMemcpyAsync(results, st.results, sizeof(kgpu_result) * (size_t)n, hipMemcpyDeviceToHost, c->stream));
   if (used_persistent)
     HIP_OK(c, hipMemcpyAsync(&c->abort_host, abort_word, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+  int32_t port_overflow = 0;
+  if (batch_ports) HIP_OK(c, hipMemcpyAsync(&port_overflow, c->st.port_overflow, 4, hipMemcpyDeviceToHost, c->stream));
   HIP_OK(c, hipStreamSynchronize(c->stream));
+  c->port_bound += batch_ports;
+  if (port_overflow) {
+    c->uploaded = false;
+    return fail(c, KGPU_E_DEVICE, "a node's host-port slots ran out during assume: re-upload the snapshot");
+  }
   if (used_persistent && c->abort_host) {
     // Pods resolved before the abort have already been assumed on the device, but their results
     // were never returned: the mirror no longer matches the caller's records.  Refuse further
@@ -1397,21 +1477,555 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
         }
         c->pod_rows.push_back(std::move(row));
       }
-      kgpu_ctx::Assumed a;
-      // the row lives on this shard, or (-1) on another rank, which owns its forget
-      a.node = results[i].node - c->st.node_base;
-      if (a.node < 0 || a.node >= c->st.N) a.node = -1;
+      kgpu_ctx::PodRec a;
+      a.node = results[i].node;  // global: the row lives on this shard or on another rank's
       a.q = qs[i];
       a.active = true;
+      a.has_res = true;
       if (pools) {
         for (int k = 0; k < qs[i].scalars.count; ++k) a.sc.push_back(pools->scalars[qs[i].scalars.begin + k]);
         for (int k = 0; k < qs[i].ports.count; ++k) a.ports.push_back(pools->ports[qs[i].ports.begin + k]);
       }
-      c->assumed.push_back(std::move(a));
+      c->recs.push_back(std::move(a));
     }
   }
   c->last_diag = diag;
   return KGPU_OK;
+}
+
+// Per-node work buffers, the percentageOfNodesToScore cut and the math.Log table: everything
+// sized by the node count that carries no state across cycles (upload and node-list rebuilds).
+int alloc_node_work(kgpu_ctx* c) {
+  DevState& st = c->st;
+  const size_t N = (size_t)st.N;
+  free_all(c->work_allocs);
+  auto& W = c->work_allocs;
+  int rc;
+  if ((rc = dalloc(c, W, &st.status, N))) return rc;
+  if ((rc = dalloc(c, W, &st.raw_taint, N))) return rc;
+  if ((rc = dalloc(c, W, &st.raw_na, N))) return rc;
+  if ((rc = dalloc(c, W, &st.partial, N))) return rc;
+  if ((rc = dalloc(c, W, &st.sbuf, (size_t)2 * kgpu::kMaxBlocks))) return rc;
+  if ((rc = dalloc(c, W, &st.kbuf, (size_t)2 * kgpu::kMaxBlocks))) return rc;
+  if ((rc = dalloc(c, W, &st.diag_raw, (size_t)KGPU_NUM_SCORES * N))) return rc;
+  if ((rc = dalloc(c, W, &st.diag_norm, (size_t)KGPU_NUM_SCORES * N))) return rc;
+  HIP_OK(c, hipMemset(st.status, 0, sizeof(uint32_t) * std::max<size_t>(N, 1)));
+  if ((rc = dalloc(c, W, &st.raw_pts, N))) return rc;
+  if ((rc = dalloc(c, W, &st.raw_ipa, N))) return rc;
+  if ((rc = dalloc(c, W, &st.raw_dpts, N))) return rc;
+  // percentageOfNodesToScore: nextStartNodeIndex lives with the generic scheduler, not the snapshot
+  // (generic_scheduler.go:451,487), so it carries over a re-upload (taken mod N on use)
+  st.to_find = num_feasible_nodes_to_find(st.n_total, c->cfg.percentage_of_nodes_to_score);
+  if (st.to_find < st.n_total) {
+    if ((rc = ensure(c, c->cut_buf, 16))) return rc;
+    if (!c->cut_init) {
+      HIP_OK(c, hipMemset(c->cut_buf.p, 0, 16));
+      c->cut_init = true;
+    }
+    st.cut_state = static_cast<int32_t*>(c->cut_buf.p);
+  } else {
+    st.cut_state = nullptr;
+  }
+  // math.Log(x) for x = 0 .. n_total + 2 (PodTopologySpread weights, scoring.go:286-288)
+  std::vector<double> lt((size_t)st.n_total + 3);
+  for (size_t x = 0; x < lt.size(); ++x) lt[x] = go_log((double)x);
+  return dcopy(c, W, &st.log_table, lt.data(), lt.size());
+}
+
+// key_unique (hostname-like keys) and the PreferNoSchedule union from the host copies.
+void rebuild_node_books(kgpu_ctx* c) {
+  const DevState& st = c->st;
+  const size_t N = (size_t)st.N;
+  c->val_nodes.assign((size_t)st.K, {});
+  c->multi_values.assign((size_t)st.K, 0);
+  c->key_unique.assign((size_t)st.K, 0);
+  for (int k = 0; k < st.K; ++k) {
+    auto& vn = c->val_nodes[(size_t)k];
+    vn.assign((size_t)std::max(c->key_n_values[(size_t)k], 1), 0);
+    for (size_t i = 0; i < N; ++i) {
+      const int32_t v = c->label_host[(size_t)k * N + i];
+      if (v < 0) continue;
+      if (v >= (int32_t)vn.size()) vn.resize((size_t)v + 1, 0);
+      if (++vn[(size_t)v] == 2) c->multi_values[(size_t)k] += 1;
+    }
+    // a key is node-unique when no value labels two nodes (and no node's value is "", which a node
+    // missing the key also stands for in PodTopologySpread's counts)
+    c->key_unique[(size_t)k] = (c->key_empty[(size_t)k] < 0 && c->multi_values[(size_t)k] == 0) ? 1 : 0;
+  }
+  c->prefer_cnt.assign((size_t)st.TW * 64, 0);
+  for (int w = 0; w < st.TW; ++w)
+    for (size_t i = 0; i < N; ++i) {
+      uint64_t b = c->prefer_host[(size_t)w * N + i];
+      while (b) {
+        c->prefer_cnt[(size_t)w * 64 + (size_t)__builtin_ctzll(b)] += 1;
+        b &= b - 1;
+      }
+    }
+  c->prefer_union.assign((size_t)st.TW, 0ull);
+  for (size_t t = 0; t < c->prefer_cnt.size(); ++t)
+    if (c->prefer_cnt[t]) c->prefer_union[t / 64] |= 1ull << (t % 64);
+  int anyp = 0;
+  for (uint64_t w : c->prefer_union) anyp |= (w != 0);
+  c->st.any_prefer_taint = anyp;
+}
+
+
+// ---------------------------------------------------------------- delta stream
+// Ops resolved on the host (slot, classes, term classes), launched as one k_delta.
+struct DeltaBuild {
+  std::vector<kgpu::DeltaOp> ops;
+  std::vector<int32_t> aux;
+};
+
+// The pod's side of the topology columns: classes it matches (mcnt) and the term classes it owns
+// (tcnt) -- the same sets an assume increments (assume_counts).
+void pod_op(kgpu_ctx* c, DeltaBuild& b, int kind, int local_node, int item, int slot) {
+  kgpu::DeltaOp op{};
+  op.kind = kind;
+  op.node = local_node;
+  op.item = item;
+  op.slot = -1;
+  op.cls.begin = (int32_t)b.aux.size();
+  const kgpu_ctx::PodRow& row = c->pod_rows[(size_t)slot];
+  if (c->st.mcnt)
+    for (int cl = 0; cl < c->classes_init; ++cl)
+      if (class_matches(c, cl, row.ns, row.flags | KGPU_PF_ACTIVE, row.pairs.data(), (int)row.pairs.size() / 2))
+        b.aux.push_back(cl);
+  op.cls.count = (int32_t)b.aux.size() - op.cls.begin;
+  op.tcls.begin = (int32_t)b.aux.size();
+  if (c->st.tcnt) b.aux.insert(b.aux.end(), row.own_tcls.begin(), row.own_tcls.end());
+  op.tcls.count = (int32_t)b.aux.size() - op.tcls.begin;
+  b.ops.push_back(op);
+}
+
+template <class T>
+int upload_span(kgpu_ctx* c, DevBuf& buf, const T* src, size_t n, const T** dst) {
+  int rc = ensure(c, buf, sizeof(T) * std::max<size_t>(n, 1));
+  if (rc) return rc;
+  if (n && src) HIP_OK(c, hipMemcpyAsync(buf.p, src, sizeof(T) * n, hipMemcpyHostToDevice, c->stream));
+  *dst = static_cast<const T*>(buf.p);
+  return KGPU_OK;
+}
+
+int launch_ops(kgpu_ctx* c, const DeltaBuild& b, const kgpu_pod_query* pods, int n_pods, const kgpu_node_row* rows,
+               int n_rows, const int32_t* ints, int n_ints, const uint64_t* words, int n_words,
+               const kgpu_scalar_req* scalars, int n_scalars, const kgpu_port* ports, int n_ports) {
+  if (b.ops.empty()) return KGPU_OK;
+  kgpu::DeltaArgs a{};
+  int rc;
+  if ((rc = upload_span(c, c->d_ops, b.ops.data(), b.ops.size(), &a.ops)) ||
+      (rc = upload_span(c, c->d_daux, b.aux.data(), b.aux.size(), &a.aux)) ||
+      (rc = upload_span(c, c->d_dpods, pods, (size_t)n_pods, &a.pods)) ||
+      (rc = upload_span(c, c->d_drows, rows, (size_t)n_rows, &a.rows)) ||
+      (rc = upload_span(c, c->d_dints, ints, (size_t)n_ints, &a.ints)) ||
+      (rc = upload_span(c, c->d_dwords, words, (size_t)n_words, &a.words)) ||
+      (rc = upload_span(c, c->d_dscalars, scalars, (size_t)n_scalars, &a.scalars)) ||
+      (rc = upload_span(c, c->d_dports, ports, (size_t)n_ports, &a.ports)))
+    return rc;
+  a.n_ops = (int32_t)b.ops.size();
+  if ((rc = ensure(c, c->dstate, sizeof(DevState)))) return rc;
+  c->st_batch = c->st;
+  HIP_OK(c, hipMemcpyAsync(c->dstate.p, &c->st_batch, sizeof(DevState), hipMemcpyHostToDevice, c->stream));
+  if (kgpu::launch_delta(static_cast<const DevState*>(c->dstate.p), a, c->stream))
+    return fail(c, KGPU_E_DEVICE, "k_delta launch failed");
+  int32_t overflow = 0;
+  HIP_OK(c, hipMemcpyAsync(&overflow, c->st.port_overflow, 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(c, hipStreamSynchronize(c->stream));
+  if (overflow) return fail(c, KGPU_E_DEVICE, "a node's host-port slots ran out while applying deltas");
+  return KGPU_OK;
+}
+
+// SET_NODE bookkeeping on the host copies (labels -> key_unique, PreferNoSchedule union).
+int set_node_books(kgpu_ctx* c, int n, const kgpu_node_row& r, const kgpu_pools& p) {
+  DevState& st = c->st;
+  const size_t N = (size_t)st.N;
+  if (r.labels.count % 2 || (r.labels.count && (!p.ints || r.labels.begin + r.labels.count > p.n_ints)))
+    return fail(c, KGPU_E_INVAL, "node row labels out of the pool");
+  if (r.taints.count && (r.taints.count != 2 * st.TW || !p.words || r.taints.begin + r.taints.count > p.n_words))
+    return fail(c, KGPU_E_INVAL, "node row taints must be 2 x taint_words words of the pool");
+  if (r.alloc_scalar.count > st.S || (r.alloc_scalar.count && (!p.words || r.alloc_scalar.begin + r.alloc_scalar.count > p.n_words)))
+    return fail(c, KGPU_E_INVAL, "node row scalars out of range");
+  std::vector<int32_t> nv((size_t)st.K, -1);
+  for (int j = 0; j < r.labels.count; j += 2) {
+    const int32_t k = p.ints[r.labels.begin + j], v = p.ints[r.labels.begin + j + 1];
+    if (k < 0 || k >= st.K) return fail(c, KGPU_E_INVAL, "node label key outside the snapshot's keys: re-upload");
+    if (v < 0 || v >= c->key_n_values[(size_t)k])
+      return fail(c, KGPU_E_INVAL, "node label value outside the key's dictionary (send key_n_values)");
+    nv[(size_t)k] = v;
+  }
+  for (int k = 0; k < st.K; ++k) {
+    int32_t& cur = c->label_host[(size_t)k * N + (size_t)n];
+    if (cur == nv[(size_t)k]) continue;
+    auto& vn = c->val_nodes[(size_t)k];
+    if (cur >= 0 && --vn[(size_t)cur] == 1) c->multi_values[(size_t)k] -= 1;
+    cur = nv[(size_t)k];
+    if (cur >= 0) {
+      if (cur >= (int32_t)vn.size()) vn.resize((size_t)cur + 1, 0);
+      if (++vn[(size_t)cur] == 2) c->multi_values[(size_t)k] += 1;
+    }
+    c->key_unique[(size_t)k] = (c->key_empty[(size_t)k] < 0 && c->multi_values[(size_t)k] == 0) ? 1 : 0;
+  }
+  for (int w = 0; w < st.TW; ++w) {
+    uint64_t& cur = c->prefer_host[(size_t)w * N + (size_t)n];
+    const uint64_t nw = r.taints.count ? p.words[r.taints.begin + st.TW + w] : 0ull;
+    for (uint64_t b = cur & ~nw; b; b &= b - 1) c->prefer_cnt[(size_t)w * 64 + (size_t)__builtin_ctzll(b)] -= 1;
+    for (uint64_t b = nw & ~cur; b; b &= b - 1) c->prefer_cnt[(size_t)w * 64 + (size_t)__builtin_ctzll(b)] += 1;
+    cur = nw;
+  }
+  c->prefer_union.assign((size_t)st.TW, 0ull);
+  int anyp = 0;
+  for (size_t t = 0; t < c->prefer_cnt.size(); ++t)
+    if (c->prefer_cnt[t]) {
+      c->prefer_union[t / 64] |= 1ull << (t % 64);
+      anyp = 1;
+    }
+  st.any_prefer_taint = anyp;
+  if (r.zone_id >= st.n_zones) st.n_zones = r.zone_id + 1;
+  return KGPU_OK;
+}
+
+// Snapshot.List() rebuild after node adds / removes (cache.go:278-301): every node column is
+// gathered on the device into the new order; new rows start empty (their SET_NODE follows).
+int reorder_nodes(kgpu_ctx* c, const kgpu_delta_batch* b) {
+  DevState& st = c->st;
+  if (c->comm) return fail(c, KGPU_E_UNSUPPORTED, "node-list rebuild on a node-sharded engine: re-upload the shards");
+  if (!b->image_off || !b->avoid_off)
+    return fail(c, KGPU_E_INVAL, "a node-list rebuild needs the ImageLocality / NodePreferAvoidPods CSR");
+  const int oldN = st.N, newN = b->n_order;
+  std::vector<int32_t> from((size_t)newN), inv((size_t)std::max(oldN, 1), -1);
+  std::unordered_map<int32_t, int32_t> first;  // order value -> first new position (aliases share it)
+  std::vector<int32_t> canon((size_t)newN);
+  for (int i = 0; i < newN; ++i) {
+    const int32_t o = b->order[i];
+    if (o >= oldN) return fail(c, KGPU_E_INVAL, "order names a node index past the old list");
+    // an old row keeps the canonical row of its node (old aliases collapse onto one node)
+    const int32_t key = o >= 0 ? c->row_canon[(size_t)o] : o;
+    auto it = first.emplace(key, i).first;
+    canon[(size_t)i] = it->second;
+    if (o >= 0 && inv[(size_t)o] < 0) inv[(size_t)o] = i;
+    from[(size_t)i] = o >= 0 ? o : -1;
+  }
+  // every old row of a node maps to the node's first new row
+  for (int o = 0; o < oldN; ++o) {
+    auto it = first.find(c->row_canon[(size_t)o]);
+    inv[(size_t)o] = it == first.end() ? -1 : it->second;
+  }
+  struct Col {
+    void** field;
+    int elem, ncols;
+    bool registered;
+  };
+  const std::vector<Col> cols = {
+      {(void**)&st.alloc_cpu, 8, 1, true},      {(void**)&st.alloc_mem, 8, 1, true},
+      {(void**)&st.alloc_eph, 8, 1, true},      {(void**)&st.alloc_pods, 4, 1, true},
+      {(void**)&st.req_cpu, 8, 1, true},        {(void**)&st.req_mem, 8, 1, true},
+      {(void**)&st.req_eph, 8, 1, true},        {(void**)&st.nz_cpu, 8, 1, true},
+      {(void**)&st.nz_mem, 8, 1, true},         {(void**)&st.num_pods, 4, 1, true},
+      {(void**)&st.alloc_scalar, 8, st.S, true}, {(void**)&st.req_scalar, 8, st.S, true},
+      {(void**)&st.unsched, 1, 1, true},        {(void**)&st.label_val, 4, st.K, true},
+      {(void**)&st.taint_nosched, 8, st.TW, true}, {(void**)&st.taint_prefer, 8, st.TW, true},
+      {(void**)&st.port_count, 4, 1, true},     {(void**)&st.ports, 16, st.PS, true},
+      {(void**)&st.zone_id, 4, 1, true},        {(void**)&st.mcnt, 4, c->Ccap, false},
+      {(void**)&st.tcnt, 4, c->TCcap, false}};
+  std::vector<kgpu::RemapCol> desc;
+  std::vector<void*> fresh(cols.size(), nullptr);
+  for (size_t i = 0; i < cols.size(); ++i) {
+    const size_t bytes = (size_t)cols[i].elem * (size_t)std::max(cols[i].ncols, 0) * (size_t)newN;
+    HIP_OK(c, hipMalloc(&fresh[i], std::max<size_t>(bytes, 16)));
+    if (bytes && *cols[i].field && oldN > 0) desc.push_back({*cols[i].field, fresh[i], cols[i].elem, cols[i].ncols});
+    else if (bytes) HIP_OK(c, hipMemsetAsync(fresh[i], 0, bytes, c->stream));
+  }
+  const int32_t* dfrom;
+  const kgpu::RemapCol* ddesc;
+  int rc;
+  if ((rc = upload_span(c, c->d_from, from.data(), from.size(), &dfrom)) ||
+      (rc = upload_span(c, c->d_remap, desc.data(), desc.size(), &ddesc)))
+    return rc;
+  if (kgpu::launch_remap(ddesc, (int)desc.size(), dfrom, oldN, newN, c->stream))
+    return fail(c, KGPU_E_DEVICE, "k_remap launch failed");
+  HIP_OK(c, hipStreamSynchronize(c->stream));
+  for (size_t i = 0; i < cols.size(); ++i) {
+    if (cols[i].registered) swap_alloc(c->snap_allocs, *cols[i].field, fresh[i]);
+    else if (*cols[i].field) (void)hipFree(*cols[i].field);
+    *cols[i].field = fresh[i];
+  }
+  // CSR lists over the new order
+  const size_t nimg = (size_t)b->image_off[newN], navoid = (size_t)b->avoid_off[newN];
+  auto recopy = [&](auto** field, const auto* src, size_t n) -> int {
+    using T = std::remove_cv_t<std::remove_pointer_t<std::remove_pointer_t<decltype(field)>>>;
+    T* np = nullptr;
+    HIP_OK(c, hipMalloc(&np, sizeof(T) * std::max<size_t>(n, 1)));
+    if (n) HIP_OK(c, hipMemcpy(np, src, sizeof(T) * n, hipMemcpyHostToDevice));
+    swap_alloc(c->snap_allocs, (void*)*field, np);
+    *field = np;
+    return KGPU_OK;
+  };
+  if ((rc = recopy(&st.image_off, b->image_off, (size_t)newN + 1)) || (rc = recopy(&st.image_id, b->image_id, nimg)) ||
+      (rc = recopy(&st.image_score, b->image_score, nimg)) ||
+      (rc = recopy(&st.avoid_off, b->avoid_off, (size_t)newN + 1)) || (rc = recopy(&st.avoid_id, b->avoid_id, navoid)))
+    return rc;
+  // host copies and pod records follow the rows
+  std::vector<int32_t> lab((size_t)st.K * newN, -1);
+  std::vector<uint64_t> pref((size_t)st.TW * newN, 0ull);
+  for (int i = 0; i < newN; ++i) {
+    const int f = from[(size_t)i];
+    if (f < 0) continue;
+    for (int k = 0; k < st.K; ++k) lab[(size_t)k * newN + i] = c->label_host[(size_t)k * oldN + f];
+    for (int w = 0; w < st.TW; ++w) pref[(size_t)w * newN + i] = c->prefer_host[(size_t)w * oldN + f];
+  }
+  c->label_host.swap(lab);
+  c->prefer_host.swap(pref);
+  for (size_t sl = 0; sl < c->recs.size(); ++sl) {
+    kgpu_ctx::PodRec& r = c->recs[sl];
+    const int nn = (r.node >= 0 && r.node < oldN) ? inv[(size_t)r.node] : -1;
+    if (nn < 0 && r.active) {
+      // cache.RemoveNode drops the NodeInfo with its pods (cache.go:626-640)
+      r.active = false;
+      c->pod_rows[sl].flags &= ~KGPU_PF_ACTIVE;
+      if (r.has_uid) c->uid_slot.erase(r.uid);
+    }
+    r.node = nn;
+    c->pod_rows[sl].node = nn;
+  }
+  c->pod_rows_dev = -1;
+  c->row_canon.swap(canon);
+  c->alias_rows.clear();
+  c->has_alias = false;
+  for (int i = 0; i < newN; ++i)
+    if (c->row_canon[(size_t)i] != i) {
+      auto& v = c->alias_rows[c->row_canon[(size_t)i]];
+      if (v.empty()) v.push_back(c->row_canon[(size_t)i]);
+      v.push_back(i);
+      c->has_alias = true;
+    }
+  st.N = newN;
+  st.n_total = newN;
+  if ((rc = alloc_node_work(c))) return rc;
+  rebuild_node_books(c);
+  return KGPU_OK;
+}
+
+// Class columns counted on canonical rows only (k_class_init walks the pod table): copy them to
+// the alias rows, in place (alias rows read their canonical row, which maps to itself).
+int copy_to_aliases(kgpu_ctx* c, int32_t* cols, int ncols) {
+  if (ncols <= 0) return KGPU_OK;
+  const kgpu::RemapCol d{cols, cols, 4, ncols};
+  const int32_t* dfrom;
+  const kgpu::RemapCol* ddesc;
+  int rc;
+  if ((rc = upload_span(c, c->d_from, c->row_canon.data(), c->row_canon.size(), &dfrom)) ||
+      (rc = upload_span(c, c->d_remap, &d, 1, &ddesc)))
+    return rc;
+  if (kgpu::launch_remap(ddesc, 1, dfrom, c->st.N, c->st.N, c->stream)) return fail(c, KGPU_E_DEVICE, "k_remap launch failed");
+  return KGPU_OK;
+}
+
+// Every row of the node that local row `r` belongs to.
+std::vector<int32_t> node_rows(const kgpu_ctx* c, int32_t r) {
+  const int32_t cr = c->row_canon.empty() ? r : c->row_canon[(size_t)r];
+  auto it = c->alias_rows.find(cr);
+  if (it == c->alias_rows.end()) return {cr};
+  return it->second;
+}
+
+// Label dictionary growth (new values of existing keys).
+int update_key_meta(kgpu_ctx* c, const kgpu_delta_batch* b) {
+  DevState& st = c->st;
+  if (!b->key_n_values) return KGPU_OK;
+  if (!b->value_off || !b->value_int || !b->value_int_ok || !b->key_empty_value)
+    return fail(c, KGPU_E_INVAL, "label dictionary update needs every key metadata array");
+  const int K = st.K;
+  for (int k = 0; k < K; ++k)
+    if (b->key_n_values[k] < c->key_n_values[(size_t)k]) return fail(c, KGPU_E_INVAL, "label dictionaries only grow");
+  const size_t nv = (size_t)b->value_off[K];
+  auto recopy = [&](auto** field, const auto* src, size_t n) -> int {
+    using T = std::remove_cv_t<std::remove_pointer_t<std::remove_pointer_t<decltype(field)>>>;
+    T* np = nullptr;
+    HIP_OK(c, hipMalloc(&np, sizeof(T) * std::max<size_t>(n, 1)));
+    if (n) HIP_OK(c, hipMemcpy(np, src, sizeof(T) * n, hipMemcpyHostToDevice));
+    swap_alloc(c->snap_allocs, (void*)*field, np);
+    *field = np;
+    return KGPU_OK;
+  };
+  int rc;
+  if ((rc = recopy(&st.key_n_values, b->key_n_values, (size_t)K)) || (rc = recopy(&st.value_off, b->value_off, (size_t)K + 1)) ||
+      (rc = recopy(&st.value_int, b->value_int, nv)) || (rc = recopy(&st.value_int_ok, b->value_int_ok, nv)) ||
+      (rc = recopy(&st.key_empty_value, b->key_empty_value, (size_t)K)))
+    return rc;
+  st.key_empty = st.key_empty_value;
+  c->key_n_values.assign(b->key_n_values, b->key_n_values + K);
+  c->key_empty.assign(b->key_empty_value, b->key_empty_value + K);
+  for (int k = 0; k < K; ++k) {
+    c->val_nodes[(size_t)k].resize((size_t)std::max(c->key_n_values[(size_t)k], 1), 0);
+    c->key_unique[(size_t)k] = (c->key_empty[(size_t)k] < 0 && c->multi_values[(size_t)k] == 0) ? 1 : 0;
+  }
+  return KGPU_OK;
+}
+
+int update_csr(kgpu_ctx* c, const kgpu_delta_batch* b) {
+  DevState& st = c->st;
+  const size_t N = (size_t)st.N;
+  auto recopy = [&](auto** field, const auto* src, size_t n) -> int {
+    using T = std::remove_cv_t<std::remove_pointer_t<std::remove_pointer_t<decltype(field)>>>;
+    T* np = nullptr;
+    HIP_OK(c, hipMalloc(&np, sizeof(T) * std::max<size_t>(n, 1)));
+    if (n) HIP_OK(c, hipMemcpy(np, src, sizeof(T) * n, hipMemcpyHostToDevice));
+    swap_alloc(c->snap_allocs, (void*)*field, np);
+    *field = np;
+    return KGPU_OK;
+  };
+  int rc;
+  if (b->image_off) {
+    const size_t ni = (size_t)b->image_off[N];
+    if ((rc = recopy(&st.image_off, b->image_off, N + 1)) || (rc = recopy(&st.image_id, b->image_id, ni)) ||
+        (rc = recopy(&st.image_score, b->image_score, ni)))
+      return rc;
+  }
+  if (b->avoid_off) {
+    const size_t na = (size_t)b->avoid_off[N];
+    if ((rc = recopy(&st.avoid_off, b->avoid_off, N + 1)) || (rc = recopy(&st.avoid_id, b->avoid_id, na))) return rc;
+  }
+  return KGPU_OK;
+}
+
+int apply_delta(kgpu_ctx* c, const kgpu_delta_batch* b, int32_t* slots) {
+  DevState& st = c->st;
+  int rc;
+  if (b->n_order > 0 && (rc = reorder_nodes(c, b))) return rc;
+  if ((rc = update_key_meta(c, b))) return rc;
+  if (b->n_order <= 0 && (rc = update_csr(c, b))) return rc;
+  if (b->n_zones > st.n_zones) st.n_zones = b->n_zones;
+  const kgpu_pools& P = b->pools;
+  const bool topo = topo_profile(c);
+  DeltaBuild db;
+  bool pods_changed = false;
+  for (int i = 0; i < b->n_deltas; ++i) {
+    const kgpu_delta& d = b->deltas[i];
+    if (slots) slots[i] = -1;
+    int local = d.node - st.node_base;
+    const bool mine = d.node >= 0 && local >= 0 && local < st.N;
+    if (mine) local = c->row_canon[(size_t)local];
+    const int32_t gnode = mine ? local + st.node_base : d.node;  // the node's canonical (first) row
+    if (d.op == KGPU_D_SET_NODE) {
+      if (d.item < 0 || d.item >= b->n_rows) return fail(c, KGPU_E_INVAL, "SET_NODE row index out of range");
+      if (d.node < 0 || d.node >= st.n_total) return fail(c, KGPU_E_INVAL, "SET_NODE node index out of range");
+      if (!mine) continue;
+      for (int32_t r : node_rows(c, local)) {
+        if ((rc = set_node_books(c, r, b->rows[d.item], P))) return rc;
+        db.ops.push_back(kgpu::DeltaOp{kgpu::kDSetNode, r, d.item, -1, {0, 0}, {0, 0}});
+      }
+      continue;
+    }
+    if (d.op != KGPU_D_ADD_POD && d.op != KGPU_D_REMOVE_POD) return fail(c, KGPU_E_INVAL, "unknown delta op");
+    if (d.item < 0 || d.item >= b->n_pods) return fail(c, KGPU_E_INVAL, "pod delta item out of range");
+    const kgpu_pod_query& q = b->pods[d.item];
+    if (q.scalars.count && q.scalars.begin + q.scalars.count > P.n_scalars) return fail(c, KGPU_E_INVAL, "pod scalars out of the pool");
+    if (q.ports.count && q.ports.begin + q.ports.count > P.n_ports) return fail(c, KGPU_E_INVAL, "pod ports out of the pool");
+    if (q.labels.count && q.labels.begin + q.labels.count > P.n_ints) return fail(c, KGPU_E_INVAL, "pod labels out of the pool");
+    for (int k = 0; k < q.scalars.count; ++k)
+      if (P.scalars[q.scalars.begin + k].col >= st.S)
+        return fail(c, KGPU_E_INVAL, "pod scalar resource outside the snapshot's scalar columns: re-upload");
+    pods_changed = true;
+    if (d.op == KGPU_D_ADD_POD) {
+      if (d.node < 0 || d.node >= st.n_total) return fail(c, KGPU_E_INVAL, "ADD_POD on a node outside Snapshot.List()");
+      if (c->uid_slot.count(d.uid)) return fail(c, KGPU_E_STATE, "ADD_POD: the pod uid is already on a node");
+      const int32_t slot = (int32_t)c->recs.size();
+      kgpu_ctx::PodRec rec;
+      rec.uid = d.uid;
+      rec.has_uid = true;
+      rec.active = true;
+      rec.has_res = true;
+      rec.node = gnode;
+      rec.q = q;
+      for (int k = 0; k < q.scalars.count; ++k) rec.sc.push_back(P.scalars[q.scalars.begin + k]);
+      for (int k = 0; k < q.ports.count; ++k) rec.ports.push_back(P.ports[q.ports.begin + k]);
+      kgpu_ctx::PodRow row;
+      row.node = gnode;
+      row.ns = q.ns;
+      row.flags = query_pod_flags(q);
+      if (q.labels.count) row.pairs.assign(P.ints + q.labels.begin, P.ints + q.labels.begin + q.labels.count);
+      if (topo) {
+        const kgpu_range tr[4] = {q.ipa_req_aff, q.ipa_req_anti, q.ipa_pref_aff, q.ipa_pref_anti};
+        const int tk[4] = {KGPU_TERM_REQ_AFF, KGPU_TERM_REQ_ANTI, KGPU_TERM_PREF_AFF, KGPU_TERM_PREF_ANTI};
+        for (int k = 0; k < 4; ++k)
+          for (int j = 0; j < tr[k].count; ++j) {
+            const kgpu_pod_term& t = P.pod_terms[tr[k].begin + j];
+            row.own_tcls.push_back(intern_tclass(c, tk[k], t.weight, t.topo_key, term_item(t, &P)));
+          }
+      }
+      c->recs.push_back(std::move(rec));
+      c->pod_rows.push_back(std::move(row));
+      c->uid_slot.emplace(d.uid, slot);
+      if (slots) slots[i] = slot;
+      if (mine) {
+        if (topo && (rc = grow_columns(c, &st.tcnt, &c->TCcap, (int)c->tclasses.size()))) return rc;
+        if ((rc = reserve_ports(c, q.ports.count))) return rc;
+        c->port_bound += q.ports.count;
+        for (int32_t r : node_rows(c, local)) pod_op(c, db, kgpu::kDAddPod, r, d.item, slot);
+      }
+    } else {
+      auto it = c->uid_slot.find(d.uid);
+      if (it == c->uid_slot.end()) return fail(c, KGPU_E_STATE, "REMOVE_POD: no pod with this uid on a node");
+      const int32_t slot = it->second;
+      kgpu_ctx::PodRec& rec = c->recs[(size_t)slot];
+      if (rec.node != gnode) return fail(c, KGPU_E_STATE, "REMOVE_POD: the pod is on another node");
+      if (mine)
+        for (int32_t r : node_rows(c, local)) pod_op(c, db, kgpu::kDRemovePod, r, d.item, slot);
+      rec.active = false;
+      c->pod_rows[(size_t)slot].flags &= ~KGPU_PF_ACTIVE;
+      c->uid_slot.erase(it);
+    }
+  }
+  if (pods_changed) c->pod_rows_dev = -1;
+  return launch_ops(c, db, b->pods, b->n_pods, b->rows, b->n_rows, P.ints, P.n_ints, P.words, P.n_words, P.scalars,
+                    P.n_scalars, P.ports, P.n_ports);
+}
+// Reserve-time assume of a pod placed by a schedule call, through k_delta on every row of the
+// chosen node (the aliased-list path of run_batch).
+int assume_via_delta(kgpu_ctx* c, const kgpu_pod_query& q, const kgpu_pools* pools, int32_t gnode) {
+  kgpu_pools empty{};
+  const kgpu_pools& P = pools ? *pools : empty;
+  const int32_t slot = (int32_t)c->recs.size();
+  kgpu_ctx::PodRec rec;
+  rec.active = true;
+  rec.has_res = true;
+  rec.q = q;
+  for (int k = 0; k < q.scalars.count; ++k) rec.sc.push_back(P.scalars[q.scalars.begin + k]);
+  for (int k = 0; k < q.ports.count; ++k) rec.ports.push_back(P.ports[q.ports.begin + k]);
+  kgpu_ctx::PodRow row;
+  row.ns = q.ns;
+  row.flags = query_pod_flags(q);
+  if (q.labels.count) row.pairs.assign(P.ints + q.labels.begin, P.ints + q.labels.begin + q.labels.count);
+  if (topo_profile(c)) {
+    const kgpu_range tr[4] = {q.ipa_req_aff, q.ipa_req_anti, q.ipa_pref_aff, q.ipa_pref_anti};
+    const int tk[4] = {KGPU_TERM_REQ_AFF, KGPU_TERM_REQ_ANTI, KGPU_TERM_PREF_AFF, KGPU_TERM_PREF_ANTI};
+    for (int k = 0; k < 4; ++k)
+      for (int j = 0; j < tr[k].count; ++j) {
+        const kgpu_pod_term& t = P.pod_terms[tr[k].begin + j];
+        row.own_tcls.push_back(intern_tclass(c, tk[k], t.weight, t.topo_key, term_item(t, &P)));
+      }
+  }
+  int local = gnode - c->st.node_base;
+  const bool mine = local >= 0 && local < c->st.N;
+  if (mine) local = c->row_canon[(size_t)local];
+  rec.node = mine ? local + c->st.node_base : gnode;
+  row.node = rec.node;
+  c->recs.push_back(std::move(rec));
+  c->pod_rows.push_back(std::move(row));
+  c->pod_rows_dev = -1;
+  if (!mine) return KGPU_OK;
+  int rc;
+  if (topo_profile(c) && (rc = grow_columns(c, &c->st.tcnt, &c->TCcap, (int)c->tclasses.size()))) return rc;
+  if ((rc = reserve_ports(c, q.ports.count))) return rc;
+  c->port_bound += q.ports.count;
+  kgpu_ctx::PodRec& r = c->recs[(size_t)slot];
+  kgpu_pod_query qq = q;
+  qq.scalars = kgpu_range{0, (int32_t)r.sc.size()};
+  qq.ports = kgpu_range{0, (int32_t)r.ports.size()};
+  DeltaBuild db;
+  for (int32_t rr : node_rows(c, local)) pod_op(c, db, kgpu::kDAddPod, rr, 0, slot);
+  return launch_ops(c, db, &qq, 1, nullptr, 0, nullptr, 0, nullptr, 0, r.sc.data(), (int)r.sc.size(), r.ports.data(),
+                    (int)r.ports.size());
 }
 
 }  // namespace
@@ -1429,7 +2043,8 @@ int kgpu_struct_sizes(int32_t* out, int32_t n) {
                        (int32_t)sizeof(kgpu_pod_query), (int32_t)sizeof(kgpu_pools),
                        (int32_t)sizeof(kgpu_resource_weight), (int32_t)sizeof(kgpu_config),
                        (int32_t)sizeof(kgpu_snapshot),  (int32_t)sizeof(kgpu_result),
-                       (int32_t)sizeof(kgpu_stats)};
+                       (int32_t)sizeof(kgpu_stats),     (int32_t)sizeof(kgpu_delta),
+                       (int32_t)sizeof(kgpu_node_row),  (int32_t)sizeof(kgpu_delta_batch)};
   const int32_t m = (int32_t)(sizeof(s) / sizeof(s[0]));
   for (int32_t i = 0; i < n && i < m; ++i) out[i] = s[i];
   return m;
@@ -1561,7 +2176,8 @@ int kgpu_upload_snapshot(kgpu_ctx* c, const kgpu_snapshot* s, int64_t generation
   HIP_OK(c, hipStreamSynchronize(c->stream));
   free_all(c->snap_allocs);
   free_all(c->work_allocs);
-  c->assumed.clear();
+  c->recs.clear();
+  c->uid_slot.clear();
   c->uploaded = false;
   DevState& st = c->st;
   const size_t N = (size_t)s->n_nodes;
@@ -1599,10 +2215,10 @@ int kgpu_upload_snapshot(kgpu_ctx* c, const kgpu_snapshot* s, int64_t generation
   std::vector<uint64_t> zeros((size_t)st.TW * N, 0ull);
   UP(taint_nosched, s->taint_words > 0 ? s->taint_nosched : zeros.data(), (size_t)st.TW * N);
   UP(taint_prefer, s->taint_words > 0 ? s->taint_prefer : zeros.data(), (size_t)st.TW * N);
-  c->prefer_union.assign(st.TW, 0ull);
-  if (s->taint_words > 0)
-    for (int w = 0; w < st.TW; ++w)
-      for (size_t i = 0; i < N; ++i) c->prefer_union[w] |= s->taint_prefer[(size_t)w * N + i];
+  c->prefer_host.assign((size_t)st.TW * N, 0ull);
+  if (s->taint_words > 0) std::memcpy(c->prefer_host.data(), s->taint_prefer, sizeof(uint64_t) * (size_t)st.TW * N);
+  c->label_host.assign((size_t)st.K * N, -1);
+  if (st.K > 0) std::memcpy(c->label_host.data(), s->label_val, sizeof(int32_t) * (size_t)st.K * N);
   // host ports: reserve room for assumed pods' ports
   st.PS = std::max(s->port_slots, 8);
   UP(port_count, s->port_count, N);
@@ -1622,60 +2238,17 @@ int kgpu_upload_snapshot(kgpu_ctx* c, const kgpu_snapshot* s, int64_t generation
   UP(avoid_id, s->avoid_id, navoid);
   UP(zone_id, s->zone_id, N);
 #undef UP
-  // work buffers
-  auto& W = c->work_allocs;
-  if ((rc = dalloc(c, W, &st.status, N))) return rc;
-  if ((rc = dalloc(c, W, &st.raw_taint, N))) return rc;
-  if ((rc = dalloc(c, W, &st.raw_na, N))) return rc;
-  if ((rc = dalloc(c, W, &st.partial, N))) return rc;
-  if ((rc = dalloc(c, W, &st.sbuf, (size_t)2 * kgpu::kMaxBlocks))) return rc;
-  if ((rc = dalloc(c, W, &st.kbuf, (size_t)2 * kgpu::kMaxBlocks))) return rc;
-  if ((rc = dalloc(c, W, &st.diag_raw, (size_t)KGPU_NUM_SCORES * N))) return rc;
-  if ((rc = dalloc(c, W, &st.diag_norm, (size_t)KGPU_NUM_SCORES * N))) return rc;
-  HIP_OK(c, hipMemset(st.status, 0, sizeof(uint32_t) * std::max<size_t>(N, 1)));
-  if ((rc = dalloc(c, W, &st.raw_pts, N))) return rc;
-  if ((rc = dalloc(c, W, &st.raw_ipa, N))) return rc;
-  if ((rc = dalloc(c, W, &st.raw_dpts, N))) return rc;
+  if ((rc = alloc_node_work(c))) return rc;
   st.key_empty = st.key_empty_value;
   st.hard_pod_affinity_weight = c->cfg.hard_pod_affinity_weight;
-  // percentageOfNodesToScore: nextStartNodeIndex lives with the generic scheduler, not the snapshot
-  // (generic_scheduler.go:451,487), so it carries over a re-upload (taken mod N on use)
-  st.to_find = num_feasible_nodes_to_find(st.n_total, c->cfg.percentage_of_nodes_to_score);
-  if (st.to_find < st.n_total) {
-    if ((rc = ensure(c, c->cut_buf, 16))) return rc;
-    if (!c->cut_init) {
-      HIP_OK(c, hipMemset(c->cut_buf.p, 0, 16));
-      c->cut_init = true;
-    }
-    st.cut_state = static_cast<int32_t*>(c->cut_buf.p);
-  } else {
-    st.cut_state = nullptr;
-  }
-  {
-    // math.Log(x) for x = 0 .. n_total + 2 (PodTopologySpread weights, scoring.go:286-288)
-    std::vector<double> lt((size_t)st.n_total + 3);
-    for (size_t x = 0; x < lt.size(); ++x) lt[x] = go_log((double)x);
-    if ((rc = dcopy(c, R, &st.log_table, lt.data(), lt.size()))) return rc;
-  }
+  if ((rc = ensure(c, c->flags_buf, 64))) return rc;
+  HIP_OK(c, hipMemset(c->flags_buf.p, 0, 64));
+  st.port_overflow = static_cast<int32_t*>(c->flags_buf.p);
   // topology state: host copies of the key metadata, the pod table, existing pods' term classes
   c->key_n_values.assign(s->key_n_values ? s->key_n_values : nullptr, s->key_n_values ? s->key_n_values + st.K : nullptr);
   c->key_empty.assign(s->key_empty_value ? s->key_empty_value : nullptr,
                       s->key_empty_value ? s->key_empty_value + st.K : nullptr);
-  c->key_unique.assign((size_t)st.K, 0);
-  for (int k = 0; k < st.K; ++k) {
-    // a key is node-unique when no value labels two nodes (and no node's value is "", which a node
-    // missing the key also stands for in PodTopologySpread's counts)
-    if (c->key_empty[(size_t)k] >= 0) continue;
-    std::vector<uint8_t> seen((size_t)std::max(c->key_n_values[(size_t)k], 1), 0);
-    bool uniq = true;
-    for (size_t i = 0; i < N && uniq; ++i) {
-      const int32_t v = s->label_val[(size_t)k * N + i];
-      if (v < 0) continue;
-      if (v >= (int32_t)seen.size() || seen[(size_t)v]) uniq = false;
-      else seen[(size_t)v] = 1;
-    }
-    c->key_unique[(size_t)k] = uniq ? 1 : 0;
-  }
+  rebuild_node_books(c);
   c->class_ids.clear();
   c->tclass_ids.clear();
   c->classes.clear();
@@ -1687,6 +2260,16 @@ int kgpu_upload_snapshot(kgpu_ctx* c, const kgpu_snapshot* s, int64_t generation
   c->pod_rows.clear();
   c->pod_rows_dev = -1;
   for (int i = 0; i < s->n_pods; ++i) {
+    kgpu_ctx::PodRec rec;
+    rec.node = s->pod_node[i];
+    rec.active = (s->pod_flags[i] & KGPU_PF_ACTIVE) != 0;
+    if (s->pod_uid) {
+      rec.uid = s->pod_uid[i];
+      rec.has_uid = true;
+      if (rec.active && !c->uid_slot.emplace(rec.uid, i).second)
+        return fail(c, KGPU_E_INVAL, "duplicate pod uid in the snapshot");
+    }
+    c->recs.push_back(std::move(rec));
     kgpu_ctx::PodRow row;
     row.node = s->pod_node[i];
     row.ns = s->pod_ns[i];
@@ -1720,9 +2303,12 @@ int kgpu_upload_snapshot(kgpu_ctx* c, const kgpu_snapshot* s, int64_t generation
     for (auto& cell : term_cells) tc_host[(size_t)cell.first * N + cell.second] += 1;
     HIP_OK(c, hipMemcpy(st.tcnt, tc_host.data(), sizeof(int32_t) * tc_host.size(), hipMemcpyHostToDevice));
   }
-  int anyp = 0;
-  for (uint64_t w : c->prefer_union) anyp |= (w != 0);
-  st.any_prefer_taint = anyp;
+  c->port_bound = 0;
+  for (size_t i = 0; i < N; ++i) c->port_bound = std::max<int64_t>(c->port_bound, s->port_count[i]);
+  c->row_canon.resize(N);
+  for (size_t i = 0; i < N; ++i) c->row_canon[i] = (int32_t)i;
+  c->alias_rows.clear();
+  c->has_alias = false;
   c->n_snapshot_pods = s->n_pods;
   c->generation = generation;
   c->uploaded = true;
@@ -1741,11 +2327,10 @@ int kgpu_schedule_one(kgpu_ctx* c, const kgpu_pod_query* q, const kgpu_pools* po
                       kgpu_result* res, int32_t* assumed_slot) {
   if (!c || !q || !res) return KGPU_E_INVAL;
   if (hipSetDevice(c->device) != hipSuccess) return KGPU_E_DEVICE;
-  size_t before = c->assumed.size();
+  size_t before = c->recs.size();
   int rc = run_batch(c, q, 1, pools, pod_seq, res, nullptr, true, assume);
   if (rc) return rc;
-  if (assumed_slot)
-    *assumed_slot = c->assumed.size() > before ? c->n_snapshot_pods + (int32_t)c->assumed.size() - 1 : -1;
+  if (assumed_slot) *assumed_slot = c->recs.size() > before ? (int32_t)c->recs.size() - 1 : -1;
   return KGPU_OK;
 }
 
@@ -1782,74 +2367,51 @@ int kgpu_read_nodes(kgpu_ctx* c, int64_t* req_cpu, int64_t* req_mem, int64_t* re
 
 int kgpu_forget_pod(kgpu_ctx* c, int32_t slot) {
   if (!c) return KGPU_E_INVAL;
-  const int32_t i = slot - c->n_snapshot_pods;
-  if (i < 0) return fail(c, KGPU_E_UNSUPPORTED, "forget of a snapshot pod: re-upload the snapshot");
-  if (i >= (int32_t)c->assumed.size() || !c->assumed[i].active) return fail(c, KGPU_E_INVAL, "no such assumed pod");
-  kgpu_ctx::Assumed& a = c->assumed[i];
-  if (a.node < 0) {  // sharded: assumed on another rank's node
-    a.active = false;
-    return KGPU_OK;
+  if (!c->uploaded) return fail(c, KGPU_E_STATE, "no snapshot uploaded");
+  if (slot < 0 || slot >= (int32_t)c->recs.size() || !c->recs[(size_t)slot].active)
+    return fail(c, KGPU_E_INVAL, "no such pod slot");
+  kgpu_ctx::PodRec& a = c->recs[(size_t)slot];
+  if (!a.has_res)
+    return fail(c, KGPU_E_UNSUPPORTED, "snapshot pod: remove it with a REMOVE_POD delta carrying the pod");
+  if (hipSetDevice(c->device) != hipSuccess) return KGPU_E_DEVICE;
+  // NodeInfo.RemovePod (types.go:484-533) as one k_delta op over the stored resource record
+  const int local = a.node - c->st.node_base;
+  int rc = KGPU_OK;
+  if (a.node >= 0 && local >= 0 && local < c->st.N) {
+    kgpu_pod_query q = a.q;
+    q.scalars = kgpu_range{0, (int32_t)a.sc.size()};
+    q.ports = kgpu_range{0, (int32_t)a.ports.size()};
+    DeltaBuild db;
+    for (int32_t r : node_rows(c, local)) pod_op(c, db, kgpu::kDRemovePod, r, 0, slot);
+    rc = launch_ops(c, db, &q, 1, nullptr, 0, nullptr, 0, nullptr, 0, a.sc.data(), (int)a.sc.size(), a.ports.data(),
+                    (int)a.ports.size());
   }
-  HIP_OK(c, hipStreamSynchronize(c->stream));
-  // NodeInfo.RemovePod (types.go:484-533): read-modify-write of one row (rare path).
-  const size_t n = (size_t)a.node, N = (size_t)c->st.N;
-  auto sub64 = [&](int64_t* col, int64_t d) -> int {
-    int64_t v;
-    HIP_OK(c, hipMemcpy(&v, col + n, 8, hipMemcpyDeviceToHost));
-    v -= d;
-    HIP_OK(c, hipMemcpy(col + n, &v, 8, hipMemcpyHostToDevice));
-    return KGPU_OK;
-  };
-  int rc;
-  if ((rc = sub64(c->st.req_cpu, a.q.req[0]))) return rc;
-  if ((rc = sub64(c->st.req_mem, a.q.req[1]))) return rc;
-  if ((rc = sub64(c->st.req_eph, a.q.req[2]))) return rc;
-  if ((rc = sub64(c->st.nz_cpu, a.q.nz[0]))) return rc;
-  if ((rc = sub64(c->st.nz_mem, a.q.nz[1]))) return rc;
-  for (const kgpu_scalar_req& s : a.sc)
-    if (s.col >= 0 && (rc = sub64(c->st.req_scalar + (size_t)s.col * N, s.value))) return rc;
-  int32_t np;
-  HIP_OK(c, hipMemcpy(&np, c->st.num_pods + n, 4, hipMemcpyDeviceToHost));
-  np -= 1;
-  HIP_OK(c, hipMemcpy(c->st.num_pods + n, &np, 4, hipMemcpyHostToDevice));
-  if (!a.ports.empty()) {
-    int32_t pc;
-    HIP_OK(c, hipMemcpy(&pc, c->st.port_count + n, 4, hipMemcpyDeviceToHost));
-    std::vector<kgpu_port> row(pc);
-    for (int sl = 0; sl < pc; ++sl)
-      HIP_OK(c, hipMemcpy(&row[sl], c->st.ports + (size_t)sl * N + n, sizeof(kgpu_port), hipMemcpyDeviceToHost));
-    std::vector<kgpu_port> keep;
-    for (const kgpu_port& p : row) {
-      bool rm = false;
-      for (const kgpu_port& w : a.ports) rm |= (p.ip == w.ip && p.proto == w.proto && p.port == w.port);
-      if (!rm) keep.push_back(p);
-    }
-    for (size_t sl = 0; sl < keep.size(); ++sl)
-      HIP_OK(c, hipMemcpy(c->st.ports + sl * N + n, &keep[sl], sizeof(kgpu_port), hipMemcpyHostToDevice));
-    int32_t kc = (int32_t)keep.size();
-    HIP_OK(c, hipMemcpy(c->st.port_count + n, &kc, 4, hipMemcpyHostToDevice));
-  }
-  // topology state: the pod leaves the match-count columns of its classes and term classes
-  const size_t slot_row = (size_t)c->n_snapshot_pods + (size_t)i;
-  if (slot_row < c->pod_rows.size() && c->st.mcnt) {
-    kgpu_ctx::PodRow& row = c->pod_rows[slot_row];
-    auto dec32 = [&](int32_t* col) -> int {
-      int32_t v;
-      HIP_OK(c, hipMemcpy(&v, col + n, 4, hipMemcpyDeviceToHost));
-      v -= 1;
-      HIP_OK(c, hipMemcpy(col + n, &v, 4, hipMemcpyHostToDevice));
-      return KGPU_OK;
-    };
-    const int np = (int)row.pairs.size() / 2;
-    for (int cl = 0; cl < c->classes_init; ++cl)
-      if (class_matches(c, cl, row.ns, row.flags, row.pairs.data(), np) && (rc = dec32(c->st.mcnt + (size_t)cl * N)))
-        return rc;
-    for (int32_t tc : row.own_tcls)
-      if ((rc = dec32(c->st.tcnt + (size_t)tc * N))) return rc;
-    row.flags &= ~KGPU_PF_ACTIVE;
-    c->pod_rows_dev = -1;
+  if (rc) {
+    c->uploaded = false;
+    return rc;
   }
   a.active = false;
+  c->pod_rows[(size_t)slot].flags &= ~KGPU_PF_ACTIVE;
+  c->pod_rows_dev = -1;
+  if (a.has_uid) c->uid_slot.erase(a.uid);
+  return KGPU_OK;
+}
+
+int kgpu_apply_delta(kgpu_ctx* c, const kgpu_delta_batch* b, int64_t generation, int32_t* slots) {
+  if (!c || !b) return KGPU_E_INVAL;
+  if (!c->uploaded) return fail(c, KGPU_E_STATE, "no snapshot uploaded");
+  if (b->n_deltas < 0 || b->n_pods < 0 || b->n_rows < 0 || b->n_order < 0 || (b->n_deltas && !b->deltas) ||
+      (b->n_pods && !b->pods) || (b->n_rows && !b->rows) || (b->n_order && !b->order))
+    return fail(c, KGPU_E_INVAL, "malformed delta batch");
+  if (hipSetDevice(c->device) != hipSuccess) return KGPU_E_DEVICE;
+  HIP_OK(c, hipStreamSynchronize(c->stream));
+  const int rc = apply_delta(c, b, slots);
+  if (rc) {
+    // a half-applied batch leaves the mirror unlike any cache state
+    c->uploaded = false;
+    return rc;
+  }
+  c->generation = generation;
   return KGPU_OK;
 }
 

@@ -209,6 +209,7 @@ struct DevState {
   // pod's EvaluatedNodes (len(filtered) + len(statuses)).  cut_state is null when to_find == N.
   int32_t to_find;
   int32_t* cut_state;
+  int32_t* port_overflow;               // set by assume / delta when a node's host-port slots run out
 };
 // Filter status word of a node the cycle never examined (findNodesThatPassFilters stopped before
 // it), or of the feasible node whose discovery cancelled the search: not in `filtered` and not in
@@ -403,5 +404,39 @@ int launch_class_init(const DevState* st, int c0, int nc, int n_pods, void* stre
 // initialization from the match-count columns (k_hist_init), then k_tbatch.  kidx: geometry.
 int tbatch_geometry(int N, int max_groups, int* per, int* groups);
 int launch_tbatch(const DevState* st, const TBatchArgs& a, int groups, int geo, int spec, void* stream);
+
+// ---------------------------------------------------------------- delta stream (kgpu_apply_delta)
+enum DeltaKind { kDAddPod = 0, kDRemovePod = 1, kDSetNode = 2 };
+// One NodeInfo change on a local row, applied in order by k_delta.
+struct DeltaOp {
+  int32_t kind;        // DeltaKind
+  int32_t node;        // local node row
+  int32_t item;        // pod (query) index / node row index
+  int32_t slot;        // pod-table slot written for an added / removed pod (-1: table not resident)
+  kgpu_range cls;      // aux ints: pod classes whose mcnt column moves by +-1
+  kgpu_range tcls;     // aux ints: term classes (the pod's own terms) whose tcnt column moves by +-1
+};
+struct DeltaArgs {
+  const DeltaOp* ops;
+  int32_t n_ops;
+  int32_t pad;
+  const kgpu_pod_query* pods;
+  const kgpu_node_row* rows;
+  const int32_t* ints;           // pools of pods / rows
+  const uint64_t* words;
+  const kgpu_scalar_req* scalars;
+  const kgpu_port* ports;
+  const int32_t* aux;
+};
+int launch_delta(const DevState* st, const DeltaArgs& a, void* stream);
+
+// Column gather for a node-list rebuild: dst[c][i] = src[c][from[i]] (0 when from[i] < 0).
+struct RemapCol {
+  const void* src;
+  void* dst;
+  int32_t elem;        // bytes per element: 1, 4, 8 or 16
+  int32_t ncols;
+};
+int launch_remap(const RemapCol* cols, int n_cols, const int32_t* from, int old_n, int new_n, void* stream);
 
 }  // namespace kgpu

@@ -644,14 +644,21 @@ __device__ void assume_row(const DevState& st, const kgpu_pod_query& q, NodeRes&
   }
   if (q.ports.count) {
     int pc = gp(st.port_count)[n];
-    for (int i = 0; i < q.ports.count && pc < st.PS; ++i) {
+    for (int i = 0; i < q.ports.count; ++i) {
       const kgpu_port w = cp(st.qp.ports)[q.ports.begin + i];
       bool dup = false;
       for (int s = 0; s < pc; ++s) {
         const kgpu_port p = gp(st.ports)[(size_t)s * st.N + n];
         if (p.ip == w.ip && p.proto == w.proto && p.port == w.port) dup = true;
       }
-      if (!dup) gp(st.ports)[(size_t)(pc++) * st.N + n] = w;
+      if (dup) continue;
+      // the host sizes PS for the batch's ports (kgpu_api.cpp reserve_ports); running out means a
+      // lost UsedPorts entry, which the host turns into an error
+      if (pc >= st.PS) {
+        gp(st.port_overflow)[0] = 1;
+        continue;
+      }
+      gp(st.ports)[(size_t)(pc++) * st.N + n] = w;
     }
     gp(st.port_count)[n] = pc;
   }
@@ -2701,6 +2708,122 @@ int launch_resolve(const DevState* st, int N, const PodArgs& a, void* stream) {
 
 int launch_shard_pack(const DevState* st, int parity, int blocks, int what, void* stream) {
   hipLaunchKernelGGL(k_shard_pack, dim3(1), dim3(kBlock), 0, (hipStream_t)stream, st, parity, blocks, what);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// ---------------------------------------------------------------- delta stream (kgpu_apply_delta)
+// NodeInfo.AddPod / RemovePod (types.go:456-533) and SetNode (types.go:587-600) for a batch of
+// cache events.  One workgroup walks the ops in order (an op's host ports depend on the previous
+// op on the same node); inside an op the lanes split the class columns, label keys and taint words.
+__global__ __launch_bounds__(kBlock) void k_delta(const DevState* __restrict__ stp, DeltaArgs a) {
+  const DevState& st = *stp;
+  const int lane = threadIdx.x;
+  const size_t N = (size_t)st.N;
+  for (int o = 0; o < a.n_ops; ++o) {
+    const DeltaOp op = a.ops[o];
+    const int n = op.node;
+    if (op.kind == kDSetNode) {
+      const kgpu_node_row r = a.rows[op.item];
+      if (lane == 0) {
+        gp(st.alloc_cpu)[n] = r.alloc_cpu;
+        gp(st.alloc_mem)[n] = r.alloc_mem;
+        gp(st.alloc_eph)[n] = r.alloc_eph;
+        gp(st.alloc_pods)[n] = r.alloc_pods;
+        gp(st.unsched)[n] = (uint8_t)(r.unschedulable ? 1 : 0);
+        gp(st.zone_id)[n] = r.zone_id;
+      }
+      for (int k = lane; k < st.K; k += kBlock) {
+        int32_t v = -1;
+        for (int j = 0; j + 1 < r.labels.count; j += 2)
+          if (a.ints[r.labels.begin + j] == k) v = a.ints[r.labels.begin + j + 1];
+        gp(st.label_val)[(size_t)k * N + n] = v;
+      }
+      for (int w = lane; w < st.TW; w += kBlock) {
+        const bool has = r.taints.count >= 2 * st.TW;
+        gp(st.taint_nosched)[(size_t)w * N + n] = has ? a.words[r.taints.begin + w] : 0ull;
+        gp(st.taint_prefer)[(size_t)w * N + n] = has ? a.words[r.taints.begin + st.TW + w] : 0ull;
+      }
+      for (int sc = lane; sc < st.S; sc += kBlock)
+        gp(st.alloc_scalar)[(size_t)sc * N + n] =
+            sc < r.alloc_scalar.count ? (int64_t)a.words[r.alloc_scalar.begin + sc] : 0;
+    } else {
+      const kgpu_pod_query q = a.pods[op.item];
+      const int64_t sg = op.kind == kDAddPod ? 1 : -1;
+      if (lane == 0) {
+        gp(st.req_cpu)[n] += sg * q.req[0];
+        gp(st.req_mem)[n] += sg * q.req[1];
+        gp(st.req_eph)[n] += sg * q.req[2];
+        gp(st.nz_cpu)[n] += sg * q.nz[0];
+        gp(st.nz_mem)[n] += sg * q.nz[1];
+        gp(st.num_pods)[n] += (int32_t)sg;
+        for (int i = 0; i < q.scalars.count; ++i) {
+          const kgpu_scalar_req sr = a.scalars[q.scalars.begin + i];
+          if (sr.col >= 0) gp(st.req_scalar)[(size_t)sr.col * N + n] += sg * sr.value;
+        }
+        // NodeInfo.UsedPorts is a set per (ip, protocol, port): Add is idempotent, Remove drops the
+        // entry (types.go:728-745, HostPortInfo.Add/Remove host_ports.go)
+        int pc = gp(st.port_count)[n];
+        for (int i = 0; i < q.ports.count; ++i) {
+          const kgpu_port w = a.ports[q.ports.begin + i];
+          int at = -1;
+          for (int s = 0; s < pc; ++s) {
+            const kgpu_port p = gp(st.ports)[(size_t)s * N + n];
+            if (p.ip == w.ip && p.proto == w.proto && p.port == w.port) at = s;
+          }
+          if (sg > 0) {
+            if (at >= 0) continue;
+            if (pc >= st.PS) {
+              gp(st.port_overflow)[0] = 1;
+              continue;
+            }
+            gp(st.ports)[(size_t)(pc++) * N + n] = w;
+          } else if (at >= 0) {
+            gp(st.ports)[(size_t)at * N + n] = gp(st.ports)[(size_t)(pc - 1) * N + n];
+            --pc;
+          }
+        }
+        gp(st.port_count)[n] = pc;
+      }
+      for (int i = lane; i < op.cls.count; i += kBlock)
+        gp(st.mcnt)[(size_t)a.aux[op.cls.begin + i] * N + n] += (int32_t)sg;
+      for (int i = lane; i < op.tcls.count; i += kBlock)
+        gp(st.tcnt)[(size_t)a.aux[op.tcls.begin + i] * N + n] += (int32_t)sg;
+    }
+    __syncthreads();
+  }
+}
+
+int launch_delta(const DevState* st, const DeltaArgs& a, void* stream) {
+  if (a.n_ops <= 0) return 0;
+  hipLaunchKernelGGL(k_delta, dim3(1), dim3(kBlock), 0, (hipStream_t)stream, st, a);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// Node-list rebuild: one grid-stride pass per column table (blockIdx.y), every element a
+// coalesced load from its old row.
+__global__ void k_remap(const RemapCol* __restrict__ cols, const int32_t* __restrict__ from, int old_n, int new_n) {
+  const RemapCol c = cols[blockIdx.y];
+  const size_t total = (size_t)c.ncols * (size_t)new_n;
+  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (size_t)gridDim.x * blockDim.x) {
+    const size_t col = e / (size_t)new_n, i = e - col * (size_t)new_n;
+    const int f = from[i];
+    const size_t so = col * (size_t)old_n + (size_t)(f < 0 ? 0 : f);
+    switch (c.elem) {
+      case 1: gp((uint8_t*)c.dst)[e] = f < 0 ? 0 : cp((const uint8_t*)c.src)[so]; break;
+      case 4: gp((int32_t*)c.dst)[e] = f < 0 ? 0 : cp((const int32_t*)c.src)[so]; break;
+      case 8: gp((int64_t*)c.dst)[e] = f < 0 ? 0 : cp((const int64_t*)c.src)[so]; break;
+      default: {
+        const kgpu_port z{0, 0, 0, 0};
+        gp((kgpu_port*)c.dst)[e] = f < 0 ? z : cp((const kgpu_port*)c.src)[so];
+      }
+    }
+  }
+}
+
+int launch_remap(const RemapCol* cols, int n_cols, const int32_t* from, int old_n, int new_n, void* stream) {
+  if (n_cols <= 0 || new_n <= 0) return 0;
+  const int blocks = (new_n + 255) / 256 < 1024 ? (new_n + 255) / 256 : 1024;
+  hipLaunchKernelGGL(k_remap, dim3(blocks, n_cols), dim3(256), 0, (hipStream_t)stream, cols, from, old_n, new_n);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -96,6 +96,22 @@ class Snapshot(C.Structure):
                 ("avoid_off", vp), ("avoid_id", vp), ("zone_id", vp), ("n_zones", C.c_int32),
                 ("n_pods", C.c_int32), ("pod_node", vp), ("pod_ns", vp), ("pod_flags", vp),
                 ("n_pod_label_keys", C.c_int32), ("n_terms", C.c_int32), ("pod_label_val", vp), ("terms", vp),
+                ("pools", Pools), ("pod_uid", vp)]
+
+
+D_ADD_POD, D_REMOVE_POD, D_SET_NODE = 1, 2, 3
+DELTA = np.dtype([("op", "<i4"), ("node", "<i4"), ("uid", "<i8"), ("item", "<i4"), ("pad", "<i4")], align=True)
+NODE_ROW = np.dtype([("alloc_cpu", "<i8"), ("alloc_mem", "<i8"), ("alloc_eph", "<i8"), ("alloc_pods", "<i4"),
+                     ("unschedulable", "<i4"), ("zone_id", "<i4"), ("pad", "<i4"), ("labels", RANGE),
+                     ("taints", RANGE), ("alloc_scalar", RANGE)], align=True)
+
+
+class DeltaBatch(C.Structure):
+    _fields_ = [("n_deltas", C.c_int32), ("n_pods", C.c_int32), ("deltas", vp), ("pods", vp),
+                ("n_rows", C.c_int32), ("n_order", C.c_int32), ("rows", vp), ("order", vp),
+                ("key_n_values", vp), ("value_off", vp), ("value_int", vp), ("value_int_ok", vp),
+                ("key_empty_value", vp), ("image_off", vp), ("image_id", vp), ("image_score", vp),
+                ("avoid_off", vp), ("avoid_id", vp), ("n_zones", C.c_int32), ("pad", C.c_int32),
                 ("pools", Pools)]
 
 
@@ -112,7 +128,8 @@ STRUCT_SIZES = [("kgpu_range", RANGE.itemsize), ("kgpu_req", REQ.itemsize), ("kg
                 ("kgpu_port", PORT.itemsize), ("kgpu_pod_query", QUERY.itemsize),
                 ("kgpu_pools", C.sizeof(Pools)), ("kgpu_resource_weight", C.sizeof(ResourceWeight)),
                 ("kgpu_config", C.sizeof(Config)), ("kgpu_snapshot", C.sizeof(Snapshot)),
-                ("kgpu_result", RESULT.itemsize), ("kgpu_stats", C.sizeof(Stats))]
+                ("kgpu_result", RESULT.itemsize), ("kgpu_stats", C.sizeof(Stats)), ("kgpu_delta", DELTA.itemsize),
+                ("kgpu_node_row", NODE_ROW.itemsize), ("kgpu_delta_batch", C.sizeof(DeltaBatch))]
 
 
 def ptr(a):

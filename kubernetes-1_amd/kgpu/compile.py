@@ -67,6 +67,10 @@ class CompileError(Exception):
     pass
 
 
+class NeedsUpload(Exception):
+    """A cluster change the device columns cannot absorb as a delta: upload the snapshot again."""
+
+
 class Pools:
     """Growable pools referenced by kgpu_range fields.
 
@@ -399,10 +403,12 @@ class Compiler:
         self.ns.add("")
 
     # -------------------------------------------------- snapshot
-    def compile_snapshot(self, nodes, existing=(), shard=None):
+    def compile_snapshot(self, nodes, existing=(), shard=None, ordered=None, uid_of=None):
         """nodes: insertion order; returns (kgpu_snapshot ctypes struct, arrays dict, node names in
-        Snapshot.List() order).  shard=(base, count) keeps only that slice of node rows."""
-        ordered = api.snapshot_order(nodes)
+        Snapshot.List() order).  shard=(base, count) keeps only that slice of node rows.
+        ordered: the node objects already in Snapshot.List() order (a cache mirror's nodeTree pass);
+        uid_of(pod) -> int64: fills kgpu_snapshot.pod_uid so that deltas can address the pods."""
+        ordered = api.snapshot_order(nodes) if ordered is None else list(ordered)
         self.order = [api.name_of(n) for n in ordered]
         self.node_index = {nm: i for i, nm in enumerate(self.order)}
         N = len(ordered)
@@ -469,7 +475,7 @@ class Compiler:
                 av.add(self.controllers.get(a))
             avoid_lists.append(sorted(av))
         # existing pods -> node rows + pod table
-        A.update(self._compile_existing(existing, A))
+        A.update(self._compile_existing(existing, A, uid_of))
         # label value metadata
         A["key_n_values"] = np.array([len(d) for d in self.nkeys.vals], np.int32) if K else np.zeros(0, np.int32)
         off = [0]
@@ -499,9 +505,12 @@ class Compiler:
                   "nz_mem", "num_pods", "alloc_scalar", "req_scalar", "unschedulable", "label_val", "key_n_values",
                   "value_off", "value_int", "value_int_ok", "key_empty_value", "taint_nosched", "taint_prefer",
                   "port_count", "ports", "image_off", "image_id", "image_score", "avoid_off", "avoid_id",
-                  "zone_id", "pod_node", "pod_ns", "pod_flags", "pod_label_val", "terms"):
+                  "zone_id", "pod_node", "pod_ns", "pod_flags", "pod_label_val", "terms", "pod_uid"):
+            if A.get(f) is None:
+                continue
             A[f] = np.ascontiguousarray(A[f])
             setattr(snap, f, abi.ptr(A[f]))
+        self.dims = {"S": S, "K": K, "TW": TW}  # device column counts fixed by this upload
         snap.n_scalar = S
         snap.n_label_keys = K
         snap.taint_words = TW
@@ -542,10 +551,10 @@ class Compiler:
                 out[fv] = A[fv][lo:hi]
         return out
 
-    def _compile_existing(self, existing, A):
+    def _compile_existing(self, existing, A, uid_of=None):
         N = len(self.order)
         pools = Pools()
-        pod_node, pod_ns, pod_flags = [], [], []
+        pod_node, pod_ns, pod_flags, pod_uid = [], [], [], []
         PK = len(self.pkeys.keys)
         plab = []
         terms = []
@@ -572,6 +581,8 @@ class Compiler:
                                                self.protos.get(pt.get("protocol", "") or "TCP"), port))
             slot = len(pod_node)
             pod_node.append(ni)
+            if uid_of is not None:
+                pod_uid.append(uid_of(p))
             pod_ns.append(self.ns.get(api.ns_of(p)))
             fl = abi.PF_ACTIVE
             if api.meta(p).get("deletionTimestamp") is not None:
@@ -599,7 +610,104 @@ class Compiler:
                "pod_flags": np.array(pod_flags, np.uint32),
                "pod_label_val": (np.array(plab, np.int32).T.copy() if P and PK else np.zeros((PK, P), np.int32)),
                "terms": np.array(terms, dtype=abi.TERM) if terms else np.zeros(0, abi.TERM),
-               "port_count": port_count, "ports": ports, "port_slots": slots, "_pools": pools}
+               "port_count": port_count, "ports": ports, "port_slots": slots, "_pools": pools,
+               "pod_uid": np.array(pod_uid, np.int64) if uid_of is not None else None}
+        return out
+
+    # -------------------------------------------------- node rows for deltas (kgpu_node_row)
+    def node_row(self, n, pools):
+        """kgpu_node_row of a v1.Node against the dictionaries of the last upload.  Raises
+        NeedsUpload when the node brings a label key, taint word or scalar resource the device
+        columns have no room for; new values of known keys grow the dictionaries (key_meta)."""
+        dims = self.dims
+        r = np.zeros((), abi.NODE_ROW)
+        al = (n.get("status") or {}).get("allocatable") or {}
+        cpu = mem = eph = pods = 0
+        sc = [0] * dims["S"]
+        for res, q in al.items():
+            if res == "cpu":
+                cpu += api.q_milli(q)
+            elif res == "memory":
+                mem += api.q_value(q)
+            elif res == "pods":
+                pods += api.q_value(q)
+            elif res == "ephemeral-storage":
+                eph += api.q_value(q)
+            elif api.is_scalar(res):
+                col = self.scalars.add(res)
+                if col >= dims["S"]:
+                    raise NeedsUpload("new scalar resource %r" % res)
+                sc[col] += api.q_value(q)
+        r["alloc_cpu"], r["alloc_mem"], r["alloc_eph"], r["alloc_pods"] = cpu, mem, eph, pods
+        r["unschedulable"] = 1 if api.spec(n).get("unschedulable") else 0
+        z = api.zone_key(n)
+        r["zone_id"] = self.zones.add(z) if z else -1
+        pairs = []
+        for k, v in sorted(api.labels_of(n).items()):
+            ki = self.nkeys.key(k)
+            if ki < 0 or ki >= dims["K"]:
+                raise NeedsUpload("new node label key %r" % k)
+            pairs += [ki, self.nkeys.add(k, v)[1]]
+        r["labels"] = pools.ints_range(pairs)
+        TW = dims["TW"]
+        words = [0] * (2 * TW)
+        for t in api.spec(n).get("taints") or []:
+            key = (t.get("key", "") or "", t.get("value", "") or "", t.get("effect", "") or "")
+            tid = self.taints.add(key)
+            w, b = divmod(tid, 64)
+            if w >= TW:
+                raise NeedsUpload("taint dictionary outgrew %d words" % TW)
+            if key[2] in ("NoSchedule", "NoExecute"):
+                words[w] |= 1 << b
+            elif key[2] == "PreferNoSchedule":
+                words[TW + w] |= 1 << b
+        r["taints"] = pools.words_range(words) if any(words) else (0, 0)
+        r["alloc_scalar"] = pools.words_range([v & 0xFFFFFFFFFFFFFFFF for v in sc]) if any(sc) else (0, 0)
+        for im in (n.get("status") or {}).get("images") or []:
+            for nm in im.get("names") or []:
+                self.images.add(nm)
+        for a in api.avoid_pods(n):
+            self.controllers.add(a)
+        return r
+
+    def key_meta(self):
+        """key_n_values / value_off / value_int / value_int_ok / key_empty_value of the node keys."""
+        K = self.dims["K"]
+        off, ints, oks, empty = [0], [], [], []
+        for ki in range(K):
+            d = self.nkeys.vals[ki]
+            for v in d.items:
+                iv = api.parse_int64(v)
+                ints.append(0 if iv is None else iv)
+                oks.append(0 if iv is None else 1)
+            off.append(len(ints))
+            empty.append(d.get(""))
+        return {"key_n_values": np.array([len(self.nkeys.vals[k]) for k in range(K)], np.int32),
+                "value_off": np.array(off, np.int32), "value_int": np.array(ints, np.int64),
+                "value_int_ok": np.array(oks, np.uint8), "key_empty_value": np.array(empty, np.int32)}
+
+    def node_lists(self, ordered, all_nodes=None):
+        """ImageLocality scaledImageScore CSR (image_locality.go:100-113: NumNodes of the image over
+        the cache's nodes, spread over len(NodeInfos().List())) and the NodePreferAvoidPods CSR, in
+        list order."""
+        N = len(ordered)
+        name_to_nodes = {}
+        for n in (ordered if all_nodes is None else all_nodes):
+            for im in (n.get("status") or {}).get("images") or []:
+                for nm in im.get("names") or []:
+                    name_to_nodes.setdefault(nm, set()).add(api.name_of(n))
+        img_lists, avoid_lists = [], []
+        for n in ordered:
+            ims = {}
+            for im in (n.get("status") or {}).get("images") or []:
+                for nm in im.get("names") or []:
+                    spread = float(len(name_to_nodes[nm])) / float(N)
+                    ims[self.images.add(nm)] = int(float(int(im.get("sizeBytes", 0))) * spread)
+            img_lists.append(sorted(ims.items()))
+            avoid_lists.append(sorted({self.controllers.add(a) for a in api.avoid_pods(n)}))
+        out = {}
+        out["image_off"], out["image_id"], out["image_score"] = self._csr(img_lists, True)
+        out["avoid_off"], out["avoid_id"], _ = self._csr([[(a, 0) for a in lst] for lst in avoid_lists], False)
         return out
 
     # -------------------------------------------------- pod terms (framework/v1alpha1/types.go:92-160)

@@ -17,7 +17,7 @@ _lib = None
 EXPORTS = ["kgpu_abi_version", "kgpu_struct_sizes", "kgpu_create", "kgpu_destroy", "kgpu_last_error",
            "kgpu_upload_snapshot", "kgpu_generation", "kgpu_schedule_one", "kgpu_schedule_batch",
            "kgpu_get_filter", "kgpu_get_scores", "kgpu_forget_pod", "kgpu_read_nodes", "kgpu_set_option",
-           "kgpu_read_phase_trace", "kgpu_comm_unique_id", "kgpu_comm_init"]
+           "kgpu_read_phase_trace", "kgpu_comm_unique_id", "kgpu_comm_init", "kgpu_apply_delta"]
 
 
 class KgpuError(RuntimeError):
@@ -53,6 +53,7 @@ def lib():
     L.kgpu_read_phase_trace.argtypes = [vp, vp, i32]
     L.kgpu_comm_unique_id.argtypes = [vp]
     L.kgpu_comm_init.argtypes = [vp, i32, i32, vp]
+    L.kgpu_apply_delta.argtypes = [vp, C.POINTER(abi.DeltaBatch), i64, vp]
     if L.kgpu_abi_version() != abi.ABI_VERSION:
         raise KgpuError(abi.E_STATE, "ABI version mismatch")
     _lib = L
@@ -151,6 +152,13 @@ class Engine:
 
     def forget(self, slot):
         self._check(lib().kgpu_forget_pod(self.h, slot))
+
+    def apply_delta(self, batch, generation, n_deltas, keep=()):
+        """kgpu_apply_delta: `batch` is an abi.DeltaBatch whose arrays `keep` holds alive.
+        Returns the pod-table slot of every delta (-1 for non-ADD_POD)."""
+        slots = np.full(max(n_deltas, 1), -1, np.int32)
+        self._check(lib().kgpu_apply_delta(self.h, C.byref(batch), generation, slots.ctypes.data))
+        return slots[:n_deltas]
 
     def comm_init(self, nranks, rank, uid):
         """Join the node-sharding communicator (RCCL): this engine holds one contiguous shard of the

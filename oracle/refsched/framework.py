@@ -297,11 +297,11 @@ def select_host(totals, index, profile, pod_seq):
 
 
 def schedule_sequence(nodes, existing_pods, pods, profile, services=(), rcs=(), rss=(), sss=(),
-                      first_seq=0, pvcs=(), order="tree"):
+                      first_seq=0, pvcs=(), order="tree", image_nodes=None):
     """scheduleOne loop: each placed pod is assumed (NodeInfo.AddPod) before the next one.
 
     Returns a list of Result (or FitError/ScheduleError instances for unschedulable pods)."""
-    snap = NI.Snapshot(nodes, existing_pods, order=order)
+    snap = NI.Snapshot(nodes, existing_pods, order=order, image_nodes=image_nodes)
     fw = Framework(profile, Handle(snap, services, rcs, rss, sss, pvcs))
     gs = GenericScheduler(fw)
     out = []

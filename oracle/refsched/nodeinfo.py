@@ -478,7 +478,10 @@ def node_tree_order(nodes):
 class Snapshot:
     """Cache snapshot: NodeInfos in Snapshot.List() order (zone round robin of add order)."""
 
-    def __init__(self, nodes, pods=(), order="tree"):
+    def __init__(self, nodes, pods=(), order="tree", image_nodes=None):
+        """image_nodes: the nodes whose images count toward ImageStateSummary.NumNodes -- the
+        scheduler cache's nodes (cache.go:658-700), which a Snapshot.List() built by UpdateSnapshot
+        may not all hold (node_tree.go:147-170); default: `nodes`."""
         by_name = {}
         for n in nodes:
             by_name[name(n)] = NodeInfo(n)
@@ -494,7 +497,7 @@ class Snapshot:
         self.map = by_name
         # image states (snapshot.go:92-125)
         exist = {}
-        for n in nodes:
+        for n in (nodes if image_nodes is None else image_nodes):
             for im in (n.get("status") or {}).get("images") or []:
                 for nm in im.get("names") or []:
                     exist.setdefault(nm, set()).add(name(n))
@@ -502,7 +505,7 @@ class Snapshot:
             st = {}
             for im in (n.get("status") or {}).get("images") or []:
                 for nm in im.get("names") or []:
-                    st[nm] = (int(im.get("sizeBytes", 0)), len(exist[nm]))
+                    st[nm] = (int(im.get("sizeBytes", 0)), len(exist.get(nm, ())))
             by_name[name(n)].image_states = st
         self._phantom_names = set()
         for p in pods:
