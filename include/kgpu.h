@@ -80,7 +80,10 @@ extern "C" {
 #define KGPU_S_DEFAULT_POD_TOPOLOGY_SPREAD 7
 #define KGPU_S_TAINT_TOLERATION 8
 #define KGPU_S_MOST_ALLOCATED 9
-#define KGPU_NUM_SCORES 10
+/* not in the default provider; enabled by a profile */
+#define KGPU_S_REQUESTED_TO_CAPACITY_RATIO 10  /* noderesources/requested_to_capacity_ratio.go:124-170 */
+#define KGPU_S_RESOURCE_LIMITS 11              /* noderesources/resource_limits.go:104-160 (NodeResourceLimits) */
+#define KGPU_NUM_SCORES 12
 
 /* ---- per-node filter status word (kgpu_get_filter):
  *   bits 0-7   index+1 in the profile's filter order of the first failing filter (0 = feasible)
@@ -239,6 +242,7 @@ typedef struct kgpu_pod_query {
   kgpu_range ipa_pref_aff;
   kgpu_range ipa_pref_anti;
   kgpu_range labels;          /* int32 pool: (pod key id, value id) pairs */
+  int64_t limits[2];          /* NodeResourceLimits: milliCPU, memory limits (resource_limits.go:145-156) */
 } kgpu_pod_query;
 
 /* Variable-length parts referenced by queries (or by snapshot terms). */
@@ -259,6 +263,13 @@ typedef struct kgpu_resource_weight {
   int32_t resource;
   int32_t weight;
 } kgpu_resource_weight;
+
+/* One point of RequestedToCapacityRatioArgs.Shape; score already scaled to MaxNodeScore
+ * (UtilizationShapePoint.Score x MaxNodeScore / MaxCustomPriorityScore, requested_to_capacity_ratio.go:54-58). */
+typedef struct kgpu_shape_point {
+  int64_t utilization;
+  int64_t score;
+} kgpu_shape_point;
 
 typedef struct kgpu_config {
   int32_t abi_version;
@@ -283,6 +294,10 @@ typedef struct kgpu_config {
   int32_t pod_capacity;                     /* existing-pod rows to reserve incl. assumed pods */
   int32_t term_capacity;                    /* existing-term rows to reserve */
   int32_t pad1;
+  int32_t n_rtcr;                           /* RequestedToCapacityRatioArgs.Resources (weight 0 -> 1) */
+  int32_t n_shape;                          /* RequestedToCapacityRatioArgs.Shape points, ascending */
+  kgpu_resource_weight rtcr[8];
+  kgpu_shape_point shape[16];
 } kgpu_config;
 
 /* Snapshot in Snapshot.List() order (the local shard of it when sharded). */

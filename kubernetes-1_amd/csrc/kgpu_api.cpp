@@ -59,7 +59,11 @@ struct kgpu_ctx {
   DevBuf trace;
   std::vector<int64_t> trace_host;
   int spec = 0;      // k_eval instantiation for the profile (kgpu::select_spec)
-  std::vector<uint64_t> prefer_union;  // PreferNoSchedule taint ids present on any node
+  std::vector<uint64_t> prefer_union;  // PreferNoSchedule taint ids present on any node of this shard
+  // node sharding: the union over every rank's shard (exchanged at kgpu_comm_init and after each
+  // delta batch), so that every rank takes the same normalize decision for a pod
+  std::vector<uint64_t> prefer_global;
+  DevBuf pref_x;
   // Every pod on a device row, by pod-table slot (parallel to pod_rows): snapshot pods first, then
   // pods assumed by a schedule call or added by kgpu_apply_delta.  The resource record is what
   // NodeInfo.RemovePod subtracts for kgpu_forget_pod; snapshot pods have none (their removal goes
@@ -91,7 +95,9 @@ struct kgpu_ctx {
   std::unordered_map<int32_t, std::vector<int32_t>> alias_rows;  // canonical row -> all its rows
   bool has_alias = false;
   DevBuf flags_buf;                                // DevState::port_overflow
-  DevBuf d_ops, d_dpods, d_drows, d_dints, d_dwords, d_dscalars, d_dports, d_daux, d_remap, d_from;
+  DevBuf d_stage, d_remap, d_from;
+  void* stage_host = nullptr;                      // pinned staging block of a delta launch
+  size_t stage_cap = 0;
   bool last_diag = false;
   std::vector<hipEvent_t> ev_pool;
   // ---- topology state (kgpu_internal.h "topology plugins")
@@ -216,12 +222,35 @@ bool has_score(const kgpu_ctx* c, int s) {
 bool needs_norm(const kgpu_ctx* c, const kgpu_pod_query& q, const kgpu_pools* p) {
   if (has_score(c, KGPU_S_NODE_AFFINITY) && q.pref_terms.count > 0) return true;
   if (has_score(c, KGPU_S_TAINT_TOLERATION)) {
-    for (size_t w = 0; w < c->prefer_union.size(); ++w) {
+    // sharded: the cluster-wide union, or ranks would disagree on the extra stat all-gather
+    const std::vector<uint64_t>& u = c->comm ? c->prefer_global : c->prefer_union;
+    for (size_t w = 0; w < u.size(); ++w) {
       uint64_t tol = (p && (int)w < q.tol_prefer.count) ? p->words[q.tol_prefer.begin + w] : 0ull;
-      if (c->prefer_union[w] & ~tol) return true;
+      if (u[w] & ~tol) return true;
     }
   }
   return false;
+}
+
+// Cluster-wide PreferNoSchedule union: all-gather every rank's shard union (TW words) and OR them.
+int sync_prefer_union(kgpu_ctx* c) {
+  const size_t TW = c->prefer_union.size();
+  const size_t bytes = sizeof(uint64_t) * TW * (size_t)(c->nranks + 1);
+  int rc = ensure(c, c->pref_x, std::max<size_t>(bytes, 8));
+  if (rc) return rc;
+  uint64_t* d = static_cast<uint64_t*>(c->pref_x.p);
+  if (TW) {
+    HIP_OK(c, hipMemcpyAsync(d, c->prefer_union.data(), sizeof(uint64_t) * TW, hipMemcpyHostToDevice, c->stream));
+    const ncclResult_t r = ncclAllGather(d, d + TW, TW, ncclUint64, c->comm, c->stream);
+    if (r != ncclSuccess) return fail(c, KGPU_E_DEVICE, std::string("ncclAllGather: ") + ncclGetErrorString(r));
+  }
+  std::vector<uint64_t> all(TW * (size_t)c->nranks);
+  if (TW) HIP_OK(c, hipMemcpyAsync(all.data(), d + TW, sizeof(uint64_t) * all.size(), hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(c, hipStreamSynchronize(c->stream));
+  c->prefer_global.assign(TW, 0ull);
+  for (int r = 0; r < c->nranks; ++r)
+    for (size_t w = 0; w < TW; ++w) c->prefer_global[w] |= all[(size_t)r * TW + w];
+  return KGPU_OK;
 }
 
 
@@ -1611,27 +1640,72 @@ int launch_ops(kgpu_ctx* c, const DeltaBuild& b, const kgpu_pod_query* pods, int
                int n_rows, const int32_t* ints, int n_ints, const uint64_t* words, int n_words,
                const kgpu_scalar_req* scalars, int n_scalars, const kgpu_port* ports, int n_ports) {
   if (b.ops.empty()) return KGPU_OK;
-  kgpu::DeltaArgs a{};
+  // group the ops by node (stable: batch order within a node), one workgroup per group
+  std::vector<int32_t> idx(b.ops.size());
+  for (size_t i = 0; i < idx.size(); ++i) idx[i] = (int32_t)i;
+  std::stable_sort(idx.begin(), idx.end(), [&](int32_t x, int32_t y) { return b.ops[(size_t)x].node < b.ops[(size_t)y].node; });
+  std::vector<kgpu::DeltaOp> ops(b.ops.size());
+  std::vector<int32_t> goff;
+  for (size_t i = 0; i < idx.size(); ++i) {
+    ops[i] = b.ops[(size_t)idx[i]];
+    if (i == 0 || ops[i].node != ops[i - 1].node) goff.push_back((int32_t)i);
+  }
+  goff.push_back((int32_t)ops.size());
+  // One pinned staging block, one copy: DevState | ops | aux | pods | rows | ints | words | scalars | ports | groups
+  // (a delta batch is latency-bound: one H2D, one launch, one 4-byte readback).
+  struct Part {
+    const void* src;
+    size_t bytes;
+  };
+  const Part parts[] = {{&c->st, sizeof(DevState)},
+                        {ops.data(), sizeof(kgpu::DeltaOp) * ops.size()},
+                        {b.aux.data(), sizeof(int32_t) * b.aux.size()},
+                        {pods, sizeof(kgpu_pod_query) * (size_t)n_pods},
+                        {rows, sizeof(kgpu_node_row) * (size_t)n_rows},
+                        {ints, sizeof(int32_t) * (size_t)n_ints},
+                        {words, sizeof(uint64_t) * (size_t)n_words},
+                        {scalars, sizeof(kgpu_scalar_req) * (size_t)n_scalars},
+                        {ports, sizeof(kgpu_port) * (size_t)n_ports},
+                        {goff.data(), sizeof(int32_t) * goff.size()}};
+  constexpr int kParts = (int)(sizeof(parts) / sizeof(parts[0]));
+  size_t off[kParts], total = 0;
+  for (int i = 0; i < kParts; ++i) {
+    off[i] = total;
+    total += (parts[i].bytes + 63) & ~(size_t)63;
+  }
+  const size_t need = total + 64;  // + the overflow readback word
+  if (c->stage_cap < need) {
+    if (c->stage_host) (void)hipHostFree(c->stage_host);
+    c->stage_host = nullptr;
+    c->stage_cap = 0;
+    HIP_OK(c, hipHostMalloc(&c->stage_host, need * 2, hipHostMallocDefault));
+    c->stage_cap = need * 2;
+  }
   int rc;
-  if ((rc = upload_span(c, c->d_ops, b.ops.data(), b.ops.size(), &a.ops)) ||
-      (rc = upload_span(c, c->d_daux, b.aux.data(), b.aux.size(), &a.aux)) ||
-      (rc = upload_span(c, c->d_dpods, pods, (size_t)n_pods, &a.pods)) ||
-      (rc = upload_span(c, c->d_drows, rows, (size_t)n_rows, &a.rows)) ||
-      (rc = upload_span(c, c->d_dints, ints, (size_t)n_ints, &a.ints)) ||
-      (rc = upload_span(c, c->d_dwords, words, (size_t)n_words, &a.words)) ||
-      (rc = upload_span(c, c->d_dscalars, scalars, (size_t)n_scalars, &a.scalars)) ||
-      (rc = upload_span(c, c->d_dports, ports, (size_t)n_ports, &a.ports)))
-    return rc;
-  a.n_ops = (int32_t)b.ops.size();
-  if ((rc = ensure(c, c->dstate, sizeof(DevState)))) return rc;
-  c->st_batch = c->st;
-  HIP_OK(c, hipMemcpyAsync(c->dstate.p, &c->st_batch, sizeof(DevState), hipMemcpyHostToDevice, c->stream));
-  if (kgpu::launch_delta(static_cast<const DevState*>(c->dstate.p), a, c->stream))
+  if ((rc = ensure(c, c->d_stage, total))) return rc;
+  char* h = static_cast<char*>(c->stage_host);
+  for (int i = 0; i < kParts; ++i)
+    if (parts[i].bytes && parts[i].src) std::memcpy(h + off[i], parts[i].src, parts[i].bytes);
+  HIP_OK(c, hipMemcpyAsync(c->d_stage.p, h, total, hipMemcpyHostToDevice, c->stream));
+  char* d = static_cast<char*>(c->d_stage.p);
+  kgpu::DeltaArgs a{};
+  a.n_ops = (int32_t)ops.size();
+  a.n_groups = (int32_t)goff.size() - 1;
+  a.group_off = reinterpret_cast<const int32_t*>(d + off[9]);
+  a.ops = reinterpret_cast<const kgpu::DeltaOp*>(d + off[1]);
+  a.aux = reinterpret_cast<const int32_t*>(d + off[2]);
+  a.pods = reinterpret_cast<const kgpu_pod_query*>(d + off[3]);
+  a.rows = reinterpret_cast<const kgpu_node_row*>(d + off[4]);
+  a.ints = reinterpret_cast<const int32_t*>(d + off[5]);
+  a.words = reinterpret_cast<const uint64_t*>(d + off[6]);
+  a.scalars = reinterpret_cast<const kgpu_scalar_req*>(d + off[7]);
+  a.ports = reinterpret_cast<const kgpu_port*>(d + off[8]);
+  if (kgpu::launch_delta(reinterpret_cast<const DevState*>(d), a, c->stream))
     return fail(c, KGPU_E_DEVICE, "k_delta launch failed");
-  int32_t overflow = 0;
-  HIP_OK(c, hipMemcpyAsync(&overflow, c->st.port_overflow, 4, hipMemcpyDeviceToHost, c->stream));
+  int32_t* ov = reinterpret_cast<int32_t*>(h + total);
+  HIP_OK(c, hipMemcpyAsync(ov, c->st.port_overflow, 4, hipMemcpyDeviceToHost, c->stream));
   HIP_OK(c, hipStreamSynchronize(c->stream));
-  if (overflow) return fail(c, KGPU_E_DEVICE, "a node's host-port slots ran out while applying deltas");
+  if (*ov) return fail(c, KGPU_E_DEVICE, "a node's host-port slots ran out while applying deltas");
   return KGPU_OK;
 }
 
@@ -2044,7 +2118,8 @@ int kgpu_struct_sizes(int32_t* out, int32_t n) {
                        (int32_t)sizeof(kgpu_resource_weight), (int32_t)sizeof(kgpu_config),
                        (int32_t)sizeof(kgpu_snapshot),  (int32_t)sizeof(kgpu_result),
                        (int32_t)sizeof(kgpu_stats),     (int32_t)sizeof(kgpu_delta),
-                       (int32_t)sizeof(kgpu_node_row),  (int32_t)sizeof(kgpu_delta_batch)};
+                       (int32_t)sizeof(kgpu_node_row),  (int32_t)sizeof(kgpu_delta_batch),
+                       (int32_t)sizeof(kgpu_shape_point)};
   const int32_t m = (int32_t)(sizeof(s) / sizeof(s[0]));
   for (int32_t i = 0; i < n && i < m; ++i) out[i] = s[i];
   return m;
@@ -2071,6 +2146,13 @@ int kgpu_create(const kgpu_config* cfg, kgpu_ctx** out) {
       if (cfg->filters[j] == cfg->filters[i]) return KGPU_E_INVAL;
   }
   if (cfg->percentage_of_nodes_to_score < 0 || cfg->percentage_of_nodes_to_score > 100) return KGPU_E_INVAL;
+  for (int i = 0; i < cfg->n_scores; ++i)
+    if (cfg->scores[i] == KGPU_S_REQUESTED_TO_CAPACITY_RATIO) {
+      // ValidateRequestedToCapacityRatioArgs: a non-empty shape with strictly increasing utilization
+      if (cfg->n_rtcr < 0 || cfg->n_rtcr > 8 || cfg->n_shape < 1 || cfg->n_shape > 16) return KGPU_E_INVAL;
+      for (int j = 1; j < cfg->n_shape; ++j)
+        if (cfg->shape[j].utilization <= cfg->shape[j - 1].utilization) return KGPU_E_INVAL;
+    }
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return KGPU_E_DEVICE;
   if (cfg->device < 0 || cfg->device >= ndev) return KGPU_E_INVAL;
@@ -2107,6 +2189,12 @@ int kgpu_create(const kgpu_config* cfg, kgpu_ctx** out) {
   if (st.most_wsum == 0) st.most_wsum = 1;
   st.tie_mode = cfg->tie_break_mode;
   st.seed = cfg->seed;
+  st.n_rtcr = cfg->n_rtcr;
+  st.n_shape = cfg->n_shape;
+  std::memcpy(st.rtcr, cfg->rtcr, sizeof(st.rtcr));
+  std::memcpy(st.shape, cfg->shape, sizeof(st.shape));
+  for (int i = 0; i < st.n_rtcr; ++i)
+    if (st.rtcr[i].weight == 0) st.rtcr[i].weight = 1;  // requested_to_capacity_ratio.go:63-66
   // default requested-resource specs {cpu: 1, memory: 1} (noderesources/resource_allocation.go:36-39)
   auto def_spec = [](const kgpu_resource_weight* r, int n) {
     return n == 2 && r[0].resource == 0 && r[0].weight == 1 && r[1].resource == 1 && r[1].weight == 1;
@@ -2129,8 +2217,10 @@ int kgpu_destroy(kgpu_ctx* c) {
                     &c->d_citems, &c->d_tclasses, &c->d_creqs, &c->d_cints, &c->d_plans, &c->d_aux,
                     &c->d_aux_terms, &c->scratch, &c->d_pods, &c->gbar, &c->cut_buf, &c->t_plans, &c->t_aux,
                     &c->t_looks, &c->t_tabs, &c->t_deltas, &c->t_hists, &c->t_sigs, &c->t_regs, &c->t_zero,
-                    &c->abort_buf, &c->t_plan_of})
+                    &c->abort_buf, &c->t_plan_of, &c->flags_buf, &c->d_stage, &c->d_remap, &c->d_from})
     if (b->p) (void)hipFree(b->p);
+  if (c->pref_x.p) (void)hipFree(c->pref_x.p);
+  if (c->stage_host) (void)hipHostFree(c->stage_host);
   if (c->st.mcnt) (void)hipFree(c->st.mcnt);
   if (c->st.tcnt) (void)hipFree(c->st.tcnt);
   if (c->shard.p) (void)hipFree(c->shard.p);
@@ -2311,6 +2401,7 @@ int kgpu_upload_snapshot(kgpu_ctx* c, const kgpu_snapshot* s, int64_t generation
   c->has_alias = false;
   c->n_snapshot_pods = s->n_pods;
   c->generation = generation;
+  if (c->comm && (rc = sync_prefer_union(c))) return rc;  // every rank re-uploads its shard together
   c->uploaded = true;
   HIP_OK(c, hipDeviceSynchronize());
   return KGPU_OK;
@@ -2405,7 +2496,8 @@ int kgpu_apply_delta(kgpu_ctx* c, const kgpu_delta_batch* b, int64_t generation,
     return fail(c, KGPU_E_INVAL, "malformed delta batch");
   if (hipSetDevice(c->device) != hipSuccess) return KGPU_E_DEVICE;
   HIP_OK(c, hipStreamSynchronize(c->stream));
-  const int rc = apply_delta(c, b, slots);
+  int rc = apply_delta(c, b, slots);
+  if (!rc && c->comm) rc = sync_prefer_union(c);  // every rank applies the same batch
   if (rc) {
     // a half-applied batch leaves the mirror unlike any cache state
     c->uploaded = false;
@@ -2452,7 +2544,7 @@ int kgpu_comm_init(kgpu_ctx* c, int32_t nranks, int32_t rank, const uint8_t id[1
   c->comm = comm;
   c->nranks = nranks;
   c->rank = rank;
-  return KGPU_OK;
+  return sync_prefer_union(c);
 }
 
 }  // extern "C"

@@ -155,6 +155,9 @@ struct DevState {
   int32_t n_least, n_most;
   kgpu_resource_weight least[8], most[8];
   int64_t least_wsum, most_wsum;
+  int32_t n_rtcr, n_shape;               // RequestedToCapacityRatio
+  kgpu_resource_weight rtcr[8];
+  kgpu_shape_point shape[16];
   int32_t tie_mode;
   int32_t pad0;
   uint64_t seed;
@@ -417,9 +420,10 @@ struct DeltaOp {
   kgpu_range tcls;     // aux ints: term classes (the pod's own terms) whose tcnt column moves by +-1
 };
 struct DeltaArgs {
-  const DeltaOp* ops;
+  const DeltaOp* ops;            // grouped by node, each group in batch order
+  const int32_t* group_off;      // [n_groups + 1] op ranges, one workgroup per node
   int32_t n_ops;
-  int32_t pad;
+  int32_t n_groups;
   const kgpu_pod_query* pods;
   const kgpu_node_row* rows;
   const int32_t* ints;           // pools of pods / rows

@@ -327,6 +327,44 @@ __device__ __forceinline__ int64_t most_score(const DevState& st, const kgpu_pod
   }
 }
 
+// RequestedToCapacityRatio (requested_to_capacity_ratio.go:124-170): the broken-linear shape over
+// utilization per resource, weighted mean over resources with a positive score, math.Round.
+__device__ __forceinline__ int64_t rtcr_shape(const DevState& st, int64_t p) {
+  for (int i = 0; i < st.n_shape; ++i)
+    if (p <= st.shape[i].utilization) {
+      if (i == 0) return st.shape[0].score;
+      // Go int64 arithmetic: the product may be negative, division truncates toward zero
+      return st.shape[i - 1].score + (st.shape[i].score - st.shape[i - 1].score) * (p - st.shape[i - 1].utilization) /
+                                         (st.shape[i].utilization - st.shape[i - 1].utilization);
+    }
+  return st.shape[st.n_shape - 1].score;
+}
+__device__ __forceinline__ int64_t rtcr_score(const DevState& st, const kgpu_pod_query& q, const NodeRes& nr, int n) {
+  int64_t node_score = 0, wsum = 0;
+  for (int i = 0; i < st.n_rtcr; ++i) {
+    int64_t cap, req;
+    alloc_req(st, q, nr, st.rtcr[i].resource, n, cap, req);
+    const int64_t util = (cap == 0 || req > cap) ? 100 : 100 - ((cap - req) * 100) / cap;
+    const int64_t rs = rtcr_shape(st, util);
+    if (rs > 0) {
+      node_score += rs * st.rtcr[i].weight;
+      wsum += st.rtcr[i].weight;
+    }
+  }
+  if (wsum == 0) return 0;
+  // math.Round(float64(a) / float64(b)) for 0 <= a, 0 < b: a / b is never within an ulp of a .5
+  // that it does not equal, so the exact half-away-from-zero integer rounding is the same value
+  return (2 * node_score + wsum) / (2 * wsum);
+}
+
+// NodeResourceLimits (resource_limits.go:104-160): 1 when the pod's cpu or memory limit fits the
+// node's allocatable.
+__device__ __forceinline__ int64_t limits_score(const kgpu_pod_query& q, const NodeRes& nr) {
+  const bool c = q.limits[0] != 0 && nr.ac != 0 && q.limits[0] <= nr.ac;
+  const bool m = q.limits[1] != 0 && nr.am != 0 && q.limits[1] <= nr.am;
+  return (c || m) ? 1 : 0;
+}
+
 // balancedResourceScorer (balanced_allocation.go:83-120): IEEE double, no contraction.
 __device__ __forceinline__ int64_t balanced_score(const kgpu_pod_query& q, const NodeRes& nr) {
   const int64_t cc = nr.ac, cr = nr.zc + q.score_req[0];
@@ -450,6 +488,8 @@ __device__ __forceinline__ int64_t score_one(int s, const DevState& st, const kg
     case KGPU_S_INTER_POD_AFFINITY: return 0;     // empty topologyScore
     case KGPU_S_TAINT_TOLERATION: e.taint = taint_raw(st, q, n); return e.taint;
     case KGPU_S_NODE_AFFINITY: e.na = na_raw(st, q, n); return e.na;
+    case KGPU_S_REQUESTED_TO_CAPACITY_RATIO: return rtcr_score(st, q, r, n);
+    case KGPU_S_RESOURCE_LIMITS: return limits_score(q, r);
     default: return 0;
   }
 }
@@ -2526,9 +2566,10 @@ constexpr uint32_t kFitFM = bit(KGPU_F_NODE_RESOURCES_FIT);
 constexpr uint32_t kFitSM = bit(KGPU_S_BALANCED_ALLOCATION) | bit(KGPU_S_LEAST_ALLOCATED) | kDefRes;
 // the default provider (algorithmprovider/registry.go:71-155)
 constexpr uint32_t kDefaultFM = (1u << KGPU_NUM_FILTERS) - 1;
-constexpr uint32_t kDefaultSM = (kSMask & ~bit(KGPU_S_MOST_ALLOCATED)) | kDefRes;
+constexpr uint32_t kProviderSM = (1u << (KGPU_S_MOST_ALLOCATED + 1)) - 1;  // the provider-era score plugins
+constexpr uint32_t kDefaultSM = (kProviderSM & ~bit(KGPU_S_MOST_ALLOCATED)) | kDefRes;
 // the ClusterAutoscalerProvider (registry.go:157-165): MostAllocated instead of LeastAllocated
-constexpr uint32_t kAutoscalerSM = (kSMask & ~bit(KGPU_S_LEAST_ALLOCATED)) | kDefRes;
+constexpr uint32_t kAutoscalerSM = (kProviderSM & ~bit(KGPU_S_LEAST_ALLOCATED)) | kDefRes;
 
 // persistent topology kernel instantiations: [profile spec][geometry] (kgpu_internal.h)
 struct TGeo {
@@ -2713,13 +2754,15 @@ int launch_shard_pack(const DevState* st, int parity, int blocks, int what, void
 
 // ---------------------------------------------------------------- delta stream (kgpu_apply_delta)
 // NodeInfo.AddPod / RemovePod (types.go:456-533) and SetNode (types.go:587-600) for a batch of
-// cache events.  One workgroup walks the ops in order (an op's host ports depend on the previous
-// op on the same node); inside an op the lanes split the class columns, label keys and taint words.
+// cache events.  One workgroup per node walks that node's ops in batch order (an op's host ports
+// depend on the previous op on the same node); rows of different nodes are disjoint, so the
+// groups run in parallel.  Inside an op the lanes split the class columns, label keys and taints.
 __global__ __launch_bounds__(kBlock) void k_delta(const DevState* __restrict__ stp, DeltaArgs a) {
   const DevState& st = *stp;
   const int lane = threadIdx.x;
   const size_t N = (size_t)st.N;
-  for (int o = 0; o < a.n_ops; ++o) {
+  const int o0 = a.group_off[blockIdx.x], o1 = a.group_off[blockIdx.x + 1];
+  for (int o = o0; o < o1; ++o) {
     const DeltaOp op = a.ops[o];
     const int n = op.node;
     if (op.kind == kDSetNode) {
@@ -2794,8 +2837,8 @@ __global__ __launch_bounds__(kBlock) void k_delta(const DevState* __restrict__ s
 }
 
 int launch_delta(const DevState* st, const DeltaArgs& a, void* stream) {
-  if (a.n_ops <= 0) return 0;
-  hipLaunchKernelGGL(k_delta, dim3(1), dim3(kBlock), 0, (hipStream_t)stream, st, a);
+  if (a.n_ops <= 0 || a.n_groups <= 0) return 0;
+  hipLaunchKernelGGL(k_delta, dim3(a.n_groups), dim3(kBlock), 0, (hipStream_t)stream, st, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -19,12 +19,13 @@ FILTER_IDS = {"NodeUnschedulable": 0, "NodeResourcesFit": 1, "NodeName": 2, "Nod
               "TaintToleration": 5, "PodTopologySpread": 6, "InterPodAffinity": 7}
 FILTER_NAMES = {v: k for k, v in FILTER_IDS.items()}
 
-(S_BALANCED, S_IMAGE, S_IPA, S_LEAST, S_NODE_AFFINITY, S_NPAP, S_PTS, S_DPTS, S_TAINT, S_MOST) = range(10)
-NUM_SCORES = 10
+(S_BALANCED, S_IMAGE, S_IPA, S_LEAST, S_NODE_AFFINITY, S_NPAP, S_PTS, S_DPTS, S_TAINT, S_MOST, S_RTCR,
+ S_LIMITS) = range(12)
+NUM_SCORES = 12
 SCORE_IDS = {"NodeResourcesBalancedAllocation": 0, "ImageLocality": 1, "InterPodAffinity": 2,
              "NodeResourcesLeastAllocated": 3, "NodeAffinity": 4, "NodePreferAvoidPods": 5,
              "PodTopologySpread": 6, "DefaultPodTopologySpread": 7, "TaintToleration": 8,
-             "NodeResourcesMostAllocated": 9}
+             "NodeResourcesMostAllocated": 9, "RequestedToCapacityRatio": 10, "NodeResourceLimits": 11}
 SCORE_NAMES = {v: k for k, v in SCORE_IDS.items()}
 
 OP_IN, OP_NOTIN, OP_EXISTS, OP_DNE, OP_GT, OP_LT = range(6)
@@ -53,7 +54,7 @@ QUERY = np.dtype([
     ("tol_nosched", RANGE), ("tol_prefer", RANGE), ("node_selector", RANGE), ("req_terms", RANGE),
     ("pref_terms", RANGE), ("images", RANGE), ("avoid_id", "<i4"), ("pad0", "<i4"), ("pts_hard", RANGE),
     ("pts_soft", RANGE), ("dpts", SELECTOR), ("ipa_req_aff", RANGE), ("ipa_req_anti", RANGE),
-    ("ipa_pref_aff", RANGE), ("ipa_pref_anti", RANGE), ("labels", RANGE)], align=True)
+    ("ipa_pref_aff", RANGE), ("ipa_pref_anti", RANGE), ("labels", RANGE), ("limits", "<i8", (2,))], align=True)
 RESULT = np.dtype([("node", "<i4"), ("feasible", "<i4"), ("evaluated", "<i4"), ("scored", "<i4"),
                    ("score", "<i8")], align=True)
 
@@ -64,6 +65,10 @@ class ResourceWeight(C.Structure):
     _fields_ = [("resource", C.c_int32), ("weight", C.c_int32)]
 
 
+class ShapePoint(C.Structure):
+    _fields_ = [("utilization", C.c_int64), ("score", C.c_int64)]
+
+
 class Config(C.Structure):
     _fields_ = [("abi_version", C.c_int32), ("device", C.c_int32), ("n_filters", C.c_int32),
                 ("filters", C.c_int32 * NUM_FILTERS), ("n_scores", C.c_int32), ("scores", C.c_int32 * NUM_SCORES),
@@ -71,7 +76,8 @@ class Config(C.Structure):
                 ("n_most", C.c_int32), ("most", ResourceWeight * 8), ("hard_pod_affinity_weight", C.c_int32),
                 ("percentage_of_nodes_to_score", C.c_int32), ("tie_break_mode", C.c_int32), ("pad0", C.c_int32),
                 ("seed", C.c_uint64), ("node_capacity", C.c_int32), ("pod_capacity", C.c_int32),
-                ("term_capacity", C.c_int32), ("pad1", C.c_int32)]
+                ("term_capacity", C.c_int32), ("pad1", C.c_int32), ("n_rtcr", C.c_int32), ("n_shape", C.c_int32),
+                ("rtcr", ResourceWeight * 8), ("shape", ShapePoint * 16)]
 
 
 class Pools(C.Structure):
@@ -129,7 +135,8 @@ STRUCT_SIZES = [("kgpu_range", RANGE.itemsize), ("kgpu_req", REQ.itemsize), ("kg
                 ("kgpu_pools", C.sizeof(Pools)), ("kgpu_resource_weight", C.sizeof(ResourceWeight)),
                 ("kgpu_config", C.sizeof(Config)), ("kgpu_snapshot", C.sizeof(Snapshot)),
                 ("kgpu_result", RESULT.itemsize), ("kgpu_stats", C.sizeof(Stats)), ("kgpu_delta", DELTA.itemsize),
-                ("kgpu_node_row", NODE_ROW.itemsize), ("kgpu_delta_batch", C.sizeof(DeltaBatch))]
+                ("kgpu_node_row", NODE_ROW.itemsize), ("kgpu_delta_batch", C.sizeof(DeltaBatch)),
+                ("kgpu_shape_point", C.sizeof(ShapePoint))]
 
 
 def ptr(a):

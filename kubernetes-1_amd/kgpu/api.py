@@ -372,3 +372,22 @@ def avoid_pods(node):
     for a in ann.get("preferAvoidPods") or []:
         out.append((a.get("kind"), a.get("uid")))
     return out
+
+
+def pod_limits(pod):
+    """getResourceLimits (resource_limits.go:145-156): containers' limits added, init containers'
+    taken as a max (Resource.Add / SetMaxResource, types.go:262-323); milliCPU and memory."""
+    cpu = mem = 0
+    for c in containers(pod):
+        lim = (c.get("resources") or {}).get("limits") or {}
+        if "cpu" in lim:
+            cpu += q_milli(lim["cpu"])
+        if "memory" in lim:
+            mem += q_value(lim["memory"])
+    for c in init_containers(pod):
+        lim = (c.get("resources") or {}).get("limits") or {}
+        if "cpu" in lim:
+            cpu = max(cpu, q_milli(lim["cpu"]))
+        if "memory" in lim:
+            mem = max(mem, q_value(lim["memory"]))
+    return cpu, mem

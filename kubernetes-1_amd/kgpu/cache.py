@@ -58,6 +58,7 @@ class SchedulerCache:
         self._log = []           # NodeInfo ops since the last sync
         self._dirty_nodes = set()
         self._node_set_changed = False  # a node added or removed: UpdateSnapshot rebuilds the list
+        self._lists_dirty = False       # some node's images / preferAvoidPods changed: resend the CSR
         self.engine = None
         self.compiler = None
         self.uploads = 0
@@ -189,6 +190,10 @@ class SchedulerCache:
             self.tree.add_node(new)
         if name not in self.nodes:
             self._node_set_changed = True
+        prev = self.nodes.get(name)
+        if prev is None or (prev.get("status") or {}).get("images") != (new.get("status") or {}).get("images") or \
+                api.avoid_pods(prev) != api.avoid_pods(new):
+            self._lists_dirty = True
         self.tree.update_node(old, new)
         self.nodes[name] = new
         self._dirty_nodes.add(name)
@@ -242,6 +247,7 @@ class SchedulerCache:
         self._log.clear()
         self._dirty_nodes.clear()
         self._node_set_changed = False
+        self._lists_dirty = False
         self.uploads += 1
         if len(uniq) != len(names):
             # a list holding one NodeInfo twice: upload it once, then alias it (kgpu_delta_batch.order)
@@ -264,23 +270,27 @@ class SchedulerCache:
     def _sync(self, reorder, new_list):
         comp = self.compiler
         old_list, old_index = self.list, self.index
-        new_index = {}
-        for i, nm in enumerate(new_list):
-            new_index.setdefault(nm, i)  # a node's first row addresses all of its rows
-        fresh = [nm for nm in new_index if nm not in old_index]
+        if reorder:
+            new_index = {}
+            for i, nm in enumerate(new_list):
+                new_index.setdefault(nm, i)  # a node's first row addresses all of its rows
+            fresh = [nm for nm in new_index if nm not in old_index]
+        else:
+            new_index, fresh = old_index, []
         pools = Pools()
         rows, pods, deltas = [], [], []
         n_vals = [len(comp.nkeys.vals[k]) for k in range(comp.dims["K"])]
         n_zones0 = len(comp.zones)
-        set_nodes = sorted({nm for nm in new_list if nm in self._dirty_nodes} | set(fresh), key=new_index.get)
+        set_nodes = sorted({nm for nm in self._dirty_nodes if nm in new_index} | set(fresh), key=new_index.get)
         for nm in set_nodes:
             rows.append(comp.node_row(self.nodes[nm], pools))
             deltas.append((abi.D_SET_NODE, new_index[nm], 0, len(rows) - 1))
-        dev = dict(self.dev_pods)
-        # pods of dropped nodes leave the device with their rows
-        for uid, nm in list(dev.items()):
-            if nm not in new_index:
-                del dev[uid]
+        dev = dict(self.dev_pods) if reorder else self.dev_pods  # copied: a NeedsUpload restarts from scratch
+        if reorder:
+            # pods of dropped nodes leave the device with their rows
+            for uid, nm in list(dev.items()):
+                if nm not in new_index:
+                    del dev[uid]
         pod_items = {}
 
         def item(pod):
@@ -334,7 +344,7 @@ class SchedulerCache:
                 if not a.size:
                     keep[f + "_z"] = np.zeros(1, a.dtype)
                     setattr(batch, f, abi.ptr(keep[f + "_z"]))
-        if reorder or set_nodes:
+        if reorder or self._lists_dirty:
             lists = comp.node_lists([self.nodes[nm] for nm in new_list], list(self.nodes.values()))
             keep.update(lists)
             for f, a in lists.items():
@@ -353,6 +363,7 @@ class SchedulerCache:
         self._log.clear()
         self._dirty_nodes.clear()
         self._node_set_changed = False
+        self._lists_dirty = False
         self._last_batch = (batch, keep)
         return self.generation
 

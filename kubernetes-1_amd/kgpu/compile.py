@@ -249,7 +249,10 @@ class Profile:
 
     def __init__(self, filters=None, scores=None, least_resources=(("cpu", 1), ("memory", 1)),
                  most_resources=(("cpu", 1), ("memory", 1)), hard_pod_affinity_weight=1, ignored_resources=(),
-                 pts_default_constraints=(), percentage_of_nodes_to_score=100, tie_break_mode=0, seed=0x7B):
+                 pts_default_constraints=(), percentage_of_nodes_to_score=100, tie_break_mode=0, seed=0x7B,
+                 rtcr_resources=(("cpu", 1), ("memory", 1)), rtcr_shape=((0, 10), (100, 0))):
+        """rtcr_*: RequestedToCapacityRatioArgs (apis/config/types_pluginargs.go): Resources as
+        (name, weight), Shape as (utilization, score 0-10)."""
         self.filters = list(self.DEFAULT_FILTERS if filters is None else filters)
         self.scores = [tuple(s) for s in (self.DEFAULT_SCORES if scores is None else scores)]
         self.least_resources = [tuple(r) for r in least_resources]
@@ -260,6 +263,8 @@ class Profile:
         self.percentage_of_nodes_to_score = percentage_of_nodes_to_score
         self.tie_break_mode = tie_break_mode
         self.seed = seed
+        self.rtcr_resources = [tuple(r) for r in rtcr_resources]
+        self.rtcr_shape = [tuple(p) for p in rtcr_shape]
         for _, rl in (("least", self.least_resources), ("most", self.most_resources)):
             for n, w in rl:
                 if w <= 0:
@@ -355,7 +360,7 @@ class Compiler:
         self.zones = StrDict()
         self.node_index = {}
         self.order = []
-        for r, _ in list(profile.least_resources) + list(profile.most_resources):
+        for r, _ in list(profile.least_resources) + list(profile.most_resources) + list(profile.rtcr_resources):
             if r not in ("cpu", "memory", "ephemeral-storage"):
                 self.scalars.add(r)
 
@@ -877,6 +882,7 @@ class Compiler:
         if api.meta(pod).get("deletionTimestamp") is not None:
             flags |= abi.Q_TERMINATING
         q["flags"] = flags
+        q["limits"] = api.pod_limits(pod)
         return q
 
     def _self_match_all(self, pod):
@@ -964,7 +970,8 @@ class Compiler:
         for i, (n, w) in enumerate(prof.scores):
             c.scores[i] = abi.SCORE_IDS[n]
             c.score_weights[i] = w or 1
-        for attr, lst in (("least", prof.least_resources), ("most", prof.most_resources)):
+        for attr, lst in (("least", prof.least_resources), ("most", prof.most_resources),
+                          ("rtcr", prof.rtcr_resources)):
             merged = {}
             for r, w in lst:
                 merged[r] = w
@@ -975,6 +982,10 @@ class Compiler:
                 if rid is None:
                     rid = 3 + self.scalars.get(r) if api.is_scalar(r) else -1
                 arr[i].resource, arr[i].weight = rid, w
+        # Shape scores scale by MaxNodeScore / MaxCustomPriorityScore (requested_to_capacity_ratio.go:54-58)
+        c.n_shape = len(prof.rtcr_shape)
+        for i, (u, sc) in enumerate(prof.rtcr_shape):
+            c.shape[i].utilization, c.shape[i].score = u, sc * (100 // 10)
         c.hard_pod_affinity_weight = prof.hard_pod_affinity_weight
         c.percentage_of_nodes_to_score = prof.percentage_of_nodes_to_score
         c.tie_break_mode = prof.tie_break_mode

@@ -953,6 +953,43 @@ static int64_t resource_scorer(const ref_state* r, const kgpu_pools* p, const kg
   return weight_sum ? node_score / weight_sum : 0;
 }
 
+/* requested_to_capacity_ratio.go:150-170 buildBrokenLinearFunction */
+static int64_t broken_linear(const kgpu_config* c, int64_t p) {
+  for (int i = 0; i < c->n_shape; ++i) {
+    if (p <= c->shape[i].utilization) {
+      if (i == 0) return c->shape[0].score;
+      return c->shape[i - 1].score + (c->shape[i].score - c->shape[i - 1].score) * (p - c->shape[i - 1].utilization) /
+                                         (c->shape[i].utilization - c->shape[i - 1].utilization);
+    }
+  }
+  return c->shape[c->n_shape - 1].score;
+}
+
+/* requested_to_capacity_ratio.go:124-148 buildRequestedToCapacityRatioScorerFunction */
+static int64_t rtcr_score(const ref_state* r, const kgpu_pools* p, const kgpu_pod_query* q, int n) {
+  int64_t node_score = 0, weight_sum = 0;
+  for (int i = 0; i < r->cfg.n_rtcr; ++i) {
+    int64_t cap, req, s;
+    int64_t w = r->cfg.rtcr[i].weight ? r->cfg.rtcr[i].weight : 1;
+    allocatable_requested(r, p, q, r->cfg.rtcr[i].resource, n, &cap, &req);
+    if (cap == 0 || req > cap) s = broken_linear(&r->cfg, 100);
+    else s = broken_linear(&r->cfg, 100 - (cap - req) * 100 / cap);
+    if (s > 0) {
+      node_score += s * w;
+      weight_sum += w;
+    }
+  }
+  if (weight_sum == 0) return 0;
+  return (int64_t)round((double)node_score / (double)weight_sum); /* math.Round: half away from zero */
+}
+
+/* resource_limits.go:118-160 */
+static int64_t limits_score(const ref_state* r, const kgpu_pod_query* q, int n) {
+  int cpu = q->limits[0] != 0 && r->alloc_cpu[n] != 0 && q->limits[0] <= r->alloc_cpu[n];
+  int mem = q->limits[1] != 0 && r->alloc_mem[n] != 0 && q->limits[1] <= r->alloc_mem[n];
+  return (cpu || mem) ? 1 : 0;
+}
+
 static double fraction_of_capacity(int64_t req, int64_t cap) { return cap == 0 ? 1.0 : (double)req / (double)cap; }
 
 static int64_t balanced_score(const ref_state* r, const kgpu_pools* p, const kgpu_pod_query* q, int n) {
@@ -1086,6 +1123,8 @@ static void process(work_t* w, int i) {
       case KGPU_S_POD_TOPOLOGY_SPREAD: v = pts_score(w->qs, r, w->q, n); break;
       case KGPU_S_DEFAULT_POD_TOPOLOGY_SPREAD: v = dpts_score(w->qs, r, w->q, n); break;
       case KGPU_S_INTER_POD_AFFINITY: v = ipa_score(w->qs, r, n); break;
+      case KGPU_S_REQUESTED_TO_CAPACITY_RATIO: v = rtcr_score(r, w->p, w->q, n); break;
+      case KGPU_S_RESOURCE_LIMITS: v = limits_score(r, w->q, n); break;
       default: v = 0; break;
     }
     w->scores[(size_t)k * w->nf + i] = v;

@@ -52,8 +52,8 @@ class RefEngine:
         q = np.ascontiguousarray(queries, dtype=abi.QUERY)
         res = np.zeros(len(q), abi.RESULT)
         st = np.zeros(self.n, np.uint32) if diag else None
-        raw = np.zeros((10, self.n), np.int64) if diag else None
-        norm = np.zeros((10, self.n), np.int64) if diag else None
+        raw = np.zeros((abi.NUM_SCORES, self.n), np.int64) if diag else None
+        norm = np.zeros((abi.NUM_SCORES, self.n), np.int64) if diag else None
         lib().kgpu_ref_schedule(self.h, q.ctypes.data, len(q), C.addressof(pools), first_seq, res.ctypes.data,
                                 st.ctypes.data if diag else None, raw.ctypes.data if diag else None,
                                 norm.ctypes.data if diag else None)

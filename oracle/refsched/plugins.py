@@ -259,6 +259,97 @@ class MostAllocated(_ResourceScorer):
         return go_div(requested * MAX_NODE_SCORE, capacity)
 
 
+def go_round(x):
+    """math.Round: half away from zero."""
+    f = math.floor(abs(x) + 0.5)
+    return int(f if x >= 0 else -f)
+
+
+class RequestedToCapacityRatio:
+    """noderesources/requested_to_capacity_ratio.go:42-170.  shape: (utilization, score 0-10)."""
+    name = "RequestedToCapacityRatio"
+
+    def __init__(self, handle, shape, resources):
+        self.handle = handle
+        # score scaled to MaxNodeScore / MaxCustomPriorityScore (:54-58)
+        self.shape = [(int(u), int(sc) * (MAX_NODE_SCORE // 10)) for u, sc in shape]
+        self.weights = {}
+        for name, w in resources:          # :61-67: weight 0 -> 1, duplicate names: last wins
+            self.weights[name] = w if w != 0 else 1
+
+    def broken_linear(self, p):           # :150-170
+        sh = self.shape
+        for i in range(len(sh)):
+            if p <= sh[i][0]:
+                if i == 0:
+                    return sh[0][1]
+                return sh[i - 1][1] + go_div((sh[i][1] - sh[i - 1][1]) * (p - sh[i - 1][0]), sh[i][0] - sh[i - 1][0])
+        return sh[-1][1]
+
+    def resource_score(self, requested, capacity):  # :127-133
+        if capacity == 0 or requested > capacity:
+            return self.broken_linear(100)
+        return self.broken_linear(100 - go_div((capacity - requested) * 100, capacity))
+
+    def score(self, state, pod, node_name):
+        ni = self.handle.snapshot.get(node_name)
+        node_score = weight_sum = 0
+        for res, w in self.weights.items():
+            alloc, req = _alloc_request(ni, pod, res)
+            rs = self.resource_score(req, alloc)
+            if rs > 0:
+                node_score += rs * w
+                weight_sum += w
+        if weight_sum == 0:
+            return 0, None
+        return go_round(float(node_score) / float(weight_sum)), None
+
+
+def resource_limits(pod):
+    """getResourceLimits (resource_limits.go:145-156): milliCPU, memory."""
+    from .quantity import milli_value, value
+    cpu = mem = 0
+    for c in NI.containers(pod):
+        lim = (c.get("resources") or {}).get("limits") or {}
+        if "cpu" in lim:
+            cpu += milli_value(lim["cpu"])
+        if "memory" in lim:
+            mem += value(lim["memory"])
+    for c in NI.init_containers(pod):
+        lim = (c.get("resources") or {}).get("limits") or {}
+        if "cpu" in lim:
+            cpu = max(cpu, milli_value(lim["cpu"]))
+        if "memory" in lim:
+            mem = max(mem, value(lim["memory"]))
+    return cpu, mem
+
+
+class ResourceLimits:
+    """noderesources/resource_limits.go:30-160 (NodeResourceLimits)."""
+    name = "NodeResourceLimits"
+
+    def __init__(self, handle):
+        self.handle = handle
+
+    def prescore(self, state, pod, nodes):
+        if len(nodes) == 0:
+            return None
+        state["PreScoreNodeResourceLimits"] = resource_limits(pod)
+        return None
+
+    def score(self, state, pod, node_name):
+        ni = self.handle.snapshot.get(node_name)
+        lim = state.get("PreScoreNodeResourceLimits")
+        if lim is None:
+            return 0, Status(ERROR, 'Error reading "PreScoreNodeResourceLimits" from cycleState')
+
+        def compute(limit, allocatable):
+            return 1 if (limit != 0 and allocatable != 0 and limit <= allocatable) else 0
+        c = compute(lim[0], ni.allocatable.milli_cpu)
+        m = compute(lim[1], ni.allocatable.memory)
+        return (1 if (c == 1 or m == 1) else 0), None
+
+
 def _fraction(req, cap):
     if cap == 0:
         return 1.0

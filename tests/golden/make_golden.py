@@ -15,7 +15,8 @@ REF = "/root/reference"
 
 GROUPS = ["noderesources", "tainttoleration", "nodeaffinity", "normalize", "generic", "node_tree",
           "podtopologyspread", "interpodaffinity", "defaultpodtopologyspread", "imagelocality",
-          "nodepreferavoidpods", "nodeports", "nodename", "nodeunschedulable", "misc"]
+          "nodepreferavoidpods", "nodeports", "nodename", "nodeunschedulable", "requestedtocapacityratio",
+          "resourcelimits", "misc"]
 
 
 def resolve(cases):

@@ -39,6 +39,10 @@ def make_plugin(name, args, handle):
         return P.DefaultPodTopologySpread(handle)
     if name == "InterPodAffinity":
         return P.InterPodAffinity(handle, a.get("hard_pod_affinity_weight", 1))
+    if name == "RequestedToCapacityRatio":
+        return P.RequestedToCapacityRatio(handle, a["shape"], [tuple(r) for r in a["resources"]])
+    if name == "NodeResourceLimits":
+        return P.ResourceLimits(handle)
     raise KeyError(name)
 
 
@@ -127,6 +131,10 @@ def oracle_eval(c):
                                 lambda t, r: t.remove_node(r) is not None)
     if kind == "pts_state":
         return pts_state(c)
+    if kind == "broken_linear":
+        pl = P.RequestedToCapacityRatio(None, [], [])
+        pl.shape = [tuple(x) for x in c["points"]]
+        return {"values": [[p, pl.broken_linear(p)] for p, _ in c["expect_values"]]}
     if kind == "image_name":
         return {"name": P.normalized_image_name(c["input"])}
     raise KeyError(kind)
@@ -241,6 +249,8 @@ def check(c, got):
     for f in ("output", "tree", "remove_errors"):
         if "expect_" + f in c and got.get(f) != c["expect_" + f]:
             bad.append((f, c["expect_" + f], got.get(f)))
+    if "expect_values" in c and got.get("values") != c["expect_values"]:
+        bad.append(("values", c["expect_values"], got.get("values")))
     if "expect_name" in c and got.get("name") != c["expect_name"]:
         bad.append(("name", c["expect_name"], got.get("name")))
     if "expect_order" in c and got.get("order") != c["expect_order"]:

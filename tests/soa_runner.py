@@ -10,7 +10,7 @@ from kgpu.framework import GpuFramework
 
 TIER1_SCORES = {"NodeResourcesLeastAllocated", "NodeResourcesMostAllocated", "NodeResourcesBalancedAllocation",
                 "TaintToleration", "NodeAffinity", "ImageLocality", "NodePreferAvoidPods", "PodTopologySpread",
-                "DefaultPodTopologySpread", "InterPodAffinity"}
+                "DefaultPodTopologySpread", "InterPodAffinity", "RequestedToCapacityRatio", "NodeResourceLimits"}
 TIER1_FILTERS = {"NodeResourcesFit", "TaintToleration", "NodeAffinity", "NodeUnschedulable", "NodeName",
                  "NodePorts", "PodTopologySpread", "InterPodAffinity"}
 
@@ -48,6 +48,9 @@ def _profile(c):
             kw["least_resources"] = [tuple(r) for r in a.get("resources", [["cpu", 1], ["memory", 1]])]
         if c["plugin"] == "NodeResourcesMostAllocated":
             kw["most_resources"] = [tuple(r) for r in a.get("resources", [["cpu", 1], ["memory", 1]])]
+        if c["plugin"] == "RequestedToCapacityRatio":
+            kw["rtcr_resources"] = [tuple(r) for r in a["resources"]]
+            kw["rtcr_shape"] = [tuple(x) for x in a["shape"]]
         return Profile(**kw)
     if c["kind"] == "filter":
         return Profile(filters=[c["plugin"]], scores=[], ignored_resources=a.get("ignored", []),
