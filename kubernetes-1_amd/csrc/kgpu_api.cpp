@@ -13,6 +13,7 @@
 #include <iterator>
 #include <cmath>
 #include <cstdio>
+#include <cstddef>
 #include <cstring>
 #include <deque>
 #include <map>
@@ -1288,9 +1289,6 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
   for (int32_t i = 0; i < n; ++i) {
     norm[(size_t)i] = (diag || needs_norm(c, qs[i], pools) || (qs[i].flags & KGPU_Q_SCORE_ERROR)) ? 1 : 0;
     if (topo_on) topo[(size_t)i] = plans[(size_t)i].topo ? 1 : 0;
-    if (sharded && topo[(size_t)i])
-      return fail(c, KGPU_E_UNSUPPORTED, "node sharding: pods with PodTopologySpread / InterPodAffinity state are "
-                                         "not sharded yet (schedule them on an unsharded context)");
   }
   // Sharded: after the evaluation (and normalize) of pod k, pack this shard's record and
   // all-gather it on the same stream; the next launch resolves pod k over every rank's record.
@@ -1358,6 +1356,51 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
       a.cut = cut ? 1 : 0;
       a.seq = first_seq + i;
       if (c->timing) HIP_OK(c, hipEventRecord(get_event(c, ev), c->stream));
+      if (sharded) {
+        // Node-sharded topology pod: every rank builds the histograms of
+        // its shard; RCCL sums them (and ORs / mins / maxes the header) between the phases, so
+        // every rank filters and scores against the cluster-wide TpPairToMatchNum, topology
+        // scores, sizes and normalize extremes; the winner exchange is the non-topology one.
+        int64_t* sc = c->st.scratch;
+        auto ar = [&](void* buf, size_t cnt, ncclDataType_t t, ncclRedOp_t op) -> int {
+          if (!cnt) return KGPU_OK;
+          const ncclResult_t r = ncclAllReduce(buf, buf, cnt, t, op, c->comm, c->stream);
+          return r == ncclSuccess ? KGPU_OK : fail(c, KGPU_E_DEVICE, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+        };
+        auto phase = [&](int ph, int64_t extra) -> int {
+          return kgpu::launch_topo_phase(dst, a, ph, blocks, extra, c->stream) ? fail(c, KGPU_E_DEVICE, "topology phase launch failed")
+                                                                                : KGPU_OK;
+        };
+        if ((rc = phase(0, 0)) || (rc = ar(sc, (size_t)pl.scratch_len, ncclInt64, ncclSum))) return rc;
+        if (min_values > 0 && (rc = phase(1, min_values))) return rc;
+        if ((rc = phase(2, 0))) return rc;
+        bool soft_sizes = false;
+        for (int k = 0; k < pl.n_soft; ++k) {
+          const kgpu::TSpread& t = pl.soft[k];
+          if (t.is_hostname || t.key < 0) continue;
+          if ((rc = ar(sc + pl.slot_off[t.rslot], (size_t)std::max(c->key_n_values[(size_t)t.key], 1), ncclInt64, ncclSum)))
+            return rc;
+          soft_sizes |= t.first_of_key != 0;
+        }
+        int32_t* h32 = reinterpret_cast<int32_t*>(sc);
+        const size_t i_feas = offsetof(kgpu::TopoHdr, feas_nonign) / 4, i_zones = offsetof(kgpu::TopoHdr, have_zones) / 4;
+        if (pl.n_soft && (rc = ar(h32 + i_feas, 1, ncclInt32, ncclSum))) return rc;
+        if (soft_sizes && (rc = phase(3, 0))) return rc;
+        if ((rc = phase(4, 0))) return rc;
+        // score extremes are max-encoded words (pts_min .. dpts_max), zone sums add, have_zones ORs
+        if ((rc = ar(sc + offsetof(kgpu::TopoHdr, pts_min) / 8, 5, ncclUint64, ncclMax)) ||
+            (rc = ar(h32 + i_zones, 1, ncclInt32, ncclMax)) ||
+            (rc = ar(sc + kgpu::kHdrWords, (size_t)std::max(c->st.n_zones, 0), ncclInt64, ncclSum)) ||
+            (rc = exchange(a.parity, 1)) || (rc = phase(5, blocks)) || (rc = exchange(a.parity, 0)) ||
+            (rc = phase(6, next)))
+          return rc;
+        scratch_zeroed_for = next > 0 ? i + 1 : -1;
+        if (c->timing) HIP_OK(c, hipEventRecord(get_event(c, ev + 1), c->stream));
+        ev += 2;
+        ++timed_passes;
+        i = i + 1;
+        continue;
+      }
       if (c->topo_fused && !c->gbar.p) {
         if ((rc = ensure(c, c->gbar, 64))) return rc;
         HIP_OK(c, hipMemsetAsync(c->gbar.p, 0, 64, c->stream));

@@ -1529,7 +1529,8 @@ __device__ __forceinline__ int soft_register(const DevState& st, const QPlan& pl
     if (c.is_hostname) continue;
     int64_t* reg = slot_ptr(st, pl, c.rslot) + nval(st, c.key, n);
     const unsigned long long old = atomicExch(reinterpret_cast<unsigned long long*>(reg), 1ull);
-    if (old == 0 && c.first_of_key) add64(&h->ssize[i], 1);
+    // node-sharded: a pair may first register on several ranks; k_topo_ssize counts the summed bins
+    if (old == 0 && c.first_of_key && !st.shard_keys) add64(&h->ssize[i], 1);
   }
   return 1;
 }
@@ -1781,6 +1782,24 @@ __device__ __forceinline__ void topo_resolve(const DevState* __restrict__ stp, P
     st.scratch[i] = 0;
 }
 
+// Node-sharded topology pods: topoSize of each ScheduleAnyway key (scoring.go:92-99) as the number of
+// registered pairs, counted after the ranks' registration slots were summed.
+__global__ __launch_bounds__(kBlock) void k_topo_ssize(const DevState* __restrict__ stp, PodArgs a) {
+  const DevState& st = *stp;
+  const QPlan& pl = st.plans[a.pod];
+  TopoHdr* h = hdr(st);
+  for (int i = 0; i < pl.n_soft; ++i) {
+    const TSpread& c = pl.soft[i];
+    if (c.is_hostname || !c.first_of_key || c.key < 0) continue;
+    const int nv = gp(st.key_n_values)[c.key];
+    const int64_t* reg = slot_ptr(st, pl, c.rslot);
+    int k = 0;
+    for (int v = blockIdx.x * kBlock + threadIdx.x; v < nv; v += gridDim.x * kBlock) k += reg[v] != 0;
+    k = wave_reduce_sum(k);
+    if (threadIdx.x == 0 && k) add64(&h->ssize[i], k);
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void k_topo_pre(const DevState* __restrict__ stp, PodArgs a) { topo_pre(stp, a); }
 __global__ __launch_bounds__(kBlock) void k_topo_min(const DevState* __restrict__ stp, PodArgs a) { topo_min(stp, a); }
 __global__ __launch_bounds__(kBlock) void k_topo_filter(const DevState* __restrict__ stp, PodArgs a) { topo_filter(stp, a); }
@@ -1900,6 +1919,34 @@ int launch_topo(const DevState* st, PodArgs a, int blocks, int64_t min_values, i
   r.prev_blocks = blocks;
   r.prev_parity = a.parity;
   hipLaunchKernelGGL(k_topo_resolve, dim3(blocks), dim3(kBlock), 0, s, st, r, next_scratch);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// One phase of the per-pod topology pipeline, for the node-sharded sequence the host interleaves
+// with RCCL exchanges (kgpu_api.cpp run_topo_sharded).  extra: min_values (phase 1), stat blocks
+// (5), next pod's scratch length (6).
+int launch_topo_phase(const DevState* st, const PodArgs& a, int phase, int blocks, int64_t extra, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  switch (phase) {
+    case 0: hipLaunchKernelGGL(k_topo_pre, dim3(blocks), dim3(kBlock), 0, s, st, a); break;
+    case 1: {
+      int64_t mb = (extra + kBlock - 1) / kBlock;
+      if (mb > kMaxBlocks) mb = kMaxBlocks;
+      if (mb > 0) hipLaunchKernelGGL(k_topo_min, dim3((int)mb), dim3(kBlock), 0, s, st, a);
+      break;
+    }
+    case 2: hipLaunchKernelGGL(k_topo_filter, dim3(blocks), dim3(kBlock), 0, s, st, a); break;
+    case 3: hipLaunchKernelGGL(k_topo_ssize, dim3(blocks), dim3(kBlock), 0, s, st, a); break;
+    case 4: hipLaunchKernelGGL(k_topo_score, dim3(blocks), dim3(kBlock), 0, s, st, a); break;
+    case 5: hipLaunchKernelGGL(k_topo_final, dim3(blocks), dim3(kBlock), 0, s, st, a, (int)extra); break;
+    default: {
+      PodArgs r = a;
+      r.prev = a.pod;
+      r.prev_blocks = blocks;
+      r.prev_parity = a.parity;
+      hipLaunchKernelGGL(k_topo_resolve, dim3(blocks), dim3(kBlock), 0, s, st, r, extra);
+    }
+  }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -123,6 +123,7 @@ class Pools:
         for k, a in P.items():
             setattr(c, k, abi.ptr(a))
             setattr(c, "n_" + k, len(a))
+        c._keep = P  # the struct holds raw pointers: the arrays live as long as it does
         return c, P
 
 

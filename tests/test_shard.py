@@ -4,7 +4,8 @@ resolve + assume by the owning rank -- against the C restatement on the unsharde
 
 The GPU box has one MI355X and RCCL refuses two ranks on one device, so the device tests run a
 one-rank communicator: every pod still goes through k_shard_pack -> ncclAllGather -> prev_winner
-over the gathered records.  The multi-rank combine rule itself is covered on the CPU with gloo
+over the gathered records, and every topology pod through the per-phase ncclAllReduce of its
+histograms, registration slots, sizes and score extremes (multi-rank: unmeasured on hardware).  The multi-rank combine rule itself is covered on the CPU with gloo
 (test_shard_cpu.py)."""
 import numpy as np
 import pytest
@@ -75,12 +76,34 @@ def test_sharded_cycle_diagnostics():
 
 
 @pytest.mark.gpu
-def test_sharded_rejects_topology_pods():
-    nodes, existing, pods, prof = cluster.taints_affinity_spread(n_nodes=50, n_pods=4)
-    fw = _sharded(prof, nodes, existing, pods)
-    q, pc, _, _ = fw.compile_pods(pods)
-    with pytest.raises(native.KgpuError, match="not sharded"):
-        fw.engine.schedule_batch(q, pc)
+def test_sharded_topology_config_c():
+    # PodTopologySpread (zone DoNotSchedule, hostname ScheduleAnyway) + taints + NodeAffinity: the
+    # histograms, sizes and score extremes go through the per-phase RCCL all-reduces
+    nodes, existing, pods, prof = cluster.taints_affinity_spread(n_nodes=500, n_pods=200)
+    _check(prof, nodes, existing, pods, chunks=2)
+
+
+@pytest.mark.gpu
+def test_sharded_topology_config_d():
+    nodes, existing, pods, prof = cluster.pod_affinity(n_nodes=300, n_existing=300, n_pods=150)
+    _check(prof, nodes, existing, pods)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [0, 3])
+def test_sharded_topology_random(seed):
+    nodes, existing, pods, services, rss = gen_random.topo_cluster(seed, n_nodes=60, n_existing=80, n_pods=40)
+    from kgpu.compile import Cluster
+    from oracle.cref import RefEngine
+    prof = Profile()
+    fw = GpuFramework(prof, nodes, existing, cluster=Cluster(services, rss=rss), pods_hint=pods, shard=(0, 1))
+    fw.init_comm(0, 1, native.comm_unique_id())
+    q, pc, _, errs = fw.compile_pods(pods)
+    assert not errs
+    want = RefEngine(fw.config, fw.snap, threads=4).schedule(q, pc)
+    got, _ = fw.engine.schedule_batch(q, pc)
+    for f in ("node", "feasible", "scored", "score"):
+        np.testing.assert_array_equal(want[f], got[f], err_msg=f)
 
 
 @pytest.mark.gpu
