@@ -1,0 +1,144 @@
+package gpueval
+
+/*
+#include "kgpu.h"
+*/
+import "C"
+
+import (
+	"encoding/json"
+	"fmt"
+	"unsafe"
+
+	v1 "k8s.io/api/core/v1"
+	metav1 "k8s.io/apimachinery/pkg/apis/meta/v1"
+	"k8s.io/apimachinery/pkg/labels"
+	"k8s.io/apimachinery/pkg/runtime"
+	framework "k8s.io/kubernetes/pkg/scheduler/framework/v1alpha1"
+)
+
+type metav1LabelSelector = metav1.LabelSelector
+
+var unsafeSizeofSnapshot = unsafe.Sizeof(C.kgpu_snapshot{})
+
+func ci64(a *arena, s []int64) *C.int64_t { return (*C.int64_t)(unsafe.Pointer(cslice(a, s))) }
+func ci32(a *arena, s []int32) *C.int32_t { return (*C.int32_t)(unsafe.Pointer(cslice(a, s))) }
+
+// argsFrom decodes the GpuEval pluginConfig args (INTEGRATION.md section 4).
+func argsFrom(obj runtime.Object) (*profileArgs, error) {
+	p := &profileArgs{HardPodAffinityWeight: 1, PercentageOfNodesToScore: 100, Mode: "select", TieBreakSeed: 0x7B,
+		LeastResources: map[string]int64{"cpu": 1, "memory": 1}, MostResources: map[string]int64{"cpu": 1, "memory": 1},
+		ignoredResources: map[string]struct{}{}}
+	if u, ok := obj.(*runtime.Unknown); ok && u != nil && len(u.Raw) > 0 {
+		if err := json.Unmarshal(u.Raw, p); err != nil {
+			return nil, fmt.Errorf("gpueval args: %v", err)
+		}
+	}
+	if len(p.Filters) == 0 && len(p.Scores) == 0 {
+		return nil, fmt.Errorf("gpueval args: no filter or score plugins to replace")
+	}
+	return p, nil
+}
+
+// defaultSelectorFromListers: helper.DefaultSelector (helper/spread.go:29-72) as a LabelSelector:
+// the selectors of the pod's Services and ReplicationControllers (label sets, merged) and of its
+// ReplicaSets and StatefulSets (label selectors, ANDed).  nil: no selector (Empty()).
+func defaultSelectorFromListers(h framework.FrameworkHandle, pod *v1.Pod) *metav1.LabelSelector {
+	f := h.SharedInformerFactory()
+	if f == nil {
+		return nil
+	}
+	set := labels.Set{}
+	var exprs []metav1.LabelSelectorRequirement
+	podLabels := labels.Set(pod.Labels)
+	if svcs, err := f.Core().V1().Services().Lister().Services(pod.Namespace).List(labels.Everything()); err == nil {
+		for _, s := range svcs {
+			if s.Spec.Selector != nil && labels.SelectorFromSet(s.Spec.Selector).Matches(podLabels) {
+				for k, v := range s.Spec.Selector {
+					set[k] = v
+				}
+			}
+		}
+	}
+	if len(pod.Labels) > 0 {
+		if rcs, err := f.Core().V1().ReplicationControllers().Lister().ReplicationControllers(pod.Namespace).List(labels.Everything()); err == nil {
+			for _, rc := range rcs {
+				if rc.Spec.Selector != nil && labels.SelectorFromSet(rc.Spec.Selector).Matches(podLabels) {
+					for k, v := range rc.Spec.Selector {
+						set[k] = v
+					}
+				}
+			}
+		}
+		if rss, err := f.Apps().V1().ReplicaSets().Lister().ReplicaSets(pod.Namespace).List(labels.Everything()); err == nil {
+			for _, rs := range rss {
+				if sel, err := metav1.LabelSelectorAsSelector(rs.Spec.Selector); err == nil && sel.Matches(podLabels) {
+					exprs = append(exprs, toExprs(rs.Spec.Selector)...)
+				}
+			}
+		}
+		if sss, err := f.Apps().V1().StatefulSets().Lister().StatefulSets(pod.Namespace).List(labels.Everything()); err == nil {
+			for _, ss := range sss {
+				if sel, err := metav1.LabelSelectorAsSelector(ss.Spec.Selector); err == nil && sel.Matches(podLabels) {
+					exprs = append(exprs, toExprs(ss.Spec.Selector)...)
+				}
+			}
+		}
+	}
+	if len(set) == 0 && len(exprs) == 0 {
+		return nil
+	}
+	return &metav1.LabelSelector{MatchLabels: set, MatchExpressions: exprs}
+}
+
+func toExprs(ls *metav1.LabelSelector) []metav1.LabelSelectorRequirement {
+	if ls == nil {
+		return nil
+	}
+	out := append([]metav1.LabelSelectorRequirement{}, ls.MatchExpressions...)
+	for k, v := range ls.MatchLabels {
+		out = append(out, metav1.LabelSelectorRequirement{Key: k, Operator: metav1.LabelSelectorOpIn, Values: []string{v}})
+	}
+	return out
+}
+
+// filterReasons rebuilds the plugins' status reasons from the device's status-word detail
+// (mirror of kubernetes-1_amd/kgpu/framework.py reasons).
+func filterReasons(plugin string, detail uint32) []string {
+	switch plugin {
+	case "NodeUnschedulable":
+		return []string{"node(s) were unschedulable"}
+	case "NodeName":
+		return []string{"node(s) didn't match the requested hostname"}
+	case "NodePorts":
+		return []string{"node(s) didn't have free ports for the requested pod ports"}
+	case "NodeAffinity":
+		return []string{"node(s) didn't match node selector"}
+	case "PodTopologySpread":
+		return []string{"node(s) didn't match pod topology spread constraints"}
+	case "TaintToleration":
+		return []string{"node(s) had taints that the pod didn't tolerate"}
+	case "NodeResourcesFit":
+		var out []string
+		if detail&1 != 0 {
+			out = append(out, "Too many pods")
+		}
+		for bit, r := range map[uint32]string{2: "cpu", 4: "memory", 8: "ephemeral-storage"} {
+			if detail&bit != 0 {
+				out = append(out, "Insufficient "+r)
+			}
+		}
+		return out
+	case "InterPodAffinity":
+		base := "node(s) didn't match pod affinity/anti-affinity"
+		switch detail {
+		case 1:
+			return []string{base, "node(s) didn't match pod affinity rules"}
+		case 2:
+			return []string{base, "node(s) didn't match pod anti-affinity rules"}
+		case 3:
+			return []string{base, "node(s) didn't satisfy existing pods anti-affinity rules"}
+		}
+	}
+	return nil
+}

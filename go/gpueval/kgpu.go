@@ -1,0 +1,157 @@
+// Package gpueval is the out-of-tree plugin set that runs kube-scheduler's per-pod node
+// evaluation on an MI355X through libkgpu.so (include/kgpu.h).  Register it with
+// app.WithPlugin(gpueval.Name, gpueval.New) (cmd/kube-scheduler/app/server.go:302-307).
+//
+// This file is the cgo binding: one method per C entry point.  All buffers handed to C are C
+// memory (cgo forbids passing Go memory that holds Go pointers), owned by an arena that the
+// caller frees after the call.
+package gpueval
+
+/*
+#cgo CFLAGS: -I${SRCDIR}/../../include
+#cgo LDFLAGS: -L${SRCDIR}/../../kubernetes-1_amd/kgpu -lkgpu -Wl,-rpath,${SRCDIR}/../../kubernetes-1_amd/kgpu
+#include <stdlib.h>
+#include <string.h>
+#include "kgpu.h"
+*/
+import "C"
+
+import (
+	"fmt"
+	"unsafe"
+)
+
+// arena owns C allocations made for one call.
+type arena struct{ ptrs []unsafe.Pointer }
+
+func (a *arena) alloc(bytes int) unsafe.Pointer {
+	if bytes <= 0 {
+		bytes = 1
+	}
+	p := C.calloc(1, C.size_t(bytes))
+	a.ptrs = append(a.ptrs, p)
+	return p
+}
+
+func (a *arena) free() {
+	for _, p := range a.ptrs {
+		C.free(p)
+	}
+	a.ptrs = nil
+}
+
+// cslice copies a Go slice of plain values (no pointers) into C memory.
+func cslice[T any](a *arena, s []T) *T {
+	if len(s) == 0 {
+		return nil
+	}
+	var z T
+	n := int(unsafe.Sizeof(z)) * len(s)
+	p := a.alloc(n)
+	C.memcpy(p, unsafe.Pointer(&s[0]), C.size_t(n))
+	return (*T)(p)
+}
+
+type engine struct{ ctx *C.kgpu_ctx }
+
+func kerr(ctx *C.kgpu_ctx, rc C.int) error {
+	if rc == C.KGPU_OK {
+		return nil
+	}
+	msg := "null context"
+	if ctx != nil {
+		msg = C.GoString(C.kgpu_last_error(ctx))
+	}
+	return fmt.Errorf("kgpu: %d: %s", int(rc), msg)
+}
+
+// newEngine replaces the framework.PluginFactory state of the replaced plugins
+// (framework/v1alpha1/registry.go:28) with the profile's plugin list, weights and args
+// (framework.go:205-298).
+func newEngine(cfg *C.kgpu_config) (*engine, error) {
+	if C.kgpu_abi_version() != C.KGPU_ABI_VERSION {
+		return nil, fmt.Errorf("kgpu: ABI version mismatch")
+	}
+	var ctx *C.kgpu_ctx
+	if rc := C.kgpu_create(cfg, &ctx); rc != C.KGPU_OK {
+		return nil, fmt.Errorf("kgpu_create: %d", int(rc))
+	}
+	return &engine{ctx: ctx}, nil
+}
+
+// uploadSnapshot mirrors cache.UpdateSnapshot (internal/cache/cache.go:202-301) from scratch.
+func (e *engine) uploadSnapshot(s *C.kgpu_snapshot, generation int64) error {
+	return kerr(e.ctx, C.kgpu_upload_snapshot(e.ctx, s, C.int64_t(generation)))
+}
+
+// applyDelta sends the NodeInfo changes since the last sync (kgpu_apply_delta): AddPod /
+// RemovePod by UID, SetNode, and the Snapshot.List() rebuild after node adds / removes.
+func (e *engine) applyDelta(b *C.kgpu_delta_batch, generation int64) ([]int32, error) {
+	n := int(b.n_deltas)
+	slots := make([]int32, n+1)
+	rc := C.kgpu_apply_delta(e.ctx, b, C.int64_t(generation), (*C.int32_t)(unsafe.Pointer(&slots[0])))
+	return slots[:n], kerr(e.ctx, rc)
+}
+
+// scheduleOne is genericScheduler.Schedule (core/generic_scheduler.go:146-209) for one pod: the
+// filter statuses, scores and the selected node stay on the device for the lookups below.
+func (e *engine) scheduleOne(q *C.kgpu_pod_query, pools *C.kgpu_pools, seq int64, assume bool) (C.kgpu_result, int32, error) {
+	var res C.kgpu_result
+	var slot C.int32_t
+	a := C.int32_t(0)
+	if assume {
+		a = 1
+	}
+	rc := C.kgpu_schedule_one(e.ctx, q, pools, C.int64_t(seq), a, &res, &slot)
+	return res, int32(slot), kerr(e.ctx, rc)
+}
+
+// scheduleBatch is the scheduleOne loop (scheduler.go:509-593) over queued pods with on-device
+// assume: the throughput path.
+func (e *engine) scheduleBatch(qs []C.kgpu_pod_query, pools *C.kgpu_pools, firstSeq int64) ([]C.kgpu_result, error) {
+	if len(qs) == 0 {
+		return nil, nil
+	}
+	var a arena
+	defer a.free()
+	cq := cslice(&a, qs)
+	res := make([]C.kgpu_result, len(qs))
+	var st C.kgpu_stats
+	rc := C.kgpu_schedule_batch(e.ctx, cq, C.int32_t(len(qs)), pools, C.int64_t(firstSeq),
+		(*C.kgpu_result)(unsafe.Pointer(&res[0])), &st)
+	return res, kerr(e.ctx, rc)
+}
+
+// filterWords copies the per-node PluginToStatus.Merge code words of the last scheduleOne
+// (framework.go:477-502): low byte = 1-based position of the first failing filter, bits 8-9 the
+// framework.Code, bits 16-31 the plugin detail.
+func (e *engine) filterWords(n int) ([]uint32, error) {
+	w := make([]uint32, n+1)
+	rc := C.kgpu_get_filter(e.ctx, (*C.uint32_t)(unsafe.Pointer(&w[0])))
+	return w[:n], kerr(e.ctx, rc)
+}
+
+// scores returns one score plugin's raw and normalized (unweighted) values per node.
+func (e *engine) scores(plugin int, n int) (raw, norm []int64, err error) {
+	raw, norm = make([]int64, n+1), make([]int64, n+1)
+	rc := C.kgpu_get_scores(e.ctx, C.int32_t(plugin), (*C.int64_t)(unsafe.Pointer(&raw[0])),
+		(*C.int64_t)(unsafe.Pointer(&norm[0])))
+	return raw[:n], norm[:n], kerr(e.ctx, rc)
+}
+
+func (e *engine) forget(slot int32) error { return kerr(e.ctx, C.kgpu_forget_pod(e.ctx, C.int32_t(slot))) }
+func (e *engine) generation() int64       { return int64(C.kgpu_generation(e.ctx)) }
+func (e *engine) close()                  { C.kgpu_destroy(e.ctx) }
+
+// Node sharding across the GPUs of one host (SURVEY.md 8(e)): one engine per GPU holding a
+// contiguous slice of Snapshot.List() (kgpu_snapshot.node_base / n_total_nodes).  Rank 0 creates
+// the RCCL id; every engine then receives the same calls with the same arguments, in order.
+func commUniqueID() ([128]byte, error) {
+	var id [128]byte
+	rc := C.kgpu_comm_unique_id((*C.uint8_t)(unsafe.Pointer(&id[0])))
+	return id, kerr(nil, rc)
+}
+
+func (e *engine) commInit(nranks, rank int, id [128]byte) error {
+	return kerr(e.ctx, C.kgpu_comm_init(e.ctx, C.int32_t(nranks), C.int32_t(rank), (*C.uint8_t)(unsafe.Pointer(&id[0]))))
+}

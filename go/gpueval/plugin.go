@@ -1,0 +1,535 @@
+package gpueval
+
+// GpuEval: one out-of-tree plugin that replaces the filter / score plugins of a profile with the
+// device (SURVEY.md 8(b) adapter pattern).  PreFilter syncs the device mirror with the Snapshot
+// the cycle runs on, compiles the pod and runs the whole cycle in one C call; Filter and Score are
+// lock-free lookups in the cycle record, safe under parallelize.Until's 16 goroutines.
+//
+// Two score modes (profileArgs.Mode):
+//   select: one score plugin (weight 1) returns 100 for the device-chosen node and 0 otherwise,
+//           so the reference selectHost (generic_scheduler.go:217-238) picks the device's node;
+//   shadow: the plugin returns the device's weighted total per node (DefaultNormalizeScore and
+//           the replaced plugins' weights applied on the device), clipped into [0, 100] only for
+//           the framework's range check -- per-plugin raw / normalized values stay available
+//           through kgpu_get_scores for parity checks.
+//
+// Reserve / Unreserve need no device call: cache.AssumePod / ForgetPod update the NodeInfo, and the
+// next PreFilter's generation diff (soa.go) sends NodeInfo.AddPod / RemovePod by UID.
+
+/*
+#include "kgpu.h"
+*/
+import "C"
+
+import (
+	"context"
+	"fmt"
+	"sort"
+	"strconv"
+	"sync/atomic"
+
+	v1 "k8s.io/api/core/v1"
+	"k8s.io/apimachinery/pkg/labels"
+	"k8s.io/apimachinery/pkg/runtime"
+	"k8s.io/apimachinery/pkg/types"
+	v1helper "k8s.io/kubernetes/pkg/apis/core/v1/helper"
+	framework "k8s.io/kubernetes/pkg/scheduler/framework/v1alpha1"
+)
+
+const Name = "GpuEval"
+
+const stateKey framework.StateKey = Name
+
+// profileArgs: the replaced plugins and their args (apis/config/types.go:115-239,
+// types_pluginargs.go), forwarded into kgpu_config.
+type profileArgs struct {
+	Filters                []string
+	Scores                 []struct{ Name string; Weight int64 }
+	LeastResources         map[string]int64
+	MostResources          map[string]int64
+	RTCRResources          map[string]int64
+	RTCRShape              [][2]int64 // (utilization, score 0-10)
+	HardPodAffinityWeight  int32
+	PercentageOfNodesToScore int32
+	TieBreakSeed           uint64
+	Mode                   string // "select" or "shadow"
+	ignoredResources       map[string]struct{}
+}
+
+var filterIDs = map[string]int32{"NodeUnschedulable": C.KGPU_F_NODE_UNSCHEDULABLE, "NodeResourcesFit": C.KGPU_F_NODE_RESOURCES_FIT,
+	"NodeName": C.KGPU_F_NODE_NAME, "NodePorts": C.KGPU_F_NODE_PORTS, "NodeAffinity": C.KGPU_F_NODE_AFFINITY,
+	"TaintToleration": C.KGPU_F_TAINT_TOLERATION, "PodTopologySpread": C.KGPU_F_POD_TOPOLOGY_SPREAD,
+	"InterPodAffinity": C.KGPU_F_INTER_POD_AFFINITY}
+
+var scoreIDs = map[string]int32{"NodeResourcesBalancedAllocation": C.KGPU_S_BALANCED_ALLOCATION,
+	"ImageLocality": C.KGPU_S_IMAGE_LOCALITY, "InterPodAffinity": C.KGPU_S_INTER_POD_AFFINITY,
+	"NodeResourcesLeastAllocated": C.KGPU_S_LEAST_ALLOCATED, "NodeAffinity": C.KGPU_S_NODE_AFFINITY,
+	"NodePreferAvoidPods": C.KGPU_S_NODE_PREFER_AVOID_PODS, "PodTopologySpread": C.KGPU_S_POD_TOPOLOGY_SPREAD,
+	"DefaultPodTopologySpread": C.KGPU_S_DEFAULT_POD_TOPOLOGY_SPREAD, "TaintToleration": C.KGPU_S_TAINT_TOLERATION,
+	"NodeResourcesMostAllocated": C.KGPU_S_MOST_ALLOCATED, "RequestedToCapacityRatio": C.KGPU_S_REQUESTED_TO_CAPACITY_RATIO,
+	"NodeResourceLimits": C.KGPU_S_RESOURCE_LIMITS}
+
+func (p *profileArgs) scalarResources() []string {
+	var out []string
+	for _, m := range []map[string]int64{p.LeastResources, p.MostResources, p.RTCRResources} {
+		for r := range m {
+			if r != "cpu" && r != "memory" && r != "ephemeral-storage" {
+				out = append(out, r)
+			}
+		}
+	}
+	sort.Strings(out)
+	return out
+}
+
+// config builds kgpu_config (kubernetes-1_amd/kgpu/compile.py Compiler.config).
+func (c *compiler) config() *C.kgpu_config {
+	p := c.prof
+	var cfg C.kgpu_config
+	cfg.abi_version = C.KGPU_ABI_VERSION
+	for _, f := range p.Filters {
+		if id, ok := filterIDs[f]; ok {
+			cfg.filters[cfg.n_filters] = C.int32_t(id)
+			cfg.n_filters++
+		}
+	}
+	for _, s := range p.Scores {
+		cfg.scores[cfg.n_scores] = C.int32_t(scoreIDs[s.Name])
+		w := s.Weight
+		if w == 0 {
+			w = 1
+		}
+		cfg.score_weights[cfg.n_scores] = C.int64_t(w)
+		cfg.n_scores++
+	}
+	res := func(name string) int32 {
+		switch name {
+		case "cpu":
+			return 0
+		case "memory":
+			return 1
+		case "ephemeral-storage":
+			return 2
+		}
+		return 3 + c.scalars.add(name)
+	}
+	fill := func(m map[string]int64, arr *[8]C.kgpu_resource_weight, n *C.int32_t) {
+		names := make([]string, 0, len(m))
+		for r := range m {
+			names = append(names, r)
+		}
+		sort.Strings(names)
+		for i, r := range names {
+			arr[i] = C.kgpu_resource_weight{resource: C.int32_t(res(r)), weight: C.int32_t(m[r])}
+		}
+		*n = C.int32_t(len(names))
+	}
+	fill(p.LeastResources, &cfg.least, &cfg.n_least)
+	fill(p.MostResources, &cfg.most, &cfg.n_most)
+	fill(p.RTCRResources, &cfg.rtcr, &cfg.n_rtcr)
+	for i, pt := range p.RTCRShape {
+		cfg.shape[i] = C.kgpu_shape_point{utilization: C.int64_t(pt[0]), score: C.int64_t(pt[1] * 10)}
+	}
+	cfg.n_shape = C.int32_t(len(p.RTCRShape))
+	cfg.hard_pod_affinity_weight = C.int32_t(p.HardPodAffinityWeight)
+	cfg.percentage_of_nodes_to_score = C.int32_t(p.PercentageOfNodesToScore)
+	cfg.seed = C.uint64_t(p.TieBreakSeed)
+	return &cfg
+}
+
+// cycle is the per-pod state read by Filter and Score.
+type cycle struct {
+	words  []uint32 // per-node filter status words (node index order)
+	total  []int64  // shadow mode: weighted total per node
+	chosen int32    // device-selected node index, -1 = FitError
+}
+
+func (c *cycle) Clone() framework.StateData { return c }
+
+type GpuEval struct {
+	h    framework.FrameworkHandle
+	prof *profileArgs
+	eng  *engine
+	comp *compiler
+	mir  *mirror
+	seq  int64
+}
+
+func (g *GpuEval) Name() string { return Name }
+
+func readCycle(cs *framework.CycleState) (*cycle, error) {
+	d, err := cs.Read(stateKey)
+	if err != nil {
+		return nil, err
+	}
+	c, ok := d.(*cycle)
+	if !ok {
+		return nil, fmt.Errorf("%+v convert to gpueval.cycle error", d)
+	}
+	return c, nil
+}
+
+// syncSnapshot brings the device mirror to the Snapshot of this cycle: a delta when the
+// dictionaries can absorb the changes, a full upload otherwise.
+func (g *GpuEval) syncSnapshot() error {
+	list, err := g.h.SnapshotSharedLister().NodeInfos().List()
+	if err != nil {
+		return err
+	}
+	var a arena
+	defer a.free()
+	if g.mir != nil {
+		b, err := g.deltaFromSnapshot(list, &a)
+		if err == nil {
+			g.mir.gen++
+			_, err = g.eng.applyDelta(b, g.mir.gen)
+			if err == nil {
+				return nil
+			}
+		}
+		if err != errNeedsUpload {
+			// the engine marks a failed batch's mirror invalid: rebuild it from scratch
+			g.mir = nil
+		}
+	}
+	return g.upload(list, &a)
+}
+
+// upload compiles the whole Snapshot.List() into kgpu_snapshot columns.
+func (g *GpuEval) upload(list []*framework.NodeInfo, a *arena) error {
+	c := newCompiler(g.prof)
+	for _, ni := range list {
+		c.registerNode(ni.Node())
+		for _, pi := range ni.Pods {
+			c.registerPod(pi.Pod)
+		}
+	}
+	for i, ni := range list {
+		if _, ok := c.nodeIndex[ni.Node().Name]; !ok {
+			c.nodeIndex[ni.Node().Name] = int32(i)
+		}
+	}
+	c.dims.K = len(c.nkeys.keys.items)
+	c.dims.S = len(c.scalars.items)
+	c.dims.TW = (len(c.taintList) + 63) / 64
+	if c.dims.TW == 0 {
+		c.dims.TW = 1
+	}
+	if g.eng == nil {
+		eng, err := newEngine(c.config())
+		if err != nil {
+			return err
+		}
+		g.eng = eng
+	}
+	g.comp = c
+	m := &mirror{index: map[string]int32{}, gens: map[string]int64{}, nodes: map[string]*v1.Node{},
+		pods: map[string]map[types.UID]*v1.Pod{}, uids: map[types.UID]int64{}}
+	if g.mir != nil {
+		m.uids, m.nextUID, m.gen = g.mir.uids, g.mir.nextUID, g.mir.gen
+	}
+	s, err := g.snapshotSoA(list, m, a)
+	if err != nil {
+		return err
+	}
+	m.gen++
+	g.mir = m
+	return g.eng.uploadSnapshot(s, m.gen)
+}
+
+// snapshotSoA fills kgpu_snapshot (one pass over the list; pods of every NodeInfo).  The list
+// is uploaded once per distinct node; a list holding a NodeInfo twice is aliased by the next
+// delta's order (kgpu_delta_batch.order).
+func (g *GpuEval) snapshotSoA(list []*framework.NodeInfo, m *mirror, a *arena) (*C.kgpu_snapshot, error) {
+	c := g.comp
+	seen := map[string]bool{}
+	var uniq []*framework.NodeInfo
+	for _, ni := range list {
+		if !seen[ni.Node().Name] {
+			seen[ni.Node().Name] = true
+			uniq = append(uniq, ni)
+		}
+	}
+	N, K, S, TW := len(uniq), c.dims.K, c.dims.S, c.dims.TW
+	i64 := func() []int64 { return make([]int64, N) }
+	allocCPU, allocMem, allocEph, reqCPU, reqMem, reqEph, nzCPU, nzMem := i64(), i64(), i64(), i64(), i64(), i64(), i64(), i64()
+	allocPods, numPods, zone, portCount := make([]int32, N), make([]int32, N), make([]int32, N), make([]int32, N)
+	unsched := make([]uint8, N)
+	labelVal := make([]int32, K*N)
+	for i := range labelVal {
+		labelVal[i] = -1
+	}
+	taintNo, taintPref := make([]uint64, TW*N), make([]uint64, TW*N)
+	allocSc, reqSc := make([]int64, S*N), make([]int64, S*N)
+	var podNode, podNs []int32
+	var podFlags []uint32
+	var podUID []int64
+	p := &pools{}
+	var terms []C.kgpu_term
+	var ports [][]C.kgpu_port
+	for i, ni := range uniq {
+		n := ni.Node()
+		m.names = append(m.names, n.Name)
+		m.index[n.Name] = int32(i)
+		m.gens[n.Name] = ni.Generation
+		m.nodes[n.Name] = n
+		r, err := c.nodeRow(n, p)
+		if err != nil {
+			return nil, err
+		}
+		allocCPU[i], allocMem[i], allocEph[i], allocPods[i] = int64(r.alloc_cpu), int64(r.alloc_mem), int64(r.alloc_eph), int32(r.alloc_pods)
+		unsched[i], zone[i] = uint8(r.unschedulable), int32(r.zone_id)
+		for j := 0; j+1 < int(r.labels.count); j += 2 {
+			labelVal[int(p.ints[int(r.labels.begin)+j])*N+i] = p.ints[int(r.labels.begin)+j+1]
+		}
+		if r.taints.count > 0 {
+			for w := 0; w < TW; w++ {
+				taintNo[w*N+i] = p.words[int(r.taints.begin)+w]
+				taintPref[w*N+i] = p.words[int(r.taints.begin)+TW+w]
+			}
+		}
+		for s := 0; s < int(r.alloc_scalar.count); s++ {
+			allocSc[s*N+i] = int64(p.words[int(r.alloc_scalar.begin)+s])
+		}
+		reqCPU[i], reqMem[i], reqEph[i] = ni.Requested.MilliCPU, ni.Requested.Memory, ni.Requested.EphemeralStorage
+		nzCPU[i], nzMem[i] = ni.NonZeroRequested.MilliCPU, ni.NonZeroRequested.Memory
+		for name, v := range ni.Requested.ScalarResources {
+			if col := c.scalars.get(string(name)); col >= 0 && int(col) < S {
+				reqSc[int(col)*N+i] = v
+			}
+		}
+		numPods[i] = int32(len(ni.Pods))
+		var used []C.kgpu_port
+		for ip, pp := range ni.UsedPorts {
+			for pr := range pp {
+				proto := map[string]int32{"TCP": 0, "UDP": 1, "SCTP": 2}[pr.Protocol]
+				used = append(used, C.kgpu_port{ip: C.int32_t(c.ips.add(ip)), proto: C.int32_t(proto), port: C.int32_t(pr.Port)})
+			}
+		}
+		ports = append(ports, used)
+		portCount[i] = int32(len(used))
+		m.pods[n.Name] = map[types.UID]*v1.Pod{}
+		for _, pi := range ni.Pods {
+			slot := int32(len(podNode))
+			m.pods[n.Name][pi.Pod.UID] = pi.Pod
+			podNode = append(podNode, int32(i))
+			podNs = append(podNs, c.ns.add(pi.Pod.Namespace))
+			fl := uint32(C.KGPU_PF_ACTIVE)
+			if pi.Pod.DeletionTimestamp != nil {
+				fl |= C.KGPU_PF_TERMINATING
+			}
+			if af := pi.Pod.Spec.Affinity; af != nil && (af.PodAffinity != nil || af.PodAntiAffinity != nil) {
+				fl |= C.KGPU_PF_WITH_AFFINITY
+			}
+			podFlags = append(podFlags, fl)
+			podUID = append(podUID, m.uid(pi.Pod.UID))
+			q, err := c.compilePod(pi.Pod, p) // the pod's terms (PodInfo, types.go:92-160)
+			if err != nil {
+				return nil, err
+			}
+			for kind, r := range []C.kgpu_range{q.ipa_req_aff, q.ipa_req_anti, q.ipa_pref_aff, q.ipa_pref_anti} {
+				for t := 0; t < int(r.count); t++ {
+					terms = append(terms, C.kgpu_term{pod: C.int32_t(slot), kind: C.int32_t(kind), t: p.podTerms[int(r.begin)+t]})
+				}
+			}
+		}
+	}
+	PK := len(c.pkeys.keys.items)
+	P := len(podNode)
+	podLab := make([]int32, PK*P)
+	for i := range podLab {
+		podLab[i] = -1
+	}
+	slot := 0
+	for _, ni := range uniq {
+		for _, pi := range ni.Pods {
+			for k, v := range pi.Pod.Labels {
+				ki, vi := c.pkeys.add(k, v)
+				if int(ki) < PK {
+					podLab[int(ki)*P+slot] = vi
+				}
+			}
+			slot++
+		}
+	}
+	PS := 1
+	for _, u := range ports {
+		if len(u) > PS {
+			PS = len(u)
+		}
+	}
+	portTab := make([]C.kgpu_port, PS*N)
+	for i, u := range ports {
+		for s, pt := range u {
+			portTab[s*N+i] = pt
+		}
+	}
+	s := (*C.kgpu_snapshot)(a.alloc(int(unsafeSizeofSnapshot)))
+	s.n_nodes, s.node_base, s.n_total_nodes = C.int32_t(N), 0, C.int32_t(N)
+	s.alloc_cpu, s.alloc_mem, s.alloc_eph = ci64(a, allocCPU), ci64(a, allocMem), ci64(a, allocEph)
+	s.alloc_pods = ci32(a, allocPods)
+	s.req_cpu, s.req_mem, s.req_eph = ci64(a, reqCPU), ci64(a, reqMem), ci64(a, reqEph)
+	s.nz_cpu, s.nz_mem = ci64(a, nzCPU), ci64(a, nzMem)
+	s.num_pods = ci32(a, numPods)
+	s.n_scalar, s.alloc_scalar, s.req_scalar = C.int32_t(S), ci64(a, allocSc), ci64(a, reqSc)
+	s.unschedulable = (*C.uint8_t)(cslice(a, unsched))
+	s.n_label_keys, s.label_val = C.int32_t(K), ci32(a, labelVal)
+	var b C.kgpu_delta_batch
+	g.keyMeta(&b, a)
+	s.key_n_values, s.value_off, s.value_int, s.value_int_ok, s.key_empty_value =
+		b.key_n_values, b.value_off, b.value_int, b.value_int_ok, b.key_empty_value
+	s.taint_words, s.taint_nosched, s.taint_prefer = C.int32_t(TW), (*C.uint64_t)(cslice(a, taintNo)), (*C.uint64_t)(cslice(a, taintPref))
+	s.port_slots, s.port_count, s.ports = C.int32_t(PS), ci32(a, portCount), cslice(a, portTab)
+	g.nodeLists(uniq, &b, a)
+	s.image_off, s.image_id, s.image_score, s.avoid_off, s.avoid_id = b.image_off, b.image_id, b.image_score, b.avoid_off, b.avoid_id
+	s.zone_id, s.n_zones = ci32(a, zone), C.int32_t(len(c.zones.items))
+	s.n_pods, s.pod_node, s.pod_ns = C.int32_t(P), ci32(a, podNode), ci32(a, podNs)
+	s.pod_flags = (*C.uint32_t)(cslice(a, podFlags))
+	s.n_pod_label_keys, s.pod_label_val = C.int32_t(PK), ci32(a, podLab)
+	s.n_terms, s.terms = C.int32_t(len(terms)), cslice(a, terms)
+	s.pools = *p.toC(a)
+	s.pod_uid = (*C.int64_t)(cslice(a, podUID))
+	return s, nil
+}
+
+// PreFilter: sync the device mirror to this cycle's Snapshot, compile the pod, run the cycle.
+func (g *GpuEval) PreFilter(ctx context.Context, cs *framework.CycleState, pod *v1.Pod) *framework.Status {
+	if err := g.syncSnapshot(); err != nil {
+		return framework.NewStatus(framework.Error, err.Error())
+	}
+	var a arena
+	defer a.free()
+	p := &pools{}
+	q, err := g.comp.compilePod(pod, p)
+	if err != nil {
+		return framework.NewStatus(framework.Error, err.Error())
+	}
+	if sel := g.defaultSelector(pod); sel != nil {
+		if q.dpts, err = g.comp.labelSelector(p, sel); err != nil {
+			return framework.NewStatus(framework.Error, err.Error())
+		}
+	}
+	cq := cslice(&a, []C.kgpu_pod_query{q})
+	res, _, err := g.eng.scheduleOne(cq, p.toC(&a), atomic.AddInt64(&g.seq, 1)-1, false)
+	if err != nil {
+		return framework.NewStatus(framework.Error, err.Error())
+	}
+	n := len(g.mir.names)
+	words, err := g.eng.filterWords(n)
+	if err != nil {
+		return framework.NewStatus(framework.Error, err.Error())
+	}
+	c := &cycle{words: words, chosen: int32(res.node)}
+	if g.prof.Mode == "shadow" {
+		c.total = make([]int64, n)
+		for _, s := range g.prof.Scores {
+			_, norm, err := g.eng.scores(int(scoreIDs[s.Name]), n)
+			if err != nil {
+				return framework.NewStatus(framework.Error, err.Error())
+			}
+			w := s.Weight
+			if w == 0 {
+				w = 1
+			}
+			for i := range norm {
+				c.total[i] += w * norm[i]
+			}
+		}
+	}
+	cs.Write(stateKey, c)
+	return nil
+}
+
+func (g *GpuEval) PreFilterExtensions() framework.PreFilterExtensions { return nil }
+
+// Filter: O(1) lookup of the node's status word.
+func (g *GpuEval) Filter(ctx context.Context, cs *framework.CycleState, pod *v1.Pod, ni *framework.NodeInfo) *framework.Status {
+	c, err := readCycle(cs)
+	if err != nil {
+		return framework.NewStatus(framework.Error, err.Error())
+	}
+	w := c.words[g.mir.index[ni.Node().Name]]
+	if w == 0 || w == C.KGPU_FS_NOT_EVALUATED {
+		return nil
+	}
+	return framework.NewStatus(framework.Code((w>>8)&3), reasons(g.prof.Filters, w)...)
+}
+
+func (g *GpuEval) Score(ctx context.Context, cs *framework.CycleState, pod *v1.Pod, node string) (int64, *framework.Status) {
+	c, err := readCycle(cs)
+	if err != nil {
+		return 0, framework.NewStatus(framework.Error, err.Error())
+	}
+	i := g.mir.index[node]
+	if c.total != nil {
+		t := c.total[i]
+		if t > framework.MaxNodeScore {
+			t = framework.MaxNodeScore // the framework's range check; selectHost order kept by select mode
+		}
+		return t, nil
+	}
+	if i == c.chosen {
+		return framework.MaxNodeScore, nil
+	}
+	return 0, nil
+}
+
+func (g *GpuEval) ScoreExtensions() framework.ScoreExtensions { return nil }
+
+// Reserve / Unreserve: cache.AssumePod / ForgetPod already changed the NodeInfo; the next
+// PreFilter's generation diff carries it to the device.
+func (g *GpuEval) Reserve(ctx context.Context, cs *framework.CycleState, pod *v1.Pod, node string) *framework.Status {
+	return nil
+}
+func (g *GpuEval) Unreserve(ctx context.Context, cs *framework.CycleState, pod *v1.Pod, node string) {}
+
+// New is the framework.PluginFactory (registry.go:28).
+func New(obj runtime.Object, h framework.FrameworkHandle) (framework.Plugin, error) {
+	prof, err := argsFrom(obj)
+	if err != nil {
+		return nil, err
+	}
+	return &GpuEval{h: h, prof: prof}, nil
+}
+
+// defaultSelector: helper.DefaultSelector (helper/spread.go:29-72) from the handle's listers.
+func (g *GpuEval) defaultSelector(pod *v1.Pod) *metav1LabelSelector {
+	return defaultSelectorFromListers(g.h, pod)
+}
+
+// ---------------------------------------------------------------- small helpers
+func reasons(filters []string, w uint32) []string {
+	pos := int(w & 0xFF)
+	if pos == 0 || pos > len(filters) {
+		return nil
+	}
+	return filterReasons(filters[pos-1], w>>16)
+}
+
+func labelsSet(m map[string]string) labels.Set { return labels.Set(m) }
+
+func parseInt64(s string) (int64, uint8) {
+	x, err := strconv.ParseInt(s, 10, 64)
+	if err != nil {
+		return 0, 0
+	}
+	return x, 1
+}
+
+func sortCSR(ids []int32, vals []int64) {
+	sort.Sort(csrSorter{ids, vals})
+}
+
+type csrSorter struct {
+	ids  []int32
+	vals []int64
+}
+
+func (s csrSorter) Len() int           { return len(s.ids) }
+func (s csrSorter) Less(i, j int) bool { return s.ids[i] < s.ids[j] }
+func (s csrSorter) Swap(i, j int) {
+	s.ids[i], s.ids[j] = s.ids[j], s.ids[i]
+	s.vals[i], s.vals[j] = s.vals[j], s.vals[i]
+}
+
+var _ = v1helper.IsScalarResourceName

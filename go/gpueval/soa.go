@@ -1,0 +1,278 @@
+package gpueval
+
+// Device mirror of the scheduling Snapshot (mirror of kubernetes-1_amd/kgpu/compile.py
+// compile_snapshot and kgpu/cache.py sync):
+//
+//   * upload():   Snapshot.List() -> kgpu_snapshot SoA columns (node order = node index).
+//   * sync():     at PreFilter, the Snapshot was just refreshed by cache.UpdateSnapshot
+//                 (internal/cache/cache.go:202-301).  NodeInfo.Generation tells which NodeInfos
+//                 changed; their pod sets are diffed by UID into KGPU_D_ADD_POD / REMOVE_POD,
+//                 changed Node objects into KGPU_D_SET_NODE, and a changed list into the
+//                 kgpu_delta_batch.order gather.  Anything the device columns cannot absorb
+//                 (a new label key, more taint words, a new scalar resource) re-uploads.
+
+/*
+#include "kgpu.h"
+*/
+import "C"
+
+import (
+	"fmt"
+	"unsafe"
+
+	v1 "k8s.io/api/core/v1"
+	"k8s.io/apimachinery/pkg/types"
+	v1helper "k8s.io/kubernetes/pkg/apis/core/v1/helper"
+	framework "k8s.io/kubernetes/pkg/scheduler/framework/v1alpha1"
+	utilnode "k8s.io/kubernetes/pkg/util/node"
+)
+
+var errNeedsUpload = fmt.Errorf("gpueval: change needs a full upload")
+
+// mirror is what the device holds, per list position.
+type mirror struct {
+	names    []string
+	index    map[string]int32            // first position of a node (aliases share it)
+	gens     map[string]int64            // NodeInfo.Generation last sent
+	nodes    map[string]*v1.Node         // Node object last sent
+	pods     map[string]map[types.UID]*v1.Pod
+	uids     map[types.UID]int64         // pod UID -> engine uid
+	nextUID  int64
+	gen      int64
+}
+
+func (m *mirror) uid(u types.UID) int64 {
+	if id, ok := m.uids[u]; ok {
+		return id
+	}
+	m.nextUID++
+	m.uids[u] = m.nextUID
+	return m.nextUID
+}
+
+// nodeRow compiles the node's own attributes (kgpu_node_row).
+func (c *compiler) nodeRow(n *v1.Node, p *pools) (C.kgpu_node_row, error) {
+	var r C.kgpu_node_row
+	al := n.Status.Allocatable
+	r.alloc_cpu = C.int64_t(al.Cpu().MilliValue())
+	r.alloc_mem = C.int64_t(al.Memory().Value())
+	r.alloc_eph = C.int64_t(al.StorageEphemeral().Value())
+	r.alloc_pods = C.int32_t(al.Pods().Value())
+	if n.Spec.Unschedulable {
+		r.unschedulable = 1
+	}
+	r.zone_id = -1
+	if z := utilnode.GetZoneKey(n); z != "" {
+		r.zone_id = C.int32_t(c.zones.add(z))
+	}
+	pairs := []int32{}
+	for k, v := range n.Labels {
+		ki := c.nkeys.key(k)
+		if ki < 0 || int(ki) >= c.dims.K {
+			return r, errNeedsUpload
+		}
+		_, vi := c.nkeys.add(k, v)
+		pairs = append(pairs, ki, vi)
+	}
+	r.labels = p.intsRange(pairs)
+	TW := c.dims.TW
+	words := make([]uint64, 2*TW)
+	any := false
+	for _, t := range n.Spec.Taints {
+		id := c.taintID(taintKey{t.Key, t.Value, string(t.Effect)})
+		if int(id)/64 >= TW {
+			return r, errNeedsUpload
+		}
+		switch t.Effect {
+		case v1.TaintEffectNoSchedule, v1.TaintEffectNoExecute:
+			words[id/64] |= 1 << (uint(id) % 64)
+			any = true
+		case v1.TaintEffectPreferNoSchedule:
+			words[TW+int(id)/64] |= 1 << (uint(id) % 64)
+			any = true
+		}
+	}
+	if any {
+		r.taints = p.wordsRange(words)
+	}
+	sc := make([]uint64, c.dims.S)
+	anyS := false
+	for res, q := range al {
+		if !v1helper.IsScalarResourceName(res) {
+			continue
+		}
+		col := c.scalars.add(string(res))
+		if int(col) >= c.dims.S {
+			return r, errNeedsUpload
+		}
+		sc[col] += uint64(q.Value())
+		anyS = true
+	}
+	if anyS {
+		r.alloc_scalar = p.wordsRange(sc)
+	}
+	return r, nil
+}
+
+// deltaFromSnapshot diffs the refreshed Snapshot against the mirror.  Returns the C batch (in the
+// arena) or errNeedsUpload.
+func (g *GpuEval) deltaFromSnapshot(list []*framework.NodeInfo, a *arena) (*C.kgpu_delta_batch, error) {
+	m, c := g.mir, g.comp
+	p := &pools{}
+	var deltas []C.kgpu_delta
+	var podsQ []C.kgpu_pod_query
+	var rows []C.kgpu_node_row
+	names := make([]string, len(list))
+	for i, ni := range list {
+		names[i] = ni.Node().Name
+	}
+	reorder := len(names) != len(m.names)
+	for i := 0; !reorder && i < len(names); i++ {
+		reorder = names[i] != m.names[i]
+	}
+	newIndex := map[string]int32{}
+	for i, nm := range names {
+		if _, ok := newIndex[nm]; !ok {
+			newIndex[nm] = int32(i)
+		}
+	}
+	var order []int32
+	rowOf := map[string]int{}
+	for _, ni := range list {
+		nm := ni.Node().Name
+		if _, seen := rowOf[nm]; seen {
+			continue
+		}
+		_, known := m.index[nm]
+		if !known || m.nodes[nm] != ni.Node() {
+			r, err := c.nodeRow(ni.Node(), p)
+			if err != nil {
+				return nil, err
+			}
+			rows = append(rows, r)
+			rowOf[nm] = len(rows) - 1
+			deltas = append(deltas, C.kgpu_delta{op: C.KGPU_D_SET_NODE, node: C.int32_t(newIndex[nm]), item: C.int32_t(len(rows) - 1)})
+		}
+	}
+	if reorder {
+		order = make([]int32, len(names))
+		for i, nm := range names {
+			if j, ok := m.index[nm]; ok {
+				order[i] = j
+			} else {
+				order[i] = int32(-1 - rowOf[nm])
+			}
+		}
+	}
+	addPod := func(nm string, pod *v1.Pod, op C.int32_t) error {
+		q, err := c.compilePod(pod, p)
+		if err != nil {
+			return err
+		}
+		podsQ = append(podsQ, q)
+		deltas = append(deltas, C.kgpu_delta{op: op, node: C.int32_t(newIndex[nm]), uid: C.int64_t(m.uid(pod.UID)),
+			item: C.int32_t(len(podsQ) - 1)})
+		return nil
+	}
+	for _, ni := range list {
+		nm := ni.Node().Name
+		if g0, ok := m.gens[nm]; ok && g0 == ni.Generation && !reorder {
+			continue
+		}
+		old := m.pods[nm]
+		_, wasListed := m.index[nm]
+		cur := map[types.UID]*v1.Pod{}
+		for _, pi := range ni.Pods {
+			cur[pi.Pod.UID] = pi.Pod
+		}
+		if wasListed {
+			for u, pod := range old { // NodeInfo.RemovePod of pods gone or changed
+				if np, ok := cur[u]; !ok || np != pod {
+					if err := addPod(nm, pod, C.KGPU_D_REMOVE_POD); err != nil {
+						return nil, err
+					}
+				}
+			}
+		}
+		for u, pod := range cur { // NodeInfo.AddPod of new or changed pods
+			if op, ok := old[u]; wasListed && ok && op == pod {
+				continue
+			}
+			if err := addPod(nm, pod, C.KGPU_D_ADD_POD); err != nil {
+				return nil, err
+			}
+		}
+		m.pods[nm] = cur
+		m.gens[nm] = ni.Generation
+		m.nodes[nm] = ni.Node()
+	}
+	b := (*C.kgpu_delta_batch)(a.alloc(int(unsafe.Sizeof(C.kgpu_delta_batch{}))))
+	b.n_deltas, b.deltas = C.int32_t(len(deltas)), cslice(a, deltas)
+	b.n_pods, b.pods = C.int32_t(len(podsQ)), cslice(a, podsQ)
+	b.n_rows, b.rows = C.int32_t(len(rows)), cslice(a, rows)
+	if reorder {
+		b.n_order, b.order = C.int32_t(len(order)), (*C.int32_t)(unsafe.Pointer(cslice(a, order)))
+	}
+	if reorder || len(rows) > 0 {
+		g.nodeLists(list, b, a) // ImageLocality / NodePreferAvoidPods CSR over the new list
+		g.keyMeta(b, a)         // label dictionaries may have grown
+	}
+	b.n_zones = C.int32_t(len(c.zones.items))
+	b.pools = *p.toC(a)
+	m.names, m.index = names, newIndex
+	return b, nil
+}
+
+// nodeLists fills the ImageLocality scaledImageScore and NodePreferAvoidPods CSR
+// (image_locality.go:100-113; node_prefer_avoid_pods.go:47-82).
+func (g *GpuEval) nodeLists(list []*framework.NodeInfo, b *C.kgpu_delta_batch, a *arena) {
+	c := g.comp
+	total := float64(len(list))
+	off, ids, scores := []int32{0}, []int32{}, []int64{}
+	aoff, aids := []int32{0}, []int32{}
+	for _, ni := range list {
+		for name, st := range ni.ImageStates {
+			ids = append(ids, c.images.add(name))
+			scores = append(scores, int64(float64(st.Size)*(float64(st.NumNodes)/total)))
+		}
+		sortCSR(ids[off[len(off)-1]:], scores[off[len(off)-1]:])
+		off = append(off, int32(len(ids)))
+		if avoids, err := v1helper.GetAvoidPodsFromNodeAnnotations(ni.Node().Annotations); err == nil {
+			for _, av := range avoids.PreferAvoidPods {
+				if pc := av.PodSignature.PodController; pc != nil {
+					aids = append(aids, c.controllers.add(pc.Kind+"/"+string(pc.UID)))
+				}
+			}
+		}
+		aoff = append(aoff, int32(len(aids)))
+	}
+	b.image_off = (*C.int32_t)(unsafe.Pointer(cslice(a, off)))
+	b.image_id = (*C.int32_t)(unsafe.Pointer(cslice(a, append(ids, 0))))
+	b.image_score = (*C.int64_t)(unsafe.Pointer(cslice(a, append(scores, 0))))
+	b.avoid_off = (*C.int32_t)(unsafe.Pointer(cslice(a, aoff)))
+	b.avoid_id = (*C.int32_t)(unsafe.Pointer(cslice(a, append(aids, 0))))
+}
+
+// keyMeta sends the node label dictionaries (key_n_values / value_off / value_int ...).
+func (g *GpuEval) keyMeta(b *C.kgpu_delta_batch, a *arena) {
+	c := g.comp
+	K := c.dims.K
+	nv, off, empty := make([]int32, K), []int32{0}, make([]int32, K)
+	ints, oks := []int64{}, []uint8{}
+	for k := 0; k < K; k++ {
+		d := c.nkeys.vals[k]
+		nv[k] = int32(len(d.items))
+		for _, v := range d.items {
+			x, ok := parseInt64(v)
+			ints = append(ints, x)
+			oks = append(oks, ok)
+		}
+		off = append(off, int32(len(ints)))
+		empty[k] = d.get("")
+	}
+	b.key_n_values = (*C.int32_t)(unsafe.Pointer(cslice(a, append(nv, 0))))
+	b.value_off = (*C.int32_t)(unsafe.Pointer(cslice(a, off)))
+	b.value_int = (*C.int64_t)(unsafe.Pointer(cslice(a, append(ints, 0))))
+	b.value_int_ok = (*C.uint8_t)(unsafe.Pointer(cslice(a, append(oks, 0))))
+	b.key_empty_value = (*C.int32_t)(unsafe.Pointer(cslice(a, append(empty, 0))))
+}
