@@ -504,6 +504,10 @@ int kgpu_read_nodes(kgpu_ctx* ctx, int64_t* req_cpu, int64_t* req_mem, int64_t* 
  * DefaultPodTopologySpread pods go through one persistent launch with device-resident domain
  * histograms; 0 = one topology pipeline per pod. */
 #define KGPU_OPT_TOPO_PERSISTENT 6
+/* KGPU_OPT_ABORT_AT (7): test hook -- the persistent run holding batch query `value` raises its
+ * abort word there, as a workgroup that lost co-residency would (-1, the default: never).  The
+ * batch then fails with KGPU_E_DEVICE and the engine refuses cycles until the next upload. */
+#define KGPU_OPT_ABORT_AT 7
 int kgpu_set_option(kgpu_ctx* ctx, int32_t option, int64_t value);
 /* Phase stamps of the last persistent run (100 MHz s_memrealtime ticks), 16 per pipeline
  * iteration (pods + 1): workgroup 0's {start, evaluated, previous pod resolved, published, end, 0,

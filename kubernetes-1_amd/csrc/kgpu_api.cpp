@@ -56,6 +56,7 @@ struct kgpu_ctx {
   int max_groups = 0;  // KGPU_OPT_PERSIST_GROUPS (0 = n_cus)
   DevBuf gran;        // persistent-kernel granules + abort word
   int32_t abort_host = 0;
+  int32_t abort_at = -1;  // KGPU_OPT_ABORT_AT: batch query index at which a persistent run aborts
   bool phase_trace = false;
   DevBuf trace;
   std::vector<int64_t> trace_host;
@@ -1162,6 +1163,7 @@ int run_tbatch(kgpu_ctx* c, TRun& tr, int first, int count, int64_t first_seq, i
   a.elig = reinterpret_cast<uint32_t*>(z + b_hist + b_tot + b_reg + b_sany);
   a.gran = reinterpret_cast<uint64_t*>(z + b_hist + b_tot + b_reg + b_sany + b_elig);
   a.abort = abort_word;
+  a.abort_at = c->abort_at >= first && c->abort_at < first + count ? c->abort_at - first : -1;
   a.trace = nullptr;
   if (c->phase_trace) {
     if ((rc = ensure(c, c->trace, sizeof(int64_t) * 16 * (size_t)(count + 1)))) return rc;
@@ -1435,6 +1437,7 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
       ba.gran = static_cast<uint64_t*>(c->gran.p);
       ba.feas = reinterpret_cast<int32_t*>(ba.gran + cells);
       ba.abort = abort_word;
+      ba.abort_at = c->abort_at >= i && c->abort_at < i + cnt ? c->abort_at - i : -1;
       ba.trace = nullptr;
       if (c->phase_trace) {
         if ((rc = ensure(c, c->trace, sizeof(int64_t) * 16 * (size_t)(cnt + 1)))) return rc;
@@ -2293,6 +2296,7 @@ int kgpu_set_option(kgpu_ctx* c, int32_t option, int64_t value) {
   else if (option == KGPU_OPT_PHASE_TRACE) c->phase_trace = value != 0;
   else if (option == KGPU_OPT_TOPO_FUSED) c->topo_fused = value != 0;
   else if (option == KGPU_OPT_TOPO_PERSISTENT) c->tfast = value != 0;
+  else if (option == KGPU_OPT_ABORT_AT) c->abort_at = value < 0 || value > INT32_MAX ? -1 : (int32_t)value;
   else return KGPU_E_INVAL;
   return KGPU_OK;
 }

@@ -247,6 +247,9 @@ struct BatchArgs {
   int64_t* trace;       // null, or [count + 1][16] s_memrealtime stamps, 8 per traced workgroup
                         // (0 and last): iteration start, evaluated, previous pod resolved,
                         // granule published, iteration end
+  int32_t abort_at;     // KGPU_OPT_ABORT_AT test hook: workgroup 0 raises the abort word at this
+                        // iteration (-1: never)
+  int32_t pad_a;
 };
 
 // ---------------------------------------------------------------- persistent topology kernel
@@ -363,8 +366,8 @@ struct TBatchArgs {
   // byte offsets of the LDS regions (histogram bins start at 0)
   int32_t o_reg, o_tot, o_sany, o_stat, o_smask, o_zsum, o_wred, o_misc, o_pt, o_lab;
   int32_t lab_keys;       // node label keys cached in LDS per workgroup ([lab_keys][per] value ids)
-  int32_t pad_l;
-  int64_t* trace;         // null, or [count + 1][16] s_memrealtime stamps (KGPU_OPT_PHASE_TRACE): per pod
+  int32_t abort_at;       // KGPU_OPT_ABORT_AT test hook (-1: never), as in BatchArgs
+  int64_t* trace;        // null, or [count + 1][16] s_memrealtime stamps (KGPU_OPT_PHASE_TRACE): per pod
                           // and traced workgroup (0, last): start, PreFilter minima, rows evaluated,
                           // stats published, stats resolved, key published, winner resolved, end
 };

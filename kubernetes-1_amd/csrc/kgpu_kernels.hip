@@ -1242,6 +1242,7 @@ __global__ __launch_bounds__(B) void k_batch(const DevState* __restrict__ stp, B
       uint64_t wkey = 0;
       int wg = -1;
       bool ok = true;
+      if (i == pa.abort_at && g == 0 && tid == 0) __hip_atomic_store(pa.abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (have_prev) ok = poll_row(prow, G, pa.abort, wkey, wg);
       KGPU_STAMP(i, 2);
       if (tid == 0) {
@@ -2324,6 +2325,7 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
   if (trc) trow[(size_t)i * 16 + (k)] = (int64_t)__builtin_amdgcn_s_memrealtime()
   for (int i = 0; i < ta.count; ++i) {
     KGPU_TSTAMP(0);
+    if (i == ta.abort_at && g == 0 && tid == 0) __hip_atomic_store(ta.abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int pod = ta.first + i;
     if (wave == W - 1 && i + 1 < ta.count && lane < (int)(sizeof(kgpu_pod_query) / 16)) {
       // warm the next pod's query record (its first touch would otherwise put a memory round
@@ -2759,8 +2761,14 @@ int launch_batch(const DevState* st, const BatchArgs& a, int groups, int geo, in
       return -1;
     attr_set[spec][geo] = true;
   }
-  hipLaunchKernelGGL(kBatch[spec][geo], dim3(groups), dim3(kGeo[geo].B), kBatchLdsPad, (hipStream_t)stream, st, a);
-  if (hipGetLastError() != hipSuccess) return -1;
+  // Cooperative: the runtime refuses a grid whose workgroups cannot all be resident at once, so
+  // the granule exchange never waits on a workgroup that has not started.
+  BatchArgs arg = a;
+  const DevState* sp = st;
+  void* args[] = {(void*)&sp, (void*)&arg};
+  if (hipLaunchCooperativeKernel(reinterpret_cast<const void*>(kBatch[spec][geo]), dim3(groups), dim3(kGeo[geo].B),
+                                 args, (unsigned)kBatchLdsPad, (hipStream_t)stream) != hipSuccess)
+    return -1;
   hipLaunchKernelGGL(k_batch_fixup, dim3((a.count + 255) / 256), dim3(256), 0, (hipStream_t)stream, st, a, groups);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -33,6 +33,43 @@ IPA_REASONS = {1: ["node(s) didn't match pod affinity/anti-affinity", "node(s) d
                    "node(s) didn't satisfy existing pods anti-affinity rules"]}
 
 
+def status_reasons(filters, nodes, pod, node_name, word):
+    """(code, plugin, reasons) of a node's device status word, formatted as the failing plugin
+    formats them; None for a feasible node.  filters: the profile's filter plugins in order;
+    nodes: name -> v1.Node."""
+    pos = word & 0xFF
+    if pos == 0:
+        return None
+    plugin = filters[pos - 1]
+    code = (word >> 8) & 3
+    detail = word >> 16
+    if plugin == "NodeResourcesFit":  # fit.go:159-176, 194-267
+        res = api.PodResources(pod)
+        out = []
+        if detail & 1:
+            out.append("Too many pods")
+        for bit, r in ((2, "cpu"), (4, "memory"), (8, "ephemeral-storage")):
+            if detail & bit:
+                out.append("Insufficient " + r)
+        for i, r in enumerate(res.scalars):
+            if detail & (16 << min(i, 11)):
+                out.append("Insufficient " + r)
+        return code, plugin, out
+    if plugin == "TaintToleration":  # taint_toleration.go:54-72
+        from .compile import _tolerates
+        tols = api.spec(pod).get("tolerations") or []
+        for t in api.spec(nodes[node_name]).get("taints") or []:
+            if t.get("effect") not in ("NoSchedule", "NoExecute"):
+                continue
+            k, v, e = t.get("key", "") or "", t.get("value", "") or "", t.get("effect")
+            if not any(_tolerates(x, k, v, e) for x in tols):
+                return code, plugin, ["node(s) had taint {%s: %s}, that the pod didn't tolerate" % (k, v)]
+        return code, plugin, []
+    if plugin == "InterPodAffinity":
+        return code, plugin, list(IPA_REASONS.get(detail, []))
+    return code, plugin, [REASON[plugin]]
+
+
 class CycleResult:
     def __init__(self, host, result, statuses, scores):
         self.host = host            # node name or None
@@ -81,37 +118,7 @@ class GpuFramework:
 
     # ------------------------------------------------------------------ reasons
     def reasons(self, pod, node_name, word):
-        pos = word & 0xFF
-        if pos == 0:
-            return None
-        plugin = self.filters[pos - 1]
-        code = (word >> 8) & 3
-        detail = word >> 16
-        if plugin == "NodeResourcesFit":  # fit.go:159-176, 194-267
-            res = api.PodResources(pod)
-            out = []
-            if detail & 1:
-                out.append("Too many pods")
-            for bit, r in ((2, "cpu"), (4, "memory"), (8, "ephemeral-storage")):
-                if detail & bit:
-                    out.append("Insufficient " + r)
-            for i, r in enumerate(res.scalars):
-                if detail & (16 << min(i, 11)):
-                    out.append("Insufficient " + r)
-            return code, plugin, out
-        if plugin == "TaintToleration":  # taint_toleration.go:54-72
-            from .compile import _tolerates
-            tols = api.spec(pod).get("tolerations") or []
-            for t in api.spec(self.nodes[node_name]).get("taints") or []:
-                if t.get("effect") not in ("NoSchedule", "NoExecute"):
-                    continue
-                k, v, e = t.get("key", "") or "", t.get("value", "") or "", t.get("effect")
-                if not any(_tolerates(x, k, v, e) for x in tols):
-                    return code, plugin, ["node(s) had taint {%s: %s}, that the pod didn't tolerate" % (k, v)]
-            return code, plugin, []
-        if plugin == "InterPodAffinity":
-            return code, plugin, list(IPA_REASONS.get(detail, []))
-        return code, plugin, [REASON[plugin]]
+        return status_reasons(self.filters, self.nodes, pod, node_name, word)
 
     # ------------------------------------------------------------------ cycles
     def cycle(self, pod, assume=False, seq=None):

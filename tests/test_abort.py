@@ -1,0 +1,96 @@
+"""Persistent-run abort (KGPU_OPT_ABORT_AT): a run that gives up mid-batch must fail the batch,
+invalidate the device mirror (later cycles refused until the next upload), and leave an engine
+that, after re-upload, schedules exactly as the C restatement does.
+
+The hook raises the abort word from workgroup 0 at a chosen pod, which is what a workgroup that
+lost co-residency does after kSpinTimeout (kgpu_kernels.hip, poll_row / tpoll_slot)."""
+import numpy as np
+import pytest
+
+from kgpu import abi, cluster
+from kgpu.compile import Profile
+from kgpu.framework import GpuFramework
+from kgpu.native import KgpuError
+
+
+def _ref(fw, q, pc):
+    from oracle.cref import RefEngine
+    ref = RefEngine(fw.config, fw.snap, threads=4)
+    return ref.schedule(q, pc)
+
+
+def _abort_then_recover(fw, q, pc, at, groups=0, must_abort=True):
+    """(aborted, placements after recovery).  A hook index that falls on a pod scheduled by the
+    per-pod launches (no persistent run holds it) does not abort: must_abort=False accepts that."""
+    e = fw.engine
+    e.upload(fw.snap, fw.arrays)
+    e.set_option(abi.OPT_PERSIST_GROUPS, groups)
+    e.set_option(abi.OPT_ABORT_AT, at)
+    try:
+        res, _ = e.schedule_batch(q, pc)
+    except KgpuError as ex:
+        assert ex.code == abi.E_DEVICE, ex
+        assert "re-upload" in str(ex)
+    else:
+        e.set_option(abi.OPT_ABORT_AT, -1)
+        assert not must_abort, "the abort hook at pod %d did not abort the batch" % at
+        return False, res
+    e.set_option(abi.OPT_ABORT_AT, -1)
+    with pytest.raises(KgpuError):      # the mirror is invalid until the next upload
+        e.schedule_batch(q[:1], pc)
+    e.upload(fw.snap, fw.arrays)
+    got, _ = e.schedule_batch(q, pc)
+    return True, got
+
+
+def _same(a, b):
+    for f in ("node", "feasible", "scored", "score"):
+        np.testing.assert_array_equal(a[f], b[f], err_msg=f)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("at,groups", [(0, 0), (37, 0), (37, 3), (199, 0)])
+def test_abort_k_batch(at, groups):
+    nodes, existing, pods, prof = cluster.fit_least_balanced(n_nodes=700, n_pods=200)
+    fw = GpuFramework(prof, nodes, existing, pods_hint=pods)
+    q, pc, _, errs = fw.compile_pods(pods)
+    assert not errs
+    _same(_ref(fw, q, pc), _abort_then_recover(fw, q, pc, at, groups)[1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("at", [0, 45])
+def test_abort_k_tbatch(at):
+    nodes, existing, pods, prof = cluster.taints_affinity_spread(n_nodes=600, n_pods=120)
+    fw = GpuFramework(prof, nodes, existing, pods_hint=pods)
+    q, pc, _, errs = fw.compile_pods(pods)
+    assert not errs
+    _same(_ref(fw, q, pc), _abort_then_recover(fw, q, pc, at)[1])
+
+
+def _mixed_batch():
+    """Config (b)-style pods under the default profile with two pods carrying preferred
+    NodeAffinity terms: their normalize maxima are not constant, so they run as per-pod launches
+    and split the batch into three persistent k_batch runs."""
+    nodes, _, pods, _ = cluster.fit_least_balanced(n_nodes=700, n_pods=200, zones=4)
+    pref = {"nodeAffinity": {"preferredDuringSchedulingIgnoredDuringExecution": [
+        {"weight": 5, "preference": {"matchExpressions": [
+            {"key": cluster.ZONE, "operator": "In", "values": ["zone1"]}]}}]}}
+    for i in (60, 130):
+        pods[i] = cluster.pod("pref%d" % i, "200m", "256Mi", affinity=pref)
+    return nodes, pods
+
+
+@pytest.mark.gpu
+def test_abort_in_one_of_several_runs():
+    """An abort in any of a batch's persistent runs must surface (one abort word per
+    batch, OR-ed on the device), and an abort hook on a per-pod launch must leave the batch exact."""
+    nodes, pods = _mixed_batch()
+    fw = GpuFramework(Profile(), nodes, [], pods_hint=pods)
+    q, pc, _, errs = fw.compile_pods(pods)
+    assert not errs
+    want = _ref(fw, q, pc)
+    for at, must in ((10, True), (60, False), (100, True), (130, False), (190, True)):
+        ab, got = _abort_then_recover(fw, q, pc, at, must_abort=must)
+        assert ab == must, at
+        _same(want, got)
