@@ -53,6 +53,20 @@ __device__ __forceinline__ const CAS T* cp(const T* p) {
   return (const CAS T*)p;
 }
 
+// Pin a record read through cp() in scalar registers.  A load from the constant address space is
+// invariant, so the compiler may re-issue it at every use instead of keeping the value; for a
+// record this workgroup has never read (one pod query per scheduling cycle) each re-issue is a
+// scalar-cache miss, ~0.4 us.  The opaque asm makes the words values the compiler must keep.
+template <class T>
+__device__ __forceinline__ void pin_sgpr(T& x) {
+  static_assert(sizeof(T) % 8 == 0, "pin_sgpr: 8-byte words");
+  uint64_t w[sizeof(T) / 8];
+  __builtin_memcpy(w, &x, sizeof(T));
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(T) / 8); ++i) asm volatile("" : "+s"(w[i]));
+  __builtin_memcpy(&x, w, sizeof(T));
+}
+
 constexpr uint32_t kRuntime = 0xFFFFFFFFu;  // FM/SM of the list-walking instantiation
 constexpr uint32_t kDefRes = 1u << 31;      // SM flag: Least/Most over {cpu: 1, memory: 1}
 constexpr uint32_t kSMask = (1u << KGPU_NUM_SCORES) - 1;
@@ -612,6 +626,26 @@ __device__ __forceinline__ int64_t wave_sum_i64(int64_t x) { return (int64_t)wav
 struct OpOrU64 {
   __device__ __forceinline__ uint64_t operator()(uint64_t a, uint64_t b) const { return a | b; }
 };
+// two independent unsigned max reductions in lockstep
+__device__ __forceinline__ void wave_red64x2(uint64_t& x, uint64_t& y) {
+#define KGPU_STEP2(C, R)              \
+  {                                   \
+    const uint64_t tx = dpp64<C, R>(x); \
+    const uint64_t ty = dpp64<C, R>(y); \
+    x = x > tx ? x : tx;              \
+    y = y > ty ? y : ty;              \
+  }
+  KGPU_STEP2(0xB1, 0xF)
+  KGPU_STEP2(0x4E, 0xF)
+  KGPU_STEP2(0x141, 0xF)
+  KGPU_STEP2(0x140, 0xF)
+  KGPU_STEP2(0x142, 0xA)
+  KGPU_STEP2(0x143, 0xC)
+#undef KGPU_STEP2
+  x = readlane64(x, 63);
+  y = readlane64(y, 63);
+}
+
 // argmax of unique keys: the maximum, then the one lane holding it
 __device__ __forceinline__ void wave_argmax(uint64_t& k, int& i) {
   const uint64_t m = wave_red64(k, OpMaxU64{});
@@ -1039,12 +1073,22 @@ __device__ __forceinline__ void assume_regs(const kgpu_pod_query& q, NodeRes& r)
 }
 
 // Key of one node for one pod: 0 = infeasible, else ((score+1) << 40) | rank40.
+// Wait for this lane's outstanding vector loads.  Used at the end of paths that load only for
+// some pods (extended resources, host ports): the join after them then carries no pending load,
+// so no later register write in the pod loop waits on vmcnt -- which counts stores too, and would
+// hold the evaluation behind the previous pod's write-through granule and assume stores.
+__device__ __forceinline__ void vm_drain() { __builtin_amdgcn_s_waitcnt(0x0F70); }  // vmcnt(0) only
+
 template <uint32_t FM, uint32_t SM>
 __device__ __forceinline__ uint64_t node_key(const DevState& st, const kgpu_pod_query& q, const NodeRes& r, int n,
                                              uint64_t tk) {
-  if (run_filters<FM>(st, q, r, n) != 0) return 0;
+  if (run_filters<FM>(st, q, r, n) != 0) {
+    if (q.scalars.count | q.ports.count) vm_drain();
+    return 0;
+  }
   NodeEval e{0, 0, 0, 0};
   run_scores<SM>(st, q, r, n, e, false);
+  if (q.scalars.count | q.ports.count) vm_drain();
   const int64_t total = key_total<SM>(st, e.partial, e.taint, e.na);
   return ((uint64_t)(total + 1) << 40) | rank40(tk, (uint64_t)(st.node_base + n), st.tie_mode);
 }
@@ -1078,22 +1122,29 @@ __device__ __forceinline__ void wg_partials(BatchShared<B>& sh, const uint64_t (
                                             int ob, int jb, uint64_t keyb) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   Cand a{0, -1, 0}, b{0, -1, 0};
+  // feasible counts through ballots (scalar popcounts), not a DPP sum chain
 #pragma unroll
   for (int j = 0; j < K; ++j) {
     const int l = j * B + lo_tid;
     const uint64_t k = keys[j];
-    if (k) {
-      ++a.feas;
-      if (k > a.key) { a.key = k; a.idx = l; }
-    }
+    a.feas += __popcll(__ballot(k != 0));
+    if (k > a.key) { a.key = k; a.idx = l; }
     const uint64_t kv = (vb && tid == ob && j == jb) ? keyb : k;
-    if (kv) {
-      ++b.feas;
-      if (kv > b.key) { b.key = kv; b.idx = l; }
-    }
+    b.feas += __popcll(__ballot(kv != 0));
+    if (kv > b.key) { b.key = kv; b.idx = l; }
   }
-  wave_reduce_cand(a);
-  if (vb) wave_reduce_cand(b);
+  if (vb) {
+    // the two max chains interleaved (independent DPP sequences overlap)
+    uint64_t ma = a.key, mb = b.key;
+    wave_red64x2(ma, mb);
+    const uint64_t ba = __ballot(a.key == ma && ma != 0), bb = __ballot(b.key == mb && mb != 0);
+    a.idx = ba ? __builtin_amdgcn_readlane(a.idx, (int)__builtin_ctzll(ba)) : -1;
+    b.idx = bb ? __builtin_amdgcn_readlane(b.idx, (int)__builtin_ctzll(bb)) : -1;
+    a.key = ma;
+    b.key = mb;
+  } else {
+    wave_argmax(a.key, a.idx);
+  }
   if (lane == 0) {
     sh.ka[wave] = a.key; sh.ia[wave] = a.idx; sh.fa[wave] = a.feas;
     sh.kb[wave] = b.key; sh.ib[wave] = b.idx; sh.fb[wave] = b.feas;
@@ -1114,9 +1165,7 @@ __device__ __forceinline__ Cand wg_combine(const BatchShared<B>& sh, bool varian
 }
 
 // Wave 0: poll pod `row`'s G (<= 256) granules and return the winning key and workgroup to every
-// lane.  The next sweep's loads are issued before the current sweep is examined, so a granule that
-// lands is seen one load latency later, not up to two; the abort word rides along with every
-// sweep.  Returns false on timeout / abort.
+// lane; the abort word rides along with every sweep.  Returns false on timeout / abort.
 struct Sweep {
   uint64_t v[4];
   int abort;
@@ -1130,13 +1179,20 @@ __device__ __forceinline__ Sweep sweep(const uint64_t* row, int G, const int32_t
   return s;
 }
 
+// One sweep in flight at a time: a speculative next sweep left in flight when the row completes
+// would be waited for at the first reuse of its registers in the node evaluation -- and vmcnt
+// counts stores too, so that wait would also hold the evaluation behind the granule, result and
+// assume stores issued since.
 __device__ __forceinline__ bool poll_row(const uint64_t* row, int G, const int32_t* abort_word, uint64_t& wkey,
                                          int& wg) {
   const int lane = threadIdx.x & 63;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  Sweep cur = sweep(row, G, abort_word);
   for (;;) {
-    const Sweep nxt = sweep(row, G, abort_word);
+    const Sweep cur = sweep(row, G, abort_word);
+    // the abort word is examined first: a load left unconsumed on the success path would be
+    // waited for at the first reuse of its register in the node evaluation -- behind every store
+    // issued since (vmcnt counts stores too)
+    if (cur.abort != 0) return false;
     bool all = true;
     uint64_t k = 0;
     int gsel = -1;
@@ -1156,8 +1212,7 @@ __device__ __forceinline__ bool poll_row(const uint64_t* row, int G, const int32
       wg = k ? gsel : -1;
       return true;
     }
-    if (cur.abort != 0 || __builtin_amdgcn_s_memrealtime() - t0 > kSpinTimeout) return false;
-    cur = nxt;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinTimeout) return false;
   }
 }
 
@@ -1182,6 +1237,10 @@ __global__ __launch_bounds__(B) void k_batch(const DevState* __restrict__ stp, B
       if constexpr ((SM & kDefRes) != 0 && SM != kRuntime) set_recips(r[j]);
     }
   }
+  // The row loads complete here.  Left to the first use inside the pod loop, their wait would sit
+  // in the loop body as a vmcnt(0) -- and vmcnt counts stores too, so every iteration would wait
+  // there for the previous iteration's write-through granule and assume stores to be acknowledged.
+  __builtin_amdgcn_s_waitcnt(0);
   // phase stamps (diagnostics): per iteration i, 8 per traced workgroup (0 and last):
   // start, evaluated, pod i-1 resolved, pod i published, iteration end
   const bool tr = pa.trace && tid == 0 && (g == 0 || g == G - 1);
@@ -1203,7 +1262,28 @@ __global__ __launch_bounds__(B) void k_batch(const DevState* __restrict__ stp, B
     const bool fast_b = have_prev && cand >= 0 && qp.scalars.count == 0 && qp.ports.count == 0;
     const int ob = cand >= 0 ? cand % B : -1, jb = cand >= 0 ? cand / B : -1;
     uint64_t keyb = 0;
-    if (have_cur) {
+    if (have_cur && FM != kRuntime) {
+      // Straight-line profiles: variant B is one more independent evaluation in the same pass
+      // (every lane evaluates a copy of its row jb, lane ob with pod i-1 assumed on it), so the
+      // two overlap in the issue stream instead of B running after A in lane ob's wave.
+      const uint64_t tk = pod_tie_key(st.seed, pa.seq0 + i);
+      const int js = jb > 0 ? jb : 0;
+      NodeRes rb = r[0];
+#pragma unroll
+      for (int j = 1; j < K; ++j)
+        if (j == js) rb = r[j];
+      if (tid == ob) assume_regs(qp, rb);
+      const int nb = lo + js * B + tid;
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        const int n = lo + j * B + tid;
+        keys[j] = n < st.N ? node_key<FM, SM>(st, q, r[j], n, tk) : 0;
+      }
+      if (fast_b) keyb = nb < st.N ? node_key<FM, SM>(st, q, rb, nb, tk) : 0;
+      KGPU_STAMP(i, 5);
+      KGPU_STAMP(i, 6);
+      wg_partials<K, B>(sh, keys, tid, fast_b, ob, jb, keyb);
+    } else if (have_cur) {
       const uint64_t tk = pod_tie_key(st.seed, pa.seq0 + i);
 #pragma unroll
       for (int j = 0; j < K; ++j) {
@@ -1226,7 +1306,11 @@ __global__ __launch_bounds__(B) void k_batch(const DevState* __restrict__ stp, B
     KGPU_STAMP(i, 1);
     // the next pod's query: issued now, consumed after the hop
     kgpu_pod_query qn{};
+#ifdef KGPU_EXPERIMENT_SAMEQ
+    if (i + 1 < pa.count) qn = *cp(st.queries + pa.first);
+#else
     if (i + 1 < pa.count) qn = *cp(st.queries + pa.first + i + 1);
+#endif
     __syncthreads();
     // ---- wave 0: resolve pod i-1, then publish pod i's granule (unless this workgroup won i-1
     //      without a precomputed variant B: it re-evaluates first)

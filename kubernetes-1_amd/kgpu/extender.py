@@ -1,0 +1,236 @@
+"""Scheduler-extender front-end over the device mirror.
+
+The reference scheduler calls an HTTP extender after its own filters and scores
+(`core/generic_scheduler.go:497-525` findNodesThatPassExtenders, `:670-708` prioritizeNodes) through
+`HTTPExtender` (`core/extender.go:273-438`): a JSON POST to `<urlPrefix>/<verb>` carrying
+`ExtenderArgs`, answered with `ExtenderFilterResult`, `HostPriorityList` or
+`ExtenderBindingResult` (`staging/src/k8s.io/kube-scheduler/extender/v1/types.go`).  This module
+serves those verbs from the GPU engine, so a stock kube-scheduler can use the device path without
+a rebuild: disable the in-tree filter/score plugins the device replaces, and list the extender
+with `filterVerb: filter`, `prioritizeVerb: prioritize`, `bindVerb: bind`, `weight: 1`,
+`nodeCacheCapable: true`.
+
+  filter      one device cycle (kgpu_schedule_one, no assume) on the mirror synced with
+              kgpu_apply_delta; the candidates that pass come back as NodeNames (or Nodes),
+              every other candidate in FailedNodes with the failing plugin's reasons.
+  prioritize  the same cycle's outcome per candidate.  mode "select" (default): 10 for the
+              device's selectHost winner, 0 otherwise -- the scheduler adds score * weight *
+              (MaxNodeScore / MaxExtenderPriority) (generic_scheduler.go:703-707), so with no
+              in-tree scorers its own selectHost lands on the device's winner.  mode "total":
+              the device's weighted score total of each node.
+  bind        the pod is bound (optional `binder` callback) and its placement goes into the
+              scheduler-cache mirror (AssumePod + FinishBinding, cache.go:338-381), so the next
+              cycle sees it without an informer round trip.
+
+A cycle is computed once per (pod UID, cache generation): filter and prioritize of one scheduling
+cycle share it.  Calls are serialized (one engine, one stream).
+"""
+import json
+import threading
+import time
+from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
+
+import numpy as np
+
+from . import abi
+from . import api
+from .compile import CompileError, Pools
+from .framework import status_reasons
+
+MAX_EXTENDER_PRIORITY = 10  # extender/v1/types.go:29
+
+
+class ExtenderError(Exception):
+    """Reported to the scheduler in the result's Error field."""
+
+
+def _pod_uid(pod):
+    return api.meta(pod).get("uid", "") or ""
+
+
+class GpuExtender:
+    def __init__(self, cache, mode="select", binder=None, clock=time.monotonic):
+        """cache: a kgpu.cache.SchedulerCache holding the cluster (the extender's node cache:
+        nodeCacheCapable).  binder(namespace, name, uid, node) -> error string or None, for the
+        API-server binding itself (None: record the placement only)."""
+        if mode not in ("select", "total"):
+            raise ValueError("mode must be 'select' or 'total'")
+        self.cache = cache
+        self.mode = mode
+        self.binder = binder
+        self.clock = clock
+        self.lock = threading.Lock()
+        self.seq = 0
+        self._memo = None      # (uid, generation, cycle)
+        self._pending = {}     # uid -> pod seen by filter / prioritize, awaiting bind
+
+    # ------------------------------------------------------------------ cycle
+    def _cycle(self, pod):
+        gen = self.cache.sync()
+        uid = _pod_uid(pod)
+        if self._memo and uid and self._memo[0] == uid and self._memo[1] == gen:
+            return self._memo[2]
+        pools = Pools()
+        try:
+            q = self.cache.compiler.compile_pod(pod, pools)
+        except CompileError as e:
+            raise ExtenderError(str(e))
+        pc, _ = pools.finalize()
+        res, _ = self.cache.engine.schedule_one(np.array([q], abi.QUERY), pc, seq=self.seq, assume=False)
+        self.seq += 1
+        n = len(self.cache.list)
+        words = self.cache.engine.filter_words(n)
+        totals = None
+        if self.mode == "total":
+            totals = np.zeros(n, np.int64)
+            for name, w in self.cache.profile.scores:
+                _, norm = self.cache.engine.scores(abi.SCORE_IDS[name], n)
+                totals += norm * w
+        node = int(res["node"])
+        cyc = {"words": words, "totals": totals, "winner": self.cache.list[node] if node >= 0 else None,
+               "error": node == -2}
+        if uid:
+            self._memo = (uid, gen, cyc)
+            self._pending[uid] = pod
+        return cyc
+
+    def _candidates(self, args):
+        """ExtenderArgs -> (names, NodeList items or None).  NodeNames when the scheduler treats
+        the extender as node-cache capable, else the full Node objects (extender.go:293-304)."""
+        names = args.get("NodeNames")
+        items = None
+        if names is None:
+            nl = args.get("Nodes")
+            if nl is None:
+                raise ExtenderError("ExtenderArgs carries neither NodeNames nor Nodes")
+            items = nl.get("items") or []
+            names = [api.name_of(n) for n in items]
+            self._sync_nodes(items)
+        self.cache.sync()
+        for nm in names:
+            if nm not in self.cache.index:
+                raise ExtenderError("node %r is not in the extender's node cache" % nm)
+        return names, items
+
+    def _sync_nodes(self, items):
+        """Node objects sent with each call (nodeCacheCapable false) refresh the mirror's copy."""
+        for n in items:
+            old = self.cache.nodes.get(api.name_of(n))
+            if old is None:
+                self.cache.add_node(n)
+            elif old != n:
+                self.cache.update_node(old, n)
+
+    # ------------------------------------------------------------------ verbs
+    def filter(self, args):
+        """ExtenderArgs -> ExtenderFilterResult (extender.go:273-338)."""
+        try:
+            with self.lock:
+                pod = args.get("Pod") or {}
+                names, items = self._candidates(args)
+                cyc = self._cycle(pod)
+                if cyc["error"]:
+                    raise ExtenderError("a score plugin failed for pod %s/%s" % (api.ns_of(pod), api.name_of(pod)))
+                keep, failed = [], {}
+                filters = [f for f in self.cache.profile.filters if f in abi.FILTER_IDS]
+                for k, nm in enumerate(names):
+                    w = int(cyc["words"][self.cache.index[nm]])
+                    if w == 0:
+                        keep.append(k)
+                        continue
+                    if w == abi.STATUS_NOT_EVALUATED:
+                        failed[nm] = "node not evaluated (percentageOfNodesToScore)"
+                        continue
+                    st = status_reasons(filters, self.cache.nodes, pod, nm, w)
+                    failed[nm] = ", ".join(st[2]) if st and st[2] else (st[1] if st else "")
+        except ExtenderError as e:
+            return {"Nodes": None, "NodeNames": None, "FailedNodes": None, "Error": str(e)}
+        out = {"Nodes": None, "NodeNames": None, "FailedNodes": failed, "Error": ""}
+        if items is None:
+            out["NodeNames"] = [names[k] for k in keep]
+        else:
+            out["Nodes"] = {"metadata": {}, "items": [items[k] for k in keep]}
+        return out
+
+    def prioritize(self, args):
+        """ExtenderArgs -> HostPriorityList (extender.go:340-382).  A failure is an HTTP error:
+        the scheduler ignores a failing prioritizer (generic_scheduler.go:686-688)."""
+        with self.lock:
+            pod = args.get("Pod") or {}
+            names, _ = self._candidates(args)
+            cyc = self._cycle(pod)
+            out = []
+            for nm in names:
+                if self.mode == "select":
+                    s = MAX_EXTENDER_PRIORITY if nm == cyc["winner"] else 0
+                else:
+                    s = int(cyc["totals"][self.cache.index[nm]]) if cyc["words"][self.cache.index[nm]] == 0 else 0
+                out.append({"Host": nm, "Score": s})
+            return out
+
+    def bind(self, args):
+        """ExtenderBindingArgs -> ExtenderBindingResult (extender.go:384-404)."""
+        with self.lock:
+            uid, node = args.get("PodUID", ""), args.get("Node", "")
+            pod = self._pending.pop(uid, None)
+            if pod is None:
+                return {"Error": "pod %s/%s (uid %s) was not filtered by this extender" %
+                                 (args.get("PodNamespace", ""), args.get("PodName", ""), uid)}
+            if node not in self.cache.index:
+                return {"Error": "node %r is not in the extender's node cache" % node}
+            if self.binder is not None:
+                err = self.binder(args.get("PodNamespace", ""), args.get("PodName", ""), uid, node)
+                if err:
+                    return {"Error": str(err)}
+            placed = dict(pod)
+            placed["spec"] = dict(api.spec(pod), nodeName=node)
+            self.cache.assume_pod(placed)
+            self.cache.finish_binding(placed, self.clock())
+            self._memo = None
+            return {"Error": ""}
+
+
+# ---------------------------------------------------------------------- HTTP
+class _Handler(BaseHTTPRequestHandler):
+    ext = None
+    prefix = ""
+
+    def log_message(self, fmt, *a):  # quiet
+        pass
+
+    def do_POST(self):
+        path = self.path
+        if not path.startswith(self.prefix + "/"):
+            return self._send(404, {"Error": "unknown path %s" % path})
+        verb = path[len(self.prefix) + 1:]
+        fn = {"filter": self.ext.filter, "prioritize": self.ext.prioritize, "bind": self.ext.bind}.get(verb)
+        if fn is None:
+            return self._send(404, {"Error": "unknown verb %s" % verb})
+        try:
+            n = int(self.headers.get("Content-Length", "0"))
+            args = json.loads(self.rfile.read(n) or b"{}")
+        except (ValueError, json.JSONDecodeError) as e:
+            return self._send(400, {"Error": "bad request body: %s" % e})
+        try:
+            out = fn(args)
+        except ExtenderError as e:      # prioritize: the scheduler treats non-200 as an error
+            return self._send(500, {"Error": str(e)})
+        self._send(200, out)
+
+    def _send(self, code, obj):
+        body = json.dumps(obj).encode()
+        self.send_response(code)
+        self.send_header("Content-Type", "application/json")
+        self.send_header("Content-Length", str(len(body)))
+        self.end_headers()
+        self.wfile.write(body)
+
+
+def serve(ext, host="127.0.0.1", port=0, prefix=""):
+    """Start the extender's HTTP server in a daemon thread; returns (server, url prefix).
+    The scheduler's `urlPrefix` is the returned URL."""
+    handler = type("ExtHandler", (_Handler,), {"ext": ext, "prefix": prefix.rstrip("/")})
+    srv = ThreadingHTTPServer((host, port), handler)
+    t = threading.Thread(target=srv.serve_forever, daemon=True)
+    t.start()
+    return srv, "http://%s:%d%s" % (host, srv.server_address[1], prefix.rstrip("/"))
