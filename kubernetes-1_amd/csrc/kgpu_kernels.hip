@@ -53,19 +53,6 @@ __device__ __forceinline__ const CAS T* cp(const T* p) {
   return (const CAS T*)p;
 }
 
-// Pin a record read through cp() in scalar registers.  A load from the constant address space is
-// invariant, so the compiler may re-issue it at every use instead of keeping the value; for a
-// record this workgroup has never read (one pod query per scheduling cycle) each re-issue is a
-// scalar-cache miss, ~0.4 us.  The opaque asm makes the words values the compiler must keep.
-template <class T>
-__device__ __forceinline__ void pin_sgpr(T& x) {
-  static_assert(sizeof(T) % 8 == 0, "pin_sgpr: 8-byte words");
-  uint64_t w[sizeof(T) / 8];
-  __builtin_memcpy(w, &x, sizeof(T));
-#pragma unroll
-  for (int i = 0; i < (int)(sizeof(T) / 8); ++i) asm volatile("" : "+s"(w[i]));
-  __builtin_memcpy(&x, w, sizeof(T));
-}
 
 constexpr uint32_t kRuntime = 0xFFFFFFFFu;  // FM/SM of the list-walking instantiation
 constexpr uint32_t kDefRes = 1u << 31;      // SM flag: Least/Most over {cpu: 1, memory: 1}
@@ -1262,28 +1249,7 @@ __global__ __launch_bounds__(B) void k_batch(const DevState* __restrict__ stp, B
     const bool fast_b = have_prev && cand >= 0 && qp.scalars.count == 0 && qp.ports.count == 0;
     const int ob = cand >= 0 ? cand % B : -1, jb = cand >= 0 ? cand / B : -1;
     uint64_t keyb = 0;
-    if (have_cur && FM != kRuntime) {
-      // Straight-line profiles: variant B is one more independent evaluation in the same pass
-      // (every lane evaluates a copy of its row jb, lane ob with pod i-1 assumed on it), so the
-      // two overlap in the issue stream instead of B running after A in lane ob's wave.
-      const uint64_t tk = pod_tie_key(st.seed, pa.seq0 + i);
-      const int js = jb > 0 ? jb : 0;
-      NodeRes rb = r[0];
-#pragma unroll
-      for (int j = 1; j < K; ++j)
-        if (j == js) rb = r[j];
-      if (tid == ob) assume_regs(qp, rb);
-      const int nb = lo + js * B + tid;
-#pragma unroll
-      for (int j = 0; j < K; ++j) {
-        const int n = lo + j * B + tid;
-        keys[j] = n < st.N ? node_key<FM, SM>(st, q, r[j], n, tk) : 0;
-      }
-      if (fast_b) keyb = nb < st.N ? node_key<FM, SM>(st, q, rb, nb, tk) : 0;
-      KGPU_STAMP(i, 5);
-      KGPU_STAMP(i, 6);
-      wg_partials<K, B>(sh, keys, tid, fast_b, ob, jb, keyb);
-    } else if (have_cur) {
+    if (have_cur) {
       const uint64_t tk = pod_tie_key(st.seed, pa.seq0 + i);
 #pragma unroll
       for (int j = 0; j < K; ++j) {
@@ -1306,11 +1272,7 @@ __global__ __launch_bounds__(B) void k_batch(const DevState* __restrict__ stp, B
     KGPU_STAMP(i, 1);
     // the next pod's query: issued now, consumed after the hop
     kgpu_pod_query qn{};
-#ifdef KGPU_EXPERIMENT_SAMEQ
-    if (i + 1 < pa.count) qn = *cp(st.queries + pa.first);
-#else
     if (i + 1 < pa.count) qn = *cp(st.queries + pa.first + i + 1);
-#endif
     __syncthreads();
     // ---- wave 0: resolve pod i-1, then publish pod i's granule (unless this workgroup won i-1
     //      without a precomputed variant B: it re-evaluates first)

@@ -1,0 +1,46 @@
+"""Per-call latency of kgpu_schedule_one (the drop-in plugin's per-cycle call) on config (b).
+
+Run under `rocprofv3 --hip-trace --kernel-trace --stats` to see where a call's time goes
+(API calls, copies, launches, synchronisation)."""
+import argparse
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "kubernetes-1_amd")]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--nodes", type=int, default=5000)
+    ap.add_argument("--pods", type=int, default=300)
+    ap.add_argument("--config", default="b")
+    args = ap.parse_args()
+    from kgpu import cluster
+    from kgpu.framework import GpuFramework
+    if args.config == "b":
+        nodes, existing, pods, prof = cluster.fit_least_balanced(n_nodes=args.nodes, n_pods=args.pods)
+    else:
+        nodes, existing, pods, prof = cluster.taints_affinity_spread(n_nodes=args.nodes, n_pods=args.pods)
+    fw = GpuFramework(prof, nodes, existing, pods_hint=pods[:16])
+    q, pc, _, errs = fw.compile_pods(pods)
+    assert not errs
+    eng = fw.engine
+    for i in range(20):  # warm
+        eng.schedule_one(q[i], pc, seq=i, assume=False)
+    lat = []
+    for i in range(len(q)):
+        t = time.perf_counter()
+        eng.schedule_one(q[i], pc, seq=i, assume=True)
+        lat.append((time.perf_counter() - t) * 1e6)
+    la = np.array(lat)
+    print("kgpu_schedule_one config %s %d nodes: p50 %.1f us, p99 %.1f us, mean %.1f us"
+          % (args.config, args.nodes, np.percentile(la, 50), np.percentile(la, 99), la.mean()))
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()
