@@ -197,9 +197,10 @@ class Result:
 class GenericScheduler:
     """core/generic_scheduler.go with the determinism contract described above."""
 
-    def __init__(self, fw):
+    def __init__(self, fw, nominator=None):
         self.fw = fw
         self.next_start = 0
+        self.nominator = nominator  # framework.PodNominator (preemption.Nominator), None: no pods nominated
 
     def num_feasible_nodes_to_find(self, n):
         pct = self.fw.profile.percentage_of_nodes_to_score
@@ -237,7 +238,13 @@ class GenericScheduler:
             # seen before it are recorded
             for i in range(len(all_nodes)):
                 ni = all_nodes[(self.next_start + i) % len(all_nodes)]
-                plugin, fst = self.fw.run_filters(state, pod, ni)
+                if self.nominator is not None:
+                    # podPassesFiltersOnNode (generic_scheduler.go:553-615): a second pass with the
+                    # node's nominated pods of equal or higher priority added
+                    from .preemption import pod_passes_filters_on_node
+                    _, plugin, fst = pod_passes_filters_on_node(self.fw, self.nominator, state, pod, ni)
+                else:
+                    plugin, fst = self.fw.run_filters(state, pod, ni)
                 if fst is not None and fst.code == P.ERROR:
                     raise ScheduleError(repr(fst))
                 if fst is None:

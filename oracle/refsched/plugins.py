@@ -741,7 +741,9 @@ class PodTopologySpread:
             if not sel.matches(plabels):
                 continue
             pair = (key, nl[key])
-            s["pairs"][pair] += delta
+            # *s.TpPairToMatchNum[pair] += delta: the reference dereferences a nil entry (panics) for a
+            # pair no eligible node registered; only reachable on a node NodeAffinity rejects -- 0 here
+            s["pairs"][pair] = s["pairs"].get(pair, 0) + delta
             s["paths"][key].update(nl[key], s["pairs"][pair])
 
     def add_pod(self, state, pod, pod_to_add, ni):
@@ -993,6 +995,22 @@ class InterPodAffinity:
         state["PreFilterInterPodAffinity"] = {"existing_anti": existing_anti, "aff": aff, "anti": anti,
                                               "pi": pi}
         return None
+
+    # ---- filtering.go:75-90 updateWithPod, :277-296 AddPod / RemovePod (nominated pods, preemption)
+    def update_with_pod(self, state, updated_pod, node, mult):
+        s = state.get("PreFilterInterPodAffinity")
+        if s is None:
+            return
+        upi = NI.PodInfo(updated_pod)
+        _update_with_anti_affinity_terms(s["existing_anti"], s["pi"].pod, node, upi.req_anti, mult)
+        _update_with_affinity_terms(s["aff"], updated_pod, node, s["pi"].req_aff, mult)
+        _update_with_anti_affinity_terms(s["anti"], updated_pod, node, s["pi"].req_anti, mult)
+
+    def add_pod(self, state, pod, pod_to_add, ni):
+        self.update_with_pod(state, pod_to_add, ni.node, 1)
+
+    def remove_pod(self, state, pod, pod_to_remove, ni):
+        self.update_with_pod(state, pod_to_remove, ni.node, -1)
 
     def filter(self, state, pod, ni):
         if ni.node is None:

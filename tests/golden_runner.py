@@ -135,9 +135,35 @@ def oracle_eval(c):
         pl = P.RequestedToCapacityRatio(None, [], [])
         pl.shape = [tuple(x) for x in c["points"]]
         return {"values": [[p, pl.broken_linear(p)] for p, _ in c["expect_values"]]}
+    if kind in ("preempt_select", "preempt_pick"):
+        return preempt_eval(c)
+    if kind == "preempt_might_help":
+        from oracle.refsched import preemption as PR
+        nodes = [NI.NodeInfo({"metadata": {"name": n}}) for n in c["node_names"]]
+        sts = {n: P.Status(code, "") for n, code in c["statuses"].items()}
+        return {"hosts": sorted(NI.name(ni.node) for ni in PR.nodes_where_preemption_might_help(nodes, sts))}
     if kind == "image_name":
         return {"name": P.normalized_image_name(c["input"])}
     raise KeyError(kind)
+
+
+def preempt_eval(c):
+    """selectNodesForPreemption (+ pickOneNodeForPreemption) over every node of the snapshot, after
+    the preemptor's PreFilter (generic_scheduler_test.go:1625-1646, 1909-1916)."""
+    from oracle.refsched import preemption as PR
+    prof = profile_from_case(c)
+    snap = NI.Snapshot(c["nodes"], c.get("pods", []), order=c.get("order", "given"))
+    fw = F.Framework(prof, F.Handle(snap))
+    state = {}
+    st = fw.run_prefilter(state, c["pod"])
+    if st is not None:
+        return {"error": repr(st)}
+    now = PR.pod_start_time({"status": {"startTime": c["now"]}}, 0)
+    n2v = PR.select_nodes_for_preemption(fw, None, state, c["pod"], snap.list, c.get("pdbs", []), now)
+    out = {"victims": {n: {"pods": sorted(NI.name(p) for p in v), "pdb": nv} for n, (v, nv) in n2v.items()}}
+    pick = PR.pick_one_node_for_preemption(n2v, now)
+    out["hosts"] = [pick] if pick else []
+    return out
 
 
 def replay_node_tree(t, ops, remove_failed):
@@ -242,6 +268,10 @@ def check(c, got):
     if "expect_possible" in c:
         if not set(got["hosts"]) <= set(c["expect_possible"]):
             bad.append(("hosts", c["expect_possible"], got["hosts"]))
+    if "expect_set" in c and sorted(got.get("hosts") or []) != c["expect_set"]:
+        bad.append(("set", c["expect_set"], got.get("hosts")))
+    if "expect_victims" in c and got.get("victims") != c["expect_victims"]:
+        bad.append(("victims", c["expect_victims"], got.get("victims")))
     if "expect_num" in c and got.get("num") != c["expect_num"]:
         bad.append(("num", c["expect_num"], got.get("num")))
     if "expect_state" in c:
