@@ -22,6 +22,10 @@
  *                                   NodeInfo.AddPod / RemovePod (types.go:456-533) by pod UID,
  *                                   NodeInfo.SetNode (types.go:587-600), and the Snapshot.List()
  *                                   rebuild after a node add / remove (cache.go:278-301)
+ *   kgpu_set_nominated              framework.PodNominator (internal/queue/scheduling_queue.go) for the
+ *                                   two-pass filter of podPassesFiltersOnNode (generic_scheduler.go:526-615)
+ *   kgpu_select_victims             selectNodesForPreemption / selectVictimsOnNode /
+ *                                   pickOneNodeForPreemption (generic_scheduler.go:718-1012)
  *   kgpu_comm_*                     node sharding over RCCL/xGMI (no reference counterpart: the
  *                                   reference parallelises over 16 goroutines only,
  *                                   internal/parallelize/parallelism.go:26-43)
@@ -41,7 +45,7 @@
 extern "C" {
 #endif
 
-#define KGPU_ABI_VERSION 1
+#define KGPU_ABI_VERSION 2
 
 /* ---- return codes */
 #define KGPU_OK 0
@@ -243,6 +247,9 @@ typedef struct kgpu_pod_query {
   kgpu_range ipa_pref_anti;
   kgpu_range labels;          /* int32 pool: (pod key id, value id) pairs */
   int64_t limits[2];          /* NodeResourceLimits: milliCPU, memory limits (resource_limits.go:145-156) */
+  int32_t priority;           /* podutil.GetPodPriority (spec.priority, 0 when unset) */
+  int32_t pad1;
+  int64_t uid;                /* caller id of the pod's types.UID (addNominatedPods skips the pod itself) */
 } kgpu_pod_query;
 
 /* Variable-length parts referenced by queries (or by snapshot terms). */
@@ -513,6 +520,63 @@ int kgpu_set_option(kgpu_ctx* ctx, int32_t option, int64_t value);
  * iteration (pods + 1): workgroup 0's {start, evaluated, previous pod resolved, published, end, 0,
  * 0, 0}, then the last workgroup's.  Returns the number of iterations written (<= max_iters). */
 int kgpu_read_phase_trace(kgpu_ctx* ctx, int64_t* out, int32_t max_iters);
+
+/* ---- nominated pods and preemption.
+ *
+ * kgpu_set_nominated replaces the engine's copy of the scheduling queue's nominator
+ * (framework.PodNominator / nominatedPodMap, internal/queue/scheduling_queue.go): pods that preempted
+ * and wait for their victims to leave, by nominated node, in nomination order.  While it is
+ * non-empty every cycle filters a node carrying nominated pods of equal or higher priority (and
+ * another UID) twice, as podPassesFiltersOnNode does (core/generic_scheduler.go:526-615): once with
+ * those pods added to the NodeInfo and to the PodTopologySpread / InterPodAffinity PreFilter state
+ * (their AddPod extensions), once without; the node fits only if both pass.  kgpu_schedule_batch
+ * then runs its pods one cycle at a time and drops each placed pod from the nominator, as
+ * scheduler.assume does (scheduler.go:448).  n = 0 clears it.  `pods` / `pools`: the nominated
+ * pods' records (compiled like queries). */
+typedef struct kgpu_nominated {
+  int32_t node;         /* global node index of NominatedNodeName */
+  int32_t item;         /* index into the pod records */
+} kgpu_nominated;
+int kgpu_set_nominated(kgpu_ctx* ctx, const kgpu_nominated* noms, int32_t n, const kgpu_pod_query* pods,
+                       const kgpu_pools* pools);
+
+/* selectNodesForPreemption + pickOneNodeForPreemption (generic_scheduler.go:718-1012) for a pod
+ * whose cycle ended in a FitError.  The candidate nodes are those whose filter status is not
+ * UnschedulableAndUnresolvable (nodesWherePreemptionMightHelp, :1014-1028); on each, every
+ * potential victim is removed (NodeInfo.RemovePod + the RemovePod extensions), the pod is filtered
+ * (two passes when pods are nominated there), and the victims are reprieved one at a time,
+ * PodDisruptionBudget-violating ones first, each group in MoreImportantPod order
+ * (util/utils.go:76-83).  One device thread per node. */
+typedef struct kgpu_victim {
+  int32_t node;         /* global node index the pod runs on */
+  int32_t slot;         /* its pod-table slot (snapshot pod index, or the slot an assume / ADD_POD gave it) */
+  int32_t item;         /* its record in `pods` (requests and host ports are subtracted as RemovePod does;
+                           priority from the record) */
+  int32_t pad;
+  int64_t start_time;   /* GetPodStartTime in any monotone unit; pods without status.startTime: the caller's now */
+  uint64_t pdb_mask;    /* bit j: PodDisruptionBudget j selects the pod (same namespace, non-empty selector
+                           matching its labels, and the pod has labels: filterPodsWithPDBViolation, :878-919) */
+} kgpu_victim;
+typedef struct kgpu_preempt_args {
+  int32_t n_victims;          /* potential victims over all nodes: pods with priority < the preemptor's, in
+                                 NodeInfo.Pods order per node (ties of MoreImportantPod keep that order) */
+  int32_t n_pdbs;             /* <= 64 */
+  const kgpu_victim* victims;
+  const int32_t* pdb_allowed; /* [n_pdbs] Status.DisruptionsAllowed */
+  const kgpu_pod_query* pods; /* victim records; their pools are the preemptor's `pools` */
+} kgpu_preempt_args;
+typedef struct kgpu_node_victims {
+  int32_t fits;               /* 1: the node is in nodeNameToVictims */
+  int32_t n_victims;          /* victims to evict */
+  int32_t num_pdb_violations;
+  int32_t first;              /* victims_out[first .. first + n_victims): indices into args.victims, in
+                                 Victims.Pods order */
+} kgpu_node_victims;
+/* nodes_out: [n_nodes of this engine]; victims_out: [n_victims]; *chosen: the node
+ * pickOneNodeForPreemption returns (global index, -1: none), ties broken by Snapshot.List() order. */
+int kgpu_select_victims(kgpu_ctx* ctx, const kgpu_pod_query* q, const kgpu_pools* pools,
+                        const kgpu_preempt_args* args, kgpu_node_victims* nodes_out, int32_t* victims_out,
+                        int32_t* chosen);
 
 /* Node sharding across GPUs (one process per GPU).  kgpu_comm_unique_id fills 128 bytes on rank
  * 0; the caller broadcasts them; every rank calls kgpu_comm_init with its shard's snapshot

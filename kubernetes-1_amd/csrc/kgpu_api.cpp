@@ -96,6 +96,25 @@ struct kgpu_ctx {
   std::vector<int32_t> row_canon;                  // [N] first row of the row's node (local index)
   std::unordered_map<int32_t, std::vector<int32_t>> alias_rows;  // canonical row -> all its rows
   bool has_alias = false;
+  // ---- nominator (kgpu_set_nominated): owned copies of the records and of their pools
+  struct Nominator {
+    std::vector<kgpu_nominated> list;
+    std::vector<kgpu_pod_query> recs;
+    std::vector<kgpu_req> reqs;
+    std::vector<int32_t> ints;
+    std::vector<uint64_t> words;
+    std::vector<kgpu_node_term> nterms;
+    std::vector<kgpu_pref_term> pterms;
+    std::vector<kgpu_spread> spreads;
+    std::vector<kgpu_pod_term> pod_terms;
+    std::vector<kgpu_scalar_req> scalars;
+    std::vector<kgpu_port> ports;
+    kgpu_pools pools{};
+  } nom;
+  // preemption / nominated-pass staging (device copies live until the stream is synchronized)
+  DevBuf p_args, p_voff, p_veff, p_noff, p_neff, p_aux, p_vrecs, p_vsc, p_vports, p_nrecs, p_nsc, p_nports,
+      p_vstate, p_order, p_out, p_outv, p_prep, p_nomstat, p_pdb;
+  kgpu::PreemptArgs pa_host{};
   DevBuf flags_buf;                                // DevState::port_overflow
   DevBuf d_stage, d_remap, d_from;
   void* stage_host = nullptr;                      // pinned staging block of a delta launch
@@ -1182,27 +1201,152 @@ int run_tbatch(kgpu_ctx* c, TRun& tr, int first, int count, int64_t first_seq, i
 int copy_to_aliases(kgpu_ctx* c, int32_t* cols, int ncols);
 int assume_via_delta(kgpu_ctx* c, const kgpu_pod_query& q, const kgpu_pools* pools, int32_t gnode);
 
-int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools* pools, int64_t first_seq,
-              kgpu_result* results, kgpu_stats* stats, bool diag, int32_t assume) {
-  if (!c->uploaded) return fail(c, KGPU_E_STATE, "no snapshot uploaded");
-  if (n <= 0) return KGPU_OK;
-  int rc;
-  if (c->has_alias && assume) {
-    // A node listed twice: the device assume updates one row only, so place pods one at a time
-    // and apply NodeInfo.AddPod to every row of the chosen node through k_delta.
-    for (int32_t i = 0; i < n; ++i) {
-      if ((rc = run_batch(c, qs + i, 1, pools, first_seq + i, results + i, stats, diag, 0))) return rc;
-      if (results[i].node >= 0 && (rc = assume_via_delta(c, qs[i], pools, results[i].node))) return rc;
+
+// ---------------------------------------------------------------- nominated pods / preemption (host)
+// labels.Selector.Matches + namespace membership of a pod term held in a query's pools
+// (util/topologies.go:40-49 PodMatchesTermsNamespaceAndSelector).
+bool pool_term_matches(const kgpu_pools* p, const kgpu_pod_term& t, int32_t ns, const int32_t* pairs, int np) {
+  bool in_ns = false;
+  for (int i = 0; i < t.ns.count; ++i) in_ns |= p->ints[t.ns.begin + i] == ns;
+  if (!in_ns || t.sel.kind != KGPU_SEL_AND) return false;
+  for (int i = 0; i < t.sel.reqs.count; ++i) {
+    const kgpu_req& r = p->reqs[t.sel.reqs.begin + i];
+    int v = -1;
+    for (int j = 0; j < np; ++j)
+      if (pairs[2 * j] == r.key) v = pairs[2 * j + 1];
+    if (r.key < 0) v = -1;
+    bool in = false;
+    for (int j = 0; j < r.vals.count; ++j) in |= p->ints[r.vals.begin + j] == v;
+    switch (r.op) {
+      case KGPU_OP_IN: if (!(v >= 0 && in)) return false; break;
+      case KGPU_OP_NOTIN: if (v >= 0 && in) return false; break;
+      case KGPU_OP_EXISTS: if (v < 0) return false; break;
+      case KGPU_OP_DNE: if (v >= 0) return false; break;
+      default: return false;
     }
-    return KGPU_OK;
   }
-  // topology plugins: plans, class columns, pools (kgpu_internal.h "topology plugins")
+  return true;
+}
+
+// A pod added to / removed from a node, resolved against the pod being scheduled `q`
+// (kgpu_internal.h PEff): which of its PreFilter states the AddPod / RemovePod extensions move.
+// exa_keys receives the topology keys of the pod's own required anti-affinity terms that match q.
+kgpu::PEff build_effect(const kgpu_ctx* c, const kgpu::QPlan* pl, int32_t ens, const int32_t* epairs, int enp) {
+  kgpu::PEff e{};
+  if (!pl) return e;
+  for (int i = 0; i < pl->n_hard; ++i)  // updateWithPod counts terminating pods too
+    if (class_matches(c, pl->hard[i].cls, ens, KGPU_PF_ACTIVE, epairs, enp)) e.pts_mask |= 1u << i;
+  for (int i = 0; i < pl->n_anti; ++i)
+    if (class_matches(c, pl->anti[i].cls, ens, KGPU_PF_ACTIVE, epairs, enp)) e.anti_mask |= 1u << i;
+  e.aff_all = (pl->n_aff > 0 && class_matches(c, pl->conj_cls, ens, KGPU_PF_ACTIVE, epairs, enp)) ? 1 : 0;
+  return e;
+}
+
+// Nominated pods of equal or higher priority (and another UID) on this shard's nodes, as pass-1
+// effects for `q`, grouped by local node in nomination order (addNominatedPods, generic_scheduler.go:526-551).
+void stage_nominated(const kgpu_ctx* c, const kgpu_pod_query& q, const kgpu_pools* qp, const kgpu::QPlan* pl,
+                     std::vector<int32_t>& n_off, std::vector<kgpu::PEff>& neff, std::vector<int32_t>& aux) {
+  const int N = c->st.N;
+  std::vector<std::vector<kgpu::PEff>> by(N);
+  const int32_t* qpairs = (qp && q.labels.count) ? qp->ints + q.labels.begin : nullptr;
+  const int qnp = q.labels.count / 2;
+  const kgpu_ctx::Nominator& nm = c->nom;
+  for (const kgpu_nominated& e : nm.list) {
+    const kgpu_pod_query& r = nm.recs[(size_t)e.item];
+    const int local = e.node - c->st.node_base;
+    if (local < 0 || local >= N || r.priority < q.priority || r.uid == q.uid) continue;
+    const int32_t* pairs = r.labels.count ? nm.pools.ints + r.labels.begin : nullptr;
+    kgpu::PEff f = build_effect(c, pl, r.ns, pairs, r.labels.count / 2);
+    f.item = e.item;
+    f.prio = r.priority;
+    f.exa.begin = (int32_t)aux.size();
+    for (int j = 0; j < r.ipa_req_anti.count; ++j) {
+      const kgpu_pod_term& t = nm.pools.pod_terms[r.ipa_req_anti.begin + j];
+      if (t.topo_key >= 0 && pool_term_matches(&nm.pools, t, q.ns, qpairs, qnp)) aux.push_back(t.topo_key);
+    }
+    f.exa.count = (int32_t)aux.size() - f.exa.begin;
+    by[(size_t)local].push_back(f);
+  }
+  n_off.assign((size_t)N + 1, 0);
+  for (int n = 0; n < N; ++n) {
+    n_off[(size_t)n + 1] = n_off[(size_t)n] + (int32_t)by[(size_t)n].size();
+    neff.insert(neff.end(), by[(size_t)n].begin(), by[(size_t)n].end());
+  }
+}
+
+// Upload the effect tables and the PreemptArgs record; returns its device address in *dev.
+struct PreemptStage {
+  std::vector<int32_t> v_off, n_off, aux;
+  std::vector<kgpu::PEff> veff, neff;
+  std::vector<kgpu_pod_query> vrecs;
+};
+int upload_preempt(kgpu_ctx* c, const PreemptStage& ps, const kgpu_pools* vpools, int preempt, int n_pdbs,
+                   const int32_t* pdb_allowed_dev, const kgpu::PreemptArgs** dev) {
+  kgpu::PreemptArgs& a = c->pa_host;
+  a = kgpu::PreemptArgs{};
+  a.pod = 0;
+  a.preempt = preempt;
+  const int N = c->st.N;
+  const size_t nv = std::max<size_t>(ps.veff.size(), 1);
+  int rc;
+  std::vector<int32_t> zero_off((size_t)N + 1, 0);
+  if ((rc = upload_vec(c, c->p_voff, ps.v_off.empty() ? zero_off : ps.v_off, &a.v_off)) ||
+      (rc = upload_vec(c, c->p_noff, ps.n_off.empty() ? zero_off : ps.n_off, &a.n_off)) ||
+      (rc = upload_vec(c, c->p_veff, ps.veff, &a.veff)) || (rc = upload_vec(c, c->p_neff, ps.neff, &a.neff)) ||
+      (rc = upload_vec(c, c->p_aux, ps.aux, &a.aux)) || (rc = upload_vec(c, c->p_vrecs, ps.vrecs, &a.v_recs)) ||
+      (rc = upload_vec(c, c->p_nrecs, c->nom.recs, &a.n_recs)) ||
+      (rc = upload_vec(c, c->p_nsc, c->nom.scalars, &a.n_scalars)) ||
+      (rc = upload_vec(c, c->p_nports, c->nom.ports, &a.n_ports)))
+    return rc;
+  if (vpools) {
+    if ((rc = upload_pool(c, c->p_vsc, vpools->scalars, vpools->n_scalars, &a.v_scalars)) ||
+        (rc = upload_pool(c, c->p_vports, vpools->ports, vpools->n_ports, &a.v_ports)))
+      return rc;
+  }
+  if ((rc = ensure(c, c->p_vstate, nv)) || (rc = ensure(c, c->p_order, sizeof(int32_t) * nv)) ||
+      (rc = ensure(c, c->p_out, sizeof(kgpu_node_victims) * (size_t)std::max(N, 1))) ||
+      (rc = ensure(c, c->p_outv, sizeof(int32_t) * nv)) || (rc = ensure(c, c->p_prep, sizeof(int64_t) * kgpu::kPrepWords)) ||
+      (rc = ensure(c, c->p_nomstat, sizeof(uint32_t) * (size_t)std::max(N, 1))) ||
+      (rc = ensure(c, c->p_args, sizeof(kgpu::PreemptArgs))))
+    return rc;
+  a.vstate = static_cast<uint8_t*>(c->p_vstate.p);
+  a.order = static_cast<int32_t*>(c->p_order.p);
+  a.out = static_cast<kgpu_node_victims*>(c->p_out.p);
+  a.out_victims = static_cast<int32_t*>(c->p_outv.p);
+  a.prep = static_cast<int64_t*>(c->p_prep.p);
+  a.nom_status = static_cast<uint32_t*>(c->p_nomstat.p);
+  a.n_pdbs = n_pdbs;
+  a.pdb_allowed = pdb_allowed_dev;
+  HIP_OK(c, hipMemsetAsync(a.nom_status, 0, sizeof(uint32_t) * (size_t)std::max(N, 1), c->stream));
+  HIP_OK(c, hipMemsetAsync(a.prep, 0xFF, sizeof(int64_t) * kgpu::kPrepWords, c->stream));
+  HIP_OK(c, hipMemcpyAsync(c->p_args.p, &c->pa_host, sizeof(kgpu::PreemptArgs), hipMemcpyHostToDevice, c->stream));
+  *dev = static_cast<const kgpu::PreemptArgs*>(c->p_args.p);
+  return KGPU_OK;
+}
+
+// scheduler.assume drops the assumed pod from the nominator (scheduler.go:448).
+void drop_nominated(kgpu_ctx* c, int64_t uid) {
+  auto& l = c->nom.list;
+  l.erase(std::remove_if(l.begin(), l.end(), [&](const kgpu_nominated& e) { return c->nom.recs[(size_t)e.item].uid == uid; }),
+          l.end());
+}
+
+// Topology plugins of a batch: plans, class columns, pools (kgpu_internal.h "topology plugins").
+struct Staged {
   std::vector<kgpu::QPlan> plans;
   std::vector<int32_t> aux;
   std::vector<kgpu::TTerm> aux_terms;
   int64_t max_scratch = 0;
-  const bool topo_on = topo_profile(c);
-  if (topo_on) {
+  bool topo_on = false;
+};
+int stage_topology(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools* pools, Staged& sg) {
+  std::vector<kgpu::QPlan>& plans = sg.plans;
+  std::vector<int32_t>& aux = sg.aux;
+  std::vector<kgpu::TTerm>& aux_terms = sg.aux_terms;
+  int64_t& max_scratch = sg.max_scratch;
+  int rc;
+  sg.topo_on = topo_profile(c);
+  if (sg.topo_on) {
     kgpu_pools empty{};
     if ((rc = build_plans(c, qs, n, pools ? pools : &empty, plans, aux, aux_terms, &max_scratch))) return rc;
     if ((rc = grow_columns(c, &c->st.mcnt, &c->Ccap, (int)c->classes.size()))) return rc;
@@ -1250,6 +1394,40 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
   } else {
     c->st.plans = nullptr;
   }
+  return KGPU_OK;
+}
+
+int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools* pools, int64_t first_seq,
+              kgpu_result* results, kgpu_stats* stats, bool diag, int32_t assume) {
+  if (!c->uploaded) return fail(c, KGPU_E_STATE, "no snapshot uploaded");
+  if (n <= 0) return KGPU_OK;
+  int rc;
+  if (c->has_alias && assume) {
+    // A node listed twice: the device assume updates one row only, so place pods one at a time
+    // and apply NodeInfo.AddPod to every row of the chosen node through k_delta.
+    for (int32_t i = 0; i < n; ++i) {
+      if ((rc = run_batch(c, qs + i, 1, pools, first_seq + i, results + i, stats, diag, 0))) return rc;
+      if (results[i].node >= 0 && (rc = assume_via_delta(c, qs[i], pools, results[i].node))) return rc;
+      if (results[i].node >= 0) drop_nominated(c, qs[i].uid);
+    }
+    return KGPU_OK;
+  }
+  if (!c->nom.list.empty()) {
+    if (c->comm)
+      return fail(c, KGPU_E_UNSUPPORTED, "nominated pods on a node-sharded engine (the two-pass filter runs unsharded)");
+    if (n > 1) {
+      // the nominator changes as pods are assumed: one cycle at a time
+      for (int32_t i = 0; i < n; ++i)
+        if ((rc = run_batch(c, qs + i, 1, pools, first_seq + i, results + i, stats, diag, assume))) return rc;
+      return KGPU_OK;
+    }
+  }
+  Staged sg;
+  if ((rc = stage_topology(c, qs, n, pools, sg))) return rc;
+  std::vector<kgpu::QPlan>& plans = sg.plans;
+  std::vector<int32_t>& aux = sg.aux;
+  std::vector<kgpu::TTerm>& aux_terms = sg.aux_terms;
+  const bool topo_on = sg.topo_on;
   int64_t batch_ports = 0;
   if (assume)
     for (int32_t i = 0; i < n; ++i) batch_ports += qs[i].ports.count;
@@ -1268,6 +1446,16 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
     HIP_OK(c, hipMemsetAsync(st.diag_raw, 0, sizeof(int64_t) * KGPU_NUM_SCORES * (size_t)st.N, c->stream));
     HIP_OK(c, hipMemsetAsync(st.diag_norm, 0, sizeof(int64_t) * KGPU_NUM_SCORES * (size_t)st.N, c->stream));
   }
+  // nominated pods that apply to this pod: pass 1 runs in k_victims before the filter phase
+  PreemptStage nps;
+  const kgpu::PreemptArgs* nom_dev = nullptr;
+  if (!c->nom.list.empty()) {
+    stage_nominated(c, qs[0], pools, topo_on ? &plans[0] : nullptr, nps.n_off, nps.neff, nps.aux);
+    if (!nps.neff.empty()) {
+      if ((rc = upload_preempt(c, nps, nullptr, 0, 0, nullptr, &nom_dev))) return rc;
+      st.nom_status = c->pa_host.nom_status;
+    }
+  }
   if ((rc = ensure(c, c->dstate, sizeof(DevState)))) return rc;
   c->st_batch = st;
   HIP_OK(c, hipMemcpyAsync(c->dstate.p, &c->st_batch, sizeof(DevState), hipMemcpyHostToDevice, c->stream));
@@ -1284,7 +1472,7 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
   if (cut && sharded)
     return fail(c, KGPU_E_UNSUPPORTED, "percentageOfNodesToScore < 100 on a node-sharded engine (nextStartNodeIndex "
                                        "rotates over the whole cluster): use 100 when sharding");
-  const int kidx = (c->persistent && !diag && !sharded && !cut) ? kgpu::batch_geometry(st.N, std::min(c->max_groups > 0 ? std::min(c->max_groups, c->n_cus) : c->n_cus, 256), &per, &groups) : -1;
+  const int kidx = (c->persistent && !diag && !sharded && !cut && !nom_dev) ? kgpu::batch_geometry(st.N, std::min(c->max_groups > 0 ? std::min(c->max_groups, c->n_cus) : c->n_cus, 256), &per, &groups) : -1;
   std::vector<uint8_t> norm((size_t)n), topo((size_t)n, 0);
   // pods that need the normalize pass or whose scoring fails take the one-launch-per-pod path;
   // pods with topology state take the topology pipeline
@@ -1312,7 +1500,7 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
   HIP_OK(c, hipMemsetAsync(c->abort_buf.p, 0, 64, c->stream));
   int32_t* abort_word = static_cast<int32_t*>(c->abort_buf.p);
   int tper = 0, tgroups = 0;
-  const int tgeo = (topo_on && c->tfast && !diag && !sharded && !cut && st.K <= 64)
+  const int tgeo = (topo_on && c->tfast && !diag && !sharded && !cut && !nom_dev && st.K <= 64)
                        ? kgpu::tbatch_geometry(st.N, std::min(c->max_groups > 0 ? std::min(c->max_groups, c->n_cus) : c->n_cus, 256),
                                                &tper, &tgroups)
                        : -1;
@@ -1409,9 +1597,10 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
         c->bar_base = 0;
       }
       if (kgpu::launch_topo(dst, a, blocks, min_values, next, c->topo_fused,
-                            static_cast<unsigned long long*>(c->gbar.p), c->bar_base, c->cfg.n_filters, c->stream))
+                            static_cast<unsigned long long*>(c->gbar.p), c->bar_base, c->cfg.n_filters, c->stream,
+                            nom_dev, st.N))
         return fail(c, KGPU_E_DEVICE, "topology pipeline launch failed");
-      if (c->topo_fused && !cut) c->bar_base += (unsigned long long)kgpu::topo_barriers(min_values) * (unsigned long long)blocks;
+      if (c->topo_fused && !cut && !nom_dev) c->bar_base += (unsigned long long)kgpu::topo_barriers(min_values) * (unsigned long long)blocks;
       scratch_zeroed_for = next > 0 ? i + 1 : -1;
       if (c->timing) HIP_OK(c, hipEventRecord(get_event(c, ev + 1), c->stream));
       ev += 2;
@@ -1472,6 +1661,8 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
         a.cut = cut ? 1 : 0;
         a.seq = first_seq + k;
         if (c->timing) HIP_OK(c, hipEventRecord(get_event(c, ev), c->stream));
+        if (nom_dev && kgpu::launch_victims(dst, nom_dev, st.N, c->stream))
+          return fail(c, KGPU_E_DEVICE, "k_victims launch failed");
         if (kgpu::launch_eval(dst, a, blocks, c->spec, c->stream))
           return fail(c, KGPU_E_DEVICE, "k_eval launch failed");
         if (cut && kgpu::launch_cut(dst, a, blocks, c->cfg.n_filters, c->stream))
@@ -1535,6 +1726,9 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
       stats->eval_launches += timed_passes;
     }
   }
+  if (assume && !c->nom.list.empty())
+    for (int32_t i = 0; i < n; ++i)
+      if (results[i].node >= 0) drop_nominated(c, qs[i].uid);
   // keep host records of assumed pods for ForgetPod (and the pod table for later classes)
   if (assume) {
     for (int32_t i = 0; i < n; ++i) {
@@ -2165,7 +2359,9 @@ int kgpu_struct_sizes(int32_t* out, int32_t n) {
                        (int32_t)sizeof(kgpu_snapshot),  (int32_t)sizeof(kgpu_result),
                        (int32_t)sizeof(kgpu_stats),     (int32_t)sizeof(kgpu_delta),
                        (int32_t)sizeof(kgpu_node_row),  (int32_t)sizeof(kgpu_delta_batch),
-                       (int32_t)sizeof(kgpu_shape_point)};
+                       (int32_t)sizeof(kgpu_shape_point), (int32_t)sizeof(kgpu_nominated),
+                       (int32_t)sizeof(kgpu_victim),    (int32_t)sizeof(kgpu_preempt_args),
+                       (int32_t)sizeof(kgpu_node_victims)};
   const int32_t m = (int32_t)(sizeof(s) / sizeof(s[0]));
   for (int32_t i = 0; i < n && i < m; ++i) out[i] = s[i];
   return m;
@@ -2263,7 +2459,10 @@ int kgpu_destroy(kgpu_ctx* c) {
                     &c->d_citems, &c->d_tclasses, &c->d_creqs, &c->d_cints, &c->d_plans, &c->d_aux,
                     &c->d_aux_terms, &c->scratch, &c->d_pods, &c->gbar, &c->cut_buf, &c->t_plans, &c->t_aux,
                     &c->t_looks, &c->t_tabs, &c->t_deltas, &c->t_hists, &c->t_sigs, &c->t_regs, &c->t_zero,
-                    &c->abort_buf, &c->t_plan_of, &c->flags_buf, &c->d_stage, &c->d_remap, &c->d_from})
+                    &c->abort_buf, &c->t_plan_of, &c->flags_buf, &c->d_stage, &c->d_remap, &c->d_from,
+                    &c->p_args, &c->p_voff, &c->p_veff, &c->p_noff, &c->p_neff, &c->p_aux, &c->p_vrecs,
+                    &c->p_vsc, &c->p_vports, &c->p_nrecs, &c->p_nsc, &c->p_nports, &c->p_vstate, &c->p_order,
+                    &c->p_out, &c->p_outv, &c->p_prep, &c->p_nomstat, &c->p_pdb})
     if (b->p) (void)hipFree(b->p);
   if (c->pref_x.p) (void)hipFree(c->pref_x.p);
   if (c->stage_host) (void)hipHostFree(c->stage_host);
@@ -2430,6 +2629,8 @@ int kgpu_upload_snapshot(kgpu_ctx* c, const kgpu_snapshot* s, int64_t generation
     const kgpu_term& tm = s->terms[t];
     const int tc = intern_tclass(c, tm.kind, tm.t.weight, tm.t.topo_key, term_item(tm.t, &s->pools));
     if (tm.pod < 0 || tm.pod >= s->n_pods || !(s->pod_flags[tm.pod] & KGPU_PF_ACTIVE)) continue;
+    // the owner's PodInfo terms: what RemovePod / a preemption removal takes back out of tcnt
+    c->pod_rows[(size_t)tm.pod].own_tcls.push_back(tc);
     const int ln = s->pod_node[tm.pod] - st.node_base;
     if (ln >= 0 && ln < st.N) term_cells.emplace_back(tc, ln);
   }
@@ -2469,6 +2670,221 @@ int kgpu_schedule_one(kgpu_ctx* c, const kgpu_pod_query* q, const kgpu_pools* po
   int rc = run_batch(c, q, 1, pools, pod_seq, res, nullptr, true, assume);
   if (rc) return rc;
   if (assumed_slot) *assumed_slot = c->recs.size() > before ? (int32_t)c->recs.size() - 1 : -1;
+  return KGPU_OK;
+}
+
+int kgpu_set_nominated(kgpu_ctx* c, const kgpu_nominated* noms, int32_t n, const kgpu_pod_query* pods,
+                       const kgpu_pools* pools) {
+  if (!c || n < 0 || (n > 0 && (!noms || !pods))) return KGPU_E_INVAL;
+  kgpu_ctx::Nominator nm;
+  int32_t n_items = 0;
+  for (int32_t i = 0; i < n; ++i) {
+    if (noms[i].item < 0) return fail(c, KGPU_E_INVAL, "kgpu_set_nominated: negative record index");
+    if (noms[i].node < 0 || noms[i].node >= std::max(c->st.n_total, c->st.N))
+      return fail(c, KGPU_E_INVAL, "kgpu_set_nominated: node index out of range");
+    n_items = std::max(n_items, noms[i].item + 1);
+  }
+  nm.list.assign(noms, noms + n);
+  nm.recs.assign(pods, pods + n_items);
+  if (pools) {  // owned copies: the records' ranges stay valid after the call
+    auto cp = [](auto& v, const auto* src, int32_t cnt) {
+      if (src && cnt > 0) v.assign(src, src + cnt);
+    };
+    cp(nm.reqs, pools->reqs, pools->n_reqs);
+    cp(nm.ints, pools->ints, pools->n_ints);
+    cp(nm.words, pools->words, pools->n_words);
+    cp(nm.nterms, pools->node_terms, pools->n_node_terms);
+    cp(nm.pterms, pools->pref_terms, pools->n_pref_terms);
+    cp(nm.spreads, pools->spreads, pools->n_spreads);
+    cp(nm.pod_terms, pools->pod_terms, pools->n_pod_terms);
+    cp(nm.scalars, pools->scalars, pools->n_scalars);
+    cp(nm.ports, pools->ports, pools->n_ports);
+  }
+  c->nom = std::move(nm);
+  kgpu_pools& v = c->nom.pools;
+  v = kgpu_pools{};
+  v.reqs = c->nom.reqs.data(); v.n_reqs = (int32_t)c->nom.reqs.size();
+  v.ints = c->nom.ints.data(); v.n_ints = (int32_t)c->nom.ints.size();
+  v.words = c->nom.words.data(); v.n_words = (int32_t)c->nom.words.size();
+  v.node_terms = c->nom.nterms.data(); v.n_node_terms = (int32_t)c->nom.nterms.size();
+  v.pref_terms = c->nom.pterms.data(); v.n_pref_terms = (int32_t)c->nom.pterms.size();
+  v.spreads = c->nom.spreads.data(); v.n_spreads = (int32_t)c->nom.spreads.size();
+  v.pod_terms = c->nom.pod_terms.data(); v.n_pod_terms = (int32_t)c->nom.pod_terms.size();
+  v.scalars = c->nom.scalars.data(); v.n_scalars = (int32_t)c->nom.scalars.size();
+  v.ports = c->nom.ports.data(); v.n_ports = (int32_t)c->nom.ports.size();
+  return KGPU_OK;
+}
+
+// pickOneNodeForPreemption (generic_scheduler.go:718-843) over the nodes that fit, walked in
+// Snapshot.List() order (the reference walks a map: any of the tied nodes).
+static int32_t pick_one_node(const std::vector<int32_t>& cand, const kgpu_node_victims* out, const int32_t* vout,
+                             const kgpu_preempt_args* a, const int32_t* prio) {
+  if (cand.empty()) return -1;
+  auto pods = [&](int32_t n) { return out[n].n_victims; };
+  auto vict = [&](int32_t n, int k) { return vout[out[n].first + k]; };
+  for (int32_t n : cand)
+    if (pods(n) == 0) return n;
+  auto narrow = [&](const std::vector<int32_t>& in, auto key) {  // nodes with the minimum key
+    std::vector<int32_t> o;
+    int64_t best = INT64_MAX;
+    for (int32_t n : in) {
+      const int64_t k = key(n);
+      if (k < best) {
+        best = k;
+        o.clear();
+      }
+      if (k == best) o.push_back(n);
+    }
+    return o;
+  };
+  std::vector<int32_t> m = narrow(cand, [&](int32_t n) { return (int64_t)out[n].num_pdb_violations; });
+  if (m.size() == 1) return m[0];
+  m = narrow(m, [&](int32_t n) { return (int64_t)prio[vict(n, 0)]; });  // Victims.Pods[0]: the highest
+  if (m.size() == 1) return m[0];
+  m = narrow(m, [&](int32_t n) {
+    int64_t sum = 0;
+    for (int k = 0; k < pods(n); ++k) sum += (int64_t)prio[vict(n, k)] + (int64_t)2147483647 + 1;
+    return sum;
+  });
+  if (m.size() == 1) return m[0];
+  m = narrow(m, [&](int32_t n) { return (int64_t)pods(n); });
+  if (m.size() == 1) return m[0];
+  // latest earliest start time among each node's highest-priority victims (util.GetEarliestPodStartTime)
+  auto earliest = [&](int32_t n) {
+    int32_t v0 = vict(n, 0);
+    int64_t t = a->victims[v0].start_time;
+    int32_t mp = prio[v0];
+    for (int k = 0; k < pods(n); ++k) {
+      const int32_t v = vict(n, k);
+      if (prio[v] == mp) {
+        if (a->victims[v].start_time < t) t = a->victims[v].start_time;
+      } else if (prio[v] > mp) {
+        mp = prio[v];
+        t = a->victims[v].start_time;
+      }
+    }
+    return t;
+  };
+  int32_t ret = m[0];
+  int64_t latest = earliest(m[0]);
+  for (size_t i = 1; i < m.size(); ++i) {
+    const int64_t t = earliest(m[i]);
+    if (t > latest) {
+      latest = t;
+      ret = m[i];
+    }
+  }
+  return ret;
+}
+
+int kgpu_select_victims(kgpu_ctx* c, const kgpu_pod_query* q, const kgpu_pools* pools, const kgpu_preempt_args* args,
+                        kgpu_node_victims* nodes_out, int32_t* victims_out, int32_t* chosen) {
+  if (!c || !q || !args || !nodes_out || (args->n_victims > 0 && (!args->victims || !args->pods || !victims_out)))
+    return KGPU_E_INVAL;
+  if (args->n_victims < 0 || args->n_pdbs < 0 || (args->n_pdbs > 0 && !args->pdb_allowed)) return KGPU_E_INVAL;
+  if (args->n_pdbs > 64) return fail(c, KGPU_E_CAPACITY, "more than 64 PodDisruptionBudgets");
+  if (hipSetDevice(c->device) != hipSuccess) return KGPU_E_DEVICE;
+  if (!c->uploaded) return fail(c, KGPU_E_STATE, "no snapshot uploaded");
+  if (c->comm) return fail(c, KGPU_E_UNSUPPORTED, "preemption on a node-sharded engine");
+  const int N = c->st.N;
+  int rc;
+  Staged sg;
+  if ((rc = stage_topology(c, q, 1, pools, sg))) return rc;
+  const kgpu::QPlan* pl = sg.topo_on ? &sg.plans[0] : nullptr;
+  if ((rc = upload_pools(c, pools))) return rc;
+  if ((rc = ensure(c, c->queries, sizeof(kgpu_pod_query)))) return rc;
+  HIP_OK(c, hipMemcpyAsync(c->queries.p, q, sizeof(kgpu_pod_query), hipMemcpyHostToDevice, c->stream));
+  DevState st = c->st;
+  st.queries = static_cast<const kgpu_pod_query*>(c->queries.p);
+  st.diag_raw = nullptr;
+  st.diag_norm = nullptr;
+  // potential victims per local node, MoreImportantPod order (stable over the caller's order)
+  PreemptStage ps;
+  std::vector<int32_t> pos_of;  // sorted position -> caller's victim index
+  std::vector<std::vector<int32_t>> by((size_t)N);
+  for (int32_t i = 0; i < args->n_victims; ++i) {
+    const kgpu_victim& v = args->victims[i];
+    const int local = v.node - c->st.node_base;
+    if (local < 0 || local >= N) return fail(c, KGPU_E_INVAL, "kgpu_select_victims: victim node out of range");
+    if (v.slot < 0 || v.slot >= (int32_t)c->pod_rows.size() || v.item < 0)
+      return fail(c, KGPU_E_INVAL, "kgpu_select_victims: bad victim slot or record");
+    if (args->pods[v.item].priority >= q->priority) continue;  // not a potential victim
+    by[(size_t)local].push_back(i);
+  }
+  const int32_t* qpairs = (pools && q->labels.count) ? pools->ints + q->labels.begin : nullptr;
+  const int qnp = q->labels.count / 2;
+  ps.v_off.assign((size_t)N + 1, 0);
+  for (int n = 0; n < N; ++n) {
+    std::vector<int32_t>& l = by[(size_t)n];
+    std::stable_sort(l.begin(), l.end(), [&](int32_t x, int32_t y) {
+      const int32_t px = args->pods[args->victims[x].item].priority, py = args->pods[args->victims[y].item].priority;
+      if (px != py) return px > py;
+      return args->victims[x].start_time < args->victims[y].start_time;
+    });
+    for (int32_t i : l) {
+      const kgpu_victim& v = args->victims[i];
+      const kgpu_ctx::PodRow& row = c->pod_rows[(size_t)v.slot];
+      kgpu::PEff f = build_effect(c, pl, row.ns, row.pairs.empty() ? nullptr : row.pairs.data(), (int)row.pairs.size() / 2);
+      f.item = (int32_t)ps.vrecs.size();
+      ps.vrecs.push_back(args->pods[v.item]);
+      f.prio = args->pods[v.item].priority;
+      f.start = v.start_time;
+      f.pdb_mask = args->n_pdbs >= 64 ? v.pdb_mask : (v.pdb_mask & ((1ull << args->n_pdbs) - 1));
+      f.exa.begin = (int32_t)ps.aux.size();
+      for (int32_t t : row.own_tcls) {
+        const kgpu::TermClassRec& tc = c->tclasses[(size_t)t];
+        if (tc.kind == KGPU_TERM_REQ_ANTI && tc.topo_key >= 0 && item_matches(c, tc.item, q->ns, qpairs, qnp))
+          ps.aux.push_back(tc.topo_key);
+      }
+      f.exa.count = (int32_t)ps.aux.size() - f.exa.begin;
+      ps.veff.push_back(f);
+      pos_of.push_back(i);
+    }
+    ps.v_off[(size_t)n + 1] = (int32_t)ps.veff.size();
+  }
+  stage_nominated(c, *q, pools, pl, ps.n_off, ps.neff, ps.aux);
+  const kgpu::PreemptArgs* dev = nullptr;
+  const int32_t* d_pdb = nullptr;
+  if ((rc = upload_pool(c, c->p_pdb, args->pdb_allowed, args->n_pdbs, &d_pdb)) ||
+      (rc = upload_preempt(c, ps, pools, 1, args->n_pdbs, d_pdb, &dev)))
+    return rc;
+  if ((rc = ensure(c, c->dstate, sizeof(DevState)))) return rc;
+  c->st_batch = st;
+  HIP_OK(c, hipMemcpyAsync(c->dstate.p, &c->st_batch, sizeof(DevState), hipMemcpyHostToDevice, c->stream));
+  const DevState* dst = static_cast<const DevState*>(c->dstate.p);
+  if (pl && pl->topo) {  // the preemptor's PreFilter state: TpPairToMatchNum / criticalPaths / IPA maps
+    HIP_OK(c, hipMemsetAsync(c->st.scratch, 0, sizeof(int64_t) * (size_t)pl->scratch_len, c->stream));
+    PodArgs a{};
+    a.pod = 0;
+    a.prev = -1;
+    int64_t min_values = 0;
+    for (int k = 0; k < pl->n_hard; ++k)
+      if (pl->hard[k].key >= 0) min_values = std::max<int64_t>(min_values, c->key_n_values[pl->hard[k].key]);
+    const int blocks = kgpu::eval_blocks(N);
+    if (kgpu::launch_topo_phase(dst, a, 0, blocks, 0, c->stream) ||
+        (min_values > 0 && kgpu::launch_topo_phase(dst, a, 1, blocks, min_values, c->stream)) ||
+        kgpu::launch_vict_prep(dst, dev, c->stream))
+      return fail(c, KGPU_E_DEVICE, "preemption PreFilter launch failed");
+  }
+  if (kgpu::launch_victims(dst, dev, N, c->stream)) return fail(c, KGPU_E_DEVICE, "k_victims launch failed");
+  std::vector<int32_t> vout(std::max<size_t>(ps.veff.size(), 1));
+  HIP_OK(c, hipMemcpyAsync(nodes_out, c->pa_host.out, sizeof(kgpu_node_victims) * (size_t)N, hipMemcpyDeviceToHost,
+                           c->stream));
+  if (!ps.veff.empty())
+    HIP_OK(c, hipMemcpyAsync(vout.data(), c->pa_host.out_victims, sizeof(int32_t) * ps.veff.size(),
+                             hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(c, hipStreamSynchronize(c->stream));
+  // sorted positions -> the caller's victim indices; pick the node
+  std::vector<int32_t> prio(std::max<int32_t>(args->n_victims, 1));
+  for (int32_t i = 0; i < args->n_victims; ++i) prio[(size_t)i] = args->pods[args->victims[i].item].priority;
+  std::vector<int32_t> cand;
+  for (int n = 0; n < N; ++n) {
+    kgpu_node_victims& o = nodes_out[n];
+    for (int k = 0; k < o.n_victims; ++k) victims_out[o.first + k] = pos_of[(size_t)vout[(size_t)(o.first + k)]];
+    if (o.fits) cand.push_back(n);
+  }
+  const int32_t pick = pick_one_node(cand, nodes_out, victims_out, args, prio.data());
+  if (chosen) *chosen = pick >= 0 ? pick + c->st.node_base : -1;
   return KGPU_OK;
 }
 

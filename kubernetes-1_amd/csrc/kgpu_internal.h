@@ -213,6 +213,10 @@ struct DevState {
   int32_t to_find;
   int32_t* cut_state;
   int32_t* port_overflow;               // set by assume / delta when a node's host-port slots run out
+  // ---- nominated pods (kgpu_set_nominated): pass-1 status word per node (0: pass 1 succeeded or the
+  // node has no nominated pods); k_eval / k_topo_filter report it instead of their own verdict.
+  // Null when the nominator is empty.
+  const uint32_t* nom_status;
 };
 // Filter status word of a node the cycle never examined (findNodesThatPassFilters stopped before
 // it), or of the feasible node whose discovery cancelled the search: not in `filtered` and not in
@@ -372,6 +376,51 @@ struct TBatchArgs {
                           // stats published, stats resolved, key published, winner resolved, end
 };
 
+// ---------------------------------------------------------------- nominated pods / preemption
+// One pod added to (nominated, pass 1) or removed from (potential victim) a node, resolved against
+// the pod being scheduled on the host (kgpu_api.cpp build_effect).  Its requests and host ports
+// come from its record (PreemptArgs::v_recs / n_recs [item]).
+struct PEff {
+  int32_t item;
+  uint32_t pts_mask;   // bit i: PodTopologySpread updateWithPod counts it for DoNotSchedule constraint i
+                       // (same namespace, selector matches; filtering.go:123-143)
+  uint32_t anti_mask;  // bit i: matches the pod's required anti-affinity term i (filtering.go:133-148)
+  int32_t aff_all;     // matches all of the pod's required affinity terms (filtering.go:115-129)
+  kgpu_range exa;      // aux ints: topology keys of its own required anti-affinity terms that match the pod
+  int32_t prio;
+  int32_t pad;
+  int64_t start;
+  uint64_t pdb_mask;
+};
+struct PreemptArgs {
+  int32_t pod;              // query index of the pod being scheduled
+  int32_t preempt;          // 1: selectVictimsOnNode, 0: nominated pass 1 only (writes nom_status)
+  const int32_t* v_off;     // [N+1] victims of local node n: veff[v_off[n] .. v_off[n+1]), MoreImportantPod order
+  const PEff* veff;
+  const int32_t* n_off;     // [N+1] nominated pods added in pass 1 (priority >= the pod's, other UID)
+  const PEff* neff;
+  const kgpu_pod_query* v_recs;   // victim records and their pools (kgpu_preempt_args::pods)
+  const kgpu_scalar_req* v_scalars;
+  const kgpu_port* v_ports;
+  const kgpu_pod_query* n_recs;   // nominated pod records and their pools (kgpu_set_nominated)
+  const kgpu_scalar_req* n_scalars;
+  const kgpu_port* n_ports;
+  const int32_t* aux;
+  int32_t n_pdbs;
+  int32_t pad;
+  const int32_t* pdb_allowed;
+  uint8_t* vstate;          // [victims] 0 removed, 1 kept, 2 evicted
+  int32_t* order;           // [victims] reprieve order (positions), per node range
+  kgpu_node_victims* out;   // [N]
+  int32_t* out_victims;     // [victims]
+  int64_t* prep;            // k_vict_prep: per DoNotSchedule constraint {min, argmin, second min}, then the
+                            // number of non-zero affinity-map entries (len(topologyToMatchedAffinityTerms))
+  uint32_t* nom_status;     // [N] pass-1 status words (nominated pass)
+};
+constexpr int kPrepWords = 3 * kMaxSpread + 1;
+int launch_vict_prep(const DevState* st, const PreemptArgs* a, void* stream);
+int launch_victims(const DevState* st, const PreemptArgs* a, int N, void* stream);
+
 // Host-side launchers (kgpu_kernels.hip).
 // The DevState lives in device memory (one copy per batch): kernel arguments stay at 40 bytes,
 // so no launch pulls a kilobyte of kernarg segment through the host-coherent path.
@@ -402,7 +451,8 @@ int launch_batch(const DevState* st, const BatchArgs& a, int groups, int kidx, i
 // bar: the fused kernel's grid-barrier counter (grows monotonically); bar_base: its value before
 // this launch.  A fused launch adds topo_barriers(min_values) * blocks arrivals.
 int launch_topo(const DevState* st, PodArgs a, int blocks, int64_t min_values, int64_t next_scratch,
-                bool fused, unsigned long long* bar, unsigned long long bar_base, int n_filters, void* stream);
+                bool fused, unsigned long long* bar, unsigned long long bar_base, int n_filters, void* stream,
+                const PreemptArgs* nom = nullptr, int N = 0);
 inline int topo_barriers(int64_t min_values) { return min_values > 0 ? 5 : 4; }
 // Initialize mcnt columns [c0, c0 + nc) from the pod table (n_pods rows).
 int launch_class_init(const DevState* st, int c0, int nc, int n_pods, void* stream);

@@ -808,7 +808,10 @@ __global__ __launch_bounds__(kBlock) void k_eval(const DevState* __restrict__ st
       assume_counts(st, a.prev, n);
     }
     NodeEval e{0, 0, 0, 0};
-    e.status = run_filters<FM>(st, q, r, n);
+    // nominated pods: a failed first pass (k_victims, nominated mode) is the node's verdict
+    // (podPassesFiltersOnNode, generic_scheduler.go:578-612)
+    const uint32_t s1 = st.nom_status ? gp(st.nom_status)[n] : 0u;
+    e.status = s1 ? s1 : run_filters<FM>(st, q, r, n);
     if (e.status == 0) {
       run_scores<SM>(st, q, r, n, e, a.diag);
       ++feas;
@@ -1608,7 +1611,8 @@ __device__ __forceinline__ void topo_filter(const DevState* __restrict__ stp, Po
   for (int n = lo + threadIdx.x; n < hi; n += kBlock) {
     NodeRes r = load_res(st, n);
     NodeEval e{0, 0, 0, 0};
-    e.status = run_filters<kRuntime>(st, q, r, n, plp);
+    const uint32_t s1 = st.nom_status ? gp(st.nom_status)[n] : 0u;
+    e.status = s1 ? s1 : run_filters<kRuntime>(st, q, r, n, plp);
     if (e.status == 0) {
       int64_t part = 0;
       for (int i = 0; i < st.n_scores; ++i) {
@@ -1939,10 +1943,14 @@ __global__ void k_class_init(const DevState* __restrict__ stp, int c0, int nc, i
   }
 }
 
+__global__ void k_vict_prep(const DevState* __restrict__ stp, const PreemptArgs* __restrict__ ap);
+__global__ void k_victims(const DevState* __restrict__ stp, const PreemptArgs* __restrict__ ap);
+
 int launch_topo(const DevState* st, PodArgs a, int blocks, int64_t min_values, int64_t next_scratch,
-                bool fused, unsigned long long* bar, unsigned long long bar_base, int n_filters, void* stream) {
+                bool fused, unsigned long long* bar, unsigned long long bar_base, int n_filters, void* stream,
+                const PreemptArgs* nom, int N) {
   hipStream_t s = (hipStream_t)stream;
-  if (fused && !a.cut) {
+  if (fused && !a.cut && !nom) {
     int do_min = min_values > 0 ? 1 : 0;
     void* args[] = {(void*)&st, (void*)&a, (void*)&do_min, (void*)&next_scratch, (void*)&bar, (void*)&bar_base};
     return hipLaunchCooperativeKernel((const void*)k_topo_fused, dim3(blocks), dim3(kBlock), args, 0, s) == hipSuccess
@@ -1953,6 +1961,10 @@ int launch_topo(const DevState* st, PodArgs a, int blocks, int64_t min_values, i
     int64_t mb = (min_values + kBlock - 1) / kBlock;
     if (mb > kMaxBlocks) mb = kMaxBlocks;
     hipLaunchKernelGGL(k_topo_min, dim3((int)mb), dim3(kBlock), 0, s, st, a);
+  }
+  if (nom) {  // nominated pods: pass 1 on the PreFilter histograms, before the filter phase reads it
+    hipLaunchKernelGGL(k_vict_prep, dim3(kMaxSpread + 1), dim3(256), 0, s, st, nom);
+    hipLaunchKernelGGL(k_victims, dim3((N + 63) / 64), dim3(64), 0, s, st, nom);
   }
   hipLaunchKernelGGL(k_topo_filter, dim3(blocks), dim3(kBlock), 0, s, st, a);
   if (a.cut) {
@@ -2968,6 +2980,486 @@ int launch_remap(const RemapCol* cols, int n_cols, const int32_t* from, int old_
   if (n_cols <= 0 || new_n <= 0) return 0;
   const int blocks = (new_n + 255) / 256 < 1024 ? (new_n + 255) / 256 : 1024;
   hipLaunchKernelGGL(k_remap, dim3(blocks, n_cols), dim3(256), 0, (hipStream_t)stream, cols, from, old_n, new_n);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// ---------------------------------------------------------------- nominated pods / preemption
+// (kgpu_internal.h "nominated pods / preemption").  Reference semantics:
+//   addNominatedPods / podPassesFiltersOnNode   core/generic_scheduler.go:526-615
+//   selectVictimsOnNode                         core/generic_scheduler.go:921-1012
+//   filterPodsWithPDBViolation                  core/generic_scheduler.go:878-919
+//   PodTopologySpread AddPod / RemovePod        podtopologyspread/filtering.go:93-180 (criticalPaths)
+//   InterPodAffinity AddPod / RemovePod         interpodaffinity/filtering.go:75-148, 277-296
+// One thread per node re-runs the profile's filters on a private, delta-adjusted view of its own
+// node: every pod added or removed by these paths sits on that node, so each plugin's state moves
+// only at the node's own topology pairs.  NodeInfo.Requested / len(Pods) / UsedPorts are the node's
+// row plus the deltas; TpPairToMatchNum and the three inter-pod affinity maps are the PreFilter
+// histograms (k_topo_pre) plus the deltas at the node's pairs; criticalPaths[0] after any sequence of
+// updates to one pair equals min(minimum over the key's other registered pairs, the pair's count)
+// (k_vict_prep supplies the minimum and the runner-up).
+enum { kVRemoved = 0, kVKept = 1, kVEvicted = 2, kVViolating = 4 };
+
+struct VCtx {
+  const DevState* st;
+  const PreemptArgs* a;
+  const kgpu_pod_query* q;
+  const QPlan* pl;     // null: no topology state (PodTopologySpread / InterPodAffinity pass)
+  int n;               // local node
+  int v0, v1, m0, m1;  // victim / nominated ranges
+  bool removal;        // the potential victims were removed (selectVictimsOnNode, first step done)
+  bool pass1;          // nominated pods added
+  int trial;           // victim being reprieved (-1 none)
+  int step;            // reprieve steps processed before the trial (a->order[v0 .. v0 + step))
+};
+
+// sign of an effect in the current view: victims -1 while removed, nominated pods +1 in pass 1
+__device__ __forceinline__ int v_sign(const VCtx& c, int v) {
+  return (c.removal && (c.a->vstate[v] & 3) != kVKept) ? -1 : 0;
+}
+
+__device__ __forceinline__ bool port_eq(const kgpu_port& x, const kgpu_port& y) {
+  return x.ip == y.ip && x.proto == y.proto && x.port == y.port;
+}
+__device__ __forceinline__ bool port_conflicts(const kgpu_port& e, const kgpu_port& w) {
+  return e.port == w.port && e.proto == w.proto && (w.ip == 0 || e.ip == 0 || e.ip == w.ip);
+}
+__device__ __forceinline__ bool rec_has_port(const kgpu_pod_query& r, const kgpu_port* pool, const kgpu_port& e) {
+  for (int i = 0; i < r.ports.count; ++i)
+    if (port_eq(pool[r.ports.begin + i], e)) return true;
+  return false;
+}
+__device__ __forceinline__ const kgpu_pod_query& vrec(const VCtx& c, int v) { return c.a->v_recs[c.a->veff[v].item]; }
+__device__ __forceinline__ const kgpu_pod_query& nrec(const VCtx& c, int m) { return c.a->n_recs[c.a->neff[m].item]; }
+
+// HostPortInfo membership of entry e on the adjusted node (types.go:726-756 set semantics): the
+// last Add / Remove touching it wins -- removals of every potential victim, then the reprieve
+// sequence (a kept pod re-adds its ports, an evicted one adds and removes them), then the trial
+// pod and (pass 1) the nominated pods.
+__device__ bool port_present(const VCtx& c, const kgpu_port& e) {
+  const DevState& st = *c.st;
+  if (c.pass1)
+    for (int m = c.m0; m < c.m1; ++m)
+      if (rec_has_port(nrec(c, m), c.a->n_ports, e)) return true;
+  if (c.removal) {
+    if (c.trial >= 0 && rec_has_port(vrec(c, c.trial), c.a->v_ports, e)) return true;
+    for (int k = c.step - 1; k >= 0; --k) {
+      const int v = c.a->order[c.v0 + k];
+      if (rec_has_port(vrec(c, v), c.a->v_ports, e)) return (c.a->vstate[v] & 3) == kVKept;
+    }
+    for (int v = c.v0; v < c.v1; ++v)
+      if (rec_has_port(vrec(c, v), c.a->v_ports, e)) return false;
+  }
+  const int have = gp(st.port_count)[c.n];
+  for (int s = 0; s < have; ++s)
+    if (port_eq(gp(st.ports)[(size_t)s * st.N + c.n], e)) return true;
+  return false;
+}
+
+__device__ bool ports_conflict_adj(const VCtx& c) {
+  const DevState& st = *c.st;
+  const kgpu_pod_query& q = *c.q;
+  for (int i = 0; i < q.ports.count; ++i) {
+    const kgpu_port w = st.qp.ports[q.ports.begin + i];
+    const int have = gp(st.port_count)[c.n];
+    for (int s = 0; s < have; ++s) {
+      const kgpu_port e = gp(st.ports)[(size_t)s * st.N + c.n];
+      if (port_conflicts(e, w) && port_present(c, e)) return true;
+    }
+    for (int v = c.v0; v < c.v1; ++v) {
+      const kgpu_pod_query& r = vrec(c, v);
+      for (int j = 0; j < r.ports.count; ++j) {
+        const kgpu_port e = c.a->v_ports[r.ports.begin + j];
+        if (port_conflicts(e, w) && port_present(c, e)) return true;
+      }
+    }
+    if (c.pass1)
+      for (int m = c.m0; m < c.m1; ++m) {
+        const kgpu_pod_query& r = nrec(c, m);
+        for (int j = 0; j < r.ports.count; ++j) {
+          const kgpu_port e = c.a->n_ports[r.ports.begin + j];
+          if (port_conflicts(e, w) && port_present(c, e)) return true;
+        }
+      }
+  }
+  return false;
+}
+
+// NodeResourcesFit on the adjusted NodeInfo (fit.go:194-267): Requested and len(Pods) move by the
+// added / removed pods' requests (NodeInfo.AddPod / RemovePod, types.go:456-533).
+__device__ uint32_t fit_adj(const VCtx& c) {
+  const DevState& st = *c.st;
+  const kgpu_pod_query& q = *c.q;
+  NodeRes r = load_res(st, c.n);
+  for (int v = c.v0; v < c.v1; ++v) {
+    const int sg = v_sign(c, v);
+    if (!sg) continue;
+    const kgpu_pod_query& p = vrec(c, v);
+    r.rc += sg * p.req[0]; r.rm += sg * p.req[1]; r.re += sg * p.req[2]; r.np += sg;
+  }
+  if (c.pass1)
+    for (int m = c.m0; m < c.m1; ++m) {
+      const kgpu_pod_query& p = nrec(c, m);
+      r.rc += p.req[0]; r.rm += p.req[1]; r.re += p.req[2]; r.np += 1;
+    }
+  uint32_t d = 0;
+  if (r.np + 1 > r.ap) d |= 1u;
+  if (!(q.flags & KGPU_Q_FIT_ALL_ZERO)) {
+    if (r.ac < q.req[0] + r.rc) d |= 2u;
+    if (r.am < q.req[1] + r.rm) d |= 4u;
+    if (r.ae < q.req[2] + r.re) d |= 8u;
+    for (int i = 0; i < q.scalars.count; ++i) {
+      const kgpu_scalar_req s = st.qp.scalars[q.scalars.begin + i];
+      if (!s.check) continue;
+      const int64_t alloc = s.col >= 0 ? gp(st.alloc_scalar)[(size_t)s.col * st.N + c.n] : 0;
+      int64_t used = s.col >= 0 ? gp(st.req_scalar)[(size_t)s.col * st.N + c.n] : 0;
+      if (s.col >= 0) {
+        for (int v = c.v0; v < c.v1; ++v) {
+          const int sg = v_sign(c, v);
+          if (!sg) continue;
+          const kgpu_pod_query& p = vrec(c, v);
+          for (int j = 0; j < p.scalars.count; ++j) {
+            const kgpu_scalar_req t = c.a->v_scalars[p.scalars.begin + j];
+            if (t.col == s.col) used += sg * t.value;
+          }
+        }
+        if (c.pass1)
+          for (int m = c.m0; m < c.m1; ++m) {
+            const kgpu_pod_query& p = nrec(c, m);
+            for (int j = 0; j < p.scalars.count; ++j) {
+              const kgpu_scalar_req t = c.a->n_scalars[p.scalars.begin + j];
+              if (t.col == s.col) used += t.value;
+            }
+          }
+      }
+      if (alloc < s.value + used) d |= 16u << (i < 11 ? i : 11);
+    }
+  }
+  return d ? (KGPU_CODE_UNSCHEDULABLE << 8) | (d << 16) : 0;
+}
+
+// Sum of the signed effects selected by `pick(PEff)` (victims then nominated pods).
+template <class Pick>
+__device__ __forceinline__ int64_t eff_sum(const VCtx& c, Pick pick) {
+  int64_t s = 0;
+  for (int v = c.v0; v < c.v1; ++v) {
+    const int sg = v_sign(c, v);
+    if (sg) s += sg * (int64_t)pick(c.a->veff[v]);
+  }
+  if (c.pass1)
+    for (int m = c.m0; m < c.m1; ++m) s += (int64_t)pick(c.a->neff[m]);
+  return s;
+}
+
+// PodTopologySpread Filter (filtering.go:276-328) after updateWithPod of the effects (:123-143).
+__device__ uint32_t pts_adj(const VCtx& c) {
+  const DevState& st = *c.st;
+  const QPlan& pl = *c.pl;
+  if (pl.n_hard == 0) return 0;
+  const TopoHdr* h = hdr(st);
+  const bool keys = all_keys(st, pl.hard, pl.n_hard, c.n);  // nodeLabelsMatchSpreadConstraints
+  int64_t d[kMaxSpread];
+  bool any = h->pany != 0;
+  for (int i = 0; i < pl.n_hard; ++i) {
+    d[i] = 0;
+    if (!keys) continue;
+    // TpPairToMatchNum is keyed by (key, value): constraints on the same key share the pair
+    for (int j = 0; j < pl.n_hard; ++j)
+      if (pl.hard[j].key == pl.hard[i].key) d[i] += eff_sum(c, [j](const PEff& e) { return (e.pts_mask >> j) & 1u; });
+    const int v = nval(st, pl.hard[i].key, c.n);
+    if (d[i] != 0 && !slot_ptr(st, pl, pl.hard[i].rslot)[v]) any = true;  // a pair no eligible node registered
+  }
+  if (!any) return 0;
+  for (int i = 0; i < pl.n_hard; ++i) {
+    const TSpread& t = pl.hard[i];
+    const int v = nval(st, t.key, c.n);
+    if (v < 0) return KGPU_CODE_UNSCHEDULABLE << 8;
+    const bool reg = slot_ptr(st, pl, t.rslot)[v] != 0;
+    const int64_t cnt = (reg ? slot_ptr(st, pl, t.cslot)[v] : 0) + d[i];
+    const int64_t* pr = c.a->prep + 3 * i;
+    const int64_t mo = (reg && v == pr[1]) ? pr[2] : pr[0];
+    int64_t mn = (reg || d[i] != 0) ? min(mo, cnt) : pr[0];
+    if (mn == INT64_MAX) mn = 2147483647;  // criticalPaths initial MatchNum
+    if (cnt + t.self_match - mn > t.max_skew) return KGPU_CODE_UNSCHEDULABLE << 8;
+  }
+  return 0;
+}
+
+// InterPodAffinity Filter (filtering.go:314-396) after updateWithPod of the effects (:75-90).
+__device__ uint32_t ipa_adj(const VCtx& c) {
+  const DevState& st = *c.st;
+  const QPlan& pl = *c.pl;
+  const TopoHdr* h = hdr(st);
+  if (pl.n_aff) {  // satisfyPodAffinity
+    const int64_t ad = eff_sum(c, [](const PEff& e) { return e.aff_all; });
+    bool exist = true;
+    int64_t nz = c.a->prep[3 * kMaxSpread];  // len(topologyToMatchedAffinityTerms) before the effects
+    for (int i = 0; i < pl.n_aff; ++i) {
+      const int v = nval(st, pl.aff[i].key, c.n);
+      if (v < 0) return (KGPU_CODE_UNRESOLVABLE << 8) | (1u << 16);
+      int mult = 0, first = i;
+      for (int j = 0; j < pl.n_aff; ++j)
+        if (pl.aff[j].slot == pl.aff[i].slot) {
+          ++mult;
+          if (j < first) first = j;
+        }
+      const int64_t b = slot_ptr(st, pl, pl.aff[i].slot)[v];
+      const int64_t val = b + ad * mult;
+      if (val <= 0) exist = false;
+      if (first == i) nz += (val != 0) - (b != 0);
+    }
+    if (!exist && !(nz == 0 && pl.self_all)) return (KGPU_CODE_UNRESOLVABLE << 8) | (1u << 16);
+  }
+  for (int i = 0; i < pl.n_anti; ++i) {  // satisfyPodAntiAffinity
+    const int v = nval(st, pl.anti[i].key, c.n);
+    if (v < 0) continue;
+    int64_t val = slot_ptr(st, pl, pl.anti[i].slot)[v];
+    for (int j = 0; j < pl.n_anti; ++j)
+      if (pl.anti[j].slot == pl.anti[i].slot) val += eff_sum(c, [j](const PEff& e) { return (e.anti_mask >> j) & 1u; });
+    if (val > 0) return (KGPU_CODE_UNSCHEDULABLE << 8) | (2u << 16);
+  }
+  // satisfyExistingPodsAntiAffinity: every node label pair; only the node's own pairs move
+  auto key_delta = [&](int key) -> int64_t {
+    int64_t s = 0;
+    for (int v = c.v0; v < c.v1; ++v) {
+      const int sg = v_sign(c, v);
+      if (!sg) continue;
+      const PEff& e = c.a->veff[v];
+      for (int k = 0; k < e.exa.count; ++k) s += sg * (c.a->aux[e.exa.begin + k] == key);
+    }
+    if (c.pass1)
+      for (int m = c.m0; m < c.m1; ++m) {
+        const PEff& e = c.a->neff[m];
+        for (int k = 0; k < e.exa.count; ++k) s += (c.a->aux[e.exa.begin + k] == key);
+      }
+    return s;
+  };
+  for (int s = 0; s < pl.n_slots; ++s) {
+    if (pl.slot_kind[s] != kSlotExA) continue;
+    const int v = nval(st, pl.slot_key[s], c.n);
+    if (v >= 0 && (h->ex_any ? slot_ptr(st, pl, s)[v] : 0) + key_delta(pl.slot_key[s]) > 0)
+      return (KGPU_CODE_UNSCHEDULABLE << 8) | (3u << 16);
+  }
+  // keys of the effects' terms that no existing pod's term registered a histogram for
+  auto key_checked = [&](int key) {
+    for (int s = 0; s < pl.n_slots; ++s)
+      if (pl.slot_kind[s] == kSlotExA && pl.slot_key[s] == key) return true;
+    return false;
+  };
+  auto scan = [&](const PEff& e) -> bool {
+    for (int k = 0; k < e.exa.count; ++k) {
+      const int key = c.a->aux[e.exa.begin + k];
+      if (key_checked(key) || nval(st, key, c.n) < 0) continue;
+      if (key_delta(key) > 0) return true;
+    }
+    return false;
+  };
+  for (int v = c.v0; v < c.v1; ++v)
+    if (v_sign(c, v) && scan(c.a->veff[v])) return (KGPU_CODE_UNSCHEDULABLE << 8) | (3u << 16);
+  if (c.pass1)
+    for (int m = c.m0; m < c.m1; ++m)
+      if (scan(c.a->neff[m])) return (KGPU_CODE_UNSCHEDULABLE << 8) | (3u << 16);
+  return 0;
+}
+
+// RunFilterPlugins + Merge on the adjusted view, profile order, first failure wins.
+__device__ uint32_t eval_adj(const VCtx& c) {
+  const DevState& st = *c.st;
+  const NodeRes r0 = load_res(st, c.n);
+  for (int i = 0; i < st.n_filters; ++i) {
+    const int f = st.filters[i];
+    uint32_t code;
+    switch (f) {
+      case KGPU_F_NODE_RESOURCES_FIT: code = fit_adj(c); break;
+      case KGPU_F_NODE_PORTS: code = (c.q->ports.count && ports_conflict_adj(c)) ? KGPU_CODE_UNSCHEDULABLE << 8 : 0; break;
+      case KGPU_F_POD_TOPOLOGY_SPREAD: code = c.pl ? pts_adj(c) : 0; break;
+      case KGPU_F_INTER_POD_AFFINITY: code = c.pl ? ipa_adj(c) : 0; break;
+      default: code = filter_one(f, st, *c.q, r0, c.n); break;  // NodeInfo-independent of pods
+    }
+    if (code) return code | (uint32_t)(i + 1);
+  }
+  return 0;
+}
+
+// podPassesFiltersOnNode: pass 1 with the nominated pods (only when some were added), pass 2 without.
+__device__ uint32_t check_two_pass(VCtx& c) {
+  if (c.m1 > c.m0) {
+    c.pass1 = true;
+    const uint32_t s = eval_adj(c);
+    c.pass1 = false;
+    if (s) return s;
+  }
+  return eval_adj(c);
+}
+
+__global__ __launch_bounds__(64) void k_victims(const DevState* __restrict__ stp, const PreemptArgs* __restrict__ ap) {
+  const DevState& st = *stp;
+  const PreemptArgs& a = *ap;
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= st.N) return;
+  VCtx c;
+  c.st = stp;
+  c.a = ap;
+  c.q = st.queries + a.pod;
+  c.pl = st.plans ? st.plans + a.pod : nullptr;
+  c.n = n;
+  c.v0 = a.v_off[n];
+  c.v1 = a.v_off[n + 1];
+  c.m0 = a.n_off[n];
+  c.m1 = a.n_off[n + 1];
+  c.removal = false;
+  c.pass1 = false;
+  c.trial = -1;
+  c.step = 0;
+  if (!a.preempt) {  // nominated pass 1 of a scheduling cycle
+    if (c.m1 > c.m0) {
+      c.pass1 = true;
+      a.nom_status[n] = eval_adj(c);
+    }
+    return;
+  }
+  kgpu_node_victims out{0, 0, 0, c.v0};
+  // nodesWherePreemptionMightHelp: the cycle's own verdict on the node
+  const uint32_t base = check_two_pass(c);
+  if (((base >> 8) & 3u) == KGPU_CODE_UNRESOLVABLE) {
+    a.out[n] = out;
+    return;
+  }
+  for (int v = c.v0; v < c.v1; ++v) a.vstate[v] = kVRemoved;
+  c.removal = true;
+  if (check_two_pass(c)) {
+    a.out[n] = out;
+    return;
+  }
+  // filterPodsWithPDBViolation over the victims in MoreImportantPod order (host-sorted)
+  int32_t allowed[64];
+  for (int j = 0; j < a.n_pdbs; ++j) allowed[j] = a.pdb_allowed[j];
+  int k = 0;
+  for (int v = c.v0; v < c.v1; ++v) {
+    uint64_t m = a.veff[v].pdb_mask;
+    bool viol = false;
+    while (m) {
+      const int j = __builtin_ctzll(m);
+      m &= m - 1;
+      if (allowed[j] <= 0) {
+        viol = true;
+        break;
+      }
+      --allowed[j];
+    }
+    if (viol) {
+      a.vstate[v] = kVRemoved | kVViolating;
+      a.order[c.v0 + k++] = v;
+    }
+  }
+  for (int v = c.v0; v < c.v1; ++v)
+    if (!(a.vstate[v] & kVViolating)) a.order[c.v0 + k++] = v;
+  // reprieve: violating victims first, then the others, most important first
+  int nv = 0, cnt = 0;
+  for (int s = 0; s < c.v1 - c.v0; ++s) {
+    const int v = a.order[c.v0 + s];
+    const uint8_t viol = a.vstate[v] & kVViolating;
+    a.vstate[v] = kVKept | viol;
+    c.trial = v;
+    c.step = s;
+    if (check_two_pass(c)) {
+      a.vstate[v] = kVEvicted | viol;
+      a.out_victims[c.v0 + cnt++] = v;
+      if (viol) ++nv;
+    }
+  }
+  out.fits = 1;
+  out.n_victims = cnt;
+  out.num_pdb_violations = nv;
+  a.out[n] = out;
+}
+
+// Per DoNotSchedule constraint: minimum count over the key's registered pairs, the pair holding it
+// (lowest value id) and the minimum over the others; then the number of non-zero entries of the
+// affinity map.  One workgroup per item.
+__global__ __launch_bounds__(256) void k_vict_prep(const DevState* __restrict__ stp, const PreemptArgs* __restrict__ ap) {
+  const DevState& st = *stp;
+  const PreemptArgs& a = *ap;
+  const QPlan& pl = st.plans[a.pod];
+  __shared__ int64_t sv[4];
+  __shared__ int32_t si[4];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  auto block_min = [&](int64_t v, int idx, int64_t& ov, int& oi) {
+    for (int o = 32; o; o >>= 1) {
+      const int64_t v2 = __shfl_xor(v, o);
+      const int i2 = __shfl_xor(idx, o);
+      if (v2 < v || (v2 == v && i2 < idx)) {
+        v = v2;
+        idx = i2;
+      }
+    }
+    if (lane == 0) {
+      sv[w] = v;
+      si[w] = idx;
+    }
+    __syncthreads();
+    ov = sv[0];
+    oi = si[0];
+    for (int k = 1; k < (int)(blockDim.x >> 6); ++k)
+      if (sv[k] < ov || (sv[k] == ov && si[k] < oi)) {
+        ov = sv[k];
+        oi = si[k];
+      }
+    __syncthreads();
+  };
+  const int b = blockIdx.x;
+  if (b < pl.n_hard) {
+    const TSpread& t = pl.hard[b];
+    const int nv = t.key >= 0 ? gp(st.key_n_values)[t.key] : 0;
+    const int64_t* reg = slot_ptr(st, pl, t.rslot);
+    const int64_t* cnt = slot_ptr(st, pl, t.cslot);
+    int64_t m1 = INT64_MAX;
+    int i1 = INT32_MAX;
+    for (int v = threadIdx.x; v < nv; v += blockDim.x)
+      if (reg[v] && cnt[v] < m1) {
+        m1 = cnt[v];
+        i1 = v;
+      }
+    int64_t mn;
+    int mi;
+    block_min(m1, i1, mn, mi);
+    int64_t m2 = INT64_MAX;
+    for (int v = threadIdx.x; v < nv; v += blockDim.x)
+      if (reg[v] && v != mi && cnt[v] < m2) m2 = cnt[v];
+    int64_t mn2;
+    int dummy;
+    block_min(m2, 0, mn2, dummy);
+    if (threadIdx.x == 0) {
+      a.prep[3 * b] = mn;
+      a.prep[3 * b + 1] = mi == INT32_MAX ? -1 : mi;
+      a.prep[3 * b + 2] = mn2;
+    }
+  } else if (b == kMaxSpread) {
+    int64_t nz = 0;
+    for (int i = 0; i < pl.n_aff; ++i) {
+      bool first = true;
+      for (int j = 0; j < i; ++j) first &= pl.aff[j].slot != pl.aff[i].slot;
+      if (!first || pl.aff[i].key < 0) continue;
+      const int nv = gp(st.key_n_values)[pl.aff[i].key];
+      const int64_t* h = slot_ptr(st, pl, pl.aff[i].slot);
+      for (int v = threadIdx.x; v < nv; v += blockDim.x) nz += h[v] != 0;
+    }
+    __shared__ int64_t ssum;
+    if (threadIdx.x == 0) ssum = 0;
+    __syncthreads();
+    atomicAdd(reinterpret_cast<unsigned long long*>(&ssum), (unsigned long long)nz);
+    __syncthreads();
+    if (threadIdx.x == 0) a.prep[3 * kMaxSpread] = ssum;
+  }
+}
+
+int launch_vict_prep(const DevState* st, const PreemptArgs* a, void* stream) {
+  hipLaunchKernelGGL(k_vict_prep, dim3(kMaxSpread + 1), dim3(256), 0, (hipStream_t)stream, st, a);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_victims(const DevState* st, const PreemptArgs* a, int N, void* stream) {
+  if (N <= 0) return 0;
+  hipLaunchKernelGGL(k_victims, dim3((N + 63) / 64), dim3(64), 0, (hipStream_t)stream, st, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

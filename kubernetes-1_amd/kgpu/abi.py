@@ -3,7 +3,7 @@ import ctypes as C
 
 import numpy as np
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 OK, E_INVAL, E_NOMEM, E_DEVICE, E_CAPACITY, E_STATE, E_UNSUPPORTED = 0, -1, -2, -3, -4, -5, -6
 ERRNAMES = {0: "OK", -1: "KGPU_E_INVAL", -2: "KGPU_E_NOMEM", -3: "KGPU_E_DEVICE", -4: "KGPU_E_CAPACITY",
             -5: "KGPU_E_STATE", -6: "KGPU_E_UNSUPPORTED"}
@@ -55,7 +55,8 @@ QUERY = np.dtype([
     ("tol_nosched", RANGE), ("tol_prefer", RANGE), ("node_selector", RANGE), ("req_terms", RANGE),
     ("pref_terms", RANGE), ("images", RANGE), ("avoid_id", "<i4"), ("pad0", "<i4"), ("pts_hard", RANGE),
     ("pts_soft", RANGE), ("dpts", SELECTOR), ("ipa_req_aff", RANGE), ("ipa_req_anti", RANGE),
-    ("ipa_pref_aff", RANGE), ("ipa_pref_anti", RANGE), ("labels", RANGE), ("limits", "<i8", (2,))], align=True)
+    ("ipa_pref_aff", RANGE), ("ipa_pref_anti", RANGE), ("labels", RANGE), ("limits", "<i8", (2,)),
+    ("priority", "<i4"), ("pad1", "<i4"), ("uid", "<i8")], align=True)
 RESULT = np.dtype([("node", "<i4"), ("feasible", "<i4"), ("evaluated", "<i4"), ("scored", "<i4"),
                    ("score", "<i8")], align=True)
 
@@ -127,6 +128,17 @@ class Stats(C.Structure):
                 ("eval_kernel_ms", C.c_double), ("eval_launches", C.c_int64)]
 
 
+NOMINATED = np.dtype([("node", "<i4"), ("item", "<i4")], align=True)
+VICTIM = np.dtype([("node", "<i4"), ("slot", "<i4"), ("item", "<i4"), ("pad", "<i4"), ("start_time", "<i8"),
+                   ("pdb_mask", "<u8")], align=True)
+NODE_VICTIMS = np.dtype([("fits", "<i4"), ("n_victims", "<i4"), ("num_pdb_violations", "<i4"), ("first", "<i4")],
+                        align=True)
+
+
+class PreemptArgs(C.Structure):
+    _fields_ = [("n_victims", C.c_int32), ("n_pdbs", C.c_int32), ("victims", vp), ("pdb_allowed", vp), ("pods", vp)]
+
+
 # declaration order of kgpu_struct_sizes
 STRUCT_SIZES = [("kgpu_range", RANGE.itemsize), ("kgpu_req", REQ.itemsize), ("kgpu_selector", SELECTOR.itemsize),
                 ("kgpu_node_term", NODE_TERM.itemsize), ("kgpu_pref_term", PREF_TERM.itemsize),
@@ -137,7 +149,9 @@ STRUCT_SIZES = [("kgpu_range", RANGE.itemsize), ("kgpu_req", REQ.itemsize), ("kg
                 ("kgpu_config", C.sizeof(Config)), ("kgpu_snapshot", C.sizeof(Snapshot)),
                 ("kgpu_result", RESULT.itemsize), ("kgpu_stats", C.sizeof(Stats)), ("kgpu_delta", DELTA.itemsize),
                 ("kgpu_node_row", NODE_ROW.itemsize), ("kgpu_delta_batch", C.sizeof(DeltaBatch)),
-                ("kgpu_shape_point", C.sizeof(ShapePoint))]
+                ("kgpu_shape_point", C.sizeof(ShapePoint)), ("kgpu_nominated", NOMINATED.itemsize),
+                ("kgpu_victim", VICTIM.itemsize), ("kgpu_preempt_args", C.sizeof(PreemptArgs)),
+                ("kgpu_node_victims", NODE_VICTIMS.itemsize)]
 
 
 def ptr(a):

@@ -353,6 +353,7 @@ class Compiler:
         self.scalars = StrDict()
         self.images = StrDict()
         self.controllers = StrDict()  # (kind, uid)
+        self.uids = StrDict()         # pod UIDs (kgpu_pod_query.uid = id + 1; 0: none)
         self.ips = StrDict()
         self.ips.add("0.0.0.0")
         self.protos = StrDict()
@@ -884,6 +885,9 @@ class Compiler:
             flags |= abi.Q_TERMINATING
         q["flags"] = flags
         q["limits"] = api.pod_limits(pod)
+        pr = api.spec(pod).get("priority")
+        q["priority"] = 0 if pr is None else int(pr)  # podutil.GetPodPriority
+        q["uid"] = 1 + self.uids.add(api.meta(pod).get("uid", "") or "%s/%s" % (api.ns_of(pod), api.name_of(pod)))
         return q
 
     def _self_match_all(self, pod):

@@ -92,6 +92,17 @@ class GpuFramework:
         self.nodes = {api.name_of(n): n for n in nodes}
         self.filters = [f for f in profile.filters if f in abi.FILTER_IDS]
         self.seq = 0
+        # NodeInfo.Pods of every listed node, in order, with each pod's pod-table slot (snapshot pods
+        # in compile order, then the pods this framework assumes); the potential victims of preemption
+        self.node_pods = {}
+        slot = 0
+        for p in existing:
+            nn = api.spec(p).get("nodeName", "") or ""
+            if nn in self.nodes:
+                self.node_pods.setdefault(nn, []).append((p, slot))
+                slot += 1
+        self.next_slot = slot
+        self.nominated = []   # [(pod, node name)] -- framework.PodNominator, in nomination order
         self.engine = None
         if create_engine:
             self.engine = Engine(self.config)
@@ -143,7 +154,20 @@ class GpuFramework:
             raw, norm = self.engine.scores(abi.SCORE_IDS[name], n)
             scores[name] = {self.order[self.snap.node_base + int(i)]: (int(raw[i]), int(norm[i])) for i in feas}
         host = self.order[res["node"]] if res["node"] >= 0 else None
+        if assume and host is not None:
+            self._placed(pod, host)
         return CycleResult(host, res, statuses, scores)
+
+    def _placed(self, pod, host):
+        """Record an assumed pod on its node (NodeInfo.AddPod) and drop it from the nominator
+        (scheduler.assume, scheduler.go:448)."""
+        placed = dict(pod)
+        placed["spec"] = dict(api.spec(pod))
+        placed["spec"]["nodeName"] = host
+        self.node_pods.setdefault(host, []).append((placed, self.next_slot))
+        self.next_slot += 1
+        key = _pod_key(pod)
+        self.nominated = [(p, n) for p, n in self.nominated if _pod_key(p) != key]
 
     def schedule(self, pods, first_seq=None, stats=None):
         """scheduleOne loop over pods; returns kgpu_result records (node index -1: FitError,
@@ -159,6 +183,9 @@ class GpuFramework:
             if j > i:
                 res, stats = self.engine.schedule_batch(q[i:j], pc, first_seq=s0 + i, stats=stats)
                 out[i:j] = res
+                for k in range(i, j):
+                    if out[k]["node"] >= 0:
+                        self._placed(pods[k], self.order[out[k]["node"]])
             if j < len(pods):
                 out[j]["node"] = -3
                 j += 1
@@ -168,3 +195,118 @@ class GpuFramework:
 
     def host_of(self, node_index):
         return self.order[node_index] if node_index >= 0 else None
+
+    # ------------------------------------------------------------------ nominated pods / preemption
+    def set_nominated(self, nominated):
+        """framework.PodNominator contents: [(pod, nominated node name)] in nomination order
+        (kgpu_set_nominated).  Every later cycle filters those nodes twice (podPassesFiltersOnNode)."""
+        self.nominated = list(nominated)
+        q, pc, pnp, errors = self.compile_pods([p for p, _ in self.nominated])
+        if errors:
+            raise CompileError(errors[min(errors)])
+        index = {nn: i for i, nn in enumerate(self.order)}
+        noms = np.zeros(len(self.nominated), abi.NOMINATED)
+        for i, (_, nn) in enumerate(self.nominated):
+            noms[i] = (index[nn], i)
+        self.engine.set_nominated(noms, q, pc)
+
+    def select_nodes_for_preemption(self, pod, pdbs=(), now=0):
+        """selectNodesForPreemption + pickOneNodeForPreemption (generic_scheduler.go:718-1012) on the
+        device.  Returns ({node name: (victim pods, numPDBViolations)} in Snapshot.List() order, the
+        picked node name or "")."""
+        prio = _priority(pod)
+        cand = []
+        for nn in self.order:
+            for p, slot in self.node_pods.get(nn, []):
+                if _priority(p) < prio:
+                    cand.append((nn, p, slot))
+        q, pc, pnp, errors = self.compile_pods([pod] + [p for _, p, _ in cand])
+        if errors:
+            raise CompileError(errors[min(errors)])
+        index = {nn: i for i, nn in enumerate(self.order)}
+        vic = np.zeros(len(cand), abi.VICTIM)
+        for i, (nn, p, slot) in enumerate(cand):
+            vic[i] = (index[nn], slot, i, 0, _start_time(p, now), _pdb_mask(p, pdbs))
+        allowed = np.array([int(b.get("disruptionsAllowed", 0)) for b in pdbs], np.int32)
+        out, vout, chosen = self.engine.select_victims(q[0], pc, vic, q[1:], allowed, self.snap.n_nodes)
+        res = {}
+        for n in range(self.snap.n_nodes):
+            o = out[n]
+            if not o["fits"]:
+                continue
+            nn = self.order[self.snap.node_base + n]
+            vs = [cand[int(vout[o["first"] + k])][1] for k in range(o["n_victims"])]
+            res[nn] = (vs, int(o["num_pdb_violations"]))
+        return res, (self.order[chosen] if chosen >= 0 else "")
+
+    def preempt(self, pod, statuses, pdbs=(), now=0):
+        """genericScheduler.Preempt (generic_scheduler.go:252-315, no extenders) after a FitError whose
+        per-node statuses are `statuses` ({node: (code, plugin, reasons)}, CycleResult.statuses).
+        Returns (node name or "", victim pods, nominated pods whose nomination is cleared)."""
+        if not self._eligible_to_preempt(pod):
+            return "", [], []
+        potential = [nn for nn in self.order
+                     if (statuses.get(nn) or (abi.CODE_SUCCESS,))[0] != abi.CODE_UNRESOLVABLE]
+        if not potential:
+            return "", [], [pod]
+        n2v, node = self.select_nodes_for_preemption(pod, pdbs, now)
+        if not node:
+            return "", [], []
+        prio = _priority(pod)
+        lower = [p for p, nn in self.nominated if nn == node and _priority(p) < prio]
+        return node, n2v[node][0], lower
+
+    def _eligible_to_preempt(self, pod):
+        """podEligibleToPreemptOthers (generic_scheduler.go:1030-1056)."""
+        if api.spec(pod).get("preemptionPolicy") == "Never":
+            return False
+        nom = (pod.get("status") or {}).get("nominatedNodeName") or ""
+        if nom and nom in self.nodes:
+            prio = _priority(pod)
+            for p, _ in self.node_pods.get(nom, []):
+                if api.meta(p).get("deletionTimestamp") is not None and _priority(p) < prio:
+                    return False
+        return True
+
+
+def _pod_key(pod):
+    return api.meta(pod).get("uid", "") or "%s/%s" % (api.ns_of(pod), api.name_of(pod))
+
+
+def _priority(pod):
+    """podutil.GetPodPriority."""
+    p = api.spec(pod).get("priority")
+    return 0 if p is None else int(p)
+
+
+def _start_time(pod, now):
+    """util.GetPodStartTime (utils.go:38-44) in ns; pods that have not started: `now`."""
+    import datetime
+    s = (pod.get("status") or {}).get("startTime")
+    if s is None:
+        return now
+    if not isinstance(s, str):
+        return int(s)
+    t = datetime.datetime.strptime(s.replace("Z", "+0000"), "%Y-%m-%dT%H:%M:%S%z")
+    return int(t.timestamp()) * 1_000_000_000
+
+
+def _pdb_mask(pod, pdbs):
+    """PodDisruptionBudgets selecting the pod (filterPodsWithPDBViolation, generic_scheduler.go:878-919):
+    same namespace, a non-empty selector matching the pod's labels; label-less pods match none."""
+    from .compile import label_selector_matches
+    labels = api.labels_of(pod)
+    m = 0
+    if not labels:
+        return 0
+    for j, b in enumerate(pdbs):
+        if (b.get("namespace", "") or "") != api.ns_of(pod):
+            continue
+        sel = b.get("selector")
+        if sel is None or (not (sel.get("matchLabels") or {}) and not (sel.get("matchExpressions") or [])):
+            continue  # Selector.Empty(): matches nothing
+        if any(e.get("operator") not in ("In", "NotIn", "Exists", "DoesNotExist") for e in sel.get("matchExpressions") or []):
+            continue  # LabelSelectorAsSelector error: the PDB is skipped
+        if label_selector_matches(sel, labels):
+            m |= 1 << j
+    return m

@@ -17,7 +17,8 @@ _lib = None
 EXPORTS = ["kgpu_abi_version", "kgpu_struct_sizes", "kgpu_create", "kgpu_destroy", "kgpu_last_error",
            "kgpu_upload_snapshot", "kgpu_generation", "kgpu_schedule_one", "kgpu_schedule_batch",
            "kgpu_get_filter", "kgpu_get_scores", "kgpu_forget_pod", "kgpu_read_nodes", "kgpu_set_option",
-           "kgpu_read_phase_trace", "kgpu_comm_unique_id", "kgpu_comm_init", "kgpu_apply_delta"]
+           "kgpu_read_phase_trace", "kgpu_comm_unique_id", "kgpu_comm_init", "kgpu_apply_delta",
+           "kgpu_set_nominated", "kgpu_select_victims"]
 
 
 class KgpuError(RuntimeError):
@@ -54,6 +55,9 @@ def lib():
     L.kgpu_comm_unique_id.argtypes = [vp]
     L.kgpu_comm_init.argtypes = [vp, i32, i32, vp]
     L.kgpu_apply_delta.argtypes = [vp, C.POINTER(abi.DeltaBatch), i64, vp]
+    L.kgpu_set_nominated.argtypes = [vp, vp, i32, vp, C.POINTER(abi.Pools)]
+    L.kgpu_select_victims.argtypes = [vp, vp, C.POINTER(abi.Pools), C.POINTER(abi.PreemptArgs), vp, vp,
+                                      C.POINTER(i32)]
     if L.kgpu_abi_version() != abi.ABI_VERSION:
         raise KgpuError(abi.E_STATE, "ABI version mismatch")
     _lib = L
@@ -159,6 +163,30 @@ class Engine:
         slots = np.full(max(n_deltas, 1), -1, np.int32)
         self._check(lib().kgpu_apply_delta(self.h, C.byref(batch), generation, slots.ctypes.data))
         return slots[:n_deltas]
+
+    def set_nominated(self, noms, pods, pools):
+        """kgpu_set_nominated: noms = abi.NOMINATED records (global node, record index), pods = their
+        abi.QUERY records compiled against `pools` (copied by the engine).  Empty clears it."""
+        n = np.ascontiguousarray(noms, abi.NOMINATED)
+        q = np.ascontiguousarray(pods, abi.QUERY)
+        self._check(lib().kgpu_set_nominated(self.h, n.ctypes.data if len(n) else None, len(n),
+                                             q.ctypes.data if len(q) else None, C.byref(pools)))
+
+    def select_victims(self, query, pools, victims, pods, pdb_allowed, n_nodes):
+        """kgpu_select_victims: returns (per-node NODE_VICTIMS records, victim index array, chosen global
+        node or -1).  victims: abi.VICTIM records; pods: their abi.QUERY records (same pools as query)."""
+        q = np.ascontiguousarray(np.asarray(query, abi.QUERY).reshape(1))
+        v = np.ascontiguousarray(victims, abi.VICTIM)
+        pr = np.ascontiguousarray(pods, abi.QUERY)
+        pa = np.ascontiguousarray(pdb_allowed, np.int32)
+        args = abi.PreemptArgs(len(v), len(pa), v.ctypes.data if len(v) else None,
+                               pa.ctypes.data if len(pa) else None, pr.ctypes.data if len(pr) else None)
+        out = np.zeros(max(n_nodes, 1), abi.NODE_VICTIMS)
+        vout = np.full(max(len(v), 1), -1, np.int32)
+        chosen = C.c_int32(-1)
+        self._check(lib().kgpu_select_victims(self.h, q.ctypes.data, C.byref(pools), C.byref(args), out.ctypes.data,
+                                              vout.ctypes.data, C.byref(chosen)))
+        return out[:n_nodes], vout[:len(v)], int(chosen.value)
 
     def comm_init(self, nranks, rank, uid):
         """Join the node-sharding communicator (RCCL): this engine holds one contiguous shard of the
