@@ -127,6 +127,7 @@ type compiler struct {
 	scalars     *strDict
 	images      *strDict
 	controllers *strDict // kind + "/" + uid
+	uids        *strDict // pod UIDs (kgpu_pod_query.uid)
 	ips         *strDict
 	zones       *strDict
 	nodeIndex   map[string]int32
@@ -135,7 +136,7 @@ type compiler struct {
 
 func newCompiler(prof *profileArgs) *compiler {
 	c := &compiler{prof: prof, nkeys: newKeySpace(), pkeys: newKeySpace(), ns: newStrDict(),
-		taints: map[taintKey]int32{}, scalars: newStrDict(), images: newStrDict(), controllers: newStrDict(),
+		taints: map[taintKey]int32{}, scalars: newStrDict(), images: newStrDict(), controllers: newStrDict(), uids: newStrDict(),
 		ips: newStrDict(), zones: newStrDict(), nodeIndex: map[string]int32{}}
 	c.ips.add("0.0.0.0")
 	for _, r := range prof.scalarResources() {
@@ -536,6 +537,10 @@ func (c *compiler) compilePod(pod *v1.Pod, p *pools) (C.kgpu_pod_query, error) {
 		}
 	}
 	q.limits[0], q.limits[1] = C.int64_t(lc), C.int64_t(lm)
+	if pod.Spec.Priority != nil { // podutil.GetPodPriority
+		q.priority = C.int32_t(*pod.Spec.Priority)
+	}
+	q.uid = C.int64_t(c.uids.add(string(pod.UID)) + 1) // addNominatedPods skips the pod itself by UID
 	q.flags = C.uint32_t(flags)
 	return q, nil
 }

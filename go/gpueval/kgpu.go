@@ -155,3 +155,36 @@ func commUniqueID() ([128]byte, error) {
 func (e *engine) commInit(nranks, rank int, id [128]byte) error {
 	return kerr(e.ctx, C.kgpu_comm_init(e.ctx, C.int32_t(nranks), C.int32_t(rank), (*C.uint8_t)(unsafe.Pointer(&id[0]))))
 }
+
+// setNominated replaces the engine's copy of the PodNominator (kgpu_set_nominated): while it is
+// non-empty every cycle runs podPassesFiltersOnNode's two passes (generic_scheduler.go:526-615).
+func (e *engine) setNominated(noms []C.kgpu_nominated, recs []C.kgpu_pod_query, pools *C.kgpu_pools) error {
+	var a arena
+	defer a.free()
+	var cn *C.kgpu_nominated
+	var cr *C.kgpu_pod_query
+	if len(noms) > 0 {
+		cn, cr = cslice(&a, noms), cslice(&a, recs)
+	}
+	return kerr(e.ctx, C.kgpu_set_nominated(e.ctx, cn, C.int32_t(len(noms)), cr, pools))
+}
+
+// selectVictims is selectNodesForPreemption + pickOneNodeForPreemption (generic_scheduler.go:718-1012):
+// per-node victims (indices into victims) and the picked node index (-1: none).
+func (e *engine) selectVictims(q *C.kgpu_pod_query, pools *C.kgpu_pools, victims []C.kgpu_victim,
+	recs []C.kgpu_pod_query, pdbAllowed []int32, n int) ([]C.kgpu_node_victims, []int32, int32, error) {
+	var a arena
+	defer a.free()
+	args := C.kgpu_preempt_args{n_victims: C.int32_t(len(victims)), n_pdbs: C.int32_t(len(pdbAllowed))}
+	if len(victims) > 0 {
+		args.victims, args.pods = cslice(&a, victims), cslice(&a, recs)
+	}
+	if len(pdbAllowed) > 0 {
+		args.pdb_allowed = (*C.int32_t)(cslice(&a, pdbAllowed))
+	}
+	out := make([]C.kgpu_node_victims, n+1)
+	vout := make([]int32, len(victims)+1)
+	var chosen C.int32_t
+	rc := C.kgpu_select_victims(e.ctx, q, pools, &args, &out[0], (*C.int32_t)(unsafe.Pointer(&vout[0])), &chosen)
+	return out[:n], vout[:len(victims)], int32(chosen), kerr(e.ctx, rc)
+}

@@ -147,12 +147,13 @@ type cycle struct {
 func (c *cycle) Clone() framework.StateData { return c }
 
 type GpuEval struct {
-	h    framework.FrameworkHandle
-	prof *profileArgs
-	eng  *engine
-	comp *compiler
-	mir  *mirror
-	seq  int64
+	h         framework.FrameworkHandle
+	prof      *profileArgs
+	eng       *engine
+	comp      *compiler
+	mir       *mirror
+	seq       int64
+	nominated bool // the engine holds a non-empty nominator
 }
 
 func (g *GpuEval) Name() string { return Name }
@@ -182,8 +183,10 @@ func (g *GpuEval) syncSnapshot() error {
 		b, err := g.deltaFromSnapshot(list, &a)
 		if err == nil {
 			g.mir.gen++
-			_, err = g.eng.applyDelta(b, g.mir.gen)
+			var slots []int32
+			slots, err = g.eng.applyDelta(b, g.mir.gen)
 			if err == nil {
+				g.mir.recordSlots(slots)
 				return nil
 			}
 		}
@@ -224,7 +227,7 @@ func (g *GpuEval) upload(list []*framework.NodeInfo, a *arena) error {
 	}
 	g.comp = c
 	m := &mirror{index: map[string]int32{}, gens: map[string]int64{}, nodes: map[string]*v1.Node{},
-		pods: map[string]map[types.UID]*v1.Pod{}, uids: map[types.UID]int64{}}
+		pods: map[string]map[types.UID]*v1.Pod{}, uids: map[types.UID]int64{}, slots: map[types.UID]int32{}}
 	if g.mir != nil {
 		m.uids, m.nextUID, m.gen = g.mir.uids, g.mir.nextUID, g.mir.gen
 	}
@@ -312,6 +315,7 @@ func (g *GpuEval) snapshotSoA(list []*framework.NodeInfo, m *mirror, a *arena) (
 		for _, pi := range ni.Pods {
 			slot := int32(len(podNode))
 			m.pods[n.Name][pi.Pod.UID] = pi.Pod
+			m.slots[pi.Pod.UID] = slot
 			podNode = append(podNode, int32(i))
 			podNs = append(podNs, c.ns.add(pi.Pod.Namespace))
 			fl := uint32(C.KGPU_PF_ACTIVE)
@@ -399,6 +403,9 @@ func (g *GpuEval) PreFilter(ctx context.Context, cs *framework.CycleState, pod *
 	}
 	var a arena
 	defer a.free()
+	if err := g.syncNominated(&a); err != nil {
+		return framework.NewStatus(framework.Error, err.Error())
+	}
 	p := &pools{}
 	q, err := g.comp.compilePod(pod, p)
 	if err != nil {
@@ -442,7 +449,9 @@ func (g *GpuEval) PreFilter(ctx context.Context, cs *framework.CycleState, pod *
 
 func (g *GpuEval) PreFilterExtensions() framework.PreFilterExtensions { return nil }
 
-// Filter: O(1) lookup of the node's status word.
+// Filter: O(1) lookup of the node's status word.  With nominated pods the framework calls Filter
+// twice per node (podPassesFiltersOnNode); the word already combines both passes, and returning it
+// for either call yields the framework's verdict and status.
 func (g *GpuEval) Filter(ctx context.Context, cs *framework.CycleState, pod *v1.Pod, ni *framework.NodeInfo) *framework.Status {
 	c, err := readCycle(cs)
 	if err != nil {

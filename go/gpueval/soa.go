@@ -39,6 +39,18 @@ type mirror struct {
 	uids     map[types.UID]int64         // pod UID -> engine uid
 	nextUID  int64
 	gen      int64
+	slots    map[types.UID]int32         // pod UID -> pod-table slot (kgpu_victim.slot)
+	added    map[int]types.UID           // delta index -> UID of an ADD_POD in the pending batch
+}
+
+// recordSlots keeps the pod-table slot of every pod the last delta batch added.
+func (m *mirror) recordSlots(slots []int32) {
+	for i, u := range m.added {
+		if i < len(slots) && slots[i] >= 0 {
+			m.slots[u] = slots[i]
+		}
+	}
+	m.added = nil
 }
 
 func (m *mirror) uid(u types.UID) int64 {
@@ -170,6 +182,12 @@ func (g *GpuEval) deltaFromSnapshot(list []*framework.NodeInfo, a *arena) (*C.kg
 			return err
 		}
 		podsQ = append(podsQ, q)
+		if op == C.KGPU_D_ADD_POD {
+			if m.added == nil {
+				m.added = map[int]types.UID{}
+			}
+			m.added[len(deltas)] = pod.UID
+		}
 		deltas = append(deltas, C.kgpu_delta{op: op, node: C.int32_t(newIndex[nm]), uid: C.int64_t(m.uid(pod.UID)),
 			item: C.int32_t(len(podsQ) - 1)})
 		return nil
