@@ -515,6 +515,10 @@ int kgpu_read_nodes(kgpu_ctx* ctx, int64_t* req_cpu, int64_t* req_mem, int64_t* 
  * abort word there, as a workgroup that lost co-residency would (-1, the default: never).  The
  * batch then fails with KGPU_E_DEVICE and the engine refuses cycles until the next upload. */
 #define KGPU_OPT_ABORT_AT 7
+/* KGPU_OPT_XGMI (8): 1 (default) = on a node-sharded engine, persistent runs exchange their per-pod
+ * granules through peer stores into every rank's mailbox ring over xGMI (kgpu_xgmi_*); 0 = the
+ * per-pod RCCL all-gather for every pod. */
+#define KGPU_OPT_XGMI 8
 int kgpu_set_option(kgpu_ctx* ctx, int32_t option, int64_t value);
 /* Phase stamps of the last persistent run (100 MHz s_memrealtime ticks), 16 per pipeline
  * iteration (pods + 1): workgroup 0's {start, evaluated, previous pod resolved, published, end, 0,
@@ -582,7 +586,17 @@ int kgpu_select_victims(kgpu_ctx* ctx, const kgpu_pod_query* q, const kgpu_pools
  * 0; the caller broadcasts them; every rank calls kgpu_comm_init with its shard's snapshot
  * already uploaded (node_base / n_total_nodes set). */
 int kgpu_comm_unique_id(uint8_t id[128]);
+/* With nranks > 1 and KGPU_OPT_XGMI on, kgpu_comm_init also sets up the xGMI mailboxes (the IPC
+ * handles travel over RCCL); kgpu_xgmi_active reports whether every rank could map every peer. */
 int kgpu_comm_init(kgpu_ctx* ctx, int32_t nranks, int32_t rank, const uint8_t id[128]);
+int kgpu_xgmi_active(const kgpu_ctx* ctx);
+/* The mailbox exchange without RCCL (the caller moves the handles, e.g. over its own transport):
+ * kgpu_xgmi_handle allocates and zeroes this rank's ring for `nranks` ranks and returns its 64-byte
+ * IPC handle; after every rank has its handle, kgpu_xgmi_init(handles = nranks x 64 bytes in rank
+ * order) maps the peers.  Every rank must then issue the same schedule calls.  Pods that need a
+ * per-pod exchange outside a persistent run (normalize / topology pods) still need kgpu_comm_init. */
+int kgpu_xgmi_handle(kgpu_ctx* ctx, int32_t nranks, uint8_t handle[64]);
+int kgpu_xgmi_init(kgpu_ctx* ctx, int32_t nranks, int32_t rank, const uint8_t* handles);
 
 #ifdef __cplusplus
 }

@@ -115,6 +115,16 @@ struct kgpu_ctx {
   DevBuf p_args, p_voff, p_veff, p_noff, p_neff, p_aux, p_vrecs, p_vsc, p_vports, p_nrecs, p_nsc, p_nports,
       p_vstate, p_order, p_out, p_outv, p_prep, p_nomstat, p_pdb;
   kgpu::PreemptArgs pa_host{};
+  // ---- node sharding over xGMI (kgpu_xgmi_init): granule mailbox ring, peers' rings opened
+  // through IPC handles, the common persistent geometry of every rank
+  int32_t xg_nranks = 0, xg_rank = 0;
+  DevBuf xg_box;                 // [kXgmiRing][GT] u64 granules | [kXgmiRing][GT] i32 feasible counts
+  std::vector<void*> xg_open;    // peers' boxes (hipIpcOpenMemHandle), closed on destroy
+  DevBuf xg_arr;                 // device array: nranks granule bases, then nranks feasible-count bases
+  int xg_geo = -1, xg_per = 0, xg_groups = 0, xg_GT = 0;
+  int64_t xg_seq = 0;            // ring sequence of the next pod (identical on every rank)
+  bool xgmi = true;              // KGPU_OPT_XGMI
+  DevBuf batch_ptrs;             // unsharded persistent runs: {gran, feas} per run
   DevBuf flags_buf;                                // DevState::port_overflow
   DevBuf d_stage, d_remap, d_from;
   void* stage_host = nullptr;                      // pinned staging block of a delta launch
@@ -1467,12 +1477,25 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
   int64_t timed_passes = 0;
   // Persistent geometry: one workgroup per CU at most, K node rows per lane in registers.
   int per = 0, groups = 0;
-  const bool sharded = c->comm != nullptr;
+  const bool xg = c->xg_nranks > 1 && c->xgmi;  // persistent runs exchange granules over xGMI
+  const bool sharded = c->comm != nullptr || xg;
   const bool cut = c->st.cut_state != nullptr;  // percentageOfNodesToScore trims the feasible set
   if (cut && sharded)
     return fail(c, KGPU_E_UNSUPPORTED, "percentageOfNodesToScore < 100 on a node-sharded engine (nextStartNodeIndex "
                                        "rotates over the whole cluster): use 100 when sharding");
-  const int kidx = (c->persistent && !diag && !sharded && !cut && !nom_dev) ? kgpu::batch_geometry(st.N, std::min(c->max_groups > 0 ? std::min(c->max_groups, c->n_cus) : c->n_cus, 256), &per, &groups) : -1;
+  int kidx = -1;
+  if (c->persistent && !diag && !cut && !nom_dev) {
+    if (xg) {
+      kidx = c->xg_geo;
+      per = c->xg_per;
+      groups = c->xg_groups;
+    } else if (!sharded) {
+      kidx = kgpu::batch_geometry(st.N, std::min(c->max_groups > 0 ? std::min(c->max_groups, c->n_cus) : c->n_cus, 256),
+                                  &per, &groups);
+    }
+  }
+  std::deque<std::array<void*, 2>> run_ptrs;  // kept until the stream is synchronized
+  if (kidx >= 0 && !xg && (rc = ensure(c, c->batch_ptrs, sizeof(void*) * 2 * (size_t)(n + 1)))) return rc;
   std::vector<uint8_t> norm((size_t)n), topo((size_t)n, 0);
   // pods that need the normalize pass or whose scoring fails take the one-launch-per-pod path;
   // pods with topology state take the topology pipeline
@@ -1483,6 +1506,9 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
   // Sharded: after the evaluation (and normalize) of pod k, pack this shard's record and
   // all-gather it on the same stream; the next launch resolves pod k over every rank's record.
   auto exchange = [&](int parity, int what) -> int {
+    if (!c->comm)
+      return fail(c, KGPU_E_STATE, "this pod needs the per-pod RCCL exchange: call kgpu_comm_init (xGMI mailboxes "
+                                   "carry persistent runs only)");
     if (kgpu::launch_shard_pack(dst, parity, blocks, what, c->stream))
       return fail(c, KGPU_E_DEVICE, "k_shard_pack launch failed");
     const ncclResult_t r =
@@ -1551,6 +1577,7 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
         // its shard; RCCL sums them (and ORs / mins / maxes the header) between the phases, so
         // every rank filters and scores against the cluster-wide TpPairToMatchNum, topology
         // scores, sizes and normalize extremes; the winner exchange is the non-topology one.
+        if (!c->comm) return fail(c, KGPU_E_STATE, "topology pods on a sharded engine need kgpu_comm_init");
         int64_t* sc = c->st.scratch;
         auto ar = [&](void* buf, size_t cnt, ncclDataType_t t, ncclRedOp_t op) -> int {
           if (!cnt) return KGPU_OK;
@@ -1610,21 +1637,45 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
     }
     if (kidx >= 0 && !norm[(size_t)i]) {
       // a run of pods with constant normalize maxima: one persistent launch
-      while (j < n && !norm[(size_t)j] && !topo[(size_t)j]) ++j;
+      while (j < n && !norm[(size_t)j] && !topo[(size_t)j] && (!xg || j - i < kgpu::kXgmiRing / 2)) ++j;
       const int32_t cnt = j - i;
-      // layout: granules [cnt][groups] u64 | feasible counts [cnt][groups] i32
-      const size_t cells = (size_t)cnt * (size_t)groups;
-      const size_t gbytes = sizeof(uint64_t) * cells + sizeof(int32_t) * cells;
-      if ((rc = ensure(c, c->gran, gbytes))) return rc;
-      HIP_OK(c, hipMemsetAsync(c->gran.p, 0, sizeof(uint64_t) * cells, c->stream));
       kgpu::BatchArgs ba{};
+      if (xg) {
+        // every rank's mailbox ring (kgpu_xgmi_init); rows are addressed by the ring sequence
+        const size_t cells = (size_t)kgpu::kXgmiRing * (size_t)c->xg_GT;
+        ba.gran = static_cast<uint64_t*>(c->xg_box.p);
+        ba.feas = reinterpret_cast<int32_t*>(ba.gran + cells);
+        ba.pgran = static_cast<uint64_t* const*>(c->xg_arr.p);
+        ba.pfeas = reinterpret_cast<int32_t* const*>(static_cast<uint64_t* const*>(c->xg_arr.p) + c->xg_nranks);
+        ba.nranks = c->xg_nranks;
+        ba.rank = c->xg_rank;
+        ba.GT = c->xg_GT;
+        ba.R = kgpu::kXgmiRing;
+        ba.xseq0 = c->xg_seq;
+        c->xg_seq += cnt;
+      } else {
+        // layout: granules [cnt][groups] u64 | feasible counts [cnt][groups] i32
+        const size_t cells = (size_t)cnt * (size_t)groups;
+        const size_t gbytes = sizeof(uint64_t) * cells + sizeof(int32_t) * cells;
+        if ((rc = ensure(c, c->gran, gbytes))) return rc;
+        HIP_OK(c, hipMemsetAsync(c->gran.p, 0, sizeof(uint64_t) * cells, c->stream));
+        ba.gran = static_cast<uint64_t*>(c->gran.p);
+        ba.feas = reinterpret_cast<int32_t*>(ba.gran + cells);
+        run_ptrs.push_back({ba.gran, ba.feas});
+        void** slot = static_cast<void**>(c->batch_ptrs.p) + 2 * (run_ptrs.size() - 1);
+        HIP_OK(c, hipMemcpyAsync(slot, run_ptrs.back().data(), sizeof(void*) * 2, hipMemcpyHostToDevice, c->stream));
+        ba.pgran = reinterpret_cast<uint64_t* const*>(slot);
+        ba.pfeas = reinterpret_cast<int32_t* const*>(slot + 1);
+        ba.nranks = 1;
+        ba.rank = 0;
+        ba.GT = groups;
+        ba.R = 0;
+      }
       ba.first = i;
       ba.count = cnt;
       ba.per = per;
       ba.assume = assume;
       ba.seq0 = first_seq + i;
-      ba.gran = static_cast<uint64_t*>(c->gran.p);
-      ba.feas = reinterpret_cast<int32_t*>(ba.gran + cells);
       ba.abort = abort_word;
       ba.abort_at = c->abort_at >= i && c->abort_at < i + cnt ? c->abort_at - i : -1;
       ba.trace = nullptr;
@@ -2462,9 +2513,13 @@ int kgpu_destroy(kgpu_ctx* c) {
                     &c->abort_buf, &c->t_plan_of, &c->flags_buf, &c->d_stage, &c->d_remap, &c->d_from,
                     &c->p_args, &c->p_voff, &c->p_veff, &c->p_noff, &c->p_neff, &c->p_aux, &c->p_vrecs,
                     &c->p_vsc, &c->p_vports, &c->p_nrecs, &c->p_nsc, &c->p_nports, &c->p_vstate, &c->p_order,
-                    &c->p_out, &c->p_outv, &c->p_prep, &c->p_nomstat, &c->p_pdb})
+                    &c->p_out, &c->p_outv, &c->p_prep, &c->p_nomstat, &c->p_pdb, &c->xg_arr,
+                    &c->batch_ptrs})
     if (b->p) (void)hipFree(b->p);
   if (c->pref_x.p) (void)hipFree(c->pref_x.p);
+  for (void* q : c->xg_open)
+    if (q) (void)hipIpcCloseMemHandle(q);
+  if (c->xg_box.p) (void)hipFree(c->xg_box.p);
   if (c->stage_host) (void)hipHostFree(c->stage_host);
   if (c->st.mcnt) (void)hipFree(c->st.mcnt);
   if (c->st.tcnt) (void)hipFree(c->st.tcnt);
@@ -2496,6 +2551,7 @@ int kgpu_set_option(kgpu_ctx* c, int32_t option, int64_t value) {
   else if (option == KGPU_OPT_TOPO_FUSED) c->topo_fused = value != 0;
   else if (option == KGPU_OPT_TOPO_PERSISTENT) c->tfast = value != 0;
   else if (option == KGPU_OPT_ABORT_AT) c->abort_at = value < 0 || value > INT32_MAX ? -1 : (int32_t)value;
+  else if (option == KGPU_OPT_XGMI) c->xgmi = value != 0;
   else return KGPU_E_INVAL;
   return KGPU_OK;
 }
@@ -2970,6 +3026,75 @@ int kgpu_apply_delta(kgpu_ctx* c, const kgpu_delta_batch* b, int64_t generation,
   return KGPU_OK;
 }
 
+// ---- node sharding over xGMI: the persistent kernel's granule exchange through peer stores
+// Geometry every rank shares: the persistent layout of the largest shard.
+static int xgmi_geometry(kgpu_ctx* c, int32_t nranks) {
+  const int64_t nmax = ((int64_t)c->st.n_total + nranks - 1) / nranks;
+  const int maxg = std::max(1, std::min(std::min(c->n_cus, 256), kgpu::kXgmiMaxGT / nranks));
+  c->xg_geo = kgpu::batch_geometry((int)nmax, maxg, &c->xg_per, &c->xg_groups);
+  c->xg_GT = nranks * c->xg_groups;
+  return c->xg_geo;
+}
+
+int kgpu_xgmi_handle(kgpu_ctx* c, int32_t nranks, uint8_t handle[64]) {
+  if (!c || !handle || nranks < 2 || nranks > kgpu::kMaxRanks) return KGPU_E_INVAL;
+  if (hipSetDevice(c->device) != hipSuccess) return KGPU_E_DEVICE;
+  if (!c->uploaded) return fail(c, KGPU_E_STATE, "upload this rank's shard before kgpu_xgmi_handle");
+  int64_t maxs = 0;  // the granule key's score field is 20 bits wide in the ring layout
+  for (int i = 0; i < c->cfg.n_scores; ++i) maxs += 100 * std::max<int64_t>(c->cfg.score_weights[i], 1);
+  if (maxs + 1 >= (1 << 20)) return fail(c, KGPU_E_UNSUPPORTED, "score weights too large for the xGMI granule key");
+  if (xgmi_geometry(c, nranks) < 0) return fail(c, KGPU_E_CAPACITY, "shard too large for the persistent kernel");
+  const size_t cells = (size_t)kgpu::kXgmiRing * (size_t)c->xg_GT;
+  for (void* q : c->xg_open)
+    if (q) (void)hipIpcCloseMemHandle(q);
+  c->xg_open.clear();
+  if (c->xg_box.p) HIP_OK(c, hipFree(c->xg_box.p));
+  c->xg_box = DevBuf{};
+  HIP_OK(c, hipMalloc(&c->xg_box.p, cells * (sizeof(uint64_t) + sizeof(int32_t))));
+  c->xg_box.bytes = cells * (sizeof(uint64_t) + sizeof(int32_t));
+  // zeroed before any peer can learn the handle: no lap of the ring reads as valid
+  HIP_OK(c, hipMemset(c->xg_box.p, 0, c->xg_box.bytes));
+  HIP_OK(c, hipDeviceSynchronize());
+  hipIpcMemHandle_t h;
+  HIP_OK(c, hipIpcGetMemHandle(&h, c->xg_box.p));
+  static_assert(sizeof(hipIpcMemHandle_t) <= 64, "IPC handle exceeds the ABI's 64 bytes");
+  std::memset(handle, 0, 64);
+  std::memcpy(handle, &h, sizeof(h));
+  c->xg_nranks = 0;  // not usable until kgpu_xgmi_init
+  return KGPU_OK;
+}
+
+int kgpu_xgmi_init(kgpu_ctx* c, int32_t nranks, int32_t rank, const uint8_t* handles) {
+  if (!c || !handles || nranks < 2 || nranks > kgpu::kMaxRanks || rank < 0 || rank >= nranks) return KGPU_E_INVAL;
+  if (hipSetDevice(c->device) != hipSuccess) return KGPU_E_DEVICE;
+  if (!c->xg_box.p || c->xg_GT != nranks * c->xg_groups)
+    return fail(c, KGPU_E_STATE, "kgpu_xgmi_handle(nranks) must precede kgpu_xgmi_init");
+  const size_t cells = (size_t)kgpu::kXgmiRing * (size_t)c->xg_GT;
+  std::vector<void*> gr((size_t)nranks), fe((size_t)nranks);
+  for (int r = 0; r < nranks; ++r) {
+    void* base = nullptr;
+    if (r == rank) {
+      base = c->xg_box.p;
+    } else {
+      hipIpcMemHandle_t h;
+      std::memcpy(&h, handles + 64 * (size_t)r, sizeof(h));
+      HIP_OK(c, hipIpcOpenMemHandle(&base, h, hipIpcMemLazyEnablePeerAccess));
+      c->xg_open.push_back(base);
+    }
+    gr[(size_t)r] = base;
+    fe[(size_t)r] = static_cast<uint64_t*>(base) + cells;
+  }
+  std::vector<void*> arr(gr);
+  arr.insert(arr.end(), fe.begin(), fe.end());
+  int rc = ensure(c, c->xg_arr, sizeof(void*) * arr.size());
+  if (rc) return rc;
+  HIP_OK(c, hipMemcpy(c->xg_arr.p, arr.data(), sizeof(void*) * arr.size(), hipMemcpyHostToDevice));
+  c->xg_nranks = nranks;
+  c->xg_rank = rank;
+  c->xg_seq = 0;
+  return KGPU_OK;
+}
+
 int kgpu_comm_unique_id(uint8_t id[128]) {
   if (!id) return KGPU_E_INVAL;
   static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId is 128 bytes");
@@ -3007,7 +3132,35 @@ int kgpu_comm_init(kgpu_ctx* c, int32_t nranks, int32_t rank, const uint8_t id[1
   c->comm = comm;
   c->nranks = nranks;
   c->rank = rank;
-  return sync_prefer_union(c);
+  if ((rc = sync_prefer_union(c))) return rc;
+  if (nranks > 1 && c->xgmi) {
+    // persistent runs exchange their granules through peer stores into every rank's mailbox; the
+    // IPC handles travel over RCCL, and every rank takes the path only if every rank could map
+    // every peer (the decision is an all-reduce MIN)
+    std::vector<uint8_t> mine(64, 0), all((size_t)64 * nranks, 0);
+    int ok = kgpu_xgmi_handle(c, nranks, mine.data()) == KGPU_OK ? 1 : 0;
+    DevBuf tmp;
+    if ((rc = ensure(c, tmp, 64 + 64 * (size_t)nranks + 64))) return rc;
+    uint8_t* d = static_cast<uint8_t*>(tmp.p);
+    HIP_OK(c, hipMemcpy(d, mine.data(), 64, hipMemcpyHostToDevice));
+    ncclResult_t nr = ncclAllGather(d, d + 64, 64, ncclUint8, comm, c->stream);
+    if (nr == ncclSuccess) HIP_OK(c, hipStreamSynchronize(c->stream));
+    if (nr == ncclSuccess) HIP_OK(c, hipMemcpy(all.data(), d + 64, 64 * (size_t)nranks, hipMemcpyDeviceToHost));
+    if (nr != ncclSuccess) ok = 0;
+    if (ok && kgpu_xgmi_init(c, nranks, rank, all.data()) != KGPU_OK) ok = 0;
+    int32_t* flag = reinterpret_cast<int32_t*>(d + 64 + 64 * (size_t)nranks);
+    HIP_OK(c, hipMemcpy(flag, &ok, sizeof(int32_t), hipMemcpyHostToDevice));
+    nr = ncclAllReduce(flag, flag, 1, ncclInt32, ncclMin, comm, c->stream);
+    if (nr == ncclSuccess) HIP_OK(c, hipStreamSynchronize(c->stream));
+    int32_t all_ok = 0;
+    if (nr == ncclSuccess) HIP_OK(c, hipMemcpy(&all_ok, flag, sizeof(int32_t), hipMemcpyDeviceToHost));
+    (void)hipFree(tmp.p);
+    if (!all_ok) c->xg_nranks = 0;  // per-pod RCCL exchange only
+    c->err.clear();
+  }
+  return KGPU_OK;
 }
+
+int kgpu_xgmi_active(const kgpu_ctx* c) { return c && c->xg_nranks > 1 && c->xgmi ? 1 : 0; }
 
 }  // extern "C"

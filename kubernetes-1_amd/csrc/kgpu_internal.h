@@ -254,7 +254,21 @@ struct BatchArgs {
   int32_t abort_at;     // KGPU_OPT_ABORT_AT test hook: workgroup 0 raises the abort word at this
                         // iteration (-1: never)
   int32_t pad_a;
+  // Node sharding over xGMI (kgpu_xgmi_init): every workgroup of every rank publishes its granule
+  // and feasible count into every rank's mailbox ring; each rank polls its own.  Unsharded:
+  // nranks 1, pgran[0] = gran, pfeas[0] = feas, GT = groups, R = 0 (rows are this launch's pods,
+  // zeroed before it).  With R > 0, pod i sits on ring row (xseq0 + i) % R and its granules carry
+  // the ring lap (xseq0 + i) / R mod 8 in bits 60-62, so rows of an earlier lap never read as
+  // valid and no rank has to clear another's mailbox.
+  uint64_t* const* pgran;  // [nranks] granule ring bases (this rank's own at [rank] == gran)
+  int32_t* const* pfeas;   // [nranks] feasible-count ring bases
+  int32_t nranks, rank;
+  int32_t GT;              // granules per pod row: nranks * groups
+  int32_t R;               // ring rows, 0 = linear rows
+  int64_t xseq0;
 };
+constexpr int kXgmiRing = 4096;      // mailbox ring rows (a persistent run holds at most half)
+constexpr int kXgmiMaxGT = 1024;     // granules per row the poll sweeps (16 per lane)
 
 // ---------------------------------------------------------------- persistent topology kernel
 // k_tbatch schedules a run of PodTopologySpread / InterPodAffinity / DefaultPodTopologySpread pods

@@ -81,6 +81,18 @@ __device__ __forceinline__ uint64_t rank40(uint64_t k, uint64_t idx, int mode) {
   return x;
 }
 
+__device__ __forceinline__ uint64_t rank40_inv(uint64_t k, uint64_t x, int mode) {
+  // inverse of rank40 (every step is a bijection on 40 bits)
+  if (mode == 1) return kMask40 - x;
+  x ^= (k >> 24) & kMask40;
+  x ^= x >> 23;                                      // 2 * 23 > 40
+  x = (x * 0x38E12D471Bull) & kMask40;               // 0x94D049BB13^-1 mod 2^40
+  x ^= (x >> 19) ^ (x >> 38);
+  x = (x * 0xB38E39396Dull) & kMask40;               // 0xD6E8FEB865^-1 mod 2^40
+  x ^= k & kMask40;
+  return x;
+}
+
 // ---------------------------------------------------------------- selectors
 __device__ __forceinline__ bool list_has(const int32_t* v, int n, int x) {
   for (int i = 0; i < n; ++i)
@@ -1154,17 +1166,25 @@ __device__ __forceinline__ Cand wg_combine(const BatchShared<B>& sh, bool varian
   return c;
 }
 
-// Wave 0: poll pod `row`'s G (<= 256) granules and return the winning key and workgroup to every
-// lane; the abort word rides along with every sweep.  Returns false on timeout / abort.
+// Wave 0: poll pod `row`'s GT granules (<= 64 * NJ) and return the winning key and granule index
+// to every lane; the abort word rides along with every sweep.  A granule counts once its top four
+// bits equal `expect` (valid bit + ring lap); the key is the rest (`kmask`).  System-scope loads
+// for a mailbox other ranks write over xGMI.  Returns false on timeout / abort.
+template <int NJ>
 struct Sweep {
-  uint64_t v[4];
+  uint64_t v[NJ];
   int abort;
 };
-__device__ __forceinline__ Sweep sweep(const uint64_t* row, int G, const int32_t* abort_word) {
+template <int NJ, bool SYS>
+__device__ __forceinline__ Sweep<NJ> sweep(const uint64_t* row, int G, const int32_t* abort_word) {
   const int lane = threadIdx.x & 63;
-  Sweep s;
+  Sweep<NJ> s;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) s.v[j] = (lane + 64 * j < G) ? load_sc1(row + lane + 64 * j) : kGValid;
+  for (int j = 0; j < NJ; ++j) {
+    uint64_t* p = const_cast<uint64_t*>(row + lane + 64 * j);
+    s.v[j] = (lane + 64 * j < G) ? (SYS ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : load_sc1(p))
+                                 : ~0ull;
+  }
   s.abort = load_sc1(abort_word);
   return s;
 }
@@ -1173,12 +1193,13 @@ __device__ __forceinline__ Sweep sweep(const uint64_t* row, int G, const int32_t
 // would be waited for at the first reuse of its registers in the node evaluation -- and vmcnt
 // counts stores too, so that wait would also hold the evaluation behind the granule, result and
 // assume stores issued since.
-__device__ __forceinline__ bool poll_row(const uint64_t* row, int G, const int32_t* abort_word, uint64_t& wkey,
-                                         int& wg) {
+template <int NJ, bool SYS>
+__device__ __forceinline__ bool poll_row(const uint64_t* row, int G, const int32_t* abort_word, uint64_t tmask,
+                                         uint64_t expect, uint64_t& wkey, int& wg) {
   const int lane = threadIdx.x & 63;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   for (;;) {
-    const Sweep cur = sweep(row, G, abort_word);
+    const Sweep<NJ> cur = sweep<NJ, SYS>(row, G, abort_word);
     // the abort word is examined first: a load left unconsumed on the success path would be
     // waited for at the first reuse of its register in the node evaluation -- behind every store
     // issued since (vmcnt counts stores too)
@@ -1187,12 +1208,13 @@ __device__ __forceinline__ bool poll_row(const uint64_t* row, int G, const int32
     uint64_t k = 0;
     int gsel = -1;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < NJ; ++j) {
       const uint64_t v = cur.v[j];
-      if (!(v & kGValid)) {
+      if (lane + 64 * j >= G) continue;
+      if ((v & tmask) != expect) {
         all = false;
-      } else if ((v & ~kGValid) > k) {
-        k = v & ~kGValid;
+      } else if ((v & ~tmask) > k) {
+        k = v & ~tmask;
         gsel = lane + 64 * j;
       }
     }
@@ -1212,6 +1234,9 @@ __global__ __launch_bounds__(B) void k_batch(const DevState* __restrict__ stp, B
   const int tid = threadIdx.x, wave = tid >> 6;
   const int G = gridDim.x, g = blockIdx.x;
   const int lo = g * pa.per;
+  const int GT = pa.GT, gme = pa.rank * G + g;  // this workgroup's granule in every row
+  const bool xg = pa.R > 0;                     // xGMI mailbox ring (node-sharded run)
+  const uint64_t tmask = xg ? (0xFull << 60) : kGValid;
   __shared__ BatchShared<B> sh;
 
   // rows stay in registers; assume_row writes every change through to the node columns as well
@@ -1279,8 +1304,25 @@ __global__ __launch_bounds__(B) void k_batch(const DevState* __restrict__ stp, B
     __syncthreads();
     // ---- wave 0: resolve pod i-1, then publish pod i's granule (unless this workgroup won i-1
     //      without a precomputed variant B: it re-evaluates first)
-    const uint64_t* prow = pa.gran + (size_t)(i - 1) * G;
-    uint64_t* row = pa.gran + (size_t)i * G;
+    auto ring_row = [&](int k) -> size_t { return xg ? (size_t)((pa.xseq0 + k) % pa.R) : (size_t)k; };
+    auto ring_tag = [&](int k) -> uint64_t {
+      return xg ? (kGValid | ((uint64_t)(((pa.xseq0 + k) / pa.R) & 7) << 60)) : kGValid;
+    };
+    const uint64_t* prow = pa.gran + ring_row(i - 1) * GT;
+    const size_t roff = ring_row(i) * GT + gme;
+    const uint64_t gtag = ring_tag(i);
+    // publish pod i's granule (and feasible count) into every rank's mailbox row
+    auto publish = [&](uint64_t key, int feas) {
+      for (int rk = 0; rk < pa.nranks; ++rk) {
+        if (xg) {
+          __hip_atomic_store(pa.pgran[rk] + roff, gtag | key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          __hip_atomic_store(pa.pfeas[rk] + roff, feas, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        } else {
+          store_sc1(pa.pgran[rk] + roff, gtag | key);
+          pa.pfeas[rk][roff] = feas;
+        }
+      }
+    };
     if (wave == 0) {
       // both variants' workgroup results are combined before the poll: after it only a select
       Cand ca{0, -1, 0}, cb{0, -1, 0};
@@ -1292,7 +1334,14 @@ __global__ __launch_bounds__(B) void k_batch(const DevState* __restrict__ stp, B
       int wg = -1;
       bool ok = true;
       if (i == pa.abort_at && g == 0 && tid == 0) __hip_atomic_store(pa.abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (have_prev) ok = poll_row(prow, G, pa.abort, wkey, wg);
+      if (have_prev) {
+        const uint64_t expect = ring_tag(i - 1);
+        if (GT <= 256)
+          ok = xg ? poll_row<4, true>(prow, GT, pa.abort, tmask, expect, wkey, wg)
+                  : poll_row<4, false>(prow, GT, pa.abort, tmask, expect, wkey, wg);
+        else
+          ok = poll_row<16, true>(prow, GT, pa.abort, tmask, expect, wkey, wg);
+      }
       KGPU_STAMP(i, 2);
       if (tid == 0) {
         if (!ok) __hip_atomic_store(pa.abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1300,11 +1349,10 @@ __global__ __launch_bounds__(B) void k_batch(const DevState* __restrict__ stp, B
         sh.wkey = wkey;
         sh.wg = wg;
         sh.cand = -1;
-        const bool won = have_prev && wg == g;
+        const bool won = have_prev && wg == gme;
         if (ok && have_cur && !(won && !fast_b)) {
           const Cand c = won ? cb : ca;
-          store_sc1(row + g, kGValid | c.key);
-          pa.feas[(size_t)i * G + g] = c.feas;
+          publish(c.key, c.feas);
           sh.cand = c.key ? c.idx : -1;
           KGPU_STAMP(i, 3);
         }
@@ -1320,16 +1368,20 @@ __global__ __launch_bounds__(B) void k_batch(const DevState* __restrict__ stp, B
       const uint64_t wkey = sh.wkey;
       const int wg = sh.wg;
       const int pod = pa.first + i - 1;
-      if (tid == 0 && ((wg >= 0 && wg == g) || (wg < 0 && g == 0))) {
+      // the record: unsharded, by the winning workgroup; xGMI-sharded, by workgroup 0 of every
+      // rank, which decodes the winner's global node index from its key
+      if (tid == 0 && (xg ? g == 0 : ((wg >= 0 && wg == gme) || (wg < 0 && g == 0)))) {
         kgpu_result res;
-        res.node = wg >= 0 ? st.node_base + lo + cand : -1;
+        res.node = wg < 0 ? -1
+                 : xg ? (int32_t)rank40_inv(pod_tie_key(st.seed, pa.seq0 + i - 1), wkey & kMask40, st.tie_mode)
+                      : st.node_base + lo + cand;
         res.feasible = 0;   // k_batch_fixup
         res.evaluated = st.n_total;
         res.scored = 0;     // k_batch_fixup
         res.score = wg >= 0 ? (int64_t)(wkey >> 40) - 1 : 0;
         gp(st.results)[pod] = res;
       }
-      if (wg == g) {
+      if (wg == gme) {
         if (pa.assume && tid == ob) {
 #pragma unroll
           for (int j = 0; j < K; ++j)
@@ -1350,8 +1402,7 @@ __global__ __launch_bounds__(B) void k_batch(const DevState* __restrict__ stp, B
           __syncthreads();
           if (tid == 0) {
             const Cand c = wg_combine<B>(sh, false);
-            store_sc1(row + g, kGValid | c.key);
-            pa.feas[(size_t)i * G + g] = c.feas;
+            publish(c.key, c.feas);
             sh.cand = c.key ? c.idx : -1;
             KGPU_STAMP(i, 3);
           }
@@ -1375,7 +1426,9 @@ __global__ void k_batch_fixup(const DevState* __restrict__ stp, BatchArgs pa, in
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= pa.count) return;
   int f = 0;
-  for (int g = 0; g < G; ++g) f += pa.feas[(size_t)i * G + g];
+  const size_t row = pa.R > 0 ? (size_t)((pa.xseq0 + i) % pa.R) : (size_t)i;
+  for (int g = 0; g < pa.GT; ++g) f += pa.feas[row * pa.GT + g];
+  (void)G;
   kgpu_result& r = gp(st.results)[pa.first + i];
   r.feasible = f;
   if (r.node >= 0 && f >= 2) {
@@ -2026,17 +2079,6 @@ int launch_class_init(const DevState* st, int c0, int nc, int n_pods, void* stre
 // rebuilt: TpPairToMatchNum[(k, v)] = sum over the pod's DoNotSchedule constraints on k of
 // H[v] (+ the key-missing bin when v is "", since node.Labels[k] of a missing key is ""), the
 // affinity maps are H[...] > 0, topologyScore[k][v] = sum of weight * H[v].
-__device__ __forceinline__ uint64_t rank40_inv(uint64_t k, uint64_t x, int mode) {
-  // inverse of rank40 (every step is a bijection on 40 bits)
-  if (mode == 1) return kMask40 - x;
-  x ^= (k >> 24) & kMask40;
-  x ^= x >> 23;                                      // 2 * 23 > 40
-  x = (x * 0x38E12D471Bull) & kMask40;               // 0x94D049BB13^-1 mod 2^40
-  x ^= (x >> 19) ^ (x >> 38);
-  x = (x * 0xB38E39396Dull) & kMask40;               // 0xD6E8FEB865^-1 mod 2^40
-  x ^= k & kMask40;
-  return x;
-}
 
 __device__ __forceinline__ bool tb_elig(const TBatchArgs& ta, int sig, int n) {
   const TSig sg = cp(ta.sigs)[sig];
@@ -2607,7 +2649,7 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
       KGPU_TSTAMP(5);
       uint64_t wkey = 0;
       int wg = -1;
-      const bool pok = poll_row(arow, G, ta.abort, wkey, wg);
+      const bool pok = poll_row<4, false>(arow, G, ta.abort, kGValid, kGValid, wkey, wg);
       if (lane == 0) {
         if (!pok) {
           __hip_atomic_store(ta.abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

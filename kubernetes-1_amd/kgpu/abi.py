@@ -11,6 +11,7 @@ ERRNAMES = {0: "OK", -1: "KGPU_E_INVAL", -2: "KGPU_E_NOMEM", -3: "KGPU_E_DEVICE"
 OPT_KERNEL_TIMING, OPT_PERSISTENT, OPT_PERSIST_GROUPS, OPT_PHASE_TRACE, OPT_TOPO_FUSED = 1, 2, 3, 4, 5
 OPT_TOPO_PERSISTENT = 6
 OPT_ABORT_AT = 7
+OPT_XGMI = 8
 CODE_SUCCESS, CODE_ERROR, CODE_UNSCHEDULABLE, CODE_UNRESOLVABLE = 0, 1, 2, 3
 STATUS_NOT_EVALUATED = 0xFF  # KGPU_FS_NOT_EVALUATED: percentageOfNodesToScore stopped before the node
 

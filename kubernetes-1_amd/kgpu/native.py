@@ -18,7 +18,7 @@ EXPORTS = ["kgpu_abi_version", "kgpu_struct_sizes", "kgpu_create", "kgpu_destroy
            "kgpu_upload_snapshot", "kgpu_generation", "kgpu_schedule_one", "kgpu_schedule_batch",
            "kgpu_get_filter", "kgpu_get_scores", "kgpu_forget_pod", "kgpu_read_nodes", "kgpu_set_option",
            "kgpu_read_phase_trace", "kgpu_comm_unique_id", "kgpu_comm_init", "kgpu_apply_delta",
-           "kgpu_set_nominated", "kgpu_select_victims"]
+           "kgpu_set_nominated", "kgpu_select_victims", "kgpu_xgmi_handle", "kgpu_xgmi_init", "kgpu_xgmi_active"]
 
 
 class KgpuError(RuntimeError):
@@ -56,6 +56,9 @@ def lib():
     L.kgpu_comm_init.argtypes = [vp, i32, i32, vp]
     L.kgpu_apply_delta.argtypes = [vp, C.POINTER(abi.DeltaBatch), i64, vp]
     L.kgpu_set_nominated.argtypes = [vp, vp, i32, vp, C.POINTER(abi.Pools)]
+    L.kgpu_xgmi_handle.argtypes = [vp, i32, vp]
+    L.kgpu_xgmi_init.argtypes = [vp, i32, i32, vp]
+    L.kgpu_xgmi_active.argtypes = [vp]
     L.kgpu_select_victims.argtypes = [vp, vp, C.POINTER(abi.Pools), C.POINTER(abi.PreemptArgs), vp, vp,
                                       C.POINTER(i32)]
     if L.kgpu_abi_version() != abi.ABI_VERSION:
@@ -187,6 +190,21 @@ class Engine:
         self._check(lib().kgpu_select_victims(self.h, q.ctypes.data, C.byref(pools), C.byref(args), out.ctypes.data,
                                               vout.ctypes.data, C.byref(chosen)))
         return out[:n_nodes], vout[:len(v)], int(chosen.value)
+
+    def xgmi_handle(self, nranks):
+        """kgpu_xgmi_handle: this rank's 64-byte mailbox IPC handle (the shard must be uploaded)."""
+        buf = (C.c_uint8 * 64)()
+        self._check(lib().kgpu_xgmi_handle(self.h, nranks, buf))
+        return bytes(buf)
+
+    def xgmi_init(self, nranks, rank, handles):
+        """kgpu_xgmi_init: handles = every rank's 64 bytes, in rank order."""
+        b = bytes(handles)
+        buf = (C.c_uint8 * len(b)).from_buffer_copy(b)
+        self._check(lib().kgpu_xgmi_init(self.h, nranks, rank, buf))
+
+    def xgmi_active(self):
+        return bool(lib().kgpu_xgmi_active(self.h))
 
     def comm_init(self, nranks, rank, uid):
         """Join the node-sharding communicator (RCCL): this engine holds one contiguous shard of the
