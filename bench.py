@@ -114,8 +114,8 @@ def main():
     sharded = dist_on or args.shard
     fw = GpuFramework(prof, nodes, existing, pods_hint=init[:16] + pods[:16], device=local,
                       shard=(rank, world) if sharded else None)
+    from kgpu import native
     if sharded:
-        from kgpu import native
         uid = [native.comm_unique_id() if rank == 0 else None]
         if dist_on:
             dist.broadcast_object_list(uid, src=0)
@@ -138,24 +138,47 @@ def main():
         if len(q_init):
             eng.schedule_batch(q_init, pc, first_seq=0)   # untimed: the cluster's initial state
 
-    # warmup (first launches, code object load) on a fresh snapshot, then reset the cluster state
-    reset()
-    for w in range(W):
-        eng.schedule_batch(q[:B], pc, first_seq=len(q_init))
-    reset()
-    torch.cuda.synchronize()
-    if dist_on:
-        dist.barrier()
-    stats = abi.Stats()
-    t0 = time.perf_counter()
-    results = []
-    for k in range(K):
-        res, stats = eng.schedule_batch(q[k * B:(k + 1) * B], pc, first_seq=len(q_init) + k * B, stats=stats)
-        results.append(res)
-    torch.cuda.synchronize()
-    if dist_on:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    xgmi = sharded and eng.xgmi_active()  # persistent runs exchange granules over xGMI mailboxes
+
+    def timed():
+        """Warmup (first launches, code object load) on a fresh snapshot, then the K timed steps."""
+        if dist_on:
+            dist.barrier()  # the persistent runs of all ranks wait for each other's granules
+        reset()
+        for w in range(W):
+            eng.schedule_batch(q[:B], pc, first_seq=len(q_init))
+        reset()
+        torch.cuda.synchronize()
+        if dist_on:
+            dist.barrier()
+        stats = abi.Stats()
+        t0 = time.perf_counter()
+        results = []
+        for k in range(K):
+            res, stats = eng.schedule_batch(q[k * B:(k + 1) * B], pc, first_seq=len(q_init) + k * B, stats=stats)
+            results.append(res)
+        torch.cuda.synchronize()
+        if dist_on:
+            dist.barrier()
+        return time.perf_counter() - t0, results
+
+    if xgmi:
+        # a mailbox exchange that gives up (a rank's granules never arrive) fails the batch on every
+        # rank; the ranks then agree to fall back to the per-pod RCCL exchange and measure that
+        failed = 0
+        try:
+            elapsed, results = timed()
+        except native.KgpuError as e:
+            log("xGMI mailbox run failed (%s): falling back to the per-pod RCCL exchange" % e)
+            failed = 1
+        f = torch.tensor([failed], device="cuda")
+        dist.all_reduce(f, op=dist.ReduceOp.MAX)
+        if int(f.item()):
+            xgmi = False
+            eng.set_option(abi.OPT_XGMI, 0)
+            elapsed, results = timed()
+    else:
+        elapsed, results = timed()
     if dist_on:
         t = torch.tensor([elapsed], device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -165,6 +188,8 @@ def main():
     pods_per_s = n_pods / elapsed
 
     # kernel timing pass (separate: per-launch events perturb the timed loop)
+    if dist_on:
+        dist.barrier()
     reset()
     eng.set_option(abi.OPT_KERNEL_TIMING, 1)
     kst = abi.Stats()
@@ -192,7 +217,7 @@ def main():
     pod_bytes = n_local * bpe + BYTES_PER_EXISTING_POD.get(args.config, 0) * len(existing)
     achieved = pod_bytes / per_pod_s / 1e9
     topo = args.config in ("c", "d")
-    persistent = not args.no_persistent and not sharded and not (topo and args.no_topo_persistent)
+    persistent = not args.no_persistent and (not sharded or (xgmi and not topo)) and not (topo and args.no_topo_persistent)
     launch_pods = B if persistent else 1
     kname = ("k_tbatch" if topo else "k_batch") if persistent else ("k_topo_* pipeline" if topo else "k_eval")
 
@@ -249,7 +274,9 @@ def main():
                                                                             "+".join(prof.filters + [s for s, _ in prof.scores])),
                        "nodes": len(nodes), "nodes_per_gpu": fw.snap.n_nodes, "pods": n_pods, "pods_per_step": B,
                        "percentage_of_nodes_to_score": 100,
-                       "parallelism": ("node shards x%d, RCCL all-gather per pod" % world) if sharded else "1 GPU"},
+                       "parallelism": ("node shards x%d, %s" % (world, "granules through xGMI peer stores (persistent kernel)"
+                                                                  if xgmi else "RCCL all-gather per pod"))
+                       if sharded else "1 GPU"},
             "node_evals_per_s": round(pods_per_s * len(nodes), 1),
             "placed": placed,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -3080,6 +3080,18 @@ int kgpu_xgmi_init(kgpu_ctx* c, int32_t nranks, int32_t rank, const uint8_t* han
       std::memcpy(&h, handles + 64 * (size_t)r, sizeof(h));
       HIP_OK(c, hipIpcOpenMemHandle(&base, h, hipIpcMemLazyEnablePeerAccess));
       c->xg_open.push_back(base);
+      // the peer's ring lives on its GPU: this device must reach it over the fabric
+      hipPointerAttribute_t at{};
+      HIP_OK(c, hipPointerGetAttributes(&at, base));
+      if (at.device != c->device && at.device >= 0) {
+        int can = 0;
+        HIP_OK(c, hipDeviceCanAccessPeer(&can, c->device, at.device));
+        if (!can) return fail(c, KGPU_E_UNSUPPORTED, "no peer access to a rank's GPU: per-pod RCCL exchange only");
+        const hipError_t pe = hipDeviceEnablePeerAccess(at.device, 0);
+        if (pe != hipSuccess && pe != hipErrorPeerAccessAlreadyEnabled)
+          return fail(c, KGPU_E_UNSUPPORTED, std::string("hipDeviceEnablePeerAccess: ") + hipGetErrorString(pe));
+        (void)hipGetLastError();
+      }
     }
     gr[(size_t)r] = base;
     fe[(size_t)r] = static_cast<uint64_t*>(base) + cells;
