@@ -1115,6 +1115,8 @@ struct BatchShared {
   int wg;          // its workgroup (-1: no feasible node)
   int abort;
   int cand;        // this workgroup's candidate (local index) for the pod just published, -1 none
+  NodeRes crow;    // the candidate's row, staged for the spare wave's variant B
+  uint64_t keyb;   // the spare wave's variant-B key
 };
 
 // Per-lane best over its K rows, then the workgroup's best through shuffles + LDS (variant A, and
@@ -1228,8 +1230,10 @@ __device__ __forceinline__ bool poll_row(const uint64_t* row, int G, const int32
   }
 }
 
-template <uint32_t FM, uint32_t SM, int K, int B>
-__global__ __launch_bounds__(B) void k_batch(const DevState* __restrict__ stp, BatchArgs pa) {
+// SP = 1: one extra wave (the spare) evaluates variant B on the candidate row staged in LDS while
+// the B / 64 row waves evaluate variant A, instead of the candidate's own lane doing both in turn.
+template <uint32_t FM, uint32_t SM, int K, int B, int SP>
+__global__ __launch_bounds__(B + 64 * SP) void k_batch(const DevState* __restrict__ stp, BatchArgs pa) {
   const DevState& st = *stp;
   const int tid = threadIdx.x, wave = tid >> 6;
   const int G = gridDim.x, g = blockIdx.x;
@@ -1241,11 +1245,12 @@ __global__ __launch_bounds__(B) void k_batch(const DevState* __restrict__ stp, B
 
   // rows stay in registers; assume_row writes every change through to the node columns as well
   NodeRes r[K];
+  const bool rows = tid < B;  // a row wave (not the spare)
 #pragma unroll
   for (int j = 0; j < K; ++j) {
     const int n = lo + j * B + tid;
     r[j] = NodeRes{};
-    if (n < st.N) {
+    if (rows && n < st.N) {
       r[j] = load_res(st, n);
       // Allocatable never changes inside the run: LeastAllocated / MostAllocated divide through
       // exact reciprocal-plus-remainder-correction division (div_recip)
@@ -1279,23 +1284,44 @@ __global__ __launch_bounds__(B) void k_batch(const DevState* __restrict__ stp, B
     uint64_t keyb = 0;
     if (have_cur) {
       const uint64_t tk = pod_tie_key(st.seed, pa.seq0 + i);
-#pragma unroll
-      for (int j = 0; j < K; ++j) {
-        const int n = lo + j * B + tid;
-        keys[j] = n < st.N ? node_key<FM, SM>(st, q, r[j], n, tk) : 0;
-      }
-      KGPU_STAMP(i, 5);
-      if (fast_b && tid == ob) {
-#pragma unroll
-        for (int j = 0; j < K; ++j)
-          if (j == jb) {
-            NodeRes rb = r[j];
+      if constexpr (SP) {
+        if (!rows) {
+          // spare wave: variant B on the staged candidate row, beside the row waves' variant A
+          if (fast_b && (tid & 63) == 0) {
+            NodeRes rb = sh.crow;
             assume_regs(qp, rb);
-            keyb = node_key<FM, SM>(st, q, rb, lo + cand, tk);
+            sh.keyb = node_key<FM, SM>(st, q, rb, lo + cand, tk);
           }
+        } else {
+#pragma unroll
+          for (int j = 0; j < K; ++j) {
+            const int n = lo + j * B + tid;
+            keys[j] = n < st.N ? node_key<FM, SM>(st, q, r[j], n, tk) : 0;
+          }
+          KGPU_STAMP(i, 5);
+          // variant B partials = variant A without the candidate; the spare's key joins in wave 0
+          wg_partials<K, B>(sh, keys, tid, fast_b, ob, jb, 0);
+          KGPU_STAMP(i, 6);
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+          const int n = lo + j * B + tid;
+          keys[j] = n < st.N ? node_key<FM, SM>(st, q, r[j], n, tk) : 0;
+        }
+        KGPU_STAMP(i, 5);
+        if (fast_b && tid == ob) {
+#pragma unroll
+          for (int j = 0; j < K; ++j)
+            if (j == jb) {
+              NodeRes rb = r[j];
+              assume_regs(qp, rb);
+              keyb = node_key<FM, SM>(st, q, rb, lo + cand, tk);
+            }
+        }
+        KGPU_STAMP(i, 6);
+        wg_partials<K, B>(sh, keys, tid, fast_b, ob, jb, keyb);
       }
-      KGPU_STAMP(i, 6);
-      wg_partials<K, B>(sh, keys, tid, fast_b, ob, jb, keyb);
     }
     KGPU_STAMP(i, 1);
     // the next pod's query: issued now, consumed after the hop
@@ -1329,6 +1355,16 @@ __global__ __launch_bounds__(B) void k_batch(const DevState* __restrict__ stp, B
       if (have_cur) {
         ca = wg_combine<B>(sh, false);
         cb = fast_b ? wg_combine<B>(sh, true) : ca;
+        if constexpr (SP) {
+          if (fast_b) {
+            const uint64_t kb = sh.keyb;
+            cb.feas += kb != 0;
+            if (kb > cb.key) {
+              cb.key = kb;
+              cb.idx = cand;
+            }
+          }
+        }
       }
       uint64_t wkey = 0;
       int wg = -1;
@@ -1398,7 +1434,7 @@ __global__ __launch_bounds__(B) void k_batch(const DevState* __restrict__ stp, B
             for (int j = 0; j < K; ++j)
               if (j == jb) keys[j] = node_key<FM, SM>(st, q, r[j], lo + cand, tk);
           }
-          wg_partials<K, B>(sh, keys, tid, false, -1, -1, 0);
+          if (rows) wg_partials<K, B>(sh, keys, tid, false, -1, -1, 0);
           __syncthreads();
           if (tid == 0) {
             const Cand c = wg_combine<B>(sh, false);
@@ -1411,6 +1447,15 @@ __global__ __launch_bounds__(B) void k_batch(const DevState* __restrict__ stp, B
       __syncthreads();
     }
     cand = sh.cand;
+    if constexpr (SP) {
+      // stage the new candidate's row (with pod i-1 assumed if it won) for the next variant B
+      if (cand >= 0 && tid == cand % B) {
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+          if (j == cand / B) sh.crow = r[j];
+      }
+      __syncthreads();
+    }
     qp = q;
     q = qn;
     KGPU_STAMP(i, 4);
@@ -2816,16 +2861,17 @@ int select_spec(const int32_t* filters, int nf, const int32_t* scores, int ns, b
 // (256 workgroups x 2048 rows) with every row in registers and no spills.  Larger shards take the
 // one-launch-per-pod path.
 struct Geo {
-  int B, K;
+  int B, K, SP;  // row threads, rows per lane, spare waves
 };
-constexpr Geo kGeo[] = {{256, 1}, {1024, 1}, {512, 4}};
-constexpr int kNumGeo = 3;
+constexpr Geo kGeo[] = {{256, 1, 1}, {768, 1, 1}, {1024, 1, 0}, {512, 4, 1}};
+constexpr int kNumGeo = 4;
 constexpr int kBatchLdsPad = 96 * 1024;
 
 template <uint32_t FM, uint32_t SM>
 struct BatchRow {
   using Fn = void (*)(const DevState*, BatchArgs);
-  static constexpr Fn fn[kNumGeo] = {k_batch<FM, SM, 1, 256>, k_batch<FM, SM, 1, 1024>, k_batch<FM, SM, 4, 512>};
+  static constexpr Fn fn[kNumGeo] = {k_batch<FM, SM, 1, 256, 1>, k_batch<FM, SM, 1, 768, 1>,
+                                     k_batch<FM, SM, 1, 1024, 0>, k_batch<FM, SM, 4, 512, 1>};
 };
 using BatchFn = void (*)(const DevState*, BatchArgs);
 static const BatchFn* const kBatch[] = {
@@ -2866,7 +2912,8 @@ int launch_batch(const DevState* st, const BatchArgs& a, int groups, int geo, in
   BatchArgs arg = a;
   const DevState* sp = st;
   void* args[] = {(void*)&sp, (void*)&arg};
-  if (hipLaunchCooperativeKernel(reinterpret_cast<const void*>(kBatch[spec][geo]), dim3(groups), dim3(kGeo[geo].B),
+  if (hipLaunchCooperativeKernel(reinterpret_cast<const void*>(kBatch[spec][geo]), dim3(groups),
+                                 dim3(kGeo[geo].B + 64 * kGeo[geo].SP),
                                  args, (unsigned)kBatchLdsPad, (hipStream_t)stream) != hipSuccess)
     return -1;
   hipLaunchKernelGGL(k_batch_fixup, dim3((a.count + 255) / 256), dim3(256), 0, (hipStream_t)stream, st, a, groups);
