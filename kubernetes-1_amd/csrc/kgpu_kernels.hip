@@ -1115,8 +1115,6 @@ struct BatchShared {
   int wg;          // its workgroup (-1: no feasible node)
   int abort;
   int cand;        // this workgroup's candidate (local index) for the pod just published, -1 none
-  NodeRes crow;    // the candidate's row, staged for the spare wave's variant B
-  uint64_t keyb;   // the spare wave's variant-B key
 };
 
 // Per-lane best over its K rows, then the workgroup's best through shuffles + LDS (variant A, and
@@ -1178,14 +1176,14 @@ struct Sweep {
   int abort;
 };
 template <int NJ, bool SYS>
-__device__ __forceinline__ Sweep<NJ> sweep(const uint64_t* row, int G, const int32_t* abort_word) {
+__device__ __forceinline__ Sweep<NJ> sweep(const uint64_t* row, int G, const int32_t* abort_word, uint64_t fill) {
   const int lane = threadIdx.x & 63;
   Sweep<NJ> s;
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     uint64_t* p = const_cast<uint64_t*>(row + lane + 64 * j);
     s.v[j] = (lane + 64 * j < G) ? (SYS ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : load_sc1(p))
-                                 : ~0ull;
+                                 : fill;  // a valid granule with key 0
   }
   s.abort = load_sc1(abort_word);
   return s;
@@ -1201,7 +1199,7 @@ __device__ __forceinline__ bool poll_row(const uint64_t* row, int G, const int32
   const int lane = threadIdx.x & 63;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   for (;;) {
-    const Sweep<NJ> cur = sweep<NJ, SYS>(row, G, abort_word);
+    const Sweep<NJ> cur = sweep<NJ, SYS>(row, G, abort_word, expect);
     // the abort word is examined first: a load left unconsumed on the success path would be
     // waited for at the first reuse of its register in the node evaluation -- behind every store
     // issued since (vmcnt counts stores too)
@@ -1212,7 +1210,6 @@ __device__ __forceinline__ bool poll_row(const uint64_t* row, int G, const int32
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const uint64_t v = cur.v[j];
-      if (lane + 64 * j >= G) continue;
       if ((v & tmask) != expect) {
         all = false;
       } else if ((v & ~tmask) > k) {
@@ -1230,27 +1227,33 @@ __device__ __forceinline__ bool poll_row(const uint64_t* row, int G, const int32
   }
 }
 
-// SP = 1: one extra wave (the spare) evaluates variant B on the candidate row staged in LDS while
-// the B / 64 row waves evaluate variant A, instead of the candidate's own lane doing both in turn.
-template <uint32_t FM, uint32_t SM, int K, int B, int SP>
-__global__ __launch_bounds__(B + 64 * SP) void k_batch(const DevState* __restrict__ stp, BatchArgs pa) {
+// XG: the node-sharded instantiation (xGMI mailbox rings); the unsharded one carries none of its code.
+template <uint32_t FM, uint32_t SM, int K, int B, bool XG>
+__global__ __launch_bounds__(B) void k_batch(const DevState* __restrict__ stp, BatchArgs pa) {
   const DevState& st = *stp;
   const int tid = threadIdx.x, wave = tid >> 6;
   const int G = gridDim.x, g = blockIdx.x;
   const int lo = g * pa.per;
   const int GT = pa.GT, gme = pa.rank * G + g;  // this workgroup's granule in every row
-  const bool xg = pa.R > 0;                     // xGMI mailbox ring (node-sharded run)
+  constexpr bool xg = XG;                       // xGMI mailbox ring (node-sharded run)
   const uint64_t tmask = xg ? (0xFull << 60) : kGValid;
   __shared__ BatchShared<B> sh;
+  __shared__ uint64_t* sh_peer_g[XG ? kMaxRanks : 1];
+  __shared__ int32_t* sh_peer_f[XG ? kMaxRanks : 1];
+  if constexpr (XG) {
+    if (tid < pa.nranks) {
+      sh_peer_g[tid] = pa.pgran[tid];
+      sh_peer_f[tid] = pa.pfeas[tid];
+    }
+  }
 
   // rows stay in registers; assume_row writes every change through to the node columns as well
   NodeRes r[K];
-  const bool rows = tid < B;  // a row wave (not the spare)
 #pragma unroll
   for (int j = 0; j < K; ++j) {
     const int n = lo + j * B + tid;
     r[j] = NodeRes{};
-    if (rows && n < st.N) {
+    if (n < st.N) {
       r[j] = load_res(st, n);
       // Allocatable never changes inside the run: LeastAllocated / MostAllocated divide through
       // exact reciprocal-plus-remainder-correction division (div_recip)
@@ -1284,44 +1287,23 @@ __global__ __launch_bounds__(B + 64 * SP) void k_batch(const DevState* __restric
     uint64_t keyb = 0;
     if (have_cur) {
       const uint64_t tk = pod_tie_key(st.seed, pa.seq0 + i);
-      if constexpr (SP) {
-        if (!rows) {
-          // spare wave: variant B on the staged candidate row, beside the row waves' variant A
-          if (fast_b && (tid & 63) == 0) {
-            NodeRes rb = sh.crow;
-            assume_regs(qp, rb);
-            sh.keyb = node_key<FM, SM>(st, q, rb, lo + cand, tk);
-          }
-        } else {
 #pragma unroll
-          for (int j = 0; j < K; ++j) {
-            const int n = lo + j * B + tid;
-            keys[j] = n < st.N ? node_key<FM, SM>(st, q, r[j], n, tk) : 0;
-          }
-          KGPU_STAMP(i, 5);
-          // variant B partials = variant A without the candidate; the spare's key joins in wave 0
-          wg_partials<K, B>(sh, keys, tid, fast_b, ob, jb, 0);
-          KGPU_STAMP(i, 6);
-        }
-      } else {
-#pragma unroll
-        for (int j = 0; j < K; ++j) {
-          const int n = lo + j * B + tid;
-          keys[j] = n < st.N ? node_key<FM, SM>(st, q, r[j], n, tk) : 0;
-        }
-        KGPU_STAMP(i, 5);
-        if (fast_b && tid == ob) {
-#pragma unroll
-          for (int j = 0; j < K; ++j)
-            if (j == jb) {
-              NodeRes rb = r[j];
-              assume_regs(qp, rb);
-              keyb = node_key<FM, SM>(st, q, rb, lo + cand, tk);
-            }
-        }
-        KGPU_STAMP(i, 6);
-        wg_partials<K, B>(sh, keys, tid, fast_b, ob, jb, keyb);
+      for (int j = 0; j < K; ++j) {
+        const int n = lo + j * B + tid;
+        keys[j] = n < st.N ? node_key<FM, SM>(st, q, r[j], n, tk) : 0;
       }
+      KGPU_STAMP(i, 5);
+      if (fast_b && tid == ob) {
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+          if (j == jb) {
+            NodeRes rb = r[j];
+            assume_regs(qp, rb);
+            keyb = node_key<FM, SM>(st, q, rb, lo + cand, tk);
+          }
+      }
+      KGPU_STAMP(i, 6);
+      wg_partials<K, B>(sh, keys, tid, fast_b, ob, jb, keyb);
     }
     KGPU_STAMP(i, 1);
     // the next pod's query: issued now, consumed after the hop
@@ -1337,15 +1319,16 @@ __global__ __launch_bounds__(B + 64 * SP) void k_batch(const DevState* __restric
     const uint64_t* prow = pa.gran + ring_row(i - 1) * GT;
     const size_t roff = ring_row(i) * GT + gme;
     const uint64_t gtag = ring_tag(i);
-    // publish pod i's granule (and feasible count) into every rank's mailbox row
+    // publish pod i's granule (and feasible count): into this launch's rows, or into every rank's
+    // mailbox ring (peer bases staged in LDS at kernel start: no pointer load on this path)
     auto publish = [&](uint64_t key, int feas) {
-      for (int rk = 0; rk < pa.nranks; ++rk) {
-        if (xg) {
-          __hip_atomic_store(pa.pgran[rk] + roff, gtag | key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          __hip_atomic_store(pa.pfeas[rk] + roff, feas, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        } else {
-          store_sc1(pa.pgran[rk] + roff, gtag | key);
-          pa.pfeas[rk][roff] = feas;
+      if constexpr (!XG) {
+        store_sc1(pa.gran + roff, gtag | key);
+        pa.feas[roff] = feas;
+      } else {
+        for (int rk = 0; rk < pa.nranks; ++rk) {
+          __hip_atomic_store(sh_peer_g[rk] + roff, gtag | key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          __hip_atomic_store(sh_peer_f[rk] + roff, feas, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
       }
     };
@@ -1355,16 +1338,6 @@ __global__ __launch_bounds__(B + 64 * SP) void k_batch(const DevState* __restric
       if (have_cur) {
         ca = wg_combine<B>(sh, false);
         cb = fast_b ? wg_combine<B>(sh, true) : ca;
-        if constexpr (SP) {
-          if (fast_b) {
-            const uint64_t kb = sh.keyb;
-            cb.feas += kb != 0;
-            if (kb > cb.key) {
-              cb.key = kb;
-              cb.idx = cand;
-            }
-          }
-        }
       }
       uint64_t wkey = 0;
       int wg = -1;
@@ -1372,9 +1345,10 @@ __global__ __launch_bounds__(B + 64 * SP) void k_batch(const DevState* __restric
       if (i == pa.abort_at && g == 0 && tid == 0) __hip_atomic_store(pa.abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (have_prev) {
         const uint64_t expect = ring_tag(i - 1);
-        if (GT <= 256)
-          ok = xg ? poll_row<4, true>(prow, GT, pa.abort, tmask, expect, wkey, wg)
-                  : poll_row<4, false>(prow, GT, pa.abort, tmask, expect, wkey, wg);
+        if constexpr (!XG)
+          ok = poll_row<4, false>(prow, GT, pa.abort, tmask, expect, wkey, wg);
+        else if (GT <= 256)
+          ok = poll_row<4, true>(prow, GT, pa.abort, tmask, expect, wkey, wg);
         else
           ok = poll_row<16, true>(prow, GT, pa.abort, tmask, expect, wkey, wg);
       }
@@ -1434,7 +1408,7 @@ __global__ __launch_bounds__(B + 64 * SP) void k_batch(const DevState* __restric
             for (int j = 0; j < K; ++j)
               if (j == jb) keys[j] = node_key<FM, SM>(st, q, r[j], lo + cand, tk);
           }
-          if (rows) wg_partials<K, B>(sh, keys, tid, false, -1, -1, 0);
+          wg_partials<K, B>(sh, keys, tid, false, -1, -1, 0);
           __syncthreads();
           if (tid == 0) {
             const Cand c = wg_combine<B>(sh, false);
@@ -1447,15 +1421,6 @@ __global__ __launch_bounds__(B + 64 * SP) void k_batch(const DevState* __restric
       __syncthreads();
     }
     cand = sh.cand;
-    if constexpr (SP) {
-      // stage the new candidate's row (with pod i-1 assumed if it won) for the next variant B
-      if (cand >= 0 && tid == cand % B) {
-#pragma unroll
-        for (int j = 0; j < K; ++j)
-          if (j == cand / B) sh.crow = r[j];
-      }
-      __syncthreads();
-    }
     qp = q;
     q = qn;
     KGPU_STAMP(i, 4);
@@ -2861,17 +2826,19 @@ int select_spec(const int32_t* filters, int nf, const int32_t* scores, int ns, b
 // (256 workgroups x 2048 rows) with every row in registers and no spills.  Larger shards take the
 // one-launch-per-pod path.
 struct Geo {
-  int B, K, SP;  // row threads, rows per lane, spare waves
+  int B, K;
 };
-constexpr Geo kGeo[] = {{256, 1, 1}, {768, 1, 1}, {1024, 1, 0}, {512, 4, 1}};
-constexpr int kNumGeo = 4;
+constexpr Geo kGeo[] = {{256, 1}, {1024, 1}, {512, 4}};
+constexpr int kNumGeo = 3;
 constexpr int kBatchLdsPad = 96 * 1024;
 
 template <uint32_t FM, uint32_t SM>
 struct BatchRow {
   using Fn = void (*)(const DevState*, BatchArgs);
-  static constexpr Fn fn[kNumGeo] = {k_batch<FM, SM, 1, 256, 1>, k_batch<FM, SM, 1, 768, 1>,
-                                     k_batch<FM, SM, 1, 1024, 0>, k_batch<FM, SM, 4, 512, 1>};
+  static constexpr Fn fn[kNumGeo] = {k_batch<FM, SM, 1, 256, false>, k_batch<FM, SM, 1, 1024, false>,
+                                     k_batch<FM, SM, 4, 512, false>};
+  static constexpr Fn xfn[kNumGeo] = {k_batch<FM, SM, 1, 256, true>, k_batch<FM, SM, 1, 1024, true>,
+                                      k_batch<FM, SM, 4, 512, true>};
 };
 using BatchFn = void (*)(const DevState*, BatchArgs);
 static const BatchFn* const kBatch[] = {
@@ -2881,6 +2848,12 @@ static const BatchFn* const kBatch[] = {
     BatchRow<kDefaultFM, kAutoscalerSM>::fn,
 };
 static_assert(sizeof(kBatch) / sizeof(kBatch[0]) == kNumSpecs, "one k_batch row per profile instantiation");
+static const BatchFn* const kBatchX[] = {
+    BatchRow<kRuntime, kRuntime>::xfn,
+    BatchRow<kFitFM, kFitSM>::xfn,
+    BatchRow<kDefaultFM, kDefaultSM>::xfn,
+    BatchRow<kDefaultFM, kAutoscalerSM>::xfn,
+};
 
 int batch_geometry(int N, int max_groups, int* per, int* groups) {
   for (int gi = 0; gi < kNumGeo; ++gi) {
@@ -2900,20 +2873,21 @@ int launch_batch(const DevState* st, const BatchArgs& a, int groups, int geo, in
   if (geo < 0 || geo >= kNumGeo) return -1;
   // One workgroup per CU: a dynamic LDS reservation above half a CU's 160 KB keeps the dispatcher
   // from stacking two persistent workgroups on one CU (they would share its SIMDs).
-  static bool attr_set[kNumSpecs][kNumGeo] = {};
-  if (!attr_set[spec][geo]) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(kBatch[spec][geo]),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, kBatchLdsPad) != hipSuccess)
+  const int x = a.R > 0 ? 1 : 0;  // node-sharded over xGMI mailboxes
+  const BatchFn fn = (x ? kBatchX : kBatch)[spec][geo];
+  static bool attr_set[2][kNumSpecs][kNumGeo] = {};
+  if (!attr_set[x][spec][geo]) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            kBatchLdsPad) != hipSuccess)
       return -1;
-    attr_set[spec][geo] = true;
+    attr_set[x][spec][geo] = true;
   }
   // Cooperative: the runtime refuses a grid whose workgroups cannot all be resident at once, so
   // the granule exchange never waits on a workgroup that has not started.
   BatchArgs arg = a;
   const DevState* sp = st;
   void* args[] = {(void*)&sp, (void*)&arg};
-  if (hipLaunchCooperativeKernel(reinterpret_cast<const void*>(kBatch[spec][geo]), dim3(groups),
-                                 dim3(kGeo[geo].B + 64 * kGeo[geo].SP),
+  if (hipLaunchCooperativeKernel(reinterpret_cast<const void*>(fn), dim3(groups), dim3(kGeo[geo].B),
                                  args, (unsigned)kBatchLdsPad, (hipStream_t)stream) != hipSuccess)
     return -1;
   hipLaunchKernelGGL(k_batch_fixup, dim3((a.count + 255) / 256), dim3(256), 0, (hipStream_t)stream, st, a, groups);

@@ -57,12 +57,10 @@ def test_persistent_random_clusters(seed):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("groups", [0, 5, 3, 2])
+@pytest.mark.parametrize("groups", [0, 5, 2])
 def test_persistent_fit_least_balanced(groups):
-    # config (b) shape at 3,000 nodes: no cap = 12 workgroups of 256 row threads x 1 row (+ the
-    # spare wave); a cap of 5 forces 4 workgroups of 768 x 1 (+ spare), a cap of 3 forces 3
-    # workgroups of 1024 x 1 (variant B in the candidate lane), a cap of 2 forces 2 workgroups of
-    # 512 threads x 4 rows (+ spare)
+    # config (b) shape at 3,000 nodes: no cap = 12 workgroups of 256 threads x 1 row; a cap of 5
+    # forces 3 workgroups of 1024 x 1, a cap of 2 forces 2 workgroups of 512 threads x 4 rows
     nodes, existing, pods, prof = cluster.fit_least_balanced(n_nodes=3000, n_pods=600)
     fw = GpuFramework(prof, nodes, existing, pods_hint=pods[:16])
     q, pc, _, errs = fw.compile_pods(pods)
