@@ -188,3 +188,7 @@ func (e *engine) selectVictims(q *C.kgpu_pod_query, pools *C.kgpu_pools, victims
 	rc := C.kgpu_select_victims(e.ctx, q, pools, &args, &out[0], (*C.int32_t)(unsafe.Pointer(&vout[0])), &chosen)
 	return out[:n], vout[:len(victims)], int32(chosen), kerr(e.ctx, rc)
 }
+
+// xgmiActive reports whether kgpu_comm_init mapped every peer's mailbox ring: persistent runs then
+// exchange their granules over xGMI instead of one RCCL all-gather per pod.
+func (e *engine) xgmiActive() bool { return C.kgpu_xgmi_active(e.ctx) != 0 }
