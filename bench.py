@@ -85,6 +85,8 @@ def main():
     ap.add_argument("--topo-fused", type=int, default=None, help="KGPU_OPT_TOPO_FUSED (default: the library's)")
     ap.add_argument("--no-topo-persistent", action="store_true",
                     help="topology pods through the per-pod topology launches instead of k_tbatch")
+    ap.add_argument("--max-groups", type=int, default=0,
+                    help="cap on the persistent kernels' workgroups (KGPU_OPT_PERSIST_GROUPS; 0: one per CU)")
     ap.add_argument("--shard", action="store_true",
                     help="at N=1: run the node-sharded path on a one-rank RCCL communicator (exchange overhead)")
     args = ap.parse_args()
@@ -132,6 +134,8 @@ def main():
         eng.set_option(abi.OPT_TOPO_FUSED, args.topo_fused)
     if args.no_topo_persistent:
         eng.set_option(abi.OPT_TOPO_PERSISTENT, 0)
+    if args.max_groups:
+        eng.set_option(abi.OPT_PERSIST_GROUPS, args.max_groups)
 
     def reset():
         eng.upload(fw.snap, fw.arrays)

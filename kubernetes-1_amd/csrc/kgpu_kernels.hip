@@ -1034,22 +1034,28 @@ __global__ __launch_bounds__(kBlock) void k_shard_pack(const DevState* __restric
 
 // ---------------------------------------------------------------- persistent batch kernel
 // A run of pods in queue order inside ONE launch.  Workgroup g owns nodes [g*per, (g+1)*per) and
-// keeps their resource rows in registers for the whole run (K rows per lane).  Per pod it
-// publishes one 8-byte granule -- valid bit | ((score+1) << 40 | rank40), 0 key = no feasible
-// node -- with a write-through (sc1) store into the pod's own slot row; wave 0 polls the row with
-// sc1 loads until every workgroup's granule is there, and every workgroup then derives the same
-// winner.  Slots are written once per launch (zeroed by the host), so a granule is its own flag.
+// keeps their resource rows in registers for the whole run: K slots per row lane, per = K*B - 1
+// (the last slot of the last lane is the spare below).  Per pod every workgroup publishes one
+// 8-byte granule -- valid bit | ((score+1) << 40 | rank40), 0 key = no feasible node -- with a
+// write-through (sc1) store into the pod's row of slots, and every workgroup derives the same
+// winner from the complete row.  Slots are written once per launch (zeroed by the host), so a
+// granule is its own flag.
 //
-// Software pipeline (one pod in flight): while pod i-1's granules travel, every workgroup already
-// evaluates pod i twice -- variant A on its rows as they are, variant B with pod i-1 assumed on
-// its own candidate for pod i-1 (the only row that changes if this workgroup wins i-1) -- and
-// publishes the right variant as soon as pod i-1 resolves.  Per pod the critical path is one
-// granule hop; the node evaluation overlaps it.  When the previous pod carries extended
-// resources or host ports (their columns live in memory) the winner re-evaluates its one row
-// after the assume instead.
+// Roles inside a workgroup (B row threads, then one communication wave):
+//  * the row waves evaluate pod i in two variants in one pass: variant A on the rows as they are,
+//    variant B on the spare slot, which holds this workgroup's candidate row for pod i-1 with pod
+//    i-1 assumed on it (staged in LDS when pod i-1 was published).  If this workgroup wins pod
+//    i-1, variant B (candidate slot replaced by the spare) is pod i's view of the changed row;
+//    otherwise variant A is.  The spare is just one more lane, so B costs no extra latency.
+//  * the communication wave polls pod i-1's row of granules while the row waves evaluate pod i
+//    and hands the winner over through LDS: the granule hop overlaps the evaluation.
+// Two barriers per pod: (c) pod i evaluated and pod i-1 resolved; (e) pod i published, pod i-1
+// assumed on the winning row, pod i's candidate row staged.  When pod i-1 carries extended
+// resources or host ports (columns that live in memory) no variant B applies: a workgroup that
+// wins such a pod re-evaluates its winning row after the assume, and that row's wave publishes.
 //
 // The chosen variant's feasible count goes to a side array; k_batch_fixup fills in
-// FeasibleNodes and the scored flag after the launch.  A workgroup that waits longer than
+// FeasibleNodes and the scored flag after the launch.  A poll that waits longer than
 // kSpinTimeout (lost co-residency) raises the abort word and every workgroup leaves the loop.
 constexpr uint64_t kGValid = 1ull << 63;
 constexpr uint64_t kSpinTimeout = 50000000ull;  // s_memrealtime ticks (100 MHz): 0.5 s
@@ -1074,13 +1080,13 @@ __device__ __forceinline__ void assume_regs(const kgpu_pod_query& q, NodeRes& r)
   r.np += 1;
 }
 
-// Key of one node for one pod: 0 = infeasible, else ((score+1) << 40) | rank40.
 // Wait for this lane's outstanding vector loads.  Used at the end of paths that load only for
 // some pods (extended resources, host ports): the join after them then carries no pending load,
 // so no later register write in the pod loop waits on vmcnt -- which counts stores too, and would
 // hold the evaluation behind the previous pod's write-through granule and assume stores.
 __device__ __forceinline__ void vm_drain() { __builtin_amdgcn_s_waitcnt(0x0F70); }  // vmcnt(0) only
 
+// Key of one node for one pod: 0 = infeasible, else ((score+1) << 40) | rank40.
 template <uint32_t FM, uint32_t SM>
 __device__ __forceinline__ uint64_t node_key(const DevState& st, const kgpu_pod_query& q, const NodeRes& r, int n,
                                              uint64_t tk) {
@@ -1106,34 +1112,53 @@ __device__ __forceinline__ void wave_reduce_cand(Cand& c) {
   wave_argmax(c.key, c.idx);
 }
 
+// Slots indexed [p] alternate by pod parity: a wave may write pod i+1's entry while a slower
+// wave still reads pod i's.
 template <int B>
 struct BatchShared {
-  static constexpr int W = B / 64;
-  uint64_t ka[W], kb[W];
-  int ia[W], ib[W], fa[W], fb[W];
-  uint64_t wkey;   // winning key of the resolved pod
-  int wg;          // its workgroup (-1: no feasible node)
-  int abort;
-  int cand;        // this workgroup's candidate (local index) for the pod just published, -1 none
+  static constexpr int W = B / 64;  // row waves
+  uint64_t ka[2][W], kb[2][W];      // per-wave partials of variants A and B
+  int ia[2][W], ib[2][W], fa[2][W], fb[2][W];
+  uint64_t rkey[2];                 // communication wave: winning key of pod p in slot p & 1
+  int rwg[2];                       // its granule (-1: no feasible node)
+  int rabort[2];                    // the poll gave up (abort word or timeout)
+  NodeRes brow[2];                  // pod p's candidate row (pod p-1 assumed) for pod p+1's variant B
+  int bready;                       // p + 1 once brow[p & 1] is written
+  int cslow[2];                     // slow path: candidate of pod p
+  int cready;                       // p + 1 once cslow[p & 1] is written
 };
 
-// Per-lane best over its K rows, then the workgroup's best through shuffles + LDS (variant A, and
-// variant B when `vb`: slot jb of lane `ob` replaced by keyb).  Leaves the wave partials in LDS.
+__device__ __forceinline__ void lds_release(int* f, int v) {
+  __hip_atomic_store(f, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_wait(int* f, int v) {
+  while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != v) __builtin_amdgcn_s_sleep(1);
+}
+
+__device__ __forceinline__ constexpr bool spare_slot(int j, int K, int tid, int B) {
+  return j == K - 1 && tid == B - 1;
+}
+
+// Per-lane best over its K slots, then per-wave partials of variant A (rows as they are, spare
+// excluded) and, when `vb`, variant B (slot jb of lane ob -- the candidate for the previous pod --
+// replaced by the spare, reported under the candidate's index).  Feasible counts through ballots.
 template <int K, int B>
-__device__ __forceinline__ void wg_partials(BatchShared<B>& sh, const uint64_t (&keys)[K], int lo_tid, bool vb,
-                                            int ob, int jb, uint64_t keyb) {
+__device__ __forceinline__ void wg_partials(BatchShared<B>& sh, int p, const uint64_t (&keys)[K], bool vb, int ob,
+                                            int jb, int cand) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   Cand a{0, -1, 0}, b{0, -1, 0};
-  // feasible counts through ballots (scalar popcounts), not a DPP sum chain
 #pragma unroll
   for (int j = 0; j < K; ++j) {
-    const int l = j * B + lo_tid;
-    const uint64_t k = keys[j];
+    const int l = j * B + tid;
+    const bool spare = spare_slot(j, K, tid, B);
+    const uint64_t k = spare ? 0 : keys[j];
     a.feas += __popcll(__ballot(k != 0));
     if (k > a.key) { a.key = k; a.idx = l; }
-    const uint64_t kv = (vb && tid == ob && j == jb) ? keyb : k;
-    b.feas += __popcll(__ballot(kv != 0));
-    if (kv > b.key) { b.key = kv; b.idx = l; }
+    if (vb) {
+      const uint64_t kv = spare ? keys[j] : ((tid == ob && j == jb) ? 0 : k);
+      b.feas += __popcll(__ballot(kv != 0));
+      if (kv > b.key) { b.key = kv; b.idx = spare ? cand : l; }
+    }
   }
   if (vb) {
     // the two max chains interleaved (independent DPP sequences overlap)
@@ -1148,28 +1173,53 @@ __device__ __forceinline__ void wg_partials(BatchShared<B>& sh, const uint64_t (
     wave_argmax(a.key, a.idx);
   }
   if (lane == 0) {
-    sh.ka[wave] = a.key; sh.ia[wave] = a.idx; sh.fa[wave] = a.feas;
-    sh.kb[wave] = b.key; sh.ib[wave] = b.idx; sh.fb[wave] = b.feas;
+    sh.ka[p][wave] = a.key; sh.ia[p][wave] = a.idx; sh.fa[p][wave] = a.feas;
+    sh.kb[p][wave] = b.key; sh.ib[p][wave] = b.idx; sh.fb[p][wave] = b.feas;
   }
 }
 
 template <int B>
-__device__ __forceinline__ Cand wg_combine(const BatchShared<B>& sh, bool variant_b) {
+__device__ __forceinline__ Cand wg_combine(const BatchShared<B>& sh, int p, bool variant_b) {
   Cand c{0, -1, 0};
 #pragma unroll
   for (int w = 0; w < B / 64; ++w) {
-    const uint64_t k = variant_b ? sh.kb[w] : sh.ka[w];
-    const int i = variant_b ? sh.ib[w] : sh.ia[w];
-    c.feas += variant_b ? sh.fb[w] : sh.fa[w];
+    const uint64_t k = variant_b ? sh.kb[p][w] : sh.ka[p][w];
+    const int i = variant_b ? sh.ib[p][w] : sh.ia[p][w];
+    c.feas += variant_b ? sh.fb[p][w] : sh.fa[p][w];
     if (k > c.key) { c.key = k; c.idx = i; }
   }
   return c;
 }
 
-// Wave 0: poll pod `row`'s GT granules (<= 64 * NJ) and return the winning key and granule index
-// to every lane; the abort word rides along with every sweep.  A granule counts once its top four
-// bits equal `expect` (valid bit + ring lap); the key is the rest (`kmask`).  System-scope loads
-// for a mailbox other ranks write over xGMI.  Returns false on timeout / abort.
+// Slow path: the wave holding the winning row recomputes its variant-A partial from its current
+// keys (the winning row re-evaluated) and combines it with the other waves' partials in LDS.
+template <int K, int B>
+__device__ __forceinline__ Cand wave_recombine(const BatchShared<B>& sh, int p, const uint64_t (&keys)[K]) {
+  const int tid = threadIdx.x, wave = tid >> 6;
+  Cand a{0, -1, 0};
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    const uint64_t k = spare_slot(j, K, tid, B) ? 0 : keys[j];
+    a.feas += __popcll(__ballot(k != 0));
+    if (k > a.key) { a.key = k; a.idx = j * B + tid; }
+  }
+  wave_argmax(a.key, a.idx);
+  Cand c{0, -1, 0};
+#pragma unroll
+  for (int w = 0; w < B / 64; ++w) {
+    const bool me = w == wave;
+    const uint64_t k = me ? a.key : sh.ka[p][w];
+    const int i = me ? a.idx : sh.ia[p][w];
+    c.feas += me ? a.feas : sh.fa[p][w];
+    if (k > c.key) { c.key = k; c.idx = i; }
+  }
+  return c;
+}
+
+// The communication wave: poll pod `row`'s GT granules (<= 64 * NJ) and return the winning key and
+// granule index to every lane; the abort word rides along with every sweep.  A granule counts once
+// its top four bits equal `expect` (valid bit + ring lap); the key is the rest (`kmask`).
+// System-scope loads for a mailbox other ranks write over xGMI.  Returns false on timeout / abort.
 template <int NJ>
 struct Sweep {
   uint64_t v[NJ];
@@ -1189,10 +1239,6 @@ __device__ __forceinline__ Sweep<NJ> sweep(const uint64_t* row, int G, const int
   return s;
 }
 
-// One sweep in flight at a time: a speculative next sweep left in flight when the row completes
-// would be waited for at the first reuse of its registers in the node evaluation -- and vmcnt
-// counts stores too, so that wait would also hold the evaluation behind the granule, result and
-// assume stores issued since.
 template <int NJ, bool SYS>
 __device__ __forceinline__ bool poll_row(const uint64_t* row, int G, const int32_t* abort_word, uint64_t tmask,
                                          uint64_t expect, uint64_t& wkey, int& wg) {
@@ -1200,9 +1246,6 @@ __device__ __forceinline__ bool poll_row(const uint64_t* row, int G, const int32
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   for (;;) {
     const Sweep<NJ> cur = sweep<NJ, SYS>(row, G, abort_word, expect);
-    // the abort word is examined first: a load left unconsumed on the success path would be
-    // waited for at the first reuse of its register in the node evaluation -- behind every store
-    // issued since (vmcnt counts stores too)
     if (cur.abort != 0) return false;
     bool all = true;
     uint64_t k = 0;
@@ -1229,9 +1272,10 @@ __device__ __forceinline__ bool poll_row(const uint64_t* row, int G, const int32
 
 // XG: the node-sharded instantiation (xGMI mailbox rings); the unsharded one carries none of its code.
 template <uint32_t FM, uint32_t SM, int K, int B, bool XG>
-__global__ __launch_bounds__(B) void k_batch(const DevState* __restrict__ stp, BatchArgs pa) {
+__global__ __launch_bounds__(B + 64) void k_batch(const DevState* __restrict__ stp, BatchArgs pa) {
   const DevState& st = *stp;
-  const int tid = threadIdx.x, wave = tid >> 6;
+  constexpr int W = B / 64;  // row waves; wave W communicates
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int G = gridDim.x, g = blockIdx.x;
   const int lo = g * pa.per;
   const int GT = pa.GT, gme = pa.rank * G + g;  // this workgroup's granule in every row
@@ -1246,14 +1290,68 @@ __global__ __launch_bounds__(B) void k_batch(const DevState* __restrict__ stp, B
       sh_peer_f[tid] = pa.pfeas[tid];
     }
   }
+  if (tid == 0) {
+    sh.bready = 0;
+    sh.cready = 0;
+  }
+  auto ring_row = [&](int k) -> size_t { return xg ? (size_t)((pa.xseq0 + k) % pa.R) : (size_t)k; };
+  auto ring_tag = [&](int k) -> uint64_t {
+    return xg ? (kGValid | ((uint64_t)(((pa.xseq0 + k) / pa.R) & 7) << 60)) : kGValid;
+  };
+  // phase stamps (diagnostics): per iteration i, 8 per traced workgroup (0 and last): row wave 0 --
+  // 0 start, 5 evaluated, 1 partials, 2 past barrier (c), 3 published, 4 iteration end; the
+  // communication wave -- 7 pod i-1 resolved
+  const bool tr = pa.trace && (g == 0 || g == G - 1);
+  int64_t* trow = pa.trace ? pa.trace + (g == 0 ? 0 : 8) : nullptr;
+#define KGPU_STAMP(i, k) \
+  if (tr && tid == 0) trow[(size_t)(i) * 16 + (k)] = (int64_t)__builtin_amdgcn_s_memrealtime()
 
-  // rows stay in registers; assume_row writes every change through to the node columns as well
+  if (wave == W) {
+    // ---- communication wave: pod i-1's winner, while the row waves evaluate pod i
+    constexpr int kQWords = (int)(sizeof(kgpu_pod_query) / 8);
+    static_assert(kQWords <= 64, "one query row per prefetch instruction");
+    for (int i = 0; i <= pa.count; ++i) {
+      if (i == pa.abort_at && g == 0 && lane == 0) __hip_atomic_store(pa.abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // pod i+2's query into L2 (the row waves' scalar load of it, an iteration later, then hits)
+      if (i + 2 < pa.count) {
+        const uint64_t v = lane < kQWords ? reinterpret_cast<const uint64_t*>(st.queries + pa.first + i + 2)[lane] : 0;
+        asm volatile("" ::"v"(v));
+      }
+      if (i > 0) {
+        const uint64_t* prow = pa.gran + ring_row(i - 1) * GT;
+        const uint64_t expect = ring_tag(i - 1);
+        uint64_t wkey = 0;
+        int wg = -1;
+        bool ok;
+        if constexpr (!XG)
+          ok = poll_row<4, false>(prow, GT, pa.abort, tmask, expect, wkey, wg);
+        else if (GT <= 256)
+          ok = poll_row<4, true>(prow, GT, pa.abort, tmask, expect, wkey, wg);
+        else
+          ok = poll_row<16, true>(prow, GT, pa.abort, tmask, expect, wkey, wg);
+        if (lane == 0) {
+          if (!ok) __hip_atomic_store(pa.abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const int s = (i - 1) & 1;
+          sh.rkey[s] = wkey;
+          sh.rwg[s] = wg;
+          sh.rabort[s] = ok ? 0 : 1;
+          if (tr) trow[(size_t)i * 16 + 7] = (int64_t)__builtin_amdgcn_s_memrealtime();
+        }
+      }
+      __syncthreads();  // (c)
+      if (i > 0 && sh.rabort[(i - 1) & 1]) break;
+    }
+    return;
+  }
+
+  // ---- row waves.  Rows stay in registers; assume_row writes every change through to the node
+  // columns as well.  The spare slot holds no node of its own.
   NodeRes r[K];
 #pragma unroll
   for (int j = 0; j < K; ++j) {
     const int n = lo + j * B + tid;
     r[j] = NodeRes{};
-    if (n < st.N) {
+    if (!spare_slot(j, K, tid, B) && n < st.N) {
       r[j] = load_res(st, n);
       // Allocatable never changes inside the run: LeastAllocated / MostAllocated divide through
       // exact reciprocal-plus-remainder-correction division (div_recip)
@@ -1264,63 +1362,70 @@ __global__ __launch_bounds__(B) void k_batch(const DevState* __restrict__ stp, B
   // in the loop body as a vmcnt(0) -- and vmcnt counts stores too, so every iteration would wait
   // there for the previous iteration's write-through granule and assume stores to be acknowledged.
   __builtin_amdgcn_s_waitcnt(0);
-  // phase stamps (diagnostics): per iteration i, 8 per traced workgroup (0 and last):
-  // start, evaluated, pod i-1 resolved, pod i published, iteration end
-  const bool tr = pa.trace && tid == 0 && (g == 0 || g == G - 1);
-  int64_t* trow = pa.trace ? pa.trace + (g == 0 ? 0 : 8) : nullptr;
-#define KGPU_STAMP(i, k) \
-  if (tr) trow[(size_t)(i) * 16 + (k)] = (int64_t)__builtin_amdgcn_s_memrealtime()
 
   kgpu_pod_query qp{};                      // pod i-1 (published, not yet resolved)
   kgpu_pod_query q = *cp(st.queries + pa.first);
   int cand = -1;                            // this workgroup's candidate for pod i-1 (uniform)
-  bool aborted = false;
+  bool staged = false;                      // its row is (being) staged in sh.brow[(i-1) & 1]
   for (int i = 0; i <= pa.count; ++i) {
     KGPU_STAMP(i, 0);
     const bool have_prev = i > 0;
     const bool have_cur = i < pa.count;
-    // ---- evaluate pod i: variant A on the rows as they are, variant B with pod i-1 assumed on
-    //      this workgroup's candidate (registers only; not for extended resources / host ports)
-    uint64_t keys[K];
-    const bool fast_b = have_prev && cand >= 0 && qp.scalars.count == 0 && qp.ports.count == 0;
+    const int p = i & 1;
+    // variant B applies when pod i-1's assume is a register-only change of the candidate row
+    const bool fast_b = have_prev && cand >= 0 && staged && pa.assume && qp.scalars.count == 0 && qp.ports.count == 0;
     const int ob = cand >= 0 ? cand % B : -1, jb = cand >= 0 ? cand / B : -1;
-    uint64_t keyb = 0;
+    const uint64_t tk = pod_tie_key(st.seed, pa.seq0 + i);
+    uint64_t keys[K];
     if (have_cur) {
-      const uint64_t tk = pod_tie_key(st.seed, pa.seq0 + i);
+      if (fast_b && wave == W - 1) {
+        lds_wait(&sh.bready, i);  // the candidate lane staged it right after barrier (c) of pod i-1
+        NodeRes t = sh.brow[(i - 1) & 1];
+        assume_regs(qp, t);
+        if (tid == B - 1) r[K - 1] = t;
+      }
 #pragma unroll
       for (int j = 0; j < K; ++j) {
-        const int n = lo + j * B + tid;
-        keys[j] = n < st.N ? node_key<FM, SM>(st, q, r[j], n, tk) : 0;
+        const bool spare = spare_slot(j, K, tid, B);
+        const int n = spare ? lo + cand : lo + j * B + tid;
+        keys[j] = (spare ? fast_b : n < st.N) ? node_key<FM, SM>(st, q, r[j], n, tk) : 0;
       }
       KGPU_STAMP(i, 5);
-      if (fast_b && tid == ob) {
-#pragma unroll
-        for (int j = 0; j < K; ++j)
-          if (j == jb) {
-            NodeRes rb = r[j];
-            assume_regs(qp, rb);
-            keyb = node_key<FM, SM>(st, q, rb, lo + cand, tk);
-          }
-      }
-      KGPU_STAMP(i, 6);
-      wg_partials<K, B>(sh, keys, tid, fast_b, ob, jb, keyb);
+      wg_partials<K, B>(sh, p, keys, fast_b, ob, jb, cand);
     }
     KGPU_STAMP(i, 1);
-    // the next pod's query: issued now, consumed after the hop
+    // the next pod's query: issued now, consumed after the barrier
     kgpu_pod_query qn{};
     if (i + 1 < pa.count) qn = *cp(st.queries + pa.first + i + 1);
-    __syncthreads();
-    // ---- wave 0: resolve pod i-1, then publish pod i's granule (unless this workgroup won i-1
-    //      without a precomputed variant B: it re-evaluates first)
-    auto ring_row = [&](int k) -> size_t { return xg ? (size_t)((pa.xseq0 + k) % pa.R) : (size_t)k; };
-    auto ring_tag = [&](int k) -> uint64_t {
-      return xg ? (kGValid | ((uint64_t)(((pa.xseq0 + k) / pa.R) & 7) << 60)) : kGValid;
-    };
-    const uint64_t* prow = pa.gran + ring_row(i - 1) * GT;
-    const size_t roff = ring_row(i) * GT + gme;
-    const uint64_t gtag = ring_tag(i);
+    __syncthreads();  // (c): pod i's partials are complete, pod i-1 is resolved
+    KGPU_STAMP(i, 2);
+    uint64_t wkey = 0;
+    int wg = -1;
+    if (have_prev) {
+      const int s = (i - 1) & 1;
+      if (sh.rabort[s]) break;
+      wkey = sh.rkey[s];
+      wg = sh.rwg[s];
+    }
+    const bool won = have_prev && wg == gme;
+    // ---- pod i-1's outcome: the record (unsharded: by the winning workgroup; xGMI-sharded: by
+    //      workgroup 0 of every rank, which decodes the winner's global node index from its key)
+    if (have_prev && tid == 0 && (xg ? g == 0 : (won || (wg < 0 && g == 0)))) {
+      const int pod = pa.first + i - 1;
+      kgpu_result res;
+      res.node = wg < 0 ? -1
+               : xg ? (int32_t)rank40_inv(pod_tie_key(st.seed, pa.seq0 + i - 1), wkey & kMask40, st.tie_mode)
+                    : st.node_base + lo + cand;
+      res.feasible = 0;   // k_batch_fixup
+      res.evaluated = st.n_total;
+      res.scored = 0;     // k_batch_fixup
+      res.score = wg >= 0 ? (int64_t)(wkey >> 40) - 1 : 0;
+      gp(st.results)[pod] = res;
+    }
     // publish pod i's granule (and feasible count): into this launch's rows, or into every rank's
     // mailbox ring (peer bases staged in LDS at kernel start: no pointer load on this path)
+    const size_t roff = ring_row(i) * GT + gme;
+    const uint64_t gtag = ring_tag(i);
     auto publish = [&](uint64_t key, int feas) {
       if constexpr (!XG) {
         store_sc1(pa.gran + roff, gtag | key);
@@ -1332,101 +1437,57 @@ __global__ __launch_bounds__(B) void k_batch(const DevState* __restrict__ stp, B
         }
       }
     };
-    if (wave == 0) {
-      // both variants' workgroup results are combined before the poll: after it only a select
-      Cand ca{0, -1, 0}, cb{0, -1, 0};
-      if (have_cur) {
-        ca = wg_combine<B>(sh, false);
-        cb = fast_b ? wg_combine<B>(sh, true) : ca;
-      }
-      uint64_t wkey = 0;
-      int wg = -1;
-      bool ok = true;
-      if (i == pa.abort_at && g == 0 && tid == 0) __hip_atomic_store(pa.abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (have_prev) {
-        const uint64_t expect = ring_tag(i - 1);
-        if constexpr (!XG)
-          ok = poll_row<4, false>(prow, GT, pa.abort, tmask, expect, wkey, wg);
-        else if (GT <= 256)
-          ok = poll_row<4, true>(prow, GT, pa.abort, tmask, expect, wkey, wg);
-        else
-          ok = poll_row<16, true>(prow, GT, pa.abort, tmask, expect, wkey, wg);
-      }
-      KGPU_STAMP(i, 2);
+    const bool slow = won && pa.assume && !fast_b;
+    if (have_cur && !slow) {
+      // every row wave derives the same combine; lane 0 of wave 0 publishes
+      const Cand c = wg_combine<B>(sh, p, won && fast_b);
       if (tid == 0) {
-        if (!ok) __hip_atomic_store(pa.abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        sh.abort = ok ? 0 : 1;
-        sh.wkey = wkey;
-        sh.wg = wg;
-        sh.cand = -1;
-        const bool won = have_prev && wg == gme;
-        if (ok && have_cur && !(won && !fast_b)) {
-          const Cand c = won ? cb : ca;
-          publish(c.key, c.feas);
-          sh.cand = c.key ? c.idx : -1;
-          KGPU_STAMP(i, 3);
+        publish(c.key, c.feas);
+        KGPU_STAMP(i, 3);
+      }
+      cand = c.key ? c.idx : -1;
+    }
+    if (won && pa.assume && tid == ob) {
+#pragma unroll
+      for (int j = 0; j < K; ++j)
+        if (j == jb) {
+          assume_row(st, qp, r[j], lo + (j * B + tid));
+          assume_counts(st, pa.first + i - 1, lo + (j * B + tid));
         }
-      }
     }
-    __syncthreads();
-    if (sh.abort) {
-      aborted = true;
-      break;
-    }
-    // ---- pod i-1's outcome: result record, assume on the winning row
-    if (have_prev) {
-      const uint64_t wkey = sh.wkey;
-      const int wg = sh.wg;
-      const int pod = pa.first + i - 1;
-      // the record: unsharded, by the winning workgroup; xGMI-sharded, by workgroup 0 of every
-      // rank, which decodes the winner's global node index from its key
-      if (tid == 0 && (xg ? g == 0 : ((wg >= 0 && wg == gme) || (wg < 0 && g == 0)))) {
-        kgpu_result res;
-        res.node = wg < 0 ? -1
-                 : xg ? (int32_t)rank40_inv(pod_tie_key(st.seed, pa.seq0 + i - 1), wkey & kMask40, st.tie_mode)
-                      : st.node_base + lo + cand;
-        res.feasible = 0;   // k_batch_fixup
-        res.evaluated = st.n_total;
-        res.scored = 0;     // k_batch_fixup
-        res.score = wg >= 0 ? (int64_t)(wkey >> 40) - 1 : 0;
-        gp(st.results)[pod] = res;
-      }
-      if (wg == gme) {
-        if (pa.assume && tid == ob) {
+    if (have_cur && slow) {
+      // the winning row changed in memory-resident columns: its wave evaluates it again and
+      // publishes from its own partial and the other waves' partials; the others wait for the
+      // candidate it found
+      if (wave == ob / 64) {
+        if (tid == ob) {
 #pragma unroll
           for (int j = 0; j < K; ++j)
-            if (j == jb) {
-              assume_row(st, qp, r[j], lo + cand);
-              assume_counts(st, pa.first + i - 1, lo + cand);
-            }
+            if (j == jb) keys[j] = node_key<FM, SM>(st, q, r[j], lo + (j * B + tid), tk);
         }
-        if (!fast_b && have_cur) {
-          // the winner's row changed in memory-resident columns: evaluate it again, republish
-          if (tid == ob) {
-            const uint64_t tk = pod_tie_key(st.seed, pa.seq0 + i);
-#pragma unroll
-            for (int j = 0; j < K; ++j)
-              if (j == jb) keys[j] = node_key<FM, SM>(st, q, r[j], lo + cand, tk);
-          }
-          wg_partials<K, B>(sh, keys, tid, false, -1, -1, 0);
-          __syncthreads();
-          if (tid == 0) {
-            const Cand c = wg_combine<B>(sh, false);
-            publish(c.key, c.feas);
-            sh.cand = c.key ? c.idx : -1;
-            KGPU_STAMP(i, 3);
-          }
+        const Cand c = wave_recombine<K, B>(sh, p, keys);
+        if (lane == 0) {
+          publish(c.key, c.feas);
+          sh.cslow[p] = c.key ? c.idx : -1;
+          lds_release(&sh.cready, i + 1);
         }
       }
-      __syncthreads();
+      lds_wait(&sh.cready, i + 1);
+      cand = sh.cslow[p];
+    } else if (have_cur && cand >= 0 && tid == cand % B) {
+      // stage pod i's candidate row (pod i-1 already assumed on it) for pod i+1's variant B
+#pragma unroll
+      for (int j = 0; j < K; ++j)
+        if (j == cand / B) sh.brow[p] = r[j];
+      lds_release(&sh.bready, i + 1);
     }
-    cand = sh.cand;
+    staged = have_cur && !slow && cand >= 0;
+    if (!have_cur) cand = -1;
     qp = q;
     q = qn;
     KGPU_STAMP(i, 4);
   }
 #undef KGPU_STAMP
-  (void)aborted;
 }
 
 // FeasibleNodes and the scored flag of every pod of a persistent run (generic_scheduler.go:184-191:
@@ -2828,17 +2889,17 @@ int select_spec(const int32_t* filters, int nf, const int32_t* scores, int ns, b
 struct Geo {
   int B, K;
 };
-constexpr Geo kGeo[] = {{256, 1}, {1024, 1}, {512, 4}};
-constexpr int kNumGeo = 3;
+constexpr Geo kGeo[] = {{256, 1}, {448, 1}, {960, 1}, {512, 4}};  // B row threads (+ one communication wave), K slots per lane
+constexpr int kNumGeo = 4;
 constexpr int kBatchLdsPad = 96 * 1024;
 
 template <uint32_t FM, uint32_t SM>
 struct BatchRow {
   using Fn = void (*)(const DevState*, BatchArgs);
-  static constexpr Fn fn[kNumGeo] = {k_batch<FM, SM, 1, 256, false>, k_batch<FM, SM, 1, 1024, false>,
-                                     k_batch<FM, SM, 4, 512, false>};
-  static constexpr Fn xfn[kNumGeo] = {k_batch<FM, SM, 1, 256, true>, k_batch<FM, SM, 1, 1024, true>,
-                                      k_batch<FM, SM, 4, 512, true>};
+  static constexpr Fn fn[kNumGeo] = {k_batch<FM, SM, 1, 256, false>, k_batch<FM, SM, 1, 448, false>,
+                                     k_batch<FM, SM, 1, 960, false>, k_batch<FM, SM, 4, 512, false>};
+  static constexpr Fn xfn[kNumGeo] = {k_batch<FM, SM, 1, 256, true>, k_batch<FM, SM, 1, 448, true>,
+                                      k_batch<FM, SM, 1, 960, true>, k_batch<FM, SM, 4, 512, true>};
 };
 using BatchFn = void (*)(const DevState*, BatchArgs);
 static const BatchFn* const kBatch[] = {
@@ -2857,7 +2918,7 @@ static const BatchFn* const kBatchX[] = {
 
 int batch_geometry(int N, int max_groups, int* per, int* groups) {
   for (int gi = 0; gi < kNumGeo; ++gi) {
-    const int p = kGeo[gi].B * kGeo[gi].K;
+    const int p = kGeo[gi].B * kGeo[gi].K - 1;  // the last slot of the last lane is the spare
     const int g = (N + p - 1) / p;
     if (g <= max_groups) {
       *per = p;
@@ -2887,7 +2948,7 @@ int launch_batch(const DevState* st, const BatchArgs& a, int groups, int geo, in
   BatchArgs arg = a;
   const DevState* sp = st;
   void* args[] = {(void*)&sp, (void*)&arg};
-  if (hipLaunchCooperativeKernel(reinterpret_cast<const void*>(fn), dim3(groups), dim3(kGeo[geo].B),
+  if (hipLaunchCooperativeKernel(reinterpret_cast<const void*>(fn), dim3(groups), dim3(kGeo[geo].B + 64),
                                  args, (unsigned)kBatchLdsPad, (hipStream_t)stream) != hipSuccess)
     return -1;
   hipLaunchKernelGGL(k_batch_fixup, dim3((a.count + 255) / 256), dim3(256), 0, (hipStream_t)stream, st, a, groups);

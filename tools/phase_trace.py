@@ -1,9 +1,12 @@
 #!/usr/bin/env python3
 """Per-pod phase breakdown of the persistent batch kernel (s_memrealtime, 10 ns ticks).
 
-phases per pipeline iteration i: eval = pod i evaluated (variants A and B, wave reductions);
-wait_prev = barrier + poll until pod i-1 resolved; publish = pod i's granule stored; assume =
-barrier + result record + assume of pod i-1 on the winning row; next = loop overhead."""
+phases per pipeline iteration i (row wave 0): eval = pod i evaluated (variant A on every row,
+variant B on the spare lane); partials = wave reductions; wait = barrier (c), i.e. the slowest row
+wave and the communication wave's poll of pod i-1; publish = pod i's granule stored; assume =
+pod i-1 assumed, candidate row staged, barrier (e); next = loop overhead.  resolved = the
+communication wave saw pod i-1 complete, measured from the later of the two traced publishes."""
+
 import argparse
 import os
 import sys
@@ -41,17 +44,17 @@ def main():
     for w, name in ((0, "wg0"), (1, "wglast")):
         a = t[:, w, :]
         per = np.diff(a[:, 0])
-        ph = {"evalA": a[:, 5] - a[:, 0], "evalB": a[:, 6] - a[:, 5], "partials": a[:, 1] - a[:, 6],
-              "wait_prev": a[:, 2] - a[:, 1], "publish": a[:, 3] - a[:, 2],
+        ph = {"eval": a[:, 5] - a[:, 0], "partials": a[:, 1] - a[:, 5],
+              "wait": a[:, 2] - a[:, 1], "publish": a[:, 3] - a[:, 2],
               "assume": a[:, 4] - a[:, 3], "next": a[1:, 0] - a[:-1, 4]}
         print("groups<=%d %s: per-pod %.0f ns | " % (args.groups, name, np.median(per)) +
               "  ".join("%s %.0f" % (k, np.median(v)) for k, v in ph.items()) + " (medians, ns)")
-    # hop: latest publish of pod i (of the two traced workgroups) -> pod i seen resolved
+    # hop: latest publish of pod i (of the two traced workgroups) -> pod i seen resolved by the
+    # communication wave (stamp 7 of iteration i+1)
     pub = np.maximum(t[:-1, 0, 3], t[:-1, 1, 3])
-    res0, res1 = t[1:, 0, 2], t[1:, 1, 2]
+    res0, res1 = t[1:, 0, 7], t[1:, 1, 7]
     print("publish skew (wg0 - wglast) %.0f ns; hop to wg0 %.0f ns, to wglast %.0f ns (medians)"
           % (np.median(t[:, 0, 3] - t[:, 1, 3]), np.median(res0 - pub), np.median(res1 - pub)))
-
 
 if __name__ == "__main__":
     main()
