@@ -1119,13 +1119,16 @@ struct BatchShared {
   static constexpr int W = B / 64;  // row waves
   uint64_t ka[2][W], kb[2][W];      // per-wave partials of variants A and B
   int ia[2][W], ib[2][W], fa[2][W], fb[2][W];
-  uint64_t rkey[2];                 // communication wave: winning key of pod p in slot p & 1
-  int rwg[2];                       // its granule (-1: no feasible node)
+  int rwg[2];                       // communication wave: winning granule of pod p in slot p & 1
+                                    // (-1: no feasible node)
   int rabort[2];                    // the poll gave up (abort word or timeout)
+  int candn[2];                     // this workgroup's published candidate for pod p (-1 none,
+                                    // -2: slow path, the winning row's wave publishes)
   NodeRes brow[2];                  // pod p's candidate row (pod p-1 assumed) for pod p+1's variant B
   int bready;                       // p + 1 once brow[p & 1] is written
   int cslow[2];                     // slow path: candidate of pod p
   int cready;                       // p + 1 once cslow[p & 1] is written
+  int pcount;                       // row waves that wrote their partials (W per pod)
 };
 
 __device__ __forceinline__ void lds_release(int* f, int v) {
@@ -1133,6 +1136,9 @@ __device__ __forceinline__ void lds_release(int* f, int v) {
 }
 __device__ __forceinline__ void lds_wait(int* f, int v) {
   while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != v) __builtin_amdgcn_s_sleep(1);
+}
+__device__ __forceinline__ void lds_wait_ge(int* f, int v) {
+  while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < v) __builtin_amdgcn_s_sleep(1);
 }
 
 __device__ __forceinline__ constexpr bool spare_slot(int j, int K, int tid, int B) {
@@ -1175,6 +1181,7 @@ __device__ __forceinline__ void wg_partials(BatchShared<B>& sh, int p, const uin
   if (lane == 0) {
     sh.ka[p][wave] = a.key; sh.ia[p][wave] = a.idx; sh.fa[p][wave] = a.feas;
     sh.kb[p][wave] = b.key; sh.ib[p][wave] = b.idx; sh.fb[p][wave] = b.feas;
+    __hip_atomic_fetch_add(&sh.pcount, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
 }
 
@@ -1239,33 +1246,43 @@ __device__ __forceinline__ Sweep<NJ> sweep(const uint64_t* row, int G, const int
   return s;
 }
 
+// Two sweeps in flight: the older one is examined while the newer one travels, so a row that
+// completes is seen about one round trip after its last granule lands rather than up to two.
+template <int NJ>
+__device__ __forceinline__ bool row_done(const Sweep<NJ>& cur, uint64_t tmask, uint64_t expect, uint64_t& wkey,
+                                         int& wg) {
+  const int lane = threadIdx.x & 63;
+  bool all = true;
+  uint64_t k = 0;
+  int gsel = -1;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const uint64_t v = cur.v[j];
+    if ((v & tmask) != expect) {
+      all = false;
+    } else if ((v & ~tmask) > k) {
+      k = v & ~tmask;
+      gsel = lane + 64 * j;
+    }
+  }
+  if (!__all(all)) return false;
+  wave_argmax(k, gsel);
+  wkey = k;
+  wg = k ? gsel : -1;
+  return true;
+}
 template <int NJ, bool SYS>
 __device__ __forceinline__ bool poll_row(const uint64_t* row, int G, const int32_t* abort_word, uint64_t tmask,
                                          uint64_t expect, uint64_t& wkey, int& wg) {
-  const int lane = threadIdx.x & 63;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  Sweep<NJ> a = sweep<NJ, SYS>(row, G, abort_word, expect);
   for (;;) {
-    const Sweep<NJ> cur = sweep<NJ, SYS>(row, G, abort_word, expect);
-    if (cur.abort != 0) return false;
-    bool all = true;
-    uint64_t k = 0;
-    int gsel = -1;
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const uint64_t v = cur.v[j];
-      if ((v & tmask) != expect) {
-        all = false;
-      } else if ((v & ~tmask) > k) {
-        k = v & ~tmask;
-        gsel = lane + 64 * j;
-      }
-    }
-    if (__all(all)) {
-      wave_argmax(k, gsel);
-      wkey = k;
-      wg = k ? gsel : -1;
-      return true;
-    }
+    const Sweep<NJ> b = sweep<NJ, SYS>(row, G, abort_word, expect);
+    if (a.abort != 0) return false;
+    if (row_done<NJ>(a, tmask, expect, wkey, wg)) return true;
+    a = sweep<NJ, SYS>(row, G, abort_word, expect);
+    if (b.abort != 0) return false;
+    if (row_done<NJ>(b, tmask, expect, wkey, wg)) return true;
     if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinTimeout) return false;
   }
 }
@@ -1285,61 +1302,127 @@ __global__ __launch_bounds__(B + 64) void k_batch(const DevState* __restrict__ s
   __shared__ uint64_t* sh_peer_g[XG ? kMaxRanks : 1];
   __shared__ int32_t* sh_peer_f[XG ? kMaxRanks : 1];
   if constexpr (XG) {
-    if (tid < pa.nranks) {
-      sh_peer_g[tid] = pa.pgran[tid];
-      sh_peer_f[tid] = pa.pfeas[tid];
+    if (wave == W && lane < pa.nranks) {
+      sh_peer_g[lane] = pa.pgran[lane];
+      sh_peer_f[lane] = pa.pfeas[lane];
     }
   }
   if (tid == 0) {
     sh.bready = 0;
     sh.cready = 0;
+    sh.pcount = 0;
   }
+  __syncthreads();
   auto ring_row = [&](int k) -> size_t { return xg ? (size_t)((pa.xseq0 + k) % pa.R) : (size_t)k; };
   auto ring_tag = [&](int k) -> uint64_t {
     return xg ? (kGValid | ((uint64_t)(((pa.xseq0 + k) / pa.R) & 7) << 60)) : kGValid;
   };
-  // phase stamps (diagnostics): per iteration i, 8 per traced workgroup (0 and last): row wave 0 --
-  // 0 start, 5 evaluated, 1 partials, 2 past barrier (c), 3 published, 4 iteration end; the
-  // communication wave -- 7 pod i-1 resolved
+  // publish pod i's granule (and feasible count): into this launch's rows, or into every rank's
+  // mailbox ring (peer bases staged in LDS at kernel start: no pointer load on this path)
+  auto publish = [&](int i, uint64_t key, int feas) {
+    const size_t roff = ring_row(i) * GT + gme;
+    const uint64_t gtag = ring_tag(i);
+    if constexpr (!XG) {
+      store_sc1(pa.gran + roff, gtag | key);
+      pa.feas[roff] = feas;
+    } else {
+      for (int rk = 0; rk < pa.nranks; ++rk) {
+        __hip_atomic_store(sh_peer_g[rk] + roff, gtag | key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(sh_peer_f[rk] + roff, feas, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+  };
+  // phase stamps (diagnostics): per iteration i, 8 per traced workgroup (0 and last).  Row wave 0:
+  // 0 start, 5 evaluated, 1 partials written, 2 past barrier (c), 4 iteration end.  The
+  // communication wave: 7 pod i-1 resolved, 6 pod i's partials complete, 3 pod i published.
   const bool tr = pa.trace && (g == 0 || g == G - 1);
   int64_t* trow = pa.trace ? pa.trace + (g == 0 ? 0 : 8) : nullptr;
 #define KGPU_STAMP(i, k) \
-  if (tr && tid == 0) trow[(size_t)(i) * 16 + (k)] = (int64_t)__builtin_amdgcn_s_memrealtime()
+  if (tr && (tid == 0 || tid == B)) trow[(size_t)(i) * 16 + (k)] = (int64_t)__builtin_amdgcn_s_memrealtime()
 
   if (wave == W) {
-    // ---- communication wave: pod i-1's winner, while the row waves evaluate pod i
+    // ---- communication wave: resolve pod i-1 while the row waves evaluate pod i, then combine
+    //      their partials and publish pod i (variant B when this workgroup won pod i-1), and write
+    //      pod i-1's result record
     constexpr int kQWords = (int)(sizeof(kgpu_pod_query) / 8);
     static_assert(kQWords <= 64, "one query row per prefetch instruction");
+    int cand = -1;        // this workgroup's candidate for pod i-1 (what it published)
+    bool staged = false;  // its row is staged for variant B
     for (int i = 0; i <= pa.count; ++i) {
+      const bool have_prev = i > 0, have_cur = i < pa.count;
+      const int p = i & 1;
       if (i == pa.abort_at && g == 0 && lane == 0) __hip_atomic_store(pa.abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       // pod i+2's query into L2 (the row waves' scalar load of it, an iteration later, then hits)
       if (i + 2 < pa.count) {
         const uint64_t v = lane < kQWords ? reinterpret_cast<const uint64_t*>(st.queries + pa.first + i + 2)[lane] : 0;
         asm volatile("" ::"v"(v));
       }
-      if (i > 0) {
+      bool qmem = false;  // pod i-1 carries extended resources or host ports: no variant B
+      if (have_prev) {
+        const kgpu_pod_query* qq = st.queries + pa.first + i - 1;
+        qmem = (cp(qq)->scalars.count | cp(qq)->ports.count) != 0;
+      }
+      const bool fast_b = have_prev && cand >= 0 && staged && pa.assume && !qmem;
+      uint64_t wkey = 0;
+      int wg = -1;
+      bool ok = true;
+      if (have_prev) {
         const uint64_t* prow = pa.gran + ring_row(i - 1) * GT;
         const uint64_t expect = ring_tag(i - 1);
-        uint64_t wkey = 0;
-        int wg = -1;
-        bool ok;
         if constexpr (!XG)
           ok = poll_row<4, false>(prow, GT, pa.abort, tmask, expect, wkey, wg);
         else if (GT <= 256)
           ok = poll_row<4, true>(prow, GT, pa.abort, tmask, expect, wkey, wg);
         else
           ok = poll_row<16, true>(prow, GT, pa.abort, tmask, expect, wkey, wg);
-        if (lane == 0) {
-          if (!ok) __hip_atomic_store(pa.abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          const int s = (i - 1) & 1;
-          sh.rkey[s] = wkey;
-          sh.rwg[s] = wg;
-          sh.rabort[s] = ok ? 0 : 1;
-          if (tr) trow[(size_t)i * 16 + 7] = (int64_t)__builtin_amdgcn_s_memrealtime();
+        KGPU_STAMP(i, 7);
+      }
+      const bool won = have_prev && wg == gme;
+      const bool slow = have_cur && won && pa.assume && !fast_b;
+      int cn = -1;
+      if (ok) {
+        // pod i-1's record (unsharded: by the winning workgroup; xGMI-sharded: by workgroup 0 of
+        // every rank, which decodes the winner's global node index from its key)
+        if (have_prev && lane == 0 && (xg ? g == 0 : (won || (wg < 0 && g == 0)))) {
+          kgpu_result res;
+          res.node = wg < 0 ? -1
+                   : xg ? (int32_t)rank40_inv(pod_tie_key(st.seed, pa.seq0 + i - 1), wkey & kMask40, st.tie_mode)
+                        : st.node_base + lo + cand;
+          res.feasible = 0;   // k_batch_fixup
+          res.evaluated = st.n_total;
+          res.scored = 0;     // k_batch_fixup
+          res.score = wg >= 0 ? (int64_t)(wkey >> 40) - 1 : 0;
+          gp(st.results)[pa.first + i - 1] = res;
         }
+        if (have_cur && !slow) {
+          lds_wait_ge(&sh.pcount, W * (i + 1));
+          KGPU_STAMP(i, 6);
+          const Cand c = wg_combine<B>(sh, p, won && fast_b);
+          if (lane == 0) publish(i, c.key, c.feas);
+          KGPU_STAMP(i, 3);
+          cn = c.key ? c.idx : -1;
+        } else if (slow) {
+          cn = -2;
+        }
+      } else if (lane == 0) {
+        __hip_atomic_store(pa.abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (lane == 0) {
+        if (have_prev) {
+          sh.rwg[(i - 1) & 1] = wg;
+          sh.rabort[(i - 1) & 1] = ok ? 0 : 1;
+        }
+        sh.candn[p] = cn;
       }
       __syncthreads();  // (c)
-      if (i > 0 && sh.rabort[(i - 1) & 1]) break;
+      if (!ok) break;
+      if (slow) {
+        lds_wait(&sh.cready, i + 1);
+        cand = sh.cslow[p];
+      } else {
+        cand = cn;
+      }
+      staged = have_cur && !slow && cand >= 0;
     }
     return;
   }
@@ -1375,9 +1458,9 @@ __global__ __launch_bounds__(B + 64) void k_batch(const DevState* __restrict__ s
     // variant B applies when pod i-1's assume is a register-only change of the candidate row
     const bool fast_b = have_prev && cand >= 0 && staged && pa.assume && qp.scalars.count == 0 && qp.ports.count == 0;
     const int ob = cand >= 0 ? cand % B : -1, jb = cand >= 0 ? cand / B : -1;
-    const uint64_t tk = pod_tie_key(st.seed, pa.seq0 + i);
     uint64_t keys[K];
     if (have_cur) {
+      const uint64_t tk = pod_tie_key(st.seed, pa.seq0 + i);
       if (fast_b && wave == W - 1) {
         lds_wait(&sh.bready, i);  // the candidate lane staged it right after barrier (c) of pod i-1
         NodeRes t = sh.brow[(i - 1) & 1];
@@ -1397,56 +1480,16 @@ __global__ __launch_bounds__(B + 64) void k_batch(const DevState* __restrict__ s
     // the next pod's query: issued now, consumed after the barrier
     kgpu_pod_query qn{};
     if (i + 1 < pa.count) qn = *cp(st.queries + pa.first + i + 1);
-    __syncthreads();  // (c): pod i's partials are complete, pod i-1 is resolved
+    __syncthreads();  // (c): pod i-1 resolved and pod i published (communication wave)
     KGPU_STAMP(i, 2);
-    uint64_t wkey = 0;
     int wg = -1;
     if (have_prev) {
       const int s = (i - 1) & 1;
       if (sh.rabort[s]) break;
-      wkey = sh.rkey[s];
       wg = sh.rwg[s];
     }
     const bool won = have_prev && wg == gme;
-    // ---- pod i-1's outcome: the record (unsharded: by the winning workgroup; xGMI-sharded: by
-    //      workgroup 0 of every rank, which decodes the winner's global node index from its key)
-    if (have_prev && tid == 0 && (xg ? g == 0 : (won || (wg < 0 && g == 0)))) {
-      const int pod = pa.first + i - 1;
-      kgpu_result res;
-      res.node = wg < 0 ? -1
-               : xg ? (int32_t)rank40_inv(pod_tie_key(st.seed, pa.seq0 + i - 1), wkey & kMask40, st.tie_mode)
-                    : st.node_base + lo + cand;
-      res.feasible = 0;   // k_batch_fixup
-      res.evaluated = st.n_total;
-      res.scored = 0;     // k_batch_fixup
-      res.score = wg >= 0 ? (int64_t)(wkey >> 40) - 1 : 0;
-      gp(st.results)[pod] = res;
-    }
-    // publish pod i's granule (and feasible count): into this launch's rows, or into every rank's
-    // mailbox ring (peer bases staged in LDS at kernel start: no pointer load on this path)
-    const size_t roff = ring_row(i) * GT + gme;
-    const uint64_t gtag = ring_tag(i);
-    auto publish = [&](uint64_t key, int feas) {
-      if constexpr (!XG) {
-        store_sc1(pa.gran + roff, gtag | key);
-        pa.feas[roff] = feas;
-      } else {
-        for (int rk = 0; rk < pa.nranks; ++rk) {
-          __hip_atomic_store(sh_peer_g[rk] + roff, gtag | key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          __hip_atomic_store(sh_peer_f[rk] + roff, feas, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-      }
-    };
-    const bool slow = won && pa.assume && !fast_b;
-    if (have_cur && !slow) {
-      // every row wave derives the same combine; lane 0 of wave 0 publishes
-      const Cand c = wg_combine<B>(sh, p, won && fast_b);
-      if (tid == 0) {
-        publish(c.key, c.feas);
-        KGPU_STAMP(i, 3);
-      }
-      cand = c.key ? c.idx : -1;
-    }
+    const int cn = have_cur ? sh.candn[p] : -1;
     if (won && pa.assume && tid == ob) {
 #pragma unroll
       for (int j = 0; j < K; ++j)
@@ -1455,34 +1498,38 @@ __global__ __launch_bounds__(B + 64) void k_batch(const DevState* __restrict__ s
           assume_counts(st, pa.first + i - 1, lo + (j * B + tid));
         }
     }
-    if (have_cur && slow) {
-      // the winning row changed in memory-resident columns: its wave evaluates it again and
-      // publishes from its own partial and the other waves' partials; the others wait for the
-      // candidate it found
+    const bool slow = cn == -2;
+    if (slow) {
+      // pod i-1 changed memory-resident columns of this workgroup's winning row: that row's wave
+      // evaluates it again and publishes from its own partial and the other waves' partials;
+      // the others wait for the candidate it found
       if (wave == ob / 64) {
         if (tid == ob) {
+          const uint64_t tk = pod_tie_key(st.seed, pa.seq0 + i);
 #pragma unroll
           for (int j = 0; j < K; ++j)
             if (j == jb) keys[j] = node_key<FM, SM>(st, q, r[j], lo + (j * B + tid), tk);
         }
         const Cand c = wave_recombine<K, B>(sh, p, keys);
         if (lane == 0) {
-          publish(c.key, c.feas);
+          publish(i, c.key, c.feas);
           sh.cslow[p] = c.key ? c.idx : -1;
           lds_release(&sh.cready, i + 1);
         }
       }
       lds_wait(&sh.cready, i + 1);
       cand = sh.cslow[p];
-    } else if (have_cur && cand >= 0 && tid == cand % B) {
-      // stage pod i's candidate row (pod i-1 already assumed on it) for pod i+1's variant B
+    } else {
+      cand = cn;
+      if (cand >= 0 && tid == cand % B) {
+        // stage pod i's candidate row (pod i-1 already assumed on it) for pod i+1's variant B
 #pragma unroll
-      for (int j = 0; j < K; ++j)
-        if (j == cand / B) sh.brow[p] = r[j];
-      lds_release(&sh.bready, i + 1);
+        for (int j = 0; j < K; ++j)
+          if (j == cand / B) sh.brow[p] = r[j];
+        lds_release(&sh.bready, i + 1);
+      }
     }
     staged = have_cur && !slow && cand >= 0;
-    if (!have_cur) cand = -1;
     qp = q;
     q = qn;
     KGPU_STAMP(i, 4);

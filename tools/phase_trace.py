@@ -1,11 +1,13 @@
 #!/usr/bin/env python3
 """Per-pod phase breakdown of the persistent batch kernel (s_memrealtime, 10 ns ticks).
 
-phases per pipeline iteration i (row wave 0): eval = pod i evaluated (variant A on every row,
-variant B on the spare lane); partials = wave reductions; wait = barrier (c), i.e. the slowest row
-wave and the communication wave's poll of pod i-1; publish = pod i's granule stored; assume =
-pod i-1 assumed, candidate row staged, barrier (e); next = loop overhead.  resolved = the
-communication wave saw pod i-1 complete, measured from the later of the two traced publishes."""
+phases per pipeline iteration i.  Row wave 0: eval = pod i evaluated (variant A on every row,
+variant B on the spare lane); partials = wave reductions; wait = barrier (c), i.e. the slowest
+row wave and the communication wave; post = pod i-1 assumed, pod i's candidate row staged; next =
+loop overhead.  Communication wave: poll_vs_rows = pod i-1 resolved minus wave 0's partials of
+pod i (positive: the granule hop, not the evaluation, sets the pace); publish = pod i published
+after the later of its partials and pod i-1's resolution; hop = latest publish of pod i (of the
+two traced workgroups) to pod i seen resolved."""
 
 import argparse
 import os
@@ -45,8 +47,9 @@ def main():
         a = t[:, w, :]
         per = np.diff(a[:, 0])
         ph = {"eval": a[:, 5] - a[:, 0], "partials": a[:, 1] - a[:, 5],
-              "wait": a[:, 2] - a[:, 1], "publish": a[:, 3] - a[:, 2],
-              "assume": a[:, 4] - a[:, 3], "next": a[1:, 0] - a[:-1, 4]}
+              "wait": a[:, 2] - a[:, 1], "post": a[:, 4] - a[:, 2], "next": a[1:, 0] - a[:-1, 4],
+              "poll_vs_rows": a[1:, 7] - a[1:, 1],
+              "publish": a[1:, 3] - np.maximum(a[1:, 6], a[1:, 7])}
         print("groups<=%d %s: per-pod %.0f ns | " % (args.groups, name, np.median(per)) +
               "  ".join("%s %.0f" % (k, np.median(v)) for k, v in ph.items()) + " (medians, ns)")
     # hop: latest publish of pod i (of the two traced workgroups) -> pod i seen resolved by the
