@@ -31,6 +31,9 @@ using kgpu::PodArgs;
 struct DevBuf {
   void* p = nullptr;
   size_t bytes = 0;
+  // host copy of the last pool uploaded into p (upload_pool skips an identical re-upload)
+  std::vector<char> shadow;
+  const void* shadow_p = nullptr;
 };
 
 struct kgpu_ctx {
@@ -46,6 +49,7 @@ struct kgpu_ctx {
   // grow-only batch buffers
   DevBuf queries, reqs, ints, words, node_terms, pref_terms, spreads, pod_terms, scalars, ports, results;
   DevBuf dstate;     // device copy of the DevState used by the kernels of the current batch
+  DevBuf ticket;     // k_final's last-workgroup ticket (zero between launches)
   DevState st_batch{};  // its host source (kept alive for the async copy)
   bool timing = false;
   bool persistent = true;  // KGPU_OPT_PERSISTENT
@@ -128,6 +132,8 @@ struct kgpu_ctx {
   DevBuf flags_buf;                                // DevState::port_overflow
   DevBuf d_stage, d_remap, d_from;
   void* stage_host = nullptr;                      // pinned staging block of a delta launch
+  void* cyc_host = nullptr;                        // pinned staging of a short cycle: DevState + queries
+                                                   // out, results + abort word + port overflow back
   size_t stage_cap = 0;
   bool last_diag = false;
   std::vector<hipEvent_t> ev_pool;
@@ -221,7 +227,23 @@ template <class T>
 int upload_pool(kgpu_ctx* c, DevBuf& b, const T* src, int32_t n, const T** dst) {
   int rc = ensure(c, b, sizeof(T) * (size_t)std::max(n, 1));
   if (rc) return rc;
-  if (n > 0) HIP_OK(c, hipMemcpyAsync(b.p, src, sizeof(T) * (size_t)n, hipMemcpyHostToDevice, c->stream));
+  const size_t bytes = sizeof(T) * (size_t)std::max(n, 0);
+  // A caller that passes the same pools every cycle (the batch's pools, one pod at a time) pays
+  // one copy, not one per cycle: the device copy is current when the bytes equal the last upload
+  // into this same allocation.  Pools above kPoolShadowMax are always copied.
+  constexpr size_t kPoolShadowMax = 256 * 1024;
+  const bool current = n > 0 && b.shadow_p == b.p && b.shadow.size() == bytes &&
+                       std::memcmp(b.shadow.data(), src, bytes) == 0;
+  if (n > 0 && !current) {
+    HIP_OK(c, hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, c->stream));
+    if (bytes <= kPoolShadowMax) {
+      b.shadow.assign(reinterpret_cast<const char*>(src), reinterpret_cast<const char*>(src) + bytes);
+      b.shadow_p = b.p;
+    } else {
+      b.shadow.clear();
+      b.shadow_p = nullptr;
+    }
+  }
   *dst = static_cast<const T*>(b.p);
   return KGPU_OK;
 }
@@ -1407,6 +1429,14 @@ int stage_topology(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_
   return KGPU_OK;
 }
 
+// Short cycles: at most kShortCycle pods.  Device block c->dstate = DevState | queries (at
+// kDsQueryOff); pinned c->cyc_host = the same image, then the results read back (at kCycResOff).
+constexpr int32_t kShortCycle = 64;
+constexpr size_t kDsQueryOff = (sizeof(DevState) + 255) & ~(size_t)255;
+constexpr size_t kCycResOff = (kDsQueryOff + sizeof(kgpu_pod_query) * kShortCycle + 255) & ~(size_t)255;
+constexpr size_t kCycResBytes = sizeof(kgpu_result) * kShortCycle;
+constexpr size_t kCycHostBytes = kCycResOff + kCycResBytes;
+
 int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools* pools, int64_t first_seq,
               kgpu_result* results, kgpu_stats* stats, bool diag, int32_t assume) {
   if (!c->uploaded) return fail(c, KGPU_E_STATE, "no snapshot uploaded");
@@ -1443,16 +1473,36 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
     for (int32_t i = 0; i < n; ++i) batch_ports += qs[i].ports.count;
   if ((rc = reserve_ports(c, batch_ports))) return rc;
   if ((rc = upload_pools(c, pools))) return rc;
-  if ((rc = ensure(c, c->queries, sizeof(kgpu_pod_query) * (size_t)n))) return rc;
-  HIP_OK(c, hipMemcpyAsync(c->queries.p, qs, sizeof(kgpu_pod_query) * (size_t)n, hipMemcpyHostToDevice, c->stream));
-  if ((rc = ensure(c, c->results, sizeof(kgpu_result) * (size_t)n))) return rc;
+  // A short cycle (kgpu_schedule_one, small batches) moves its DevState and queries with ONE copy
+  // from pinned memory -- the queries sit right after the DevState in the same device block -- and
+  // reads its results, abort word and port-overflow word back with one copy: every stream
+  // operation saved is several microseconds of the per-cycle latency.
+  const bool short_cycle = n <= kShortCycle;
+  if (short_cycle) {
+    if (!c->cyc_host) HIP_OK(c, hipHostMalloc(&c->cyc_host, kCycHostBytes, hipHostMallocDefault));
+    if ((rc = ensure(c, c->dstate, kDsQueryOff + sizeof(kgpu_pod_query) * kShortCycle))) return rc;
+    if ((rc = ensure(c, c->results, kCycResBytes))) return rc;
+  } else {
+    if ((rc = ensure(c, c->queries, sizeof(kgpu_pod_query) * (size_t)n))) return rc;
+    HIP_OK(c, hipMemcpyAsync(c->queries.p, qs, sizeof(kgpu_pod_query) * (size_t)n, hipMemcpyHostToDevice, c->stream));
+    if ((rc = ensure(c, c->results, sizeof(kgpu_result) * (size_t)n))) return rc;
+  }
+  if (!c->ticket.p) {
+    if ((rc = ensure(c, c->ticket, 64))) return rc;
+    HIP_OK(c, hipMemset(c->ticket.p, 0, 64));
+  }
   DevState st = c->st;
-  st.queries = static_cast<const kgpu_pod_query*>(c->queries.p);
+  st.ticket = static_cast<int32_t*>(c->ticket.p);
+  st.queries = short_cycle ? reinterpret_cast<const kgpu_pod_query*>(static_cast<char*>(c->dstate.p) + kDsQueryOff)
+                           : static_cast<const kgpu_pod_query*>(c->queries.p);
   st.results = static_cast<kgpu_result*>(c->results.p);
+  // Per-plugin scores of a diagnostic cycle: every pod of a batch without topology pods goes
+  // through k_eval, which then zeroes each node's rows itself; otherwise two memsets do.
+  const bool zero_diag = diag && !topo_on && c->comm == nullptr;
   if (!diag) {
     st.diag_raw = nullptr;
     st.diag_norm = nullptr;
-  } else {
+  } else if (!zero_diag) {
     HIP_OK(c, hipMemsetAsync(st.diag_raw, 0, sizeof(int64_t) * KGPU_NUM_SCORES * (size_t)st.N, c->stream));
     HIP_OK(c, hipMemsetAsync(st.diag_norm, 0, sizeof(int64_t) * KGPU_NUM_SCORES * (size_t)st.N, c->stream));
   }
@@ -1468,11 +1518,20 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
   }
   if ((rc = ensure(c, c->dstate, sizeof(DevState)))) return rc;
   c->st_batch = st;
-  HIP_OK(c, hipMemcpyAsync(c->dstate.p, &c->st_batch, sizeof(DevState), hipMemcpyHostToDevice, c->stream));
+  if (short_cycle) {
+    char* h = static_cast<char*>(c->cyc_host);
+    std::memcpy(h, &c->st_batch, sizeof(DevState));
+    std::memcpy(h + kDsQueryOff, qs, sizeof(kgpu_pod_query) * (size_t)n);
+    HIP_OK(c, hipMemcpyAsync(c->dstate.p, h, kDsQueryOff + sizeof(kgpu_pod_query) * (size_t)n, hipMemcpyHostToDevice,
+                             c->stream));
+  } else {
+    HIP_OK(c, hipMemcpyAsync(c->dstate.p, &c->st_batch, sizeof(DevState), hipMemcpyHostToDevice, c->stream));
+  }
   const DevState* dst = static_cast<const DevState*>(c->dstate.p);
   const int blocks = kgpu::eval_blocks(st.N);
   hipEvent_t t0 = get_event(c, 0), t1 = get_event(c, 1);
-  HIP_OK(c, hipEventRecord(t0, c->stream));
+  const bool timed = stats != nullptr || c->timing;  // the cycle's device time is reported in stats only
+  if (timed) HIP_OK(c, hipEventRecord(t0, c->stream));
   size_t ev = 2;
   int64_t timed_passes = 0;
   // Persistent geometry: one workgroup per CU at most, K node rows per lane in registers.
@@ -1523,13 +1582,14 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
   // one abort word for every persistent run of this batch (OR-ed on the device)
   int rc_abort = ensure(c, c->abort_buf, 64);
   if (rc_abort) return rc_abort;
-  HIP_OK(c, hipMemsetAsync(c->abort_buf.p, 0, 64, c->stream));
   int32_t* abort_word = static_cast<int32_t*>(c->abort_buf.p);
   int tper = 0, tgroups = 0;
   const int tgeo = (topo_on && c->tfast && !diag && !sharded && !cut && !nom_dev && st.K <= 64)
                        ? kgpu::tbatch_geometry(st.N, std::min(c->max_groups > 0 ? std::min(c->max_groups, c->n_cus) : c->n_cus, 256),
                                                &tper, &tgroups)
                        : -1;
+  // zeroed only when a persistent run can start (a one-launch-per-pod cycle never reads it)
+  if (kidx >= 0 || tgeo >= 0) HIP_OK(c, hipMemsetAsync(c->abort_buf.p, 0, 64, c->stream));
   std::deque<TRun> runs;
   int32_t scratch_zeroed_for = -1;
   int32_t i = 0;
@@ -1699,6 +1759,7 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
       // one launch per pod; the next launch resolves (and assumes) the previous pod's winner
       while (j < n && (kidx < 0 || norm[(size_t)j]) && !topo[(size_t)j]) ++j;
       int prev = -1;
+      bool resolved_in_final = false;
       for (int32_t k = i; k < j; ++k) {
         PodArgs a{};
         a.pod = k;
@@ -1709,8 +1770,12 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
         a.norm = (diag || cut || needs_norm(c, qs[k], pools)) ? 1 : 0;
         a.assume = assume;
         a.diag = diag ? 1 : 0;
+        a.zero_diag = zero_diag ? 1 : 0;
         a.cut = cut ? 1 : 0;
         a.seq = first_seq + k;
+        // the chain's last pod with a normalize pass: k_final's last workgroup resolves it
+        a.resolve_self = (k == j - 1 && a.norm && !sharded) ? 1 : 0;
+        resolved_in_final = a.resolve_self != 0;
         if (c->timing) HIP_OK(c, hipEventRecord(get_event(c, ev), c->stream));
         if (nom_dev && kgpu::launch_victims(dst, nom_dev, st.N, c->stream))
           return fail(c, KGPU_E_DEVICE, "k_victims launch failed");
@@ -1727,24 +1792,29 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
         if (sharded && (rc = exchange(a.parity, 0))) return rc;
         prev = k;
       }
-      PodArgs r{};
-      r.pod = -1;
-      r.prev = prev;
-      r.prev_blocks = blocks;
-      r.prev_parity = prev & 1;
-      r.assume = assume;
-      r.cut = cut ? 1 : 0;
-      if (kgpu::launch_resolve(dst, st.N, r, c->stream)) return fail(c, KGPU_E_DEVICE, "k_resolve launch failed");
+      if (!resolved_in_final) {
+        PodArgs r{};
+        r.pod = -1;
+        r.prev = prev;
+        r.prev_blocks = blocks;
+        r.prev_parity = prev & 1;
+        r.assume = assume;
+        r.cut = cut ? 1 : 0;
+        if (kgpu::launch_resolve(dst, st.N, r, c->stream)) return fail(c, KGPU_E_DEVICE, "k_resolve launch failed");
+      }
     }
     i = j;
   }
-  HIP_OK(c, hipEventRecord(t1, c->stream));
-  HIP_OK(c, hipMemcpyAsync(results, st.results, sizeof(kgpu_result) * (size_t)n, hipMemcpyDeviceToHost, c->stream));
+  if (timed) HIP_OK(c, hipEventRecord(t1, c->stream));
+  kgpu_result* res_host = short_cycle ? reinterpret_cast<kgpu_result*>(static_cast<char*>(c->cyc_host) + kCycResOff)
+                                      : results;
+  HIP_OK(c, hipMemcpyAsync(res_host, st.results, sizeof(kgpu_result) * (size_t)n, hipMemcpyDeviceToHost, c->stream));
   if (used_persistent)
     HIP_OK(c, hipMemcpyAsync(&c->abort_host, abort_word, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
   int32_t port_overflow = 0;
   if (batch_ports) HIP_OK(c, hipMemcpyAsync(&port_overflow, c->st.port_overflow, 4, hipMemcpyDeviceToHost, c->stream));
   HIP_OK(c, hipStreamSynchronize(c->stream));
+  if (short_cycle) std::memcpy(results, res_host, sizeof(kgpu_result) * (size_t)n);
   c->port_bound += batch_ports;
   if (port_overflow) {
     c->uploaded = false;
@@ -2505,7 +2575,7 @@ int kgpu_destroy(kgpu_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   free_all(c->snap_allocs);
   free_all(c->work_allocs);
-  for (DevBuf* b : {&c->dstate, &c->queries, &c->reqs, &c->ints, &c->words, &c->node_terms, &c->pref_terms, &c->spreads,
+  for (DevBuf* b : {&c->dstate, &c->ticket, &c->queries, &c->reqs, &c->ints, &c->words, &c->node_terms, &c->pref_terms, &c->spreads,
                     &c->pod_terms, &c->scalars, &c->ports, &c->results, &c->gran, &c->trace, &c->d_classes,
                     &c->d_citems, &c->d_tclasses, &c->d_creqs, &c->d_cints, &c->d_plans, &c->d_aux,
                     &c->d_aux_terms, &c->scratch, &c->d_pods, &c->gbar, &c->cut_buf, &c->t_plans, &c->t_aux,
@@ -2521,6 +2591,7 @@ int kgpu_destroy(kgpu_ctx* c) {
     if (q) (void)hipIpcCloseMemHandle(q);
   if (c->xg_box.p) (void)hipFree(c->xg_box.p);
   if (c->stage_host) (void)hipHostFree(c->stage_host);
+  if (c->cyc_host) (void)hipHostFree(c->cyc_host);
   if (c->st.mcnt) (void)hipFree(c->st.mcnt);
   if (c->st.tcnt) (void)hipFree(c->st.tcnt);
   if (c->shard.p) (void)hipFree(c->shard.p);

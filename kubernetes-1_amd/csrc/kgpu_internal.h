@@ -217,6 +217,8 @@ struct DevState {
   // node has no nominated pods); k_eval / k_topo_filter report it instead of their own verdict.
   // Null when the nominator is empty.
   const uint32_t* nom_status;
+  // zeroed word: k_final's last workgroup ticket when it resolves its own pod (PodArgs.resolve_self)
+  int32_t* ticket;
 };
 // Filter status word of a node the cycle never examined (findNodesThatPassFilters stopped before
 // it), or of the feasible node whose discovery cancelled the search: not in `filtered` and not in
@@ -234,6 +236,8 @@ struct PodArgs {
   int32_t assume;       // apply NodeInfo.AddPod for resolved winners
   int32_t diag;         // write per-plugin raw/normalized scores
   int32_t cut;          // 1: numFeasibleNodesToFind < N -- k_cut trims the feasible set (R2)
+  int32_t zero_diag;    // 1: k_eval zeroes every node's diag rows itself (no memset launches)
+  int32_t resolve_self; // 1: k_final's last workgroup resolves and assumes `pod` (no k_resolve launch)
   int32_t pad;
   int64_t seq;          // tie-break sequence number of `pod`
 };

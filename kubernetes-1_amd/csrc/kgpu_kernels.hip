@@ -766,10 +766,10 @@ __device__ __forceinline__ Winner prev_winner(const DevState& st, const PodArgs&
 // The pending pod's outcome (generic_scheduler.go:171-208): FitError, the len==1 shortcut, or
 // the scored winner.  Returns the local row to assume (-1 none).
 __device__ __forceinline__ int settle_prev(const DevState& st, const PodArgs& a, const kgpu_pod_query& pq,
-                                           const Winner& w, int gidx) {
+                                           const Winner& w, int gidx, bool writer) {
   const bool error = (pq.flags & KGPU_Q_SCORE_ERROR) && w.feasible >= 2;
   const bool placed = w.feasible > 0 && !error;
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
+  if (writer) {
     kgpu_result r;
     r.node = placed ? gidx : (error ? -2 : -1);
     r.feasible = w.feasible;
@@ -806,7 +806,7 @@ __global__ __launch_bounds__(kBlock) void k_eval(const DevState* __restrict__ st
   if (a.prev >= 0) {
     int gidx;
     const Winner w = prev_winner(st, a, &gidx);
-    assume_idx = settle_prev(st, a, *cp(pq), w, gidx);
+    assume_idx = settle_prev(st, a, *cp(pq), w, gidx, blockIdx.x == 0 && threadIdx.x == 0);
   }
   const uint64_t tk = pod_tie_key(st.seed, a.seq);
   const bool write_nodes = a.norm || a.diag;
@@ -818,6 +818,15 @@ __global__ __launch_bounds__(kBlock) void k_eval(const DevState* __restrict__ st
     if (n == assume_idx) {
       assume_row(st, *cp(pq), r, n);
       assume_counts(st, a.prev, n);
+    }
+    if (a.zero_diag) {
+      // a diagnostic cycle without memsets: this node's rows start at 0 (a plugin outside the
+      // profile, or a node that fails a filter, reads 0 as after hipMemset)
+#pragma unroll
+      for (int s = 0; s < KGPU_NUM_SCORES; ++s) {
+        gp(st.diag_raw)[(size_t)s * st.N + n] = 0;
+        gp(st.diag_norm)[(size_t)s * st.N + n] = 0;
+      }
     }
     NodeEval e{0, 0, 0, 0};
     // nominated pods: a failed first pass (k_victims, nominated mode) is the node's verdict
@@ -894,6 +903,38 @@ __global__ __launch_bounds__(kBlock) void k_final(const DevState* __restrict__ s
   wave_reduce_key(best, best_i);
   bf = wave_reduce_sum(bf);
   if (threadIdx.x == 0) gp(st.kbuf)[(size_t)a.parity * kMaxBlocks + blockIdx.x] = BlkKey{best, best_i, bf};
+  if (a.resolve_self) {
+    // The last workgroup to finish resolves this pod -- selectHost, the result record and the
+    // assume -- in place of a k_resolve launch (the end of a short cycle).  Release / acquire
+    // fences around the ticket make every workgroup's partial visible to it across XCDs.
+    __shared__ int last;
+    if (threadIdx.x == 0) {
+      __threadfence();
+      last = atomicAdd(st.ticket, 1) == (int)gridDim.x - 1;
+    }
+    __syncthreads();
+    if (last) {
+      __threadfence();
+      PodArgs r{};
+      r.prev = a.pod;
+      r.prev_blocks = (int32_t)gridDim.x;
+      r.prev_parity = a.parity;
+      r.assume = a.assume;
+      r.cut = a.cut;
+      int gidx;
+      const Winner w = prev_winner(st, r, &gidx);
+      const kgpu_pod_query pq = *cp(st.queries + a.pod);
+      const int idx = settle_prev(st, r, pq, w, gidx, threadIdx.x == 0);
+      if (threadIdx.x == 0) {
+        if (idx >= 0) {
+          NodeRes row = load_res(st, idx);
+          assume_row(st, pq, row, idx);
+          assume_counts(st, a.pod, idx);
+        }
+        __hip_atomic_store(st.ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // for the next cycle
+      }
+    }
+  }
 }
 
 // Resolve-only launch (end of a batch / single cycle), with the evaluation grid's chunk mapping
@@ -905,7 +946,7 @@ __global__ __launch_bounds__(kBlock) void k_resolve(const DevState* __restrict__
   int gidx;
   const Winner w = prev_winner(st, a, &gidx);
   const kgpu_pod_query pq = *cp(st.queries + a.prev);
-  const int idx = settle_prev(st, a, pq, w, gidx);
+  const int idx = settle_prev(st, a, pq, w, gidx, blockIdx.x == 0 && threadIdx.x == 0);
   if (idx >= lo && idx < hi && ((idx - lo) % kBlock) == (int)threadIdx.x) {
     NodeRes r = load_res(st, idx);
     assume_row(st, pq, r, idx);
@@ -1994,7 +2035,7 @@ __device__ __forceinline__ void topo_resolve(const DevState* __restrict__ stp, P
   int gidx;
   const Winner w = prev_winner(st, a, &gidx);
   const kgpu_pod_query pq = *cp(st.queries + a.prev);
-  const int idx = settle_prev(st, a, pq, w, gidx);
+  const int idx = settle_prev(st, a, pq, w, gidx, blockIdx.x == 0 && threadIdx.x == 0);
   if (idx >= lo && idx < hi && ((idx - lo) % kBlock) == (int)threadIdx.x) {
     NodeRes r = load_res(st, idx);
     assume_row(st, pq, r, idx);
