@@ -133,7 +133,10 @@ struct kgpu_ctx {
   DevBuf d_stage, d_remap, d_from;
   void* stage_host = nullptr;                      // pinned staging block of a delta launch
   void* cyc_host = nullptr;                        // pinned staging of a short cycle: DevState + queries
-                                                   // out, results + abort word + port overflow back
+  void* res_pin = nullptr;                         // pinned coherent block the short cycle's kernels
+  kgpu_result* res_dev = nullptr;                  // write their result records into (its device address)
+  DevState ds_last{};                              // the DevState image last uploaded by a short cycle
+  const void* ds_ptr = nullptr;                    // ... into this dstate allocation (null: none)
   size_t stage_cap = 0;
   bool last_diag = false;
   std::vector<hipEvent_t> ev_pool;
@@ -1402,6 +1405,7 @@ int stage_topology(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_
       if (c->pod_rows_dev != (int)c->pod_rows.size() && (rc = upload_pod_table(c))) return rc;
       if ((rc = ensure(c, c->dstate, sizeof(DevState)))) return rc;
       c->st_batch = c->st;
+      c->ds_ptr = nullptr;  // the short cycle's cached DevState image is stale
       HIP_OK(c, hipMemcpyAsync(c->dstate.p, &c->st_batch, sizeof(DevState), hipMemcpyHostToDevice, c->stream));
       if (kgpu::launch_class_init(static_cast<const DevState*>(c->dstate.p), c->classes_init,
                                   (int)c->classes.size() - c->classes_init, (int)c->pod_rows.size(), c->stream))
@@ -1481,7 +1485,12 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
   if (short_cycle) {
     if (!c->cyc_host) HIP_OK(c, hipHostMalloc(&c->cyc_host, kCycHostBytes, hipHostMallocDefault));
     if ((rc = ensure(c, c->dstate, kDsQueryOff + sizeof(kgpu_pod_query) * kShortCycle))) return rc;
-    if ((rc = ensure(c, c->results, kCycResBytes))) return rc;
+    if (!c->res_pin) {
+      HIP_OK(c, hipHostMalloc(&c->res_pin, kCycResBytes, hipHostMallocCoherent | hipHostMallocMapped));
+      void* d = nullptr;
+      HIP_OK(c, hipHostGetDevicePointer(&d, c->res_pin, 0));
+      c->res_dev = static_cast<kgpu_result*>(d);
+    }
   } else {
     if ((rc = ensure(c, c->queries, sizeof(kgpu_pod_query) * (size_t)n))) return rc;
     HIP_OK(c, hipMemcpyAsync(c->queries.p, qs, sizeof(kgpu_pod_query) * (size_t)n, hipMemcpyHostToDevice, c->stream));
@@ -1495,7 +1504,8 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
   st.ticket = static_cast<int32_t*>(c->ticket.p);
   st.queries = short_cycle ? reinterpret_cast<const kgpu_pod_query*>(static_cast<char*>(c->dstate.p) + kDsQueryOff)
                            : static_cast<const kgpu_pod_query*>(c->queries.p);
-  st.results = static_cast<kgpu_result*>(c->results.p);
+  // a short cycle's records go straight to pinned host memory (no read-back copy)
+  st.results = short_cycle ? c->res_dev : static_cast<kgpu_result*>(c->results.p);
   // Per-plugin scores of a diagnostic cycle: every pod of a batch without topology pods goes
   // through k_eval, which then zeroes each node's rows itself; otherwise two memsets do.
   const bool zero_diag = diag && !topo_on && c->comm == nullptr;
@@ -1518,13 +1528,26 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
   }
   if ((rc = ensure(c, c->dstate, sizeof(DevState)))) return rc;
   c->st_batch = st;
+  // A one-pod diagnostic cycle on k_eval + k_final (kgpu_schedule_one) passes its query in the
+  // launch arguments; its DevState is re-sent only when it differs from the image already there.
+  const bool inline_q = short_cycle && n == 1 && diag && !topo_on && c->comm == nullptr && !(c->xg_nranks > 1) &&
+                        c->st.cut_state == nullptr && nom_dev == nullptr;
   if (short_cycle) {
     char* h = static_cast<char*>(c->cyc_host);
-    std::memcpy(h, &c->st_batch, sizeof(DevState));
-    std::memcpy(h + kDsQueryOff, qs, sizeof(kgpu_pod_query) * (size_t)n);
-    HIP_OK(c, hipMemcpyAsync(c->dstate.p, h, kDsQueryOff + sizeof(kgpu_pod_query) * (size_t)n, hipMemcpyHostToDevice,
-                             c->stream));
+    const bool ds_same = c->ds_ptr == c->dstate.p && std::memcmp(&c->ds_last, &c->st_batch, sizeof(DevState)) == 0;
+    if (!inline_q) {
+      std::memcpy(h, &c->st_batch, sizeof(DevState));
+      std::memcpy(h + kDsQueryOff, qs, sizeof(kgpu_pod_query) * (size_t)n);
+      HIP_OK(c, hipMemcpyAsync(c->dstate.p, h, kDsQueryOff + sizeof(kgpu_pod_query) * (size_t)n, hipMemcpyHostToDevice,
+                               c->stream));
+    } else if (!ds_same) {
+      std::memcpy(h, &c->st_batch, sizeof(DevState));
+      HIP_OK(c, hipMemcpyAsync(c->dstate.p, h, sizeof(DevState), hipMemcpyHostToDevice, c->stream));
+    }
+    c->ds_last = c->st_batch;
+    c->ds_ptr = c->dstate.p;
   } else {
+    c->ds_ptr = nullptr;
     HIP_OK(c, hipMemcpyAsync(c->dstate.p, &c->st_batch, sizeof(DevState), hipMemcpyHostToDevice, c->stream));
   }
   const DevState* dst = static_cast<const DevState*>(c->dstate.p);
@@ -1776,6 +1799,10 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
         // the chain's last pod with a normalize pass: k_final's last workgroup resolves it
         a.resolve_self = (k == j - 1 && a.norm && !sharded) ? 1 : 0;
         resolved_in_final = a.resolve_self != 0;
+        if (inline_q) {
+          a.q_inline = 1;
+          a.q = qs[k];
+        }
         if (c->timing) HIP_OK(c, hipEventRecord(get_event(c, ev), c->stream));
         if (nom_dev && kgpu::launch_victims(dst, nom_dev, st.N, c->stream))
           return fail(c, KGPU_E_DEVICE, "k_victims launch failed");
@@ -1806,9 +1833,9 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
     i = j;
   }
   if (timed) HIP_OK(c, hipEventRecord(t1, c->stream));
-  kgpu_result* res_host = short_cycle ? reinterpret_cast<kgpu_result*>(static_cast<char*>(c->cyc_host) + kCycResOff)
-                                      : results;
-  HIP_OK(c, hipMemcpyAsync(res_host, st.results, sizeof(kgpu_result) * (size_t)n, hipMemcpyDeviceToHost, c->stream));
+  kgpu_result* res_host = short_cycle ? static_cast<kgpu_result*>(c->res_pin) : results;
+  if (!short_cycle)
+    HIP_OK(c, hipMemcpyAsync(res_host, st.results, sizeof(kgpu_result) * (size_t)n, hipMemcpyDeviceToHost, c->stream));
   if (used_persistent)
     HIP_OK(c, hipMemcpyAsync(&c->abort_host, abort_word, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
   int32_t port_overflow = 0;
@@ -2592,6 +2619,7 @@ int kgpu_destroy(kgpu_ctx* c) {
   if (c->xg_box.p) (void)hipFree(c->xg_box.p);
   if (c->stage_host) (void)hipHostFree(c->stage_host);
   if (c->cyc_host) (void)hipHostFree(c->cyc_host);
+  if (c->res_pin) (void)hipHostFree(c->res_pin);
   if (c->st.mcnt) (void)hipFree(c->st.mcnt);
   if (c->st.tcnt) (void)hipFree(c->st.tcnt);
   if (c->shard.p) (void)hipFree(c->shard.p);
@@ -2976,6 +3004,7 @@ int kgpu_select_victims(kgpu_ctx* c, const kgpu_pod_query* q, const kgpu_pools* 
       (rc = upload_preempt(c, ps, pools, 1, args->n_pdbs, d_pdb, &dev)))
     return rc;
   if ((rc = ensure(c, c->dstate, sizeof(DevState)))) return rc;
+  c->ds_ptr = nullptr;  // the short cycle's cached DevState image is stale
   c->st_batch = st;
   HIP_OK(c, hipMemcpyAsync(c->dstate.p, &c->st_batch, sizeof(DevState), hipMemcpyHostToDevice, c->stream));
   const DevState* dst = static_cast<const DevState*>(c->dstate.p);

@@ -238,8 +238,9 @@ struct PodArgs {
   int32_t cut;          // 1: numFeasibleNodesToFind < N -- k_cut trims the feasible set (R2)
   int32_t zero_diag;    // 1: k_eval zeroes every node's diag rows itself (no memset launches)
   int32_t resolve_self; // 1: k_final's last workgroup resolves and assumes `pod` (no k_resolve launch)
-  int32_t pad;
+  int32_t q_inline;     // 1: `pod`'s query is `q` below (a one-pod cycle: no query upload)
   int64_t seq;          // tie-break sequence number of `pod`
+  kgpu_pod_query q;
 };
 
 // Persistent batch launch: a run of `count` pods (queries first..first+count-1) in one kernel.

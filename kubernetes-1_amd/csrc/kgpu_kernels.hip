@@ -800,7 +800,7 @@ __global__ __launch_bounds__(kBlock) void k_eval(const DevState* __restrict__ st
   // partials -- so that their latencies overlap instead of chaining.
   NodeRes r0{};
   if (n0 < hi) r0 = load_res(st, n0);
-  const kgpu_pod_query q = *cp(st.queries + a.pod);
+  const kgpu_pod_query q = a.q_inline ? a.q : (kgpu_pod_query)*cp(st.queries + a.pod);
   int assume_idx = -1;
   const kgpu_pod_query* pq = st.queries + (a.prev >= 0 ? a.prev : 0);
   if (a.prev >= 0) {
@@ -923,7 +923,7 @@ __global__ __launch_bounds__(kBlock) void k_final(const DevState* __restrict__ s
       r.cut = a.cut;
       int gidx;
       const Winner w = prev_winner(st, r, &gidx);
-      const kgpu_pod_query pq = *cp(st.queries + a.pod);
+      const kgpu_pod_query pq = a.q_inline ? a.q : (kgpu_pod_query)*cp(st.queries + a.pod);
       const int idx = settle_prev(st, r, pq, w, gidx, threadIdx.x == 0);
       if (threadIdx.x == 0) {
         if (idx >= 0) {
