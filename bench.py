@@ -259,15 +259,18 @@ def main():
                             "/".join(sorted(rates, key=int)), "identical to" if ok else "DIFFERENT from")}
 
     # HBM traffic of the dominant kernel per launch, from the committed rocprofv3 --pmc passes of
-    # this exact workload (profiles/r01_pmc_traffic.json, tools/gpu_pmc.sh); null when none exist
+    # this exact workload (the newest profiles/r*_pmc_traffic.json holding it; tools/gpu_pmc1.sh);
+    # null when none exist
     traffic = None
-    try:
-        with open(os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")) as fh:
-            pmc = json.load(fh).get("%s:%d:%d" % (args.config, n_local, launch_pods))
+    for fname in ("r02_pmc_traffic.json", "r01_pmc_traffic.json"):
+        try:
+            with open(os.path.join(ROOT, "profiles", fname)) as fh:
+                pmc = json.load(fh).get("%s:%d:%d" % (args.config, n_local, launch_pods))
+        except (OSError, ValueError):
+            continue
         if pmc and pmc["kernel"] == kname:
             traffic = pmc["traffic_bytes_per_launch"]
-    except (OSError, ValueError):
-        pass
+            break
 
     if rank == 0:
         line = {
