@@ -1175,12 +1175,32 @@ struct BatchShared {
 __device__ __forceinline__ void lds_release(int* f, int v) {
   __hip_atomic_store(f, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-__device__ __forceinline__ void lds_wait(int* f, int v) {
-  while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != v) __builtin_amdgcn_s_sleep(1);
+// LDS hand-offs between the waves of a workgroup.  A wait that outlives kSpinTimeout (a protocol
+// fault, never expected) raises the run's abort word instead of hanging the workgroup: the
+// communication wave's next sweep sees it, every wave leaves the pod loop, and the host reports
+// KGPU_E_DEVICE and invalidates the mirror.
+template <bool GE>
+__device__ __forceinline__ void lds_wait_t(int* f, int v, int32_t* abort_word) {
+  // the clock is read only once the first check failed, and then every 64 spins: an s_memrealtime
+  // in flight would hold every LDS read behind it (both count in lgkmcnt)
+  uint64_t t0 = 0;
+  for (int it = 0;; ++it) {
+    const int x = __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (GE ? x >= v : x == v) return;
+    __builtin_amdgcn_s_sleep(1);
+    if ((it & 63) == 0) {
+      const uint64_t now = __builtin_amdgcn_s_memrealtime();
+      if (it == 0) {
+        t0 = now;
+      } else if (now - t0 > kSpinTimeout) {
+        __hip_atomic_store(abort_word, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+      }
+    }
+  }
 }
-__device__ __forceinline__ void lds_wait_ge(int* f, int v) {
-  while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < v) __builtin_amdgcn_s_sleep(1);
-}
+__device__ __forceinline__ void lds_wait(int* f, int v, int32_t* abort_word) { lds_wait_t<false>(f, v, abort_word); }
+__device__ __forceinline__ void lds_wait_ge(int* f, int v, int32_t* abort_word) { lds_wait_t<true>(f, v, abort_word); }
 
 __device__ __forceinline__ constexpr bool spare_slot(int j, int K, int tid, int B) {
   return j == K - 1 && tid == B - 1;
@@ -1436,7 +1456,7 @@ __global__ __launch_bounds__(B + 64) void k_batch(const DevState* __restrict__ s
           gp(st.results)[pa.first + i - 1] = res;
         }
         if (have_cur && !slow) {
-          lds_wait_ge(&sh.pcount, W * (i + 1));
+          lds_wait_ge(&sh.pcount, W * (i + 1), pa.abort);
           KGPU_STAMP(i, 6);
           const Cand c = wg_combine<B>(sh, p, won && fast_b);
           if (lane == 0) publish(i, c.key, c.feas);
@@ -1458,7 +1478,7 @@ __global__ __launch_bounds__(B + 64) void k_batch(const DevState* __restrict__ s
       __syncthreads();  // (c)
       if (!ok) break;
       if (slow) {
-        lds_wait(&sh.cready, i + 1);
+        lds_wait(&sh.cready, i + 1, pa.abort);
         cand = sh.cslow[p];
       } else {
         cand = cn;
@@ -1503,7 +1523,7 @@ __global__ __launch_bounds__(B + 64) void k_batch(const DevState* __restrict__ s
     if (have_cur) {
       const uint64_t tk = pod_tie_key(st.seed, pa.seq0 + i);
       if (fast_b && wave == W - 1) {
-        lds_wait(&sh.bready, i);  // the candidate lane staged it right after barrier (c) of pod i-1
+        lds_wait(&sh.bready, i, pa.abort);  // the candidate lane staged it right after barrier (c) of pod i-1
         NodeRes t = sh.brow[(i - 1) & 1];
         assume_regs(qp, t);
         if (tid == B - 1) r[K - 1] = t;
@@ -1558,7 +1578,7 @@ __global__ __launch_bounds__(B + 64) void k_batch(const DevState* __restrict__ s
           lds_release(&sh.cready, i + 1);
         }
       }
-      lds_wait(&sh.cready, i + 1);
+      lds_wait(&sh.cready, i + 1, pa.abort);
       cand = sh.cslow[p];
     } else {
       cand = cn;
