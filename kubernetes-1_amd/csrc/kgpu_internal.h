@@ -457,8 +457,9 @@ int eval_blocks(int N);
 // Node sharding: reduce this shard's `blocks` partials of buffer half `parity` to one record in
 // shard_send_key (what = 0, global node index) or shard_send_stat (what = 1).
 int launch_shard_pack(const DevState* st, int parity, int blocks, int what, void* stream);
-// Geometry index (workgroup size x rows per lane) and grid of the persistent kernel, -1 when N
-// does not fit in max_groups workgroups.
+// Geometry index (B row threads x K slots per lane, plus one communication wave) and grid of the
+// persistent kernel: *per = B*K - 1 nodes per workgroup (the last slot of the last lane is the
+// variant-B spare), -1 when N does not fit in max_groups workgroups.
 int batch_geometry(int N, int max_groups, int* per, int* groups);
 int launch_batch(const DevState* st, const BatchArgs& a, int groups, int kidx, int spec, void* stream);
 // Topology pipeline for one pod (PodArgs.pod): domain histograms, critical-path minima, filters,
