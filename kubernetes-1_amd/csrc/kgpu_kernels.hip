@@ -2997,17 +2997,17 @@ int select_spec(const int32_t* filters, int nf, const int32_t* scores, int ns, b
 struct Geo {
   int B, K;
 };
-constexpr Geo kGeo[] = {{192, 1}, {256, 1}, {448, 1}, {960, 1}, {512, 4}};  // B row threads (+ one communication wave), K slots per lane
+constexpr Geo kGeo[] = {{128, 1}, {192, 1}, {448, 1}, {960, 1}, {512, 4}};  // B row threads (+ one communication wave), K slots per lane
 constexpr int kNumGeo = 5;
 constexpr int kBatchLdsPad = 96 * 1024;
 
 template <uint32_t FM, uint32_t SM>
 struct BatchRow {
   using Fn = void (*)(const DevState*, BatchArgs);
-  static constexpr Fn fn[kNumGeo] = {k_batch<FM, SM, 1, 192, false>, k_batch<FM, SM, 1, 256, false>,
+  static constexpr Fn fn[kNumGeo] = {k_batch<FM, SM, 1, 128, false>, k_batch<FM, SM, 1, 192, false>,
                                      k_batch<FM, SM, 1, 448, false>, k_batch<FM, SM, 1, 960, false>,
                                      k_batch<FM, SM, 4, 512, false>};
-  static constexpr Fn xfn[kNumGeo] = {k_batch<FM, SM, 1, 192, true>, k_batch<FM, SM, 1, 256, true>,
+  static constexpr Fn xfn[kNumGeo] = {k_batch<FM, SM, 1, 128, true>, k_batch<FM, SM, 1, 192, true>,
                                       k_batch<FM, SM, 1, 448, true>, k_batch<FM, SM, 1, 960, true>,
                                       k_batch<FM, SM, 4, 512, true>};
 };
