@@ -598,6 +598,14 @@ int kgpu_xgmi_active(const kgpu_ctx* ctx);
 int kgpu_xgmi_handle(kgpu_ctx* ctx, int32_t nranks, uint8_t handle[64]);
 int kgpu_xgmi_init(kgpu_ctx* ctx, int32_t nranks, int32_t rank, const uint8_t* handles);
 
+/* Test hook (fault injection): the countdown-th host allocation point reached from now on, in any
+ * context, throws std::bad_alloc as operator new would (0 = off).  Points: context creation, snapshot
+ * upload, the batch / cycle staging, the topology plans, the delta stream.  The entry point that
+ * reaches it returns KGPU_E_NOMEM with last_error set -- the exception barrier every extern "C" entry
+ * carries -- and a state-changing entry (upload / schedule / delta / forget) also invalidates the
+ * device mirror (KGPU_E_STATE until the next kgpu_upload_snapshot). */
+int kgpu_debug_fail_alloc(int32_t countdown);
+
 #ifdef __cplusplus
 }
 #endif

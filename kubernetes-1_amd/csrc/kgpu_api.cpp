@@ -10,6 +10,10 @@
 
 #include <algorithm>
 #include <array>
+#include <atomic>
+#include <exception>
+#include <memory>
+#include <new>
 #include <iterator>
 #include <cmath>
 #include <cstdio>
@@ -179,6 +183,47 @@ namespace {
 
 int fail(kgpu_ctx* c, int code, const std::string& msg) {
   if (c) c->err = msg;
+  return code;
+}
+
+// ---- exception barrier: no C++ exception crosses the C ABI (include/kgpu.h conventions).  Every
+// extern "C" entry is a function-try-block whose handler maps the exception in flight to a KGPU_E_*
+// code and last_error.  A state-changing entry (upload, schedule, delta, forget) that throws may have
+// left the host books and the device mirror apart, so its handler also invalidates the mirror: the
+// engine then refuses cycles (KGPU_E_STATE) until the next kgpu_upload_snapshot.
+std::atomic<int32_t> g_fail_alloc{0};  // kgpu_debug_fail_alloc countdown (0: off)
+
+// A host allocation point the fault-injection hook can fail (std::bad_alloc, as operator new would).
+void fail_point() {
+  if (g_fail_alloc.load(std::memory_order_relaxed) > 0 && g_fail_alloc.fetch_sub(1) == 1) throw std::bad_alloc();
+}
+
+int on_exception(kgpu_ctx* c, bool invalidate) noexcept {
+  int code = KGPU_E_STATE;
+  const char* msg = "internal error (unknown exception)";
+  std::string what;
+  try {
+    throw;
+  } catch (const std::bad_alloc&) {
+    code = KGPU_E_NOMEM;
+    msg = "host memory allocation failed";
+  } catch (const std::exception& e) {
+    msg = "internal error";
+    try {
+      what = e.what();
+    } catch (...) {
+    }
+  } catch (...) {
+  }
+  if (c) {
+    if (invalidate) c->uploaded = false;
+    try {
+      c->err = std::string(msg) + (what.empty() ? "" : ": " + what) +
+               (invalidate ? " (device mirror invalidated: upload the snapshot again)" : "");
+    } catch (...) {
+      c->err.clear();
+    }
+  }
   return code;
 }
 
@@ -474,6 +519,7 @@ struct SlotAlloc {
 int build_plans(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools* p,
                 std::vector<kgpu::QPlan>& plans, std::vector<int32_t>& aux, std::vector<kgpu::TTerm>& aux_terms,
                 int64_t* max_scratch) {
+  fail_point();
   const bool fp = has_filter(c, KGPU_F_POD_TOPOLOGY_SPREAD), fi = has_filter(c, KGPU_F_INTER_POD_AFFINITY);
   const bool sp = has_score(c, KGPU_S_POD_TOPOLOGY_SPREAD), si = has_score(c, KGPU_S_INTER_POD_AFFINITY);
   const bool sd = has_score(c, KGPU_S_DEFAULT_POD_TOPOLOGY_SPREAD);
@@ -1446,6 +1492,7 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
   if (!c->uploaded) return fail(c, KGPU_E_STATE, "no snapshot uploaded");
   if (n <= 0) return KGPU_OK;
   int rc;
+  fail_point();
   if (c->has_alias && assume) {
     // A node listed twice: the device assume updates one row only, so place pods one at a time
     // and apply NodeInfo.AddPod to every row of the chosen node through k_delta.
@@ -2354,6 +2401,7 @@ int apply_delta(kgpu_ctx* c, const kgpu_delta_batch* b, int32_t* slots) {
   DevState& st = c->st;
   int rc;
   if (b->n_order > 0 && (rc = reorder_nodes(c, b))) return rc;
+  fail_point();
   if ((rc = update_key_meta(c, b))) return rc;
   if (b->n_order <= 0 && (rc = update_csr(c, b))) return rc;
   if (b->n_zones > st.n_zones) st.n_zones = b->n_zones;
@@ -2515,7 +2563,7 @@ int kgpu_struct_sizes(int32_t* out, int32_t n) {
   return m;
 }
 
-int kgpu_create(const kgpu_config* cfg, kgpu_ctx** out) {
+int kgpu_create(const kgpu_config* cfg, kgpu_ctx** out) try {
   if (!cfg || !out) return KGPU_E_INVAL;
   *out = nullptr;
   if (cfg->abi_version != KGPU_ABI_VERSION) return KGPU_E_INVAL;
@@ -2543,20 +2591,19 @@ int kgpu_create(const kgpu_config* cfg, kgpu_ctx** out) {
       for (int j = 1; j < cfg->n_shape; ++j)
         if (cfg->shape[j].utilization <= cfg->shape[j - 1].utilization) return KGPU_E_INVAL;
     }
+  fail_point();
+  std::unique_ptr<kgpu_ctx> holder(new kgpu_ctx());  // freed on every early return and on a throw
+  kgpu_ctx* c = holder.get();
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return KGPU_E_DEVICE;
   if (cfg->device < 0 || cfg->device >= ndev) return KGPU_E_INVAL;
-  kgpu_ctx* c = new kgpu_ctx();
   c->cfg = *cfg;
   c->device = cfg->device;
-  if (hipSetDevice(c->device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
-    delete c;
+  if (hipSetDevice(c->device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
     return KGPU_E_DEVICE;
-  }
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, c->device) != hipSuccess) {
     (void)hipStreamDestroy(c->stream);
-    delete c;
     return KGPU_E_DEVICE;
   }
   c->n_cus = prop.multiProcessorCount;
@@ -2592,11 +2639,13 @@ int kgpu_create(const kgpu_config* cfg, kgpu_ctx** out) {
   const bool has_least = has_score(c, KGPU_S_LEAST_ALLOCATED), has_most = has_score(c, KGPU_S_MOST_ALLOCATED);
   const bool def_res = (!has_least || def_spec(cfg->least, cfg->n_least)) && (!has_most || def_spec(cfg->most, cfg->n_most));
   c->spec = kgpu::select_spec(cfg->filters, cfg->n_filters, cfg->scores, cfg->n_scores, def_res);
-  *out = c;
+  *out = holder.release();
   return KGPU_OK;
+} catch (...) {
+  return on_exception(nullptr, false);
 }
 
-int kgpu_destroy(kgpu_ctx* c) {
+int kgpu_destroy(kgpu_ctx* c) try {
   if (!c) return KGPU_OK;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
@@ -2628,20 +2677,24 @@ int kgpu_destroy(kgpu_ctx* c) {
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return KGPU_OK;
+} catch (...) {
+  return on_exception(c, false);
 }
 
 const char* kgpu_last_error(const kgpu_ctx* c) { return c ? c->err.c_str() : "null context"; }
 
 int64_t kgpu_generation(const kgpu_ctx* c) { return c ? c->generation : -1; }
 
-int kgpu_read_phase_trace(kgpu_ctx* c, int64_t* out, int32_t max_pods) {
+int kgpu_read_phase_trace(kgpu_ctx* c, int64_t* out, int32_t max_pods) try {
   if (!c || !out || max_pods < 0) return KGPU_E_INVAL;
   const int32_t n = std::min<int32_t>(max_pods, (int32_t)(c->trace_host.size() / 16));
   std::memcpy(out, c->trace_host.data(), sizeof(int64_t) * 16 * (size_t)n);
   return n;
+} catch (...) {
+  return on_exception(c, false);
 }
 
-int kgpu_set_option(kgpu_ctx* c, int32_t option, int64_t value) {
+int kgpu_set_option(kgpu_ctx* c, int32_t option, int64_t value) try {
   if (!c) return KGPU_E_INVAL;
   if (option == KGPU_OPT_KERNEL_TIMING) c->timing = value != 0;
   else if (option == KGPU_OPT_PERSISTENT) c->persistent = value != 0;
@@ -2653,9 +2706,11 @@ int kgpu_set_option(kgpu_ctx* c, int32_t option, int64_t value) {
   else if (option == KGPU_OPT_XGMI) c->xgmi = value != 0;
   else return KGPU_E_INVAL;
   return KGPU_OK;
+} catch (...) {
+  return on_exception(c, false);
 }
 
-int kgpu_upload_snapshot(kgpu_ctx* c, const kgpu_snapshot* s, int64_t generation) {
+int kgpu_upload_snapshot(kgpu_ctx* c, const kgpu_snapshot* s, int64_t generation) try {
   if (!c || !s) return KGPU_E_INVAL;
   if (s->n_nodes < 0 || s->n_label_keys < 0 || s->n_scalar < 0 || s->taint_words < 0 || s->port_slots < 0)
     return fail(c, KGPU_E_INVAL, "negative snapshot dimension");
@@ -2667,6 +2722,7 @@ int kgpu_upload_snapshot(kgpu_ctx* c, const kgpu_snapshot* s, int64_t generation
   HIP_OK(c, hipStreamSynchronize(c->stream));
   free_all(c->snap_allocs);
   free_all(c->work_allocs);
+  fail_point();
   c->recs.clear();
   c->uid_slot.clear();
   c->uploaded = false;
@@ -2808,17 +2864,21 @@ int kgpu_upload_snapshot(kgpu_ctx* c, const kgpu_snapshot* s, int64_t generation
   c->uploaded = true;
   HIP_OK(c, hipDeviceSynchronize());
   return KGPU_OK;
+} catch (...) {
+  return on_exception(c, true);
 }
 
 int kgpu_schedule_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools* pools, int64_t first_seq,
-                        kgpu_result* results, kgpu_stats* stats) {
+                        kgpu_result* results, kgpu_stats* stats) try {
   if (!c || (n > 0 && (!qs || !results))) return KGPU_E_INVAL;
   if (hipSetDevice(c->device) != hipSuccess) return KGPU_E_DEVICE;
   return run_batch(c, qs, n, pools, first_seq, results, stats, false, 1);
+} catch (...) {
+  return on_exception(c, true);
 }
 
 int kgpu_schedule_one(kgpu_ctx* c, const kgpu_pod_query* q, const kgpu_pools* pools, int64_t pod_seq, int32_t assume,
-                      kgpu_result* res, int32_t* assumed_slot) {
+                      kgpu_result* res, int32_t* assumed_slot) try {
   if (!c || !q || !res) return KGPU_E_INVAL;
   if (hipSetDevice(c->device) != hipSuccess) return KGPU_E_DEVICE;
   size_t before = c->recs.size();
@@ -2826,10 +2886,12 @@ int kgpu_schedule_one(kgpu_ctx* c, const kgpu_pod_query* q, const kgpu_pools* po
   if (rc) return rc;
   if (assumed_slot) *assumed_slot = c->recs.size() > before ? (int32_t)c->recs.size() - 1 : -1;
   return KGPU_OK;
+} catch (...) {
+  return on_exception(c, true);
 }
 
 int kgpu_set_nominated(kgpu_ctx* c, const kgpu_nominated* noms, int32_t n, const kgpu_pod_query* pods,
-                       const kgpu_pools* pools) {
+                       const kgpu_pools* pools) try {
   if (!c || n < 0 || (n > 0 && (!noms || !pods))) return KGPU_E_INVAL;
   kgpu_ctx::Nominator nm;
   int32_t n_items = 0;
@@ -2868,6 +2930,8 @@ int kgpu_set_nominated(kgpu_ctx* c, const kgpu_nominated* noms, int32_t n, const
   v.scalars = c->nom.scalars.data(); v.n_scalars = (int32_t)c->nom.scalars.size();
   v.ports = c->nom.ports.data(); v.n_ports = (int32_t)c->nom.ports.size();
   return KGPU_OK;
+} catch (...) {
+  return on_exception(c, false);
 }
 
 // pickOneNodeForPreemption (generic_scheduler.go:718-843) over the nodes that fit, walked in
@@ -2933,7 +2997,7 @@ static int32_t pick_one_node(const std::vector<int32_t>& cand, const kgpu_node_v
 }
 
 int kgpu_select_victims(kgpu_ctx* c, const kgpu_pod_query* q, const kgpu_pools* pools, const kgpu_preempt_args* args,
-                        kgpu_node_victims* nodes_out, int32_t* victims_out, int32_t* chosen) {
+                        kgpu_node_victims* nodes_out, int32_t* victims_out, int32_t* chosen) try {
   if (!c || !q || !args || !nodes_out || (args->n_victims > 0 && (!args->victims || !args->pods || !victims_out)))
     return KGPU_E_INVAL;
   if (args->n_victims < 0 || args->n_pdbs < 0 || (args->n_pdbs > 0 && !args->pdb_allowed)) return KGPU_E_INVAL;
@@ -3042,16 +3106,20 @@ int kgpu_select_victims(kgpu_ctx* c, const kgpu_pod_query* q, const kgpu_pools* 
   const int32_t pick = pick_one_node(cand, nodes_out, victims_out, args, prio.data());
   if (chosen) *chosen = pick >= 0 ? pick + c->st.node_base : -1;
   return KGPU_OK;
+} catch (...) {
+  return on_exception(c, false);
 }
 
-int kgpu_get_filter(kgpu_ctx* c, uint32_t* words) {
+int kgpu_get_filter(kgpu_ctx* c, uint32_t* words) try {
   if (!c || !words) return KGPU_E_INVAL;
   if (!c->last_diag) return fail(c, KGPU_E_STATE, "no kgpu_schedule_one cycle to report");
   HIP_OK(c, hipMemcpy(words, c->st.status, sizeof(uint32_t) * (size_t)c->st.N, hipMemcpyDeviceToHost));
   return KGPU_OK;
+} catch (...) {
+  return on_exception(c, false);
 }
 
-int kgpu_get_scores(kgpu_ctx* c, int32_t plugin, int64_t* raw, int64_t* normalized) {
+int kgpu_get_scores(kgpu_ctx* c, int32_t plugin, int64_t* raw, int64_t* normalized) try {
   if (!c || plugin < 0 || plugin >= KGPU_NUM_SCORES) return KGPU_E_INVAL;
   if (!c->last_diag) return fail(c, KGPU_E_STATE, "no kgpu_schedule_one cycle to report");
   const size_t N = (size_t)c->st.N;
@@ -3059,10 +3127,12 @@ int kgpu_get_scores(kgpu_ctx* c, int32_t plugin, int64_t* raw, int64_t* normaliz
   if (normalized)
     HIP_OK(c, hipMemcpy(normalized, c->st.diag_norm + plugin * N, sizeof(int64_t) * N, hipMemcpyDeviceToHost));
   return KGPU_OK;
+} catch (...) {
+  return on_exception(c, false);
 }
 
 int kgpu_read_nodes(kgpu_ctx* c, int64_t* req_cpu, int64_t* req_mem, int64_t* req_eph, int64_t* nz_cpu,
-                    int64_t* nz_mem, int32_t* num_pods) {
+                    int64_t* nz_mem, int32_t* num_pods) try {
   if (!c || !c->uploaded) return KGPU_E_INVAL;
   HIP_OK(c, hipStreamSynchronize(c->stream));
   const size_t N = (size_t)c->st.N;
@@ -3073,9 +3143,11 @@ int kgpu_read_nodes(kgpu_ctx* c, int64_t* req_cpu, int64_t* req_mem, int64_t* re
   if (nz_mem) HIP_OK(c, hipMemcpy(nz_mem, c->st.nz_mem, 8 * N, hipMemcpyDeviceToHost));
   if (num_pods) HIP_OK(c, hipMemcpy(num_pods, c->st.num_pods, 4 * N, hipMemcpyDeviceToHost));
   return KGPU_OK;
+} catch (...) {
+  return on_exception(c, false);
 }
 
-int kgpu_forget_pod(kgpu_ctx* c, int32_t slot) {
+int kgpu_forget_pod(kgpu_ctx* c, int32_t slot) try {
   if (!c) return KGPU_E_INVAL;
   if (!c->uploaded) return fail(c, KGPU_E_STATE, "no snapshot uploaded");
   if (slot < 0 || slot >= (int32_t)c->recs.size() || !c->recs[(size_t)slot].active)
@@ -3105,9 +3177,11 @@ int kgpu_forget_pod(kgpu_ctx* c, int32_t slot) {
   c->pod_rows_dev = -1;
   if (a.has_uid) c->uid_slot.erase(a.uid);
   return KGPU_OK;
+} catch (...) {
+  return on_exception(c, true);
 }
 
-int kgpu_apply_delta(kgpu_ctx* c, const kgpu_delta_batch* b, int64_t generation, int32_t* slots) {
+int kgpu_apply_delta(kgpu_ctx* c, const kgpu_delta_batch* b, int64_t generation, int32_t* slots) try {
   if (!c || !b) return KGPU_E_INVAL;
   if (!c->uploaded) return fail(c, KGPU_E_STATE, "no snapshot uploaded");
   if (b->n_deltas < 0 || b->n_pods < 0 || b->n_rows < 0 || b->n_order < 0 || (b->n_deltas && !b->deltas) ||
@@ -3124,6 +3198,8 @@ int kgpu_apply_delta(kgpu_ctx* c, const kgpu_delta_batch* b, int64_t generation,
   }
   c->generation = generation;
   return KGPU_OK;
+} catch (...) {
+  return on_exception(c, true);
 }
 
 // ---- node sharding over xGMI: the persistent kernel's granule exchange through peer stores
@@ -3136,7 +3212,7 @@ static int xgmi_geometry(kgpu_ctx* c, int32_t nranks) {
   return c->xg_geo;
 }
 
-int kgpu_xgmi_handle(kgpu_ctx* c, int32_t nranks, uint8_t handle[64]) {
+int kgpu_xgmi_handle(kgpu_ctx* c, int32_t nranks, uint8_t handle[64]) try {
   if (!c || !handle || nranks < 2 || nranks > kgpu::kMaxRanks) return KGPU_E_INVAL;
   if (hipSetDevice(c->device) != hipSuccess) return KGPU_E_DEVICE;
   if (!c->uploaded) return fail(c, KGPU_E_STATE, "upload this rank's shard before kgpu_xgmi_handle");
@@ -3162,9 +3238,11 @@ int kgpu_xgmi_handle(kgpu_ctx* c, int32_t nranks, uint8_t handle[64]) {
   std::memcpy(handle, &h, sizeof(h));
   c->xg_nranks = 0;  // not usable until kgpu_xgmi_init
   return KGPU_OK;
+} catch (...) {
+  return on_exception(c, false);
 }
 
-int kgpu_xgmi_init(kgpu_ctx* c, int32_t nranks, int32_t rank, const uint8_t* handles) {
+int kgpu_xgmi_init(kgpu_ctx* c, int32_t nranks, int32_t rank, const uint8_t* handles) try {
   if (!c || !handles || nranks < 2 || nranks > kgpu::kMaxRanks || rank < 0 || rank >= nranks) return KGPU_E_INVAL;
   if (hipSetDevice(c->device) != hipSuccess) return KGPU_E_DEVICE;
   if (!c->xg_box.p || c->xg_GT != nranks * c->xg_groups)
@@ -3205,18 +3283,22 @@ int kgpu_xgmi_init(kgpu_ctx* c, int32_t nranks, int32_t rank, const uint8_t* han
   c->xg_rank = rank;
   c->xg_seq = 0;
   return KGPU_OK;
+} catch (...) {
+  return on_exception(c, false);
 }
 
-int kgpu_comm_unique_id(uint8_t id[128]) {
+int kgpu_comm_unique_id(uint8_t id[128]) try {
   if (!id) return KGPU_E_INVAL;
   static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId is 128 bytes");
   ncclUniqueId u;
   if (ncclGetUniqueId(&u) != ncclSuccess) return KGPU_E_DEVICE;
   std::memcpy(id, &u, 128);
   return KGPU_OK;
+} catch (...) {
+  return on_exception(nullptr, false);
 }
 
-int kgpu_comm_init(kgpu_ctx* c, int32_t nranks, int32_t rank, const uint8_t id[128]) {
+int kgpu_comm_init(kgpu_ctx* c, int32_t nranks, int32_t rank, const uint8_t id[128]) try {
   if (!c || !id) return KGPU_E_INVAL;
   if (nranks < 1 || nranks > kgpu::kMaxRanks || rank < 0 || rank >= nranks)
     return fail(c, KGPU_E_INVAL, "nranks must be in [1, 64] and 0 <= rank < nranks");
@@ -3271,8 +3353,15 @@ int kgpu_comm_init(kgpu_ctx* c, int32_t nranks, int32_t rank, const uint8_t id[1
     c->err.clear();
   }
   return KGPU_OK;
+} catch (...) {
+  return on_exception(c, false);
 }
 
 int kgpu_xgmi_active(const kgpu_ctx* c) { return c && c->xg_nranks > 1 && c->xgmi ? 1 : 0; }
+
+int kgpu_debug_fail_alloc(int32_t countdown) {
+  g_fail_alloc.store(countdown > 0 ? countdown : 0, std::memory_order_relaxed);
+  return KGPU_OK;
+}
 
 }  // extern "C"

@@ -179,4 +179,44 @@ def pod_affinity(n_nodes=5000, n_existing=5000, n_pods=10000):
     return nodes, existing, pods, _c.Profile()
 
 
-CONFIGS = {"a": scheduling_basic, "b": fit_least_balanced, "c": taints_affinity_spread, "d": pod_affinity}
+# ----------------------------------------------------------------------------- (e)
+def sharded_spread(n_nodes=1_000_000, n_pods=10000, seed=CLUSTER_SEED, n_zones=64):
+    """Config (e): the generator of (b)+(c) with zone = i % 64 -- config (b)'s
+    node resources (cpu {4..64}, memory {16..256}Gi, 110 pods, 100Gi ephemeral) carrying config (c)'s
+    taints (10% dedicated=infra:NoSchedule, 20% spot=true:PreferNoSchedule) and labels (zone, hostname),
+    and config (c)'s pods (requests as (b), 50% tolerate `dedicated`, PodTopologySpread on zone
+    (DoNotSchedule, maxSkew 1) and hostname (ScheduleAnyway), app=web) under the default profile.
+    The required NodeAffinity admits the first 30% of the zones (zone1..zone19 of 64), the share
+    (c)'s zone1..zone3 of 10 admits.  Meant for 1M nodes as contiguous shards over 8 GPUs."""
+    r = Rng(seed)
+    nodes = []
+    for i in range(n_nodes):
+        taints = []
+        if r.chance(1, 10):
+            taints.append({"key": "dedicated", "value": "infra", "effect": "NoSchedule"})
+        if r.chance(2, 10):
+            taints.append({"key": "spot", "value": "true", "effect": "PreferNoSchedule"})
+        nodes.append(node("node%d" % i, str(r.pick([4, 8, 16, 32, 64])), "%dGi" % r.pick([16, 32, 64, 128, 256]),
+                          110, "100Gi", labels={ZONE: "zone%d" % (i % n_zones), HOSTNAME: "node%d" % i},
+                          taints=taints))
+    admit = ["zone%d" % z for z in range(1, max(2, (3 * n_zones) // 10 + 1))]
+    na = {"nodeAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": {"nodeSelectorTerms": [
+        {"matchExpressions": [{"key": ZONE, "operator": "In", "values": admit}]}]}}}
+    sel = {"matchLabels": {"app": "web"}}
+    tsc = [{"maxSkew": 1, "topologyKey": ZONE, "whenUnsatisfiable": "DoNotSchedule", "labelSelector": sel},
+           {"maxSkew": 1, "topologyKey": HOSTNAME, "whenUnsatisfiable": "ScheduleAnyway", "labelSelector": sel}]
+    pods = []
+    for i in range(n_pods):
+        spec = {"affinity": na, "topologySpreadConstraints": tsc}
+        if r.chance(1, 2):
+            spec["tolerations"] = [{"key": "dedicated", "operator": "Equal", "value": "infra", "effect": "NoSchedule"}]
+        if r.chance(1, 10):
+            pods.append(pod("p%d" % i, labels={"app": "web"}, **spec))
+        else:
+            pods.append(pod("p%d" % i, "%dm" % (100 * (1 + r.below(40))), "%dMi" % (128 * (1 + r.below(64))),
+                            labels={"app": "web"}, **spec))
+    return nodes, [], pods, _c.Profile()
+
+
+CONFIGS = {"a": scheduling_basic, "b": fit_least_balanced, "c": taints_affinity_spread, "d": pod_affinity,
+           "e": sharded_spread}

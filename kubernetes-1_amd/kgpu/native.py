@@ -18,7 +18,8 @@ EXPORTS = ["kgpu_abi_version", "kgpu_struct_sizes", "kgpu_create", "kgpu_destroy
            "kgpu_upload_snapshot", "kgpu_generation", "kgpu_schedule_one", "kgpu_schedule_batch",
            "kgpu_get_filter", "kgpu_get_scores", "kgpu_forget_pod", "kgpu_read_nodes", "kgpu_set_option",
            "kgpu_read_phase_trace", "kgpu_comm_unique_id", "kgpu_comm_init", "kgpu_apply_delta",
-           "kgpu_set_nominated", "kgpu_select_victims", "kgpu_xgmi_handle", "kgpu_xgmi_init", "kgpu_xgmi_active"]
+           "kgpu_set_nominated", "kgpu_select_victims", "kgpu_xgmi_handle", "kgpu_xgmi_init", "kgpu_xgmi_active",
+           "kgpu_debug_fail_alloc"]
 
 
 class KgpuError(RuntimeError):
@@ -59,6 +60,7 @@ def lib():
     L.kgpu_xgmi_handle.argtypes = [vp, i32, vp]
     L.kgpu_xgmi_init.argtypes = [vp, i32, i32, vp]
     L.kgpu_xgmi_active.argtypes = [vp]
+    L.kgpu_debug_fail_alloc.argtypes = [i32]
     L.kgpu_select_victims.argtypes = [vp, vp, C.POINTER(abi.Pools), C.POINTER(abi.PreemptArgs), vp, vp,
                                       C.POINTER(i32)]
     if L.kgpu_abi_version() != abi.ABI_VERSION:
@@ -220,6 +222,12 @@ def comm_unique_id():
     if rc != 0:
         raise KgpuError(rc, "kgpu_comm_unique_id failed")
     return bytes(buf)
+
+
+def debug_fail_alloc(countdown):
+    """Test hook: the countdown-th host allocation point from now on throws std::bad_alloc inside
+    the library (0: off); the entry point that reaches it must return KGPU_E_NOMEM."""
+    lib().kgpu_debug_fail_alloc(int(countdown))
 
 
 def shard_range(n_nodes, world, rank):

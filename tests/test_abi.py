@@ -38,3 +38,23 @@ def test_create_without_gpu_fails_loudly():
     h = ctypes.c_void_p()
     rc = native.lib().kgpu_create(ctypes.byref(cfg), ctypes.byref(h))
     assert rc == abi.E_DEVICE
+
+
+def test_allocation_failure_returns_error_code():
+    """The exception barrier (include/kgpu.h conventions: no exception crosses the ABI): a host
+    allocation failure injected inside kgpu_create comes back as KGPU_E_NOMEM, not as a C++
+    exception unwinding into the caller (cgo would abort the scheduler)."""
+    cfg = abi.Config()
+    cfg.abi_version = abi.ABI_VERSION
+    h = ctypes.c_void_p()
+    native.debug_fail_alloc(1)
+    try:
+        rc = native.lib().kgpu_create(ctypes.byref(cfg), ctypes.byref(h))
+    finally:
+        native.debug_fail_alloc(0)
+    assert rc == abi.E_NOMEM
+    assert not h.value
+    # the hook is spent: the next call reaches the device check again
+    import torch
+    if not torch.cuda.is_available():
+        assert native.lib().kgpu_create(ctypes.byref(cfg), ctypes.byref(h)) == abi.E_DEVICE

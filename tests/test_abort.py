@@ -94,3 +94,40 @@ def test_abort_in_one_of_several_runs():
         ab, got = _abort_then_recover(fw, q, pc, at, must_abort=must)
         assert ab == must, at
         _same(want, got)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("point", [1, 2])
+def test_allocation_failure_invalidates_and_recovers(point):
+    """Fault injection (kgpu_debug_fail_alloc): a std::bad_alloc thrown inside kgpu_schedule_batch
+    -- at the batch staging (1) or inside the topology plans (2) -- comes back through the C ABI as
+    KGPU_E_NOMEM, the mirror is invalidated (KGPU_E_STATE until the next upload), and after the
+    re-upload the engine schedules exactly as the C restatement."""
+    from kgpu import native
+    nodes, existing, pods, prof = cluster.taints_affinity_spread(n_nodes=300, n_pods=60)
+    fw = GpuFramework(prof, nodes, existing, pods_hint=pods)
+    q, pc, _, errs = fw.compile_pods(pods)
+    assert not errs
+    e = fw.engine
+    native.debug_fail_alloc(point)
+    try:
+        with pytest.raises(KgpuError) as ex:
+            e.schedule_batch(q, pc)
+    finally:
+        native.debug_fail_alloc(0)
+    assert ex.value.code == abi.E_NOMEM, ex.value
+    assert "invalidated" in str(ex.value)
+    with pytest.raises(KgpuError) as ex2:
+        e.schedule_batch(q[:1], pc)
+    assert ex2.value.code == abi.E_STATE
+    # an allocation failure inside the upload itself: reported, and the next upload recovers
+    native.debug_fail_alloc(1)
+    try:
+        with pytest.raises(KgpuError) as ex3:
+            e.upload(fw.snap, fw.arrays)
+    finally:
+        native.debug_fail_alloc(0)
+    assert ex3.value.code == abi.E_NOMEM
+    e.upload(fw.snap, fw.arrays)
+    got, _ = e.schedule_batch(q, pc)
+    _same(_ref(fw, q, pc), got)

@@ -1,0 +1,47 @@
+"""Which library's exit handler faults after rocprofv3's tool finalization?
+
+Runs one small step of a chosen variant, then copies /proc/self/maps to a file so that the
+addresses of a crash report from the same process can be resolved to libraries:
+  torch   -- torch only: one device tensor and a synchronize
+  kgpu    -- libkgpu.so only (no torch import): create a context, upload 64 nodes, one batch, destroy
+  both    -- torch first, then the kgpu variant
+Usage: python3 tools/exit_probe.py <variant> <maps-out>"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "kubernetes-1_amd")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def run_torch():
+    import torch
+    x = torch.zeros(1024, device="cuda")
+    x += 1
+    torch.cuda.synchronize()
+
+
+def run_kgpu():
+    from kgpu.cluster import fit_least_balanced
+    from kgpu.framework import GpuFramework
+    nodes, existing, pods, prof = fit_least_balanced(n_nodes=64, n_pods=32)
+    fw = GpuFramework(prof, nodes, existing, pods_hint=pods, device=0)
+    res = fw.schedule(pods, first_seq=0)
+    assert (res["node"] >= 0).sum() > 0
+    fw.engine.close()
+
+
+def main():
+    variant, out = sys.argv[1], sys.argv[2]
+    if variant in ("torch", "both"):
+        run_torch()
+    if variant in ("kgpu", "both"):
+        run_kgpu()
+    with open("/proc/self/maps") as src, open(out, "w") as dst:
+        dst.write(src.read())
+    print("exit_probe %s: done, maps in %s" % (variant, out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
