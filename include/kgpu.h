@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define KGPU_ABI_VERSION 2
+#define KGPU_ABI_VERSION 3
 
 /* ---- return codes */
 #define KGPU_OK 0
@@ -364,6 +364,11 @@ typedef struct kgpu_snapshot {
   kgpu_pools pools;             /* pools referenced by terms */
   const int64_t* pod_uid;       /* [n_pods] caller id of each pod's types.UID (kgpu_apply_delta); NULL:
                                    the snapshot pods cannot be addressed by deltas */
+  const uint8_t* key_unique;    /* [n_label_keys] 1: no value of the key labels two nodes of the WHOLE
+                                   cluster (every shard of Snapshot.List()): hostname-like keys, whose
+                                   topology counts are a node's own.  NULL: derived from this snapshot's
+                                   nodes -- exact unsharded; a node-sharded engine then treats every key
+                                   as shared (ADVICE/DESIGN: sharded topology runs need the caller's view) */
 } kgpu_snapshot;
 
 typedef struct kgpu_result {
@@ -478,6 +483,8 @@ typedef struct kgpu_delta_batch {
   int32_t n_zones;                   /* zone ids in use (0: unchanged) */
   int32_t pad;
   kgpu_pools pools;                  /* pools of `pods` and `rows` */
+  const uint8_t* key_unique;         /* [n_label_keys] as kgpu_snapshot.key_unique after this batch; NULL:
+                                        the caller's flags are unchanged */
 } kgpu_delta_batch;
 
 /* Apply one batch of cache deltas to the device mirror and stamp it with `generation`

@@ -131,6 +131,11 @@ struct kgpu_ctx {
   DevBuf xg_arr;                 // device array: nranks granule bases, then nranks feasible-count bases
   int xg_geo = -1, xg_per = 0, xg_groups = 0, xg_GT = 0;
   int64_t xg_seq = 0;            // ring sequence of the next pod (identical on every rank)
+  // the persistent topology kernel's cross-rank exchange: TX ring (one row per pod) and the init
+  // mailbox of the histogram reduction, both inside xg_box after the granule / feasible rings
+  size_t xg_tx_off = 0, xg_init_off = 0;  // byte offsets in xg_box
+  int64_t xt_seq = 0;            // TX ring sequence of the next topology pod (identical on every rank)
+  uint64_t xr_seq = 0;           // init reductions issued (identical on every rank)
   bool xgmi = true;              // KGPU_OPT_XGMI
   DevBuf batch_ptrs;             // unsharded persistent runs: {gran, feas} per run
   DevBuf flags_buf;                                // DevState::port_overflow
@@ -165,7 +170,9 @@ struct kgpu_ctx {
   std::vector<PodRow> pod_rows;
   int pod_rows_dev = -1;         // rows present in the device pod table (-1: table never uploaded)
   std::vector<int32_t> key_n_values, key_empty;
-  std::vector<uint8_t> key_unique;  // every value of the key sits on at most one node (hostname-like)
+  std::vector<uint8_t> key_unique;  // every value of the key sits on at most one node of THIS shard
+  // kgpu_snapshot / kgpu_delta_batch.key_unique: the caller's cluster-wide view (empty: not given)
+  std::vector<uint8_t> key_unique_caller;
   int64_t max_key_values = 1;
   // persistent topology runs (k_tbatch)
   bool tfast = true;                // KGPU_OPT_TOPO_PERSISTENT
@@ -369,6 +376,15 @@ bool has_filter(const kgpu_ctx* c, int f) {
   for (int i = 0; i < c->cfg.n_filters; ++i)
     if (c->cfg.filters[i] == f) return true;
   return false;
+}
+
+// A hostname-like key (every value on at most one node): its topology counts are read from the
+// node's own column instead of a domain histogram.  Unique on this shard AND, when the caller gave its
+// cluster-wide view, unique there; a node-sharded engine without that view treats the key as shared.
+bool key_uniq(const kgpu_ctx* c, int k) {
+  if (k < 0 || !c->key_unique[(size_t)k]) return false;
+  if (!c->key_unique_caller.empty()) return c->key_unique_caller[(size_t)k] != 0;
+  return c->comm == nullptr && c->xg_nranks <= 1 && c->st.n_total == c->st.N;
 }
 
 struct ItemSrc {
@@ -898,7 +914,7 @@ int t_hist(TRun& tr, const kgpu_ctx* c, int kind, int col, int key, int sig) {
   h.key = key;
   h.sig = sig;
   h.D = key >= 0 ? c->key_n_values[(size_t)key] : 0;
-  const bool uniq = key >= 0 && c->key_unique[(size_t)key];
+  const bool uniq = key_uniq(c, key);
   h.off = uniq ? -1 : tr.lds_bins;
   if (!uniq) tr.lds_bins += h.D + 1;
   const int id = (int)tr.hists.size();
@@ -1058,7 +1074,7 @@ bool t_add(TRun& tr, const kgpu_ctx* c, const kgpu_pod_query& q, const kgpu::QPl
       th.self_match = sp.self_match;
       th.tab = -1;
       if (sp.key < 0) continue;  // nothing registers: the filter passes every node (pany == 0)
-      if (c->key_unique[(size_t)sp.key]) return fail_();
+      if (key_uniq(c, sp.key)) return fail_();
       const int ti = tab_for(t0, 0, sp.key);
       t0[(size_t)ti].t.reg = t_reg(tr, c, tp.hard_sig, sp.key);
       t0[(size_t)ti].t.empty_v = c->key_empty[(size_t)sp.key];
@@ -1076,7 +1092,7 @@ bool t_add(TRun& tr, const kgpu_ctx* c, const kgpu_pod_query& q, const kgpu::QPl
     tp.soft_sig = -1;
     if (sp.is_hostname) {
       tp.soft_mode = 1;
-    } else if (sp.key >= 0 && c->key_unique[(size_t)sp.key]) {
+    } else if (key_uniq(c, sp.key)) {
       tp.soft_mode = 2;
       int32_t k1 = sp.key;
       tp.soft_sig = t_sig(tr, q, p, qi, &k1, 1);
@@ -1191,7 +1207,7 @@ void t_finish(TRun& tr) {
 
 // Upload a planned run and launch k_sig_init + k_hist_init + k_tbatch on the engine's stream.
 int run_tbatch(kgpu_ctx* c, TRun& tr, int first, int count, int64_t first_seq, int32_t assume, int per, int groups,
-               int geo, int32_t* abort_word) {
+               int geo, int32_t* abort_word, bool xg) {
   t_finish(tr);
   int rc;
   kgpu::TBatchArgs a{};
@@ -1271,7 +1287,31 @@ int run_tbatch(kgpu_ctx* c, TRun& tr, int first, int count, int64_t first_seq, i
     a.trace = static_cast<int64_t*>(c->trace.p);
     c->trace_host.assign((size_t)(count + 1) * 16, 0);
   }
-  if (kgpu::launch_tbatch(static_cast<const DevState*>(c->dstate.p), a, groups, geo, c->spec, c->stream))
+  const DevState* dst = static_cast<const DevState*>(c->dstate.p);
+  if (kgpu::launch_tbatch_init(dst, a, groups, c->stream))
+    return fail(c, KGPU_E_DEVICE, "k_sig_init / k_hist_init launch failed");
+  if (xg) {
+    // node-sharded run: cluster-wide histograms from every rank's partial, then the
+    // XG kernel exchanges one record per rank per pod through the topology ring
+    void* const* arr = static_cast<void* const*>(c->xg_arr.p);
+    a.ptx = reinterpret_cast<uint64_t* const*>(arr + 2 * (size_t)c->xg_nranks);
+    a.nranks = c->xg_nranks;
+    a.rank = c->xg_rank;
+    a.xseq0 = c->xt_seq;
+    c->xt_seq += count;
+    kgpu::XReduce x{};
+    x.pinit = reinterpret_cast<int32_t* const*>(arr + 3 * (size_t)c->xg_nranks);
+    x.nranks = c->xg_nranks;
+    x.rank = c->xg_rank;
+    x.seq = ++c->xr_seq;
+    x.parity = (int32_t)(x.seq & 1);
+    x.buf = a.hist_init;
+    x.n_sum = (int32_t)((b_hist + b_tot) / 4);     // hist_init | tot_init: summed
+    x.n_or = (int32_t)((b_reg + b_sany) / 4);      // reg_init | sig_any: OR-ed
+    x.abort = abort_word;
+    if (kgpu::launch_xreduce(x, c->stream)) return fail(c, KGPU_E_DEVICE, "cross-rank histogram reduction launch failed");
+  }
+  if (kgpu::launch_tbatch(dst, a, groups, geo, c->spec, xg, c->stream))
     return fail(c, KGPU_E_DEVICE, std::string("k_tbatch launch failed: ") + hipGetErrorString(hipGetLastError()));
   if (a.trace)
     HIP_OK(c, hipMemcpyAsync(c->trace_host.data(), a.trace, sizeof(int64_t) * 16 * (size_t)(count + 1),
@@ -1654,7 +1694,9 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
   if (rc_abort) return rc_abort;
   int32_t* abort_word = static_cast<int32_t*>(c->abort_buf.p);
   int tper = 0, tgroups = 0;
-  const int tgeo = (topo_on && c->tfast && !diag && !sharded && !cut && !nom_dev && st.K <= 64)
+  // node-sharded engines take the persistent topology kernel over the xGMI mailboxes (the XG
+  // instantiation); without them, the per-pod RCCL pipeline
+  const int tgeo = (topo_on && c->tfast && !diag && (!sharded || xg) && !cut && !nom_dev && st.K <= 64)
                        ? kgpu::tbatch_geometry(st.N, std::min(c->max_groups > 0 ? std::min(c->max_groups, c->n_cus) : c->n_cus, 256),
                                                &tper, &tgroups)
                        : -1;
@@ -1673,7 +1715,7 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
       while (j < n && topo[(size_t)j] && t_add(tr, c, qs[j], plans[(size_t)j], pp, aux, aux_terms, j)) ++j;
       if (j > i) {
         if (c->timing) HIP_OK(c, hipEventRecord(get_event(c, ev), c->stream));
-        if ((rc = run_tbatch(c, tr, i, j - i, first_seq, assume, tper, tgroups, tgeo, abort_word))) return rc;
+        if ((rc = run_tbatch(c, tr, i, j - i, first_seq, assume, tper, tgroups, tgeo, abort_word, xg))) return rc;
         if (c->timing) HIP_OK(c, hipEventRecord(get_event(c, ev + 1), c->stream));
         ev += 2;
         timed_passes += j - i;
@@ -2403,6 +2445,7 @@ int apply_delta(kgpu_ctx* c, const kgpu_delta_batch* b, int32_t* slots) {
   if (b->n_order > 0 && (rc = reorder_nodes(c, b))) return rc;
   fail_point();
   if ((rc = update_key_meta(c, b))) return rc;
+  if (b->key_unique) c->key_unique_caller.assign(b->key_unique, b->key_unique + st.K);
   if (b->n_order <= 0 && (rc = update_csr(c, b))) return rc;
   if (b->n_zones > st.n_zones) st.n_zones = b->n_zones;
   const kgpu_pools& P = b->pools;
@@ -2796,6 +2839,8 @@ int kgpu_upload_snapshot(kgpu_ctx* c, const kgpu_snapshot* s, int64_t generation
   c->key_empty.assign(s->key_empty_value ? s->key_empty_value : nullptr,
                       s->key_empty_value ? s->key_empty_value + st.K : nullptr);
   rebuild_node_books(c);
+  c->key_unique_caller.clear();
+  if (s->key_unique) c->key_unique_caller.assign(s->key_unique, s->key_unique + st.K);
   c->class_ids.clear();
   c->tclass_ids.clear();
   c->classes.clear();
@@ -3226,8 +3271,14 @@ int kgpu_xgmi_handle(kgpu_ctx* c, int32_t nranks, uint8_t handle[64]) try {
   c->xg_open.clear();
   if (c->xg_box.p) HIP_OK(c, hipFree(c->xg_box.p));
   c->xg_box = DevBuf{};
-  HIP_OK(c, hipMalloc(&c->xg_box.p, cells * (sizeof(uint64_t) + sizeof(int32_t))));
-  c->xg_box.bytes = cells * (sizeof(uint64_t) + sizeof(int32_t));
+  // [granule ring | feasible-count ring | topology TX ring | init-reduction mailbox]
+  auto up256 = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  c->xg_tx_off = up256(cells * (sizeof(uint64_t) + sizeof(int32_t)));
+  c->xg_init_off = up256(c->xg_tx_off + sizeof(uint64_t) * (size_t)kgpu::kTXRing * (size_t)kgpu::tx_row_words(nranks));
+  const size_t box = c->xg_init_off + sizeof(int32_t) * 2 * (size_t)nranks * kgpu::kXInitCap +
+                     sizeof(uint64_t) * 2 * (size_t)nranks;
+  HIP_OK(c, hipMalloc(&c->xg_box.p, box));
+  c->xg_box.bytes = box;
   // zeroed before any peer can learn the handle: no lap of the ring reads as valid
   HIP_OK(c, hipMemset(c->xg_box.p, 0, c->xg_box.bytes));
   HIP_OK(c, hipDeviceSynchronize());
@@ -3248,7 +3299,7 @@ int kgpu_xgmi_init(kgpu_ctx* c, int32_t nranks, int32_t rank, const uint8_t* han
   if (!c->xg_box.p || c->xg_GT != nranks * c->xg_groups)
     return fail(c, KGPU_E_STATE, "kgpu_xgmi_handle(nranks) must precede kgpu_xgmi_init");
   const size_t cells = (size_t)kgpu::kXgmiRing * (size_t)c->xg_GT;
-  std::vector<void*> gr((size_t)nranks), fe((size_t)nranks);
+  std::vector<void*> gr((size_t)nranks), fe((size_t)nranks), tx((size_t)nranks), xi((size_t)nranks);
   for (int r = 0; r < nranks; ++r) {
     void* base = nullptr;
     if (r == rank) {
@@ -3273,15 +3324,22 @@ int kgpu_xgmi_init(kgpu_ctx* c, int32_t nranks, int32_t rank, const uint8_t* han
     }
     gr[(size_t)r] = base;
     fe[(size_t)r] = static_cast<uint64_t*>(base) + cells;
+    tx[(size_t)r] = static_cast<char*>(base) + c->xg_tx_off;
+    xi[(size_t)r] = static_cast<char*>(base) + c->xg_init_off;
   }
+  // device array: granule bases | feasible-count bases | TX ring bases | init mailbox bases
   std::vector<void*> arr(gr);
   arr.insert(arr.end(), fe.begin(), fe.end());
+  arr.insert(arr.end(), tx.begin(), tx.end());
+  arr.insert(arr.end(), xi.begin(), xi.end());
   int rc = ensure(c, c->xg_arr, sizeof(void*) * arr.size());
   if (rc) return rc;
   HIP_OK(c, hipMemcpy(c->xg_arr.p, arr.data(), sizeof(void*) * arr.size(), hipMemcpyHostToDevice));
   c->xg_nranks = nranks;
   c->xg_rank = rank;
   c->xg_seq = 0;
+  c->xt_seq = 0;
+  c->xr_seq = 0;
   return KGPU_OK;
 } catch (...) {
   return on_exception(c, false);

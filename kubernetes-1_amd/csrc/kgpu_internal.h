@@ -393,7 +393,38 @@ struct TBatchArgs {
   int64_t* trace;        // null, or [count + 1][16] s_memrealtime stamps (KGPU_OPT_PHASE_TRACE): per pod
                           // and traced workgroup (0, last): start, PreFilter minima, rows evaluated,
                           // stats published, stats resolved, key published, winner resolved, end
+  // ---- node sharding over xGMI (the XG instantiation; kgpu_xgmi_init).  Each rank runs the local
+  // protocol above over its own shard, then one record per rank crosses the ranks through the
+  // topology mailbox ring (TX row, below): its combined statistics (published by workgroup 0) and its
+  // best key with the winning node's label values and signature bits (published by the rank's local
+  // winner, info before key).  Every workgroup of every rank combines the nranks records itself.
+  // Pod i sits on ring row (xseq0 + i) % kTXRing; records carry the lap in bits 60-62.
+  uint64_t* const* ptx;   // [nranks] TX ring bases (this rank's own at [rank])
+  int32_t nranks, rank;
+  int64_t xseq0;
 };
+
+// TX row of the topology mailbox ring, in u64 words: stats [nranks][kTXRCap] | keys [nranks] |
+// info [nranks][kTXInfo / 2] (int32: the winner's value of each of the first 64 node label keys, then
+// two words of signature bits).  Stats records are biased by kTXBias into bits 0-59.
+constexpr int kTXRing = 8;
+constexpr int kTXRCap = 64;          // >= kTFixed + kTMaxSoftWords + kTMaxZones
+constexpr int kTXInfo = 68;          // int32 per info record (64 label values + 2 signature words + pad)
+constexpr int64_t kTXBias = 1ll << 58;
+constexpr int64_t tx_row_words(int nranks) { return (int64_t)nranks * (kTXRCap + 1 + kTXInfo / 2); }
+// Cross-rank reduction of a run's histogram initialization (k_xput / k_xflag / k_xsum): words
+// [0, n_sum) are summed over the ranks, [n_sum, n_sum + n_or) OR-ed.  Per rank the init mailbox holds
+// [2 parities][nranks][kXInitCap] int32 partials, then [2][nranks] u64 arrival flags (sequence numbers).
+constexpr int kXInitCap = 40960;
+struct XReduce {
+  int32_t* const* pinit;  // [nranks] init mailbox bases (own at [rank])
+  int32_t nranks, rank, parity, pad;
+  uint64_t seq;           // identical on every rank: the flag value of this reduction
+  int32_t* buf;           // local partials in, reduced values out
+  int32_t n_sum, n_or;
+  int32_t* abort;
+};
+int launch_xreduce(const XReduce& x, void* stream);
 
 // ---------------------------------------------------------------- nominated pods / preemption
 // One pod added to (nominated, pass 1) or removed from (potential victim) a node, resolved against
@@ -480,7 +511,10 @@ int launch_topo_phase(const DevState* st, const PodArgs& a, int phase, int block
 // Persistent topology run: signature bitmaps + pair registrations (k_sig_init), histogram
 // initialization from the match-count columns (k_hist_init), then k_tbatch.  kidx: geometry.
 int tbatch_geometry(int N, int max_groups, int* per, int* groups);
-int launch_tbatch(const DevState* st, const TBatchArgs& a, int groups, int geo, int spec, void* stream);
+// k_sig_init + k_hist_init over the local nodes (a.per * groups >= N); then, on a node-sharded
+// engine, launch_xreduce over the init region; then launch_tbatch (xg: the XG instantiation).
+int launch_tbatch_init(const DevState* st, const TBatchArgs& a, int groups, void* stream);
+int launch_tbatch(const DevState* st, const TBatchArgs& a, int groups, int geo, int spec, bool xg, void* stream);
 
 // ---------------------------------------------------------------- delta stream (kgpu_apply_delta)
 enum DeltaKind { kDAddPod = 0, kDRemovePod = 1, kDSetNode = 2 };

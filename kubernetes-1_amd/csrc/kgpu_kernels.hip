@@ -31,6 +31,8 @@
 //   assume   framework/v1alpha1/types.go:456-480 (NodeInfo.AddPod)
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "kgpu_internal.h"
 
 // Address spaces exist only in the device pass; the host pass parses the same code unqualified.
@@ -2336,8 +2338,10 @@ __device__ __forceinline__ int64_t wave_op_i64(int op, int64_t x) {
     default: return (int64_t)wave_red64((uint64_t)x, OpOrU64{});
   }
 }
+// identities of the statistics operations: beyond every real value, and inside the +-2^58 range the
+// cross-rank records carry (kTXBias)
 __device__ __forceinline__ int64_t tident(int op) {
-  return op == kOpMax ? INT64_MIN / 4 : (op == kOpMin ? INT64_MAX / 4 : 0);
+  return op == kOpMax ? -(1ll << 56) : (op == kOpMin ? (1ll << 56) : 0);
 }
 
 struct TMisc {
@@ -2377,6 +2381,48 @@ __device__ __forceinline__ bool tpoll_slot(const uint64_t* row, int G, const int
       return true;
     }
     if (load_sc1(abort_word) != 0 || __builtin_amdgcn_s_memrealtime() - t0 > kSpinTimeout) return false;
+  }
+}
+
+// ---- node sharding over xGMI (k_tbatch XG): the topology mailbox ring (kgpu_internal.h TX row)
+constexpr uint64_t kTagMask = 0xFull << 60;
+constexpr uint64_t kPayload60 = (1ull << 60) - 1;
+__device__ __forceinline__ void store_sys(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void store_sys(int32_t* p, int32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint64_t load_sys(const uint64_t* p) {
+  return __hip_atomic_load(const_cast<uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ int32_t load_sys(const int32_t* p) {
+  return __hip_atomic_load(const_cast<int32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ int32_t* tx_info(uint64_t* row, int nranks, int r) {
+  return reinterpret_cast<int32_t*>(row + (size_t)nranks * (kTXRCap + 1)) + (size_t)r * kTXInfo;
+}
+// Every rank's record of one statistics slot (`base` = the slot of rank 0 in this pod's row),
+// combined with the slot's operation; the record of rank r is at base + r * kTXRCap.  False on timeout
+// or abort.
+__device__ __forceinline__ bool xpoll_stat(const uint64_t* base, int nranks, const int32_t* abort_word, int op,
+                                           uint64_t tag, int64_t& out) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  for (;;) {
+    bool ok = true;
+    int64_t v = tident(op);
+    if (lane < nranks) {
+      const uint64_t u = load_sys(base + (size_t)lane * kTXRCap);
+      if ((u & kTagMask) != tag) ok = false;
+      else v = (int64_t)(u & kPayload60) - kTXBias;
+    }
+    if (__all(ok)) {
+      out = wave_op_i64(op, v);
+      return true;
+    }
+    if (load_sc1(abort_word) != 0 || __builtin_amdgcn_s_memrealtime() - t0 > kSpinTimeout) return false;
+    __builtin_amdgcn_s_sleep(1);
   }
 }
 
@@ -2551,9 +2597,10 @@ __device__ __forceinline__ uint32_t trow_eval(const DevState& st, const TBatchAr
   return 0;
 }
 
-template <int B, int K, uint32_t FM, uint32_t SM, bool kDef>
+template <int B, int K, uint32_t FM, uint32_t SM, bool kDef, bool XG>
 __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, TBatchArgs ta) {
   const DevState& st = *stp;
+  __shared__ uint64_t* sh_ptx[XG ? kMaxRanks : 1];  // every rank's TX ring base (XG)
   extern __shared__ __attribute__((aligned(16))) char lds_raw[];
   int32_t* H = reinterpret_cast<int32_t*>(lds_raw);
   uint32_t* REG = reinterpret_cast<uint32_t*>(lds_raw + ta.o_reg);
@@ -2579,6 +2626,10 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
     LAB[i] = n < st.N ? gp(st.label_val)[(size_t)k * st.N + n] : -1;
   }
   if (tid == 0) M.abort = 0;
+  if constexpr (XG) {
+    if (tid < ta.nranks) sh_ptx[tid] = ta.ptx[tid];
+  }
+  const int64_t txw = XG ? tx_row_words(ta.nranks) : 0;
   NodeRes r[K];
   TStatic sr[K];
 #pragma unroll
@@ -2737,11 +2788,34 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
     }
     KGPU_TSTAMP(3);
     bool ok = true;
+    // XG: this pod's TX row and record tag (ring lap in bits 60-62)
+    uint64_t* txrow = nullptr;
+    uint64_t txtag = 0;
+    if constexpr (XG) {
+      txrow = sh_ptx[ta.rank] + (size_t)((ta.xseq0 + i) % kTXRing) * txw;
+      txtag = kGValid | ((uint64_t)(((ta.xseq0 + i) / kTXRing) & 7) << 60);
+    }
     for (int rr = wave; rr < R; rr += W) {
       const int op = rr < kTFixed ? tstat_op(rr) : (rr < kTFixed + ta.soft_words ? kOpOr : kOpSum);
       int64_t x;
       if (!tpoll_slot(srow + (size_t)rr * G, G, ta.abort, op, x)) { ok = false; break; }
+      if constexpr (XG) {
+        // this rank's combined slot: workgroup 0 publishes it into every rank's ring
+        if (g == 0 && lane < ta.nranks) {
+          const size_t off = (size_t)(txrow - sh_ptx[ta.rank]) + (size_t)ta.rank * kTXRCap + rr;
+          store_sys(sh_ptx[lane] + off, txtag | (uint64_t)(x + kTXBias));
+        }
+      }
       if (lane == 0) STAT[rr] = x;
+    }
+    if constexpr (XG) {
+      // every rank's record of the wave's slots, combined: the cluster-wide statistics
+      for (int rr = wave; ok && rr < R; rr += W) {
+        const int op = rr < kTFixed ? tstat_op(rr) : (rr < kTFixed + ta.soft_words ? kOpOr : kOpSum);
+        int64_t x;
+        if (!xpoll_stat(txrow + rr, ta.nranks, ta.abort, op, txtag, x)) { ok = false; break; }
+        if (lane == 0) STAT[rr] = x;
+      }
     }
     if (!ok && lane == 0) {
       __hip_atomic_store(ta.abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2828,8 +2902,67 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
       KGPU_TSTAMP(5);
       uint64_t wkey = 0;
       int wg = -1;
-      const bool pok = poll_row<4, false>(arow, G, ta.abort, kGValid, kGValid, wkey, wg);
-      if (lane == 0) {
+      bool pok = poll_row<4, false>(arow, G, ta.abort, kGValid, kGValid, wkey, wg);
+      if constexpr (XG) {
+        // this rank's best: its local winner publishes the record -- the winning node's label values
+        // and signature bits first, then (after a system-scope release) the key; workgroup 0 publishes
+        // a key-0 record when no node of this rank is feasible
+        const size_t roff = (size_t)(txrow - sh_ptx[ta.rank]);
+        if (pok && (wg >= 0 ? wg == g : g == 0)) {
+          if (wkey) {
+            const int wl = (int)rank40_inv(tk, wkey & kMask40, st.tie_mode) - st.node_base;
+            const int lab = lane < ta.n_keys ? (lane < ta.lab_keys ? LAB[lane * ta.per + (wl - lo)]
+                                                                  : gp(st.label_val)[(size_t)lane * st.N + wl])
+                                             : -1;
+            const uint64_t eb = __ballot(lane < ta.n_sigs && tb_elig(ta, lane, wl));
+            for (int rk = 0; rk < ta.nranks; ++rk) {
+              int32_t* inf = tx_info(sh_ptx[rk] + roff, ta.nranks, ta.rank);
+              store_sys(inf + lane, lab);
+              if (lane < 2) store_sys(inf + 64 + lane, (int32_t)(uint32_t)(eb >> (32 * lane)));
+            }
+            __threadfence_system();
+          }
+          if (lane < ta.nranks) store_sys(sh_ptx[lane] + roff + (size_t)ta.nranks * kTXRCap + ta.rank, txtag | wkey);
+        }
+        // every rank's best: the cluster-wide winner and its rank's record
+        uint64_t gk = 0;
+        int gr = -1;
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (pok) {
+          bool all = true;
+          uint64_t k = 0;
+          if (lane < ta.nranks) {
+            const uint64_t u = load_sys(txrow + (size_t)ta.nranks * kTXRCap + lane);
+            if ((u & kTagMask) != txtag) all = false;
+            else k = u & kPayload60;
+          }
+          if (__all(all)) {
+            int li = lane;
+            wave_argmax(k, li);
+            gk = k;
+            gr = k ? li : -1;
+            break;
+          }
+          if (load_sc1(ta.abort) != 0 || __builtin_amdgcn_s_memrealtime() - t0 > kSpinTimeout) pok = false;
+          else __builtin_amdgcn_s_sleep(1);
+        }
+        if (pok && gk) {
+          const int32_t* inf = tx_info(txrow, ta.nranks, gr);
+          const int32_t lab = load_sys(inf + lane);
+          const uint32_t ew = (uint32_t)load_sys(inf + 64 + (lane >> 5));
+          if (lane < ta.n_keys) M.wlab[lane] = lab;
+          if (lane < ta.n_sigs) M.welig[lane] = (int32_t)((ew >> (lane & 31)) & 1u);
+        }
+        if (lane == 0) {
+          if (!pok) {
+            __hip_atomic_store(ta.abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            M.abort = 1;
+          }
+          M.wkey = gk;
+          M.wg = (gr == ta.rank) ? wg : -1;  // the local winner applies the assume on the owning rank
+          M.wnode = gk ? (int)rank40_inv(tk, gk & kMask40, st.tie_mode) : -1;
+        }
+      } else if (lane == 0) {
         if (!pok) {
           __hip_atomic_store(ta.abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           M.abort = 1;
@@ -2846,7 +2979,9 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
     const int wnode = M.wnode;  // global index
     const bool error = (q.flags & KGPU_Q_SCORE_ERROR) && feas_total >= 2;
     const bool placed = feas_total > 0 && !error;
-    if (tid == 0 && ((M.wg >= 0 && M.wg == g) || (M.wg < 0 && g == 0))) {
+    // the record: unsharded by the winning workgroup; XG by workgroup 0 of every rank (every rank
+    // returns the same records)
+    if (tid == 0 && (XG ? g == 0 : ((M.wg >= 0 && M.wg == g) || (M.wg < 0 && g == 0)))) {
       kgpu_result res;
       res.node = placed ? wnode : (error ? -2 : -1);
       res.feasible = (int32_t)feas_total;
@@ -2857,10 +2992,13 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
     }
     if (placed && ta.assume) {
       const int wl = wnode - st.node_base;
-      // the winner's label values and signature bits, staged once for every delta
-      if (tid < ta.n_keys) M.wlab[tid] = gp(st.label_val)[(size_t)tid * st.N + wl];
-      else if (tid >= 64 && tid - 64 < ta.n_sigs) M.welig[tid - 64] = tb_elig(ta, tid - 64, wl) ? 1 : 0;
-      __syncthreads();
+      // the winner's label values and signature bits, staged once for every delta (XG: from the
+      // winning rank's record, staged by wave 0)
+      if constexpr (!XG) {
+        if (tid < ta.n_keys) M.wlab[tid] = gp(st.label_val)[(size_t)tid * st.N + wl];
+        else if (tid >= 64 && tid - 64 < ta.n_sigs) M.welig[tid - 64] = tb_elig(ta, tid - 64, wl) ? 1 : 0;
+        __syncthreads();
+      }
       for (int d = tid; d < tp.deltas.count; d += B) {
         const TDelta dl = cp(ta.deltas)[tp.deltas.begin + d];
         if (dl.sig >= 0 && !M.welig[dl.sig]) continue;
@@ -2887,6 +3025,70 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
 #undef KGPU_TSTAMP
 }
 
+// ---------------------------------------------------------------- cross-rank init reduction
+// A node-sharded persistent topology run starts from cluster-wide histograms: every rank's partial
+// (k_hist_init over its own nodes) is summed -- and its pair registrations / signature flags OR-ed --
+// over the ranks through the init mailbox (kgpu_internal.h XReduce).  Three launches on the stream:
+// k_xput copies the partial into every rank's mailbox slot of this rank, k_xflag raises this rank's
+// arrival flag everywhere after a system-scope release, k_xsum waits for every rank's flag and reduces
+// the nranks partials in its own mailbox into the local buffer.  Parity-indexed slots: a rank reaches
+// reduction s + 2 only after every rank finished reading reduction s.
+__global__ void k_xput(XReduce x) {
+  const int n = x.n_sum + x.n_or;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int32_t v = x.buf[i];
+    for (int r = 0; r < x.nranks; ++r)
+      store_sys(x.pinit[r] + ((size_t)x.parity * x.nranks + x.rank) * kXInitCap + i, v);
+  }
+}
+__device__ __forceinline__ uint64_t* xflags(int32_t* base, int nranks) {
+  return reinterpret_cast<uint64_t*>(base + 2 * (size_t)nranks * kXInitCap);
+}
+__global__ void k_xflag(XReduce x) {
+  __threadfence_system();
+  for (int r = 0; r < x.nranks; ++r) store_sys(xflags(x.pinit[r], x.nranks) + x.parity * x.nranks + x.rank, x.seq);
+}
+__global__ void k_xsum(XReduce x) {
+  __shared__ int ok;
+  if (threadIdx.x == 0) {
+    const uint64_t* f = xflags(x.pinit[x.rank], x.nranks) + x.parity * x.nranks;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    ok = 1;
+    for (int r = 0; r < x.nranks && ok; ++r)
+      while (load_sys(f + r) != x.seq) {
+        if (load_sc1(x.abort) != 0 || __builtin_amdgcn_s_memrealtime() - t0 > kSpinTimeout) {
+          __hip_atomic_store(x.abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ok = 0;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+  }
+  __syncthreads();
+  if (!ok) return;
+  const int n = x.n_sum + x.n_or;
+  const int32_t* own = x.pinit[x.rank] + (size_t)x.parity * x.nranks * kXInitCap;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    int32_t acc = 0;
+    for (int r = 0; r < x.nranks; ++r) {
+      const int32_t v = load_sys(own + (size_t)r * kXInitCap + i);
+      acc = i < x.n_sum ? acc + v : (acc | v);
+    }
+    x.buf[i] = acc;
+  }
+}
+
+int launch_xreduce(const XReduce& x, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const int n = x.n_sum + x.n_or;
+  if (n <= 0 || n > kXInitCap || x.nranks < 1 || x.nranks > kMaxRanks) return -1;
+  const int nb = std::min((n + 255) / 256, 256);
+  hipLaunchKernelGGL(k_xput, dim3(nb), dim3(256), 0, s, x);
+  hipLaunchKernelGGL(k_xflag, dim3(1), dim3(1), 0, s, x);
+  hipLaunchKernelGGL(k_xsum, dim3(std::min(nb, 64)), dim3(256), 0, s, x);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 // ---------------------------------------------------------------- profile instantiations
 constexpr uint32_t bit(int i) { return 1u << i; }
 // config (b) of BASELINE.json: NodeResourcesFit + BalancedAllocation + LeastAllocated
@@ -2908,15 +3110,17 @@ struct TGeo {
 constexpr TGeo kTGeo[] = {{512, 1}, {512, 2}};
 constexpr int kNumTGeo = 2;
 using TBatchFn = void (*)(const DevState*, TBatchArgs);
-template <uint32_t FM, uint32_t SM, bool kDef>
+template <uint32_t FM, uint32_t SM, bool kDef, bool XG>
 struct TBatchRow {
-  static constexpr TBatchFn fn[kNumTGeo] = {k_tbatch<512, 1, FM, SM, kDef>, k_tbatch<512, 2, FM, SM, kDef>};
+  static constexpr TBatchFn fn[kNumTGeo] = {k_tbatch<512, 1, FM, SM, kDef, XG>, k_tbatch<512, 2, FM, SM, kDef, XG>};
 };
 // rows: 0 generic, 1 generic with Least/Most over {cpu:1, memory:1}, 2 default provider,
-// 3 ClusterAutoscaler provider
-static const TBatchFn* const kTBatch[] = {
-    TBatchRow<kRuntime, kRuntime, false>::fn, TBatchRow<kRuntime, kRuntime, true>::fn,
-    TBatchRow<kDefaultFM, kDefaultSM, true>::fn, TBatchRow<kDefaultFM, kAutoscalerSM, true>::fn};
+// 3 ClusterAutoscaler provider; [1]: the node-sharded (xGMI) instantiations
+static const TBatchFn* const kTBatch[2][4] = {
+    {TBatchRow<kRuntime, kRuntime, false, false>::fn, TBatchRow<kRuntime, kRuntime, true, false>::fn,
+     TBatchRow<kDefaultFM, kDefaultSM, true, false>::fn, TBatchRow<kDefaultFM, kAutoscalerSM, true, false>::fn},
+    {TBatchRow<kRuntime, kRuntime, false, true>::fn, TBatchRow<kRuntime, kRuntime, true, true>::fn,
+     TBatchRow<kDefaultFM, kDefaultSM, true, true>::fn, TBatchRow<kDefaultFM, kAutoscalerSM, true, true>::fn}};
 
 int tbatch_geometry(int N, int max_groups, int* per, int* groups) {
   for (int gi = 0; gi < kNumTGeo; ++gi) {
@@ -2931,23 +3135,27 @@ int tbatch_geometry(int N, int max_groups, int* per, int* groups) {
   return -1;
 }
 
-// spec: the k_eval profile instantiation (select_spec), def_res from the TBatchArgs
-int launch_tbatch(const DevState* st, const TBatchArgs& a, int groups, int geo, int spec, void* stream) {
-  if (geo < 0 || geo >= kNumTGeo) return -1;
+int launch_tbatch_init(const DevState* st, const TBatchArgs& a, int groups, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const int N = a.per * groups;  // >= st->N
   const int nb = (N + 255) / 256;
   hipLaunchKernelGGL(k_sig_init, dim3(nb), dim3(256), 0, s, st, a);
   hipLaunchKernelGGL(k_hist_init, dim3(nb), dim3(256), 0, s, st, a);
-  if (hipGetLastError() != hipSuccess) return -1;
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// spec: the k_eval profile instantiation (select_spec), def_res from the TBatchArgs
+int launch_tbatch(const DevState* st, const TBatchArgs& a, int groups, int geo, int spec, bool xg, void* stream) {
+  if (geo < 0 || geo >= kNumTGeo) return -1;
+  hipStream_t s = (hipStream_t)stream;
   const int row = spec == 2 ? 2 : (spec == 3 ? 3 : (a.def_res ? 1 : 0));
-  const TBatchFn fn = kTBatch[row][geo];
-  static bool attr[4][kNumTGeo] = {};
-  if (!attr[row][geo]) {
+  const TBatchFn fn = kTBatch[xg ? 1 : 0][row][geo];
+  static bool attr[2][4][kNumTGeo] = {};
+  if (!attr[xg ? 1 : 0][row][geo]) {
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
                             kTLdsBudget) != hipSuccess)
       return -1;
-    attr[row][geo] = true;
+    attr[xg ? 1 : 0][row][geo] = true;
   }
   // one workgroup per CU (>= 80 KB of LDS each); the cooperative launch checks co-residency
   TBatchArgs arg = a;

@@ -3,7 +3,7 @@ import ctypes as C
 
 import numpy as np
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 OK, E_INVAL, E_NOMEM, E_DEVICE, E_CAPACITY, E_STATE, E_UNSUPPORTED = 0, -1, -2, -3, -4, -5, -6
 ERRNAMES = {0: "OK", -1: "KGPU_E_INVAL", -2: "KGPU_E_NOMEM", -3: "KGPU_E_DEVICE", -4: "KGPU_E_CAPACITY",
             -5: "KGPU_E_STATE", -6: "KGPU_E_UNSUPPORTED"}
@@ -105,7 +105,7 @@ class Snapshot(C.Structure):
                 ("avoid_off", vp), ("avoid_id", vp), ("zone_id", vp), ("n_zones", C.c_int32),
                 ("n_pods", C.c_int32), ("pod_node", vp), ("pod_ns", vp), ("pod_flags", vp),
                 ("n_pod_label_keys", C.c_int32), ("n_terms", C.c_int32), ("pod_label_val", vp), ("terms", vp),
-                ("pools", Pools), ("pod_uid", vp)]
+                ("pools", Pools), ("pod_uid", vp), ("key_unique", vp)]
 
 
 D_ADD_POD, D_REMOVE_POD, D_SET_NODE = 1, 2, 3
@@ -121,7 +121,7 @@ class DeltaBatch(C.Structure):
                 ("key_n_values", vp), ("value_off", vp), ("value_int", vp), ("value_int_ok", vp),
                 ("key_empty_value", vp), ("image_off", vp), ("image_id", vp), ("image_score", vp),
                 ("avoid_off", vp), ("avoid_id", vp), ("n_zones", C.c_int32), ("pad", C.c_int32),
-                ("pools", Pools)]
+                ("pools", Pools), ("key_unique", vp)]
 
 
 class Stats(C.Structure):

@@ -500,6 +500,7 @@ class Compiler:
         A["value_int"] = np.array(ints, np.int64)
         A["value_int_ok"] = np.array(oks, np.uint8)
         A["key_empty_value"] = np.array(empty, np.int32)
+        A["key_unique"] = self.key_unique(A["label_val"])
         # images / avoid CSR
         A["image_off"], A["image_id"], A["image_score"] = self._csr(img_lists, True)
         A["avoid_off"], A["avoid_id"], _ = self._csr([[(a, 0) for a in lst] for lst in avoid_lists], False)
@@ -512,7 +513,7 @@ class Compiler:
                   "nz_mem", "num_pods", "alloc_scalar", "req_scalar", "unschedulable", "label_val", "key_n_values",
                   "value_off", "value_int", "value_int_ok", "key_empty_value", "taint_nosched", "taint_prefer",
                   "port_count", "ports", "image_off", "image_id", "image_score", "avoid_off", "avoid_id",
-                  "zone_id", "pod_node", "pod_ns", "pod_flags", "pod_label_val", "terms", "pod_uid"):
+                  "zone_id", "pod_node", "pod_ns", "pod_flags", "pod_label_val", "terms", "pod_uid", "key_unique"):
             if A.get(f) is None:
                 continue
             A[f] = np.ascontiguousarray(A[f])
@@ -529,6 +530,18 @@ class Compiler:
         snap.pools, A["_pools_np"] = A["_pools"].finalize()
         A["_snap"] = snap
         return snap, A, self.order
+
+    @staticmethod
+    def key_unique(label_val):
+        """kgpu_snapshot.key_unique over the WHOLE list (before any shard slice): per node label key,
+        1 when no value labels two nodes -- the engine's hostname-like keys, whose counts a sharded
+        topology run reads from the node's own column."""
+        K = label_val.shape[0]
+        out = np.zeros(K, np.uint8)
+        for k in range(K):
+            v = label_val[k][label_val[k] >= 0]
+            out[k] = 1 if len(np.unique(v)) == len(v) else 0
+        return out
 
     @staticmethod
     def _csr(lists, with_val):

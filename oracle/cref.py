@@ -9,7 +9,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB = os.path.join(HERE, "build", "libkgpu_ref.so")
+# KGPU_REF_LIB: another build of the same source (tests/test_sanitizers.py loads the ASan/UBSan one)
+LIB = os.environ.get("KGPU_REF_LIB") or os.path.join(HERE, "build", "libkgpu_ref.so")
 _lib = None
 
 
