@@ -7,8 +7,10 @@ pods run through the scheduleOne loop (filter -> score -> selectHost -> assume, 
 order) on the device-resident snapshot; K steps x pods-per-step = the config's 10,000 pods.
 
 Prints ONE JSON line (rank 0) with pods/s, node-evals/s, the roofline of the dominant kernel
-(k_eval, timed with HIP events on the engine's stream) and the CPU baseline (the C restatement of
-the reference algorithm, oracle/c, timed on this host's cores on a bounded sample).
+(k_batch / k_tbatch, timed with HIP events on the engine's stream) and the CPU baseline (the C
+restatement of the reference algorithm, oracle/c, timed on this host's cores on a bounded sample).
+At N=1 the line carries an `extra` record of the same config at 100,000 nodes, timed in the same
+run with its own roofline and a 16-worker CPU baseline (BASELINE.json: "at 5k & 100k nodes").
 """
 import argparse
 import json
@@ -22,7 +24,7 @@ for p in (ROOT, os.path.join(ROOT, "kubernetes-1_amd")):
         sys.path.insert(0, p)
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md chip table)
-BYTES_PER_NODE_EVAL = {"b": 72, "a": 73, "c": 121, "d": 84}  # SURVEY.md 8(d) algorithmic bytes per node-eval
+BYTES_PER_NODE_EVAL = {"b": 72, "a": 73, "c": 121, "d": 84, "e": 121}  # SURVEY.md 8(d) algorithmic bytes per node-eval
 BYTES_PER_EXISTING_POD = {"d": 24}  # IPA reads {node, ns, label bitset} per existing pod per pod
 
 
@@ -66,57 +68,45 @@ def make_workload(cfg, n_nodes, n_pods):
     if cfg == "d":
         nodes, ex, pods, prof = cluster.pod_affinity(n_nodes=n_nodes, n_existing=n_nodes, n_pods=n_pods)
         return nodes, ex, [], pods, prof
+    if cfg == "e":  # (b)+(c), zone = i % 64: --nodes is the shard per GPU (1M over 8 GPUs: --nodes 125000)
+        nodes, ex, pods, prof = cluster.sharded_spread(n_nodes=n_nodes, n_pods=n_pods)
+        return nodes, ex, [], pods, prof
     raise SystemExit("config %r not benchmarked yet" % cfg)
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", default="b")
-    ap.add_argument("--nodes", type=int, default=5000)
-    ap.add_argument("--pods-per-step", type=int, default=1000)
-    ap.add_argument("--cpu-sample", type=int, default=-1,
-                    help="pods timed for the CPU baseline (-1: the whole workload, 0: skip)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--latency-pods", type=int, default=200, help="pods timed one at a time through kgpu_schedule_one")
-    ap.add_argument("--no-persistent", action="store_true", help="one evaluation launch per pod")
-    ap.add_argument("--topo-fused", type=int, default=None, help="KGPU_OPT_TOPO_FUSED (default: the library's)")
-    ap.add_argument("--no-topo-persistent", action="store_true",
-                    help="topology pods through the per-pod topology launches instead of k_tbatch")
-    ap.add_argument("--max-groups", type=int, default=0,
-                    help="cap on the persistent kernels' workgroups (KGPU_OPT_PERSIST_GROUPS; 0: one per CU)")
-    ap.add_argument("--shard", action="store_true",
-                    help="at N=1: run the node-sharded path on a one-rank RCCL communicator (exchange overhead)")
-    args = ap.parse_args()
+def pmc_traffic(cfg, n_local, launch_pods, kname):
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 --pmc passes of this
+    exact workload (the newest profiles/r*_pmc_traffic.json holding it; tools/pmc_summary.py), or None."""
+    for fname in ("r03_pmc_traffic.json", "r02_pmc_traffic.json", "r01_pmc_traffic.json"):
+        try:
+            with open(os.path.join(ROOT, "profiles", fname)) as fh:
+                pmc = json.load(fh).get("%s:%d:%d" % (cfg, n_local, launch_pods))
+        except (OSError, ValueError):
+            continue
+        if pmc and pmc["kernel"] == kname:
+            return pmc["traffic_bytes_per_launch"]
+    return None
 
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+
+def measure(args, cfg, n_nodes_per_gpu, B, K, W, cpu_sample, cpu_threads, latency_pods, rank, world, local,
+            dist_on, cpu_thread_counts=None):
+    """One workload: K timed steps of B pods after W warmup steps.  Returns the JSON record (rank 0)."""
     import numpy as np
     import torch
     import torch.distributed as dist
-    dist_on = world > 1
-    if dist_on:
-        dist.init_process_group("nccl", rank=rank, world_size=world)
-        torch.cuda.set_device(local)
-
-    from kgpu import abi
+    from kgpu import abi, native
     from kgpu.framework import GpuFramework
 
-    B, K, W = args.pods_per_step, args.steps, args.warmup
     n_pods = B * K
     t_gen = time.time()
     # N > 1: the cluster is sharded by node across the ranks (SURVEY.md 8(e)); each GPU holds a
-    # --nodes-sized contiguous shard of Snapshot.List() (weak scaling in nodes: the cluster grows
-    # with N), and every pod's shard winners are all-gathered over RCCL.
-    n_cluster = args.nodes * world
-    nodes, existing, init, pods, prof = make_workload(args.config, n_cluster, n_pods)
+    # n_nodes_per_gpu contiguous shard of Snapshot.List() (weak scaling in nodes: the cluster grows
+    # with N), and every pod's shard winners are combined over RCCL / xGMI.
+    n_cluster = n_nodes_per_gpu * world
+    nodes, existing, init, pods, prof = make_workload(cfg, n_cluster, n_pods)
     sharded = dist_on or args.shard
     fw = GpuFramework(prof, nodes, existing, pods_hint=init[:16] + pods[:16], device=local,
                       shard=(rank, world) if sharded else None)
-    from kgpu import native
     if sharded:
         uid = [native.comm_unique_id() if rank == 0 else None]
         if dist_on:
@@ -125,8 +115,8 @@ def main():
     q_all, pc, pnp, errs = fw.compile_pods(init + pods)
     assert not errs, errs
     q_init, q = q_all[:len(init)], q_all[len(init):]
-    log("workload: %d nodes (%d on this rank), %d pods, compiled in %.1fs"
-        % (len(nodes), fw.snap.n_nodes, len(pods), time.time() - t_gen))
+    log("workload %s: %d nodes (%d on this rank), %d pods, compiled in %.1fs"
+        % (cfg, len(nodes), fw.snap.n_nodes, len(pods), time.time() - t_gen))
     eng = fw.engine
     if args.no_persistent:
         eng.set_option(abi.OPT_PERSISTENT, 0)
@@ -202,9 +192,9 @@ def main():
     # per-pod latency of the drop-in step: kgpu_schedule_one (one cycle with assume and the per-node
     # filter / score diagnostics the Go shim's Filter/Score lookups read), wall clock per call
     lat = []
-    if args.latency_pods > 0:
+    if latency_pods > 0:
         reset()
-        for i in range(min(args.latency_pods, len(q))):
+        for i in range(min(latency_pods, len(q))):
             t1 = time.perf_counter()
             eng.schedule_one(q[i], pc, seq=len(q_init) + i, assume=True)
             lat.append((time.perf_counter() - t1) * 1e6)
@@ -216,27 +206,27 @@ def main():
     # eval_launches counts node-evaluation passes (one per pod); with the persistent kernel one
     # launch covers the whole batch, so the per-launch duration is kernel_ms / launches_made
     per_pod_s = kst.eval_kernel_ms / 1e3 / max(kst.eval_launches, 1)
-    bpe = BYTES_PER_NODE_EVAL.get(args.config, 72)
+    bpe = BYTES_PER_NODE_EVAL.get(cfg, 72)
     n_local = fw.snap.n_nodes
-    pod_bytes = n_local * bpe + BYTES_PER_EXISTING_POD.get(args.config, 0) * len(existing)
+    pod_bytes = n_local * bpe + BYTES_PER_EXISTING_POD.get(cfg, 0) * len(existing)
     achieved = pod_bytes / per_pod_s / 1e9
-    topo = args.config in ("c", "d")
-    persistent = not args.no_persistent and (not sharded or (xgmi and not topo)) and not (topo and args.no_topo_persistent)
+    topo = cfg in ("c", "d", "e")
+    persistent = (not args.no_persistent and (not sharded or xgmi) and not (topo and args.no_topo_persistent))
     launch_pods = B if persistent else 1
     kname = ("k_tbatch" if topo else "k_batch") if persistent else ("k_topo_* pipeline" if topo else "k_eval")
 
-    # CPU baseline: the C restatement of the reference algorithm on this host's cores.  Three
-    # worker counts are timed -- 1, the reference's parallelism (16 goroutines,
-    # internal/parallelize/parallelism.go:26), and every core this process may run on -- and the
-    # fastest is reported (the strongest baseline); each one's rate is listed beside it.
+    # CPU baseline: the C restatement of the reference algorithm on this host's cores, at 1 worker,
+    # the reference's parallelism (16 goroutines, internal/parallelize/parallelism.go:26) and every
+    # core this process may run on; the fastest is reported, each rate listed beside it.
     cpu = None
-    if rank == 0 and world == 1 and args.cpu_sample != 0:
+    if rank == 0 and world == 1 and cpu_sample != 0:
         from oracle.cref import RefEngine
-        S = n_pods if args.cpu_sample < 0 else min(args.cpu_sample, n_pods)
+        S = n_pods if cpu_sample < 0 else min(cpu_sample, n_pods)
         host = host_info()
         rates = {}
         best = None
-        for th in sorted({1, args.cpu_threads, host["affinity_cpus"]}):
+        counts = cpu_thread_counts or sorted({1, cpu_threads, host["affinity_cpus"]})
+        for th in counts:
             ref = RefEngine(fw.config, fw.snap, threads=th)
             if len(q_init):
                 ref.schedule(q_init, pc)   # untimed, like the GPU's
@@ -246,7 +236,8 @@ def main():
             ref.close()
             ok = bool(np.array_equal(rres["node"], res_all["node"][:S]))
             rates[str(th)] = round(S / tcpu, 2)
-            log("cpu baseline: %d thread(s): %.1f pods/s (placements %s)" % (th, S / tcpu, "match" if ok else "DIFFER"))
+            log("cpu baseline %s: %d thread(s): %.1f pods/s (placements %s)"
+                % (cfg, th, S / tcpu, "match" if ok else "DIFFER"))
             if best is None or S / tcpu > best[0]:
                 best = (S / tcpu, th, tcpu, ok)
         rate, th, tcpu, ok = best
@@ -258,50 +249,90 @@ def main():
                          % ("the whole workload" if S == n_pods else "the first %d pods" % S, S, tcpu, th,
                             "/".join(sorted(rates, key=int)), "identical to" if ok else "DIFFERENT from")}
 
-    # HBM traffic of the dominant kernel per launch, from the committed rocprofv3 --pmc passes of
-    # this exact workload (the newest profiles/r*_pmc_traffic.json holding it; tools/gpu_pmc1.sh);
-    # null when none exist
-    traffic = None
-    for fname in ("r02_pmc_traffic.json", "r01_pmc_traffic.json"):
-        try:
-            with open(os.path.join(ROOT, "profiles", fname)) as fh:
-                pmc = json.load(fh).get("%s:%d:%d" % (args.config, n_local, launch_pods))
-        except (OSError, ValueError):
-            continue
-        if pmc and pmc["kernel"] == kname:
-            traffic = pmc["traffic_bytes_per_launch"]
-            break
-
-    if rank == 0:
-        line = {
-            "metric": "pods scheduled/sec", "value": round(pods_per_s, 2), "unit": "pods/s", "n_gpus": world,
-            "steps": K, "warmup": W, "ms_per_step": round(1e3 * elapsed / K, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "int64", "data": "synthetic",
-            "config": {"workload": "config(%s): %d nodes / %d pods, %s" % (args.config, len(nodes), n_pods,
-                                                                            "+".join(prof.filters + [s for s, _ in prof.scores])),
-                       "nodes": len(nodes), "nodes_per_gpu": fw.snap.n_nodes, "pods": n_pods, "pods_per_step": B,
-                       "percentage_of_nodes_to_score": 100,
-                       "parallelism": ("node shards x%d, %s" % (world, "granules through xGMI peer stores (persistent kernel)"
-                                                                  if xgmi else "RCCL all-gather per pod"))
-                       if sharded else "1 GPU"},
-            "node_evals_per_s": round(pods_per_s * len(nodes), 1),
-            "placed": placed,
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                         "kernel": kname,
-                         "bytes_per_node_eval": bpe,
-                         "avg_kernel_us": round(per_pod_s * launch_pods * 1e6, 3), "pods_per_launch": launch_pods,
-                         "us_per_pod": round(per_pod_s * 1e6, 4),
-                         "bytes_per_launch": pod_bytes * launch_pods},
-            "cpu_baseline": cpu,
-            "latency": lat_rec,
-        }
-        print(json.dumps(line), flush=True)
-    # release the device context before interpreter teardown (under rocprofv3 the HIP runtime may
-    # be finalized before a garbage-collected engine would be)
+    traffic = pmc_traffic(cfg, n_local, launch_pods, kname)
+    rec = {
+        "metric": "pods scheduled/sec", "value": round(pods_per_s, 2), "unit": "pods/s", "n_gpus": world,
+        "steps": K, "warmup": W, "ms_per_step": round(1e3 * elapsed / K, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "int64", "data": "synthetic",
+        "config": {"workload": "config(%s): %d nodes / %d pods, %s" % (cfg, len(nodes), n_pods,
+                                                                        "+".join(prof.filters + [s for s, _ in prof.scores])),
+                   "nodes": len(nodes), "nodes_per_gpu": fw.snap.n_nodes, "pods": n_pods, "pods_per_step": B,
+                   "percentage_of_nodes_to_score": 100,
+                   "parallelism": ("node shards x%d, %s" % (world, "granules through xGMI peer stores (persistent kernel)"
+                                                              if xgmi else "RCCL all-gather per pod"))
+                   if sharded else "1 GPU"},
+        "node_evals_per_s": round(pods_per_s * len(nodes), 1),
+        "placed": placed,
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                     "kernel": kname,
+                     "bytes_per_node_eval": bpe,
+                     "avg_kernel_us": round(per_pod_s * launch_pods * 1e6, 3), "pods_per_launch": launch_pods,
+                     "us_per_pod": round(per_pod_s * 1e6, 4),
+                     "bytes_per_launch": pod_bytes * launch_pods},
+        "cpu_baseline": cpu,
+        "latency": lat_rec,
+    }
+    # release the device context before the next workload and before interpreter teardown (under
+    # rocprofv3 the HIP runtime may be finalized before a garbage-collected engine would be)
     eng.close()
+    return rec
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="b")
+    ap.add_argument("--nodes", type=int, default=5000)
+    ap.add_argument("--pods-per-step", type=int, default=1000)
+    ap.add_argument("--cpu-sample", type=int, default=-1,
+                    help="pods timed for the CPU baseline (-1: the whole workload, 0: skip)")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--latency-pods", type=int, default=200, help="pods timed one at a time through kgpu_schedule_one")
+    ap.add_argument("--no-persistent", action="store_true", help="one evaluation launch per pod")
+    ap.add_argument("--topo-fused", type=int, default=None, help="KGPU_OPT_TOPO_FUSED (default: the library's)")
+    ap.add_argument("--no-topo-persistent", action="store_true",
+                    help="topology pods through the per-pod topology launches instead of k_tbatch")
+    ap.add_argument("--max-groups", type=int, default=0,
+                    help="cap on the persistent kernels' workgroups (KGPU_OPT_PERSIST_GROUPS; 0: one per CU)")
+    ap.add_argument("--shard", action="store_true",
+                    help="at N=1: run the node-sharded path on a one-rank RCCL communicator (exchange overhead)")
+    ap.add_argument("--extra-nodes", type=int, default=100000,
+                    help="N=1, default workload: a second record, timed in the same run, of the same config at this "
+                         "many nodes (BASELINE.json's metric is quoted at 5k and 100k nodes); 0: none")
+    ap.add_argument("--extra-cpu-sample", type=int, default=1000, help="pods of the extra record's CPU baseline")
+    ap.add_argument("--os-exit", action="store_true",
+                    help="leave through os._exit(0) after printing (profiling runs: see DESIGN.md, rocprofv3 exit)")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    dist_on = world > 1
+    if dist_on:
+        dist.init_process_group("nccl", rank=rank, world_size=world)
+        torch.cuda.set_device(local)
+
+    line = measure(args, args.config, args.nodes, args.pods_per_step, args.steps, args.warmup, args.cpu_sample,
+                   args.cpu_threads, args.latency_pods, rank, world, local, dist_on)
+    if world == 1 and args.extra_nodes > 0 and args.extra_nodes != args.nodes and not args.shard:
+        # the same config at 100k nodes, its own roofline and a 16-worker CPU baseline over
+        # extra_cpu_sample pods (the reference's parallelize.Until width)
+        line["extra"] = [measure(args, args.config, args.extra_nodes, args.pods_per_step, args.steps, args.warmup,
+                                 args.extra_cpu_sample, args.cpu_threads, args.latency_pods, rank, world, local,
+                                 dist_on, cpu_thread_counts=[args.cpu_threads])]
+    if rank == 0:
+        print(json.dumps(line), flush=True)
     if dist_on:
         dist.destroy_process_group()
+    if args.os_exit:
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0)
 
 
 if __name__ == "__main__":

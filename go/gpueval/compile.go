@@ -103,15 +103,15 @@ func (p *pools) wordsRange(ws []uint64) C.kgpu_range {
 // toC copies the pools into C memory owned by the arena.
 func (p *pools) toC(a *arena) *C.kgpu_pools {
 	c := (*C.kgpu_pools)(a.alloc(int(unsafe.Sizeof(C.kgpu_pools{}))))
-	c.reqs, c.n_reqs = cslice(a, p.reqs), C.int32_t(len(p.reqs))
-	c.ints, c.n_ints = (*C.int32_t)(unsafe.Pointer(cslice(a, p.ints))), C.int32_t(len(p.ints))
-	c.words, c.n_words = (*C.uint64_t)(unsafe.Pointer(cslice(a, p.words))), C.int32_t(len(p.words))
-	c.node_terms, c.n_node_terms = cslice(a, p.nodeTerms), C.int32_t(len(p.nodeTerms))
-	c.pref_terms, c.n_pref_terms = cslice(a, p.prefTerms), C.int32_t(len(p.prefTerms))
-	c.spreads, c.n_spreads = cslice(a, p.spreads), C.int32_t(len(p.spreads))
-	c.pod_terms, c.n_pod_terms = cslice(a, p.podTerms), C.int32_t(len(p.podTerms))
-	c.scalars, c.n_scalars = cslice(a, p.scalars), C.int32_t(len(p.scalars))
-	c.ports, c.n_ports = cslice(a, p.ports), C.int32_t(len(p.ports))
+	c.reqs, c.n_reqs = cReqs(a, p.reqs), C.int32_t(len(p.reqs))
+	c.ints, c.n_ints = ci32(a, p.ints), C.int32_t(len(p.ints))
+	c.words, c.n_words = cu64(a, p.words), C.int32_t(len(p.words))
+	c.node_terms, c.n_node_terms = cNodeTerms(a, p.nodeTerms), C.int32_t(len(p.nodeTerms))
+	c.pref_terms, c.n_pref_terms = cPrefTerms(a, p.prefTerms), C.int32_t(len(p.prefTerms))
+	c.spreads, c.n_spreads = cSpreads(a, p.spreads), C.int32_t(len(p.spreads))
+	c.pod_terms, c.n_pod_terms = cPodTerms(a, p.podTerms), C.int32_t(len(p.podTerms))
+	c.scalars, c.n_scalars = cScalars(a, p.scalars), C.int32_t(len(p.scalars))
+	c.ports, c.n_ports = cPorts(a, p.ports), C.int32_t(len(p.ports))
 	return c
 }
 

@@ -21,8 +21,6 @@ type metav1LabelSelector = metav1.LabelSelector
 
 var unsafeSizeofSnapshot = unsafe.Sizeof(C.kgpu_snapshot{})
 
-func ci64(a *arena, s []int64) *C.int64_t { return (*C.int64_t)(unsafe.Pointer(cslice(a, s))) }
-func ci32(a *arena, s []int32) *C.int32_t { return (*C.int32_t)(unsafe.Pointer(cslice(a, s))) }
 
 // argsFrom decodes the GpuEval pluginConfig args (INTEGRATION.md section 4).
 func argsFrom(obj runtime.Object) (*profileArgs, error) {
@@ -119,12 +117,13 @@ func filterReasons(plugin string, detail uint32) []string {
 	case "TaintToleration":
 		return []string{"node(s) had taints that the pod didn't tolerate"}
 	case "NodeResourcesFit":
+		// fit.go:194-267 order: pods, cpu, memory, ephemeral-storage
 		var out []string
 		if detail&1 != 0 {
 			out = append(out, "Too many pods")
 		}
-		for bit, r := range map[uint32]string{2: "cpu", 4: "memory", 8: "ephemeral-storage"} {
-			if detail&bit != 0 {
+		for i, r := range []string{"cpu", "memory", "ephemeral-storage"} {
+			if detail&(2<<uint(i)) != 0 {
 				out = append(out, "Insufficient "+r)
 			}
 		}

@@ -40,16 +40,139 @@ func (a *arena) free() {
 	a.ptrs = nil
 }
 
-// cslice copies a Go slice of plain values (no pointers) into C memory.
-func cslice[T any](a *arena, s []T) *T {
+// cmem copies n elements of elem bytes from a Go slice of plain values (no Go pointers inside)
+// into C memory owned by the arena.  The typed wrappers below replace a generic helper: the
+// reference tree builds with go 1.13 (/root/reference/go.mod), which has no type parameters.
+func cmem(a *arena, first unsafe.Pointer, n, elem int) unsafe.Pointer {
+	p := a.alloc(n * elem)
+	C.memcpy(p, first, C.size_t(n*elem))
+	return p
+}
+
+func ci32(a *arena, s []int32) *C.int32_t {
 	if len(s) == 0 {
 		return nil
 	}
-	var z T
-	n := int(unsafe.Sizeof(z)) * len(s)
-	p := a.alloc(n)
-	C.memcpy(p, unsafe.Pointer(&s[0]), C.size_t(n))
-	return (*T)(p)
+	return (*C.int32_t)(cmem(a, unsafe.Pointer(&s[0]), len(s), 4))
+}
+
+func ci64(a *arena, s []int64) *C.int64_t {
+	if len(s) == 0 {
+		return nil
+	}
+	return (*C.int64_t)(cmem(a, unsafe.Pointer(&s[0]), len(s), 8))
+}
+
+func cu8(a *arena, s []uint8) *C.uint8_t {
+	if len(s) == 0 {
+		return nil
+	}
+	return (*C.uint8_t)(cmem(a, unsafe.Pointer(&s[0]), len(s), 1))
+}
+
+func cu32(a *arena, s []uint32) *C.uint32_t {
+	if len(s) == 0 {
+		return nil
+	}
+	return (*C.uint32_t)(cmem(a, unsafe.Pointer(&s[0]), len(s), 4))
+}
+
+func cu64(a *arena, s []uint64) *C.uint64_t {
+	if len(s) == 0 {
+		return nil
+	}
+	return (*C.uint64_t)(cmem(a, unsafe.Pointer(&s[0]), len(s), 8))
+}
+
+func cReqs(a *arena, s []C.kgpu_req) *C.kgpu_req {
+	if len(s) == 0 {
+		return nil
+	}
+	return (*C.kgpu_req)(cmem(a, unsafe.Pointer(&s[0]), len(s), int(unsafe.Sizeof(s[0]))))
+}
+
+func cNodeTerms(a *arena, s []C.kgpu_node_term) *C.kgpu_node_term {
+	if len(s) == 0 {
+		return nil
+	}
+	return (*C.kgpu_node_term)(cmem(a, unsafe.Pointer(&s[0]), len(s), int(unsafe.Sizeof(s[0]))))
+}
+
+func cPrefTerms(a *arena, s []C.kgpu_pref_term) *C.kgpu_pref_term {
+	if len(s) == 0 {
+		return nil
+	}
+	return (*C.kgpu_pref_term)(cmem(a, unsafe.Pointer(&s[0]), len(s), int(unsafe.Sizeof(s[0]))))
+}
+
+func cSpreads(a *arena, s []C.kgpu_spread) *C.kgpu_spread {
+	if len(s) == 0 {
+		return nil
+	}
+	return (*C.kgpu_spread)(cmem(a, unsafe.Pointer(&s[0]), len(s), int(unsafe.Sizeof(s[0]))))
+}
+
+func cPodTerms(a *arena, s []C.kgpu_pod_term) *C.kgpu_pod_term {
+	if len(s) == 0 {
+		return nil
+	}
+	return (*C.kgpu_pod_term)(cmem(a, unsafe.Pointer(&s[0]), len(s), int(unsafe.Sizeof(s[0]))))
+}
+
+func cTerms(a *arena, s []C.kgpu_term) *C.kgpu_term {
+	if len(s) == 0 {
+		return nil
+	}
+	return (*C.kgpu_term)(cmem(a, unsafe.Pointer(&s[0]), len(s), int(unsafe.Sizeof(s[0]))))
+}
+
+func cScalars(a *arena, s []C.kgpu_scalar_req) *C.kgpu_scalar_req {
+	if len(s) == 0 {
+		return nil
+	}
+	return (*C.kgpu_scalar_req)(cmem(a, unsafe.Pointer(&s[0]), len(s), int(unsafe.Sizeof(s[0]))))
+}
+
+func cPorts(a *arena, s []C.kgpu_port) *C.kgpu_port {
+	if len(s) == 0 {
+		return nil
+	}
+	return (*C.kgpu_port)(cmem(a, unsafe.Pointer(&s[0]), len(s), int(unsafe.Sizeof(s[0]))))
+}
+
+func cQueries(a *arena, s []C.kgpu_pod_query) *C.kgpu_pod_query {
+	if len(s) == 0 {
+		return nil
+	}
+	return (*C.kgpu_pod_query)(cmem(a, unsafe.Pointer(&s[0]), len(s), int(unsafe.Sizeof(s[0]))))
+}
+
+func cNominated(a *arena, s []C.kgpu_nominated) *C.kgpu_nominated {
+	if len(s) == 0 {
+		return nil
+	}
+	return (*C.kgpu_nominated)(cmem(a, unsafe.Pointer(&s[0]), len(s), int(unsafe.Sizeof(s[0]))))
+}
+
+func cVictims(a *arena, s []C.kgpu_victim) *C.kgpu_victim {
+	if len(s) == 0 {
+		return nil
+	}
+	return (*C.kgpu_victim)(cmem(a, unsafe.Pointer(&s[0]), len(s), int(unsafe.Sizeof(s[0]))))
+}
+
+func cDeltas(a *arena, s []C.kgpu_delta) *C.kgpu_delta {
+	if len(s) == 0 {
+		return nil
+	}
+	return (*C.kgpu_delta)(cmem(a, unsafe.Pointer(&s[0]), len(s), int(unsafe.Sizeof(s[0]))))
+}
+
+func cNodeRows(a *arena, s []C.kgpu_node_row) *C.kgpu_node_row {
+	if len(s) == 0 {
+		return nil
+	}
+	return (*C.kgpu_node_row)(cmem(a, unsafe.Pointer(&s[0]), len(s), int(unsafe.Sizeof(s[0]))))
 }
 
 type engine struct{ ctx *C.kgpu_ctx }
@@ -114,7 +237,7 @@ func (e *engine) scheduleBatch(qs []C.kgpu_pod_query, pools *C.kgpu_pools, first
 	}
 	var a arena
 	defer a.free()
-	cq := cslice(&a, qs)
+	cq := cQueries(&a, qs)
 	res := make([]C.kgpu_result, len(qs))
 	var st C.kgpu_stats
 	rc := C.kgpu_schedule_batch(e.ctx, cq, C.int32_t(len(qs)), pools, C.int64_t(firstSeq),
@@ -164,7 +287,7 @@ func (e *engine) setNominated(noms []C.kgpu_nominated, recs []C.kgpu_pod_query, 
 	var cn *C.kgpu_nominated
 	var cr *C.kgpu_pod_query
 	if len(noms) > 0 {
-		cn, cr = cslice(&a, noms), cslice(&a, recs)
+		cn, cr = cNominated(&a, noms), cQueries(&a, recs)
 	}
 	return kerr(e.ctx, C.kgpu_set_nominated(e.ctx, cn, C.int32_t(len(noms)), cr, pools))
 }
@@ -177,10 +300,10 @@ func (e *engine) selectVictims(q *C.kgpu_pod_query, pools *C.kgpu_pools, victims
 	defer a.free()
 	args := C.kgpu_preempt_args{n_victims: C.int32_t(len(victims)), n_pdbs: C.int32_t(len(pdbAllowed))}
 	if len(victims) > 0 {
-		args.victims, args.pods = cslice(&a, victims), cslice(&a, recs)
+		args.victims, args.pods = cVictims(&a, victims), cQueries(&a, recs)
 	}
 	if len(pdbAllowed) > 0 {
-		args.pdb_allowed = (*C.int32_t)(cslice(&a, pdbAllowed))
+		args.pdb_allowed = ci32(&a, pdbAllowed)
 	}
 	out := make([]C.kgpu_node_victims, n+1)
 	vout := make([]int32, len(victims)+1)

@@ -376,23 +376,23 @@ func (g *GpuEval) snapshotSoA(list []*framework.NodeInfo, m *mirror, a *arena) (
 	s.nz_cpu, s.nz_mem = ci64(a, nzCPU), ci64(a, nzMem)
 	s.num_pods = ci32(a, numPods)
 	s.n_scalar, s.alloc_scalar, s.req_scalar = C.int32_t(S), ci64(a, allocSc), ci64(a, reqSc)
-	s.unschedulable = (*C.uint8_t)(cslice(a, unsched))
+	s.unschedulable = cu8(a, unsched)
 	s.n_label_keys, s.label_val = C.int32_t(K), ci32(a, labelVal)
 	var b C.kgpu_delta_batch
 	g.keyMeta(&b, a)
 	s.key_n_values, s.value_off, s.value_int, s.value_int_ok, s.key_empty_value =
 		b.key_n_values, b.value_off, b.value_int, b.value_int_ok, b.key_empty_value
-	s.taint_words, s.taint_nosched, s.taint_prefer = C.int32_t(TW), (*C.uint64_t)(cslice(a, taintNo)), (*C.uint64_t)(cslice(a, taintPref))
-	s.port_slots, s.port_count, s.ports = C.int32_t(PS), ci32(a, portCount), cslice(a, portTab)
+	s.taint_words, s.taint_nosched, s.taint_prefer = C.int32_t(TW), cu64(a, taintNo), cu64(a, taintPref)
+	s.port_slots, s.port_count, s.ports = C.int32_t(PS), ci32(a, portCount), cPorts(a, portTab)
 	g.nodeLists(uniq, &b, a)
 	s.image_off, s.image_id, s.image_score, s.avoid_off, s.avoid_id = b.image_off, b.image_id, b.image_score, b.avoid_off, b.avoid_id
 	s.zone_id, s.n_zones = ci32(a, zone), C.int32_t(len(c.zones.items))
 	s.n_pods, s.pod_node, s.pod_ns = C.int32_t(P), ci32(a, podNode), ci32(a, podNs)
-	s.pod_flags = (*C.uint32_t)(cslice(a, podFlags))
+	s.pod_flags = cu32(a, podFlags)
 	s.n_pod_label_keys, s.pod_label_val = C.int32_t(PK), ci32(a, podLab)
-	s.n_terms, s.terms = C.int32_t(len(terms)), cslice(a, terms)
+	s.n_terms, s.terms = C.int32_t(len(terms)), cTerms(a, terms)
 	s.pools = *p.toC(a)
-	s.pod_uid = (*C.int64_t)(cslice(a, podUID))
+	s.pod_uid = ci64(a, podUID)
 	return s, nil
 }
 
@@ -416,7 +416,7 @@ func (g *GpuEval) PreFilter(ctx context.Context, cs *framework.CycleState, pod *
 			return framework.NewStatus(framework.Error, err.Error())
 		}
 	}
-	cq := cslice(&a, []C.kgpu_pod_query{q})
+	cq := cQueries(&a, []C.kgpu_pod_query{q})
 	res, _, err := g.eng.scheduleOne(cq, p.toC(&a), atomic.AddInt64(&g.seq, 1)-1, false)
 	if err != nil {
 		return framework.NewStatus(framework.Error, err.Error())

@@ -18,6 +18,7 @@ import "C"
 
 import (
 	"context"
+	"fmt"
 
 	v1 "k8s.io/api/core/v1"
 	policy "k8s.io/api/policy/v1beta1"
@@ -54,24 +55,25 @@ func (g *GpuEval) syncNominated(a *arena) error {
 	return g.eng.setNominated(noms, recs, p.toC(a))
 }
 
-// pdbMask: the PodDisruptionBudgets selecting the pod (filterPodsWithPDBViolation,
-// generic_scheduler.go:886-905).
-func pdbMask(pod *v1.Pod, pdbs []*policy.PodDisruptionBudget) uint64 {
-	var m uint64
+// pdbsOf: indices of the PodDisruptionBudgets selecting the pod, in the caller's order
+// (filterPodsWithPDBViolation, generic_scheduler.go:886-905: same namespace, a non-empty selector
+// matching the pod's labels; a label-less pod matches none).
+func pdbsOf(pod *v1.Pod, pdbs []*policy.PodDisruptionBudget) []int {
+	var out []int
 	if len(pod.Labels) == 0 {
-		return 0
+		return nil
 	}
 	for j, pdb := range pdbs {
-		if j >= 64 || pdb.Namespace != pod.Namespace {
+		if pdb.Namespace != pod.Namespace {
 			continue
 		}
 		sel, err := metav1.LabelSelectorAsSelector(pdb.Spec.Selector)
 		if err != nil || sel.Empty() || !sel.Matches(labels.Set(pod.Labels)) {
 			continue
 		}
-		m |= 1 << uint(j)
+		out = append(out, j)
 	}
-	return m
+	return out
 }
 
 // SelectVictims runs selectNodesForPreemption + pickOneNodeForPreemption for a pod whose cycle
@@ -98,6 +100,12 @@ func (g *GpuEval) SelectVictims(ctx context.Context, pod *v1.Pod, pdbs []*policy
 	var victims []C.kgpu_victim
 	var recs []C.kgpu_pod_query
 	var pods []*v1.Pod
+	var victimPDBs [][]int
+	// Preempt lists every PDB of the cluster (labels.Everything()), but filterPodsWithPDBViolation
+	// only touches the ones that select a potential victim, walking them in order: the engine gets
+	// that subset, renumbered in the same order, so its 64-bit masks cover any cluster.
+	used := map[int]int{}
+	var usedOrder []int
 	for _, ni := range list {
 		idx, ok := g.mir.index[ni.Node().Name]
 		if !ok {
@@ -107,22 +115,49 @@ func (g *GpuEval) SelectVictims(ctx context.Context, pod *v1.Pod, pdbs []*policy
 			if podutil.GetPodPriority(pi.Pod) >= prio {
 				continue
 			}
+			slot, ok := g.mir.slots[pi.Pod.UID]
+			if !ok {
+				// a pod the device mirror does not hold: its effects would be read from another
+				// pod's slot; resync before preempting
+				g.mir = nil
+				return "", nil, fmt.Errorf("gpueval: pod %s/%s is not in the device mirror (resynced; retry)",
+					pi.Pod.Namespace, pi.Pod.Name)
+			}
 			r, err := g.comp.compilePod(pi.Pod, p)
 			if err != nil {
 				return "", nil, err
 			}
-			victims = append(victims, C.kgpu_victim{node: C.int32_t(idx), slot: C.int32_t(g.mir.slots[pi.Pod.UID]),
-				item: C.int32_t(len(recs)), start_time: C.int64_t(util.GetPodStartTime(pi.Pod).UnixNano()),
-				pdb_mask: C.uint64_t(pdbMask(pi.Pod, pdbs))})
+			js := pdbsOf(pi.Pod, pdbs)
+			for _, j := range js {
+				if _, seen := used[j]; !seen {
+					used[j] = -1
+					usedOrder = append(usedOrder, j)
+				}
+			}
+			victims = append(victims, C.kgpu_victim{node: C.int32_t(idx), slot: C.int32_t(slot),
+				item: C.int32_t(len(recs)), start_time: C.int64_t(util.GetPodStartTime(pi.Pod).UnixNano())})
+			victimPDBs = append(victimPDBs, js)
 			recs = append(recs, r)
 			pods = append(pods, pi.Pod)
 		}
 	}
-	allowed := make([]int32, 0, len(pdbs))
-	for _, pdb := range pdbs {
-		allowed = append(allowed, pdb.Status.DisruptionsAllowed)
+	sortInts(usedOrder)
+	if len(usedOrder) > 64 {
+		return "", nil, fmt.Errorf("gpueval: %d PodDisruptionBudgets select potential victims (the engine takes 64)", len(usedOrder))
 	}
-	cq := cslice(&a, []C.kgpu_pod_query{q})
+	allowed := make([]int32, 0, len(usedOrder))
+	for k, j := range usedOrder {
+		used[j] = k
+		allowed = append(allowed, pdbs[j].Status.DisruptionsAllowed)
+	}
+	for i, js := range victimPDBs {
+		var m uint64
+		for _, j := range js {
+			m |= 1 << uint(used[j])
+		}
+		victims[i].pdb_mask = C.uint64_t(m)
+	}
+	cq := cQueries(&a, []C.kgpu_pod_query{q})
 	out, vout, chosen, err := g.eng.selectVictims(cq, p.toC(&a), victims, recs, allowed, len(g.mir.names))
 	if err != nil || chosen < 0 {
 		return "", nil, err
@@ -133,6 +168,14 @@ func (g *GpuEval) SelectVictims(ctx context.Context, pod *v1.Pod, pdbs []*policy
 		res = append(res, pods[vout[int(o.first)+k]])
 	}
 	return g.mir.names[chosen], res, nil
+}
+
+func sortInts(x []int) {
+	for i := 1; i < len(x); i++ {
+		for k := i; k > 0 && x[k] < x[k-1]; k-- {
+			x[k], x[k-1] = x[k-1], x[k]
+		}
+	}
 }
 
 // PostFilter (interface.go:276-290): the device's preemption choice as the nominated node.  In

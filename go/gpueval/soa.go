@@ -225,11 +225,11 @@ func (g *GpuEval) deltaFromSnapshot(list []*framework.NodeInfo, a *arena) (*C.kg
 		m.nodes[nm] = ni.Node()
 	}
 	b := (*C.kgpu_delta_batch)(a.alloc(int(unsafe.Sizeof(C.kgpu_delta_batch{}))))
-	b.n_deltas, b.deltas = C.int32_t(len(deltas)), cslice(a, deltas)
-	b.n_pods, b.pods = C.int32_t(len(podsQ)), cslice(a, podsQ)
-	b.n_rows, b.rows = C.int32_t(len(rows)), cslice(a, rows)
+	b.n_deltas, b.deltas = C.int32_t(len(deltas)), cDeltas(a, deltas)
+	b.n_pods, b.pods = C.int32_t(len(podsQ)), cQueries(a, podsQ)
+	b.n_rows, b.rows = C.int32_t(len(rows)), cNodeRows(a, rows)
 	if reorder {
-		b.n_order, b.order = C.int32_t(len(order)), (*C.int32_t)(unsafe.Pointer(cslice(a, order)))
+		b.n_order, b.order = C.int32_t(len(order)), ci32(a, order)
 	}
 	if reorder || len(rows) > 0 {
 		g.nodeLists(list, b, a) // ImageLocality / NodePreferAvoidPods CSR over the new list
@@ -264,11 +264,11 @@ func (g *GpuEval) nodeLists(list []*framework.NodeInfo, b *C.kgpu_delta_batch, a
 		}
 		aoff = append(aoff, int32(len(aids)))
 	}
-	b.image_off = (*C.int32_t)(unsafe.Pointer(cslice(a, off)))
-	b.image_id = (*C.int32_t)(unsafe.Pointer(cslice(a, append(ids, 0))))
-	b.image_score = (*C.int64_t)(unsafe.Pointer(cslice(a, append(scores, 0))))
-	b.avoid_off = (*C.int32_t)(unsafe.Pointer(cslice(a, aoff)))
-	b.avoid_id = (*C.int32_t)(unsafe.Pointer(cslice(a, append(aids, 0))))
+	b.image_off = ci32(a, off)
+	b.image_id = ci32(a, append(ids, 0))
+	b.image_score = ci64(a, append(scores, 0))
+	b.avoid_off = ci32(a, aoff)
+	b.avoid_id = ci32(a, append(aids, 0))
 }
 
 // keyMeta sends the node label dictionaries (key_n_values / value_off / value_int ...).
@@ -288,9 +288,9 @@ func (g *GpuEval) keyMeta(b *C.kgpu_delta_batch, a *arena) {
 		off = append(off, int32(len(ints)))
 		empty[k] = d.get("")
 	}
-	b.key_n_values = (*C.int32_t)(unsafe.Pointer(cslice(a, append(nv, 0))))
-	b.value_off = (*C.int32_t)(unsafe.Pointer(cslice(a, off)))
-	b.value_int = (*C.int64_t)(unsafe.Pointer(cslice(a, append(ints, 0))))
-	b.value_int_ok = (*C.uint8_t)(unsafe.Pointer(cslice(a, append(oks, 0))))
-	b.key_empty_value = (*C.int32_t)(unsafe.Pointer(cslice(a, append(empty, 0))))
+	b.key_n_values = ci32(a, append(nv, 0))
+	b.value_off = ci32(a, off)
+	b.value_int = ci64(a, append(ints, 0))
+	b.value_int_ok = cu8(a, append(oks, 0))
+	b.key_empty_value = ci32(a, append(empty, 0))
 }

@@ -1,0 +1,132 @@
+package gpueval
+
+// Change tracking for the device mirror: which NodeInfos of the Snapshot may have moved since the
+// last sync, so that PreFilter's sync is O(changed) instead of a walk of Snapshot.List().
+//
+// The reference's UpdateSnapshot (internal/cache/cache.go:218-247) walks the cache's
+// generation-ordered node list from its head and stops at the first NodeInfo not newer than the
+// snapshot.  A plugin sees only the Snapshot (FrameworkHandle.SnapshotSharedLister), not that list, so
+// it learns of changes from the same sources the cache does:
+//
+//   * Reserve / Unreserve (interface.go:332-368): the node of every assume / forget the scheduler
+//     makes (scheduler.go:586-593 assume, the binding cycle's ForgetPod);
+//   * the shared informers' pod and node events (eventhandlers.go:93-295 feed the cache from the same
+//     informers): a pod's old and new nodeName, a node's name.
+//
+// A marked node is re-checked at every sync until its NodeInfo.Generation moves (an event can reach
+// this handler before the cache applied it) or markTTL syncs passed.  Nothing can reach the cache
+// without passing through one of these sources except an assumed pod's expiry
+// (cache.cleanupAssumedPods, cache.go:704-737) and an event whose handler ran late, so every
+// fullEvery syncs the whole list's generations are compared as well (a tight loop over positions:
+// no map operations).  ExactSync in the plugin args compares every generation at every sync.
+
+import (
+	"sync"
+
+	v1 "k8s.io/api/core/v1"
+	"k8s.io/client-go/tools/cache"
+)
+
+const (
+	markTTL   = 32   // syncs a mark stays without its NodeInfo's generation moving
+	fullEvery = 1024 // syncs between full generation scans
+)
+
+type tracker struct {
+	mu    sync.Mutex
+	marks map[string]int // node name -> syncs left
+}
+
+func newTracker() *tracker { return &tracker{marks: map[string]int{}} }
+
+func (t *tracker) mark(node string) {
+	if node == "" {
+		return
+	}
+	t.mu.Lock()
+	t.marks[node] = markTTL
+	t.mu.Unlock()
+}
+
+// take returns the marked nodes and ages the marks; keep(name) re-arms a mark whose NodeInfo has not
+// moved yet (its event may not have reached the cache).
+func (t *tracker) take() []string {
+	t.mu.Lock()
+	defer t.mu.Unlock()
+	out := make([]string, 0, len(t.marks))
+	for n, left := range t.marks {
+		out = append(out, n)
+		if left <= 1 {
+			delete(t.marks, n)
+		} else {
+			t.marks[n] = left - 1
+		}
+	}
+	return out
+}
+
+// settle drops the mark of a node whose change was applied.
+func (t *tracker) settle(node string) {
+	t.mu.Lock()
+	delete(t.marks, node)
+	t.mu.Unlock()
+}
+
+func podOf(obj interface{}) *v1.Pod {
+	switch o := obj.(type) {
+	case *v1.Pod:
+		return o
+	case cache.DeletedFinalStateUnknown:
+		if p, ok := o.Obj.(*v1.Pod); ok {
+			return p
+		}
+	}
+	return nil
+}
+
+func nodeOf(obj interface{}) *v1.Node {
+	switch o := obj.(type) {
+	case *v1.Node:
+		return o
+	case cache.DeletedFinalStateUnknown:
+		if n, ok := o.Obj.(*v1.Node); ok {
+			return n
+		}
+	}
+	return nil
+}
+
+// watch registers the informer handlers (FrameworkHandle.SharedInformerFactory, interface.go:515).
+// Without informers every sync compares every generation.
+func (g *GpuEval) watch() {
+	f := g.h.SharedInformerFactory()
+	if f == nil {
+		g.exact = true
+		return
+	}
+	t := g.track
+	onPod := func(objs ...interface{}) {
+		for _, o := range objs {
+			if p := podOf(o); p != nil {
+				t.mark(p.Spec.NodeName)
+			}
+		}
+	}
+	f.Core().V1().Pods().Informer().AddEventHandler(cache.ResourceEventHandlerFuncs{
+		AddFunc:    func(o interface{}) { onPod(o) },
+		UpdateFunc: func(o, n interface{}) { onPod(o, n) },
+		DeleteFunc: func(o interface{}) { onPod(o) },
+	})
+	onNode := func(objs ...interface{}) {
+		for _, o := range objs {
+			if n := nodeOf(o); n != nil {
+				t.mark(n.Name)
+			}
+		}
+	}
+	f.Core().V1().Nodes().Informer().AddEventHandler(cache.ResourceEventHandlerFuncs{
+		AddFunc:    func(o interface{}) { onNode(o) },
+		UpdateFunc: func(o, n interface{}) { onNode(o, n) },
+		DeleteFunc: func(o interface{}) { onNode(o) },
+	})
+}

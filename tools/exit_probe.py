@@ -5,7 +5,9 @@ addresses of a crash report from the same process can be resolved to libraries:
   torch   -- torch only: one device tensor and a synchronize
   kgpu    -- libkgpu.so only (no torch import): create a context, upload 64 nodes, one batch, destroy
   both    -- torch first, then the kgpu variant
-Usage: python3 tools/exit_probe.py <variant> <maps-out>"""
+Usage: python3 tools/exit_probe.py <variant> <maps-out> [--os-exit]
+  --os-exit: leave through os._exit(0) after the work (no exit handlers run: does rocprofv3 still write
+             its files?)"""
 import os
 import sys
 
@@ -41,6 +43,10 @@ def main():
     with open("/proc/self/maps") as src, open(out, "w") as dst:
         dst.write(src.read())
     print("exit_probe %s: done, maps in %s" % (variant, out), flush=True)
+    if "--os-exit" in sys.argv:
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0)
 
 
 if __name__ == "__main__":
