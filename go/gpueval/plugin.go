@@ -8,13 +8,14 @@ package gpueval
 // Two score modes (profileArgs.Mode):
 //   select: one score plugin (weight 1) returns 100 for the device-chosen node and 0 otherwise,
 //           so the reference selectHost (generic_scheduler.go:217-238) picks the device's node;
-//   shadow: the plugin returns the device's weighted total per node (DefaultNormalizeScore and
-//           the replaced plugins' weights applied on the device), clipped into [0, 100] only for
-//           the framework's range check -- per-plugin raw / normalized values stay available
-//           through kgpu_get_scores for parity checks.
+//   shadow: one GPU score plugin per replaced score plugin (ShadowPlugins, shadow.go), each returning
+//           that plugin's device-normalized 0-100 value; the profile gives them the reference weights,
+//           so the framework's range check, weighting and sum (framework.go:632-648) and the reference
+//           selectHost run unchanged on the device's per-plugin scores.
 //
 // Reserve / Unreserve need no device call: cache.AssumePod / ForgetPod update the NodeInfo, and the
-// next PreFilter's generation diff (soa.go) sends NodeInfo.AddPod / RemovePod by UID.
+// next PreFilter's generation diff (soa.go) sends NodeInfo.AddPod / RemovePod by UID; they mark the
+// node for that diff (track.go).
 
 /*
 #include "kgpu.h"
@@ -27,6 +28,7 @@ import (
 	"sort"
 	"strconv"
 	"sync/atomic"
+	"unsafe"
 
 	v1 "k8s.io/api/core/v1"
 	"k8s.io/apimachinery/pkg/labels"
@@ -53,6 +55,7 @@ type profileArgs struct {
 	PercentageOfNodesToScore int32
 	TieBreakSeed           uint64
 	Mode                   string // "select" or "shadow"
+	ExactSync              bool   // compare every NodeInfo generation at every sync (track.go)
 	ignoredResources       map[string]struct{}
 }
 
@@ -137,11 +140,12 @@ func (c *compiler) config() *C.kgpu_config {
 	return &cfg
 }
 
-// cycle is the per-pod state read by Filter and Score.
+// cycle is the per-pod state read by Filter and Score (and by the shadow score plugins).
 type cycle struct {
-	words  []uint32 // per-node filter status words (node index order)
-	total  []int64  // shadow mode: weighted total per node
-	chosen int32    // device-selected node index, -1 = FitError
+	words  []uint32           // per-node filter status words (node index order)
+	norm   map[int32][]int64  // shadow mode: per score plugin id, the device-normalized 0-100 value per node
+	index  map[string]int32   // node name -> node index of this cycle's mirror
+	chosen int32              // device-selected node index, -1 = FitError
 }
 
 func (c *cycle) Clone() framework.StateData { return c }
@@ -153,7 +157,10 @@ type GpuEval struct {
 	comp      *compiler
 	mir       *mirror
 	seq       int64
-	nominated bool // the engine holds a non-empty nominator
+	nominated bool     // the engine holds a non-empty nominator
+	track     *tracker // nodes whose NodeInfo may have moved since the last sync (track.go)
+	exact     bool     // compare every generation at every sync
+	syncs     int
 }
 
 func (g *GpuEval) Name() string { return Name }
@@ -212,6 +219,7 @@ func (g *GpuEval) upload(list []*framework.NodeInfo, a *arena) error {
 			c.nodeIndex[ni.Node().Name] = int32(i)
 		}
 	}
+	g.track.take() // a full upload covers every mark
 	c.dims.K = len(c.nkeys.keys.items)
 	c.dims.S = len(c.scalars.items)
 	c.dims.TW = (len(c.taintList) + 63) / 64
@@ -228,6 +236,13 @@ func (g *GpuEval) upload(list []*framework.NodeInfo, a *arena) error {
 	g.comp = c
 	m := &mirror{index: map[string]int32{}, gens: map[string]int64{}, nodes: map[string]*v1.Node{},
 		pods: map[string]map[types.UID]*v1.Pod{}, uids: map[types.UID]int64{}, slots: map[types.UID]int32{}}
+	m.genAt = make([]int64, len(list))
+	for i, ni := range list {
+		m.genAt[i] = ni.Generation
+	}
+	if len(list) > 0 {
+		m.listData = unsafe.Pointer(&list[0])
+	}
 	if g.mir != nil {
 		m.uids, m.nextUID, m.gen = g.mir.uids, g.mir.nextUID, g.mir.gen
 	}
@@ -283,7 +298,9 @@ func (g *GpuEval) snapshotSoA(list []*framework.NodeInfo, m *mirror, a *arena) (
 		allocCPU[i], allocMem[i], allocEph[i], allocPods[i] = int64(r.alloc_cpu), int64(r.alloc_mem), int64(r.alloc_eph), int32(r.alloc_pods)
 		unsched[i], zone[i] = uint8(r.unschedulable), int32(r.zone_id)
 		for j := 0; j+1 < int(r.labels.count); j += 2 {
-			labelVal[int(p.ints[int(r.labels.begin)+j])*N+i] = p.ints[int(r.labels.begin)+j+1]
+			k, v := p.ints[int(r.labels.begin)+j], p.ints[int(r.labels.begin)+j+1]
+			labelVal[int(k)*N+i] = v
+			m.labels.add(k, v, 1)
 		}
 		if r.taints.count > 0 {
 			for w := 0; w < TW; w++ {
@@ -393,6 +410,7 @@ func (g *GpuEval) snapshotSoA(list []*framework.NodeInfo, m *mirror, a *arena) (
 	s.n_terms, s.terms = C.int32_t(len(terms)), cTerms(a, terms)
 	s.pools = *p.toC(a)
 	s.pod_uid = ci64(a, podUID)
+	s.key_unique = cu8(a, m.labels.unique(K)) // the whole Snapshot.List(): the cluster-wide view
 	return s, nil
 }
 
@@ -426,21 +444,18 @@ func (g *GpuEval) PreFilter(ctx context.Context, cs *framework.CycleState, pod *
 	if err != nil {
 		return framework.NewStatus(framework.Error, err.Error())
 	}
-	c := &cycle{words: words, chosen: int32(res.node)}
+	c := &cycle{words: words, chosen: int32(res.node), index: g.mir.index}
 	if g.prof.Mode == "shadow" {
-		c.total = make([]int64, n)
+		// every replaced score plugin's normalized (unweighted) value per node: the shadow plugins
+		// return them, the framework weights and sums them (framework.go:632-648)
+		c.norm = make(map[int32][]int64, len(g.prof.Scores))
 		for _, s := range g.prof.Scores {
-			_, norm, err := g.eng.scores(int(scoreIDs[s.Name]), n)
+			id := scoreIDs[s.Name]
+			_, norm, err := g.eng.scores(int(id), n)
 			if err != nil {
 				return framework.NewStatus(framework.Error, err.Error())
 			}
-			w := s.Weight
-			if w == 0 {
-				w = 1
-			}
-			for i := range norm {
-				c.total[i] += w * norm[i]
-			}
+			c.norm[id] = norm
 		}
 	}
 	cs.Write(stateKey, c)
@@ -469,13 +484,9 @@ func (g *GpuEval) Score(ctx context.Context, cs *framework.CycleState, pod *v1.P
 	if err != nil {
 		return 0, framework.NewStatus(framework.Error, err.Error())
 	}
-	i := g.mir.index[node]
-	if c.total != nil {
-		t := c.total[i]
-		if t > framework.MaxNodeScore {
-			t = framework.MaxNodeScore // the framework's range check; selectHost order kept by select mode
-		}
-		return t, nil
+	i, ok := c.index[node]
+	if !ok {
+		return 0, framework.NewStatus(framework.Error, fmt.Sprintf("node %q is not in the device mirror", node))
 	}
 	if i == c.chosen {
 		return framework.MaxNodeScore, nil
@@ -485,12 +496,16 @@ func (g *GpuEval) Score(ctx context.Context, cs *framework.CycleState, pod *v1.P
 
 func (g *GpuEval) ScoreExtensions() framework.ScoreExtensions { return nil }
 
-// Reserve / Unreserve: cache.AssumePod / ForgetPod already changed the NodeInfo; the next
-// PreFilter's generation diff carries it to the device.
+// Reserve / Unreserve: cache.AssumePod (scheduler.go:586-593, right after Reserve) / ForgetPod change
+// the NodeInfo; the next PreFilter's generation diff carries it to the device.  The node is marked so
+// that diff looks at it (track.go).
 func (g *GpuEval) Reserve(ctx context.Context, cs *framework.CycleState, pod *v1.Pod, node string) *framework.Status {
+	g.track.mark(node)
 	return nil
 }
-func (g *GpuEval) Unreserve(ctx context.Context, cs *framework.CycleState, pod *v1.Pod, node string) {}
+func (g *GpuEval) Unreserve(ctx context.Context, cs *framework.CycleState, pod *v1.Pod, node string) {
+	g.track.mark(node)
+}
 
 // New is the framework.PluginFactory (registry.go:28).
 func New(obj runtime.Object, h framework.FrameworkHandle) (framework.Plugin, error) {
@@ -498,7 +513,9 @@ func New(obj runtime.Object, h framework.FrameworkHandle) (framework.Plugin, err
 	if err != nil {
 		return nil, err
 	}
-	return &GpuEval{h: h, prof: prof}, nil
+	g := &GpuEval{h: h, prof: prof, track: newTracker(), exact: prof.ExactSync}
+	g.watch()
+	return g, nil
 }
 
 // defaultSelector: helper.DefaultSelector (helper/spread.go:29-72) from the handle's listers.

@@ -41,6 +41,9 @@ type mirror struct {
 	gen      int64
 	slots    map[types.UID]int32         // pod UID -> pod-table slot (kgpu_victim.slot)
 	added    map[int]types.UID           // delta index -> UID of an ADD_POD in the pending batch
+	genAt    []int64                     // NodeInfo.Generation last sent, by list position
+	listData unsafe.Pointer              // backing array of the Snapshot.List() last synced
+	labels   labelCounts                 // per key, nodes carrying each value (key_unique)
 }
 
 // recordSlots keeps the pod-table slot of every pod the last delta batch added.
@@ -126,119 +129,251 @@ func (c *compiler) nodeRow(n *v1.Node, p *pools) (C.kgpu_node_row, error) {
 	return r, nil
 }
 
-// deltaFromSnapshot diffs the refreshed Snapshot against the mirror.  Returns the C batch (in the
-// arena) or errNeedsUpload.
-func (g *GpuEval) deltaFromSnapshot(list []*framework.NodeInfo, a *arena) (*C.kgpu_delta_batch, error) {
-	m, c := g.mir, g.comp
-	p := &pools{}
-	var deltas []C.kgpu_delta
-	var podsQ []C.kgpu_pod_query
-	var rows []C.kgpu_node_row
-	names := make([]string, len(list))
-	for i, ni := range list {
-		names[i] = ni.Node().Name
+// labelCounts: per node label key, how many listed nodes carry each value id; multi[k] counts the
+// values carried by two or more nodes.  A key with multi 0 is hostname-like (kgpu_snapshot.key_unique,
+// cluster-wide because this mirror sees the whole Snapshot).
+type labelCounts struct {
+	cnt   [][]int32
+	multi []int32
+}
+
+func (lc *labelCounts) add(k, v int32, d int32) {
+	for int(k) >= len(lc.cnt) {
+		lc.cnt = append(lc.cnt, nil)
+		lc.multi = append(lc.multi, 0)
 	}
-	reorder := len(names) != len(m.names)
-	for i := 0; !reorder && i < len(names); i++ {
-		reorder = names[i] != m.names[i]
+	for int(v) >= len(lc.cnt[k]) {
+		lc.cnt[k] = append(lc.cnt[k], 0)
 	}
-	newIndex := map[string]int32{}
-	for i, nm := range names {
-		if _, ok := newIndex[nm]; !ok {
-			newIndex[nm] = int32(i)
+	before := lc.cnt[k][v]
+	lc.cnt[k][v] += d
+	if before < 2 && lc.cnt[k][v] >= 2 {
+		lc.multi[k]++
+	} else if before >= 2 && lc.cnt[k][v] < 2 {
+		lc.multi[k]--
+	}
+}
+
+func (lc *labelCounts) unique(K int) []uint8 {
+	out := make([]uint8, K)
+	for k := 0; k < K; k++ {
+		if k >= len(lc.multi) || lc.multi[k] == 0 {
+			out[k] = 1
 		}
 	}
-	var order []int32
-	rowOf := map[string]int{}
-	for _, ni := range list {
-		nm := ni.Node().Name
-		if _, seen := rowOf[nm]; seen {
+	return out
+}
+
+// nodeLabels: (key id, value id) pairs of a node against the compiler's dictionaries.
+func (c *compiler) nodeLabels(n *v1.Node) [][2]int32 {
+	var out [][2]int32
+	for k, v := range n.Labels {
+		ki := c.nkeys.key(k)
+		if ki < 0 {
 			continue
 		}
-		_, known := m.index[nm]
-		if !known || m.nodes[nm] != ni.Node() {
-			r, err := c.nodeRow(ni.Node(), p)
+		out = append(out, [2]int32{ki, c.nkeys.val(ki, v)})
+	}
+	return out
+}
+
+// deltaBuild accumulates one kgpu_delta_batch.
+type deltaBuild struct {
+	p          *pools
+	deltas     []C.kgpu_delta
+	podsQ      []C.kgpu_pod_query
+	rows       []C.kgpu_node_row
+	rowOf      map[string]int
+	labelMoved bool
+}
+
+// diffNode sends one NodeInfo's changes: SET_NODE when its Node object changed, then
+// NodeInfo.RemovePod / AddPod (types.go:456-533) by UID for the pods gone, new or replaced.
+func (g *GpuEval) diffNode(b *deltaBuild, ni *framework.NodeInfo, pos int32, wasListed bool) error {
+	m, c := g.mir, g.comp
+	nm := ni.Node().Name
+	if !wasListed || m.nodes[nm] != ni.Node() {
+		if _, done := b.rowOf[nm]; !done {
+			r, err := c.nodeRow(ni.Node(), b.p)
 			if err != nil {
-				return nil, err
+				return err
 			}
-			rows = append(rows, r)
-			rowOf[nm] = len(rows) - 1
-			deltas = append(deltas, C.kgpu_delta{op: C.KGPU_D_SET_NODE, node: C.int32_t(newIndex[nm]), item: C.int32_t(len(rows) - 1)})
+			b.rows = append(b.rows, r)
+			b.rowOf[nm] = len(b.rows) - 1
+			b.deltas = append(b.deltas, C.kgpu_delta{op: C.KGPU_D_SET_NODE, node: C.int32_t(pos), item: C.int32_t(len(b.rows) - 1)})
+			if old := m.nodes[nm]; old != nil {
+				for _, kv := range c.nodeLabels(old) {
+					m.labels.add(kv[0], kv[1], -1)
+				}
+			}
+			for _, kv := range c.nodeLabels(ni.Node()) {
+				m.labels.add(kv[0], kv[1], 1)
+			}
+			b.labelMoved = true
 		}
 	}
-	if reorder {
-		order = make([]int32, len(names))
-		for i, nm := range names {
-			if j, ok := m.index[nm]; ok {
-				order[i] = j
-			} else {
-				order[i] = int32(-1 - rowOf[nm])
-			}
-		}
-	}
-	addPod := func(nm string, pod *v1.Pod, op C.int32_t) error {
-		q, err := c.compilePod(pod, p)
+	podDelta := func(pod *v1.Pod, op C.int32_t) error {
+		q, err := c.compilePod(pod, b.p)
 		if err != nil {
 			return err
 		}
-		podsQ = append(podsQ, q)
+		b.podsQ = append(b.podsQ, q)
 		if op == C.KGPU_D_ADD_POD {
 			if m.added == nil {
 				m.added = map[int]types.UID{}
 			}
-			m.added[len(deltas)] = pod.UID
+			m.added[len(b.deltas)] = pod.UID
 		}
-		deltas = append(deltas, C.kgpu_delta{op: op, node: C.int32_t(newIndex[nm]), uid: C.int64_t(m.uid(pod.UID)),
-			item: C.int32_t(len(podsQ) - 1)})
+		b.deltas = append(b.deltas, C.kgpu_delta{op: op, node: C.int32_t(pos), uid: C.int64_t(m.uid(pod.UID)),
+			item: C.int32_t(len(b.podsQ) - 1)})
 		return nil
 	}
-	for _, ni := range list {
-		nm := ni.Node().Name
-		if g0, ok := m.gens[nm]; ok && g0 == ni.Generation && !reorder {
-			continue
-		}
-		old := m.pods[nm]
-		_, wasListed := m.index[nm]
-		cur := map[types.UID]*v1.Pod{}
-		for _, pi := range ni.Pods {
-			cur[pi.Pod.UID] = pi.Pod
-		}
-		if wasListed {
-			for u, pod := range old { // NodeInfo.RemovePod of pods gone or changed
-				if np, ok := cur[u]; !ok || np != pod {
-					if err := addPod(nm, pod, C.KGPU_D_REMOVE_POD); err != nil {
-						return nil, err
-					}
+	old := m.pods[nm]
+	cur := make(map[types.UID]*v1.Pod, len(ni.Pods))
+	for _, pi := range ni.Pods {
+		cur[pi.Pod.UID] = pi.Pod
+	}
+	if wasListed {
+		for u, pod := range old { // NodeInfo.RemovePod of pods gone or changed
+			if np, ok := cur[u]; !ok || np != pod {
+				if err := podDelta(pod, C.KGPU_D_REMOVE_POD); err != nil {
+					return err
 				}
 			}
 		}
-		for u, pod := range cur { // NodeInfo.AddPod of new or changed pods
-			if op, ok := old[u]; wasListed && ok && op == pod {
-				continue
+	}
+	for u, pod := range cur { // NodeInfo.AddPod of new or changed pods
+		if op, ok := old[u]; wasListed && ok && op == pod {
+			continue
+		}
+		if err := podDelta(pod, C.KGPU_D_ADD_POD); err != nil {
+			return err
+		}
+	}
+	m.pods[nm] = cur
+	m.gens[nm] = ni.Generation
+	m.nodes[nm] = ni.Node()
+	return nil
+}
+
+// deltaFromSnapshot diffs the refreshed Snapshot against the mirror.  Returns the C batch (in the
+// arena) or errNeedsUpload.
+//
+// Cost.  UpdateSnapshot rebuilds Snapshot.List() only when a node was added or removed
+// (cache.go:258-301); otherwise the list is the same slice and its NodeInfos are updated in place
+// (cache.go:236-243: `*existing = *clone`).  So an unchanged list is recognized in O(1) (same backing
+// array, same length), and only the NodeInfos the tracker marked (track.go: Reserve / Unreserve and the
+// informers' pod and node events) are compared by generation: O(changed), as UpdateSnapshot's own walk
+// of the cache's generation-ordered list.  Every fullEvery syncs (and with ExactSync, every sync) all
+// positions' generations are compared as well, a tight loop over a slice.  A rebuilt list takes the
+// full walk (node adds / removes are rare).
+func (g *GpuEval) deltaFromSnapshot(list []*framework.NodeInfo, a *arena) (*C.kgpu_delta_batch, error) {
+	m, c := g.mir, g.comp
+	b := &deltaBuild{p: &pools{}, rowOf: map[string]int{}}
+	g.syncs++
+	same := len(list) == len(m.names) && (len(list) == 0 || unsafe.Pointer(&list[0]) == m.listData)
+	var order []int32
+	if same {
+		if g.exact || g.syncs%fullEvery == 0 {
+			for i, ni := range list {
+				if int32(i) != m.index[ni.Node().Name] || ni.Generation == m.genAt[i] {
+					continue // an alias position, or unchanged
+				}
+				if err := g.diffNode(b, ni, int32(i), true); err != nil {
+					return nil, err
+				}
+				m.genAt[i] = ni.Generation
+				g.track.settle(ni.Node().Name)
 			}
-			if err := addPod(nm, pod, C.KGPU_D_ADD_POD); err != nil {
-				return nil, err
+		} else {
+			for _, nm := range g.track.take() {
+				i, ok := m.index[nm]
+				if !ok {
+					continue // not listed: its add shows as a rebuilt list
+				}
+				ni := list[i]
+				if ni.Generation == m.genAt[i] {
+					continue // the event has not reached the cache yet: the mark stays (markTTL)
+				}
+				if err := g.diffNode(b, ni, i, true); err != nil {
+					return nil, err
+				}
+				m.genAt[i] = ni.Generation
+				g.track.settle(nm)
 			}
 		}
-		m.pods[nm] = cur
-		m.gens[nm] = ni.Generation
-		m.nodes[nm] = ni.Node()
+	} else {
+		// the list was rebuilt: new positions, every NodeInfo compared
+		names := make([]string, len(list))
+		newIndex := make(map[string]int32, len(list))
+		for i, ni := range list {
+			names[i] = ni.Node().Name
+			if _, ok := newIndex[names[i]]; !ok {
+				newIndex[names[i]] = int32(i)
+			}
+		}
+		order = make([]int32, len(names))
+		for _, ni := range list {
+			nm := ni.Node().Name
+			if _, known := m.index[nm]; !known {
+				if err := g.diffNode(b, ni, newIndex[nm], false); err != nil {
+					return nil, err
+				}
+			}
+		}
+		for i, nm := range names {
+			if j, ok := m.index[nm]; ok {
+				order[i] = j
+			} else {
+				order[i] = int32(-1 - b.rowOf[nm])
+			}
+		}
+		for _, ni := range list {
+			nm := ni.Node().Name
+			if _, known := m.index[nm]; known && (m.gens[nm] != ni.Generation || m.nodes[nm] != ni.Node()) {
+				if err := g.diffNode(b, ni, newIndex[nm], true); err != nil {
+					return nil, err
+				}
+			}
+		}
+		// labels of the nodes that left the list
+		for nm, n := range m.nodes {
+			if _, ok := newIndex[nm]; !ok {
+				for _, kv := range c.nodeLabels(n) {
+					m.labels.add(kv[0], kv[1], -1)
+				}
+				delete(m.nodes, nm)
+				delete(m.pods, nm)
+				delete(m.gens, nm)
+				b.labelMoved = true
+			}
+		}
+		m.names, m.index = names, newIndex
+		m.genAt = make([]int64, len(list))
+		for i, ni := range list {
+			m.genAt[i] = ni.Generation
+		}
+		if len(list) > 0 {
+			m.listData = unsafe.Pointer(&list[0])
+		}
 	}
-	b := (*C.kgpu_delta_batch)(a.alloc(int(unsafe.Sizeof(C.kgpu_delta_batch{}))))
-	b.n_deltas, b.deltas = C.int32_t(len(deltas)), cDeltas(a, deltas)
-	b.n_pods, b.pods = C.int32_t(len(podsQ)), cQueries(a, podsQ)
-	b.n_rows, b.rows = C.int32_t(len(rows)), cNodeRows(a, rows)
-	if reorder {
-		b.n_order, b.order = C.int32_t(len(order)), ci32(a, order)
+	bt := (*C.kgpu_delta_batch)(a.alloc(int(unsafe.Sizeof(C.kgpu_delta_batch{}))))
+	bt.n_deltas, bt.deltas = C.int32_t(len(b.deltas)), cDeltas(a, b.deltas)
+	bt.n_pods, bt.pods = C.int32_t(len(b.podsQ)), cQueries(a, b.podsQ)
+	bt.n_rows, bt.rows = C.int32_t(len(b.rows)), cNodeRows(a, b.rows)
+	if !same {
+		bt.n_order, bt.order = C.int32_t(len(order)), ci32(a, order)
 	}
-	if reorder || len(rows) > 0 {
-		g.nodeLists(list, b, a) // ImageLocality / NodePreferAvoidPods CSR over the new list
-		g.keyMeta(b, a)         // label dictionaries may have grown
+	if !same || len(b.rows) > 0 {
+		g.nodeLists(list, bt, a) // ImageLocality / NodePreferAvoidPods CSR over the new list
+		g.keyMeta(bt, a)         // label dictionaries may have grown
 	}
-	b.n_zones = C.int32_t(len(c.zones.items))
-	b.pools = *p.toC(a)
-	m.names, m.index = names, newIndex
-	return b, nil
+	if b.labelMoved {
+		bt.key_unique = cu8(a, m.labels.unique(c.dims.K))
+	}
+	bt.n_zones = C.int32_t(len(c.zones.items))
+	bt.pools = *b.p.toC(a)
+	return bt, nil
 }
 
 // nodeLists fills the ImageLocality scaledImageScore and NodePreferAvoidPods CSR

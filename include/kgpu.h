@@ -413,6 +413,19 @@ int kgpu_schedule_batch(kgpu_ctx* ctx, const kgpu_pod_query* qs, int32_t n, cons
  * normalized (unweighted) scores of one score plugin over the feasible nodes (others: 0). */
 int kgpu_get_filter(kgpu_ctx* ctx, uint32_t* status_words);
 int kgpu_get_scores(kgpu_ctx* ctx, int32_t plugin, int64_t* raw, int64_t* normalized);
+/* Diagnostics (parity against the reference's PodTopologySpread state tables,
+ * podtopologyspread/filtering_test.go:543 and scoring_test.go:38): the state the device builds for one
+ * pod, for its constraint `constraint` (0-based, in kgpu_pod_query.pts_hard / pts_soft order), per
+ * value id v of the constraint's key (key_n_values[key] entries):
+ *   kind 0, PreFilter (calPreFilterState, filtering.go:198-273): registered[v] = the pair is a
+ *           TpPairToMatchNum key (an eligible node carries it), counts[v] = TpPairToMatchNum; *scalar =
+ *           criticalPaths[0].MatchNum (MaxInt32 when no pair is registered);
+ *   kind 1, PreScore over the nodes the profile's filters pass (initPreScoreState, scoring.go:59-169):
+ *           registered[v] = the pair is a TopologyPairToPodCounts key, counts[v] its count; *scalar = the
+ *           topology size behind topologyNormalizingWeight (-1: not the key's first constraint).
+ * Unsharded engines only. */
+int kgpu_debug_pts_state(kgpu_ctx* ctx, const kgpu_pod_query* q, const kgpu_pools* pools, int32_t kind,
+                         int32_t constraint, uint8_t* registered, int64_t* counts, int64_t* scalar);
 
 /* Mirror coherence: ForgetPod / RemovePod of an existing pod slot (cache.go:383-410). */
 int kgpu_forget_pod(kgpu_ctx* ctx, int32_t pod_slot);
@@ -526,6 +539,11 @@ int kgpu_read_nodes(kgpu_ctx* ctx, int64_t* req_cpu, int64_t* req_mem, int64_t* 
  * granules through peer stores into every rank's mailbox ring over xGMI (kgpu_xgmi_*); 0 = the
  * per-pod RCCL all-gather for every pod. */
 #define KGPU_OPT_XGMI 8
+/* KGPU_OPT_SKIP_RELEASE_AT (9): test hook -- in the persistent run holding batch query `value`, the
+ * workgroups' candidate rows are staged for the next pod but the LDS hand-off is never released, so
+ * the next pod's wait on it times out (the path a lost LDS release would take): the batch fails with
+ * KGPU_E_DEVICE and the mirror is invalidated (-1, the default: never). */
+#define KGPU_OPT_SKIP_RELEASE_AT 9
 int kgpu_set_option(kgpu_ctx* ctx, int32_t option, int64_t value);
 /* Phase stamps of the last persistent run (100 MHz s_memrealtime ticks), 16 per pipeline
  * iteration (pods + 1): workgroup 0's {start, evaluated, previous pod resolved, published, end, 0,

@@ -65,6 +65,7 @@ struct kgpu_ctx {
   DevBuf gran;        // persistent-kernel granules + abort word
   int32_t abort_host = 0;
   int32_t abort_at = -1;  // KGPU_OPT_ABORT_AT: batch query index at which a persistent run aborts
+  int32_t skip_release_at = -1;  // KGPU_OPT_SKIP_RELEASE_AT: batch query whose LDS hand-off is never released
   bool phase_trace = false;
   DevBuf trace;
   std::vector<int64_t> trace_host;
@@ -1850,6 +1851,7 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
       ba.seq0 = first_seq + i;
       ba.abort = abort_word;
       ba.abort_at = c->abort_at >= i && c->abort_at < i + cnt ? c->abort_at - i : -1;
+      ba.skip_release_at = c->skip_release_at >= i && c->skip_release_at < i + cnt ? c->skip_release_at - i : -1;
       ba.trace = nullptr;
       if (c->phase_trace) {
         if ((rc = ensure(c, c->trace, sizeof(int64_t) * 16 * (size_t)(cnt + 1)))) return rc;
@@ -2747,6 +2749,7 @@ int kgpu_set_option(kgpu_ctx* c, int32_t option, int64_t value) try {
   else if (option == KGPU_OPT_TOPO_PERSISTENT) c->tfast = value != 0;
   else if (option == KGPU_OPT_ABORT_AT) c->abort_at = value < 0 || value > INT32_MAX ? -1 : (int32_t)value;
   else if (option == KGPU_OPT_XGMI) c->xgmi = value != 0;
+  else if (option == KGPU_OPT_SKIP_RELEASE_AT) c->skip_release_at = value < 0 || value > INT32_MAX ? -1 : (int32_t)value;
   else return KGPU_E_INVAL;
   return KGPU_OK;
 } catch (...) {
@@ -3150,6 +3153,72 @@ int kgpu_select_victims(kgpu_ctx* c, const kgpu_pod_query* q, const kgpu_pools* 
   }
   const int32_t pick = pick_one_node(cand, nodes_out, victims_out, args, prio.data());
   if (chosen) *chosen = pick >= 0 ? pick + c->st.node_base : -1;
+  return KGPU_OK;
+} catch (...) {
+  return on_exception(c, false);
+}
+
+int kgpu_debug_pts_state(kgpu_ctx* c, const kgpu_pod_query* q, const kgpu_pools* pools, int32_t kind,
+                         int32_t constraint, uint8_t* registered, int64_t* counts, int64_t* scalar) try {
+  if (!c || !q || !registered || !counts || !scalar || (kind != 0 && kind != 1) || constraint < 0) return KGPU_E_INVAL;
+  if (hipSetDevice(c->device) != hipSuccess) return KGPU_E_DEVICE;
+  if (!c->uploaded) return fail(c, KGPU_E_STATE, "no snapshot uploaded");
+  if (c->comm || c->xg_nranks > 1)
+    return fail(c, KGPU_E_UNSUPPORTED, "kgpu_debug_pts_state reads one engine's state: unsharded only");
+  if (!has_filter(c, KGPU_F_POD_TOPOLOGY_SPREAD) && kind == 0)
+    return fail(c, KGPU_E_INVAL, "the profile has no PodTopologySpread filter");
+  if (!has_score(c, KGPU_S_POD_TOPOLOGY_SPREAD) && kind == 1)
+    return fail(c, KGPU_E_INVAL, "the profile has no PodTopologySpread score");
+  int rc;
+  Staged sg;
+  if ((rc = stage_topology(c, q, 1, pools, sg))) return rc;
+  const kgpu::QPlan& pl = sg.plans[0];
+  if (constraint >= (kind == 0 ? pl.n_hard : pl.n_soft)) return fail(c, KGPU_E_INVAL, "no such constraint");
+  const kgpu::TSpread& sp = kind == 0 ? pl.hard[constraint] : pl.soft[constraint];
+  if ((rc = upload_pools(c, pools))) return rc;
+  if ((rc = ensure(c, c->queries, sizeof(kgpu_pod_query)))) return rc;
+  HIP_OK(c, hipMemcpyAsync(c->queries.p, q, sizeof(kgpu_pod_query), hipMemcpyHostToDevice, c->stream));
+  DevState st = c->st;
+  st.queries = static_cast<const kgpu_pod_query*>(c->queries.p);
+  st.diag_raw = nullptr;
+  st.diag_norm = nullptr;
+  st.nom_status = nullptr;
+  if ((rc = ensure(c, c->results, sizeof(kgpu_result)))) return rc;
+  st.results = static_cast<kgpu_result*>(c->results.p);
+  if ((rc = ensure(c, c->dstate, sizeof(DevState)))) return rc;
+  c->ds_ptr = nullptr;  // the short cycle's cached DevState image is stale
+  c->st_batch = st;
+  HIP_OK(c, hipMemcpyAsync(c->dstate.p, &c->st_batch, sizeof(DevState), hipMemcpyHostToDevice, c->stream));
+  const DevState* dst = static_cast<const DevState*>(c->dstate.p);
+  HIP_OK(c, hipMemsetAsync(c->st.scratch, 0, sizeof(int64_t) * (size_t)pl.scratch_len, c->stream));
+  PodArgs a{};
+  a.pod = 0;
+  a.prev = -1;
+  const int blocks = kgpu::eval_blocks(c->st.N);
+  const int64_t D = sp.key >= 0 ? c->key_n_values[(size_t)sp.key] : 0;
+  // PreFilter: the histograms (k_topo_pre), the critical-path minima (k_topo_min); PreScore: the
+  // registrations of the filtered nodes (k_topo_filter) too
+  if (kgpu::launch_topo_phase(dst, a, 0, blocks, 0, c->stream) ||
+      (kind == 0 && D > 0 && kgpu::launch_topo_phase(dst, a, 1, blocks, D, c->stream)) ||
+      (kind == 1 && kgpu::launch_topo_phase(dst, a, 2, blocks, 0, c->stream)))
+    return fail(c, KGPU_E_DEVICE, "topology phase launch failed");
+  std::vector<int64_t> sc((size_t)pl.scratch_len);
+  HIP_OK(c, hipMemcpyAsync(sc.data(), c->st.scratch, sizeof(int64_t) * sc.size(), hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(c, hipStreamSynchronize(c->stream));
+  const kgpu::TopoHdr* h = reinterpret_cast<const kgpu::TopoHdr*>(sc.data());
+  for (int64_t v = 0; v < D; ++v) {
+    registered[v] = sc[(size_t)(pl.slot_off[sp.rslot] + v)] != 0 ? 1 : 0;
+    counts[v] = sc[(size_t)(pl.slot_off[sp.cslot] + v)];
+  }
+  if (kind == 0) {
+    // criticalPaths[0].MatchNum: MaxInt32 when no pair registered (filtering.go:86-90)
+    const uint64_t u = static_cast<uint64_t>(h->pmin[constraint]);
+    *scalar = u ? (int64_t)(~u ^ (1ull << 63)) : 2147483647;
+  } else {
+    // topologyNormalizingWeight's size (scoring.go:92-102): registered pairs of the key, or for
+    // kubernetes.io/hostname the filtered nodes that carry every soft key
+    *scalar = sp.is_hostname ? (int64_t)h->feas_nonign : (sp.first_of_key ? h->ssize[constraint] : -1);
+  }
   return KGPU_OK;
 } catch (...) {
   return on_exception(c, false);

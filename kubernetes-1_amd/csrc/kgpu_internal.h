@@ -258,7 +258,9 @@ struct BatchArgs {
                         // granule published, iteration end
   int32_t abort_at;     // KGPU_OPT_ABORT_AT test hook: workgroup 0 raises the abort word at this
                         // iteration (-1: never)
-  int32_t pad_a;
+  int32_t skip_release_at;  // KGPU_OPT_SKIP_RELEASE_AT test hook: at this iteration the candidate lane
+                            // stages its row but never releases the hand-off, so the next pod's LDS
+                            // wait times out (-1: never)
   // Node sharding over xGMI (kgpu_xgmi_init): every workgroup of every rank publishes its granule
   // and feasible count into every rank's mailbox ring; each rank polls its own.  Unsharded:
   // nranks 1, pgran[0] = gran, pfeas[0] = feas, GT = groups, R = 0 (rows are this launch's pods,

@@ -1589,7 +1589,7 @@ __global__ __launch_bounds__(B + 64) void k_batch(const DevState* __restrict__ s
 #pragma unroll
         for (int j = 0; j < K; ++j)
           if (j == cand / B) sh.brow[p] = r[j];
-        lds_release(&sh.bready, i + 1);
+        if (i != pa.skip_release_at) lds_release(&sh.bready, i + 1);
       }
     }
     staged = have_cur && !slow && cand >= 0;

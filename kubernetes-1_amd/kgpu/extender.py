@@ -14,17 +14,23 @@ with `filterVerb: filter`, `prioritizeVerb: prioritize`, `bindVerb: bind`, `weig
               kgpu_apply_delta; the candidates that pass come back as NodeNames (or Nodes),
               every other candidate in FailedNodes with the failing plugin's reasons.
   prioritize  the same cycle's outcome per candidate.  mode "select" (default): 10 for the
-              device's selectHost winner, 0 otherwise -- the scheduler adds score * weight *
-              (MaxNodeScore / MaxExtenderPriority) (generic_scheduler.go:703-707), so with no
-              in-tree scorers its own selectHost lands on the device's winner.  mode "total":
-              the device's weighted score total of each node.
+              selectHost winner AMONG THE CANDIDATES the scheduler sent (the device's weighted
+              totals of those nodes, the build's tie-break key), 0 otherwise -- the scheduler adds
+              score * weight * (MaxNodeScore / MaxExtenderPriority) (generic_scheduler.go:703-707),
+              so with no in-tree scorers its own selectHost lands on that node.  The scheduler may
+              send a subset: numFeasibleNodesToFind already cut the list (generic_scheduler.go:436-441)
+              and in-tree filters or earlier extenders may have trimmed it.  mode "total": the
+              device's weighted score total of each node.
   bind        the pod is bound (optional `binder` callback) and its placement goes into the
               scheduler-cache mirror (AssumePod + FinishBinding, cache.go:338-381), so the next
               cycle sees it without an informer round trip.
 
 A cycle is computed once per (pod UID, cache generation): filter and prioritize of one scheduling
-cycle share it.  Calls are serialized (one engine, one stream).
+cycle share it.  Calls are serialized (one engine, one stream).  The extender's own profile must
+evaluate every node (percentageOfNodesToScore 100): the scheduler has already applied its cut to the
+candidate list, and a second cut would drop valid candidates as "not evaluated".
 """
+import collections
 import json
 import threading
 import time
@@ -34,10 +40,13 @@ import numpy as np
 
 from . import abi
 from . import api
+from . import tiebreak
 from .compile import CompileError, Pools
 from .framework import status_reasons
 
 MAX_EXTENDER_PRIORITY = 10  # extender/v1/types.go:29
+PENDING_MAX = 4096          # pods filtered but not (yet) bound that the extender remembers
+PENDING_TTL = 600.0         # seconds: an unbound pod's record expires (unschedulable / bound elsewhere)
 
 
 class ExtenderError(Exception):
@@ -55,6 +64,10 @@ class GpuExtender:
         API-server binding itself (None: record the placement only)."""
         if mode not in ("select", "total"):
             raise ValueError("mode must be 'select' or 'total'")
+        pct = getattr(cache.profile, "percentage_of_nodes_to_score", 100)
+        if pct not in (None, 100):
+            raise ValueError("the extender's profile must score every node (percentage_of_nodes_to_score 100): "
+                             "the scheduler cuts the candidate list before calling the extender")
         self.cache = cache
         self.mode = mode
         self.binder = binder
@@ -62,7 +75,9 @@ class GpuExtender:
         self.lock = threading.Lock()
         self.seq = 0
         self._memo = None      # (uid, generation, cycle)
-        self._pending = {}     # uid -> pod seen by filter / prioritize, awaiting bind
+        # uid -> (pod, time) seen by filter / prioritize, awaiting bind; bounded (PENDING_MAX, oldest
+        # first) and aged (PENDING_TTL): pods that never bind here must not accumulate
+        self._pending = collections.OrderedDict()
 
     # ------------------------------------------------------------------ cycle
     def _cycle(self, pod):
@@ -76,23 +91,51 @@ class GpuExtender:
         except CompileError as e:
             raise ExtenderError(str(e))
         pc, _ = pools.finalize()
-        res, _ = self.cache.engine.schedule_one(np.array([q], abi.QUERY), pc, seq=self.seq, assume=False)
+        seq = self.seq
+        res, _ = self.cache.engine.schedule_one(np.array([q], abi.QUERY), pc, seq=seq, assume=False)
         self.seq += 1
         n = len(self.cache.list)
         words = self.cache.engine.filter_words(n)
-        totals = None
-        if self.mode == "total":
-            totals = np.zeros(n, np.int64)
+        # the device's weighted total of every feasible node (framework.go:633-648): the candidates'
+        # winner in select mode, the scores in total mode
+        totals = np.zeros(n, np.int64)
+        if self.cache.profile.scores:
             for name, w in self.cache.profile.scores:
                 _, norm = self.cache.engine.scores(abi.SCORE_IDS[name], n)
-                totals += norm * w
+                totals += norm * max(int(w), 1)
+        else:
+            totals[:] = 1  # no score plugins: every feasible node scores 1 (generic_scheduler.go:631-640)
         node = int(res["node"])
         cyc = {"words": words, "totals": totals, "winner": self.cache.list[node] if node >= 0 else None,
-               "error": node == -2}
+               "error": node == -2, "seq": seq}
         if uid:
             self._memo = (uid, gen, cyc)
-            self._pending[uid] = pod
+            self._remember(uid, pod)
         return cyc
+
+    def _remember(self, uid, pod):
+        now = self.clock()
+        self._pending.pop(uid, None)
+        self._pending[uid] = (pod, now)
+        while self._pending and (len(self._pending) > PENDING_MAX or
+                                 now - next(iter(self._pending.values()))[1] > PENDING_TTL):
+            self._pending.popitem(last=False)
+
+    def _winner(self, cyc, names):
+        """selectHost over the candidates the device found feasible: the maximum of
+        total << 40 | rank40 (the build's tie-break, kgpu/tiebreak.py)."""
+        prof = self.cache.profile
+        seed = int(getattr(prof, "seed", 0x7B))
+        mode = int(getattr(prof, "tie_break_mode", tiebreak.MODE_HASH))
+        best, best_nm = -1, None
+        for nm in names:
+            i = self.cache.index[nm]
+            if int(cyc["words"][i]) != 0:
+                continue
+            k = tiebreak.key(int(cyc["totals"][i]), i, seed, cyc["seq"], mode)
+            if k > best:
+                best, best_nm = k, nm
+        return best_nm
 
     def _candidates(self, args):
         """ExtenderArgs -> (names, NodeList items or None).  NodeNames when the scheduler treats
@@ -159,10 +202,11 @@ class GpuExtender:
             pod = args.get("Pod") or {}
             names, _ = self._candidates(args)
             cyc = self._cycle(pod)
+            winner = self._winner(cyc, names) if self.mode == "select" else None
             out = []
             for nm in names:
                 if self.mode == "select":
-                    s = MAX_EXTENDER_PRIORITY if nm == cyc["winner"] else 0
+                    s = MAX_EXTENDER_PRIORITY if nm == winner else 0
                 else:
                     s = int(cyc["totals"][self.cache.index[nm]]) if cyc["words"][self.cache.index[nm]] == 0 else 0
                 out.append({"Host": nm, "Score": s})
@@ -172,7 +216,8 @@ class GpuExtender:
         """ExtenderBindingArgs -> ExtenderBindingResult (extender.go:384-404)."""
         with self.lock:
             uid, node = args.get("PodUID", ""), args.get("Node", "")
-            pod = self._pending.pop(uid, None)
+            rec = self._pending.pop(uid, None)
+            pod = rec[0] if rec is not None else None
             if pod is None:
                 return {"Error": "pod %s/%s (uid %s) was not filtered by this extender" %
                                  (args.get("PodNamespace", ""), args.get("PodName", ""), uid)}

@@ -224,10 +224,20 @@ class GpuFramework:
         if errors:
             raise CompileError(errors[min(errors)])
         index = {nn: i for i, nn in enumerate(self.order)}
+        # Preempt passes every PDB of the cluster; filterPodsWithPDBViolation only touches those that
+        # select a potential victim, in order: the engine gets that subset, renumbered (64-bit masks)
+        sel = [_pdbs_of(p, pdbs) for _, p, _ in cand]
+        used = sorted({j for js in sel for j in js})
+        if len(used) > 64:
+            raise ValueError("%d PodDisruptionBudgets select potential victims (the engine takes 64)" % len(used))
+        renum = {j: k for k, j in enumerate(used)}
         vic = np.zeros(len(cand), abi.VICTIM)
         for i, (nn, p, slot) in enumerate(cand):
-            vic[i] = (index[nn], slot, i, 0, _start_time(p, now), _pdb_mask(p, pdbs))
-        allowed = np.array([int(b.get("disruptionsAllowed", 0)) for b in pdbs], np.int32)
+            m = 0
+            for j in sel[i]:
+                m |= 1 << renum[j]
+            vic[i] = (index[nn], slot, i, 0, _start_time(p, now), m)
+        allowed = np.array([int(pdbs[j].get("disruptionsAllowed", 0)) for j in used], np.int32)
         out, vout, chosen = self.engine.select_victims(q[0], pc, vic, q[1:], allowed, self.snap.n_nodes)
         res = {}
         for n in range(self.snap.n_nodes):
@@ -291,9 +301,16 @@ def _start_time(pod, now):
     return int(t.timestamp()) * 1_000_000_000
 
 
+def _pdbs_of(pod, pdbs):
+    """Indices of the PodDisruptionBudgets selecting the pod, in order."""
+    m = _pdb_mask(pod, pdbs)
+    return [j for j in range(len(pdbs)) if (m >> j) & 1]
+
+
 def _pdb_mask(pod, pdbs):
     """PodDisruptionBudgets selecting the pod (filterPodsWithPDBViolation, generic_scheduler.go:878-919):
-    same namespace, a non-empty selector matching the pod's labels; label-less pods match none."""
+    same namespace, a non-empty selector matching the pod's labels; label-less pods match none.
+    A Python int: bit j for PDB j, any number of PDBs."""
     from .compile import label_selector_matches
     labels = api.labels_of(pod)
     m = 0

@@ -19,7 +19,7 @@ EXPORTS = ["kgpu_abi_version", "kgpu_struct_sizes", "kgpu_create", "kgpu_destroy
            "kgpu_get_filter", "kgpu_get_scores", "kgpu_forget_pod", "kgpu_read_nodes", "kgpu_set_option",
            "kgpu_read_phase_trace", "kgpu_comm_unique_id", "kgpu_comm_init", "kgpu_apply_delta",
            "kgpu_set_nominated", "kgpu_select_victims", "kgpu_xgmi_handle", "kgpu_xgmi_init", "kgpu_xgmi_active",
-           "kgpu_debug_fail_alloc"]
+           "kgpu_debug_fail_alloc", "kgpu_debug_pts_state"]
 
 
 class KgpuError(RuntimeError):
@@ -61,6 +61,7 @@ def lib():
     L.kgpu_xgmi_init.argtypes = [vp, i32, i32, vp]
     L.kgpu_xgmi_active.argtypes = [vp]
     L.kgpu_debug_fail_alloc.argtypes = [i32]
+    L.kgpu_debug_pts_state.argtypes = [vp, vp, C.POINTER(abi.Pools), i32, i32, vp, vp, C.POINTER(i64)]
     L.kgpu_select_victims.argtypes = [vp, vp, C.POINTER(abi.Pools), C.POINTER(abi.PreemptArgs), vp, vp,
                                       C.POINTER(i32)]
     if L.kgpu_abi_version() != abi.ABI_VERSION:
@@ -204,6 +205,17 @@ class Engine:
         b = bytes(handles)
         buf = (C.c_uint8 * len(b)).from_buffer_copy(b)
         self._check(lib().kgpu_xgmi_init(self.h, nranks, rank, buf))
+
+    def pts_state(self, query, pools, kind, constraint, n_values):
+        """kgpu_debug_pts_state: (registered[n_values] bool, counts[n_values] int64, scalar) of one pod's
+        PodTopologySpread PreFilter (kind 0) or PreScore (kind 1) state on the device."""
+        q = np.ascontiguousarray(np.asarray(query, abi.QUERY).reshape(1))
+        reg = np.zeros(max(n_values, 1), np.uint8)
+        cnt = np.zeros(max(n_values, 1), np.int64)
+        out = C.c_int64(0)
+        self._check(lib().kgpu_debug_pts_state(self.h, q.ctypes.data, C.byref(pools), kind, constraint,
+                                                reg.ctypes.data, cnt.ctypes.data, C.byref(out)))
+        return reg[:n_values].astype(bool), cnt[:n_values], int(out.value)
 
     def xgmi_active(self):
         return bool(lib().kgpu_xgmi_active(self.h))

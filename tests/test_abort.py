@@ -131,3 +131,27 @@ def test_allocation_failure_invalidates_and_recovers(point):
     e.upload(fw.snap, fw.arrays)
     got, _ = e.schedule_batch(q, pc)
     _same(_ref(fw, q, pc), got)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("at", [5, 120])
+def test_lds_handoff_timeout_recovers(at):
+    """An LDS hand-off that never completes (KGPU_OPT_SKIP_RELEASE_AT: the candidate row is staged
+    but its release skipped): the waiting wave times out after kSpinTimeout and raises the
+    abort word, the batch fails with KGPU_E_DEVICE, the mirror is invalidated, and after the
+    re-upload the engine schedules exactly as the C restatement."""
+    nodes, existing, pods, prof = cluster.fit_least_balanced(n_nodes=700, n_pods=200)
+    fw = GpuFramework(prof, nodes, existing, pods_hint=pods)
+    q, pc, _, errs = fw.compile_pods(pods)
+    assert not errs
+    e = fw.engine
+    e.set_option(abi.OPT_SKIP_RELEASE_AT, at)
+    with pytest.raises(KgpuError) as ex:
+        e.schedule_batch(q, pc)
+    assert ex.value.code == abi.E_DEVICE and "re-upload" in str(ex.value)
+    e.set_option(abi.OPT_SKIP_RELEASE_AT, -1)
+    with pytest.raises(KgpuError):
+        e.schedule_batch(q[:1], pc)
+    e.upload(fw.snap, fw.arrays)
+    got, _ = e.schedule_batch(q, pc)
+    _same(_ref(fw, q, pc), got)

@@ -19,6 +19,7 @@ import urllib.request
 import pytest
 
 from oracle.refsched import framework as F
+from oracle.refsched import tiebreak as TB
 from kgpu import cluster as K
 from kgpu.cache import SchedulerCache
 from kgpu.compile import Cluster, Profile
@@ -77,6 +78,9 @@ def test_argument_errors_without_engine():
     ext = GpuExtender(c)
     with pytest.raises(ValueError):
         GpuExtender(c, mode="sum")
+    # the scheduler cuts the candidate list itself: a second cut in the extender is refused
+    with pytest.raises(ValueError):
+        GpuExtender(SchedulerCache(Profile(percentage_of_nodes_to_score=50), nodes, create_engine=False))
     pod = K.pod("p", "100m", "128Mi")
     pod["metadata"]["uid"] = "u1"
     out = ext.filter({"Pod": pod, "Nodes": None, "NodeNames": ["n0", "nX"]})
@@ -102,7 +106,7 @@ def test_extender_cycles_match_oracle(seed):
     r = random.Random(seed)
     try:
         s = Stream(seed, c, nodes, services, rss, gpu=True)
-        placed = 0
+        placed = subset_checked = 0
         for i in range(40):
             if i % 5 == 4:
                 s.step()       # informer events between cycles reach the device as deltas
@@ -135,6 +139,17 @@ def test_extender_cycles_match_oracle(seed):
             assert len(top) <= 1
             if want.host in out["NodeNames"]:
                 assert top == [want.host]
+            else:
+                # the scheduler sent a strict subset without the overall winner (its own cut or
+                # filters): select mode ranks the candidates it sent, by the oracle's totals
+                # and the build's tie-break key
+                idx = {}
+                for k, n in enumerate(c.list):
+                    idx.setdefault(n, k)
+                tot = dict(want.totals) if want.totals else {n: 1 for n in out["NodeNames"]}
+                exp = max(out["NodeNames"], key=lambda n: TB.key(tot[n], idx[n], seq, 0x7B))
+                assert top == [exp], (i, top, exp)
+                subset_checked += 1
             if not top:
                 continue
             code, b = _post(url, "bind", {"PodName": pod["metadata"]["name"], "PodNamespace": "default",
@@ -183,3 +198,20 @@ def test_extender_total_mode_and_node_objects():
     finally:
         srv.shutdown()
         c.close()
+
+
+def test_pending_pods_are_bounded():
+    """Pods filtered but never bound here (unschedulable, bound by another path, deleted) expire from
+    the extender's pending map: bounded by count and by age."""
+    from kgpu import extender as E
+    nodes = [K.node("n%d" % i, "4", "8Gi") for i in range(2)]
+    now = [0.0]
+    c = SchedulerCache(Profile(), nodes, create_engine=False)
+    ext = GpuExtender(c, clock=lambda: now[0])
+    for i in range(E.PENDING_MAX + 50):
+        ext._remember("u%d" % i, {"metadata": {"uid": "u%d" % i}})
+    assert len(ext._pending) == E.PENDING_MAX
+    assert "u0" not in ext._pending and "u%d" % (E.PENDING_MAX + 49) in ext._pending
+    now[0] = E.PENDING_TTL + 1.0
+    ext._remember("fresh", {"metadata": {"uid": "fresh"}})
+    assert list(ext._pending) == ["fresh"]

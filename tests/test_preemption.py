@@ -209,3 +209,31 @@ def test_preempt_flow_and_eligibility():
     never["spec"]["preemptionPolicy"] = "Never"
     assert fw.preempt(never, cr.statuses, pdbs, NOW) == ("", [], [])
     fw.engine.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(3))
+def test_many_pdbs_only_matching_ones_reach_the_engine(seed):
+    """Preempt lists every PodDisruptionBudget of the cluster: 80 PDBs, most selecting no
+    potential victim, the matching ones scattered past index 64.  The engine gets the matching subset
+    renumbered in order (filterPodsWithPDBViolation walks only those), and the victims, violation
+    counts and picked node equal the oracle's over the full list."""
+    nodes, existing, pods, services, rss, pdbs, noms = _scenario(seed, False)
+    r = random.Random(900 + seed)
+    many = [{"namespace": "nowhere", "selector": {"matchLabels": {"app": "x%d" % j}}, "disruptionsAllowed": 0}
+            for j in range(80)]
+    for k, p in enumerate(pdbs):
+        many[r.randrange(60, 80) if k % 2 else r.randrange(0, 80)] = p
+    fw = GpuFramework(Profile(), nodes, existing, cluster=Cluster(services=services, rss=rss), pods_hint=pods)
+    checked = 0
+    for pod in pods:
+        want = _oracle_preempt(nodes, existing, pod, services, rss, many, [])
+        if want is None:
+            continue
+        n2v, pick = fw.select_nodes_for_preemption(pod, many, NOW)
+        got = {n: ([NI.name(p) for p in v], nv) for n, (v, nv) in n2v.items()}
+        assert got == want[0], (seed, NI.name(pod))
+        assert pick == want[1], (seed, NI.name(pod))
+        checked += 1
+    assert checked
+    fw.engine.close()

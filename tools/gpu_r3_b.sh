@@ -9,6 +9,7 @@ R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/${1:-r3b}
 mkdir -p $O
 cd $R && export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests/test_pts_state_device.py tests/test_abort.py tests/test_extender.py tests/test_preemption.py -x -q -m gpu --timeout 300 --timeout-method thread > $O/pytest_new.log 2>&1 || exit 1
 timeout -k 10 400 python -u bench.py > $O/bench_default.log 2>&1 || exit 1
 cd /tmp
 timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $O/probe_osexit -o run -- python3 -u $R/tools/exit_probe.py kgpu $O/maps_osexit.txt --os-exit > $O/probe_osexit.log 2>&1
