@@ -220,3 +220,24 @@ def sharded_spread(n_nodes=1_000_000, n_pods=10000, seed=CLUSTER_SEED, n_zones=6
 
 CONFIGS = {"a": scheduling_basic, "b": fit_least_balanced, "c": taints_affinity_spread, "d": pod_affinity,
            "e": sharded_spread}
+
+
+def uneven_zones(sizes=(("a", 30), ("b", 2), ("c", 30)), n_pods=24):
+    """Zones of uneven size for node-sharding tests: nodeTree's zone round robin
+    (node_tree.go:147-170) exhausts the 2-node zone b early, so both of its nodes sit in the first
+    contiguous shard of Snapshot.List().  b holds the smallest match count, so every other shard
+    needs the first shard's pair registrations to see criticalPaths[0] (filtering.go:246-270):
+    without the cross-shard union its zones a / c would pass the skew check that the cluster-wide
+    minimum fails.  Pods: PodTopologySpread zone (DoNotSchedule) + hostname (ScheduleAnyway)."""
+    nodes = []
+    for z, n in sizes:
+        nodes += [node("%s%d" % (z, i), "4", "32Gi", 110, labels={ZONE: z, HOSTNAME: "%s%d" % (z, i)})
+                  for i in range(n)]
+    existing = [pod("e%d" % i, "100m", "128Mi", labels={"app": "web"}, node_name=nn)
+                for i, nn in enumerate(["a3", "a7", "a20", "c1", "c28"])]
+    sel = {"matchLabels": {"app": "web"}}
+    tsc = [{"maxSkew": 1, "topologyKey": ZONE, "whenUnsatisfiable": "DoNotSchedule", "labelSelector": sel},
+           {"maxSkew": 1, "topologyKey": HOSTNAME, "whenUnsatisfiable": "ScheduleAnyway", "labelSelector": sel}]
+    pods = [pod("p%d" % i, "100m", "128Mi", labels={"app": "web"}, topologySpreadConstraints=tsc)
+            for i in range(n_pods)]
+    return nodes, existing, pods, _c.Profile()

@@ -38,8 +38,10 @@ def _workload(name):
         nodes, existing, pods, prof = cluster.taints_affinity_spread(n_nodes=1200, n_pods=160)
     elif name == "affinity":  # config (d): existing pods' and incoming pods' (anti-)affinity terms
         nodes, existing, pods, prof = cluster.pod_affinity(n_nodes=900, n_existing=900, n_pods=128)
-    else:  # config (e): (b)+(c) generator, zone = i % 64
+    elif name == "sharded_e":  # config (e): (b)+(c) generator, zone = i % 64
         nodes, existing, pods, prof = cluster.sharded_spread(n_nodes=2000, n_pods=160)
+    else:  # a zone whose nodes all sit in rank 0's shard holds the critical path
+        nodes, existing, pods, prof = cluster.uneven_zones()
     return nodes, existing, pods, prof
 
 
@@ -77,7 +79,7 @@ def _rank_main(rank, world, port, name, out):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["spread", "affinity", "sharded_e"])
+@pytest.mark.parametrize("name", ["spread", "affinity", "sharded_e", "uneven"])
 def test_xgmi_topology_two_ranks_one_gpu(name, tmp_path):
     from oracle.cref import RefEngine
     nodes, existing, pods, prof = _workload(name)
