@@ -631,6 +631,13 @@ int kgpu_xgmi_init(kgpu_ctx* ctx, int32_t nranks, int32_t rank, const uint8_t* h
  * device mirror (KGPU_E_STATE until the next kgpu_upload_snapshot). */
 int kgpu_debug_fail_alloc(int32_t countdown);
 
+/* Diagnostic: the device's broken-linear shape function (the one RequestedToCapacityRatio scores
+ * with) evaluated at n utilizations over n_points ascending points taken as given (unscaled).
+ * Replaces buildBrokenLinearFunction's direct use in requested_to_capacity_ratio_test.go:119
+ * (pkg/scheduler/framework/plugins/noderesources/requested_to_capacity_ratio.go:150-170). */
+int kgpu_debug_broken_linear(kgpu_ctx* ctx, const kgpu_shape_point* points, int32_t n_points, const int64_t* p,
+                             int32_t n, int64_t* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -3224,6 +3224,25 @@ int kgpu_debug_pts_state(kgpu_ctx* c, const kgpu_pod_query* q, const kgpu_pools*
   return on_exception(c, false);
 }
 
+int kgpu_debug_broken_linear(kgpu_ctx* c, const kgpu_shape_point* points, int32_t n_points, const int64_t* p,
+                             int32_t n, int64_t* out) try {
+  if (!c || !points || !p || !out || n_points <= 0 || n_points > 16 || n <= 0) return KGPU_E_INVAL;
+  if (hipSetDevice(c->device) != hipSuccess) return KGPU_E_DEVICE;
+  fail_point();
+  int64_t* d = nullptr;
+  HIP_OK(c, hipMalloc(&d, sizeof(int64_t) * 2 * (size_t)n));
+  int rc = KGPU_OK;
+  if (hipMemcpyAsync(d, p, sizeof(int64_t) * (size_t)n, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+      kgpu::launch_debug_broken_linear(points, n_points, d, d + n, n, c->stream) ||
+      hipMemcpyAsync(out, d + n, sizeof(int64_t) * (size_t)n, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+      hipStreamSynchronize(c->stream) != hipSuccess)
+    rc = fail(c, KGPU_E_DEVICE, "broken-linear probe failed");
+  (void)hipFree(d);
+  return rc;
+} catch (...) {
+  return on_exception(c, false);
+}
+
 int kgpu_get_filter(kgpu_ctx* c, uint32_t* words) try {
   if (!c || !words) return KGPU_E_INVAL;
   if (!c->last_diag) return fail(c, KGPU_E_STATE, "no kgpu_schedule_one cycle to report");

@@ -509,6 +509,8 @@ int launch_topo(const DevState* st, PodArgs a, int blocks, int64_t min_values, i
 inline int topo_barriers(int64_t min_values) { return min_values > 0 ? 5 : 4; }
 // Initialize mcnt columns [c0, c0 + nc) from the pod table (n_pods rows).
 int launch_class_init(const DevState* st, int c0, int nc, int n_pods, void* stream);
+int launch_debug_broken_linear(const kgpu_shape_point* pts, int n_pts, const int64_t* p, int64_t* out, int n,
+                               void* stream);
 int launch_topo_phase(const DevState* st, const PodArgs& a, int phase, int blocks, int64_t extra, void* stream);
 // Persistent topology run: signature bitmaps + pair registrations (k_sig_init), histogram
 // initialization from the match-count columns (k_hist_init), then k_tbatch.  kidx: geometry.

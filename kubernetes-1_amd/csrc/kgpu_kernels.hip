@@ -344,15 +344,28 @@ __device__ __forceinline__ int64_t most_score(const DevState& st, const kgpu_pod
 
 // RequestedToCapacityRatio (requested_to_capacity_ratio.go:124-170): the broken-linear shape over
 // utilization per resource, weighted mean over resources with a positive score, math.Round.
-__device__ __forceinline__ int64_t rtcr_shape(const DevState& st, int64_t p) {
-  for (int i = 0; i < st.n_shape; ++i)
-    if (p <= st.shape[i].utilization) {
-      if (i == 0) return st.shape[0].score;
+// buildBrokenLinearFunction (requested_to_capacity_ratio.go:150-170) over `n` ascending points
+__device__ __forceinline__ int64_t broken_linear(const kgpu_shape_point* sh, int n, int64_t p) {
+  for (int i = 0; i < n; ++i)
+    if (p <= sh[i].utilization) {
+      if (i == 0) return sh[0].score;
       // Go int64 arithmetic: the product may be negative, division truncates toward zero
-      return st.shape[i - 1].score + (st.shape[i].score - st.shape[i - 1].score) * (p - st.shape[i - 1].utilization) /
-                                         (st.shape[i].utilization - st.shape[i - 1].utilization);
+      return sh[i - 1].score + (sh[i].score - sh[i - 1].score) * (p - sh[i - 1].utilization) /
+                                   (sh[i].utilization - sh[i - 1].utilization);
     }
-  return st.shape[st.n_shape - 1].score;
+  return sh[n - 1].score;
+}
+__device__ __forceinline__ int64_t rtcr_shape(const DevState& st, int64_t p) { return broken_linear(st.shape, st.n_shape, p); }
+
+// kgpu_debug_broken_linear: the device's broken-linear function at given utilizations (the reference's
+// requested_to_capacity_ratio_test.go:119 table, unscaled points)
+struct ShapeProbe {
+  kgpu_shape_point pts[16];
+  int32_t n;
+};
+__global__ void k_dbg_broken_linear(ShapeProbe s, const int64_t* __restrict__ p, int64_t* __restrict__ out, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = broken_linear(s.pts, s.n, p[i]);
 }
 __device__ __forceinline__ int64_t rtcr_score(const DevState& st, const kgpu_pod_query& q, const NodeRes& nr, int n) {
   int64_t node_score = 0, wsum = 0;
@@ -2240,6 +2253,16 @@ int launch_topo_phase(const DevState* st, const PodArgs& a, int phase, int block
       hipLaunchKernelGGL(k_topo_resolve, dim3(blocks), dim3(kBlock), 0, s, st, r, extra);
     }
   }
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_debug_broken_linear(const kgpu_shape_point* pts, int n_pts, const int64_t* p, int64_t* out, int n,
+                               void* stream) {
+  if (n_pts <= 0 || n_pts > 16 || n <= 0) return -1;
+  ShapeProbe s{};
+  for (int i = 0; i < n_pts; ++i) s.pts[i] = pts[i];
+  s.n = n_pts;
+  hipLaunchKernelGGL(k_dbg_broken_linear, dim3((n + 63) / 64), dim3(64), 0, (hipStream_t)stream, s, p, out, n);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -78,6 +78,13 @@ class CycleResult:
         self.scores = scores        # {plugin: {node: (raw, normalized)}} over feasible nodes
 
 
+def nodes_where_preemption_might_help(order, codes):
+    """nodesWherePreemptionMightHelp (generic_scheduler.go:1041-1056): every node of `order` whose
+    filter status in `codes` ({node: status code}; absent = success) is not
+    UnschedulableAndUnresolvable -- removing pods cannot fix such a node."""
+    return [nn for nn in order if codes.get(nn, abi.CODE_SUCCESS) != abi.CODE_UNRESOLVABLE]
+
+
 class GpuFramework:
     def __init__(self, profile, nodes, existing=(), cluster=None, pods_hint=(), device=0, create_engine=True,
                  shard=None):
@@ -210,13 +217,20 @@ class GpuFramework:
             noms[i] = (index[nn], i)
         self.engine.set_nominated(noms, q, pc)
 
-    def select_nodes_for_preemption(self, pod, pdbs=(), now=0):
+    def select_nodes_for_preemption(self, pod, pdbs=(), now=0, nodes=None):
         """selectNodesForPreemption + pickOneNodeForPreemption (generic_scheduler.go:718-1012) on the
-        device.  Returns ({node name: (victim pods, numPDBViolations)} in Snapshot.List() order, the
-        picked node name or "")."""
+        device over `nodes` (default: every node).  Returns ({node name: (victim pods,
+        numPDBViolations)} in Snapshot.List() order, the picked node name or "").
+
+        A node outside `nodes` gets no potential victims, so the engine re-filters it as it stands --
+        it failed this cycle's filters, so it fails again and is never a candidate: the result is the
+        reference's selection over potentialNodes only (generic_scheduler.go:279-289)."""
         prio = _priority(pod)
+        keep = None if nodes is None else set(nodes)
         cand = []
         for nn in self.order:
+            if keep is not None and nn not in keep:
+                continue
             for p, slot in self.node_pods.get(nn, []):
                 if _priority(p) < prio:
                     cand.append((nn, p, slot))
@@ -255,11 +269,11 @@ class GpuFramework:
         Returns (node name or "", victim pods, nominated pods whose nomination is cleared)."""
         if not self._eligible_to_preempt(pod):
             return "", [], []
-        potential = [nn for nn in self.order
-                     if (statuses.get(nn) or (abi.CODE_SUCCESS,))[0] != abi.CODE_UNRESOLVABLE]
+        potential = nodes_where_preemption_might_help(
+            self.order, {nn: st[0] for nn, st in statuses.items() if st})
         if not potential:
             return "", [], [pod]
-        n2v, node = self.select_nodes_for_preemption(pod, pdbs, now)
+        n2v, node = self.select_nodes_for_preemption(pod, pdbs, now, nodes=potential)
         if not node:
             return "", [], []
         prio = _priority(pod)

@@ -19,7 +19,7 @@ EXPORTS = ["kgpu_abi_version", "kgpu_struct_sizes", "kgpu_create", "kgpu_destroy
            "kgpu_get_filter", "kgpu_get_scores", "kgpu_forget_pod", "kgpu_read_nodes", "kgpu_set_option",
            "kgpu_read_phase_trace", "kgpu_comm_unique_id", "kgpu_comm_init", "kgpu_apply_delta",
            "kgpu_set_nominated", "kgpu_select_victims", "kgpu_xgmi_handle", "kgpu_xgmi_init", "kgpu_xgmi_active",
-           "kgpu_debug_fail_alloc", "kgpu_debug_pts_state"]
+           "kgpu_debug_fail_alloc", "kgpu_debug_pts_state", "kgpu_debug_broken_linear"]
 
 
 class KgpuError(RuntimeError):
@@ -62,6 +62,7 @@ def lib():
     L.kgpu_xgmi_active.argtypes = [vp]
     L.kgpu_debug_fail_alloc.argtypes = [i32]
     L.kgpu_debug_pts_state.argtypes = [vp, vp, C.POINTER(abi.Pools), i32, i32, vp, vp, C.POINTER(i64)]
+    L.kgpu_debug_broken_linear.argtypes = [vp, vp, i32, vp, i32, vp]
     L.kgpu_select_victims.argtypes = [vp, vp, C.POINTER(abi.Pools), C.POINTER(abi.PreemptArgs), vp, vp,
                                       C.POINTER(i32)]
     if L.kgpu_abi_version() != abi.ABI_VERSION:
@@ -216,6 +217,17 @@ class Engine:
         self._check(lib().kgpu_debug_pts_state(self.h, q.ctypes.data, C.byref(pools), kind, constraint,
                                                 reg.ctypes.data, cnt.ctypes.data, C.byref(out)))
         return reg[:n_values].astype(bool), cnt[:n_values], int(out.value)
+
+    def broken_linear(self, points, utilizations):
+        """kgpu_debug_broken_linear: the device's broken-linear shape function (the one
+        RequestedToCapacityRatio scores with) over `points` [(utilization, score)], unscaled."""
+        pts = (abi.ShapePoint * len(points))()
+        for i, (u, sc) in enumerate(points):
+            pts[i].utilization, pts[i].score = int(u), int(sc)
+        p = np.ascontiguousarray(utilizations, np.int64)
+        out = np.zeros(len(p), np.int64)
+        self._check(lib().kgpu_debug_broken_linear(self.h, pts, len(points), p.ctypes.data, len(p), out.ctypes.data))
+        return [int(x) for x in out]
 
     def xgmi_active(self):
         return bool(lib().kgpu_xgmi_active(self.h))

@@ -1362,3 +1362,11 @@ int kgpu_ref_read_nodes(const ref_state* r, int64_t* req_cpu, int64_t* req_mem, 
   if (num_pods) memcpy(num_pods, r->num_pods, 4 * N);
   return 0;
 }
+
+/* The broken-linear function alone over a config's shape points (requested_to_capacity_ratio_test.go:119
+ * checks buildBrokenLinearFunction directly, with unscaled points). */
+int kgpu_ref_broken_linear(const kgpu_config* cfg, const int64_t* p, int n, int64_t* out) {
+  if (!cfg || cfg->n_shape <= 0) return -1;
+  for (int i = 0; i < n; ++i) out[i] = broken_linear(cfg, p[i]);
+  return 0;
+}

@@ -30,8 +30,23 @@ def lib():
         L.kgpu_ref_destroy.argtypes = [vp]
         L.kgpu_ref_schedule.argtypes = [vp, vp, C.c_int, vp, C.c_int64, vp, vp, vp, vp]
         L.kgpu_ref_read_nodes.argtypes = [vp, vp, vp, vp, vp, vp, vp]
+        L.kgpu_ref_broken_linear.argtypes = [vp, vp, C.c_int, vp]
         _lib = L
     return _lib
+
+
+def broken_linear(points, utilizations):
+    """buildBrokenLinearFunction over unscaled `points` at `utilizations` (the C restatement)."""
+    from kgpu import abi
+    cfg = abi.Config()
+    cfg.n_shape = len(points)
+    for i, (u, sc) in enumerate(points):
+        cfg.shape[i].utilization, cfg.shape[i].score = int(u), int(sc)
+    p = np.ascontiguousarray(utilizations, np.int64)
+    out = np.zeros(len(p), np.int64)
+    if lib().kgpu_ref_broken_linear(C.addressof(cfg), p.ctypes.data, len(p), out.ctypes.data):
+        raise ValueError("no shape points")
+    return [int(x) for x in out]
 
 
 class RefEngine:

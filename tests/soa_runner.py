@@ -25,7 +25,7 @@ def supported(c):
         return c["plugin"] in TIER1_SCORES
     if k == "filter":
         return c["plugin"] in TIER1_FILTERS
-    if k in ("image_name", "node_tree", "node_tree_ops"):
+    if k in ("image_name", "node_tree", "node_tree_ops", "normalize", "broken_linear"):
         return True
     if k == "schedule":
         prof = c.get("profile") or {}
@@ -60,7 +60,55 @@ def _profile(c):
                    scores=[tuple(s) for s in p.get("scores", Profile.DEFAULT_SCORES)])
 
 
+def normalize_case(c):
+    """A helper/normalize_score_test.go row (DefaultNormalizeScore over given raw scores) as a score
+    case of the plugin that normalizes with it: reverse -> TaintToleration (raw = the node's
+    intolerable PreferNoSchedule taints, taint_toleration.go:123-157), not reverse -> NodeAffinity
+    (raw = the summed weights of the matched preferred terms, node_affinity.go:66-111).  Node i
+    carries raw score scores[i]; the product's normalize path must give the table's values."""
+    assert c["max_priority"] == 100
+    raws = [int(v) for _, v in c["scores"]]
+    nodes, terms = [], []
+    for i, v in enumerate(raws):
+        meta = {"name": str(i)}
+        spec = {}
+        if c["reverse"]:
+            spec["taints"] = [{"key": "t%d_%d" % (i, j), "value": "x", "effect": "PreferNoSchedule"} for j in range(v)]
+        else:
+            # v as terms of weight <= 100, each matched by this node's own label
+            labels, left, j = {}, v, 0
+            while left > 0:
+                w = min(left, 100)
+                labels["k%d_%d" % (i, j)] = "y"
+                terms.append({"weight": w, "preference": {"matchExpressions": [
+                    {"key": "k%d_%d" % (i, j), "operator": "In", "values": ["y"]}]}})
+                left -= w
+                j += 1
+            meta["labels"] = labels
+        nodes.append({"metadata": meta, "spec": spec, "status": {"allocatable": {}}})
+    pod = {"metadata": {"name": "p", "namespace": ""}, "spec": {}}
+    if terms:
+        pod["spec"]["affinity"] = {"nodeAffinity": {"preferredDuringSchedulingIgnoredDuringExecution": terms}}
+    return {"kind": "score", "plugin": "TaintToleration" if c["reverse"] else "NodeAffinity", "normalize": True,
+            "nodes": nodes, "pod": pod, "pods": [], "args": {}, "name": c["name"], "src": c["src"]}
+
+
 def soa_eval(c, backend):
+    if c["kind"] == "normalize":
+        return soa_eval(normalize_case(c), backend)
+    if c["kind"] == "broken_linear":
+        ps = [p for p, _ in c["expect_values"]]
+        if backend == "gpu":
+            node = {"metadata": {"name": "n0"}, "spec": {}, "status": {"allocatable": {"cpu": "1"}}}
+            fw = GpuFramework(Profile(filters=[], scores=[]), [node], [], device=0)
+            try:
+                vals = fw.engine.broken_linear(c["points"], ps)
+            finally:
+                fw.engine.close()
+        else:
+            from oracle import cref
+            vals = cref.broken_linear(c["points"], ps)
+        return {"values": [[p, v] for p, v in zip(ps, vals)]}
     if c["kind"] == "node_tree":
         return {"order": [api.name_of(n) for n in api.snapshot_order(c["nodes"])]}
     if c["kind"] == "node_tree_ops":

@@ -237,3 +237,16 @@ def test_many_pdbs_only_matching_ones_reach_the_engine(seed):
         checked += 1
     assert checked
     fw.engine.close()
+
+
+MIGHT_HELP = [c for c in load_golden("preemption") if c["kind"] == "preempt_might_help"]
+
+
+@pytest.mark.parametrize("case", MIGHT_HELP, ids=[c["name"][:60] for c in MIGHT_HELP])
+def test_golden_nodes_where_preemption_might_help(case):
+    """TestNodesWherePreemptionMightHelp (generic_scheduler_test.go) through the product's host step
+    (kgpu.framework.nodes_where_preemption_might_help), which Preempt uses to pick the nodes that get
+    potential victims."""
+    from kgpu.framework import nodes_where_preemption_might_help
+    got = nodes_where_preemption_might_help(case["node_names"], case["statuses"])
+    assert sorted(got) == case["expect_set"], (case["name"], got)

@@ -42,8 +42,9 @@ def test_pts_state_on_device(case):
     checked = 0
     for i, (max_skew, key, _sel) in enumerate(want["constraints"]):
         ki = nk.key(key)
-        if ki < 0:
+        if ki < 0:  # no node carries the key: no pair can be registered
             assert not pairs.get(key), (case["name"], key)
+            checked += 1
             continue
         D = len(nk.vals[ki].items)
         reg, cnt, scalar = fw.engine.pts_state(q[0], pc, kind, i, D)

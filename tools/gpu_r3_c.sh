@@ -14,6 +14,9 @@ step pytest_gpu timeout -k 10 700 python -u -m pytest tests -x -q -m gpu --timeo
   --durations=25 || exit 1
 step smoke timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" || exit 1
 step bench_default timeout -k 10 400 python -u bench.py || exit 1
+step trace_b timeout -k 10 180 python -u tools/phase_trace.py || exit 1
+step trace_c timeout -k 10 180 python -u tools/phase_trace_topo.py --config c || exit 1
+step trace_d timeout -k 10 180 python -u tools/phase_trace_topo.py --config d || exit 1
 cd /tmp
 step probe_osexit timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $O/probe_osexit -o run \
   -- python3 -u $R/tools/exit_probe.py kgpu $O/maps_osexit.txt --os-exit || exit 1
