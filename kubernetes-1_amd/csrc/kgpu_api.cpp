@@ -7,6 +7,7 @@
 // into the head of the next launch (kgpu_kernels.hip).  The host never waits between pods.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#include <dlfcn.h>
 
 #include <algorithm>
 #include <array>
@@ -26,6 +27,39 @@
 #include <vector>
 
 #include "kgpu_internal.h"
+
+// ---- RCCL, loaded on first use.  Only node sharding (kgpu_comm_unique_id / kgpu_comm_init) needs
+// it, so a one-GPU process never maps librccl: RCCL's own exit-time teardown then cannot run after a
+// profiler's finalization has shut the HSA runtime down (rocprofv3 runs faulted in exit handlers).
+namespace {
+struct Rccl {
+  decltype(&ncclGetUniqueId) GetUniqueId = nullptr;
+  decltype(&ncclCommInitRank) CommInitRank = nullptr;
+  decltype(&ncclCommDestroy) CommDestroy = nullptr;
+  decltype(&ncclAllGather) AllGather = nullptr;
+  decltype(&ncclAllReduce) AllReduce = nullptr;
+  decltype(&ncclGetErrorString) GetErrorString = nullptr;
+  bool ok = false;
+};
+const Rccl& rccl() {
+  static const Rccl r = [] {
+    Rccl x;
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_LOCAL);
+    if (!h) return x;
+    x.GetUniqueId = reinterpret_cast<decltype(x.GetUniqueId)>(dlsym(h, "ncclGetUniqueId"));
+    x.CommInitRank = reinterpret_cast<decltype(x.CommInitRank)>(dlsym(h, "ncclCommInitRank"));
+    x.CommDestroy = reinterpret_cast<decltype(x.CommDestroy)>(dlsym(h, "ncclCommDestroy"));
+    x.AllGather = reinterpret_cast<decltype(x.AllGather)>(dlsym(h, "ncclAllGather"));
+    x.AllReduce = reinterpret_cast<decltype(x.AllReduce)>(dlsym(h, "ncclAllReduce"));
+    x.GetErrorString = reinterpret_cast<decltype(x.GetErrorString)>(dlsym(h, "ncclGetErrorString"));
+    x.ok = x.GetUniqueId && x.CommInitRank && x.CommDestroy && x.AllGather && x.AllReduce && x.GetErrorString;
+    return x;
+  }();
+  return r;
+}
+}  // namespace
 
 using kgpu::BlkKey;
 using kgpu::BlkStat;
@@ -149,6 +183,8 @@ struct kgpu_ctx {
   const void* ds_ptr = nullptr;                    // ... into this dstate allocation (null: none)
   size_t stage_cap = 0;
   bool last_diag = false;
+  std::vector<int64_t> trace_wg_host;             // k_tbatch per-workgroup stamps of the last traced run
+  int32_t trace_wg_groups = 0;
   std::vector<hipEvent_t> ev_pool;
   // ---- topology state (kgpu_internal.h "topology plugins")
   std::map<std::vector<int64_t>, int> class_ids, tclass_ids;
@@ -177,7 +213,9 @@ struct kgpu_ctx {
   int64_t max_key_values = 1;
   // persistent topology runs (k_tbatch)
   bool tfast = true;                // KGPU_OPT_TOPO_PERSISTENT
-  DevBuf t_plans, t_plan_of, t_aux, t_looks, t_tabs, t_deltas, t_hists, t_sigs, t_regs, t_zero, abort_buf;
+  DevBuf t_tables, t_zero, abort_buf;
+  void* t_stage_host = nullptr;  // pinned staging of the runs' tables (bump-allocated, wraps after a sync)
+  size_t t_stage_cap = 0, t_stage_used = 0;
   // ---- node sharding (kgpu_comm_init): this context holds one contiguous slice of the
   // snapshot; per pod the shard winners (and normalize maxima) are all-gathered over RCCL
   ncclComm_t comm = nullptr;
@@ -350,8 +388,8 @@ int sync_prefer_union(kgpu_ctx* c) {
   uint64_t* d = static_cast<uint64_t*>(c->pref_x.p);
   if (TW) {
     HIP_OK(c, hipMemcpyAsync(d, c->prefer_union.data(), sizeof(uint64_t) * TW, hipMemcpyHostToDevice, c->stream));
-    const ncclResult_t r = ncclAllGather(d, d + TW, TW, ncclUint64, c->comm, c->stream);
-    if (r != ncclSuccess) return fail(c, KGPU_E_DEVICE, std::string("ncclAllGather: ") + ncclGetErrorString(r));
+    const ncclResult_t r = rccl().AllGather(d, d + TW, TW, ncclUint64, c->comm, c->stream);
+    if (r != ncclSuccess) return fail(c, KGPU_E_DEVICE, std::string("ncclAllGather: ") + rccl().GetErrorString(r));
   }
   std::vector<uint64_t> all(TW * (size_t)c->nranks);
   if (TW) HIP_OK(c, hipMemcpyAsync(all.data(), d + TW, sizeof(uint64_t) * all.size(), hipMemcpyDeviceToHost, c->stream));
@@ -1206,12 +1244,13 @@ void t_finish(TRun& tr) {
   tr.plans.swap(uniq);
 }
 
-// Upload a planned run and launch k_sig_init + k_hist_init + k_tbatch on the engine's stream.
+// Upload a planned run and launch k_tbatch_init + k_tbatch on the engine's stream.
 int run_tbatch(kgpu_ctx* c, TRun& tr, int first, int count, int64_t first_seq, int32_t assume, int per, int groups,
-               int geo, int32_t* abort_word, bool xg) {
+               int geo, int32_t* abort_word, bool xg, bool diag) {
   t_finish(tr);
   int rc;
   kgpu::TBatchArgs a{};
+  a.diag = diag ? 1 : 0;
   a.first = first;
   a.count = count;
   a.per = per;
@@ -1240,21 +1279,60 @@ int run_tbatch(kgpu_ctx* c, TRun& tr, int first, int count, int64_t first_seq, i
   const size_t N = (size_t)c->st.N;
   const size_t ew = (N + 31) / 32;
   for (size_t s = 0; s < tr.sigs.size(); ++s) tr.sigs[s].elig_word = (int32_t)(s * ew);
-  const kgpu::TPlan* dpl;
-  const int32_t* dax;
-  const kgpu::TLook* dlk;
-  const kgpu::TTab* dtb;
-  const kgpu::TDelta* ddl;
-  const kgpu::THist* dh;
-  const kgpu::TSig* dsg;
-  const kgpu::TReg* drg;
-  const int32_t* dpo;
-  if ((rc = upload_vec(c, c->t_plans, tr.plans, &dpl)) || (rc = upload_vec(c, c->t_aux, tr.aux.v, &dax)) ||
-      (rc = upload_vec(c, c->t_plan_of, tr.plan_of, &dpo)) ||
-      (rc = upload_vec(c, c->t_looks, tr.looks.v, &dlk)) || (rc = upload_vec(c, c->t_hists, tr.hists, &dh)) ||
-      (rc = upload_vec(c, c->t_tabs, tr.tabs.v, &dtb)) || (rc = upload_vec(c, c->t_deltas, tr.deltas.v, &ddl)) ||
-      (rc = upload_vec(c, c->t_sigs, tr.sigs, &dsg)) || (rc = upload_vec(c, c->t_regs, tr.regs, &drg)))
-    return rc;
+  // Every table of the run in one pinned block and ONE copy: a copy from pageable memory costs
+  // microseconds each, and nine of them dominated a one-pod (kgpu_schedule_one) run.  The pinned
+  // block is bump-allocated per run; it wraps only after a stream synchronize, so no staged bytes are
+  // overwritten before their copy ran.
+  size_t toff = 0;
+  auto place = [&](size_t bytes) {
+    const size_t o = toff;
+    toff += a16(std::max<size_t>(bytes, 16));
+    return o;
+  };
+  const size_t o_pl = place(sizeof(kgpu::TPlan) * tr.plans.size()), o_ax = place(sizeof(int32_t) * tr.aux.v.size()),
+               o_po = place(sizeof(int32_t) * tr.plan_of.size()), o_lk = place(sizeof(kgpu::TLook) * tr.looks.v.size()),
+               o_h = place(sizeof(kgpu::THist) * tr.hists.size()), o_tb = place(sizeof(kgpu::TTab) * tr.tabs.v.size()),
+               o_dl = place(sizeof(kgpu::TDelta) * tr.deltas.v.size()), o_sg = place(sizeof(kgpu::TSig) * tr.sigs.size()),
+               o_rg = place(sizeof(kgpu::TReg) * tr.regs.size());
+  const size_t tbytes = toff;
+  if (c->t_stage_used + tbytes > c->t_stage_cap) {
+    HIP_OK(c, hipStreamSynchronize(c->stream));
+    c->t_stage_used = 0;
+    if (tbytes > c->t_stage_cap) {
+      if (c->t_stage_host) (void)hipHostFree(c->t_stage_host);
+      c->t_stage_host = nullptr;
+      c->t_stage_cap = 0;
+      const size_t cap = std::max<size_t>(tbytes * 2, 1 << 20);
+      HIP_OK(c, hipHostMalloc(&c->t_stage_host, cap, hipHostMallocDefault));
+      c->t_stage_cap = cap;
+    }
+  }
+  char* th = static_cast<char*>(c->t_stage_host) + c->t_stage_used;
+  auto stage = [&](size_t o, const auto& v) {
+    if (!v.empty()) std::memcpy(th + o, v.data(), sizeof(v[0]) * v.size());
+  };
+  stage(o_pl, tr.plans);
+  stage(o_ax, tr.aux.v);
+  stage(o_po, tr.plan_of);
+  stage(o_lk, tr.looks.v);
+  stage(o_h, tr.hists);
+  stage(o_tb, tr.tabs.v);
+  stage(o_dl, tr.deltas.v);
+  stage(o_sg, tr.sigs);
+  stage(o_rg, tr.regs);
+  if ((rc = ensure(c, c->t_tables, tbytes))) return rc;
+  HIP_OK(c, hipMemcpyAsync(c->t_tables.p, th, tbytes, hipMemcpyHostToDevice, c->stream));
+  c->t_stage_used += tbytes;
+  const char* td = static_cast<const char*>(c->t_tables.p);
+  const kgpu::TPlan* dpl = reinterpret_cast<const kgpu::TPlan*>(td + o_pl);
+  const int32_t* dax = reinterpret_cast<const int32_t*>(td + o_ax);
+  const int32_t* dpo = reinterpret_cast<const int32_t*>(td + o_po);
+  const kgpu::TLook* dlk = reinterpret_cast<const kgpu::TLook*>(td + o_lk);
+  const kgpu::THist* dh = reinterpret_cast<const kgpu::THist*>(td + o_h);
+  const kgpu::TTab* dtb = reinterpret_cast<const kgpu::TTab*>(td + o_tb);
+  const kgpu::TDelta* ddl = reinterpret_cast<const kgpu::TDelta*>(td + o_dl);
+  const kgpu::TSig* dsg = reinterpret_cast<const kgpu::TSig*>(td + o_sg);
+  const kgpu::TReg* drg = reinterpret_cast<const kgpu::TReg*>(td + o_rg);
   a.plans = dpl;
   a.plan_of = dpo;
   a.aux = dax;
@@ -1282,15 +1360,20 @@ int run_tbatch(kgpu_ctx* c, TRun& tr, int first, int count, int64_t first_seq, i
   a.abort = abort_word;
   a.abort_at = c->abort_at >= first && c->abort_at < first + count ? c->abort_at - first : -1;
   a.trace = nullptr;
+  a.trace_wg = nullptr;
   if (c->phase_trace) {
-    if ((rc = ensure(c, c->trace, sizeof(int64_t) * 16 * (size_t)(count + 1)))) return rc;
-    HIP_OK(c, hipMemsetAsync(c->trace.p, 0, sizeof(int64_t) * 16 * (size_t)(count + 1), c->stream));
+    const size_t tw = 16 * (size_t)(count + 1), ww = (size_t)count * (size_t)groups * 4;
+    if ((rc = ensure(c, c->trace, sizeof(int64_t) * (tw + ww)))) return rc;
+    HIP_OK(c, hipMemsetAsync(c->trace.p, 0, sizeof(int64_t) * (tw + ww), c->stream));
     a.trace = static_cast<int64_t*>(c->trace.p);
-    c->trace_host.assign((size_t)(count + 1) * 16, 0);
+    a.trace_wg = a.trace + tw;
+    c->trace_host.assign(tw, 0);
+    c->trace_wg_host.assign(ww, 0);
+    c->trace_wg_groups = groups;
   }
   const DevState* dst = static_cast<const DevState*>(c->dstate.p);
   if (kgpu::launch_tbatch_init(dst, a, groups, c->stream))
-    return fail(c, KGPU_E_DEVICE, "k_sig_init / k_hist_init launch failed");
+    return fail(c, KGPU_E_DEVICE, "k_tbatch_init launch failed");
   if (xg) {
     // node-sharded run: cluster-wide histograms from every rank's partial, then the
     // XG kernel exchanges one record per rank per pod through the topology ring
@@ -1314,9 +1397,12 @@ int run_tbatch(kgpu_ctx* c, TRun& tr, int first, int count, int64_t first_seq, i
   }
   if (kgpu::launch_tbatch(dst, a, groups, geo, c->spec, xg, c->stream))
     return fail(c, KGPU_E_DEVICE, std::string("k_tbatch launch failed: ") + hipGetErrorString(hipGetLastError()));
-  if (a.trace)
+  if (a.trace) {
     HIP_OK(c, hipMemcpyAsync(c->trace_host.data(), a.trace, sizeof(int64_t) * 16 * (size_t)(count + 1),
                              hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(c, hipMemcpyAsync(c->trace_wg_host.data(), a.trace_wg, sizeof(int64_t) * c->trace_wg_host.size(),
+                             hipMemcpyDeviceToHost, c->stream));
+  }
   return KGPU_OK;
 }
 
@@ -1478,9 +1564,11 @@ int stage_topology(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_
     const kgpu::TermClassRec* dtc;
     const kgpu_req* dcr;
     const int32_t* dcint;
-    if ((rc = upload_vec(c, c->d_classes, c->classes, &dcl)) || (rc = upload_vec(c, c->d_citems, c->citems, &dci)) ||
-        (rc = upload_vec(c, c->d_tclasses, c->tclasses, &dtc)) || (rc = upload_vec(c, c->d_creqs, c->creqs, &dcr)) ||
-        (rc = upload_vec(c, c->d_cints, c->cints, &dcint)))
+    // the class tables only grow: re-sent when they changed since the last cycle (upload_pool)
+    auto up = [&](DevBuf& b, const auto& v, auto** d) { return upload_pool(c, b, v.data(), (int32_t)v.size(), d); };
+    if ((rc = up(c->d_classes, c->classes, &dcl)) || (rc = up(c->d_citems, c->citems, &dci)) ||
+        (rc = up(c->d_tclasses, c->tclasses, &dtc)) || (rc = up(c->d_creqs, c->creqs, &dcr)) ||
+        (rc = up(c->d_cints, c->cints, &dcint)))
       return rc;
     c->st.classes = dcl;
     c->st.class_items = dci;
@@ -1682,11 +1770,11 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
     if (kgpu::launch_shard_pack(dst, parity, blocks, what, c->stream))
       return fail(c, KGPU_E_DEVICE, "k_shard_pack launch failed");
     const ncclResult_t r =
-        what == 0 ? ncclAllGather(c->st.shard_send_key, c->st.shard_keys + (size_t)parity * kgpu::kMaxRanks,
+        what == 0 ? rccl().AllGather(c->st.shard_send_key, c->st.shard_keys + (size_t)parity * kgpu::kMaxRanks,
                                   sizeof(BlkKey) / 8, ncclUint64, c->comm, c->stream)
-                  : ncclAllGather(c->st.shard_send_stat, c->st.shard_stats + (size_t)parity * kgpu::kMaxRanks,
+                  : rccl().AllGather(c->st.shard_send_stat, c->st.shard_stats + (size_t)parity * kgpu::kMaxRanks,
                                   sizeof(BlkStat) / 4, ncclInt32, c->comm, c->stream);
-    if (r != ncclSuccess) return fail(c, KGPU_E_DEVICE, std::string("ncclAllGather: ") + ncclGetErrorString(r));
+    if (r != ncclSuccess) return fail(c, KGPU_E_DEVICE, std::string("ncclAllGather: ") + rccl().GetErrorString(r));
     return KGPU_OK;
   };
   bool used_persistent = false;
@@ -1697,7 +1785,9 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
   int tper = 0, tgroups = 0;
   // node-sharded engines take the persistent topology kernel over the xGMI mailboxes (the XG
   // instantiation); without them, the per-pod RCCL pipeline
-  const int tgeo = (topo_on && c->tfast && !diag && (!sharded || xg) && !cut && !nom_dev && st.K <= 64)
+  // a diagnostic cycle (kgpu_schedule_one: status words and per-plugin scores) of one topology pod
+  // runs as a one-pod persistent run too
+  const int tgeo = (topo_on && c->tfast && (!diag || n == 1) && (!sharded || xg) && !cut && !nom_dev && st.K <= 64)
                        ? kgpu::tbatch_geometry(st.N, std::min(c->max_groups > 0 ? std::min(c->max_groups, c->n_cus) : c->n_cus, 256),
                                                &tper, &tgroups)
                        : -1;
@@ -1716,7 +1806,7 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
       while (j < n && topo[(size_t)j] && t_add(tr, c, qs[j], plans[(size_t)j], pp, aux, aux_terms, j)) ++j;
       if (j > i) {
         if (c->timing) HIP_OK(c, hipEventRecord(get_event(c, ev), c->stream));
-        if ((rc = run_tbatch(c, tr, i, j - i, first_seq, assume, tper, tgroups, tgeo, abort_word, xg))) return rc;
+        if ((rc = run_tbatch(c, tr, i, j - i, first_seq, assume, tper, tgroups, tgeo, abort_word, xg, diag))) return rc;
         if (c->timing) HIP_OK(c, hipEventRecord(get_event(c, ev + 1), c->stream));
         ev += 2;
         timed_passes += j - i;
@@ -1754,8 +1844,8 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
         int64_t* sc = c->st.scratch;
         auto ar = [&](void* buf, size_t cnt, ncclDataType_t t, ncclRedOp_t op) -> int {
           if (!cnt) return KGPU_OK;
-          const ncclResult_t r = ncclAllReduce(buf, buf, cnt, t, op, c->comm, c->stream);
-          return r == ncclSuccess ? KGPU_OK : fail(c, KGPU_E_DEVICE, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+          const ncclResult_t r = rccl().AllReduce(buf, buf, cnt, t, op, c->comm, c->stream);
+          return r == ncclSuccess ? KGPU_OK : fail(c, KGPU_E_DEVICE, std::string("ncclAllReduce: ") + rccl().GetErrorString(r));
         };
         auto phase = [&](int ph, int64_t extra) -> int {
           return kgpu::launch_topo_phase(dst, a, ph, blocks, extra, c->stream) ? fail(c, KGPU_E_DEVICE, "topology phase launch failed")
@@ -2699,9 +2789,8 @@ int kgpu_destroy(kgpu_ctx* c) try {
   for (DevBuf* b : {&c->dstate, &c->ticket, &c->queries, &c->reqs, &c->ints, &c->words, &c->node_terms, &c->pref_terms, &c->spreads,
                     &c->pod_terms, &c->scalars, &c->ports, &c->results, &c->gran, &c->trace, &c->d_classes,
                     &c->d_citems, &c->d_tclasses, &c->d_creqs, &c->d_cints, &c->d_plans, &c->d_aux,
-                    &c->d_aux_terms, &c->scratch, &c->d_pods, &c->gbar, &c->cut_buf, &c->t_plans, &c->t_aux,
-                    &c->t_looks, &c->t_tabs, &c->t_deltas, &c->t_hists, &c->t_sigs, &c->t_regs, &c->t_zero,
-                    &c->abort_buf, &c->t_plan_of, &c->flags_buf, &c->d_stage, &c->d_remap, &c->d_from,
+                    &c->d_aux_terms, &c->scratch, &c->d_pods, &c->gbar, &c->cut_buf, &c->t_tables, &c->t_zero,
+                    &c->abort_buf, &c->flags_buf, &c->d_stage, &c->d_remap, &c->d_from,
                     &c->p_args, &c->p_voff, &c->p_veff, &c->p_noff, &c->p_neff, &c->p_aux, &c->p_vrecs,
                     &c->p_vsc, &c->p_vports, &c->p_nrecs, &c->p_nsc, &c->p_nports, &c->p_vstate, &c->p_order,
                     &c->p_out, &c->p_outv, &c->p_prep, &c->p_nomstat, &c->p_pdb, &c->xg_arr,
@@ -2713,11 +2802,12 @@ int kgpu_destroy(kgpu_ctx* c) try {
   if (c->xg_box.p) (void)hipFree(c->xg_box.p);
   if (c->stage_host) (void)hipHostFree(c->stage_host);
   if (c->cyc_host) (void)hipHostFree(c->cyc_host);
+  if (c->t_stage_host) (void)hipHostFree(c->t_stage_host);
   if (c->res_pin) (void)hipHostFree(c->res_pin);
   if (c->st.mcnt) (void)hipFree(c->st.mcnt);
   if (c->st.tcnt) (void)hipFree(c->st.tcnt);
   if (c->shard.p) (void)hipFree(c->shard.p);
-  if (c->comm) (void)ncclCommDestroy(c->comm);
+  if (c->comm) (void)rccl().CommDestroy(c->comm);
   for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -2735,6 +2825,16 @@ int kgpu_read_phase_trace(kgpu_ctx* c, int64_t* out, int32_t max_pods) try {
   const int32_t n = std::min<int32_t>(max_pods, (int32_t)(c->trace_host.size() / 16));
   std::memcpy(out, c->trace_host.data(), sizeof(int64_t) * 16 * (size_t)n);
   return n;
+} catch (...) {
+  return on_exception(c, false);
+}
+
+int kgpu_debug_wg_trace(kgpu_ctx* c, int64_t* out, int64_t max_words, int32_t* groups) try {
+  if (!c || !out || !groups || max_words < 0) return KGPU_E_INVAL;
+  const size_t n = std::min<size_t>((size_t)max_words, c->trace_wg_host.size());
+  std::memcpy(out, c->trace_wg_host.data(), sizeof(int64_t) * n);
+  *groups = c->trace_wg_groups;
+  return (int)std::min<size_t>(n, INT32_MAX);
 } catch (...) {
   return on_exception(c, false);
 }
@@ -3436,8 +3536,9 @@ int kgpu_xgmi_init(kgpu_ctx* c, int32_t nranks, int32_t rank, const uint8_t* han
 int kgpu_comm_unique_id(uint8_t id[128]) try {
   if (!id) return KGPU_E_INVAL;
   static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId is 128 bytes");
+  if (!rccl().ok) return KGPU_E_UNSUPPORTED;  // librccl could not be loaded
   ncclUniqueId u;
-  if (ncclGetUniqueId(&u) != ncclSuccess) return KGPU_E_DEVICE;
+  if (rccl().GetUniqueId(&u) != ncclSuccess) return KGPU_E_DEVICE;
   std::memcpy(id, &u, 128);
   return KGPU_OK;
 } catch (...) {
@@ -3454,12 +3555,13 @@ int kgpu_comm_init(kgpu_ctx* c, int32_t nranks, int32_t rank, const uint8_t id[1
   ncclUniqueId u;
   std::memcpy(&u, id, 128);
   ncclComm_t comm = nullptr;
-  const ncclResult_t r = ncclCommInitRank(&comm, nranks, u, rank);
-  if (r != ncclSuccess) return fail(c, KGPU_E_DEVICE, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+  if (!rccl().ok) return fail(c, KGPU_E_UNSUPPORTED, "librccl could not be loaded");
+  const ncclResult_t r = rccl().CommInitRank(&comm, nranks, u, rank);
+  if (r != ncclSuccess) return fail(c, KGPU_E_DEVICE, std::string("ncclCommInitRank: ") + rccl().GetErrorString(r));
   const size_t bytes = sizeof(BlkKey) + sizeof(BlkStat) + 2 * kgpu::kMaxRanks * (sizeof(BlkKey) + sizeof(BlkStat));
   int rc;
   if ((rc = ensure(c, c->shard, bytes))) {
-    (void)ncclCommDestroy(comm);
+    (void)rccl().CommDestroy(comm);
     return rc;
   }
   HIP_OK(c, hipMemset(c->shard.p, 0, bytes));
@@ -3483,14 +3585,14 @@ int kgpu_comm_init(kgpu_ctx* c, int32_t nranks, int32_t rank, const uint8_t id[1
     if ((rc = ensure(c, tmp, 64 + 64 * (size_t)nranks + 64))) return rc;
     uint8_t* d = static_cast<uint8_t*>(tmp.p);
     HIP_OK(c, hipMemcpy(d, mine.data(), 64, hipMemcpyHostToDevice));
-    ncclResult_t nr = ncclAllGather(d, d + 64, 64, ncclUint8, comm, c->stream);
+    ncclResult_t nr = rccl().AllGather(d, d + 64, 64, ncclUint8, comm, c->stream);
     if (nr == ncclSuccess) HIP_OK(c, hipStreamSynchronize(c->stream));
     if (nr == ncclSuccess) HIP_OK(c, hipMemcpy(all.data(), d + 64, 64 * (size_t)nranks, hipMemcpyDeviceToHost));
     if (nr != ncclSuccess) ok = 0;
     if (ok && kgpu_xgmi_init(c, nranks, rank, all.data()) != KGPU_OK) ok = 0;
     int32_t* flag = reinterpret_cast<int32_t*>(d + 64 + 64 * (size_t)nranks);
     HIP_OK(c, hipMemcpy(flag, &ok, sizeof(int32_t), hipMemcpyHostToDevice));
-    nr = ncclAllReduce(flag, flag, 1, ncclInt32, ncclMin, comm, c->stream);
+    nr = rccl().AllReduce(flag, flag, 1, ncclInt32, ncclMin, comm, c->stream);
     if (nr == ncclSuccess) HIP_OK(c, hipStreamSynchronize(c->stream));
     int32_t all_ok = 0;
     if (nr == ncclSuccess) HIP_OK(c, hipMemcpy(&all_ok, flag, sizeof(int32_t), hipMemcpyDeviceToHost));

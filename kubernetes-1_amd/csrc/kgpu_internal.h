@@ -377,7 +377,7 @@ struct TBatchArgs {
   int32_t soft_words, zones;
   const TSig* sigs;
   const TReg* regs;
-  int32_t* hist_init;     // [lds_bins] zeroed, filled by k_hist_init
+  int32_t* hist_init;     // [lds_bins] zeroed, filled by k_tbatch_init
   int32_t* tot_init;      // [n_hists]
   uint32_t* reg_init;     // [reg_words]
   int32_t* sig_any;       // [n_sigs]
@@ -392,9 +392,13 @@ struct TBatchArgs {
   int32_t o_reg, o_tot, o_sany, o_stat, o_smask, o_zsum, o_wred, o_misc, o_pt, o_lab;
   int32_t lab_keys;       // node label keys cached in LDS per workgroup ([lab_keys][per] value ids)
   int32_t abort_at;       // KGPU_OPT_ABORT_AT test hook (-1: never), as in BatchArgs
+  int32_t diag;           // kgpu_schedule_one: status word and per-plugin raw / normalized scores of every
+                          // node (the run is one pod; the host zeroed the diagnostic rows)
   int64_t* trace;        // null, or [count + 1][16] s_memrealtime stamps (KGPU_OPT_PHASE_TRACE): per pod
                           // and traced workgroup (0, last): start, PreFilter minima, rows evaluated,
                           // stats published, stats resolved, key published, winner resolved, end
+  int64_t* trace_wg;      // null, or [count][groups][4] stamps of EVERY workgroup (thread 0): pod start,
+                          // rows done (wave 0), statistics published, key published
   // ---- node sharding over xGMI (the XG instantiation; kgpu_xgmi_init).  Each rank runs the local
   // protocol above over its own shard, then one record per rank crosses the ranks through the
   // topology mailbox ring (TX row, below): its combined statistics (published by workgroup 0) and its
@@ -512,10 +516,10 @@ int launch_class_init(const DevState* st, int c0, int nc, int n_pods, void* stre
 int launch_debug_broken_linear(const kgpu_shape_point* pts, int n_pts, const int64_t* p, int64_t* out, int n,
                                void* stream);
 int launch_topo_phase(const DevState* st, const PodArgs& a, int phase, int blocks, int64_t extra, void* stream);
-// Persistent topology run: signature bitmaps + pair registrations (k_sig_init), histogram
-// initialization from the match-count columns (k_hist_init), then k_tbatch.  kidx: geometry.
+// Persistent topology run: signature bitmaps + pair registrations and histogram
+// initialization from the match-count columns (k_tbatch_init), then k_tbatch.  kidx: geometry.
 int tbatch_geometry(int N, int max_groups, int* per, int* groups);
-// k_sig_init + k_hist_init over the local nodes (a.per * groups >= N); then, on a node-sharded
+// k_tbatch_init over the local nodes (a.per * groups >= N); then, on a node-sharded
 // engine, launch_xreduce over the init region; then launch_tbatch (xg: the XG instantiation).
 int launch_tbatch_init(const DevState* st, const TBatchArgs& a, int groups, void* stream);
 int launch_tbatch(const DevState* st, const TBatchArgs& a, int groups, int geo, int spec, bool xg, void* stream);

@@ -2289,18 +2289,28 @@ __device__ __forceinline__ bool tb_elig(const TBatchArgs& ta, int sig, int n) {
   return (gp(ta.elig)[sg.elig_word + (n >> 5)] >> (n & 31)) & 1u;
 }
 
-// signature bitmaps (nodes a pod's nodeSelector / required NodeAffinity admits that carry every
-// key of the signature: filtering.go:229-238, scoring.go:143-150) and the DoNotSchedule pair
-// registrations of each (signature, key) (filtering.go:239-243).
-__global__ void k_sig_init(const DevState* __restrict__ stp, TBatchArgs ta) {
+// One pass per node at the start of a run:
+//  * signature bitmaps: nodes a pod's nodeSelector / required NodeAffinity admits that carry every key
+//    of the signature (filtering.go:229-238, scoring.go:143-150), and the DoNotSchedule pair
+//    registrations of each (signature, key) (filtering.go:239-243);
+//  * domain histograms (and their totals over the nodes carrying the key) from the columns, counted
+//    only over the nodes the histogram's signature admits -- read from the node's own bits in a
+//    register (a run has at most 64 signatures), not back from the bitmap.
+__device__ __forceinline__ const int32_t* tb_col(const DevState& st, const THist& h) {
+  return (h.col_kind == 0 ? st.mcnt : st.tcnt) + (size_t)h.col * st.N;
+}
+
+__global__ void k_tbatch_init(const DevState* __restrict__ stp, TBatchArgs ta) {
   const DevState& st = *stp;
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
   if (n >= st.N) return;
+  uint64_t em = 0;
   for (int s = 0; s < ta.n_sigs; ++s) {
     const TSig sg = cp(ta.sigs)[s];
     bool ok = sg.n_keys >= 0 && node_affinity_ok(st, *cp(st.queries + sg.rep), n);
     for (int k = 0; k < sg.n_keys && ok; ++k) ok = sg.keys[k] >= 0 && gp(st.label_val)[(size_t)sg.keys[k] * st.N + n] >= 0;
     if (!ok) continue;
+    em |= 1ull << s;
     atomicOr(gp(ta.elig) + sg.elig_word + (n >> 5), 1u << (n & 31));
     __hip_atomic_store(gp(ta.sig_any) + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (int r = 0; r < ta.n_regs; ++r) {
@@ -2310,22 +2320,11 @@ __global__ void k_sig_init(const DevState* __restrict__ stp, TBatchArgs ta) {
       atomicOr(gp(ta.reg_init) + rg.word + (v >> 5), 1u << (v & 31));
     }
   }
-}
-
-__device__ __forceinline__ const int32_t* tb_col(const DevState& st, const THist& h) {
-  return (h.col_kind == 0 ? st.mcnt : st.tcnt) + (size_t)h.col * st.N;
-}
-
-// domain histograms (and their totals over the nodes carrying the key) from the columns
-__global__ void k_hist_init(const DevState* __restrict__ stp, TBatchArgs ta) {
-  const DevState& st = *stp;
-  const int n = blockIdx.x * blockDim.x + threadIdx.x;
-  if (n >= st.N) return;
   for (int i = 0; i < ta.n_hists; ++i) {
     const THist h = cp(ta.hists)[i];
     const int c = gp(tb_col(st, h))[n];
     if (!c) continue;
-    if (h.sig >= 0 && !tb_elig(ta, h.sig, n)) continue;
+    if (h.sig >= 0 && !((em >> h.sig) & 1u)) continue;
     const int v = h.key >= 0 ? gp(st.label_val)[(size_t)h.key * st.N + n] : -1;
     if (h.off >= 0) atomicAdd(gp(ta.hist_init) + h.off + (v >= 0 ? v : h.D), c);
     if (v >= 0) atomicAdd(gp(ta.tot_init) + i, c);
@@ -2465,7 +2464,7 @@ constexpr uint32_t kTopoSM = (1u << KGPU_S_POD_TOPOLOGY_SPREAD) | (1u << KGPU_S_
 // caller adds it), not from the columns.
 template <uint32_t SM, bool kDef>
 __device__ __forceinline__ void tscores(const DevState& st, const kgpu_pod_query& q, const NodeRes& r, int n, NodeEval& e,
-                                        bool reg_taint) {
+                                        bool reg_taint, bool diag) {
   if constexpr (SM == kRuntime) {
     int64_t p = 0;
     for (int si = 0; si < st.n_scores; ++si) {
@@ -2473,12 +2472,13 @@ __device__ __forceinline__ void tscores(const DevState& st, const kgpu_pod_query
       if ((kTopoSM >> s) & 1u) continue;
       if (s == KGPU_S_TAINT_TOLERATION && reg_taint) continue;
       const int64_t v = score_one<kDef>(s, st, q, r, n, e);
+      if (diag) gp(st.diag_raw)[(size_t)s * st.N + n] = v;
       if (!normalized(s)) p += v * cp(st.w_of)[s];
     }
     e.partial = p;
   } else {
-    if (reg_taint) run_scores<SM & ~kTopoSM & ~(1u << KGPU_S_TAINT_TOLERATION)>(st, q, r, n, e, false);
-    else run_scores<SM & ~kTopoSM>(st, q, r, n, e, false);
+    if (reg_taint) run_scores<SM & ~kTopoSM & ~(1u << KGPU_S_TAINT_TOLERATION)>(st, q, r, n, e, diag);
+    else run_scores<SM & ~kTopoSM>(st, q, r, n, e, diag);
   }
 }
 
@@ -2499,7 +2499,7 @@ template <uint32_t FM, uint32_t SM, bool kDef>
 __device__ __forceinline__ uint32_t trow_eval(const DevState& st, const TBatchArgs& ta, const kgpu_pod_query& q,
                                          const TPlan& tp, const NodeRes& r, int n, const int32_t* H,
                                          const int64_t* PT, const TMisc& M, bool pany, bool aff_any,
-                                         const int32_t* LAB, int li, const TStatic& sr, TRow& o) {
+                                         const int32_t* LAB, int li, const TStatic& sr, TRow& o, bool diag) {
   // node label value ids from the workgroup's LDS copy (keys < lab_keys), else from the column
   auto nval = [&](int key) -> int {
     if (key < 0) return -1;
@@ -2541,7 +2541,7 @@ __device__ __forceinline__ uint32_t trow_eval(const DevState& st, const TBatchAr
     return 0;
   };
   // NodeAffinity (node_affinity.go:53-62): the pod's selector program was evaluated once per run for
-  // every node (k_sig_init); here it is one bit
+  // every node (k_tbatch_init); here it is one bit
   auto one = [&](int f) -> uint32_t {
     if (f == KGPU_F_POD_TOPOLOGY_SPREAD) return pts();
     if (f == KGPU_F_INTER_POD_AFFINITY) return ipa();
@@ -2577,12 +2577,13 @@ __device__ __forceinline__ uint32_t trow_eval(const DevState& st, const TBatchAr
   }
   if (status) return status;
   NodeEval e{0, 0, 0, 0};
-  tscores<SM, kDef>(st, q, r, n, e, st.TW <= 2);
+  tscores<SM, kDef>(st, q, r, n, e, st.TW <= 2, diag);
   if (st.TW <= 2 && st.w_of[KGPU_S_TAINT_TOLERATION] && st.any_prefer_taint) {  // taint_toleration.go:123-152
     for (int w = 0; w < st.TW; ++w) {
       const uint64_t tol = w < q.tol_prefer.count ? cp(st.qp.words)[q.tol_prefer.begin + w] : 0ull;
       e.taint += __popcll(sr.tpr[w] & ~tol);
     }
+    if (diag) gp(st.diag_raw)[(size_t)KGPU_S_TAINT_TOLERATION * st.N + n] = e.taint;
   }
   o.part = e.partial;
   o.taint = e.taint;
@@ -2676,8 +2677,11 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
   int64_t* trow = ta.trace ? ta.trace + (g == 0 ? 0 : 8) : nullptr;
 #define KGPU_TSTAMP(k) \
   if (trc) trow[(size_t)i * 16 + (k)] = (int64_t)__builtin_amdgcn_s_memrealtime()
+#define KGPU_WSTAMP(k) \
+  if (ta.trace_wg && tid == 0) ta.trace_wg[((size_t)i * G + g) * 4 + (k)] = (int64_t)__builtin_amdgcn_s_memrealtime()
   for (int i = 0; i < ta.count; ++i) {
     KGPU_TSTAMP(0);
+    KGPU_WSTAMP(0);
     if (i == ta.abort_at && g == 0 && tid == 0) __hip_atomic_store(ta.abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int pod = ta.first + i;
     if (wave == W - 1 && i + 1 < ta.count && lane < (int)(sizeof(kgpu_pod_query) / 16)) {
@@ -2730,8 +2734,10 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
       const int n = lo + j * B + tid;
       feas[j] = false;
       if (n >= st.N) continue;
-      if (trow_eval<FM, SM, kDef>(st, ta, q, tp, r[j], n, H, PT, M, pany, aff_any, LAB, j * B + tid, sr[j], o[j]))
-        continue;
+      const uint32_t sw =
+          trow_eval<FM, SM, kDef>(st, ta, q, tp, r[j], n, H, PT, M, pany, aff_any, LAB, j * B + tid, sr[j], o[j], ta.diag);
+      if (ta.diag) gp(st.status)[n] = sw;  // kgpu_schedule_one: the cycle's Filter verdicts
+      if (sw) continue;
       feas[j] = true;
       ++sf;
       smaxT = max(smaxT, (uint32_t)o[j].taint);
@@ -2755,6 +2761,7 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
       }
     }
     KGPU_TSTAMP(2);
+    KGPU_WSTAMP(1);
     // ---- statistics round: wave reductions (DPP), workgroup (LDS atomics), granules, every workgroup
     sf = wave_sum32(sf);
     smaxT = wave_max32u(smaxT);
@@ -2810,6 +2817,7 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
       store_sc1(srow + (size_t)tid * G + g, enc_stat(x));
     }
     KGPU_TSTAMP(3);
+    KGPU_WSTAMP(2);
     bool ok = true;
     // XG: this pod's TX row and record tag (ring lap in bits 60-62)
     uint64_t* txrow = nullptr;
@@ -2909,6 +2917,26 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
       if (st.n_scores == 0) total = 1;
       const uint64_t key = ((uint64_t)(total + 1) << 40) | rank40(tk, (uint64_t)(st.node_base + n), st.tie_mode);
       if (key > bkey) { bkey = key; bidx = j * B + tid; }
+      if (ta.diag) {  // per-plugin raw and normalized scores of the cycle (as k_topo_score / k_topo_final)
+        const size_t N = (size_t)st.N;
+        gp(st.diag_raw)[KGPU_S_POD_TOPOLOGY_SPREAD * N + n] =
+            (o[j].adj == INT64_MIN || !tp.n_soft) ? 0 : (int64_t)((double)o[j].adj * wsoft);
+        gp(st.diag_raw)[KGPU_S_INTER_POD_AFFINITY * N + n] = o[j].ipa;
+        gp(st.diag_raw)[KGPU_S_DEFAULT_POD_TOPOLOGY_SPREAD * N + n] = tp.dpts_cls == -2 ? 0 : o[j].ds;
+        for (int si = 0; si < st.n_scores; ++si) {
+          const int s = cp(st.scores)[si];
+          int64_t v;
+          switch (s) {
+            case KGPU_S_TAINT_TOLERATION: v = vt; break;
+            case KGPU_S_NODE_AFFINITY: v = vn; break;
+            case KGPU_S_POD_TOPOLOGY_SPREAD: v = vp; break;
+            case KGPU_S_INTER_POD_AFFINITY: v = vi; break;
+            case KGPU_S_DEFAULT_POD_TOPOLOGY_SPREAD: v = vd; break;
+            default: v = gp(st.diag_raw)[(size_t)s * N + n];
+          }
+          gp(st.diag_norm)[(size_t)s * N + n] = v;
+        }
+      }
     }
     wave_argmax(bkey, bidx);
     if (lane == 0) {
@@ -2923,6 +2951,7 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
       wave_argmax(bk, bi);
       if (lane == 0) store_sc1(arow + g, kGValid | bk);
       KGPU_TSTAMP(5);
+      KGPU_WSTAMP(3);
       uint64_t wkey = 0;
       int wg = -1;
       bool pok = poll_row<4, false>(arow, G, ta.abort, kGValid, kGValid, wkey, wg);
@@ -3046,11 +3075,12 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
     KGPU_TSTAMP(7);
   }
 #undef KGPU_TSTAMP
+#undef KGPU_WSTAMP
 }
 
 // ---------------------------------------------------------------- cross-rank init reduction
 // A node-sharded persistent topology run starts from cluster-wide histograms: every rank's partial
-// (k_hist_init over its own nodes) is summed -- and its pair registrations / signature flags OR-ed --
+// (k_tbatch_init over its own nodes) is summed -- and its pair registrations / signature flags OR-ed --
 // over the ranks through the init mailbox (kgpu_internal.h XReduce).  Three launches on the stream:
 // k_xput copies the partial into every rank's mailbox slot of this rank, k_xflag raises this rank's
 // arrival flag everywhere after a system-scope release, k_xsum waits for every rank's flag and reduces
@@ -3162,8 +3192,7 @@ int launch_tbatch_init(const DevState* st, const TBatchArgs& a, int groups, void
   hipStream_t s = (hipStream_t)stream;
   const int N = a.per * groups;  // >= st->N
   const int nb = (N + 255) / 256;
-  hipLaunchKernelGGL(k_sig_init, dim3(nb), dim3(256), 0, s, st, a);
-  hipLaunchKernelGGL(k_hist_init, dim3(nb), dim3(256), 0, s, st, a);
+  hipLaunchKernelGGL(k_tbatch_init, dim3(nb), dim3(256), 0, s, st, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -19,7 +19,8 @@ EXPORTS = ["kgpu_abi_version", "kgpu_struct_sizes", "kgpu_create", "kgpu_destroy
            "kgpu_get_filter", "kgpu_get_scores", "kgpu_forget_pod", "kgpu_read_nodes", "kgpu_set_option",
            "kgpu_read_phase_trace", "kgpu_comm_unique_id", "kgpu_comm_init", "kgpu_apply_delta",
            "kgpu_set_nominated", "kgpu_select_victims", "kgpu_xgmi_handle", "kgpu_xgmi_init", "kgpu_xgmi_active",
-           "kgpu_debug_fail_alloc", "kgpu_debug_pts_state", "kgpu_debug_broken_linear"]
+           "kgpu_debug_fail_alloc", "kgpu_debug_pts_state", "kgpu_debug_broken_linear",
+           "kgpu_debug_wg_trace"]
 
 
 class KgpuError(RuntimeError):
@@ -63,6 +64,7 @@ def lib():
     L.kgpu_debug_fail_alloc.argtypes = [i32]
     L.kgpu_debug_pts_state.argtypes = [vp, vp, C.POINTER(abi.Pools), i32, i32, vp, vp, C.POINTER(i64)]
     L.kgpu_debug_broken_linear.argtypes = [vp, vp, i32, vp, i32, vp]
+    L.kgpu_debug_wg_trace.argtypes = [vp, vp, i64, C.POINTER(i32)]
     L.kgpu_select_victims.argtypes = [vp, vp, C.POINTER(abi.Pools), C.POINTER(abi.PreemptArgs), vp, vp,
                                       C.POINTER(i32)]
     if L.kgpu_abi_version() != abi.ABI_VERSION:
@@ -217,6 +219,15 @@ class Engine:
         self._check(lib().kgpu_debug_pts_state(self.h, q.ctypes.data, C.byref(pools), kind, constraint,
                                                 reg.ctypes.data, cnt.ctypes.data, C.byref(out)))
         return reg[:n_values].astype(bool), cnt[:n_values], int(out.value)
+
+    def wg_trace(self, pods):
+        """kgpu_debug_wg_trace: [pods][groups][4] per-workgroup stamps of the last traced k_tbatch run."""
+        g = C.c_int32(0)
+        probe = np.zeros(1, np.int64)
+        lib().kgpu_debug_wg_trace(self.h, probe.ctypes.data, 0, C.byref(g))  # the run's workgroup count
+        out = np.zeros(max(pods * g.value * 4, 1), np.int64)
+        n = lib().kgpu_debug_wg_trace(self.h, out.ctypes.data, len(out), C.byref(g))
+        return out[:n].reshape(-1, g.value, 4) if g.value else out[:0].reshape(0, 0, 4)
 
     def broken_linear(self, points, utilizations):
         """kgpu_debug_broken_linear: the device's broken-linear shape function (the one

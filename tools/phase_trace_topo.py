@@ -46,6 +46,23 @@ def main():
         print("config %s %d nodes groups<=%d %s: per-pod %.0f ns | " % (args.config, args.nodes, args.groups, name,
                                                                        np.median(per)) +
               "  ".join("%s %.0f" % (k, np.median(v)) for k, v in ph.items()) + " (medians, ns)")
+    # every workgroup: when its rows were done and when it published its statistics / key, relative to
+    # the earliest pod start; the spread across workgroups is what the statistics / key waits pay
+    wt = eng.wg_trace(len(q)).astype(np.float64) * 10.0
+    if wt.size:
+        wt = wt[1:len(q) - 1]
+        t0 = wt[:, :, 0].min(axis=1, keepdims=True)
+        rows, spub, kpub = wt[:, :, 1] - t0, wt[:, :, 2] - t0, wt[:, :, 3] - t0
+        G = wt.shape[1]
+        print("per-workgroup medians over pods (ns after the earliest pod start), %d workgroups:" % G)
+        print("  rows done     " + " ".join("%5.0f" % x for x in np.median(rows, axis=0)))
+        print("  stats pub     " + " ".join("%5.0f" % x for x in np.median(spub, axis=0)))
+        print("  key pub       " + " ".join("%5.0f" % x for x in np.median(kpub, axis=0)))
+        print("  start         " + " ".join("%5.0f" % x for x in np.median(wt[:, :, 0] - t0, axis=0)))
+        last = np.argmax(spub, axis=1)
+        print("  last stats publisher: " + " ".join("%d:%d" % (gg, int((last == gg).sum())) for gg in range(G)))
+        print("  stats spread (max - min) median %.0f ns, key spread median %.0f ns" %
+              (np.median(spub.max(1) - spub.min(1)), np.median(kpub.max(1) - kpub.min(1))))
 
 
 if __name__ == "__main__":
