@@ -303,6 +303,7 @@ def main():
                     help="N=1, default workload: a second record, timed in the same run, of the same config at this "
                          "many nodes (BASELINE.json's metric is quoted at 5k and 100k nodes); 0: none")
     ap.add_argument("--extra-cpu-sample", type=int, default=1000, help="pods of the extra record's CPU baseline")
+    ap.add_argument("--reset-at-exit", action="store_true", help="hipDeviceReset() before exiting (profiling runs)")
     ap.add_argument("--os-exit", action="store_true",
                     help="leave through os._exit(0) after printing (profiling runs: see DESIGN.md, rocprofv3 exit)")
     args = ap.parse_args()
@@ -329,6 +330,11 @@ def main():
         print(json.dumps(line), flush=True)
     if dist_on:
         dist.destroy_process_group()
+    if args.reset_at_exit:
+        # profiling runs: release the HIP runtime's device state while rocprofv3's tool is attached (its
+        # finalization runs in an exit handler before HIP's own; see DESIGN.md "rocprofv3 at exit")
+        import ctypes
+        ctypes.CDLL("libamdhip64.so").hipDeviceReset()
     if args.os_exit:
         sys.stdout.flush()
         sys.stderr.flush()

@@ -636,8 +636,9 @@ int kgpu_debug_fail_alloc(int32_t countdown);
  * Replaces buildBrokenLinearFunction's direct use in requested_to_capacity_ratio_test.go:119
  * (pkg/scheduler/framework/plugins/noderesources/requested_to_capacity_ratio.go:150-170). */
 /* Diagnostic: the per-workgroup phase stamps of the last traced persistent topology run
- * (KGPU_OPT_PHASE_TRACE): [pods][groups][4] s_memrealtime ticks (pod start, rows done, statistics
- * published, key published); *groups = the run's workgroups.  Returns the words copied. */
+ * (KGPU_OPT_PHASE_TRACE): [pods][groups][8] s_memrealtime ticks (pod start, rows done, statistics
+ * published, key published, statistics reduced over the workgroup, statistics received, winner
+ * received, unused); *groups = the run's workgroups.  Returns the words copied. */
 int kgpu_debug_wg_trace(kgpu_ctx* ctx, int64_t* out, int64_t max_words, int32_t* groups);
 
 int kgpu_debug_broken_linear(kgpu_ctx* ctx, const kgpu_shape_point* points, int32_t n_points, const int64_t* p,

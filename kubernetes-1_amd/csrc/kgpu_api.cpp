@@ -993,8 +993,8 @@ size_t t_layout(const TRun& tr, kgpu::TBatchArgs* a, int B, int lab_keys = 0, in
   o = a16(o + (size_t)kgpu::kTMaxSoftWords * 4);
   const size_t o_zsum = o;
   o = a16(o + (size_t)std::max(tr.zones, 1) * 4);
-  const size_t o_wred = o;
-  o = a16(o + (size_t)(B / 64) * kgpu::kTFixed * 8);
+  const size_t o_gat = o;
+  o = a16(o + (size_t)64 * (size_t)R * 8);
   const size_t o_pt = o;
   o = a16(o + (size_t)std::max(tr.pt_max, 1) * 8);
   const size_t o_misc = o;
@@ -1010,7 +1010,7 @@ size_t t_layout(const TRun& tr, kgpu::TBatchArgs* a, int B, int lab_keys = 0, in
     a->o_stat = (int32_t)o_stat;
     a->o_smask = (int32_t)o_smask;
     a->o_zsum = (int32_t)o_zsum;
-    a->o_wred = (int32_t)o_wred;
+    a->o_gat = (int32_t)o_gat;
     a->o_pt = (int32_t)o_pt;
     a->o_misc = (int32_t)o_misc;
     a->R = R;
@@ -1362,7 +1362,7 @@ int run_tbatch(kgpu_ctx* c, TRun& tr, int first, int count, int64_t first_seq, i
   a.trace = nullptr;
   a.trace_wg = nullptr;
   if (c->phase_trace) {
-    const size_t tw = 16 * (size_t)(count + 1), ww = (size_t)count * (size_t)groups * 4;
+    const size_t tw = 16 * (size_t)(count + 1), ww = (size_t)count * (size_t)groups * 8;
     if ((rc = ensure(c, c->trace, sizeof(int64_t) * (tw + ww)))) return rc;
     HIP_OK(c, hipMemsetAsync(c->trace.p, 0, sizeof(int64_t) * (tw + ww), c->stream));
     a.trace = static_cast<int64_t*>(c->trace.p);

@@ -382,14 +382,15 @@ struct TBatchArgs {
   uint32_t* reg_init;     // [reg_words]
   int32_t* sig_any;       // [n_sigs]
   uint32_t* elig;         // [n_sigs][ceil(N/32)]
-  uint64_t* gran;         // [count][R + 1][groups] granules, zeroed before the launch
+  uint64_t* gran;         // per pod: [groups][R] statistics records, then [groups] key granules; zeroed
   int32_t* abort;
   int32_t lds_bytes;
   int32_t def_res;        // Least/Most over {cpu: 1, memory: 1}
   int32_t pt_words;       // largest per-pod table area of the run (int64 words)
   int32_t n_keys;         // node label keys the run's deltas read (winner's labels staged in LDS)
   // byte offsets of the LDS regions (histogram bins start at 0)
-  int32_t o_reg, o_tot, o_sany, o_stat, o_smask, o_zsum, o_wred, o_misc, o_pt, o_lab;
+  int32_t o_reg, o_tot, o_sany, o_stat, o_smask, o_zsum, o_gat, o_misc, o_pt, o_lab;  // o_gat: [64][R] int64,
+                          // the statistics poll's per-lane partials
   int32_t lab_keys;       // node label keys cached in LDS per workgroup ([lab_keys][per] value ids)
   int32_t abort_at;       // KGPU_OPT_ABORT_AT test hook (-1: never), as in BatchArgs
   int32_t diag;           // kgpu_schedule_one: status word and per-plugin raw / normalized scores of every
@@ -397,8 +398,9 @@ struct TBatchArgs {
   int64_t* trace;        // null, or [count + 1][16] s_memrealtime stamps (KGPU_OPT_PHASE_TRACE): per pod
                           // and traced workgroup (0, last): start, PreFilter minima, rows evaluated,
                           // stats published, stats resolved, key published, winner resolved, end
-  int64_t* trace_wg;      // null, or [count][groups][4] stamps of EVERY workgroup (thread 0): pod start,
-                          // rows done (wave 0), statistics published, key published
+  int64_t* trace_wg;      // null, or [count][groups][8] stamps of EVERY workgroup (thread 0): pod start,
+                          // rows done (wave 0), statistics published, key published, every wave's
+                          // statistics reduced (barrier), statistics received, winner received
   // ---- node sharding over xGMI (the XG instantiation; kgpu_xgmi_init).  Each rank runs the local
   // protocol above over its own shard, then one record per rank crosses the ranks through the
   // topology mailbox ring (TX row, below): its combined statistics (published by workgroup 0) and its

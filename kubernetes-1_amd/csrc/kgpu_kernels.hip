@@ -2380,30 +2380,52 @@ struct TMisc {
   int64_t acc64[2];          // kTIpaMin, kTIpaMax
 };
 
-// Wave `w` polls statistics slots w, w + waves, ... of pod row `row`: every workgroup's granule
-// of the slot, combined with the slot's operation.  False on timeout / abort.
-__device__ __forceinline__ bool tpoll_slot(const uint64_t* row, int G, const int32_t* abort_word, int op,
-                                           int64_t& out) {
+// The statistics round of one pod, run by ONE wave (the other waves wait at the workgroup barrier,
+// so the polling CU's memory queue carries only this wave's loads): every workgroup published its R
+// slots as one record (row[g * R + slot]); lane l folds records l, l + 64, ... into its partials in
+// GAT[l][slot], then lane `slot` folds the 64 partials into STAT[slot].  False on timeout / abort.
+__device__ __forceinline__ int tslot_op(int rr, int soft_words) {
+  return rr < kTFixed ? tstat_op(rr) : (rr < kTFixed + soft_words ? kOpOr : kOpSum);
+}
+__device__ bool tstats_gather(const uint64_t* row, int G, int R, int soft_words, const int32_t* abort_word,
+                              int64_t* GAT, int64_t* STAT) {
   const int lane = threadIdx.x & 63;
+  int64_t* mine = GAT + lane * R;
+  if (lane >= G)
+    for (int rr = 0; rr < R; ++rr) mine[rr] = tident(tslot_op(rr, soft_words));
+  bool ok = true;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  for (;;) {
-    bool all = true;
-    int64_t acc = tident(op);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int g = lane + 64 * j;
-      if (g < G) {
-        const uint64_t v = load_sc1(row + g);
-        if (!(v & kGValid)) all = false;
-        else acc = tcombine(op, acc, dec_stat(v));
+  for (int gg = lane; gg < G && ok; gg += 64) {
+    const uint64_t* rec = row + (size_t)gg * R;
+    const bool first = gg < 64;
+    for (;;) {
+      // the first record of a lane decodes straight into its partials (overwritten until valid)
+      bool all = true;
+      for (int rr = 0; rr < R; ++rr) {
+        const uint64_t v = load_sc1(rec + rr);
+        all &= (v & kGValid) != 0;
+        if (first) mine[rr] = dec_stat(v);
       }
+      if (all) break;
+      if (load_sc1(abort_word) != 0 || __builtin_amdgcn_s_memrealtime() - t0 > kSpinTimeout) {
+        ok = false;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
     }
-    if (__all(all)) {
-      out = wave_op_i64(op, acc);
-      return true;
-    }
-    if (load_sc1(abort_word) != 0 || __builtin_amdgcn_s_memrealtime() - t0 > kSpinTimeout) return false;
+    if (!ok || first) continue;
+    for (int rr = 0; rr < R; ++rr)  // G > 64: later records fold in
+      mine[rr] = tcombine(tslot_op(rr, soft_words), mine[rr], dec_stat(load_sc1(rec + rr)));
   }
+  ok = __all(ok);
+  if (ok && lane < R) {
+    const int op = tslot_op(lane, soft_words);
+    int64_t acc = tident(op);
+    const int n = G < 64 ? G : 64;
+    for (int l = 0; l < n; ++l) acc = tcombine(op, acc, GAT[l * R + lane]);
+    STAT[lane] = acc;
+  }
+  return ok;
 }
 
 // ---- node sharding over xGMI (k_tbatch XG): the topology mailbox ring (kgpu_internal.h TX row)
@@ -2549,7 +2571,9 @@ __device__ __forceinline__ uint32_t trow_eval(const DevState& st, const TBatchAr
     if (f == KGPU_F_NODE_UNSCHEDULABLE)  // node_unschedulable.go:51-65
       return (sr.unsched && !(q.flags & KGPU_Q_TOLERATES_UNSCHEDULABLE)) ? KGPU_CODE_UNRESOLVABLE << 8 : 0;
     if (f == KGPU_F_TAINT_TOLERATION && st.TW <= 2) {  // taint_toleration.go:54-72
-      for (int w = 0; w < st.TW; ++w) {
+#pragma unroll
+      for (int w = 0; w < 2; ++w) {
+        if (w >= st.TW) break;
         const uint64_t tol = w < q.tol_nosched.count ? cp(st.qp.words)[q.tol_nosched.begin + w] : 0ull;
         if (sr.tns[w] & ~tol) return KGPU_CODE_UNRESOLVABLE << 8;
       }
@@ -2579,7 +2603,9 @@ __device__ __forceinline__ uint32_t trow_eval(const DevState& st, const TBatchAr
   NodeEval e{0, 0, 0, 0};
   tscores<SM, kDef>(st, q, r, n, e, st.TW <= 2, diag);
   if (st.TW <= 2 && st.w_of[KGPU_S_TAINT_TOLERATION] && st.any_prefer_taint) {  // taint_toleration.go:123-152
-    for (int w = 0; w < st.TW; ++w) {
+#pragma unroll
+    for (int w = 0; w < 2; ++w) {
+      if (w >= st.TW) break;
       const uint64_t tol = w < q.tol_prefer.count ? cp(st.qp.words)[q.tol_prefer.begin + w] : 0ull;
       e.taint += __popcll(sr.tpr[w] & ~tol);
     }
@@ -2635,6 +2661,7 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
   int32_t* ZSUM = reinterpret_cast<int32_t*>(lds_raw + ta.o_zsum);
   int64_t* PT = reinterpret_cast<int64_t*>(lds_raw + ta.o_pt);
   int32_t* LAB = reinterpret_cast<int32_t*>(lds_raw + ta.o_lab);  // [lab_keys][per] label value ids
+  int64_t* GAT = reinterpret_cast<int64_t*>(lds_raw + ta.o_gat);  // [64][R] statistics poll partials
   TMisc& M = *reinterpret_cast<TMisc*>(lds_raw + ta.o_misc);
   constexpr int W = B / 64;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -2666,7 +2693,10 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
       if constexpr (kDef) set_recips(r[j]);
       sr[j].unsched = gp(st.unsched)[n];
       sr[j].zone = gp(st.zone_id)[n];
-      for (int w = 0; w < st.TW && w < 2; ++w) {
+      // constant indices only: a dynamically indexed private array lives in scratch memory
+#pragma unroll
+      for (int w = 0; w < 2; ++w) {
+        if (w >= st.TW) break;
         sr[j].tns[w] = gp(st.taint_nosched)[(size_t)w * st.N + n];
         sr[j].tpr[w] = gp(st.taint_prefer)[(size_t)w * st.N + n];
       }
@@ -2678,7 +2708,7 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
 #define KGPU_TSTAMP(k) \
   if (trc) trow[(size_t)i * 16 + (k)] = (int64_t)__builtin_amdgcn_s_memrealtime()
 #define KGPU_WSTAMP(k) \
-  if (ta.trace_wg && tid == 0) ta.trace_wg[((size_t)i * G + g) * 4 + (k)] = (int64_t)__builtin_amdgcn_s_memrealtime()
+  if (ta.trace_wg && tid == 0) ta.trace_wg[((size_t)i * G + g) * 8 + (k)] = (int64_t)__builtin_amdgcn_s_memrealtime()
   for (int i = 0; i < ta.count; ++i) {
     KGPU_TSTAMP(0);
     KGPU_WSTAMP(0);
@@ -2798,7 +2828,8 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
       }
     }
     __syncthreads();
-    uint64_t* srow = ta.gran + (size_t)i * (R + 1) * G;
+    KGPU_WSTAMP(4);
+    uint64_t* srow = ta.gran + (size_t)i * (R + 1) * G;  // [G][R] statistics records | [G] keys
     if (tid < R) {
       int64_t x;
       switch (tid) {
@@ -2814,10 +2845,110 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
         case kTZoned: x = (uint32_t)M.acc32[7]; break;
         default: x = tid < kTFixed + ta.soft_words ? (int64_t)SMASK[tid - kTFixed] : (int64_t)ZSUM[tid - kTFixed - ta.soft_words];
       }
-      store_sc1(srow + (size_t)tid * G + g, enc_stat(x));
+      store_sc1(srow + (size_t)g * R + tid, enc_stat(x));  // this workgroup's record
     }
     KGPU_TSTAMP(3);
     KGPU_WSTAMP(2);
+    // ---- NormalizeScore of every plugin under statistics S, weights, and the packed key of this
+    // lane's best row; with write_diag, the cycle's per-plugin scores (as k_topo_score / k_topo_final)
+    auto best_under = [&](const int64_t* S, bool write_diag, uint64_t& bkey, int& bidx) {
+      const int maxT = (int)S[kTMaxT], maxNA = (int)S[kTMaxNA];
+      int64_t pmx = 0, pmn = INT64_MAX;
+      double wsoft = 0.0;
+      if (tp.n_soft) {
+        int64_t size = S[kTNonIgn];
+        if (tp.soft_mode == 0) {
+          size = 0;
+          for (int w = 0; w < tp.soft_words; ++w) size += __popc((uint32_t)S[kTFixed + w]);
+        }
+        wsoft = st.log_table[size + 2];  // topologyNormalizingWeight (scoring.go:286-288)
+        if (S[kTNonIgn] > 0) {
+          // int64(cnt * w) does not decrease with cnt: the extremes come from the extreme counts
+          pmn = (int64_t)((double)S[kTAdjMin] * wsoft);
+          pmx = max((int64_t)((double)S[kTAdjMax] * wsoft), (int64_t)0);
+        }
+      }
+      const int64_t imx = max(S[kTIpaMax], (int64_t)0), imn = min(S[kTIpaMin], (int64_t)0);
+      const int64_t idiff = imx - imn;
+      const int64_t dmax_node = max(S[kTDptsMax], (int64_t)0);
+      int64_t dmax_zone = 0;
+      for (int z = 0; z < ta.zones; ++z) dmax_zone = max(dmax_zone, S[kTFixed + ta.soft_words + z]);
+      const bool have_zones = S[kTZoned] != 0;
+      const double Mx = 100.0, zwt = 2.0 / 3.0;
+      bkey = 0;
+      bidx = -1;
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        if (!feas[j]) continue;
+        const int n = lo + j * B + tid;
+        // DefaultNormalizeScore (helper/normalize_score.go:26-54): non-negative operands, exact
+        // through div_nonneg
+        const int64_t vt = maxT == 0 ? 100 : 100 - div_nonneg(100 * (int64_t)o[j].taint, maxT);
+        const int64_t vn = maxNA == 0 ? (int64_t)o[j].na : div_nonneg(100 * (int64_t)o[j].na, maxNA);
+        int64_t vp;
+        if (o[j].adj == INT64_MIN) {
+          vp = 0;
+        } else {
+          // scoring.go:248-256; pmn <= ps <= pmx, so the dividend is non-negative
+          const int64_t ps = tp.n_soft ? (int64_t)((double)o[j].adj * wsoft) : 0;
+          vp = pmx == 0 ? 100 : div_nonneg(100 * (pmx + pmn - ps), pmx);
+        }
+        const int64_t vi = idiff > 0 ? (int64_t)(Mx * ((double)(o[j].ipa - imn) / (double)idiff)) : 0;
+        int64_t vd = 0;
+        if (tp.dpts_cls != -2) {
+          double f = Mx;
+          if (dmax_node > 0) f = Mx * ((double)(dmax_node - o[j].ds) / (double)dmax_node);
+          const int z = sr[j].zone;
+          if (have_zones && z >= 0) {
+            double zs = Mx;
+            if (dmax_zone > 0) zs = Mx * ((double)(dmax_zone - S[kTFixed + ta.soft_words + z]) / (double)dmax_zone);
+            f = (f * (1.0 - zwt)) + (zwt * zs);
+          }
+          vd = (int64_t)f;
+        }
+        int64_t total = o[j].part + vt * st.w_of[KGPU_S_TAINT_TOLERATION] + vn * st.w_of[KGPU_S_NODE_AFFINITY] +
+                        vp * st.w_of[KGPU_S_POD_TOPOLOGY_SPREAD] + vi * st.w_of[KGPU_S_INTER_POD_AFFINITY] +
+                        vd * st.w_of[KGPU_S_DEFAULT_POD_TOPOLOGY_SPREAD];
+        if (st.n_scores == 0) total = 1;
+        const uint64_t key = ((uint64_t)(total + 1) << 40) | rank40(tk, (uint64_t)(st.node_base + n), st.tie_mode);
+        if (key > bkey) {
+          bkey = key;
+          bidx = j * B + tid;
+        }
+        if (write_diag) {
+          const size_t N = (size_t)st.N;
+          gp(st.diag_raw)[KGPU_S_POD_TOPOLOGY_SPREAD * N + n] =
+              (o[j].adj == INT64_MIN || !tp.n_soft) ? 0 : (int64_t)((double)o[j].adj * wsoft);
+          gp(st.diag_raw)[KGPU_S_INTER_POD_AFFINITY * N + n] = o[j].ipa;
+          gp(st.diag_raw)[KGPU_S_DEFAULT_POD_TOPOLOGY_SPREAD * N + n] = tp.dpts_cls == -2 ? 0 : o[j].ds;
+          for (int si = 0; si < st.n_scores; ++si) {
+            const int s = cp(st.scores)[si];
+            int64_t v;
+            switch (s) {
+              case KGPU_S_TAINT_TOLERATION: v = vt; break;
+              case KGPU_S_NODE_AFFINITY: v = vn; break;
+              case KGPU_S_POD_TOPOLOGY_SPREAD: v = vp; break;
+              case KGPU_S_INTER_POD_AFFINITY: v = vi; break;
+              case KGPU_S_DEFAULT_POD_TOPOLOGY_SPREAD: v = vd; break;
+              default: v = gp(st.diag_raw)[(size_t)s * N + n];
+            }
+            gp(st.diag_norm)[(size_t)s * N + n] = v;
+          }
+        }
+      }
+    };
+    // the workgroup's best key: wave partials through LDS, combined by wave 0 (every wave calls it)
+    auto wg_best = [&](uint64_t bkey, int bidx, uint64_t& bk, int& bi) {
+      wave_argmax(bkey, bidx);
+      if (lane == 0) {
+        M.akey[wave] = bkey;
+        M.aidx[wave] = bidx;
+      }
+      __syncthreads();
+      bk = lane < W ? M.akey[lane] : 0;
+      bi = lane < W ? M.aidx[lane] : -1;
+      wave_argmax(bk, bi);
+    };
     bool ok = true;
     // XG: this pod's TX row and record tag (ring lap in bits 60-62)
     uint64_t* txrow = nullptr;
@@ -2826,23 +2957,20 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
       txrow = sh_ptx[ta.rank] + (size_t)((ta.xseq0 + i) % kTXRing) * txw;
       txtag = kGValid | ((uint64_t)(((ta.xseq0 + i) / kTXRing) & 7) << 60);
     }
-    for (int rr = wave; rr < R; rr += W) {
-      const int op = rr < kTFixed ? tstat_op(rr) : (rr < kTFixed + ta.soft_words ? kOpOr : kOpSum);
-      int64_t x;
-      if (!tpoll_slot(srow + (size_t)rr * G, G, ta.abort, op, x)) { ok = false; break; }
-      if constexpr (XG) {
-        // this rank's combined slot: workgroup 0 publishes it into every rank's ring
+    if (wave == 0) ok = tstats_gather(srow, G, R, ta.soft_words, ta.abort, GAT, STAT);
+    if constexpr (XG) {
+      // this rank's combined slots: workgroup 0 publishes them into every rank's ring; then every
+      // rank's record of each slot, combined: the cluster-wide statistics
+      if (wave == 0 && !ok && lane == 0) M.abort = 1;
+      __syncthreads();
+      ok = !M.abort;
+      for (int rr = wave; ok && rr < R; rr += W) {
+        const int op = tslot_op(rr, ta.soft_words);
+        const int64_t x0 = STAT[rr];
         if (g == 0 && lane < ta.nranks) {
           const size_t off = (size_t)(txrow - sh_ptx[ta.rank]) + (size_t)ta.rank * kTXRCap + rr;
-          store_sys(sh_ptx[lane] + off, txtag | (uint64_t)(x + kTXBias));
+          store_sys(sh_ptx[lane] + off, txtag | (uint64_t)(x0 + kTXBias));
         }
-      }
-      if (lane == 0) STAT[rr] = x;
-    }
-    if constexpr (XG) {
-      // every rank's record of the wave's slots, combined: the cluster-wide statistics
-      for (int rr = wave; ok && rr < R; rr += W) {
-        const int op = rr < kTFixed ? tstat_op(rr) : (rr < kTFixed + ta.soft_words ? kOpOr : kOpSum);
         int64_t x;
         if (!xpoll_stat(txrow + rr, ta.nranks, ta.abort, op, txtag, x)) { ok = false; break; }
         if (lane == 0) STAT[rr] = x;
@@ -2855,100 +2983,15 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
     __syncthreads();
     if (M.abort) break;
     KGPU_TSTAMP(4);
-    // ---- NormalizeScore of every plugin, weights, packed-key argmax
+    KGPU_WSTAMP(5);
     const int64_t feas_total = STAT[kTFeas];
-    const int maxT = (int)STAT[kTMaxT], maxNA = (int)STAT[kTMaxNA];
-    int64_t pmx = 0, pmn = INT64_MAX;
-    double wsoft = 0.0;
-    if (tp.n_soft) {
-      int64_t size = STAT[kTNonIgn];
-      if (tp.soft_mode == 0) {
-        size = 0;
-        for (int w = 0; w < tp.soft_words; ++w) size += __popc((uint32_t)STAT[kTFixed + w]);
-      }
-      wsoft = st.log_table[size + 2];  // topologyNormalizingWeight (scoring.go:286-288)
-      if (STAT[kTNonIgn] > 0) {
-        // int64(cnt * w) does not decrease with cnt: the extremes come from the extreme counts
-        pmn = (int64_t)((double)STAT[kTAdjMin] * wsoft);
-        pmx = max((int64_t)((double)STAT[kTAdjMax] * wsoft), (int64_t)0);
-      }
-    }
-    const int64_t imx = max(STAT[kTIpaMax], (int64_t)0), imn = min(STAT[kTIpaMin], (int64_t)0);
-    const int64_t idiff = imx - imn;
-    const int64_t dmax_node = max(STAT[kTDptsMax], (int64_t)0);
-    int64_t dmax_zone = 0;
-    for (int z = 0; z < ta.zones; ++z) dmax_zone = max(dmax_zone, STAT[kTFixed + ta.soft_words + z]);
-    const bool have_zones = STAT[kTZoned] != 0;
-    const double Mx = 100.0, zwt = 2.0 / 3.0;
-    uint64_t bkey = 0;
-    int bidx = -1;
-#pragma unroll
-    for (int j = 0; j < K; ++j) {
-      if (!feas[j]) continue;
-      const int n = lo + j * B + tid;
-      // DefaultNormalizeScore (helper/normalize_score.go:26-54): non-negative operands, exact
-      // through div_nonneg
-      const int64_t vt = maxT == 0 ? 100 : 100 - div_nonneg(100 * (int64_t)o[j].taint, maxT);
-      const int64_t vn = maxNA == 0 ? (int64_t)o[j].na : div_nonneg(100 * (int64_t)o[j].na, maxNA);
-      int64_t vp;
-      if (o[j].adj == INT64_MIN) {
-        vp = 0;
-      } else {
-        // scoring.go:248-256; pmn <= ps <= pmx, so the dividend is non-negative
-        const int64_t ps = tp.n_soft ? (int64_t)((double)o[j].adj * wsoft) : 0;
-        vp = pmx == 0 ? 100 : div_nonneg(100 * (pmx + pmn - ps), pmx);
-      }
-      const int64_t vi = idiff > 0 ? (int64_t)(Mx * ((double)(o[j].ipa - imn) / (double)idiff)) : 0;
-      int64_t vd = 0;
-      if (tp.dpts_cls != -2) {
-        double f = Mx;
-        if (dmax_node > 0) f = Mx * ((double)(dmax_node - o[j].ds) / (double)dmax_node);
-        const int z = sr[j].zone;
-        if (have_zones && z >= 0) {
-          double zs = Mx;
-          if (dmax_zone > 0) zs = Mx * ((double)(dmax_zone - STAT[kTFixed + ta.soft_words + z]) / (double)dmax_zone);
-          f = (f * (1.0 - zwt)) + (zwt * zs);
-        }
-        vd = (int64_t)f;
-      }
-      int64_t total = o[j].part + vt * st.w_of[KGPU_S_TAINT_TOLERATION] + vn * st.w_of[KGPU_S_NODE_AFFINITY] +
-                      vp * st.w_of[KGPU_S_POD_TOPOLOGY_SPREAD] + vi * st.w_of[KGPU_S_INTER_POD_AFFINITY] +
-                      vd * st.w_of[KGPU_S_DEFAULT_POD_TOPOLOGY_SPREAD];
-      if (st.n_scores == 0) total = 1;
-      const uint64_t key = ((uint64_t)(total + 1) << 40) | rank40(tk, (uint64_t)(st.node_base + n), st.tie_mode);
-      if (key > bkey) { bkey = key; bidx = j * B + tid; }
-      if (ta.diag) {  // per-plugin raw and normalized scores of the cycle (as k_topo_score / k_topo_final)
-        const size_t N = (size_t)st.N;
-        gp(st.diag_raw)[KGPU_S_POD_TOPOLOGY_SPREAD * N + n] =
-            (o[j].adj == INT64_MIN || !tp.n_soft) ? 0 : (int64_t)((double)o[j].adj * wsoft);
-        gp(st.diag_raw)[KGPU_S_INTER_POD_AFFINITY * N + n] = o[j].ipa;
-        gp(st.diag_raw)[KGPU_S_DEFAULT_POD_TOPOLOGY_SPREAD * N + n] = tp.dpts_cls == -2 ? 0 : o[j].ds;
-        for (int si = 0; si < st.n_scores; ++si) {
-          const int s = cp(st.scores)[si];
-          int64_t v;
-          switch (s) {
-            case KGPU_S_TAINT_TOLERATION: v = vt; break;
-            case KGPU_S_NODE_AFFINITY: v = vn; break;
-            case KGPU_S_POD_TOPOLOGY_SPREAD: v = vp; break;
-            case KGPU_S_INTER_POD_AFFINITY: v = vi; break;
-            case KGPU_S_DEFAULT_POD_TOPOLOGY_SPREAD: v = vd; break;
-            default: v = gp(st.diag_raw)[(size_t)s * N + n];
-          }
-          gp(st.diag_norm)[(size_t)s * N + n] = v;
-        }
-      }
-    }
-    wave_argmax(bkey, bidx);
-    if (lane == 0) {
-      M.akey[wave] = bkey;
-      M.aidx[wave] = bidx;
-    }
-    __syncthreads();
     uint64_t* arow = srow + (size_t)R * G;
+    // ---- NormalizeScore of every plugin, weights, packed-key argmax
+    uint64_t bkey0, bk;
+    int bidx0, bi;
+    best_under(STAT, ta.diag != 0, bkey0, bidx0);
+    wg_best(bkey0, bidx0, bk, bi);
     if (wave == 0) {
-      uint64_t bk = lane < W ? M.akey[lane] : 0;
-      int bi = lane < W ? M.aidx[lane] : -1;
-      wave_argmax(bk, bi);
       if (lane == 0) store_sc1(arow + g, kGValid | bk);
       KGPU_TSTAMP(5);
       KGPU_WSTAMP(3);
@@ -3027,6 +3070,7 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
     __syncthreads();
     if (M.abort) break;
     KGPU_TSTAMP(6);
+    KGPU_WSTAMP(6);
     // ---- outcome (generic_scheduler.go:171-208) and assume (types.go:456-480)
     const int wnode = M.wnode;  // global index
     const bool error = (q.flags & KGPU_Q_SCORE_ERROR) && feas_total >= 2;

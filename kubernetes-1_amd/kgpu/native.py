@@ -221,13 +221,13 @@ class Engine:
         return reg[:n_values].astype(bool), cnt[:n_values], int(out.value)
 
     def wg_trace(self, pods):
-        """kgpu_debug_wg_trace: [pods][groups][4] per-workgroup stamps of the last traced k_tbatch run."""
+        """kgpu_debug_wg_trace: [pods][groups][8] per-workgroup stamps of the last traced k_tbatch run."""
         g = C.c_int32(0)
         probe = np.zeros(1, np.int64)
         lib().kgpu_debug_wg_trace(self.h, probe.ctypes.data, 0, C.byref(g))  # the run's workgroup count
-        out = np.zeros(max(pods * g.value * 4, 1), np.int64)
+        out = np.zeros(max(pods * g.value * 8, 1), np.int64)
         n = lib().kgpu_debug_wg_trace(self.h, out.ctypes.data, len(out), C.byref(g))
-        return out[:n].reshape(-1, g.value, 4) if g.value else out[:0].reshape(0, 0, 4)
+        return out[:n].reshape(-1, g.value, 8) if g.value else out[:0].reshape(0, 0, 8)
 
     def broken_linear(self, points, utilizations):
         """kgpu_debug_broken_linear: the device's broken-linear shape function (the one

@@ -7,7 +7,10 @@ addresses of a crash report from the same process can be resolved to libraries:
   both    -- torch first, then the kgpu variant
 Usage: python3 tools/exit_probe.py <variant> <maps-out> [--os-exit]
   --os-exit: leave through os._exit(0) after the work (no exit handlers run: does rocprofv3 still write
-             its files?)"""
+             its files?  It does not: the tool finalizes in an exit handler)
+  --no-persistent: no persistent (cooperative) launch, one k_eval launch per pod
+  --reset:   hipDeviceReset() before a normal exit (the runtime's queues and allocations released while
+             the profiler is still attached)"""
 import os
 import sys
 
@@ -29,6 +32,9 @@ def run_kgpu():
     from kgpu.framework import GpuFramework
     nodes, existing, pods, prof = fit_least_balanced(n_nodes=64, n_pods=32)
     fw = GpuFramework(prof, nodes, existing, pods_hint=pods, device=0)
+    if "--no-persistent" in sys.argv:  # k_eval launches only: no cooperative launch in the process
+        from kgpu import abi
+        fw.engine.set_option(abi.OPT_PERSISTENT, 0)
     res = fw.schedule(pods, first_seq=0)
     assert (res["node"] >= 0).sum() > 0
     fw.engine.close()
@@ -43,6 +49,11 @@ def main():
     with open("/proc/self/maps") as src, open(out, "w") as dst:
         dst.write(src.read())
     print("exit_probe %s: done, maps in %s" % (variant, out), flush=True)
+    if "--reset" in sys.argv:
+        # tear the HIP runtime's device state down now, while a profiler's tool is still alive
+        import ctypes
+        rc = ctypes.CDLL("libamdhip64.so").hipDeviceReset()
+        print("exit_probe: hipDeviceReset rc=%d" % rc, flush=True)
     if "--os-exit" in sys.argv:
         sys.stdout.flush()
         sys.stderr.flush()

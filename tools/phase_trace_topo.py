@@ -56,7 +56,10 @@ def main():
         G = wt.shape[1]
         print("per-workgroup medians over pods (ns after the earliest pod start), %d workgroups:" % G)
         print("  rows done     " + " ".join("%5.0f" % x for x in np.median(rows, axis=0)))
+        print("  stats reduced " + " ".join("%5.0f" % x for x in np.median(wt[:, :, 4] - t0, axis=0)))
         print("  stats pub     " + " ".join("%5.0f" % x for x in np.median(spub, axis=0)))
+        print("  stats recv    " + " ".join("%5.0f" % x for x in np.median(wt[:, :, 5] - t0, axis=0)))
+        print("  winner recv   " + " ".join("%5.0f" % x for x in np.median(wt[:, :, 6] - t0, axis=0)))
         print("  key pub       " + " ".join("%5.0f" % x for x in np.median(kpub, axis=0)))
         print("  start         " + " ".join("%5.0f" % x for x in np.median(wt[:, :, 0] - t0, axis=0)))
         last = np.argmax(spub, axis=1)
