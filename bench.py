@@ -120,6 +120,8 @@ def measure(args, cfg, n_nodes_per_gpu, B, K, W, cpu_sample, cpu_threads, latenc
     eng = fw.engine
     if args.no_persistent:
         eng.set_option(abi.OPT_PERSISTENT, 0)
+    if args.no_coop:
+        eng.set_option(abi.OPT_COOPERATIVE, 0)
     if args.topo_fused is not None:
         eng.set_option(abi.OPT_TOPO_FUSED, args.topo_fused)
     if args.no_topo_persistent:
@@ -304,6 +306,8 @@ def main():
                          "many nodes (BASELINE.json's metric is quoted at 5k and 100k nodes); 0: none")
     ap.add_argument("--extra-cpu-sample", type=int, default=1000, help="pods of the extra record's CPU baseline")
     ap.add_argument("--reset-at-exit", action="store_true", help="hipDeviceReset() before exiting (profiling runs)")
+    ap.add_argument("--no-coop", action="store_true",
+                    help="KGPU_OPT_COOPERATIVE = 0: ordinary launches of the persistent kernels (profiling runs)")
     ap.add_argument("--os-exit", action="store_true",
                     help="leave through os._exit(0) after printing (profiling runs: see DESIGN.md, rocprofv3 exit)")
     args = ap.parse_args()

@@ -544,6 +544,11 @@ int kgpu_read_nodes(kgpu_ctx* ctx, int64_t* req_cpu, int64_t* req_mem, int64_t* 
  * the next pod's wait on it times out (the path a lost LDS release would take): the batch fails with
  * KGPU_E_DEVICE and the mirror is invalidated (-1, the default: never). */
 #define KGPU_OPT_SKIP_RELEASE_AT 9
+/* KGPU_OPT_COOPERATIVE (10): 1 (default) = persistent kernels go through hipLaunchCooperativeKernel,
+ * which refuses a grid that cannot be co-resident; 0 = an ordinary launch of the same grid (one
+ * workgroup per CU on an idle device; a workgroup that never starts turns into KGPU_E_DEVICE through
+ * the spin timeouts).  For tools whose exit path faults after cooperative launches (rocprofv3). */
+#define KGPU_OPT_COOPERATIVE 10
 int kgpu_set_option(kgpu_ctx* ctx, int32_t option, int64_t value);
 /* Phase stamps of the last persistent run (100 MHz s_memrealtime ticks), 16 per pipeline
  * iteration (pods + 1): workgroup 0's {start, evaluated, previous pod resolved, published, end, 0,

@@ -85,7 +85,7 @@ struct kgpu_ctx {
   int64_t generation = -1;
   bool uploaded = false;
   // grow-only batch buffers
-  DevBuf queries, reqs, ints, words, node_terms, pref_terms, spreads, pod_terms, scalars, ports, results;
+  DevBuf queries, results;
   DevBuf dstate;     // device copy of the DevState used by the kernels of the current batch
   DevBuf ticket;     // k_final's last-workgroup ticket (zero between launches)
   DevState st_batch{};  // its host source (kept alive for the async copy)
@@ -213,8 +213,12 @@ struct kgpu_ctx {
   int64_t max_key_values = 1;
   // persistent topology runs (k_tbatch)
   bool tfast = true;                // KGPU_OPT_TOPO_PERSISTENT
+  bool coop = true;                 // KGPU_OPT_COOPERATIVE
   DevBuf t_tables, t_zero, abort_buf;
   void* t_stage_host = nullptr;  // pinned staging of the runs' tables (bump-allocated, wraps after a sync)
+  DevBuf pool_blk;               // the call's query pools, packed (upload_pools)
+  void* pool_host = nullptr;     // ... and their pinned staging
+  size_t pool_host_cap = 0;
   size_t t_stage_cap = 0, t_stage_used = 0;
   // ---- node sharding (kgpu_comm_init): this context holds one contiguous slice of the
   // snapshot; per pod the shard winners (and normalize maxima) are all-gathered over RCCL
@@ -342,20 +346,69 @@ int upload_pool(kgpu_ctx* c, DevBuf& b, const T* src, int32_t n, const T** dst) 
   return KGPU_OK;
 }
 
+// The query pools of a call, packed into one pinned block and moved with ONE copy (skipped when
+// the bytes equal the last upload): a pageable copy per pool cost microseconds each on the per-pod
+// (kgpu_schedule_one) path.  The staging block is rewritten only by the next call, after this call's
+// stream synchronize.
 int upload_pools(kgpu_ctx* c, const kgpu_pools* p) {
   kgpu_pools empty{};
   if (!p) p = &empty;
   kgpu::DevPools& q = c->st.qp;
+  size_t off = 0;
+  auto place = [&](size_t bytes) {
+    const size_t o = off;
+    off += (std::max<size_t>(bytes, 16) + 15) & ~(size_t)15;
+    return o;
+  };
+  auto nb = [](int32_t n, size_t sz) { return sz * (size_t)std::max(n, 0); };
+  const size_t o_req = place(nb(p->n_reqs, sizeof(kgpu_req))), o_int = place(nb(p->n_ints, sizeof(int32_t))),
+               o_wrd = place(nb(p->n_words, sizeof(uint64_t))), o_nt = place(nb(p->n_node_terms, sizeof(kgpu_node_term))),
+               o_pt = place(nb(p->n_pref_terms, sizeof(kgpu_pref_term))), o_sp = place(nb(p->n_spreads, sizeof(kgpu_spread))),
+               o_pd = place(nb(p->n_pod_terms, sizeof(kgpu_pod_term))), o_sc = place(nb(p->n_scalars, sizeof(kgpu_scalar_req))),
+               o_po = place(nb(p->n_ports, sizeof(kgpu_port)));
+  const size_t total = off;
+  if (total > c->pool_host_cap) {
+    HIP_OK(c, hipStreamSynchronize(c->stream));
+    if (c->pool_host) (void)hipHostFree(c->pool_host);
+    c->pool_host = nullptr;
+    c->pool_host_cap = 0;
+    const size_t cap = std::max<size_t>(total * 2, 64 * 1024);
+    HIP_OK(c, hipHostMalloc(&c->pool_host, cap, hipHostMallocDefault));
+    c->pool_host_cap = cap;
+  }
+  char* h = static_cast<char*>(c->pool_host);
+  std::memset(h, 0, total);
+  auto put = [&](size_t o, const void* src, size_t bytes) {
+    if (src && bytes) std::memcpy(h + o, src, bytes);
+  };
+  put(o_req, p->reqs, nb(p->n_reqs, sizeof(kgpu_req)));
+  put(o_int, p->ints, nb(p->n_ints, sizeof(int32_t)));
+  put(o_wrd, p->words, nb(p->n_words, sizeof(uint64_t)));
+  put(o_nt, p->node_terms, nb(p->n_node_terms, sizeof(kgpu_node_term)));
+  put(o_pt, p->pref_terms, nb(p->n_pref_terms, sizeof(kgpu_pref_term)));
+  put(o_sp, p->spreads, nb(p->n_spreads, sizeof(kgpu_spread)));
+  put(o_pd, p->pod_terms, nb(p->n_pod_terms, sizeof(kgpu_pod_term)));
+  put(o_sc, p->scalars, nb(p->n_scalars, sizeof(kgpu_scalar_req)));
+  put(o_po, p->ports, nb(p->n_ports, sizeof(kgpu_port)));
   int rc;
-  if ((rc = upload_pool(c, c->reqs, p->reqs, p->n_reqs, &q.reqs))) return rc;
-  if ((rc = upload_pool(c, c->ints, p->ints, p->n_ints, &q.ints))) return rc;
-  if ((rc = upload_pool(c, c->words, p->words, p->n_words, &q.words))) return rc;
-  if ((rc = upload_pool(c, c->node_terms, p->node_terms, p->n_node_terms, &q.node_terms))) return rc;
-  if ((rc = upload_pool(c, c->pref_terms, p->pref_terms, p->n_pref_terms, &q.pref_terms))) return rc;
-  if ((rc = upload_pool(c, c->spreads, p->spreads, p->n_spreads, &q.spreads))) return rc;
-  if ((rc = upload_pool(c, c->pod_terms, p->pod_terms, p->n_pod_terms, &q.pod_terms))) return rc;
-  if ((rc = upload_pool(c, c->scalars, p->scalars, p->n_scalars, &q.scalars))) return rc;
-  if ((rc = upload_pool(c, c->ports, p->ports, p->n_ports, &q.ports))) return rc;
+  if ((rc = ensure(c, c->pool_blk, total))) return rc;
+  const bool current = c->pool_blk.shadow_p == c->pool_blk.p && c->pool_blk.shadow.size() == total &&
+                       std::memcmp(c->pool_blk.shadow.data(), h, total) == 0;
+  if (!current) {
+    HIP_OK(c, hipMemcpyAsync(c->pool_blk.p, h, total, hipMemcpyHostToDevice, c->stream));
+    c->pool_blk.shadow.assign(h, h + total);
+    c->pool_blk.shadow_p = c->pool_blk.p;
+  }
+  const char* d = static_cast<const char*>(c->pool_blk.p);
+  q.reqs = reinterpret_cast<const kgpu_req*>(d + o_req);
+  q.ints = reinterpret_cast<const int32_t*>(d + o_int);
+  q.words = reinterpret_cast<const uint64_t*>(d + o_wrd);
+  q.node_terms = reinterpret_cast<const kgpu_node_term*>(d + o_nt);
+  q.pref_terms = reinterpret_cast<const kgpu_pref_term*>(d + o_pt);
+  q.spreads = reinterpret_cast<const kgpu_spread*>(d + o_sp);
+  q.pod_terms = reinterpret_cast<const kgpu_pod_term*>(d + o_pd);
+  q.scalars = reinterpret_cast<const kgpu_scalar_req*>(d + o_sc);
+  q.ports = reinterpret_cast<const kgpu_port*>(d + o_po);
   return KGPU_OK;
 }
 
@@ -993,8 +1046,6 @@ size_t t_layout(const TRun& tr, kgpu::TBatchArgs* a, int B, int lab_keys = 0, in
   o = a16(o + (size_t)kgpu::kTMaxSoftWords * 4);
   const size_t o_zsum = o;
   o = a16(o + (size_t)std::max(tr.zones, 1) * 4);
-  const size_t o_gat = o;
-  o = a16(o + (size_t)64 * (size_t)R * 8);
   const size_t o_pt = o;
   o = a16(o + (size_t)std::max(tr.pt_max, 1) * 8);
   const size_t o_misc = o;
@@ -1010,7 +1061,6 @@ size_t t_layout(const TRun& tr, kgpu::TBatchArgs* a, int B, int lab_keys = 0, in
     a->o_stat = (int32_t)o_stat;
     a->o_smask = (int32_t)o_smask;
     a->o_zsum = (int32_t)o_zsum;
-    a->o_gat = (int32_t)o_gat;
     a->o_pt = (int32_t)o_pt;
     a->o_misc = (int32_t)o_misc;
     a->R = R;
@@ -1300,6 +1350,7 @@ int run_tbatch(kgpu_ctx* c, TRun& tr, int first, int count, int64_t first_seq, i
     c->t_stage_used = 0;
     if (tbytes > c->t_stage_cap) {
       if (c->t_stage_host) (void)hipHostFree(c->t_stage_host);
+  if (c->pool_host) (void)hipHostFree(c->pool_host);
       c->t_stage_host = nullptr;
       c->t_stage_cap = 0;
       const size_t cap = std::max<size_t>(tbytes * 2, 1 << 20);
@@ -1395,7 +1446,7 @@ int run_tbatch(kgpu_ctx* c, TRun& tr, int first, int count, int64_t first_seq, i
     x.abort = abort_word;
     if (kgpu::launch_xreduce(x, c->stream)) return fail(c, KGPU_E_DEVICE, "cross-rank histogram reduction launch failed");
   }
-  if (kgpu::launch_tbatch(dst, a, groups, geo, c->spec, xg, c->stream))
+  if (kgpu::launch_tbatch(dst, a, groups, geo, c->spec, xg, c->coop, c->stream))
     return fail(c, KGPU_E_DEVICE, std::string("k_tbatch launch failed: ") + hipGetErrorString(hipGetLastError()));
   if (a.trace) {
     HIP_OK(c, hipMemcpyAsync(c->trace_host.data(), a.trace, sizeof(int64_t) * 16 * (size_t)(count + 1),
@@ -1683,15 +1734,21 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
   // a short cycle's records go straight to pinned host memory (no read-back copy)
   st.results = short_cycle ? c->res_dev : static_cast<kgpu_result*>(c->results.p);
   // Per-plugin scores of a diagnostic cycle: every pod of a batch without topology pods goes
-  // through k_eval, which then zeroes each node's rows itself; otherwise two memsets do.
+  // through k_eval, which then zeroes each node's rows itself; a one-pod persistent topology run's
+  // k_tbatch_init does too; otherwise one memset does, issued before the first launch that needs it.
   const bool zero_diag = diag && !topo_on && c->comm == nullptr;
+  bool diag_zeroed = !diag || zero_diag;
   if (!diag) {
     st.diag_raw = nullptr;
     st.diag_norm = nullptr;
-  } else if (!zero_diag) {
-    HIP_OK(c, hipMemsetAsync(st.diag_raw, 0, sizeof(int64_t) * KGPU_NUM_SCORES * (size_t)st.N, c->stream));
-    HIP_OK(c, hipMemsetAsync(st.diag_norm, 0, sizeof(int64_t) * KGPU_NUM_SCORES * (size_t)st.N, c->stream));
   }
+  auto zero_diag_rows = [&]() -> int {
+    if (!diag_zeroed) {
+      HIP_OK(c, hipMemsetAsync(c->st.diag_raw, 0, sizeof(int64_t) * 2 * KGPU_NUM_SCORES * (size_t)c->st.N, c->stream));
+      diag_zeroed = true;
+    }
+    return KGPU_OK;
+  };
   // nominated pods that apply to this pod: pass 1 runs in k_victims before the filter phase
   PreemptStage nps;
   const kgpu::PreemptArgs* nom_dev = nullptr;
@@ -1807,6 +1864,7 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
       if (j > i) {
         if (c->timing) HIP_OK(c, hipEventRecord(get_event(c, ev), c->stream));
         if ((rc = run_tbatch(c, tr, i, j - i, first_seq, assume, tper, tgroups, tgeo, abort_word, xg, diag))) return rc;
+        if (diag) diag_zeroed = true;  // k_tbatch_init zeroed the rows (a diagnostic run is one pod)
         if (c->timing) HIP_OK(c, hipEventRecord(get_event(c, ev + 1), c->stream));
         ev += 2;
         timed_passes += j - i;
@@ -1816,6 +1874,7 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
       }
     }
     if (topo[(size_t)i]) {
+      if ((rc = zero_diag_rows())) return rc;
       const kgpu::QPlan& pl = plans[(size_t)i];
       // the previous pod's resolve launch zeroes this pod's scratch only when it went through this
       // pipeline too (a persistent topology run in between leaves it dirty)
@@ -1950,7 +2009,7 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
         c->trace_host.assign((size_t)(cnt + 1) * 16, 0);
       }
       if (c->timing) HIP_OK(c, hipEventRecord(get_event(c, ev), c->stream));
-      if (kgpu::launch_batch(dst, ba, groups, kidx, c->spec, c->stream))
+      if (kgpu::launch_batch(dst, ba, groups, kidx, c->spec, c->coop, c->stream))
         return fail(c, KGPU_E_DEVICE, "k_batch launch failed");
       if (c->timing) HIP_OK(c, hipEventRecord(get_event(c, ev + 1), c->stream));
       ev += 2;
@@ -1984,6 +2043,7 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
           a.q_inline = 1;
           a.q = qs[k];
         }
+        if ((rc = zero_diag_rows())) return rc;
         if (c->timing) HIP_OK(c, hipEventRecord(get_event(c, ev), c->stream));
         if (nom_dev && kgpu::launch_victims(dst, nom_dev, st.N, c->stream))
           return fail(c, KGPU_E_DEVICE, "k_victims launch failed");
@@ -2105,8 +2165,9 @@ int alloc_node_work(kgpu_ctx* c) {
   if ((rc = dalloc(c, W, &st.partial, N))) return rc;
   if ((rc = dalloc(c, W, &st.sbuf, (size_t)2 * kgpu::kMaxBlocks))) return rc;
   if ((rc = dalloc(c, W, &st.kbuf, (size_t)2 * kgpu::kMaxBlocks))) return rc;
-  if ((rc = dalloc(c, W, &st.diag_raw, (size_t)KGPU_NUM_SCORES * N))) return rc;
-  if ((rc = dalloc(c, W, &st.diag_norm, (size_t)KGPU_NUM_SCORES * N))) return rc;
+  // raw | normalized in one block: a diagnostic cycle zeroes both with one memset
+  if ((rc = dalloc(c, W, &st.diag_raw, (size_t)2 * KGPU_NUM_SCORES * N))) return rc;
+  st.diag_norm = st.diag_raw + (size_t)KGPU_NUM_SCORES * N;
   HIP_OK(c, hipMemset(st.status, 0, sizeof(uint32_t) * std::max<size_t>(N, 1)));
   if ((rc = dalloc(c, W, &st.raw_pts, N))) return rc;
   if ((rc = dalloc(c, W, &st.raw_ipa, N))) return rc;
@@ -2786,8 +2847,7 @@ int kgpu_destroy(kgpu_ctx* c) try {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   free_all(c->snap_allocs);
   free_all(c->work_allocs);
-  for (DevBuf* b : {&c->dstate, &c->ticket, &c->queries, &c->reqs, &c->ints, &c->words, &c->node_terms, &c->pref_terms, &c->spreads,
-                    &c->pod_terms, &c->scalars, &c->ports, &c->results, &c->gran, &c->trace, &c->d_classes,
+  for (DevBuf* b : {&c->dstate, &c->ticket, &c->queries, &c->pool_blk, &c->results, &c->gran, &c->trace, &c->d_classes,
                     &c->d_citems, &c->d_tclasses, &c->d_creqs, &c->d_cints, &c->d_plans, &c->d_aux,
                     &c->d_aux_terms, &c->scratch, &c->d_pods, &c->gbar, &c->cut_buf, &c->t_tables, &c->t_zero,
                     &c->abort_buf, &c->flags_buf, &c->d_stage, &c->d_remap, &c->d_from,
@@ -2803,6 +2863,7 @@ int kgpu_destroy(kgpu_ctx* c) try {
   if (c->stage_host) (void)hipHostFree(c->stage_host);
   if (c->cyc_host) (void)hipHostFree(c->cyc_host);
   if (c->t_stage_host) (void)hipHostFree(c->t_stage_host);
+  if (c->pool_host) (void)hipHostFree(c->pool_host);
   if (c->res_pin) (void)hipHostFree(c->res_pin);
   if (c->st.mcnt) (void)hipFree(c->st.mcnt);
   if (c->st.tcnt) (void)hipFree(c->st.tcnt);
@@ -2847,6 +2908,7 @@ int kgpu_set_option(kgpu_ctx* c, int32_t option, int64_t value) try {
   else if (option == KGPU_OPT_PHASE_TRACE) c->phase_trace = value != 0;
   else if (option == KGPU_OPT_TOPO_FUSED) c->topo_fused = value != 0;
   else if (option == KGPU_OPT_TOPO_PERSISTENT) c->tfast = value != 0;
+  else if (option == KGPU_OPT_COOPERATIVE) c->coop = value != 0;
   else if (option == KGPU_OPT_ABORT_AT) c->abort_at = value < 0 || value > INT32_MAX ? -1 : (int32_t)value;
   else if (option == KGPU_OPT_XGMI) c->xgmi = value != 0;
   else if (option == KGPU_OPT_SKIP_RELEASE_AT) c->skip_release_at = value < 0 || value > INT32_MAX ? -1 : (int32_t)value;

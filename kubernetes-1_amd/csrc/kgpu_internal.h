@@ -382,15 +382,14 @@ struct TBatchArgs {
   uint32_t* reg_init;     // [reg_words]
   int32_t* sig_any;       // [n_sigs]
   uint32_t* elig;         // [n_sigs][ceil(N/32)]
-  uint64_t* gran;         // per pod: [groups][R] statistics records, then [groups] key granules; zeroed
+  uint64_t* gran;         // per pod: [R][groups] statistics granules, then [groups] key granules; zeroed
   int32_t* abort;
   int32_t lds_bytes;
   int32_t def_res;        // Least/Most over {cpu: 1, memory: 1}
   int32_t pt_words;       // largest per-pod table area of the run (int64 words)
   int32_t n_keys;         // node label keys the run's deltas read (winner's labels staged in LDS)
   // byte offsets of the LDS regions (histogram bins start at 0)
-  int32_t o_reg, o_tot, o_sany, o_stat, o_smask, o_zsum, o_gat, o_misc, o_pt, o_lab;  // o_gat: [64][R] int64,
-                          // the statistics poll's per-lane partials
+  int32_t o_reg, o_tot, o_sany, o_stat, o_smask, o_zsum, o_misc, o_pt, o_lab;
   int32_t lab_keys;       // node label keys cached in LDS per workgroup ([lab_keys][per] value ids)
   int32_t abort_at;       // KGPU_OPT_ABORT_AT test hook (-1: never), as in BatchArgs
   int32_t diag;           // kgpu_schedule_one: status word and per-plugin raw / normalized scores of every
@@ -500,7 +499,7 @@ int launch_shard_pack(const DevState* st, int parity, int blocks, int what, void
 // persistent kernel: *per = B*K - 1 nodes per workgroup (the last slot of the last lane is the
 // variant-B spare), -1 when N does not fit in max_groups workgroups.
 int batch_geometry(int N, int max_groups, int* per, int* groups);
-int launch_batch(const DevState* st, const BatchArgs& a, int groups, int kidx, int spec, void* stream);
+int launch_batch(const DevState* st, const BatchArgs& a, int groups, int kidx, int spec, bool coop, void* stream);
 // Topology pipeline for one pod (PodArgs.pod): domain histograms, critical-path minima, filters,
 // scores, normalize + argmax, resolve + assume.  next_scratch: words of the next topology pod's
 // scratch to zero in the resolve launch (0 none).
@@ -524,7 +523,8 @@ int tbatch_geometry(int N, int max_groups, int* per, int* groups);
 // k_tbatch_init over the local nodes (a.per * groups >= N); then, on a node-sharded
 // engine, launch_xreduce over the init region; then launch_tbatch (xg: the XG instantiation).
 int launch_tbatch_init(const DevState* st, const TBatchArgs& a, int groups, void* stream);
-int launch_tbatch(const DevState* st, const TBatchArgs& a, int groups, int geo, int spec, bool xg, void* stream);
+int launch_tbatch(const DevState* st, const TBatchArgs& a, int groups, int geo, int spec, bool xg, bool coop,
+                  void* stream);
 
 // ---------------------------------------------------------------- delta stream (kgpu_apply_delta)
 enum DeltaKind { kDAddPod = 0, kDRemovePod = 1, kDSetNode = 2 };

@@ -1178,8 +1178,6 @@ struct BatchShared {
   int rwg[2];                       // communication wave: winning granule of pod p in slot p & 1
                                     // (-1: no feasible node)
   int rabort[2];                    // the poll gave up (abort word or timeout)
-  int candn[2];                     // this workgroup's published candidate for pod p (-1 none,
-                                    // -2: slow path, the winning row's wave publishes)
   NodeRes brow[2];                  // pod p's candidate row (pod p-1 assumed) for pod p+1's variant B
   int bready;                       // p + 1 once brow[p & 1] is written
   int cslow[2];                     // slow path: candidate of pod p
@@ -1455,7 +1453,6 @@ __global__ __launch_bounds__(B + 64) void k_batch(const DevState* __restrict__ s
       }
       const bool won = have_prev && wg == gme;
       const bool slow = have_cur && won && pa.assume && !fast_b;
-      int cn = -1;
       if (ok) {
         // pod i-1's record (unsharded: by the winning workgroup; xGMI-sharded: by workgroup 0 of
         // every rank, which decodes the winner's global node index from its key)
@@ -1470,28 +1467,26 @@ __global__ __launch_bounds__(B + 64) void k_batch(const DevState* __restrict__ s
           res.score = wg >= 0 ? (int64_t)(wkey >> 40) - 1 : 0;
           gp(st.results)[pa.first + i - 1] = res;
         }
-        if (have_cur && !slow) {
-          lds_wait_ge(&sh.pcount, W * (i + 1), pa.abort);
-          KGPU_STAMP(i, 6);
-          const Cand c = wg_combine<B>(sh, p, won && fast_b);
-          if (lane == 0) publish(i, c.key, c.feas);
-          KGPU_STAMP(i, 3);
-          cn = c.key ? c.idx : -1;
-        } else if (slow) {
-          cn = -2;
-        }
       } else if (lane == 0) {
         __hip_atomic_store(pa.abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      if (lane == 0) {
-        if (have_prev) {
-          sh.rwg[(i - 1) & 1] = wg;
-          sh.rabort[(i - 1) & 1] = ok ? 0 : 1;
-        }
-        sh.candn[p] = cn;
+      if (lane == 0 && have_prev) {
+        sh.rwg[(i - 1) & 1] = wg;
+        sh.rabort[(i - 1) & 1] = ok ? 0 : 1;
       }
+      // (c): pod i-1 resolved here, pod i's partials written by the row waves.  The row waves take
+      // their candidate for pod i from the partials themselves and go on (assume, staging) while this
+      // wave combines and publishes -- nobody waits for the publish.
       __syncthreads();  // (c)
       if (!ok) break;
+      int cn = -1;
+      if (have_cur && !slow) {
+        KGPU_STAMP(i, 6);
+        const Cand c = wg_combine<B>(sh, p, won && fast_b);
+        if (lane == 0) publish(i, c.key, c.feas);
+        KGPU_STAMP(i, 3);
+        cn = c.key ? c.idx : -1;
+      }
       if (slow) {
         lds_wait(&sh.cready, i + 1, pa.abort);
         cand = sh.cslow[p];
@@ -1565,7 +1560,17 @@ __global__ __launch_bounds__(B + 64) void k_batch(const DevState* __restrict__ s
       wg = sh.rwg[s];
     }
     const bool won = have_prev && wg == gme;
-    const int cn = have_cur ? sh.candn[p] : -1;
+    // pod i's candidate: what the communication wave publishes (the same combine of the partials),
+    // or -2 when pod i-1's win makes this workgroup's winning row a slow-path re-evaluation
+    int cn = -1;
+    if (have_cur) {
+      if (won && pa.assume && !fast_b) {
+        cn = -2;
+      } else {
+        const Cand c = wg_combine<B>(sh, p, won && fast_b);
+        cn = c.key ? c.idx : -1;
+      }
+    }
     if (won && pa.assume && tid == ob) {
 #pragma unroll
       for (int j = 0; j < K; ++j)
@@ -2300,34 +2305,73 @@ __device__ __forceinline__ const int32_t* tb_col(const DevState& st, const THist
   return (h.col_kind == 0 ? st.mcnt : st.tcnt) + (size_t)h.col * st.N;
 }
 
+// Wave-aggregated atomics: the lanes targeting one word combine through a DPP reduction and one lane
+// issues the atomic -- every node of a cluster hits the same few words (signature flags, the pair
+// registrations and histogram bins of a few topology domains), which per-lane atomics serialize.
+// Called by every lane of the wave (pend: this lane has a contribution).
+__device__ __forceinline__ void or_agg(uint32_t* base, int word, uint32_t bits, bool pend) {
+  const int lane = threadIdx.x & 63;
+  for (;;) {
+    const uint64_t m = __ballot(pend);
+    if (!m) return;
+    const int leader = (int)__builtin_ctzll(m);
+    const int w0 = __builtin_amdgcn_readlane(word, leader);
+    const bool mine = pend && word == w0;
+    const uint32_t acc = (uint32_t)wave_red64(mine ? bits : 0u, OpOrU64{});
+    if (lane == leader) atomicOr(base + w0, acc);
+    if (mine) pend = false;
+  }
+}
+__device__ __forceinline__ void add_agg(int32_t* base, int idx, int val, bool pend) {
+  const int lane = threadIdx.x & 63;
+  for (;;) {
+    const uint64_t m = __ballot(pend);
+    if (!m) return;
+    const int leader = (int)__builtin_ctzll(m);
+    const int i0 = __builtin_amdgcn_readlane(idx, leader);
+    const bool mine = pend && idx == i0;
+    const uint32_t acc = wave_sum32(mine ? (uint32_t)val : 0u);
+    if (lane == leader) atomicAdd(base + i0, (int)acc);
+    if (mine) pend = false;
+  }
+}
+
 __global__ void k_tbatch_init(const DevState* __restrict__ stp, TBatchArgs ta) {
   const DevState& st = *stp;
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
-  if (n >= st.N) return;
+  const bool on = n < st.N;  // every lane stays in the wave-wide aggregations
+  const int lane = threadIdx.x & 63;
   uint64_t em = 0;
   for (int s = 0; s < ta.n_sigs; ++s) {
     const TSig sg = cp(ta.sigs)[s];
-    bool ok = sg.n_keys >= 0 && node_affinity_ok(st, *cp(st.queries + sg.rep), n);
+    bool ok = on && sg.n_keys >= 0 && node_affinity_ok(st, *cp(st.queries + sg.rep), n);
     for (int k = 0; k < sg.n_keys && ok; ++k) ok = sg.keys[k] >= 0 && gp(st.label_val)[(size_t)sg.keys[k] * st.N + n] >= 0;
-    if (!ok) continue;
-    em |= 1ull << s;
-    atomicOr(gp(ta.elig) + sg.elig_word + (n >> 5), 1u << (n & 31));
-    __hip_atomic_store(gp(ta.sig_any) + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (ok) em |= 1ull << s;
+    or_agg(gp(ta.elig) + sg.elig_word, n >> 5, 1u << (n & 31), ok);
+    const uint64_t any = __ballot(ok);
+    if (any && lane == (int)__builtin_ctzll(any))
+      __hip_atomic_store(gp(ta.sig_any) + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (int r = 0; r < ta.n_regs; ++r) {
       const TReg rg = cp(ta.regs)[r];
-      if (rg.sig != s) continue;
-      const int v = gp(st.label_val)[(size_t)rg.key * st.N + n];
-      atomicOr(gp(ta.reg_init) + rg.word + (v >> 5), 1u << (v & 31));
+      if (rg.sig != s) continue;  // uniform
+      const int v = ok ? gp(st.label_val)[(size_t)rg.key * st.N + n] : 0;
+      or_agg(gp(ta.reg_init) + rg.word, v >> 5, 1u << (v & 31), ok);
     }
   }
   for (int i = 0; i < ta.n_hists; ++i) {
     const THist h = cp(ta.hists)[i];
-    const int c = gp(tb_col(st, h))[n];
-    if (!c) continue;
-    if (h.sig >= 0 && !((em >> h.sig) & 1u)) continue;
-    const int v = h.key >= 0 ? gp(st.label_val)[(size_t)h.key * st.N + n] : -1;
-    if (h.off >= 0) atomicAdd(gp(ta.hist_init) + h.off + (v >= 0 ? v : h.D), c);
-    if (v >= 0) atomicAdd(gp(ta.tot_init) + i, c);
+    const int c = on ? gp(tb_col(st, h))[n] : 0;
+    const bool cnt = c != 0 && (h.sig < 0 || ((em >> h.sig) & 1u));
+    const int v = (cnt && h.key >= 0) ? gp(st.label_val)[(size_t)h.key * st.N + n] : -1;
+    add_agg(gp(ta.hist_init), h.off + (v >= 0 ? v : h.D), c, cnt && h.off >= 0);
+    add_agg(gp(ta.tot_init), i, c, cnt && v >= 0);
+  }
+  if (ta.diag && on) {
+    // a diagnostic (kgpu_schedule_one) run: this node's per-plugin raw / normalized rows start at 0
+    for (int sc = 0; sc < KGPU_NUM_SCORES; ++sc) {
+      gp(st.diag_raw)[(size_t)sc * st.N + n] = 0;
+      gp(st.diag_norm)[(size_t)sc * st.N + n] = 0;
+    }
   }
 }
 
@@ -2380,52 +2424,33 @@ struct TMisc {
   int64_t acc64[2];          // kTIpaMin, kTIpaMax
 };
 
-// The statistics round of one pod, run by ONE wave (the other waves wait at the workgroup barrier,
-// so the polling CU's memory queue carries only this wave's loads): every workgroup published its R
-// slots as one record (row[g * R + slot]); lane l folds records l, l + 64, ... into its partials in
-// GAT[l][slot], then lane `slot` folds the 64 partials into STAT[slot].  False on timeout / abort.
 __device__ __forceinline__ int tslot_op(int rr, int soft_words) {
   return rr < kTFixed ? tstat_op(rr) : (rr < kTFixed + soft_words ? kOpOr : kOpSum);
 }
-__device__ bool tstats_gather(const uint64_t* row, int G, int R, int soft_words, const int32_t* abort_word,
-                              int64_t* GAT, int64_t* STAT) {
+// Wave `w` polls statistics slots w, w + waves, ... of pod row `row`: every workgroup's granule
+// of the slot, combined with the slot's operation.  False on timeout / abort.
+__device__ __forceinline__ bool tpoll_slot(const uint64_t* row, int G, const int32_t* abort_word, int op,
+                                           int64_t& out) {
   const int lane = threadIdx.x & 63;
-  int64_t* mine = GAT + lane * R;
-  if (lane >= G)
-    for (int rr = 0; rr < R; ++rr) mine[rr] = tident(tslot_op(rr, soft_words));
-  bool ok = true;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  for (int gg = lane; gg < G && ok; gg += 64) {
-    const uint64_t* rec = row + (size_t)gg * R;
-    const bool first = gg < 64;
-    for (;;) {
-      // the first record of a lane decodes straight into its partials (overwritten until valid)
-      bool all = true;
-      for (int rr = 0; rr < R; ++rr) {
-        const uint64_t v = load_sc1(rec + rr);
-        all &= (v & kGValid) != 0;
-        if (first) mine[rr] = dec_stat(v);
-      }
-      if (all) break;
-      if (load_sc1(abort_word) != 0 || __builtin_amdgcn_s_memrealtime() - t0 > kSpinTimeout) {
-        ok = false;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-    if (!ok || first) continue;
-    for (int rr = 0; rr < R; ++rr)  // G > 64: later records fold in
-      mine[rr] = tcombine(tslot_op(rr, soft_words), mine[rr], dec_stat(load_sc1(rec + rr)));
-  }
-  ok = __all(ok);
-  if (ok && lane < R) {
-    const int op = tslot_op(lane, soft_words);
+  for (;;) {
+    bool all = true;
     int64_t acc = tident(op);
-    const int n = G < 64 ? G : 64;
-    for (int l = 0; l < n; ++l) acc = tcombine(op, acc, GAT[l * R + lane]);
-    STAT[lane] = acc;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int g = lane + 64 * j;
+      if (g < G) {
+        const uint64_t v = load_sc1(row + g);
+        if (!(v & kGValid)) all = false;
+        else acc = tcombine(op, acc, dec_stat(v));
+      }
+    }
+    if (__all(all)) {
+      out = wave_op_i64(op, acc);
+      return true;
+    }
+    if (load_sc1(abort_word) != 0 || __builtin_amdgcn_s_memrealtime() - t0 > kSpinTimeout) return false;
   }
-  return ok;
 }
 
 // ---- node sharding over xGMI (k_tbatch XG): the topology mailbox ring (kgpu_internal.h TX row)
@@ -2661,7 +2686,6 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
   int32_t* ZSUM = reinterpret_cast<int32_t*>(lds_raw + ta.o_zsum);
   int64_t* PT = reinterpret_cast<int64_t*>(lds_raw + ta.o_pt);
   int32_t* LAB = reinterpret_cast<int32_t*>(lds_raw + ta.o_lab);  // [lab_keys][per] label value ids
-  int64_t* GAT = reinterpret_cast<int64_t*>(lds_raw + ta.o_gat);  // [64][R] statistics poll partials
   TMisc& M = *reinterpret_cast<TMisc*>(lds_raw + ta.o_misc);
   constexpr int W = B / 64;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -2829,7 +2853,7 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
     }
     __syncthreads();
     KGPU_WSTAMP(4);
-    uint64_t* srow = ta.gran + (size_t)i * (R + 1) * G;  // [G][R] statistics records | [G] keys
+    uint64_t* srow = ta.gran + (size_t)i * (R + 1) * G;  // [R][G] statistics granules | [G] keys
     if (tid < R) {
       int64_t x;
       switch (tid) {
@@ -2845,7 +2869,7 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
         case kTZoned: x = (uint32_t)M.acc32[7]; break;
         default: x = tid < kTFixed + ta.soft_words ? (int64_t)SMASK[tid - kTFixed] : (int64_t)ZSUM[tid - kTFixed - ta.soft_words];
       }
-      store_sc1(srow + (size_t)g * R + tid, enc_stat(x));  // this workgroup's record
+      store_sc1(srow + (size_t)tid * G + g, enc_stat(x));
     }
     KGPU_TSTAMP(3);
     KGPU_WSTAMP(2);
@@ -2957,20 +2981,23 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
       txrow = sh_ptx[ta.rank] + (size_t)((ta.xseq0 + i) % kTXRing) * txw;
       txtag = kGValid | ((uint64_t)(((ta.xseq0 + i) / kTXRing) & 7) << 60);
     }
-    if (wave == 0) ok = tstats_gather(srow, G, R, ta.soft_words, ta.abort, GAT, STAT);
-    if constexpr (XG) {
-      // this rank's combined slots: workgroup 0 publishes them into every rank's ring; then every
-      // rank's record of each slot, combined: the cluster-wide statistics
-      if (wave == 0 && !ok && lane == 0) M.abort = 1;
-      __syncthreads();
-      ok = !M.abort;
-      for (int rr = wave; ok && rr < R; rr += W) {
-        const int op = tslot_op(rr, ta.soft_words);
-        const int64_t x0 = STAT[rr];
+    for (int rr = wave; rr < R; rr += W) {
+      const int op = tslot_op(rr, ta.soft_words);
+      int64_t x;
+      if (!tpoll_slot(srow + (size_t)rr * G, G, ta.abort, op, x)) { ok = false; break; }
+      if constexpr (XG) {
+        // this rank's combined slot: workgroup 0 publishes it into every rank's ring
         if (g == 0 && lane < ta.nranks) {
           const size_t off = (size_t)(txrow - sh_ptx[ta.rank]) + (size_t)ta.rank * kTXRCap + rr;
-          store_sys(sh_ptx[lane] + off, txtag | (uint64_t)(x0 + kTXBias));
+          store_sys(sh_ptx[lane] + off, txtag | (uint64_t)(x + kTXBias));
         }
+      }
+      if (lane == 0) STAT[rr] = x;
+    }
+    if constexpr (XG) {
+      // every rank's record of the wave's slots, combined: the cluster-wide statistics
+      for (int rr = wave; ok && rr < R; rr += W) {
+        const int op = tslot_op(rr, ta.soft_words);
         int64_t x;
         if (!xpoll_stat(txrow + rr, ta.nranks, ta.abort, op, txtag, x)) { ok = false; break; }
         if (lane == 0) STAT[rr] = x;
@@ -3241,7 +3268,8 @@ int launch_tbatch_init(const DevState* st, const TBatchArgs& a, int groups, void
 }
 
 // spec: the k_eval profile instantiation (select_spec), def_res from the TBatchArgs
-int launch_tbatch(const DevState* st, const TBatchArgs& a, int groups, int geo, int spec, bool xg, void* stream) {
+int launch_tbatch(const DevState* st, const TBatchArgs& a, int groups, int geo, int spec, bool xg, bool coop,
+                  void* stream) {
   if (geo < 0 || geo >= kNumTGeo) return -1;
   hipStream_t s = (hipStream_t)stream;
   const int row = spec == 2 ? 2 : (spec == 3 ? 3 : (a.def_res ? 1 : 0));
@@ -3257,6 +3285,10 @@ int launch_tbatch(const DevState* st, const TBatchArgs& a, int groups, int geo, 
   TBatchArgs arg = a;
   const DevState* sp = st;
   void* args[] = {(void*)&sp, (void*)&arg};
+  if (!coop) {  // KGPU_OPT_COOPERATIVE off: as launch_batch
+    hipLaunchKernelGGL(fn, dim3(groups), dim3(kTGeo[geo].B), (unsigned)a.lds_bytes, s, sp, arg);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+  }
   return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(fn), dim3(groups), dim3(kTGeo[geo].B), args,
                                     (unsigned)a.lds_bytes, s) == hipSuccess
              ? 0
@@ -3343,7 +3375,7 @@ int batch_geometry(int N, int max_groups, int* per, int* groups) {
   return -1;
 }
 
-int launch_batch(const DevState* st, const BatchArgs& a, int groups, int geo, int spec, void* stream) {
+int launch_batch(const DevState* st, const BatchArgs& a, int groups, int geo, int spec, bool coop, void* stream) {
   if (spec < 0 || spec >= kNumSpecs) spec = 0;
   if (geo < 0 || geo >= kNumGeo) return -1;
   // One workgroup per CU: a dynamic LDS reservation above half a CU's 160 KB keeps the dispatcher
@@ -3362,9 +3394,16 @@ int launch_batch(const DevState* st, const BatchArgs& a, int groups, int geo, in
   BatchArgs arg = a;
   const DevState* sp = st;
   void* args[] = {(void*)&sp, (void*)&arg};
-  if (hipLaunchCooperativeKernel(reinterpret_cast<const void*>(fn), dim3(groups), dim3(kGeo[geo].B + 64),
-                                 args, (unsigned)kBatchLdsPad, (hipStream_t)stream) != hipSuccess)
+  // (coop false, KGPU_OPT_COOPERATIVE: an ordinary launch of the same grid -- at most one workgroup per
+  // CU on an otherwise idle device, so every workgroup is resident; were one not, the spins time out
+  // into the abort word rather than hang)
+  if (!coop) {
+    hipLaunchKernelGGL(fn, dim3(groups), dim3(kGeo[geo].B + 64), (unsigned)kBatchLdsPad, (hipStream_t)stream, sp, arg);
+    if (hipGetLastError() != hipSuccess) return -1;
+  } else if (hipLaunchCooperativeKernel(reinterpret_cast<const void*>(fn), dim3(groups), dim3(kGeo[geo].B + 64),
+                                        args, (unsigned)kBatchLdsPad, (hipStream_t)stream) != hipSuccess) {
     return -1;
+  }
   hipLaunchKernelGGL(k_batch_fixup, dim3((a.count + 255) / 256), dim3(256), 0, (hipStream_t)stream, st, a, groups);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -9,6 +9,7 @@ Usage: python3 tools/exit_probe.py <variant> <maps-out> [--os-exit]
   --os-exit: leave through os._exit(0) after the work (no exit handlers run: does rocprofv3 still write
              its files?  It does not: the tool finalizes in an exit handler)
   --no-persistent: no persistent (cooperative) launch, one k_eval launch per pod
+  --no-coop: persistent kernels through ordinary launches (KGPU_OPT_COOPERATIVE = 0)
   --reset:   hipDeviceReset() before a normal exit (the runtime's queues and allocations released while
              the profiler is still attached)"""
 import os
@@ -32,9 +33,11 @@ def run_kgpu():
     from kgpu.framework import GpuFramework
     nodes, existing, pods, prof = fit_least_balanced(n_nodes=64, n_pods=32)
     fw = GpuFramework(prof, nodes, existing, pods_hint=pods, device=0)
+    from kgpu import abi
     if "--no-persistent" in sys.argv:  # k_eval launches only: no cooperative launch in the process
-        from kgpu import abi
         fw.engine.set_option(abi.OPT_PERSISTENT, 0)
+    if "--no-coop" in sys.argv:  # the persistent kernels through ordinary launches
+        fw.engine.set_option(abi.OPT_COOPERATIVE, 0)
     res = fw.schedule(pods, first_seq=0)
     assert (res["node"] >= 0).sum() > 0
     fw.engine.close()
