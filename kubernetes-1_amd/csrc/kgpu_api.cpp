@@ -8,6 +8,9 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 #include <dlfcn.h>
+#include <execinfo.h>
+#include <signal.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <array>
@@ -18,6 +21,7 @@
 #include <iterator>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstddef>
 #include <cstring>
 #include <deque>
@@ -1350,7 +1354,6 @@ int run_tbatch(kgpu_ctx* c, TRun& tr, int first, int count, int64_t first_seq, i
     c->t_stage_used = 0;
     if (tbytes > c->t_stage_cap) {
       if (c->t_stage_host) (void)hipHostFree(c->t_stage_host);
-  if (c->pool_host) (void)hipHostFree(c->pool_host);
       c->t_stage_host = nullptr;
       c->t_stage_cap = 0;
       const size_t cap = std::max<size_t>(tbytes * 2, 1 << 20);
@@ -2759,8 +2762,20 @@ int kgpu_struct_sizes(int32_t* out, int32_t n) {
   return m;
 }
 
+// KGPU_SEGV_TRACE=1 (diagnostics): a host SIGSEGV prints this library's native backtrace to stderr
+// before the default action (a Python faulthandler shows only the interpreter's frames).
+static void segv_trace(int sig) {
+  void* fr[64];
+  const int n = backtrace(fr, 64);
+  backtrace_symbols_fd(fr, n, 2);
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+
 int kgpu_create(const kgpu_config* cfg, kgpu_ctx** out) try {
   if (!cfg || !out) return KGPU_E_INVAL;
+  if (const char* e = std::getenv("KGPU_SEGV_TRACE"))
+    if (e[0] == '1') signal(SIGSEGV, segv_trace);
   *out = nullptr;
   if (cfg->abi_version != KGPU_ABI_VERSION) return KGPU_E_INVAL;
   if (cfg->n_filters < 0 || cfg->n_filters > KGPU_NUM_FILTERS || cfg->n_scores < 0 ||
