@@ -56,6 +56,7 @@ type profileArgs struct {
 	TieBreakSeed           uint64
 	Mode                   string // "select" or "shadow"
 	ExactSync              bool   // compare every NodeInfo generation at every sync (track.go)
+	BatchAhead             int    // > 1: schedule the pod with the next BatchAhead-1 queued pods (ahead.go)
 	ignoredResources       map[string]struct{}
 }
 
@@ -158,6 +159,7 @@ type GpuEval struct {
 	mir       *mirror
 	seq       int64
 	nominated bool     // the engine holds a non-empty nominator
+	ahead     *ahead   // batch-ahead (ahead.go; profileArgs.BatchAhead > 1, select mode)
 	track     *tracker // nodes whose NodeInfo may have moved since the last sync (track.go)
 	exact     bool     // compare every generation at every sync
 	syncs     int
@@ -414,8 +416,27 @@ func (g *GpuEval) snapshotSoA(list []*framework.NodeInfo, m *mirror, a *arena) (
 	return s, nil
 }
 
-// PreFilter: sync the device mirror to this cycle's Snapshot, compile the pod, run the cycle.
+// PreFilter: sync the device mirror to this cycle's Snapshot, compile the pod, run the cycle.  With
+// batch-ahead the cycle may be served from (or start) a batch of the pods the queue pops next.
 func (g *GpuEval) PreFilter(ctx context.Context, cs *framework.CycleState, pod *v1.Pod) *framework.Status {
+	seq := atomic.AddInt64(&g.seq, 1) - 1
+	if g.ahead != nil {
+		res, ok, err := g.serveAhead(pod, seq)
+		if err != nil {
+			return framework.NewStatus(framework.Error, err.Error())
+		}
+		if ok && res.node >= 0 {
+			cs.Write(stateKey, &cycle{chosen: int32(res.node), index: g.mir.index})
+			return nil
+		}
+		if ok {
+			// unschedulable in the batch: its FitError statuses come from a diagnostic cycle on the
+			// state without the speculation
+			if err := g.invalidate(); err != nil {
+				return framework.NewStatus(framework.Error, err.Error())
+			}
+		}
+	}
 	if err := g.syncSnapshot(); err != nil {
 		return framework.NewStatus(framework.Error, err.Error())
 	}
@@ -434,8 +455,23 @@ func (g *GpuEval) PreFilter(ctx context.Context, cs *framework.CycleState, pod *
 			return framework.NewStatus(framework.Error, err.Error())
 		}
 	}
+	if g.ahead != nil && !g.nominated {
+		if res, ok, err := g.startBatch(pod, q, p, seq); err != nil {
+			return framework.NewStatus(framework.Error, err.Error())
+		} else if ok && res.node >= 0 {
+			cs.Write(stateKey, &cycle{chosen: int32(res.node), index: g.mir.index})
+			return nil
+		} else if ok {
+			if err := g.invalidate(); err != nil { // FitError: statuses from a diagnostic cycle
+				return framework.NewStatus(framework.Error, err.Error())
+			}
+			if err := g.syncSnapshot(); err != nil {
+				return framework.NewStatus(framework.Error, err.Error())
+			}
+		}
+	}
 	cq := cQueries(&a, []C.kgpu_pod_query{q})
-	res, _, err := g.eng.scheduleOne(cq, p.toC(&a), atomic.AddInt64(&g.seq, 1)-1, false)
+	res, _, err := g.eng.scheduleOne(cq, p.toC(&a), seq, false)
 	if err != nil {
 		return framework.NewStatus(framework.Error, err.Error())
 	}
@@ -471,6 +507,12 @@ func (g *GpuEval) Filter(ctx context.Context, cs *framework.CycleState, pod *v1.
 	c, err := readCycle(cs)
 	if err != nil {
 		return framework.NewStatus(framework.Error, err.Error())
+	}
+	if c.words == nil { // a batch-served cycle: the chosen node passes, the framework takes it unscored
+		if c.index[ni.Node().Name] == c.chosen {
+			return nil
+		}
+		return framework.NewStatus(framework.Unschedulable, "node(s) were not chosen by the batched cycle")
 	}
 	w := c.words[g.mir.index[ni.Node().Name]]
 	if w == 0 || w == C.KGPU_FS_NOT_EVALUATED {
@@ -514,6 +556,9 @@ func New(obj runtime.Object, h framework.FrameworkHandle) (framework.Plugin, err
 		return nil, err
 	}
 	g := &GpuEval{h: h, prof: prof, track: newTracker(), exact: prof.ExactSync}
+	if prof.BatchAhead > 1 && prof.Mode != "shadow" {
+		g.ahead = &ahead{depth: prof.BatchAhead}
+	}
 	g.watch()
 	return g, nil
 }

@@ -65,6 +65,17 @@ func (t *tracker) take() []string {
 	return out
 }
 
+// peek returns the marked nodes without aging the marks.
+func (t *tracker) peek() []string {
+	t.mu.Lock()
+	defer t.mu.Unlock()
+	out := make([]string, 0, len(t.marks))
+	for n := range t.marks {
+		out = append(out, n)
+	}
+	return out
+}
+
 // settle drops the mark of a node whose change was applied.
 func (t *tracker) settle(node string) {
 	t.mu.Lock()

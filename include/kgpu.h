@@ -430,6 +430,16 @@ int kgpu_debug_pts_state(kgpu_ctx* ctx, const kgpu_pod_query* q, const kgpu_pool
 /* Mirror coherence: ForgetPod / RemovePod of an existing pod slot (cache.go:383-410). */
 int kgpu_forget_pod(kgpu_ctx* ctx, int32_t pod_slot);
 
+/* Batch-ahead (a caller that runs kgpu_schedule_batch with assume for the pods its queue pops next,
+ * then serves the per-pod cycles from the results): the slot the next pod assumed by
+ * kgpu_schedule_* will get (slots are consecutive in batch order, placed pods only), and adoption --
+ * when the scheduler's own cache.AssumePod (cache.go:338-361) lands the pod on the node the device
+ * already assumed it on, the pod's UID is registered for that slot, so later deltas (REMOVE_POD by
+ * UID) address it and no ADD_POD is sent for it.  A speculative assume that is not adopted is undone
+ * with kgpu_forget_pod. */
+int kgpu_next_slot(const kgpu_ctx* ctx);
+int kgpu_adopt_pod(kgpu_ctx* ctx, int32_t pod_slot, int64_t uid);
+
 /* ---- delta stream (kgpu_apply_delta).  The caller keeps the scheduler cache's bookkeeping
  * (podStates / assumedPods / nodeTree, cache.go) and sends the NodeInfo changes it implies; the
  * engine applies them to the device mirror in one launch and de-duplicates pods by UID. */

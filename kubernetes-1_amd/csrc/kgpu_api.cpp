@@ -3491,6 +3491,26 @@ int kgpu_forget_pod(kgpu_ctx* c, int32_t slot) try {
   return on_exception(c, true);
 }
 
+int kgpu_next_slot(const kgpu_ctx* c) { return c ? (int)std::min<size_t>(c->recs.size(), INT32_MAX) : -1; }
+
+int kgpu_adopt_pod(kgpu_ctx* c, int32_t slot, int64_t uid) try {
+  if (!c) return KGPU_E_INVAL;
+  if (!c->uploaded) return fail(c, KGPU_E_STATE, "no snapshot uploaded");
+  if (slot < 0 || slot >= (int32_t)c->recs.size() || !c->recs[(size_t)slot].active || !c->recs[(size_t)slot].has_res)
+    return fail(c, KGPU_E_INVAL, "no pod assumed by kgpu_schedule_* at this slot");
+  kgpu_ctx::PodRec& a = c->recs[(size_t)slot];
+  if (a.has_uid && a.uid == uid) return KGPU_OK;
+  auto it = c->uid_slot.find(uid);
+  if (it != c->uid_slot.end()) return fail(c, KGPU_E_STATE, "the pod uid is already on a node");
+  if (a.has_uid) c->uid_slot.erase(a.uid);
+  a.uid = uid;
+  a.has_uid = true;
+  c->uid_slot.emplace(uid, slot);
+  return KGPU_OK;
+} catch (...) {
+  return on_exception(c, false);
+}
+
 int kgpu_apply_delta(kgpu_ctx* c, const kgpu_delta_batch* b, int64_t generation, int32_t* slots) try {
   if (!c || !b) return KGPU_E_INVAL;
   if (!c->uploaded) return fail(c, KGPU_E_STATE, "no snapshot uploaded");

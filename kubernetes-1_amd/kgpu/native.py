@@ -20,7 +20,8 @@ EXPORTS = ["kgpu_abi_version", "kgpu_struct_sizes", "kgpu_create", "kgpu_destroy
            "kgpu_read_phase_trace", "kgpu_comm_unique_id", "kgpu_comm_init", "kgpu_apply_delta",
            "kgpu_set_nominated", "kgpu_select_victims", "kgpu_xgmi_handle", "kgpu_xgmi_init", "kgpu_xgmi_active",
            "kgpu_debug_fail_alloc", "kgpu_debug_pts_state", "kgpu_debug_broken_linear",
-           "kgpu_debug_wg_trace"]
+           "kgpu_debug_wg_trace",
+           "kgpu_next_slot", "kgpu_adopt_pod"]
 
 
 class KgpuError(RuntimeError):
@@ -65,6 +66,8 @@ def lib():
     L.kgpu_debug_pts_state.argtypes = [vp, vp, C.POINTER(abi.Pools), i32, i32, vp, vp, C.POINTER(i64)]
     L.kgpu_debug_broken_linear.argtypes = [vp, vp, i32, vp, i32, vp]
     L.kgpu_debug_wg_trace.argtypes = [vp, vp, i64, C.POINTER(i32)]
+    L.kgpu_next_slot.argtypes = [vp]
+    L.kgpu_adopt_pod.argtypes = [vp, i32, i64]
     L.kgpu_select_victims.argtypes = [vp, vp, C.POINTER(abi.Pools), C.POINTER(abi.PreemptArgs), vp, vp,
                                       C.POINTER(i32)]
     if L.kgpu_abi_version() != abi.ABI_VERSION:
@@ -219,6 +222,14 @@ class Engine:
         self._check(lib().kgpu_debug_pts_state(self.h, q.ctypes.data, C.byref(pools), kind, constraint,
                                                 reg.ctypes.data, cnt.ctypes.data, C.byref(out)))
         return reg[:n_values].astype(bool), cnt[:n_values], int(out.value)
+
+    def next_slot(self):
+        """kgpu_next_slot: the slot the next pod assumed by kgpu_schedule_* gets."""
+        return int(lib().kgpu_next_slot(self.h))
+
+    def adopt_pod(self, slot, uid):
+        """kgpu_adopt_pod: register the UID of a pod the device assumed in a batch (batch-ahead)."""
+        self._check(lib().kgpu_adopt_pod(self.h, int(slot), int(uid)))
 
     def wg_trace(self, pods):
         """kgpu_debug_wg_trace: [pods][groups][8] per-workgroup stamps of the last traced k_tbatch run."""
