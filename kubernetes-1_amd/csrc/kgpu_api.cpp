@@ -183,6 +183,11 @@ struct kgpu_ctx {
   void* cyc_host = nullptr;                        // pinned staging of a short cycle: DevState + queries
   void* res_pin = nullptr;                         // pinned coherent block the short cycle's kernels
   kgpu_result* res_dev = nullptr;                  // write their result records into (its device address)
+  // short-cycle arena (arena_put): bump offset and capacity in cyc_host / dstate, the byte range
+  // still to be copied, and whether a copy from cyc_host may still be pending on the stream
+  size_t ar_used = 0, ar_cap = 0, ar_lo = 0, ar_hi = 0;
+  bool ar_on = false, ar_inflight = false;
+  bool tb_abort_mapped = false;                    // the last k_tbatch run wrote its abort word to res_pin
   DevState ds_last{};                              // the DevState image last uploaded by a short cycle
   const void* ds_ptr = nullptr;                    // ... into this dstate allocation (null: none)
   size_t stage_cap = 0;
@@ -325,6 +330,72 @@ int ensure(kgpu_ctx* c, DevBuf& b, size_t bytes) {
   return KGPU_OK;
 }
 
+// ---- short-cycle arena.  A short cycle (kgpu_schedule_one, small batches) stages what it must send
+// -- changed query pools, topology plans, DevState + queries, a one-pod persistent topology run's
+// tables and zeroed words -- in the pinned block c->cyc_host, at the offsets they take in the device
+// block c->dstate, and moves them with ONE copy (arena_flush, before the cycle's first launch that
+// reads them): each stream operation saved is several microseconds of the per-cycle latency.  Items
+// that do not fit take their own copies.  The arena is live only inside run_batch (ArenaScope).
+constexpr size_t kArenaBytes = 1 << 20;
+// Short cycles: at most kShortCycle pods.  Device block c->dstate = DevState | n queries (at
+// kDsQueryOff) | the cycle's arena; pinned c->cyc_host = the same image.  The kernels write the
+// result records into the pinned block c->res_pin (kCycResBytes), a k_tbatch run its abort word
+// right after them.
+constexpr int32_t kShortCycle = 64;
+constexpr size_t kDsQueryOff = (sizeof(DevState) + 255) & ~(size_t)255;
+constexpr size_t kCycHostBytes = kDsQueryOff + sizeof(kgpu_pod_query) * kShortCycle + kArenaBytes;
+constexpr size_t kCycResBytes = sizeof(kgpu_result) * kShortCycle;
+constexpr size_t kCycAbortOff = kCycResBytes;  // int32 in res_pin
+
+void arena_mark(kgpu_ctx* c, size_t lo, size_t hi) {
+  if (c->ar_hi <= c->ar_lo) {
+    c->ar_lo = lo;
+    c->ar_hi = hi;
+  } else {
+    c->ar_lo = std::min(c->ar_lo, lo);
+    c->ar_hi = std::max(c->ar_hi, hi);
+  }
+}
+
+// `bytes` of the arena: host and device addresses (false: no arena, or full)
+bool arena_reserve(kgpu_ctx* c, size_t bytes, char** host, char** dev) {
+  if (!c->ar_on) return false;
+  const size_t o = c->ar_used, sz = (std::max<size_t>(bytes, 16) + 15) & ~(size_t)15;
+  if (o + sz > c->ar_cap) return false;
+  c->ar_used = o + sz;
+  arena_mark(c, o, o + bytes);
+  *host = static_cast<char*>(c->cyc_host) + o;
+  *dev = static_cast<char*>(c->dstate.p) + o;
+  return true;
+}
+
+// a copy of `src` (zeros when null) in the arena: its device address, or null
+void* arena_put(kgpu_ctx* c, const void* src, size_t bytes) {
+  char *h, *d;
+  if (!arena_reserve(c, bytes, &h, &d)) return nullptr;
+  if (src) std::memcpy(h, src, bytes);
+  else std::memset(h, 0, bytes);
+  return d;
+}
+
+int arena_flush(kgpu_ctx* c) {
+  if (c->ar_hi > c->ar_lo) {
+    HIP_OK(c, hipMemcpyAsync(static_cast<char*>(c->dstate.p) + c->ar_lo, static_cast<char*>(c->cyc_host) + c->ar_lo,
+                             c->ar_hi - c->ar_lo, hipMemcpyHostToDevice, c->stream));
+    c->ar_inflight = true;
+  }
+  c->ar_lo = c->ar_hi = 0;
+  return KGPU_OK;
+}
+
+struct ArenaScope {
+  kgpu_ctx* c;
+  ~ArenaScope() {
+    c->ar_on = false;
+    c->ar_lo = c->ar_hi = 0;
+  }
+};
+
 template <class T>
 int upload_pool(kgpu_ctx* c, DevBuf& b, const T* src, int32_t n, const T** dst) {
   int rc = ensure(c, b, sizeof(T) * (size_t)std::max(n, 1));
@@ -398,12 +469,17 @@ int upload_pools(kgpu_ctx* c, const kgpu_pools* p) {
   if ((rc = ensure(c, c->pool_blk, total))) return rc;
   const bool current = c->pool_blk.shadow_p == c->pool_blk.p && c->pool_blk.shadow.size() == total &&
                        std::memcmp(c->pool_blk.shadow.data(), h, total) == 0;
-  if (!current) {
-    HIP_OK(c, hipMemcpyAsync(c->pool_blk.p, h, total, hipMemcpyHostToDevice, c->stream));
-    c->pool_blk.shadow.assign(h, h + total);
-    c->pool_blk.shadow_p = c->pool_blk.p;
-  }
   const char* d = static_cast<const char*>(c->pool_blk.p);
+  if (!current) {
+    // a short cycle's changed pools ride in its arena copy (pool_blk and its shadow stay as they were)
+    if (const void* a = arena_put(c, h, total)) {
+      d = static_cast<const char*>(a);
+    } else {
+      HIP_OK(c, hipMemcpyAsync(c->pool_blk.p, h, total, hipMemcpyHostToDevice, c->stream));
+      c->pool_blk.shadow.assign(h, h + total);
+      c->pool_blk.shadow_p = c->pool_blk.p;
+    }
+  }
   q.reqs = reinterpret_cast<const kgpu_req*>(d + o_req);
   q.ints = reinterpret_cast<const int32_t*>(d + o_int);
   q.words = reinterpret_cast<const uint64_t*>(d + o_wrd);
@@ -824,6 +900,11 @@ int upload_pod_table(kgpu_ctx* c) {
 
 template <class T>
 int upload_vec(kgpu_ctx* c, DevBuf& b, const std::vector<T>& v, const T** dst) {
+  if (!v.empty())
+    if (const void* a = arena_put(c, v.data(), sizeof(T) * v.size())) {
+      *dst = static_cast<const T*>(a);
+      return KGPU_OK;
+    }
   int rc = ensure(c, b, sizeof(T) * std::max<size_t>(v.size(), 1));
   if (rc) return rc;
   if (!v.empty()) HIP_OK(c, hipMemcpyAsync(b.p, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice, c->stream));
@@ -1349,7 +1430,11 @@ int run_tbatch(kgpu_ctx* c, TRun& tr, int first, int count, int64_t first_seq, i
                o_dl = place(sizeof(kgpu::TDelta) * tr.deltas.v.size()), o_sg = place(sizeof(kgpu::TSig) * tr.sigs.size()),
                o_rg = place(sizeof(kgpu::TReg) * tr.regs.size());
   const size_t tbytes = toff;
-  if (c->t_stage_used + tbytes > c->t_stage_cap) {
+  // a short cycle's tables ride in its arena copy
+  char* th = nullptr;
+  char* tdev = nullptr;
+  const bool t_arena = arena_reserve(c, tbytes, &th, &tdev);
+  if (!t_arena && c->t_stage_used + tbytes > c->t_stage_cap) {
     HIP_OK(c, hipStreamSynchronize(c->stream));
     c->t_stage_used = 0;
     if (tbytes > c->t_stage_cap) {
@@ -1361,7 +1446,7 @@ int run_tbatch(kgpu_ctx* c, TRun& tr, int first, int count, int64_t first_seq, i
       c->t_stage_cap = cap;
     }
   }
-  char* th = static_cast<char*>(c->t_stage_host) + c->t_stage_used;
+  if (!t_arena) th = static_cast<char*>(c->t_stage_host) + c->t_stage_used;
   auto stage = [&](size_t o, const auto& v) {
     if (!v.empty()) std::memcpy(th + o, v.data(), sizeof(v[0]) * v.size());
   };
@@ -1374,10 +1459,13 @@ int run_tbatch(kgpu_ctx* c, TRun& tr, int first, int count, int64_t first_seq, i
   stage(o_dl, tr.deltas.v);
   stage(o_sg, tr.sigs);
   stage(o_rg, tr.regs);
-  if ((rc = ensure(c, c->t_tables, tbytes))) return rc;
-  HIP_OK(c, hipMemcpyAsync(c->t_tables.p, th, tbytes, hipMemcpyHostToDevice, c->stream));
-  c->t_stage_used += tbytes;
-  const char* td = static_cast<const char*>(c->t_tables.p);
+  if (!t_arena) {
+    if ((rc = ensure(c, c->t_tables, tbytes))) return rc;
+    HIP_OK(c, hipMemcpyAsync(c->t_tables.p, th, tbytes, hipMemcpyHostToDevice, c->stream));
+    c->t_stage_used += tbytes;
+    tdev = static_cast<char*>(c->t_tables.p);
+  }
+  const char* td = tdev;
   const kgpu::TPlan* dpl = reinterpret_cast<const kgpu::TPlan*>(td + o_pl);
   const int32_t* dax = reinterpret_cast<const int32_t*>(td + o_ax);
   const int32_t* dpo = reinterpret_cast<const int32_t*>(td + o_po);
@@ -1402,15 +1490,33 @@ int run_tbatch(kgpu_ctx* c, TRun& tr, int first, int count, int64_t first_seq, i
   const size_t b_elig = a16(std::max<size_t>(tr.sigs.size() * ew, 1) * 4);
   const size_t b_gran = (size_t)count * (size_t)(a.R + 1) * (size_t)groups * 8;
   const size_t total = b_hist + b_tot + b_reg + b_sany + b_elig + b_gran;
-  if ((rc = ensure(c, c->t_zero, total))) return rc;
-  HIP_OK(c, hipMemsetAsync(c->t_zero.p, 0, total, c->stream));
-  char* z = static_cast<char*>(c->t_zero.p);
+  // abort_word null: a one-pod run of a short cycle -- its own abort word and workgroup counter after
+  // the zeroed region, and the abort word copied to res_pin by the kernel (run_batch reads it there)
+  const bool own_abort = abort_word == nullptr;
+  char* z = own_abort ? static_cast<char*>(arena_put(c, nullptr, total + 16)) : nullptr;
+  c->tb_abort_mapped = z != nullptr;
+  if (!z) {
+    if ((rc = ensure(c, c->t_zero, total))) return rc;
+    HIP_OK(c, hipMemsetAsync(c->t_zero.p, 0, total, c->stream));
+    z = static_cast<char*>(c->t_zero.p);
+    if (own_abort) {
+      HIP_OK(c, hipMemsetAsync(c->abort_buf.p, 0, 64, c->stream));
+      abort_word = static_cast<int32_t*>(c->abort_buf.p);
+    }
+  }
   a.hist_init = reinterpret_cast<int32_t*>(z);
   a.tot_init = reinterpret_cast<int32_t*>(z + b_hist);
   a.reg_init = reinterpret_cast<uint32_t*>(z + b_hist + b_tot);
   a.sig_any = reinterpret_cast<int32_t*>(z + b_hist + b_tot + b_reg);
   a.elig = reinterpret_cast<uint32_t*>(z + b_hist + b_tot + b_reg + b_sany);
   a.gran = reinterpret_cast<uint64_t*>(z + b_hist + b_tot + b_reg + b_sany + b_elig);
+  if (c->tb_abort_mapped) {
+    abort_word = reinterpret_cast<int32_t*>(z + total);
+    a.done = abort_word + 1;
+    int32_t* out = reinterpret_cast<int32_t*>(static_cast<char*>(c->res_pin) + kCycAbortOff);
+    __atomic_store_n(out, -1, __ATOMIC_RELEASE);  // overwritten by the kernel's last workgroup
+    a.abort_out = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(c->res_dev) + kCycAbortOff);
+  }
   a.abort = abort_word;
   a.abort_at = c->abort_at >= first && c->abort_at < first + count ? c->abort_at - first : -1;
   a.trace = nullptr;
@@ -1425,6 +1531,7 @@ int run_tbatch(kgpu_ctx* c, TRun& tr, int first, int count, int64_t first_seq, i
     c->trace_wg_host.assign(ww, 0);
     c->trace_wg_groups = groups;
   }
+  if ((rc = arena_flush(c))) return rc;  // the short cycle's one copy: DevState, queries, pools, tables, zeros
   const DevState* dst = static_cast<const DevState*>(c->dstate.p);
   if (kgpu::launch_tbatch_init(dst, a, groups, c->stream))
     return fail(c, KGPU_E_DEVICE, "k_tbatch_init launch failed");
@@ -1662,14 +1769,6 @@ int stage_topology(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_
   return KGPU_OK;
 }
 
-// Short cycles: at most kShortCycle pods.  Device block c->dstate = DevState | queries (at
-// kDsQueryOff); pinned c->cyc_host = the same image, then the results read back (at kCycResOff).
-constexpr int32_t kShortCycle = 64;
-constexpr size_t kDsQueryOff = (sizeof(DevState) + 255) & ~(size_t)255;
-constexpr size_t kCycResOff = (kDsQueryOff + sizeof(kgpu_pod_query) * kShortCycle + 255) & ~(size_t)255;
-constexpr size_t kCycResBytes = sizeof(kgpu_result) * kShortCycle;
-constexpr size_t kCycHostBytes = kCycResOff + kCycResBytes;
-
 int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools* pools, int64_t first_seq,
               kgpu_result* results, kgpu_stats* stats, bool diag, int32_t assume) {
   if (!c->uploaded) return fail(c, KGPU_E_STATE, "no snapshot uploaded");
@@ -1696,6 +1795,31 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
       return KGPU_OK;
     }
   }
+  // A short cycle (kgpu_schedule_one, small batches) moves what it sends -- DevState, queries and the
+  // items of its arena -- with ONE copy from pinned memory into one device block, and its kernels
+  // write the result records straight into pinned host memory: every stream operation saved is
+  // several microseconds of the per-cycle latency.
+  const bool short_cycle = n <= kShortCycle;
+  ArenaScope arena_scope{c};
+  if (short_cycle) {
+    if (!c->cyc_host) HIP_OK(c, hipHostMalloc(&c->cyc_host, kCycHostBytes, hipHostMallocDefault));
+    if ((rc = ensure(c, c->dstate, kCycHostBytes))) return rc;
+    if (!c->res_pin) {
+      HIP_OK(c, hipHostMalloc(&c->res_pin, kCycResBytes + 64, hipHostMallocCoherent | hipHostMallocMapped));
+      void* d = nullptr;
+      HIP_OK(c, hipHostGetDevicePointer(&d, c->res_pin, 0));
+      c->res_dev = static_cast<kgpu_result*>(d);
+    }
+    // the previous cycle's arena copy may still read cyc_host when that cycle failed before its
+    // stream synchronize
+    if (c->ar_inflight) HIP_OK(c, hipStreamSynchronize(c->stream));
+    c->ar_inflight = false;
+    c->ar_on = true;
+    c->ar_used = (kDsQueryOff + sizeof(kgpu_pod_query) * (size_t)n + 255) & ~(size_t)255;
+    c->ar_cap = kCycHostBytes;
+    c->ar_lo = c->ar_hi = 0;
+  }
+  c->tb_abort_mapped = false;
   Staged sg;
   if ((rc = stage_topology(c, qs, n, pools, sg))) return rc;
   std::vector<kgpu::QPlan>& plans = sg.plans;
@@ -1707,21 +1831,7 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
     for (int32_t i = 0; i < n; ++i) batch_ports += qs[i].ports.count;
   if ((rc = reserve_ports(c, batch_ports))) return rc;
   if ((rc = upload_pools(c, pools))) return rc;
-  // A short cycle (kgpu_schedule_one, small batches) moves its DevState and queries with ONE copy
-  // from pinned memory -- the queries sit right after the DevState in the same device block -- and
-  // reads its results, abort word and port-overflow word back with one copy: every stream
-  // operation saved is several microseconds of the per-cycle latency.
-  const bool short_cycle = n <= kShortCycle;
-  if (short_cycle) {
-    if (!c->cyc_host) HIP_OK(c, hipHostMalloc(&c->cyc_host, kCycHostBytes, hipHostMallocDefault));
-    if ((rc = ensure(c, c->dstate, kDsQueryOff + sizeof(kgpu_pod_query) * kShortCycle))) return rc;
-    if (!c->res_pin) {
-      HIP_OK(c, hipHostMalloc(&c->res_pin, kCycResBytes, hipHostMallocCoherent | hipHostMallocMapped));
-      void* d = nullptr;
-      HIP_OK(c, hipHostGetDevicePointer(&d, c->res_pin, 0));
-      c->res_dev = static_cast<kgpu_result*>(d);
-    }
-  } else {
+  if (!short_cycle) {
     if ((rc = ensure(c, c->queries, sizeof(kgpu_pod_query) * (size_t)n))) return rc;
     HIP_OK(c, hipMemcpyAsync(c->queries.p, qs, sizeof(kgpu_pod_query) * (size_t)n, hipMemcpyHostToDevice, c->stream));
     if ((rc = ensure(c, c->results, sizeof(kgpu_result) * (size_t)n))) return rc;
@@ -1771,14 +1881,14 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
   if (short_cycle) {
     char* h = static_cast<char*>(c->cyc_host);
     const bool ds_same = c->ds_ptr == c->dstate.p && std::memcmp(&c->ds_last, &c->st_batch, sizeof(DevState)) == 0;
+    // staged only: the arena copy (arena_flush, below or in run_tbatch) moves it
     if (!inline_q) {
       std::memcpy(h, &c->st_batch, sizeof(DevState));
       std::memcpy(h + kDsQueryOff, qs, sizeof(kgpu_pod_query) * (size_t)n);
-      HIP_OK(c, hipMemcpyAsync(c->dstate.p, h, kDsQueryOff + sizeof(kgpu_pod_query) * (size_t)n, hipMemcpyHostToDevice,
-                               c->stream));
+      arena_mark(c, 0, kDsQueryOff + sizeof(kgpu_pod_query) * (size_t)n);
     } else if (!ds_same) {
       std::memcpy(h, &c->st_batch, sizeof(DevState));
-      HIP_OK(c, hipMemcpyAsync(c->dstate.p, h, sizeof(DevState), hipMemcpyHostToDevice, c->stream));
+      arena_mark(c, 0, sizeof(DevState));
     }
     c->ds_last = c->st_batch;
     c->ds_ptr = c->dstate.p;
@@ -1851,8 +1961,11 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
                        ? kgpu::tbatch_geometry(st.N, std::min(c->max_groups > 0 ? std::min(c->max_groups, c->n_cus) : c->n_cus, 256),
                                                &tper, &tgroups)
                        : -1;
+  // A one-pod persistent topology run (kgpu_schedule_one of a topology pod) keeps its abort word in
+  // the arena, and k_tbatch copies it into res_pin at exit: no memset, no read-back copy.
+  const bool tb_arena = short_cycle && n == 1 && topo[0] && tgeo >= 0 && !xg && c->ar_on;
   // zeroed only when a persistent run can start (a one-launch-per-pod cycle never reads it)
-  if (kidx >= 0 || tgeo >= 0) HIP_OK(c, hipMemsetAsync(c->abort_buf.p, 0, 64, c->stream));
+  if (kidx >= 0 || (tgeo >= 0 && !tb_arena)) HIP_OK(c, hipMemsetAsync(c->abort_buf.p, 0, 64, c->stream));
   std::deque<TRun> runs;
   int32_t scratch_zeroed_for = -1;
   int32_t i = 0;
@@ -1866,7 +1979,9 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
       while (j < n && topo[(size_t)j] && t_add(tr, c, qs[j], plans[(size_t)j], pp, aux, aux_terms, j)) ++j;
       if (j > i) {
         if (c->timing) HIP_OK(c, hipEventRecord(get_event(c, ev), c->stream));
-        if ((rc = run_tbatch(c, tr, i, j - i, first_seq, assume, tper, tgroups, tgeo, abort_word, xg, diag))) return rc;
+        if ((rc = run_tbatch(c, tr, i, j - i, first_seq, assume, tper, tgroups, tgeo, tb_arena ? nullptr : abort_word, xg,
+                             diag)))
+          return rc;
         if (diag) diag_zeroed = true;  // k_tbatch_init zeroed the rows (a diagnostic run is one pod)
         if (c->timing) HIP_OK(c, hipEventRecord(get_event(c, ev + 1), c->stream));
         ev += 2;
@@ -1876,6 +1991,7 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
         continue;
       }
     }
+    if ((rc = arena_flush(c))) return rc;  // every other launch reads DevState / queries / pools from it
     if (topo[(size_t)i]) {
       if ((rc = zero_diag_rows())) return rc;
       const kgpu::QPlan& pl = plans[(size_t)i];
@@ -2080,12 +2196,19 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
   kgpu_result* res_host = short_cycle ? static_cast<kgpu_result*>(c->res_pin) : results;
   if (!short_cycle)
     HIP_OK(c, hipMemcpyAsync(res_host, st.results, sizeof(kgpu_result) * (size_t)n, hipMemcpyDeviceToHost, c->stream));
-  if (used_persistent)
+  if (used_persistent && !c->tb_abort_mapped)
     HIP_OK(c, hipMemcpyAsync(&c->abort_host, abort_word, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
   int32_t port_overflow = 0;
   if (batch_ports) HIP_OK(c, hipMemcpyAsync(&port_overflow, c->st.port_overflow, 4, hipMemcpyDeviceToHost, c->stream));
   HIP_OK(c, hipStreamSynchronize(c->stream));
+  c->ar_inflight = false;
   if (short_cycle) std::memcpy(results, res_host, sizeof(kgpu_result) * (size_t)n);
+  if (used_persistent && c->tb_abort_mapped) {
+    // k_tbatch's last workgroup wrote the abort word (-1 left by the host: the run never finished)
+    const int32_t w = __atomic_load_n(reinterpret_cast<int32_t*>(static_cast<char*>(c->res_pin) + kCycAbortOff),
+                                      __ATOMIC_ACQUIRE);
+    c->abort_host = w != 0 ? 1 : 0;
+  }
   c->port_bound += batch_ports;
   if (port_overflow) {
     c->uploaded = false;

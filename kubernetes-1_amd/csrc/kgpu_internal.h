@@ -384,6 +384,9 @@ struct TBatchArgs {
   uint32_t* elig;         // [n_sigs][ceil(N/32)]
   uint64_t* gran;         // per pod: [R][groups] statistics granules, then [groups] key granules; zeroed
   int32_t* abort;
+  int32_t* done;          // null, or a zeroed counter of workgroups that left the pod loop ...
+  int32_t* abort_out;     // ... and the pinned host word the last of them copies the abort word into
+                          // (a short cycle reads it after its stream synchronize: no read-back copy)
   int32_t lds_bytes;
   int32_t def_res;        // Least/Most over {cpu: 1, memory: 1}
   int32_t pt_words;       // largest per-pod table area of the run (int64 words)

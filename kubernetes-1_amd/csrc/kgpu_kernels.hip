@@ -275,16 +275,6 @@ __device__ __forceinline__ void alloc_req(const DevState& st, const kgpu_pod_que
   }
 }
 
-// floor(a / b) for 0 <= a < 2^52, 0 < b < 2^52 from a precomputed inv ~ 1/b: the product is within
-// one of the quotient, and the remainder test makes the result exact.
-__device__ __forceinline__ int64_t div_recip(int64_t a, int64_t b, double inv) {
-  int64_t q = (int64_t)((double)a * inv);
-  const int64_t r = a - q * b;
-  if (r < 0) q -= 1;
-  else if (r >= b) q += 1;
-  return q;
-}
-
 // leastResourceScorer / mostResourceScorer per resource (least_allocated.go:93-101,
 // most_allocated.go:93-107), Go's truncating int64 arithmetic.
 __device__ __forceinline__ int64_t least_one(int64_t cap, int64_t req) {
@@ -295,17 +285,33 @@ __device__ __forceinline__ int64_t most_one(int64_t cap, int64_t req) {
   if (cap == 0 || req > cap) return 0;
   return (req >= 0 && cap > 0) ? div_nonneg(req * 100, cap) : (req * 100) / cap;
 }
-__device__ __forceinline__ int64_t least_one(int64_t cap, int64_t req, double inv) {
-  if (cap == 0 || req > cap) return 0;
-  const int64_t x = (cap - req) * 100;
-  if (inv != 0.0 && x >= 0 && x < (1ll << 52)) return div_recip(x, cap, inv);
-  return least_one(cap, req);
+// floor(x / cap) for 0 <= x <= 100 * cap, 0 < cap < 2^52 (inv ~ 1/cap != 0 only then), without a
+// branch: the quotient is 0..100, so one int32 conversion of the product suffices, and the remainder
+// test makes it exact.  A lane outside that range sets `slow` (the caller re-runs it through the
+// integer division): per-lane branches around the fallback cost more exec-mask updates and taken
+// branches than the arithmetic they skip.
+__device__ __forceinline__ int64_t ratio100(int64_t x, int64_t cap, double inv, bool& slow) {
+  const bool ok = inv != 0.0 && x >= 0 && x <= 100 * cap && x < (1ll << 52);
+  slow = !ok;
+  const int64_t xs = ok ? x : 0;
+  int32_t q = (int32_t)((double)xs * inv);
+  const int64_t r = xs - (int64_t)q * cap;
+  q += r < 0 ? -1 : (r >= cap ? 1 : 0);
+  return q;
 }
-__device__ __forceinline__ int64_t most_one(int64_t cap, int64_t req, double inv) {
-  if (cap == 0 || req > cap) return 0;
-  const int64_t x = req * 100;
-  if (inv != 0.0 && x >= 0 && x < (1ll << 52)) return div_recip(x, cap, inv);
-  return most_one(cap, req);
+__device__ __forceinline__ int64_t least_one(int64_t cap, int64_t req, double inv, bool& slow) {
+  const bool zero = cap == 0 || req > cap;
+  bool s;
+  const int64_t q = ratio100((cap - req) * 100, cap, inv, s);
+  slow |= s && !zero;
+  return zero ? 0 : q;
+}
+__device__ __forceinline__ int64_t most_one(int64_t cap, int64_t req, double inv, bool& slow) {
+  const bool zero = cap == 0 || req > cap;
+  bool s;
+  const int64_t q = ratio100(req * 100, cap, inv, s);
+  slow |= s && !zero;
+  return zero ? 0 : q;
 }
 __device__ __forceinline__ int64_t wdiv(int64_t s, int64_t w) { return s >= 0 ? div_nonneg(s, w) : s / w; }
 __device__ __forceinline__ int64_t half(int64_t s) { return s >= 0 ? (s >> 1) : s / 2; }
@@ -314,7 +320,14 @@ template <bool kDef>
 __device__ __forceinline__ int64_t least_score(const DevState& st, const kgpu_pod_query& q, const NodeRes& nr,
                                                int n) {
   if constexpr (kDef) {
-    return half(least_one(nr.ac, nr.zc + q.score_req[0], nr.ic) + least_one(nr.am, nr.zm + q.score_req[1], nr.im));
+    const int64_t rc = nr.zc + q.score_req[0], rm = nr.zm + q.score_req[1];
+    bool slow = false;
+    int64_t a = least_one(nr.ac, rc, nr.ic, slow), b = least_one(nr.am, rm, nr.im, slow);
+    if (slow) {
+      a = least_one(nr.ac, rc);
+      b = least_one(nr.am, rm);
+    }
+    return half(a + b);
   } else {
     int64_t s = 0;
     for (int i = 0; i < st.n_least; ++i) {
@@ -330,7 +343,14 @@ template <bool kDef>
 __device__ __forceinline__ int64_t most_score(const DevState& st, const kgpu_pod_query& q, const NodeRes& nr,
                                               int n) {
   if constexpr (kDef) {
-    return half(most_one(nr.ac, nr.zc + q.score_req[0], nr.ic) + most_one(nr.am, nr.zm + q.score_req[1], nr.im));
+    const int64_t rc = nr.zc + q.score_req[0], rm = nr.zm + q.score_req[1];
+    bool slow = false;
+    int64_t a = most_one(nr.ac, rc, nr.ic, slow), b = most_one(nr.am, rm, nr.im, slow);
+    if (slow) {
+      a = most_one(nr.ac, rc);
+      b = most_one(nr.am, rm);
+    }
+    return half(a + b);
   } else {
     int64_t s = 0;
     for (int i = 0; i < st.n_most; ++i) {
@@ -1146,7 +1166,11 @@ __device__ __forceinline__ void vm_drain() { __builtin_amdgcn_s_waitcnt(0x0F70);
 template <uint32_t FM, uint32_t SM>
 __device__ __forceinline__ uint64_t node_key(const DevState& st, const kgpu_pod_query& q, const NodeRes& r, int n,
                                              uint64_t tk) {
-  if (run_filters<FM>(st, q, r, n) != 0) {
+  // Scores run on every lane whose wave has a feasible node and are discarded for the infeasible
+  // ones (read-only, in-bounds): a per-lane branch around them costs exec-mask updates on every
+  // evaluation and saves nothing when the wave diverges.
+  const uint32_t fs = run_filters<FM>(st, q, r, n);
+  if (__ballot(fs == 0) == 0) {
     if (q.scalars.count | q.ports.count) vm_drain();
     return 0;
   }
@@ -1154,7 +1178,8 @@ __device__ __forceinline__ uint64_t node_key(const DevState& st, const kgpu_pod_
   run_scores<SM>(st, q, r, n, e, false);
   if (q.scalars.count | q.ports.count) vm_drain();
   const int64_t total = key_total<SM>(st, e.partial, e.taint, e.na);
-  return ((uint64_t)(total + 1) << 40) | rank40(tk, (uint64_t)(st.node_base + n), st.tie_mode);
+  const uint64_t key = ((uint64_t)(total + 1) << 40) | rank40(tk, (uint64_t)(st.node_base + n), st.tie_mode);
+  return fs ? 0 : key;
 }
 
 struct Cand {
@@ -1182,7 +1207,6 @@ struct BatchShared {
   int bready;                       // p + 1 once brow[p & 1] is written
   int cslow[2];                     // slow path: candidate of pod p
   int cready;                       // p + 1 once cslow[p & 1] is written
-  int pcount;                       // row waves that wrote their partials (W per pod)
 };
 
 __device__ __forceinline__ void lds_release(int* f, int v) {
@@ -1255,7 +1279,6 @@ __device__ __forceinline__ void wg_partials(BatchShared<B>& sh, int p, const uin
   if (lane == 0) {
     sh.ka[p][wave] = a.key; sh.ia[p][wave] = a.idx; sh.fa[p][wave] = a.feas;
     sh.kb[p][wave] = b.key; sh.ib[p][wave] = b.idx; sh.fb[p][wave] = b.feas;
-    __hip_atomic_fetch_add(&sh.pcount, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
 }
 
@@ -1384,7 +1407,6 @@ __global__ __launch_bounds__(B + 64) void k_batch(const DevState* __restrict__ s
   if (tid == 0) {
     sh.bready = 0;
     sh.cready = 0;
-    sh.pcount = 0;
   }
   __syncthreads();
   auto ring_row = [&](int k) -> size_t { return xg ? (size_t)((pa.xseq0 + k) % pa.R) : (size_t)k; };
@@ -1508,7 +1530,7 @@ __global__ __launch_bounds__(B + 64) void k_batch(const DevState* __restrict__ s
     if (!spare_slot(j, K, tid, B) && n < st.N) {
       r[j] = load_res(st, n);
       // Allocatable never changes inside the run: LeastAllocated / MostAllocated divide through
-      // exact reciprocal-plus-remainder-correction division (div_recip)
+      // exact reciprocal-plus-remainder-correction division (ratio100)
       if constexpr ((SM & kDefRes) != 0 && SM != kRuntime) set_recips(r[j]);
     }
   }
@@ -2336,11 +2358,39 @@ __device__ __forceinline__ void add_agg(int32_t* base, int idx, int val, bool pe
   }
 }
 
+// The kernel is one short pass per node, so its time is the chain of dependent loads: the
+// histogram columns and their label values (independent of the signature pass) are issued for the
+// first kInitPre histograms before anything else and land while the signatures evaluate.
+constexpr int kInitPre = 8;
+
+// LH: the histogram bins and totals are first summed in the workgroup's LDS (lds_bins + n_hists
+// int32, zeroed here) and flushed with one global atomic per non-zero bin -- a zone histogram gives
+// every wave as many distinct bins as there are zones, which the wave-aggregated form serializes.
+// Without LH (bins beyond kInitLdsBins) the wave-aggregated atomics go straight to global memory.
+constexpr int kInitLdsBins = 16384;
+
+template <bool LH>
 __global__ void k_tbatch_init(const DevState* __restrict__ stp, TBatchArgs ta) {
   const DevState& st = *stp;
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
   const bool on = n < st.N;  // every lane stays in the wave-wide aggregations
   const int lane = threadIdx.x & 63;
+  extern __shared__ int32_t lh[];  // LH: [lds_bins] bins | [n_hists] totals
+  const int nlh = ta.lds_bins + ta.n_hists;
+  if constexpr (LH) {
+    for (int b = threadIdx.x; b < nlh; b += blockDim.x) lh[b] = 0;
+  }
+  int pc[kInitPre], pv[kInitPre];
+#pragma unroll
+  for (int i = 0; i < kInitPre; ++i) {
+    pc[i] = 0;
+    pv[i] = -1;
+    if (i < ta.n_hists && on) {
+      const THist h = cp(ta.hists)[i];
+      pc[i] = gp(tb_col(st, h))[n];
+      if (h.key >= 0) pv[i] = gp(st.label_val)[(size_t)h.key * st.N + n];
+    }
+  }
   uint64_t em = 0;
   for (int s = 0; s < ta.n_sigs; ++s) {
     const TSig sg = cp(ta.sigs)[s];
@@ -2358,13 +2408,34 @@ __global__ void k_tbatch_init(const DevState* __restrict__ stp, TBatchArgs ta) {
       or_agg(gp(ta.reg_init) + rg.word, v >> 5, 1u << (v & 31), ok);
     }
   }
-  for (int i = 0; i < ta.n_hists; ++i) {
+  if constexpr (LH) __syncthreads();  // the zeroed bins (the signature pass above hid the wait)
+  auto hist = [&](int i, const THist& h, int c, int v) {
+    const bool cnt = c != 0 && (h.sig < 0 || ((em >> h.sig) & 1u));
+    if (!cnt) v = -1;
+    if constexpr (LH) {
+      if (cnt && h.off >= 0) atomicAdd(lh + h.off + (v >= 0 ? v : h.D), c);
+      if (cnt && v >= 0) atomicAdd(lh + ta.lds_bins + i, c);
+    } else {
+      add_agg(gp(ta.hist_init), h.off + (v >= 0 ? v : h.D), c, cnt && h.off >= 0);
+      add_agg(gp(ta.tot_init), i, c, cnt && v >= 0);
+    }
+  };
+#pragma unroll
+  for (int i = 0; i < kInitPre; ++i) {
+    if (i >= ta.n_hists) break;  // uniform
+    hist(i, cp(ta.hists)[i], pc[i], pv[i]);
+  }
+  for (int i = kInitPre; i < ta.n_hists; ++i) {
     const THist h = cp(ta.hists)[i];
     const int c = on ? gp(tb_col(st, h))[n] : 0;
-    const bool cnt = c != 0 && (h.sig < 0 || ((em >> h.sig) & 1u));
-    const int v = (cnt && h.key >= 0) ? gp(st.label_val)[(size_t)h.key * st.N + n] : -1;
-    add_agg(gp(ta.hist_init), h.off + (v >= 0 ? v : h.D), c, cnt && h.off >= 0);
-    add_agg(gp(ta.tot_init), i, c, cnt && v >= 0);
+    hist(i, h, c, (c != 0 && h.key >= 0) ? gp(st.label_val)[(size_t)h.key * st.N + n] : -1);
+  }
+  if constexpr (LH) {
+    __syncthreads();
+    for (int b = threadIdx.x; b < nlh; b += blockDim.x) {
+      const int x = lh[b];
+      if (x) atomicAdd(b < ta.lds_bins ? gp(ta.hist_init) + b : gp(ta.tot_init) + (b - ta.lds_bins), x);
+    }
   }
   if (ta.diag && on) {
     // a diagnostic (kgpu_schedule_one) run: this node's per-plugin raw / normalized rows start at 0
@@ -3147,6 +3218,15 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
   }
 #undef KGPU_TSTAMP
 #undef KGPU_WSTAMP
+  // every workgroup gets here, aborted or not (the pod loop only breaks): the last one to leave
+  // copies the run's abort word into the caller's pinned block
+  if (ta.abort_out && tid == 0) {
+    __threadfence();
+    if (atomicAdd(ta.done, 1) == G - 1) {
+      __threadfence();
+      __hip_atomic_store(ta.abort_out, load_sc1(ta.abort), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
 }
 
 // ---------------------------------------------------------------- cross-rank init reduction
@@ -3263,7 +3343,11 @@ int launch_tbatch_init(const DevState* st, const TBatchArgs& a, int groups, void
   hipStream_t s = (hipStream_t)stream;
   const int N = a.per * groups;  // >= st->N
   const int nb = (N + 255) / 256;
-  hipLaunchKernelGGL(k_tbatch_init, dim3(nb), dim3(256), 0, s, st, a);
+  const int nlh = a.lds_bins + a.n_hists;
+  if (nlh <= kInitLdsBins)
+    hipLaunchKernelGGL(k_tbatch_init<true>, dim3(nb), dim3(256), (unsigned)(sizeof(int32_t) * (size_t)std::max(nlh, 1)), s, st, a);
+  else
+    hipLaunchKernelGGL(k_tbatch_init<false>, dim3(nb), dim3(256), 0, s, st, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

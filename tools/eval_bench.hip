@@ -30,7 +30,7 @@ __global__ __launch_bounds__(B) void k_evalbench(const DevState* __restrict__ st
     const uint64_t tk = pod_tie_key(st.seed, it);
     if (FRESHQ) {
       q = *cp(qs + it);  // a query record never read before (as in k_batch: one per pod)
-      if (PIN) pin_sgpr(q);
+      (void)PIN;
     }
     uint64_t k[NEV];
 #pragma unroll

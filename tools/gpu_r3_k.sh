@@ -10,3 +10,8 @@ step pytest_ahead timeout -k 10 400 python -u -m pytest tests/test_ahead.py test
 step ahead_b timeout -k 10 400 python -u tools/ahead_bench.py --config b --nodes 5000 --pods 2000 || exit 1
 step ahead_c timeout -k 10 400 python -u tools/ahead_bench.py --config c --nodes 5000 --pods 1500 || exit 1
 step ahead_d timeout -k 10 400 python -u tools/ahead_bench.py --config d --nodes 5000 --pods 1500 || exit 1
+step bench_e125k timeout -k 10 600 python -u bench.py --config e --nodes 125000 --steps 3 --cpu-sample 200 --latency-pods 0 --extra-nodes 0 || exit 1
+step lat_c_sixlaunch timeout -k 10 300 python -u bench.py --config c --steps 2 --cpu-sample 0 --extra-nodes 0 --latency-pods 300 --no-topo-persistent || exit 1
+step lat_c_probe timeout -k 10 300 python -u tools/latency_probe.py --config c --pods 300 || exit 1
+step lat_trace_c timeout -k 10 300 rocprofv3 --kernel-trace --hip-trace --stats --output-format csv -d $O/lat_trace_c -o run \
+  -- python -u tools/latency_probe.py --config c --pods 120 || exit 1
