@@ -2763,13 +2763,35 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
   const int G = gridDim.x, g = blockIdx.x;
   const int lo = g * ta.per;
 
-  for (int i = tid; i < ta.lds_bins; i += B) H[i] = gp(ta.hist_init)[i];
+  // LDS replicas and the workgroup's label values: eight independent loads in flight per thread
+  // and round (a one-pod run pays this start-up in full; a strided loop would wait for each load)
+  constexpr int kU = 8;
+  for (int base = 0; base < ta.lds_bins; base += kU * B) {
+    int32_t v[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int i = base + u * B + tid;
+      v[u] = i < ta.lds_bins ? gp(ta.hist_init)[i] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+      if (base + u * B + tid < ta.lds_bins) H[base + u * B + tid] = v[u];
+  }
   for (int i = tid; i < ta.reg_words; i += B) REG[i] = gp(ta.reg_init)[i];
   for (int i = tid; i < ta.n_hists; i += B) TOT[i] = gp(ta.tot_init)[i];
   for (int i = tid; i < ta.n_sigs; i += B) SANY[i] = gp(ta.sig_any)[i];
-  for (int i = tid; i < ta.lab_keys * ta.per; i += B) {
-    const int k = i / ta.per, n = lo + i % ta.per;
-    LAB[i] = n < st.N ? gp(st.label_val)[(size_t)k * st.N + n] : -1;
+  const int nlab = ta.lab_keys * ta.per;
+  for (int base = 0; base < nlab; base += kU * B) {
+    int32_t v[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int i = base + u * B + tid;
+      const int k = i / ta.per, n = lo + i % ta.per;
+      v[u] = (i < nlab && n < st.N) ? gp(st.label_val)[(size_t)k * st.N + n] : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+      if (base + u * B + tid < nlab) LAB[base + u * B + tid] = v[u];
   }
   if (tid == 0) M.abort = 0;
   if constexpr (XG) {
