@@ -122,6 +122,8 @@ def measure(args, cfg, n_nodes_per_gpu, B, K, W, cpu_sample, cpu_threads, latenc
         eng.set_option(abi.OPT_PERSISTENT, 0)
     if args.no_coop:
         eng.set_option(abi.OPT_COOPERATIVE, 0)
+    if args.batch_geo is not None:
+        eng.set_option(abi.OPT_BATCH_GEO, args.batch_geo)
     if args.topo_fused is not None:
         eng.set_option(abi.OPT_TOPO_FUSED, args.topo_fused)
     if args.no_topo_persistent:
@@ -306,6 +308,8 @@ def main():
                          "many nodes (BASELINE.json's metric is quoted at 5k and 100k nodes); 0: none")
     ap.add_argument("--extra-cpu-sample", type=int, default=1000, help="pods of the extra record's CPU baseline")
     ap.add_argument("--reset-at-exit", action="store_true", help="hipDeviceReset() before exiting (profiling runs)")
+    ap.add_argument("--batch-geo", type=int, default=None,
+                    help="smallest k_batch geometry index considered (KGPU_OPT_BATCH_GEO; 0 = 64 row threads)")
     ap.add_argument("--no-coop", action="store_true",
                     help="KGPU_OPT_COOPERATIVE = 0: ordinary launches of the persistent kernels (profiling runs)")
     ap.add_argument("--os-exit", action="store_true",

@@ -559,6 +559,10 @@ int kgpu_read_nodes(kgpu_ctx* ctx, int64_t* req_cpu, int64_t* req_mem, int64_t* 
  * workgroup per CU on an idle device; a workgroup that never starts turns into KGPU_E_DEVICE through
  * the spin timeouts).  For tools whose exit path faults after cooperative launches (rocprofv3). */
 #define KGPU_OPT_COOPERATIVE 10
+/* KGPU_OPT_BATCH_GEO (11): the smallest k_batch geometry considered (index into the geometry table
+ * of kgpu_kernels.hip: 0 = 64 row threads, 1 = 128, 2 = 192, 3 = 448, 4 = 960, 5 = 512 x 4 rows per
+ * lane); the first one whose workgroups fit the GPU is used.  Default 0. */
+#define KGPU_OPT_BATCH_GEO 11
 int kgpu_set_option(kgpu_ctx* ctx, int32_t option, int64_t value);
 /* Phase stamps of the last persistent run (100 MHz s_memrealtime ticks), 16 per pipeline
  * iteration (pods + 1): workgroup 0's {start, evaluated, previous pod resolved, published, end, 0,

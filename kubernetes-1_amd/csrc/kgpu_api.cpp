@@ -223,6 +223,7 @@ struct kgpu_ctx {
   // persistent topology runs (k_tbatch)
   bool tfast = true;                // KGPU_OPT_TOPO_PERSISTENT
   bool coop = true;                 // KGPU_OPT_COOPERATIVE
+  int batch_geo_first = 0;          // KGPU_OPT_BATCH_GEO
   DevBuf t_tables, t_zero, abort_buf;
   void* t_stage_host = nullptr;  // pinned staging of the runs' tables (bump-allocated, wraps after a sync)
   DevBuf pool_blk;               // the call's query pools, packed (upload_pools)
@@ -1919,7 +1920,7 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
       groups = c->xg_groups;
     } else if (!sharded) {
       kidx = kgpu::batch_geometry(st.N, std::min(c->max_groups > 0 ? std::min(c->max_groups, c->n_cus) : c->n_cus, 256),
-                                  &per, &groups);
+                                  &per, &groups, c->batch_geo_first);
     }
   }
   std::deque<std::array<void*, 2>> run_ptrs;  // kept until the stream is synchronized
@@ -3047,6 +3048,7 @@ int kgpu_set_option(kgpu_ctx* c, int32_t option, int64_t value) try {
   else if (option == KGPU_OPT_TOPO_FUSED) c->topo_fused = value != 0;
   else if (option == KGPU_OPT_TOPO_PERSISTENT) c->tfast = value != 0;
   else if (option == KGPU_OPT_COOPERATIVE) c->coop = value != 0;
+  else if (option == KGPU_OPT_BATCH_GEO) c->batch_geo_first = (int)std::max<int64_t>(0, value);
   else if (option == KGPU_OPT_ABORT_AT) c->abort_at = value < 0 || value > INT32_MAX ? -1 : (int32_t)value;
   else if (option == KGPU_OPT_XGMI) c->xgmi = value != 0;
   else if (option == KGPU_OPT_SKIP_RELEASE_AT) c->skip_release_at = value < 0 || value > INT32_MAX ? -1 : (int32_t)value;
@@ -3660,7 +3662,7 @@ int kgpu_apply_delta(kgpu_ctx* c, const kgpu_delta_batch* b, int64_t generation,
 static int xgmi_geometry(kgpu_ctx* c, int32_t nranks) {
   const int64_t nmax = ((int64_t)c->st.n_total + nranks - 1) / nranks;
   const int maxg = std::max(1, std::min(std::min(c->n_cus, 256), kgpu::kXgmiMaxGT / nranks));
-  c->xg_geo = kgpu::batch_geometry((int)nmax, maxg, &c->xg_per, &c->xg_groups);
+  c->xg_geo = kgpu::batch_geometry((int)nmax, maxg, &c->xg_per, &c->xg_groups, c->batch_geo_first);
   c->xg_GT = nranks * c->xg_groups;
   return c->xg_geo;
 }

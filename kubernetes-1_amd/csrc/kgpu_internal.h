@@ -501,7 +501,8 @@ int launch_shard_pack(const DevState* st, int parity, int blocks, int what, void
 // Geometry index (B row threads x K slots per lane, plus one communication wave) and grid of the
 // persistent kernel: *per = B*K - 1 nodes per workgroup (the last slot of the last lane is the
 // variant-B spare), -1 when N does not fit in max_groups workgroups.
-int batch_geometry(int N, int max_groups, int* per, int* groups);
+// first: the smallest geometry index considered (KGPU_OPT_BATCH_GEO; 0 = all)
+int batch_geometry(int N, int max_groups, int* per, int* groups, int first = 0);
 int launch_batch(const DevState* st, const BatchArgs& a, int groups, int kidx, int spec, bool coop, void* stream);
 // Topology pipeline for one pod (PodArgs.pod): domain histograms, critical-path minima, filters,
 // scores, normalize + argmax, resolve + assume.  next_scratch: words of the next topology pod's

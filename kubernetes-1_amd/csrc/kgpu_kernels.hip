@@ -1548,6 +1548,11 @@ __global__ __launch_bounds__(B + 64) void k_batch(const DevState* __restrict__ s
     const bool have_prev = i > 0;
     const bool have_cur = i < pa.count;
     const int p = i & 1;
+#ifdef KGPU_QN_EARLY
+    // the next pod's query: issued before the evaluation, consumed after the barrier
+    kgpu_pod_query qn{};
+    if (i + 1 < pa.count) qn = *cp(st.queries + pa.first + i + 1);
+#endif
     // variant B applies when pod i-1's assume is a register-only change of the candidate row
     const bool fast_b = have_prev && cand >= 0 && staged && pa.assume && qp.scalars.count == 0 && qp.ports.count == 0;
     const int ob = cand >= 0 ? cand % B : -1, jb = cand >= 0 ? cand / B : -1;
@@ -1570,9 +1575,11 @@ __global__ __launch_bounds__(B + 64) void k_batch(const DevState* __restrict__ s
       wg_partials<K, B>(sh, p, keys, fast_b, ob, jb, cand);
     }
     KGPU_STAMP(i, 1);
+#ifndef KGPU_QN_EARLY
     // the next pod's query: issued now, consumed after the barrier
     kgpu_pod_query qn{};
     if (i + 1 < pa.count) qn = *cp(st.queries + pa.first + i + 1);
+#endif
     __syncthreads();  // (c): pod i-1 resolved and pod i published (communication wave)
     KGPU_STAMP(i, 2);
     int wg = -1;
@@ -3439,19 +3446,19 @@ int select_spec(const int32_t* filters, int nf, const int32_t* scores, int ns, b
 struct Geo {
   int B, K;
 };
-constexpr Geo kGeo[] = {{128, 1}, {192, 1}, {448, 1}, {960, 1}, {512, 4}};  // B row threads (+ one communication wave), K slots per lane
-constexpr int kNumGeo = 5;
+constexpr Geo kGeo[] = {{64, 1}, {128, 1}, {192, 1}, {448, 1}, {960, 1}, {512, 4}};  // B row threads (+ one communication wave), K slots per lane
+constexpr int kNumGeo = 6;
 constexpr int kBatchLdsPad = 96 * 1024;
 
 template <uint32_t FM, uint32_t SM>
 struct BatchRow {
   using Fn = void (*)(const DevState*, BatchArgs);
-  static constexpr Fn fn[kNumGeo] = {k_batch<FM, SM, 1, 128, false>, k_batch<FM, SM, 1, 192, false>,
-                                     k_batch<FM, SM, 1, 448, false>, k_batch<FM, SM, 1, 960, false>,
-                                     k_batch<FM, SM, 4, 512, false>};
-  static constexpr Fn xfn[kNumGeo] = {k_batch<FM, SM, 1, 128, true>, k_batch<FM, SM, 1, 192, true>,
-                                      k_batch<FM, SM, 1, 448, true>, k_batch<FM, SM, 1, 960, true>,
-                                      k_batch<FM, SM, 4, 512, true>};
+  static constexpr Fn fn[kNumGeo] = {k_batch<FM, SM, 1, 64, false>,  k_batch<FM, SM, 1, 128, false>,
+                                     k_batch<FM, SM, 1, 192, false>, k_batch<FM, SM, 1, 448, false>,
+                                     k_batch<FM, SM, 1, 960, false>, k_batch<FM, SM, 4, 512, false>};
+  static constexpr Fn xfn[kNumGeo] = {k_batch<FM, SM, 1, 64, true>,  k_batch<FM, SM, 1, 128, true>,
+                                      k_batch<FM, SM, 1, 192, true>, k_batch<FM, SM, 1, 448, true>,
+                                      k_batch<FM, SM, 1, 960, true>, k_batch<FM, SM, 4, 512, true>};
 };
 using BatchFn = void (*)(const DevState*, BatchArgs);
 static const BatchFn* const kBatch[] = {
@@ -3468,8 +3475,8 @@ static const BatchFn* const kBatchX[] = {
     BatchRow<kDefaultFM, kAutoscalerSM>::xfn,
 };
 
-int batch_geometry(int N, int max_groups, int* per, int* groups) {
-  for (int gi = 0; gi < kNumGeo; ++gi) {
+int batch_geometry(int N, int max_groups, int* per, int* groups, int first) {
+  for (int gi = first < 0 ? 0 : first; gi < kNumGeo; ++gi) {
     const int p = kGeo[gi].B * kGeo[gi].K - 1;  // the last slot of the last lane is the spare
     const int g = (N + p - 1) / p;
     if (g <= max_groups) {

@@ -11,7 +11,8 @@ import numpy as np
 from . import abi
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libkgpu.so")
+# KGPU_LIB_PATH: an alternative build of the same library (kernel experiments side by side)
+LIB_PATH = os.environ.get("KGPU_LIB_PATH") or os.path.join(_HERE, "libkgpu.so")
 _lib = None
 
 EXPORTS = ["kgpu_abi_version", "kgpu_struct_sizes", "kgpu_create", "kgpu_destroy", "kgpu_last_error",

@@ -20,10 +20,11 @@ def _ref(fw, q, pc, threads=4):
     return ref.schedule(q, pc), ref.read_nodes()
 
 
-def _gpu(fw, q, pc, persistent=1, groups=0, chunks=1):
+def _gpu(fw, q, pc, persistent=1, groups=0, chunks=1, geo=0):
     fw.engine.upload(fw.snap, fw.arrays)
     fw.engine.set_option(abi.OPT_PERSISTENT, persistent)
     fw.engine.set_option(abi.OPT_PERSIST_GROUPS, groups)
+    fw.engine.set_option(abi.OPT_BATCH_GEO, geo)
     out = []
     step = (len(q) + chunks - 1) // chunks
     for s in range(0, len(q), step):
@@ -87,3 +88,26 @@ def test_persistent_mixed_with_normalize_pods():
         got, rows = _gpu(fw, q, pc, persistent, 0)
         _same(want, got, "persistent=%d" % persistent)
         _rows(want_rows, rows, "persistent=%d" % persistent)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("geo", [0, 1, 2])
+def test_persistent_geometries(geo):
+    # KGPU_OPT_BATCH_GEO: 64, 128 and 192 row threads per workgroup (one, two and three row waves
+    # beside the communication wave) on the config (b) shape and on random clusters
+    nodes, existing, pods, prof = cluster.fit_least_balanced(n_nodes=2500, n_pods=500)
+    fw = GpuFramework(prof, nodes, existing, pods_hint=pods[:16])
+    q, pc, _, errs = fw.compile_pods(pods)
+    assert not errs
+    want, want_rows = _ref(fw, q, pc, threads=8)
+    got, rows = _gpu(fw, q, pc, 1, 0, chunks=2, geo=geo)
+    _same(want, got, "geo=%d" % geo)
+    _rows(want_rows, rows, "geo=%d" % geo)
+    nodes, existing, pods = gen_random.cluster(5)
+    fw = GpuFramework(Profile(), nodes, existing, pods_hint=pods)
+    q, pc, _, errs = fw.compile_pods(pods)
+    assert not errs
+    want, want_rows = _ref(fw, q, pc)
+    got, rows = _gpu(fw, q, pc, 1, 0, geo=geo)
+    _same(want, got, "random geo=%d" % geo)
+    _rows(want_rows, rows, "random geo=%d" % geo)

@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--pods", type=int, default=1000)
     ap.add_argument("--config", default="b")
     ap.add_argument("--groups", type=int, default=0, help="KGPU_OPT_PERSIST_GROUPS cap (0: one per CU)")
+    ap.add_argument("--batch-geo", type=int, default=None, help="KGPU_OPT_BATCH_GEO")
     args = ap.parse_args()
     import numpy as np
     from kgpu import abi, cluster
@@ -38,6 +39,8 @@ def main():
     eng.schedule_batch(q[:64], pc)
     eng.upload(fw.snap, fw.arrays)
     eng.set_option(abi.OPT_PHASE_TRACE, 1)
+    if args.batch_geo is not None:
+        eng.set_option(abi.OPT_BATCH_GEO, args.batch_geo)
     if args.groups:
         eng.set_option(abi.OPT_PERSIST_GROUPS, args.groups)
     eng.schedule_batch(q, pc)
