@@ -1548,11 +1548,10 @@ __global__ __launch_bounds__(B + 64) void k_batch(const DevState* __restrict__ s
     const bool have_prev = i > 0;
     const bool have_cur = i < pa.count;
     const int p = i & 1;
-#ifdef KGPU_QN_EARLY
-    // the next pod's query: issued before the evaluation, consumed after the barrier
+    // the next pod's query: issued before the evaluation, consumed after the barrier (issued after
+    // the partials, its scalar loads held barrier (c) -- whose wait drains them -- 80 ns longer)
     kgpu_pod_query qn{};
     if (i + 1 < pa.count) qn = *cp(st.queries + pa.first + i + 1);
-#endif
     // variant B applies when pod i-1's assume is a register-only change of the candidate row
     const bool fast_b = have_prev && cand >= 0 && staged && pa.assume && qp.scalars.count == 0 && qp.ports.count == 0;
     const int ob = cand >= 0 ? cand % B : -1, jb = cand >= 0 ? cand / B : -1;
@@ -1575,11 +1574,6 @@ __global__ __launch_bounds__(B + 64) void k_batch(const DevState* __restrict__ s
       wg_partials<K, B>(sh, p, keys, fast_b, ob, jb, cand);
     }
     KGPU_STAMP(i, 1);
-#ifndef KGPU_QN_EARLY
-    // the next pod's query: issued now, consumed after the barrier
-    kgpu_pod_query qn{};
-    if (i + 1 < pa.count) qn = *cp(st.queries + pa.first + i + 1);
-#endif
     __syncthreads();  // (c): pod i-1 resolved and pod i published (communication wave)
     KGPU_STAMP(i, 2);
     int wg = -1;
