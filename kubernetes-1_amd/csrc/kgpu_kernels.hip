@@ -2312,6 +2312,20 @@ int launch_class_init(const DevState* st, int c0, int nc, int n_pods, void* stre
 // H[v] (+ the key-missing bin when v is "", since node.Labels[k] of a missing key is ""), the
 // affinity maps are H[...] > 0, topologyScore[k][v] = sum of weight * H[v].
 
+// Scalar-cache prefetch of L 64-byte lines at p (wave-uniform): the lines land in the CU's scalar
+// cache, where the other waves' first reads of the same record then hit.  The calling wave waits for
+// the loads, so it is called by a wave that would be idle anyway.
+// Only offsets inside [p, p + bytes) are read: one dword per line, at line offsets below `bytes`.
+template <int L>
+__device__ __forceinline__ void kcache_prefetch(const void* p, int bytes) {
+  const CAS uint32_t* q = (const CAS uint32_t*)p;
+  uint32_t v[L];
+#pragma unroll
+  for (int l = 0; l < L; ++l) v[l] = l * 64 < bytes ? q[l * 16] : 0u;
+#pragma unroll
+  for (int l = 0; l < L; ++l) asm volatile("" ::"s"(v[l]));
+}
+
 __device__ __forceinline__ bool tb_elig(const TBatchArgs& ta, int sig, int n) {
   const TSig sg = cp(ta.sigs)[sig];
   return (gp(ta.elig)[sg.elig_word + (n >> 5)] >> (n & 31)) & 1u;
@@ -3187,6 +3201,13 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
         M.wg = wg;
         M.wnode = wkey ? (int)rank40_inv(tk, wkey & kMask40, st.tie_mode) : -1;
       }
+    } else if (wave == 1 && i + 1 < ta.count) {
+      // while wave 0 waits for the winner: the next pod's query, plan and lookup tables into the
+      // scalar cache (their first reads head the next pod's PreFilter phase, one dependent load each)
+      kcache_prefetch<8>(st.queries + pod + 1, (int)sizeof(kgpu_pod_query));
+      const TPlan& np = *cp(ta.plans + cp(ta.plan_of)[i + 1]);
+      kcache_prefetch<8>(&np, (int)sizeof(TPlan));
+      kcache_prefetch<4>(cp(ta.tabs) + np.tabs.begin, np.tabs.count * (int)sizeof(TTab));
     }
     __syncthreads();
     if (M.abort) break;
