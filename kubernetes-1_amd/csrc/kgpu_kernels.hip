@@ -1146,6 +1146,24 @@ __device__ __forceinline__ int load_sc1(const int32_t* p) {
   return __hip_atomic_load(const_cast<int32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Lane `src`'s row (wave-uniform src), in every lane.
+__device__ __forceinline__ int64_t lane64(int64_t x, int src) {
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)x, src);
+  const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)((uint64_t)x >> 32), src);
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ NodeRes lane_row(const NodeRes& r, int src) {
+  NodeRes t;
+  t.ac = lane64(r.ac, src); t.am = lane64(r.am, src); t.ae = lane64(r.ae, src);
+  t.rc = lane64(r.rc, src); t.rm = lane64(r.rm, src); t.re = lane64(r.re, src);
+  t.zc = lane64(r.zc, src); t.zm = lane64(r.zm, src);
+  t.ap = __builtin_amdgcn_readlane(r.ap, src);
+  t.np = __builtin_amdgcn_readlane(r.np, src);
+  t.ic = __builtin_bit_cast(double, lane64(__builtin_bit_cast(int64_t, r.ic), src));
+  t.im = __builtin_bit_cast(double, lane64(__builtin_bit_cast(int64_t, r.im), src));
+  return t;
+}
+
 // NodeInfo.AddPod on a register copy only (the variant-B row): resource columns and pod count.
 __device__ __forceinline__ void assume_regs(const kgpu_pod_query& q, NodeRes& r) {
   r.rc += q.req[0];
@@ -1559,8 +1577,17 @@ __global__ __launch_bounds__(B + 64) void k_batch(const DevState* __restrict__ s
     if (have_cur) {
       const uint64_t tk = pod_tie_key(st.seed, pa.seq0 + i);
       if (fast_b && wave == W - 1) {
-        lds_wait(&sh.bready, i, pa.abort);  // the candidate lane staged it right after barrier (c) of pod i-1
-        NodeRes t = sh.brow[(i - 1) & 1];
+        NodeRes t;
+        if constexpr (W == 1) {
+          // one row wave: the candidate row is read from its lane directly (it is unchanged since
+          // barrier (c) of pod i-1, where the multi-wave geometries stage it in LDS)
+#pragma unroll
+          for (int j = 0; j < K; ++j)
+            if (j == jb) t = lane_row(r[j], ob);
+        } else {
+          lds_wait(&sh.bready, i, pa.abort);  // the candidate lane staged it right after barrier (c) of pod i-1
+          t = sh.brow[(i - 1) & 1];
+        }
         assume_regs(qp, t);
         if (tid == B - 1) r[K - 1] = t;
       }
@@ -1625,7 +1652,7 @@ __global__ __launch_bounds__(B + 64) void k_batch(const DevState* __restrict__ s
       cand = sh.cslow[p];
     } else {
       cand = cn;
-      if (cand >= 0 && tid == cand % B) {
+      if (W > 1 && cand >= 0 && tid == cand % B) {
         // stage pod i's candidate row (pod i-1 already assumed on it) for pod i+1's variant B
 #pragma unroll
         for (int j = 0; j < K; ++j)
@@ -2311,20 +2338,6 @@ int launch_class_init(const DevState* st, int c0, int nc, int n_pods, void* stre
 // rebuilt: TpPairToMatchNum[(k, v)] = sum over the pod's DoNotSchedule constraints on k of
 // H[v] (+ the key-missing bin when v is "", since node.Labels[k] of a missing key is ""), the
 // affinity maps are H[...] > 0, topologyScore[k][v] = sum of weight * H[v].
-
-// Scalar-cache prefetch of L 64-byte lines at p (wave-uniform): the lines land in the CU's scalar
-// cache, where the other waves' first reads of the same record then hit.  The calling wave waits for
-// the loads, so it is called by a wave that would be idle anyway.
-// Only offsets inside [p, p + bytes) are read: one dword per line, at line offsets below `bytes`.
-template <int L>
-__device__ __forceinline__ void kcache_prefetch(const void* p, int bytes) {
-  const CAS uint32_t* q = (const CAS uint32_t*)p;
-  uint32_t v[L];
-#pragma unroll
-  for (int l = 0; l < L; ++l) v[l] = l * 64 < bytes ? q[l * 16] : 0u;
-#pragma unroll
-  for (int l = 0; l < L; ++l) asm volatile("" ::"s"(v[l]));
-}
 
 __device__ __forceinline__ bool tb_elig(const TBatchArgs& ta, int sig, int n) {
   const TSig sg = cp(ta.sigs)[sig];
@@ -3201,13 +3214,6 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
         M.wg = wg;
         M.wnode = wkey ? (int)rank40_inv(tk, wkey & kMask40, st.tie_mode) : -1;
       }
-    } else if (wave == 1 && i + 1 < ta.count) {
-      // while wave 0 waits for the winner: the next pod's query, plan and lookup tables into the
-      // scalar cache (their first reads head the next pod's PreFilter phase, one dependent load each)
-      kcache_prefetch<8>(st.queries + pod + 1, (int)sizeof(kgpu_pod_query));
-      const TPlan& np = *cp(ta.plans + cp(ta.plan_of)[i + 1]);
-      kcache_prefetch<8>(&np, (int)sizeof(TPlan));
-      kcache_prefetch<4>(cp(ta.tabs) + np.tabs.begin, np.tabs.count * (int)sizeof(TTab));
     }
     __syncthreads();
     if (M.abort) break;

@@ -145,6 +145,9 @@ def test_lds_handoff_timeout_recovers(at):
     q, pc, _, errs = fw.compile_pods(pods)
     assert not errs
     e = fw.engine
+    # 128 row threads: two row waves, so the candidate row crosses waves through LDS (one row wave
+    # reads it from the candidate lane directly and has no such hand-off)
+    e.set_option(abi.OPT_BATCH_GEO, 1)
     e.set_option(abi.OPT_SKIP_RELEASE_AT, at)
     with pytest.raises(KgpuError) as ex:
         e.schedule_batch(q, pc)
