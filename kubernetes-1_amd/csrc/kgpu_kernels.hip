@@ -1266,7 +1266,7 @@ __device__ __forceinline__ constexpr bool spare_slot(int j, int K, int tid, int 
 // replaced by the spare, reported under the candidate's index).  Feasible counts through ballots.
 template <int K, int B>
 __device__ __forceinline__ void wg_partials(BatchShared<B>& sh, int p, const uint64_t (&keys)[K], bool vb, int ob,
-                                            int jb, int cand) {
+                                            int jb, int cand, Cand& ra, Cand& rb) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   Cand a{0, -1, 0}, b{0, -1, 0};
 #pragma unroll
@@ -1298,6 +1298,8 @@ __device__ __forceinline__ void wg_partials(BatchShared<B>& sh, int p, const uin
     sh.ka[p][wave] = a.key; sh.ia[p][wave] = a.idx; sh.fa[p][wave] = a.feas;
     sh.kb[p][wave] = b.key; sh.ib[p][wave] = b.idx; sh.fb[p][wave] = b.feas;
   }
+  ra = a;
+  rb = b;
 }
 
 template <int B>
@@ -1566,14 +1568,11 @@ __global__ __launch_bounds__(B + 64) void k_batch(const DevState* __restrict__ s
     const bool have_prev = i > 0;
     const bool have_cur = i < pa.count;
     const int p = i & 1;
-    // the next pod's query: issued before the evaluation, consumed after the barrier (issued after
-    // the partials, its scalar loads held barrier (c) -- whose wait drains them -- 80 ns longer)
-    kgpu_pod_query qn{};
-    if (i + 1 < pa.count) qn = *cp(st.queries + pa.first + i + 1);
     // variant B applies when pod i-1's assume is a register-only change of the candidate row
     const bool fast_b = have_prev && cand >= 0 && staged && pa.assume && qp.scalars.count == 0 && qp.ports.count == 0;
     const int ob = cand >= 0 ? cand % B : -1, jb = cand >= 0 ? cand / B : -1;
     uint64_t keys[K];
+    Cand own_a{0, -1, 0}, own_b{0, -1, 0};  // this wave's variant-A / B reduction of pod i
     if (have_cur) {
       const uint64_t tk = pod_tie_key(st.seed, pa.seq0 + i);
       if (fast_b && wave == W - 1) {
@@ -1598,9 +1597,15 @@ __global__ __launch_bounds__(B + 64) void k_batch(const DevState* __restrict__ s
         keys[j] = (spare ? fast_b : n < st.N) ? node_key<FM, SM>(st, q, r[j], n, tk) : 0;
       }
       KGPU_STAMP(i, 5);
-      wg_partials<K, B>(sh, p, keys, fast_b, ob, jb, cand);
+      wg_partials<K, B>(sh, p, keys, fast_b, ob, jb, cand, own_a, own_b);
     }
     KGPU_STAMP(i, 1);
+    // the next pod's query: issued now, consumed after the barrier.  (Issued before the evaluation
+    // instead, it costs config (a)'s default-profile kernel 2.77 -> 2.93 us per pod -- the query's
+    // fields then stay live through the evaluation -- and gains config (b) nothing once the
+    // variant-B row is read across lanes: profiles/r03_qn_bench.jsonl.)
+    kgpu_pod_query qn{};
+    if (i + 1 < pa.count) qn = *cp(st.queries + pa.first + i + 1);
     __syncthreads();  // (c): pod i-1 resolved and pod i published (communication wave)
     KGPU_STAMP(i, 2);
     int wg = -1;
@@ -1617,7 +1622,8 @@ __global__ __launch_bounds__(B + 64) void k_batch(const DevState* __restrict__ s
       if (won && pa.assume && !fast_b) {
         cn = -2;
       } else {
-        const Cand c = wg_combine<B>(sh, p, won && fast_b);
+        // one row wave: its own reduction is the workgroup's (no LDS read back)
+        const Cand c = W == 1 ? ((won && fast_b) ? own_b : own_a) : wg_combine<B>(sh, p, won && fast_b);
         cn = c.key ? c.idx : -1;
       }
     }
