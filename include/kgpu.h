@@ -563,6 +563,11 @@ int kgpu_read_nodes(kgpu_ctx* ctx, int64_t* req_cpu, int64_t* req_mem, int64_t* 
  * of kgpu_kernels.hip: 0 = 64 row threads, 1 = 128, 2 = 192, 3 = 448, 4 = 960, 5 = 512 x 4 rows per
  * lane); the first one whose workgroups fit the GPU is used.  Default 0. */
 #define KGPU_OPT_BATCH_GEO 11
+/* KGPU_OPT_ARENA_BYTES (12): bytes a short cycle (kgpu_schedule_one, batches of up to 64 pods) may
+ * stage beside its DevState and queries for its single host-to-device copy (changed pools, topology
+ * plans, a one-pod persistent topology run's tables and zeroed words); items beyond it take copies of
+ * their own.  0 = no staging beyond DevState and queries.  Default and maximum 1 MiB. */
+#define KGPU_OPT_ARENA_BYTES 12
 int kgpu_set_option(kgpu_ctx* ctx, int32_t option, int64_t value);
 /* Phase stamps of the last persistent run (100 MHz s_memrealtime ticks), 16 per pipeline
  * iteration (pods + 1): workgroup 0's {start, evaluated, previous pod resolved, published, end, 0,

@@ -188,6 +188,7 @@ struct kgpu_ctx {
   size_t ar_used = 0, ar_cap = 0, ar_lo = 0, ar_hi = 0;
   bool ar_on = false, ar_inflight = false;
   bool tb_abort_mapped = false;                    // the last k_tbatch run wrote its abort word to res_pin
+  size_t ar_limit = 1 << 20;                       // KGPU_OPT_ARENA_BYTES (bytes of arena items per cycle)
   DevState ds_last{};                              // the DevState image last uploaded by a short cycle
   const void* ds_ptr = nullptr;                    // ... into this dstate allocation (null: none)
   size_t stage_cap = 0;
@@ -1815,9 +1816,9 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
     // stream synchronize
     if (c->ar_inflight) HIP_OK(c, hipStreamSynchronize(c->stream));
     c->ar_inflight = false;
-    c->ar_on = true;
     c->ar_used = (kDsQueryOff + sizeof(kgpu_pod_query) * (size_t)n + 255) & ~(size_t)255;
-    c->ar_cap = kCycHostBytes;
+    c->ar_cap = std::min(kCycHostBytes, c->ar_used + c->ar_limit);
+    c->ar_on = c->ar_limit > 0;
     c->ar_lo = c->ar_hi = 0;
   }
   c->tb_abort_mapped = false;
@@ -3049,6 +3050,7 @@ int kgpu_set_option(kgpu_ctx* c, int32_t option, int64_t value) try {
   else if (option == KGPU_OPT_TOPO_PERSISTENT) c->tfast = value != 0;
   else if (option == KGPU_OPT_COOPERATIVE) c->coop = value != 0;
   else if (option == KGPU_OPT_BATCH_GEO) c->batch_geo_first = (int)std::max<int64_t>(0, value);
+  else if (option == KGPU_OPT_ARENA_BYTES) c->ar_limit = (size_t)std::min<int64_t>(std::max<int64_t>(0, value), (int64_t)kArenaBytes);
   else if (option == KGPU_OPT_ABORT_AT) c->abort_at = value < 0 || value > INT32_MAX ? -1 : (int32_t)value;
   else if (option == KGPU_OPT_XGMI) c->xgmi = value != 0;
   else if (option == KGPU_OPT_SKIP_RELEASE_AT) c->skip_release_at = value < 0 || value > INT32_MAX ? -1 : (int32_t)value;
