@@ -2558,6 +2558,39 @@ __device__ __forceinline__ bool tpoll_slot(const uint64_t* row, int G, const int
   }
 }
 
+// G <= 64 workgroups: wave `wave` polls ALL of its statistics slots (wave, wave + W, ... below R,
+// at most MS of them) in one sweep, one granule per lane and slot, and reduces each slot once every
+// granule of every slot is there.  Polling the slots one after another costs a wave with two slots a
+// second memory round trip after the data has landed.  Writes STAT[rr]; false on timeout / abort.
+template <int MS>
+__device__ __forceinline__ bool tpoll_slots(const uint64_t* srow, int G, int R, int W, int soft_words,
+                                            const int32_t* abort_word, int64_t* STAT) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  for (;;) {
+    uint64_t v[MS];
+    bool all = true;
+#pragma unroll
+    for (int k = 0; k < MS; ++k) {
+      const int rr = wave + k * W;
+      v[k] = (rr < R && lane < G) ? load_sc1(srow + (size_t)rr * G + lane) : kGValid;
+      if (!(v[k] & kGValid)) all = false;
+    }
+    if (__all(all)) {
+#pragma unroll
+      for (int k = 0; k < MS; ++k) {
+        const int rr = wave + k * W;
+        if (rr >= R) break;  // uniform
+        const int op = tslot_op(rr, soft_words);
+        const int64_t x = wave_op_i64(op, lane < G ? dec_stat(v[k]) : tident(op));
+        if (lane == 0) STAT[rr] = x;
+      }
+      return true;
+    }
+    if (load_sc1(abort_word) != 0 || __builtin_amdgcn_s_memrealtime() - t0 > kSpinTimeout) return false;
+  }
+}
+
 // ---- node sharding over xGMI (k_tbatch XG): the topology mailbox ring (kgpu_internal.h TX row)
 constexpr uint64_t kTagMask = 0xFull << 60;
 constexpr uint64_t kPayload60 = (1ull << 60) - 1;
@@ -2982,20 +3015,23 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
     KGPU_WSTAMP(4);
     uint64_t* srow = ta.gran + (size_t)i * (R + 1) * G;  // [R][G] statistics granules | [G] keys
     if (tid < R) {
+      // one slot per thread.  Every thread reads its candidate words first -- clamped addresses, one
+      // LDS round trip -- and then selects: a switch over the slot puts an LDS read and its wait in
+      // each of a dozen divergent branches, which the wave runs one after another (0.7 us per pod).
+      const int i32 = tid < 6 ? tid : (tid == kTDptsMax ? 6 : 7);
+      const uint32_t w32 = (uint32_t)M.acc32[i32];
+      const int64_t w64 = M.acc64[tid == kTIpaMax ? 1 : 0];
+      const int vi = tid - kTFixed;
+      const int voff = vi < 0 ? ta.o_smask : (vi < ta.soft_words ? ta.o_smask + 4 * vi : ta.o_zsum + 4 * (vi - ta.soft_words));
+      const int32_t wv = *reinterpret_cast<const int32_t*>(lds_raw + voff);
       int64_t x;
-      switch (tid) {
-        case kTFeas: x = M.acc32[0]; break;
-        case kTMaxT: x = (uint32_t)M.acc32[1]; break;
-        case kTMaxNA: x = (uint32_t)M.acc32[2]; break;
-        case kTNonIgn: x = M.acc32[3]; break;
-        case kTAdjMin: x = tp.n_soft ? (int64_t)(uint32_t)~(uint32_t)M.acc32[4] : tident(kOpMin); break;
-        case kTAdjMax: x = tp.n_soft ? (int64_t)(uint32_t)M.acc32[5] : tident(kOpMax); break;
-        case kTIpaMin: x = M.acc64[0] == INT64_MAX ? tident(kOpMin) : M.acc64[0]; break;
-        case kTIpaMax: x = M.acc64[1] == INT64_MIN ? tident(kOpMax) : M.acc64[1]; break;
-        case kTDptsMax: x = (uint32_t)M.acc32[6]; break;
-        case kTZoned: x = (uint32_t)M.acc32[7]; break;
-        default: x = tid < kTFixed + ta.soft_words ? (int64_t)SMASK[tid - kTFixed] : (int64_t)ZSUM[tid - kTFixed - ta.soft_words];
-      }
+      if (tid >= kTFixed) x = vi < ta.soft_words ? (int64_t)(uint32_t)wv : (int64_t)wv;  // SMASK bits / ZSUM
+      else if (tid == kTIpaMin) x = w64 == INT64_MAX ? tident(kOpMin) : w64;
+      else if (tid == kTIpaMax) x = w64 == INT64_MIN ? tident(kOpMax) : w64;
+      else if (tid == kTAdjMin) x = tp.n_soft ? (int64_t)(uint32_t)~w32 : tident(kOpMin);
+      else if (tid == kTAdjMax) x = tp.n_soft ? (int64_t)w32 : tident(kOpMax);
+      else if (tid == kTFeas || tid == kTNonIgn) x = (int32_t)w32;
+      else x = (int64_t)w32;  // kTMaxT, kTMaxNA, kTDptsMax, kTZoned
       store_sc1(srow + (size_t)tid * G + g, enc_stat(x));
     }
     KGPU_TSTAMP(3);
@@ -3026,6 +3062,10 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
       for (int z = 0; z < ta.zones; ++z) dmax_zone = max(dmax_zone, S[kTFixed + ta.soft_words + z]);
       const bool have_zones = S[kTZoned] != 0;
       const double Mx = 100.0, zwt = 2.0 / 3.0;
+      // DefaultNormalizeScore / PTS normalize quotients are 0..100 with this pod's (uniform) maxima
+      // as divisors: one reciprocal each, and ratio100's exact quotient per node
+      const double invT = maxT > 0 ? 1.0 / (double)maxT : 0.0, invNA = maxNA > 0 ? 1.0 / (double)maxNA : 0.0;
+      const double invP = (pmx > 0 && pmx < (1ll << 52)) ? 1.0 / (double)pmx : 0.0;
       bkey = 0;
       bidx = -1;
 #pragma unroll
@@ -3034,16 +3074,16 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
         const int n = lo + j * B + tid;
         // DefaultNormalizeScore (helper/normalize_score.go:26-54): non-negative operands, exact
         // through div_nonneg
-        const int64_t vt = maxT == 0 ? 100 : 100 - div_nonneg(100 * (int64_t)o[j].taint, maxT);
-        const int64_t vn = maxNA == 0 ? (int64_t)o[j].na : div_nonneg(100 * (int64_t)o[j].na, maxNA);
-        int64_t vp;
-        if (o[j].adj == INT64_MIN) {
-          vp = 0;
-        } else {
-          // scoring.go:248-256; pmn <= ps <= pmx, so the dividend is non-negative
-          const int64_t ps = tp.n_soft ? (int64_t)((double)o[j].adj * wsoft) : 0;
-          vp = pmx == 0 ? 100 : div_nonneg(100 * (pmx + pmn - ps), pmx);
-        }
+        const int64_t ps = (o[j].adj != INT64_MIN && tp.n_soft) ? (int64_t)((double)o[j].adj * wsoft) : 0;
+        bool s1 = false, s2 = false, s3 = false;
+        const int64_t qt = ratio100(100 * (int64_t)o[j].taint, maxT, invT, s1);
+        const int64_t qn = ratio100(100 * (int64_t)o[j].na, maxNA, invNA, s2);
+        // scoring.go:248-256; pmn <= ps <= pmx, so the dividend is non-negative
+        const bool pdiv = o[j].adj != INT64_MIN && pmx != 0;  // pmn is set whenever pmx is
+        const int64_t qp = ratio100(pdiv ? 100 * (pmx + pmn - ps) : 0, pmx, invP, s3);
+        const int64_t vt = maxT == 0 ? 100 : 100 - (s1 ? div_nonneg(100 * (int64_t)o[j].taint, maxT) : qt);
+        const int64_t vn = maxNA == 0 ? (int64_t)o[j].na : (s2 ? div_nonneg(100 * (int64_t)o[j].na, maxNA) : qn);
+        const int64_t vp = o[j].adj == INT64_MIN ? 0 : (pmx == 0 ? 100 : (s3 ? div_nonneg(100 * (pmx + pmn - ps), pmx) : qp));
         const int64_t vi = idiff > 0 ? (int64_t)(Mx * ((double)(o[j].ipa - imn) / (double)idiff)) : 0;
         int64_t vd = 0;
         if (tp.dpts_cls != -2) {
@@ -3108,7 +3148,9 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
       txrow = sh_ptx[ta.rank] + (size_t)((ta.xseq0 + i) % kTXRing) * txw;
       txtag = kGValid | ((uint64_t)(((ta.xseq0 + i) / kTXRing) & 7) << 60);
     }
-    for (int rr = wave; rr < R; rr += W) {
+    if (!XG && G <= 64 && R <= 4 * W) {
+      ok = tpoll_slots<4>(srow, G, R, W, ta.soft_words, ta.abort, STAT);
+    } else for (int rr = wave; rr < R; rr += W) {
       const int op = tslot_op(rr, ta.soft_words);
       int64_t x;
       if (!tpoll_slot(srow + (size_t)rr * G, G, ta.abort, op, x)) { ok = false; break; }
