@@ -12,7 +12,7 @@ cd $R && export TMPDIR=/tmp
 step() { local name=$1; shift; "$@" > $O/$name.log 2>&1; local rc=$?; echo "$name rc=$rc" >> $O/status.txt; return $rc; }
 cd /tmp
 B="--steps 5 --cpu-sample 0 --latency-pods 0 --extra-nodes 0 --no-coop"
-for cfg in b c d; do
+for cfg in ${CFGS:-b c d}; do
   for n in 5000 100000; do
     step prof_${cfg}${n} timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_${cfg}${n} -o run \
       -- python3 -u $R/bench.py --config $cfg --nodes $n $B || exit 1
