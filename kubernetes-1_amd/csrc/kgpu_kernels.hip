@@ -3062,12 +3062,10 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
       for (int z = 0; z < ta.zones; ++z) dmax_zone = max(dmax_zone, S[kTFixed + ta.soft_words + z]);
       const bool have_zones = S[kTZoned] != 0;
       const double Mx = 100.0, zwt = 2.0 / 3.0;
-#ifdef KGPU_TB_EXP
       // DefaultNormalizeScore / PTS normalize quotients are 0..100 with this pod's (uniform) maxima
       // as divisors: one reciprocal each, and ratio100's exact quotient per node
       const double invT = maxT > 0 ? 1.0 / (double)maxT : 0.0, invNA = maxNA > 0 ? 1.0 / (double)maxNA : 0.0;
       const double invP = (pmx > 0 && pmx < (1ll << 52)) ? 1.0 / (double)pmx : 0.0;
-#endif
       bkey = 0;
       bidx = -1;
 #pragma unroll
@@ -3076,7 +3074,6 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
         const int n = lo + j * B + tid;
         // DefaultNormalizeScore (helper/normalize_score.go:26-54): non-negative operands, exact
         // through div_nonneg
-#ifdef KGPU_TB_EXP
         const int64_t ps = (o[j].adj != INT64_MIN && tp.n_soft) ? (int64_t)((double)o[j].adj * wsoft) : 0;
         bool s1 = false, s2 = false, s3 = false;
         const int64_t qt = ratio100(100 * (int64_t)o[j].taint, maxT, invT, s1);
@@ -3087,18 +3084,6 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
         const int64_t vt = maxT == 0 ? 100 : 100 - (s1 ? div_nonneg(100 * (int64_t)o[j].taint, maxT) : qt);
         const int64_t vn = maxNA == 0 ? (int64_t)o[j].na : (s2 ? div_nonneg(100 * (int64_t)o[j].na, maxNA) : qn);
         const int64_t vp = o[j].adj == INT64_MIN ? 0 : (pmx == 0 ? 100 : (s3 ? div_nonneg(100 * (pmx + pmn - ps), pmx) : qp));
-#else
-        const int64_t vt = maxT == 0 ? 100 : 100 - div_nonneg(100 * (int64_t)o[j].taint, maxT);
-        const int64_t vn = maxNA == 0 ? (int64_t)o[j].na : div_nonneg(100 * (int64_t)o[j].na, maxNA);
-        int64_t vp;
-        if (o[j].adj == INT64_MIN) {
-          vp = 0;
-        } else {
-          // scoring.go:248-256; pmn <= ps <= pmx, so the dividend is non-negative
-          const int64_t ps = tp.n_soft ? (int64_t)((double)o[j].adj * wsoft) : 0;
-          vp = pmx == 0 ? 100 : div_nonneg(100 * (pmx + pmn - ps), pmx);
-        }
-#endif
         const int64_t vi = idiff > 0 ? (int64_t)(Mx * ((double)(o[j].ipa - imn) / (double)idiff)) : 0;
         int64_t vd = 0;
         if (tp.dpts_cls != -2) {
@@ -3163,12 +3148,9 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
       txrow = sh_ptx[ta.rank] + (size_t)((ta.xseq0 + i) % kTXRing) * txw;
       txtag = kGValid | ((uint64_t)(((ta.xseq0 + i) / kTXRing) & 7) << 60);
     }
-#ifdef KGPU_TB_EXP
     if (!XG && G <= 64 && R <= 4 * W) {
       ok = tpoll_slots<4>(srow, G, R, W, ta.soft_words, ta.abort, STAT);
-    } else
-#endif
-    for (int rr = wave; rr < R; rr += W) {
+    } else for (int rr = wave; rr < R; rr += W) {
       const int op = tslot_op(rr, ta.soft_words);
       int64_t x;
       if (!tpoll_slot(srow + (size_t)rr * G, G, ta.abort, op, x)) { ok = false; break; }
