@@ -2558,23 +2558,28 @@ __device__ __forceinline__ bool tpoll_slot(const uint64_t* row, int G, const int
   }
 }
 
-// G <= 64 workgroups: wave `wave` polls ALL of its statistics slots (wave, wave + W, ... below R,
-// at most MS of them) in one sweep, one granule per lane and slot, and reduces each slot once every
+// Wave `wave` polls ALL of its statistics slots (wave, wave + W, ... below R, at most MS of them) in
+// one sweep, NJ granules per lane and slot, and reduces each slot once every
 // granule of every slot is there.  Polling the slots one after another costs a wave with two slots a
 // second memory round trip after the data has landed.  Writes STAT[rr]; false on timeout / abort.
-template <int MS>
+// NJ granules per lane and slot (G <= 64 * NJ).
+template <int MS, int NJ>
 __device__ __forceinline__ bool tpoll_slots(const uint64_t* srow, int G, int R, int W, int soft_words,
                                             const int32_t* abort_word, int64_t* STAT) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   for (;;) {
-    uint64_t v[MS];
+    uint64_t v[MS][NJ];
     bool all = true;
 #pragma unroll
     for (int k = 0; k < MS; ++k) {
       const int rr = wave + k * W;
-      v[k] = (rr < R && lane < G) ? load_sc1(srow + (size_t)rr * G + lane) : kGValid;
-      if (!(v[k] & kGValid)) all = false;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int gg = lane + 64 * j;
+        v[k][j] = (rr < R && gg < G) ? load_sc1(srow + (size_t)rr * G + gg) : kGValid;
+        if (!(v[k][j] & kGValid)) all = false;
+      }
     }
     if (__all(all)) {
 #pragma unroll
@@ -2582,7 +2587,11 @@ __device__ __forceinline__ bool tpoll_slots(const uint64_t* srow, int G, int R, 
         const int rr = wave + k * W;
         if (rr >= R) break;  // uniform
         const int op = tslot_op(rr, soft_words);
-        const int64_t x = wave_op_i64(op, lane < G ? dec_stat(v[k]) : tident(op));
+        int64_t acc = tident(op);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+          if (lane + 64 * j < G) acc = tcombine(op, acc, dec_stat(v[k][j]));
+        const int64_t x = wave_op_i64(op, acc);
         if (lane == 0) STAT[rr] = x;
       }
       return true;
@@ -3149,7 +3158,9 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
       txtag = kGValid | ((uint64_t)(((ta.xseq0 + i) / kTXRing) & 7) << 60);
     }
     if (!XG && G <= 64 && R <= 4 * W) {
-      ok = tpoll_slots<4>(srow, G, R, W, ta.soft_words, ta.abort, STAT);
+      ok = tpoll_slots<4, 1>(srow, G, R, W, ta.soft_words, ta.abort, STAT);
+    } else if (!XG && G <= 256 && R <= 2 * W) {
+      ok = tpoll_slots<2, 4>(srow, G, R, W, ta.soft_words, ta.abort, STAT);
     } else for (int rr = wave; rr < R; rr += W) {
       const int op = tslot_op(rr, ta.soft_words);
       int64_t x;
