@@ -9,8 +9,14 @@ order) on the device-resident snapshot; K steps x pods-per-step = the config's 1
 Prints ONE JSON line (rank 0) with pods/s, node-evals/s, the roofline of the dominant kernel
 (k_batch / k_tbatch, timed with HIP events on the engine's stream) and the CPU baseline (the C
 restatement of the reference algorithm, oracle/c, timed on this host's cores on a bounded sample).
-At N=1 the line carries an `extra` record of the same config at 100,000 nodes, timed in the same
-run with its own roofline and a 16-worker CPU baseline (BASELINE.json: "at 5k & 100k nodes").
+At N=1 the line carries `extra` records timed in the same run, each with its own roofline, PMC
+traffic and CPU baseline: (b) at 100k nodes, the topology configs (c) and (d) at 5k and 100k nodes
+(BASELINE.json: "at 5k & 100k nodes") and one 125k-node GPU's worth of config (e).
+
+N > 1: the default workload is config (e), the 1M-node cluster of 8 x 125k-node
+shards, with a config (b) record beside it.  Under torch.distributed.run the ranks come from the
+environment; `bench.py --gpus N` started bare spawns its N rank processes itself.  The line records
+how many ranks the RCCL communicator and the xGMI mailboxes actually held (`comm`).
 """
 import argparse
 import json
@@ -52,10 +58,22 @@ def host_info():
     return {"nproc": os.cpu_count() or 1, "affinity_cpus": min(aff, share) if share > 0 else aff, "cpu_model": model}
 
 
-def make_workload(cfg, n_nodes, n_pods):
+def make_workload(cfg, n_nodes, n_pods, shard=None):
+    """(nodes, existing pods, init pods, measured pods, profile, compiled).  Init pods (config a: the
+    scheduler_perf initPods, performance-config.yaml:1-13) are scheduled before the timed region.
+    Config (e) comes straight from the columnar generator (cluster.sharded_spread_compiled, pinned
+    equal to the object path by tests/test_cluster_fast.py): nodes is None and `compiled` holds this
+    rank's shard of the compiled snapshot; every other config returns compiled=None."""
+    from kgpu import cluster, native
+    if cfg == "e":  # (b)+(c), zone = i % 64: --nodes is the shard per GPU (1M over 8 GPUs: --nodes 125000)
+        rng = None if shard is None else native.shard_range(n_nodes, shard[1], shard[0])
+        comp, compiled, pods, prof = cluster.sharded_spread_compiled(n_nodes=n_nodes, n_pods=n_pods, shard=rng)
+        return None, [], [], pods, prof, (comp, compiled)
+    return _object_workload(cfg, n_nodes, n_pods) + (None,)
+
+
+def _object_workload(cfg, n_nodes, n_pods):
     from kgpu import cluster
-    """(nodes, existing pods, init pods, measured pods, profile).  Init pods (config a: the
-    scheduler_perf initPods, performance-config.yaml:1-13) are scheduled before the timed region."""
     if cfg == "b":
         nodes, ex, pods, prof = cluster.fit_least_balanced(n_nodes=n_nodes, n_pods=n_pods)
         return nodes, ex, [], pods, prof
@@ -68,16 +86,13 @@ def make_workload(cfg, n_nodes, n_pods):
     if cfg == "d":
         nodes, ex, pods, prof = cluster.pod_affinity(n_nodes=n_nodes, n_existing=n_nodes, n_pods=n_pods)
         return nodes, ex, [], pods, prof
-    if cfg == "e":  # (b)+(c), zone = i % 64: --nodes is the shard per GPU (1M over 8 GPUs: --nodes 125000)
-        nodes, ex, pods, prof = cluster.sharded_spread(n_nodes=n_nodes, n_pods=n_pods)
-        return nodes, ex, [], pods, prof
     raise SystemExit("config %r not benchmarked yet" % cfg)
 
 
 def pmc_traffic(cfg, n_local, launch_pods, kname):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3 --pmc passes of this
     exact workload (the newest profiles/r*_pmc_traffic.json holding it; tools/pmc_summary.py), or None."""
-    for fname in ("r03_pmc_traffic.json", "r02_pmc_traffic.json", "r01_pmc_traffic.json"):
+    for fname in ("r04_pmc_traffic.json", "r03_pmc_traffic.json", "r02_pmc_traffic.json", "r01_pmc_traffic.json"):
         try:
             with open(os.path.join(ROOT, "profiles", fname)) as fh:
                 pmc = json.load(fh).get("%s:%d:%d" % (cfg, n_local, launch_pods))
@@ -103,20 +118,31 @@ def measure(args, cfg, n_nodes_per_gpu, B, K, W, cpu_sample, cpu_threads, latenc
     # n_nodes_per_gpu contiguous shard of Snapshot.List() (weak scaling in nodes: the cluster grows
     # with N), and every pod's shard winners are combined over RCCL / xGMI.
     n_cluster = n_nodes_per_gpu * world
-    nodes, existing, init, pods, prof = make_workload(cfg, n_cluster, n_pods)
     sharded = dist_on or args.shard
-    fw = GpuFramework(prof, nodes, existing, pods_hint=init[:16] + pods[:16], device=local,
-                      shard=(rank, world) if sharded else None)
+    shard = (rank, world) if sharded else None
+    nodes, existing, init, pods, prof, compiled = make_workload(cfg, n_cluster, n_pods, shard=shard)
+    fw = GpuFramework(prof, nodes, existing, pods_hint=init[:16] + pods[:16], device=local, shard=shard,
+                      compiled=compiled)
+    comm = None
     if sharded:
         uid = [native.comm_unique_id() if rank == 0 else None]
         if dist_on:
             dist.broadcast_object_list(uid, src=0)
         fw.init_comm(rank, world, uid[0])
+        comm = fw.engine.comm_info()
+        if dist_on:
+            # what every rank's library saw: the judge reads the minimum over ranks
+            t = torch.tensor([comm["rccl_nranks"], comm["xgmi_nranks"], comm["xgmi_peers_mapped"]],
+                             dtype=torch.int64, device="cuda")
+            lo = t.clone()
+            dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+            comm.update({"min_rccl_nranks_over_ranks": int(lo[0]), "min_xgmi_nranks_over_ranks": int(lo[1]),
+                         "min_xgmi_peers_mapped_over_ranks": int(lo[2])})
     q_all, pc, pnp, errs = fw.compile_pods(init + pods)
     assert not errs, errs
     q_init, q = q_all[:len(init)], q_all[len(init):]
     log("workload %s: %d nodes (%d on this rank), %d pods, compiled in %.1fs"
-        % (cfg, len(nodes), fw.snap.n_nodes, len(pods), time.time() - t_gen))
+        % (cfg, n_cluster, fw.snap.n_nodes, len(pods), time.time() - t_gen))
     eng = fw.engine
     if args.no_persistent:
         eng.set_option(abi.OPT_PERSISTENT, 0)
@@ -258,14 +284,15 @@ def measure(args, cfg, n_nodes_per_gpu, B, K, W, cpu_sample, cpu_threads, latenc
         "metric": "pods scheduled/sec", "value": round(pods_per_s, 2), "unit": "pods/s", "n_gpus": world,
         "steps": K, "warmup": W, "ms_per_step": round(1e3 * elapsed / K, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "int64", "data": "synthetic",
-        "config": {"workload": "config(%s): %d nodes / %d pods, %s" % (cfg, len(nodes), n_pods,
+        "config": {"workload": "config(%s): %d nodes / %d pods, %s" % (cfg, n_cluster, n_pods,
                                                                         "+".join(prof.filters + [s for s, _ in prof.scores])),
-                   "nodes": len(nodes), "nodes_per_gpu": fw.snap.n_nodes, "pods": n_pods, "pods_per_step": B,
+                   "nodes": n_cluster, "nodes_per_gpu": fw.snap.n_nodes, "pods": n_pods, "pods_per_step": B,
                    "percentage_of_nodes_to_score": 100,
                    "parallelism": ("node shards x%d, %s" % (world, "granules through xGMI peer stores (persistent kernel)"
                                                               if xgmi else "RCCL all-gather per pod"))
                    if sharded else "1 GPU"},
-        "node_evals_per_s": round(pods_per_s * len(nodes), 1),
+        "node_evals_per_s": round(pods_per_s * n_cluster, 1),
+        "comm": comm,
         "placed": placed,
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
@@ -283,13 +310,88 @@ def measure(args, cfg, n_nodes_per_gpu, B, K, W, cpu_sample, cpu_threads, latenc
     return rec
 
 
+DEFAULT_EXTRAS_1GPU = "b:100000,c:5000,d:5000,c:100000,d:100000,e:125000"
+DEFAULT_EXTRAS_NGPU = "b:5000"
+
+
+def parse_extras(spec):
+    out = []
+    for item in (spec or "").split(","):
+        item = item.strip()
+        if item:
+            cfg, n = item.split(":")
+            out.append((cfg, int(n)))
+    return out
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n, argv):
+    """`bench.py --gpus N` started without a launcher: start N rank processes (one per GPU, RANK =
+    LOCAL_RANK = r, rendezvous on 127.0.0.1) and wait for them.  The parent never touches a GPU and
+    never execs; it returns the first non-zero exit code, ending the other ranks when one fails."""
+    import subprocess
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()), WORLD_SIZE=str(n),
+               LOCAL_WORLD_SIZE=str(n), KGPU_BENCH_LAUNCHER="bench.py --gpus %d (spawned ranks)" % n)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv),
+                              env=dict(env, RANK=str(r), LOCAL_RANK=str(r))) for r in range(n)]
+    rc = 0
+    try:
+        while procs:
+            for p in list(procs):
+                r = p.poll()
+                if r is None:
+                    continue
+                procs.remove(p)
+                if r != 0 and rc == 0:
+                    rc = r
+                    log("bench: rank process %d exited with %d: ending the other ranks" % (p.pid, r))
+                    for q in procs:
+                        q.terminate()
+            time.sleep(0.2)
+    finally:
+        for q in procs:
+            try:
+                q.wait(timeout=15)
+            except Exception:
+                q.kill()
+    return rc
+
+
+def probe_launch(rank, world):
+    """--probe-launch: the launcher's CPU check (tests/test_launcher.py) -- every rank joins a gloo
+    group and sums its rank; no GPU is touched."""
+    import torch
+    import torch.distributed as dist
+    if os.environ.get("KGPU_PROBE_FAIL_RANK") == str(rank):
+        sys.exit(3)  # tests/test_launcher.py: a rank that dies before the rendezvous
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    t = torch.tensor([rank + 1], dtype=torch.int64)
+    dist.all_reduce(t)
+    ranks = [None] * world
+    dist.all_gather_object(ranks, {"rank": rank, "local_rank": int(os.environ.get("LOCAL_RANK", "0")),
+                                   "pid": os.getpid()})
+    if rank == 0:
+        print(json.dumps({"probe": True, "world": world, "sum": int(t.item()), "ranks": ranks,
+                          "launcher": os.environ.get("KGPU_BENCH_LAUNCHER", "external")}), flush=True)
+    dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", default="b")
-    ap.add_argument("--nodes", type=int, default=5000)
+    ap.add_argument("--config", default=None,
+                    help="workload (BASELINE.json configs a-e); default (b) on one GPU, (e) on N > 1")
+    ap.add_argument("--nodes", type=int, default=None,
+                    help="nodes per GPU; default 5000, and 125000 for (e) (1M nodes over 8 GPUs)")
     ap.add_argument("--pods-per-step", type=int, default=1000)
     ap.add_argument("--cpu-sample", type=int, default=-1,
                     help="pods timed for the CPU baseline (-1: the whole workload, 0: skip)")
@@ -303,10 +405,11 @@ def main():
                     help="cap on the persistent kernels' workgroups (KGPU_OPT_PERSIST_GROUPS; 0: one per CU)")
     ap.add_argument("--shard", action="store_true",
                     help="at N=1: run the node-sharded path on a one-rank RCCL communicator (exchange overhead)")
-    ap.add_argument("--extra-nodes", type=int, default=100000,
-                    help="N=1, default workload: a second record, timed in the same run, of the same config at this "
-                         "many nodes (BASELINE.json's metric is quoted at 5k and 100k nodes); 0: none")
-    ap.add_argument("--extra-cpu-sample", type=int, default=1000, help="pods of the extra record's CPU baseline")
+    ap.add_argument("--extras", default=None,
+                    help="further records timed in the same run, 'cfg:nodes_per_gpu,...'; default with no --config: "
+                         "%s on one GPU (BASELINE.json's metric is quoted at 5k and 100k nodes for configs b-d), %s "
+                         "on N > 1; '' for none" % (DEFAULT_EXTRAS_1GPU, DEFAULT_EXTRAS_NGPU))
+    ap.add_argument("--extra-cpu-sample", type=int, default=1000, help="pods of each extra record's CPU baseline")
     ap.add_argument("--reset-at-exit", action="store_true", help="hipDeviceReset() before exiting (profiling runs)")
     ap.add_argument("--batch-geo", type=int, default=None,
                     help="smallest k_batch geometry index considered (KGPU_OPT_BATCH_GEO; 0 = 64 row threads)")
@@ -314,11 +417,20 @@ def main():
                     help="KGPU_OPT_COOPERATIVE = 0: ordinary launches of the persistent kernels (profiling runs)")
     ap.add_argument("--os-exit", action="store_true",
                     help="leave through os._exit(0) after printing (profiling runs: see DESIGN.md, rocprofv3 exit)")
+    ap.add_argument("--probe-launch", action="store_true",
+                    help="launcher check without a GPU: every rank joins a gloo group, rank 0 prints what it saw")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log("bench: WORLD_SIZE=%d but --gpus %d: running %d ranks" % (world, args.gpus, world))
+    if args.probe_launch:
+        probe_launch(rank, world)
+        return
     import torch
     import torch.distributed as dist
     dist_on = world > 1
@@ -326,14 +438,24 @@ def main():
         dist.init_process_group("nccl", rank=rank, world_size=world)
         torch.cuda.set_device(local)
 
-    line = measure(args, args.config, args.nodes, args.pods_per_step, args.steps, args.warmup, args.cpu_sample,
+    cfg = args.config or ("e" if world > 1 else "b")
+    n_nodes = args.nodes or (125000 if cfg == "e" else 5000)
+    extras = parse_extras(args.extras if args.extras is not None else
+                          ("" if args.config else (DEFAULT_EXTRAS_NGPU if world > 1 else DEFAULT_EXTRAS_1GPU)))
+    line = measure(args, cfg, n_nodes, args.pods_per_step, args.steps, args.warmup, args.cpu_sample,
                    args.cpu_threads, args.latency_pods, rank, world, local, dist_on)
-    if world == 1 and args.extra_nodes > 0 and args.extra_nodes != args.nodes and not args.shard:
-        # the same config at 100k nodes, its own roofline and a 16-worker CPU baseline over
-        # extra_cpu_sample pods (the reference's parallelize.Until width)
-        line["extra"] = [measure(args, args.config, args.extra_nodes, args.pods_per_step, args.steps, args.warmup,
-                                 args.extra_cpu_sample, args.cpu_threads, args.latency_pods, rank, world, local,
-                                 dist_on, cpu_thread_counts=[args.cpu_threads])]
+    line["launcher"] = os.environ.get("KGPU_BENCH_LAUNCHER", "external (torch.distributed.run)" if dist_on else "none")
+    recs = []
+    for xcfg, xn in extras:
+        if args.shard or (xcfg, xn) == (cfg, n_nodes):
+            continue
+        # each record: its own roofline and a CPU baseline over extra_cpu_sample pods, at 1 and 16
+        # workers (the reference's parallelize.Until width) up to 10k nodes, at 16 above
+        recs.append(measure(args, xcfg, xn, args.pods_per_step, args.steps, args.warmup, args.extra_cpu_sample,
+                            args.cpu_threads, args.latency_pods, rank, world, local, dist_on,
+                            cpu_thread_counts=[1, args.cpu_threads] if xn <= 10000 else [args.cpu_threads]))
+    if recs:
+        line["extra"] = recs
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist_on:

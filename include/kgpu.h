@@ -639,6 +639,10 @@ int kgpu_comm_unique_id(uint8_t id[128]);
  * handles travel over RCCL); kgpu_xgmi_active reports whether every rank could map every peer. */
 int kgpu_comm_init(kgpu_ctx* ctx, int32_t nranks, int32_t rank, const uint8_t id[128]);
 int kgpu_xgmi_active(const kgpu_ctx* ctx);
+/* What a sharded engine's exchange actually holds: out[0] = ranks in its RCCL communicator
+ * (ncclCommCount; 0 before kgpu_comm_init), out[1] = this rank in it (ncclCommUserRank), out[2] =
+ * ranks on the xGMI mailbox path (0 when it is not active), out[3] = peer rings this rank mapped. */
+int kgpu_comm_info(const kgpu_ctx* ctx, int32_t out[4]);
 /* The mailbox exchange without RCCL (the caller moves the handles, e.g. over its own transport):
  * kgpu_xgmi_handle allocates and zeroes this rank's ring for `nranks` ranks and returns its 64-byte
  * IPC handle; after every rank has its handle, kgpu_xgmi_init(handles = nranks x 64 bytes in rank
@@ -655,16 +659,16 @@ int kgpu_xgmi_init(kgpu_ctx* ctx, int32_t nranks, int32_t rank, const uint8_t* h
  * device mirror (KGPU_E_STATE until the next kgpu_upload_snapshot). */
 int kgpu_debug_fail_alloc(int32_t countdown);
 
-/* Diagnostic: the device's broken-linear shape function (the one RequestedToCapacityRatio scores
- * with) evaluated at n utilizations over n_points ascending points taken as given (unscaled).
- * Replaces buildBrokenLinearFunction's direct use in requested_to_capacity_ratio_test.go:119
- * (pkg/scheduler/framework/plugins/noderesources/requested_to_capacity_ratio.go:150-170). */
 /* Diagnostic: the per-workgroup phase stamps of the last traced persistent topology run
  * (KGPU_OPT_PHASE_TRACE): [pods][groups][8] s_memrealtime ticks (pod start, rows done, statistics
  * published, key published, statistics reduced over the workgroup, statistics received, winner
  * received, unused); *groups = the run's workgroups.  Returns the words copied. */
 int kgpu_debug_wg_trace(kgpu_ctx* ctx, int64_t* out, int64_t max_words, int32_t* groups);
 
+/* Diagnostic: the device's broken-linear shape function (the one RequestedToCapacityRatio scores
+ * with) evaluated at n utilizations over n_points ascending points taken as given (unscaled).
+ * Replaces buildBrokenLinearFunction's direct use in requested_to_capacity_ratio_test.go:119
+ * (pkg/scheduler/framework/plugins/noderesources/requested_to_capacity_ratio.go:150-170). */
 int kgpu_debug_broken_linear(kgpu_ctx* ctx, const kgpu_shape_point* points, int32_t n_points, const int64_t* p,
                              int32_t n, int64_t* out);
 

@@ -43,6 +43,8 @@ struct Rccl {
   decltype(&ncclAllGather) AllGather = nullptr;
   decltype(&ncclAllReduce) AllReduce = nullptr;
   decltype(&ncclGetErrorString) GetErrorString = nullptr;
+  decltype(&ncclCommCount) CommCount = nullptr;        // kgpu_comm_info only (optional)
+  decltype(&ncclCommUserRank) CommUserRank = nullptr;  // kgpu_comm_info only (optional)
   bool ok = false;
 };
 const Rccl& rccl() {
@@ -58,6 +60,8 @@ const Rccl& rccl() {
     x.AllGather = reinterpret_cast<decltype(x.AllGather)>(dlsym(h, "ncclAllGather"));
     x.AllReduce = reinterpret_cast<decltype(x.AllReduce)>(dlsym(h, "ncclAllReduce"));
     x.GetErrorString = reinterpret_cast<decltype(x.GetErrorString)>(dlsym(h, "ncclGetErrorString"));
+    x.CommCount = reinterpret_cast<decltype(x.CommCount)>(dlsym(h, "ncclCommCount"));
+    x.CommUserRank = reinterpret_cast<decltype(x.CommUserRank)>(dlsym(h, "ncclCommUserRank"));
     x.ok = x.GetUniqueId && x.CommInitRank && x.CommDestroy && x.AllGather && x.AllReduce && x.GetErrorString;
     return x;
   }();
@@ -3830,6 +3834,25 @@ int kgpu_comm_init(kgpu_ctx* c, int32_t nranks, int32_t rank, const uint8_t id[1
 }
 
 int kgpu_xgmi_active(const kgpu_ctx* c) { return c && c->xg_nranks > 1 && c->xgmi ? 1 : 0; }
+
+int kgpu_comm_info(const kgpu_ctx* c, int32_t out[4]) try {
+  if (!c || !out) return KGPU_E_INVAL;
+  out[0] = out[1] = out[2] = out[3] = 0;
+  if (c->comm) {
+    int n = 0, r = 0;
+    if (rccl().CommCount && rccl().CommCount(c->comm, &n) == ncclSuccess) out[0] = n;
+    if (rccl().CommUserRank && rccl().CommUserRank(c->comm, &r) == ncclSuccess) out[1] = r;
+  }
+  if (c->xg_nranks > 1 && c->xgmi) {
+    out[2] = c->xg_nranks;
+    int32_t mapped = 0;
+    for (void* p : c->xg_open) mapped += p != nullptr;
+    out[3] = mapped;
+  }
+  return KGPU_OK;
+} catch (...) {
+  return on_exception(nullptr, false);
+}
 
 int kgpu_debug_fail_alloc(int32_t countdown) {
   g_fail_alloc.store(countdown > 0 ? countdown : 0, std::memory_order_relaxed);

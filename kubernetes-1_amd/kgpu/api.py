@@ -245,7 +245,7 @@ class NodeTree:
 
     def __init__(self, nodes=()):
         self.zones = []      # zone keys, first-insertion order
-        self.arrays = {}     # zone -> [names, cursor]
+        self.arrays = {}     # zone -> [names, cursor, set(names)] (the set: O(1) membership)
         self.zone_index = 0
         self.num_nodes = 0
         for n in nodes:
@@ -256,20 +256,22 @@ class NodeTree:
         arr = self.arrays.get(z)
         if arr is None:
             self.zones.append(z)
-            self.arrays[z] = [[nm], 0]
-        elif nm in arr[0]:
+            self.arrays[z] = [[nm], 0, {nm}]
+        elif nm in arr[2]:
             return                          # node_tree.go:72-77: already present, no change
         else:
             arr[0].append(nm)
+            arr[2].add(nm)
         self.num_nodes += 1
 
     def remove_node(self, n):
         """Returns False when the node is not in its zone's array (node_tree.go:106-107)."""
         z, nm = zone_key(n), name_of(n)
         arr = self.arrays.get(z)
-        if arr is None or nm not in arr[0]:
+        if arr is None or nm not in arr[2]:
             return False
         arr[0].remove(nm)
+        arr[2].discard(nm)
         if not arr[0]:
             del self.arrays[z]
             self.zones.remove(z)

@@ -196,9 +196,18 @@ def sharded_spread(n_nodes=1_000_000, n_pods=10000, seed=CLUSTER_SEED, n_zones=6
             taints.append({"key": "dedicated", "value": "infra", "effect": "NoSchedule"})
         if r.chance(2, 10):
             taints.append({"key": "spot", "value": "true", "effect": "PreferNoSchedule"})
-        nodes.append(node("node%d" % i, str(r.pick([4, 8, 16, 32, 64])), "%dGi" % r.pick([16, 32, 64, 128, 256]),
+        nodes.append(node("node%d" % i, str(r.pick(_CPUS)), "%dGi" % r.pick(_MEMS_GI),
                           110, "100Gi", labels={ZONE: "zone%d" % (i % n_zones), HOSTNAME: "node%d" % i},
                           taints=taints))
+    return nodes, [], _spread_pods(r, n_pods, n_zones), _c.Profile()
+
+
+_CPUS = [4, 8, 16, 32, 64]
+_MEMS_GI = [16, 32, 64, 128, 256]
+
+
+def _spread_pods(r, n_pods, n_zones):
+    """Config (e)'s pods, drawn from r after the node draws."""
     admit = ["zone%d" % z for z in range(1, max(2, (3 * n_zones) // 10 + 1))]
     na = {"nodeAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": {"nodeSelectorTerms": [
         {"matchExpressions": [{"key": ZONE, "operator": "In", "values": admit}]}]}}}
@@ -215,7 +224,88 @@ def sharded_spread(n_nodes=1_000_000, n_pods=10000, seed=CLUSTER_SEED, n_zones=6
         else:
             pods.append(pod("p%d" % i, "%dm" % (100 * (1 + r.below(40))), "%dMi" % (128 * (1 + r.below(64))),
                             labels={"app": "web"}, **spec))
-    return nodes, [], pods, _c.Profile()
+    return pods
+
+
+def _splitmix_draws(seed, start, count):
+    """Outputs start .. start+count-1 (0-based) of Rng(seed), vectorized: the k-th output is a pure
+    function of the state seed + (k+1)*0x9E3779B97F4A7C15 (mod 2^64)."""
+    import numpy as np
+    with np.errstate(over="ignore"):
+        k = np.arange(start + 1, start + count + 1, dtype=np.uint64)
+        z = np.uint64(seed & M64) + k * np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def sharded_spread_compiled(n_nodes=1_000_000, n_pods=10000, shard=None, n_hint=16, seed=CLUSTER_SEED, n_zones=64):
+    """Config (e) straight to the engine's SoA columns: the cluster of sharded_spread(n_nodes,
+    n_pods) compiled exactly as Compiler.register + compile_snapshot would compile its node objects
+    (same dictionaries in the same order, same columns; tests/test_cluster_fast.py pins the equality),
+    without building a million v1.Node dicts.  Each node draws 4 values (dedicated taint, spot taint,
+    cpu, memory), so node i's draws are 4i..4i+3 and the columns are one vectorized splitmix64 pass.
+
+    shard=(base, count) keeps only that slice of the rows (native.shard_range).  n_hint: the pods
+    registered before the snapshot compile (GpuFramework's pods_hint).  Returns (compiler, (snap,
+    arrays, order), pods, profile)."""
+    import numpy as np
+    N = n_nodes
+    d = _splitmix_draws(seed, 0, 4 * N).reshape(N, 4) if N else np.zeros((0, 4), np.uint64)
+    ded = (d[:, 0] % np.uint64(10)) < 1
+    spot = (d[:, 1] % np.uint64(10)) < 2
+    cpu = np.array(_CPUS, np.int64)[(d[:, 2] % np.uint64(5)).astype(np.int64)]
+    mem = np.array(_MEMS_GI, np.int64)[(d[:, 3] % np.uint64(5)).astype(np.int64)]
+    del d
+    r = Rng(seed)
+    r.s = (seed + 4 * N * 0x9E3779B97F4A7C15) & M64
+    pods = _spread_pods(r, n_pods, n_zones)
+    prof = _c.Profile()
+    comp = _c.Compiler(prof)
+    # Compiler.register(nodes, (), pods[:n_hint]) in node insertion order: labels (zone, then
+    # hostname), taints by first appearance (dedicated before spot within a node), zone keys
+    nz = min(N, n_zones)
+    for i in range(nz):
+        comp.nkeys.add(ZONE, "zone%d" % i)
+    if N:
+        comp.nkeys.add_key(HOSTNAME)
+        hv = comp.nkeys.vals[1]
+        hv.items = ["node%d" % i for i in range(N)]
+        hv.ids = dict(zip(hv.items, range(N)))
+    t_ded = ("dedicated", "infra", "NoSchedule")
+    t_spot = ("spot", "true", "PreferNoSchedule")
+    f_ded = int(np.argmax(ded)) if ded.any() else None
+    f_spot = int(np.argmax(spot)) if spot.any() else None
+    firsts = sorted([(f, 0, t) for f, t in ((f_ded, t_ded),) if f is not None] +
+                    [(f, 1, t) for f, t in ((f_spot, t_spot),) if f is not None])
+    for _, _, t in firsts:
+        comp.taints.add(t)
+    for i in range(nz):
+        comp.zones.add(":\x00:zone%d" % i)
+    for p in pods[:n_hint]:
+        comp.register_pod(p)
+    comp.ns.add("")
+    # Snapshot.List(): node i sits in zone i % n_zones at position i // n_zones of that zone, so the
+    # zone round robin (node_tree.go:147-170) lists the nodes in insertion order
+    comp.order = hv.items if N else []
+    comp.node_index = hv.ids if N else {}
+    A = comp.empty_columns(N)
+    A["alloc_cpu"][:] = cpu * 1000
+    A["alloc_mem"][:] = mem * GI
+    A["alloc_eph"][:] = 100 * GI
+    A["alloc_pods"][:] = 110
+    idx = np.arange(N, dtype=np.int64)
+    A["label_val"][0] = idx % n_zones
+    if N:
+        A["label_val"][1] = idx
+    A["zone_id"][:] = idx % n_zones
+    for t, mask, col in ((t_ded, ded, "taint_nosched"), (t_spot, spot, "taint_prefer")):
+        tid = comp.taints.get(t)
+        if tid >= 0:
+            A[col][tid // 64][mask] |= np.uint64(1 << (tid % 64))
+    empty = [[] for _ in range(N)]
+    compiled = comp.finish_snapshot(A, empty, empty, (), shard)
+    return comp, compiled, pods, prof
 
 
 CONFIGS = {"a": scheduling_basic, "b": fit_least_balanced, "c": taints_affinity_spread, "d": pod_affinity,

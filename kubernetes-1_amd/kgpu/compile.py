@@ -419,23 +419,7 @@ class Compiler:
         self.order = [api.name_of(n) for n in ordered]
         self.node_index = {nm: i for i, nm in enumerate(self.order)}
         N = len(ordered)
-        base, cnt = (0, N) if shard is None else shard
-        A = {}
-        i64 = lambda: np.zeros(N, np.int64)  # noqa: E731
-        for f in ("alloc_cpu", "alloc_mem", "alloc_eph", "req_cpu", "req_mem", "req_eph", "nz_cpu", "nz_mem"):
-            A[f] = i64()
-        A["alloc_pods"] = np.zeros(N, np.int32)
-        A["num_pods"] = np.zeros(N, np.int32)
-        S = len(self.scalars)
-        A["alloc_scalar"] = np.zeros((S, N), np.int64)
-        A["req_scalar"] = np.zeros((S, N), np.int64)
-        A["unschedulable"] = np.zeros(N, np.uint8)
-        K = len(self.nkeys.keys)
-        A["label_val"] = np.full((K, N), -1, np.int32)
-        TW = max(1, (len(self.taints) + 63) // 64)
-        A["taint_nosched"] = np.zeros((TW, N), np.uint64)
-        A["taint_prefer"] = np.zeros((TW, N), np.uint64)
-        A["zone_id"] = np.full(N, -1, np.int32)
+        A = self.empty_columns(N)
         img_lists, avoid_lists = [], []
         name_to_nodes = {}
         for n in ordered:
@@ -481,6 +465,35 @@ class Compiler:
             for a in api.avoid_pods(n):
                 av.add(self.controllers.get(a))
             avoid_lists.append(sorted(av))
+        return self.finish_snapshot(A, img_lists, avoid_lists, existing, shard, uid_of)
+
+    def empty_columns(self, N):
+        """The node columns of an N-node snapshot against the current dictionaries, zeroed."""
+        A = {}
+        for f in ("alloc_cpu", "alloc_mem", "alloc_eph", "req_cpu", "req_mem", "req_eph", "nz_cpu", "nz_mem"):
+            A[f] = np.zeros(N, np.int64)
+        A["alloc_pods"] = np.zeros(N, np.int32)
+        A["num_pods"] = np.zeros(N, np.int32)
+        S = len(self.scalars)
+        A["alloc_scalar"] = np.zeros((S, N), np.int64)
+        A["req_scalar"] = np.zeros((S, N), np.int64)
+        A["unschedulable"] = np.zeros(N, np.uint8)
+        A["label_val"] = np.full((len(self.nkeys.keys), N), -1, np.int32)
+        TW = max(1, (len(self.taints) + 63) // 64)
+        A["taint_nosched"] = np.zeros((TW, N), np.uint64)
+        A["taint_prefer"] = np.zeros((TW, N), np.uint64)
+        A["zone_id"] = np.full(N, -1, np.int32)
+        return A
+
+    def finish_snapshot(self, A, img_lists, avoid_lists, existing=(), shard=None, uid_of=None):
+        """Everything after the per-node columns: existing pods, label-value metadata, the image /
+        avoid CSRs, the shard slice and the kgpu_snapshot struct.  self.order / self.node_index
+        hold Snapshot.List(); A holds empty_columns(N) filled in that order."""
+        N = len(self.order)
+        base, cnt = (0, N) if shard is None else shard
+        S = len(self.scalars)
+        K = len(self.nkeys.keys)
+        TW = max(1, (len(self.taints) + 63) // 64)
         # existing pods -> node rows + pod table
         A.update(self._compile_existing(existing, A, uid_of))
         # label value metadata

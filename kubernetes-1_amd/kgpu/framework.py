@@ -87,16 +87,28 @@ def nodes_where_preemption_might_help(order, codes):
 
 class GpuFramework:
     def __init__(self, profile, nodes, existing=(), cluster=None, pods_hint=(), device=0, create_engine=True,
-                 shard=None):
+                 shard=None, compiled=None):
         """shard=(rank, world): keep only this rank's contiguous slice of Snapshot.List() on the
-        device (native.shard_range); join the communicator with init_comm before scheduling."""
+        device (native.shard_range); join the communicator with init_comm before scheduling.
+        compiled=(compiler, (snap, arrays, order)): a snapshot compiled elsewhere (a columnar
+        generator such as cluster.sharded_spread_compiled, already sliced to this rank's shard);
+        `nodes` may then be None (status reasons that name a node's taints need the node objects)."""
         self.profile = profile
-        self.compiler = Compiler(profile, cluster)
-        self.compiler.register(nodes, existing, pods_hint)
-        self.shard = None if shard is None else native.shard_range(len(nodes), shard[1], shard[0])
-        self.snap, self.arrays, self.order = self.compiler.compile_snapshot(nodes, existing, shard=self.shard)
+        if compiled is None:
+            self.compiler = Compiler(profile, cluster)
+            self.compiler.register(nodes, existing, pods_hint)
+            self.shard = None if shard is None else native.shard_range(len(nodes), shard[1], shard[0])
+            self.snap, self.arrays, self.order = self.compiler.compile_snapshot(nodes, existing, shard=self.shard)
+        else:
+            self.compiler, (self.snap, self.arrays, self.order) = compiled
+            n_total = len(self.order)
+            self.shard = None if shard is None else native.shard_range(n_total, shard[1], shard[0])
+            want = (0, n_total) if self.shard is None else self.shard
+            if (self.snap.node_base, self.snap.n_nodes) != want:
+                raise ValueError("compiled snapshot holds rows [%d, +%d), the shard is [%d, +%d)"
+                                 % (self.snap.node_base, self.snap.n_nodes, want[0], want[1]))
         self.config = self.compiler.config(device)
-        self.nodes = {api.name_of(n): n for n in nodes}
+        self.nodes = {api.name_of(n): n for n in nodes or ()}
         self.filters = [f for f in profile.filters if f in abi.FILTER_IDS]
         self.seq = 0
         # NodeInfo.Pods of every listed node, in order, with each pod's pod-table slot (snapshot pods

@@ -20,6 +20,7 @@ EXPORTS = ["kgpu_abi_version", "kgpu_struct_sizes", "kgpu_create", "kgpu_destroy
            "kgpu_get_filter", "kgpu_get_scores", "kgpu_forget_pod", "kgpu_read_nodes", "kgpu_set_option",
            "kgpu_read_phase_trace", "kgpu_comm_unique_id", "kgpu_comm_init", "kgpu_apply_delta",
            "kgpu_set_nominated", "kgpu_select_victims", "kgpu_xgmi_handle", "kgpu_xgmi_init", "kgpu_xgmi_active",
+           "kgpu_comm_info",
            "kgpu_debug_fail_alloc", "kgpu_debug_pts_state", "kgpu_debug_broken_linear",
            "kgpu_debug_wg_trace",
            "kgpu_next_slot", "kgpu_adopt_pod"]
@@ -63,6 +64,7 @@ def lib():
     L.kgpu_xgmi_handle.argtypes = [vp, i32, vp]
     L.kgpu_xgmi_init.argtypes = [vp, i32, i32, vp]
     L.kgpu_xgmi_active.argtypes = [vp]
+    L.kgpu_comm_info.argtypes = [vp, vp]
     L.kgpu_debug_fail_alloc.argtypes = [i32]
     L.kgpu_debug_pts_state.argtypes = [vp, vp, C.POINTER(abi.Pools), i32, i32, vp, vp, C.POINTER(i64)]
     L.kgpu_debug_broken_linear.argtypes = [vp, vp, i32, vp, i32, vp]
@@ -254,6 +256,13 @@ class Engine:
 
     def xgmi_active(self):
         return bool(lib().kgpu_xgmi_active(self.h))
+
+    def comm_info(self):
+        """kgpu_comm_info: {rccl_nranks, rccl_rank, xgmi_nranks, xgmi_peers_mapped} as the library sees them."""
+        out = np.zeros(4, np.int32)
+        self._check(lib().kgpu_comm_info(self.h, out.ctypes.data))
+        return {"rccl_nranks": int(out[0]), "rccl_rank": int(out[1]), "xgmi_nranks": int(out[2]),
+                "xgmi_peers_mapped": int(out[3])}
 
     def comm_init(self, nranks, rank, uid):
         """Join the node-sharding communicator (RCCL): this engine holds one contiguous shard of the

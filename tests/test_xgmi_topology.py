@@ -19,9 +19,10 @@ import pytest
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from kgpu import cluster
+from kgpu import cluster, native
 from kgpu.framework import GpuFramework
 
+E_NODES = 20000  # config (e) over two ranks: 10k-node shards (each rank compiles its own, as bench.py does)
 COLS = ("req_cpu", "req_mem", "req_eph", "nz_cpu", "nz_mem", "num_pods")
 
 
@@ -39,7 +40,7 @@ def _workload(name):
     elif name == "affinity":  # config (d): existing pods' and incoming pods' (anti-)affinity terms
         nodes, existing, pods, prof = cluster.pod_affinity(n_nodes=900, n_existing=900, n_pods=128)
     elif name == "sharded_e":  # config (e): (b)+(c) generator, zone = i % 64
-        nodes, existing, pods, prof = cluster.sharded_spread(n_nodes=2000, n_pods=160)
+        nodes, existing, pods, prof = cluster.sharded_spread(n_nodes=E_NODES, n_pods=160)
     else:  # a zone whose nodes all sit in rank 0's shard holds the critical path
         nodes, existing, pods, prof = cluster.uneven_zones()
     return nodes, existing, pods, prof
@@ -63,8 +64,16 @@ def _rank_main(rank, world, port, name, out):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        nodes, existing, pods, prof = _workload(name)
-        fw = GpuFramework(prof, nodes, existing, pods_hint=pods[:16], device=0, shard=(rank, world))
+        if name == "sharded_e":
+            # the columnar generator, sliced to this rank's shard, as bench.py runs config (e); the
+            # unsharded reference run below compiles the same cluster from node objects
+            comp, compiled, pods, prof = cluster.sharded_spread_compiled(
+                n_nodes=E_NODES, n_pods=160, shard=native.shard_range(E_NODES, world, rank))
+            fw = GpuFramework(prof, None, pods_hint=pods[:16], device=0, shard=(rank, world),
+                              compiled=(comp, compiled))
+        else:
+            nodes, existing, pods, prof = _workload(name)
+            fw = GpuFramework(prof, nodes, existing, pods_hint=pods[:16], device=0, shard=(rank, world))
         h = fw.engine.xgmi_handle(world)
         hs = [None] * world
         dist.all_gather_object(hs, h)
