@@ -665,6 +665,16 @@ int kgpu_debug_fail_alloc(int32_t countdown);
  * received, unused); *groups = the run's workgroups.  Returns the words copied. */
 int kgpu_debug_wg_trace(kgpu_ctx* ctx, int64_t* out, int64_t max_words, int32_t* groups);
 
+/* Diagnostic: the InterPodAffinity PreFilter state the device builds for one pod on the current
+ * snapshot (preFilterState, pkg/scheduler/framework/plugins/interpodaffinity/filtering.go:166-271;
+ * replaces getPreFilterState in filtering_test.go:1697 TestPreFilterStateAddRemovePod and :2045
+ * TestGetTPMapMatchingIncomingAffinityAntiAffinity).  One histogram per (map, topology key):
+ * kinds[m] = 0 topologyToMatchedExistingAntiAffinityTerms, 1 topologyToMatchedAffinityTerms,
+ * 2 topologyToMatchedAntiAffinityTerms; keys[m] = node label key id; counts[m * max_values + v] =
+ * the pair (key, value v)'s count.  *n_maps = histograms written.  Unsharded engines only. */
+int kgpu_debug_ipa_state(kgpu_ctx* ctx, const kgpu_pod_query* q, const kgpu_pools* pools, int32_t max_maps,
+                         int32_t max_values, int32_t* kinds, int32_t* keys, int64_t* counts, int32_t* n_maps);
+
 /* Diagnostic: the device's broken-linear shape function (the one RequestedToCapacityRatio scores
  * with) evaluated at n utilizations over n_points ascending points taken as given (unscaled).
  * Replaces buildBrokenLinearFunction's direct use in requested_to_capacity_ratio_test.go:119

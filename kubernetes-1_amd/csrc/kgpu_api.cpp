@@ -3466,23 +3466,21 @@ int kgpu_select_victims(kgpu_ctx* c, const kgpu_pod_query* q, const kgpu_pools* 
   return on_exception(c, false);
 }
 
-int kgpu_debug_pts_state(kgpu_ctx* c, const kgpu_pod_query* q, const kgpu_pools* pools, int32_t kind,
-                         int32_t constraint, uint8_t* registered, int64_t* counts, int64_t* scalar) try {
-  if (!c || !q || !registered || !counts || !scalar || (kind != 0 && kind != 1) || constraint < 0) return KGPU_E_INVAL;
-  if (hipSetDevice(c->device) != hipSuccess) return KGPU_E_DEVICE;
-  if (!c->uploaded) return fail(c, KGPU_E_STATE, "no snapshot uploaded");
-  if (c->comm || c->xg_nranks > 1)
-    return fail(c, KGPU_E_UNSUPPORTED, "kgpu_debug_pts_state reads one engine's state: unsharded only");
-  if (!has_filter(c, KGPU_F_POD_TOPOLOGY_SPREAD) && kind == 0)
-    return fail(c, KGPU_E_INVAL, "the profile has no PodTopologySpread filter");
-  if (!has_score(c, KGPU_S_POD_TOPOLOGY_SPREAD) && kind == 1)
-    return fail(c, KGPU_E_INVAL, "the profile has no PodTopologySpread score");
+// The per-pod topology phases of one pod on the engine's current state (diagnostics only): the
+// histograms (k_topo_pre) always; for kind 0 the critical-path minima of hard constraint `constraint`
+// (k_topo_min), for kind 1 the registrations of the filtered nodes (k_topo_filter).  The pod's
+// scratch (TopoHdr + slots) comes back in sc, its plan in sg.
+static int debug_topo_scratch(kgpu_ctx* c, const kgpu_pod_query* q, const kgpu_pools* pools, int32_t kind,
+                              int32_t constraint, Staged& sg, std::vector<int64_t>& sc) {
   int rc;
-  Staged sg;
   if ((rc = stage_topology(c, q, 1, pools, sg))) return rc;
   const kgpu::QPlan& pl = sg.plans[0];
-  if (constraint >= (kind == 0 ? pl.n_hard : pl.n_soft)) return fail(c, KGPU_E_INVAL, "no such constraint");
-  const kgpu::TSpread& sp = kind == 0 ? pl.hard[constraint] : pl.soft[constraint];
+  int64_t D = 0;
+  if (kind == 0 || kind == 1) {
+    if (constraint >= (kind == 0 ? pl.n_hard : pl.n_soft)) return fail(c, KGPU_E_INVAL, "no such constraint");
+    const kgpu::TSpread& sp = kind == 0 ? pl.hard[constraint] : pl.soft[constraint];
+    D = sp.key >= 0 ? c->key_n_values[(size_t)sp.key] : 0;
+  }
   if ((rc = upload_pools(c, pools))) return rc;
   if ((rc = ensure(c, c->queries, sizeof(kgpu_pod_query)))) return rc;
   HIP_OK(c, hipMemcpyAsync(c->queries.p, q, sizeof(kgpu_pod_query), hipMemcpyHostToDevice, c->stream));
@@ -3503,16 +3501,39 @@ int kgpu_debug_pts_state(kgpu_ctx* c, const kgpu_pod_query* q, const kgpu_pools*
   a.pod = 0;
   a.prev = -1;
   const int blocks = kgpu::eval_blocks(c->st.N);
-  const int64_t D = sp.key >= 0 ? c->key_n_values[(size_t)sp.key] : 0;
-  // PreFilter: the histograms (k_topo_pre), the critical-path minima (k_topo_min); PreScore: the
-  // registrations of the filtered nodes (k_topo_filter) too
   if (kgpu::launch_topo_phase(dst, a, 0, blocks, 0, c->stream) ||
       (kind == 0 && D > 0 && kgpu::launch_topo_phase(dst, a, 1, blocks, D, c->stream)) ||
       (kind == 1 && kgpu::launch_topo_phase(dst, a, 2, blocks, 0, c->stream)))
     return fail(c, KGPU_E_DEVICE, "topology phase launch failed");
-  std::vector<int64_t> sc((size_t)pl.scratch_len);
+  sc.assign((size_t)pl.scratch_len, 0);
   HIP_OK(c, hipMemcpyAsync(sc.data(), c->st.scratch, sizeof(int64_t) * sc.size(), hipMemcpyDeviceToHost, c->stream));
   HIP_OK(c, hipStreamSynchronize(c->stream));
+  return KGPU_OK;
+}
+
+static int debug_topo_check(kgpu_ctx* c) {
+  if (hipSetDevice(c->device) != hipSuccess) return KGPU_E_DEVICE;
+  if (!c->uploaded) return fail(c, KGPU_E_STATE, "no snapshot uploaded");
+  if (c->comm || c->xg_nranks > 1)
+    return fail(c, KGPU_E_UNSUPPORTED, "the topology state diagnostics read one engine's state: unsharded only");
+  return KGPU_OK;
+}
+
+int kgpu_debug_pts_state(kgpu_ctx* c, const kgpu_pod_query* q, const kgpu_pools* pools, int32_t kind,
+                         int32_t constraint, uint8_t* registered, int64_t* counts, int64_t* scalar) try {
+  if (!c || !q || !registered || !counts || !scalar || (kind != 0 && kind != 1) || constraint < 0) return KGPU_E_INVAL;
+  int rc;
+  if ((rc = debug_topo_check(c))) return rc;
+  if (!has_filter(c, KGPU_F_POD_TOPOLOGY_SPREAD) && kind == 0)
+    return fail(c, KGPU_E_INVAL, "the profile has no PodTopologySpread filter");
+  if (!has_score(c, KGPU_S_POD_TOPOLOGY_SPREAD) && kind == 1)
+    return fail(c, KGPU_E_INVAL, "the profile has no PodTopologySpread score");
+  Staged sg;
+  std::vector<int64_t> sc;
+  if ((rc = debug_topo_scratch(c, q, pools, kind, constraint, sg, sc))) return rc;
+  const kgpu::QPlan& pl = sg.plans[0];
+  const kgpu::TSpread& sp = kind == 0 ? pl.hard[constraint] : pl.soft[constraint];
+  const int64_t D = sp.key >= 0 ? c->key_n_values[(size_t)sp.key] : 0;
   const kgpu::TopoHdr* h = reinterpret_cast<const kgpu::TopoHdr*>(sc.data());
   for (int64_t v = 0; v < D; ++v) {
     registered[v] = sc[(size_t)(pl.slot_off[sp.rslot] + v)] != 0 ? 1 : 0;
@@ -3527,6 +3548,39 @@ int kgpu_debug_pts_state(kgpu_ctx* c, const kgpu_pod_query* q, const kgpu_pools*
     // kubernetes.io/hostname the filtered nodes that carry every soft key
     *scalar = sp.is_hostname ? (int64_t)h->feas_nonign : (sp.first_of_key ? h->ssize[constraint] : -1);
   }
+  return KGPU_OK;
+} catch (...) {
+  return on_exception(c, false);
+}
+
+int kgpu_debug_ipa_state(kgpu_ctx* c, const kgpu_pod_query* q, const kgpu_pools* pools, int32_t max_maps,
+                         int32_t max_values, int32_t* kinds, int32_t* keys, int64_t* counts, int32_t* n_maps) try {
+  if (!c || !q || !kinds || !keys || !counts || !n_maps || max_maps < 0 || max_values < 0) return KGPU_E_INVAL;
+  int rc;
+  if ((rc = debug_topo_check(c))) return rc;
+  if (!has_filter(c, KGPU_F_INTER_POD_AFFINITY))
+    return fail(c, KGPU_E_INVAL, "the profile has no InterPodAffinity filter");
+  Staged sg;
+  std::vector<int64_t> sc;
+  if ((rc = debug_topo_scratch(c, q, pools, 2, 0, sg, sc))) return rc;
+  const kgpu::QPlan& pl = sg.plans[0];
+  // preFilterState's three maps (interpodaffinity/filtering.go:166-271), one histogram per (map,
+  // topology key): the terms of one map that share a key add into the same pairs, as they do there
+  int m = 0;
+  for (int s = 0; s < pl.n_slots; ++s) {
+    const int k = pl.slot_kind[s];
+    const int kind = k == kgpu::kSlotExA ? 0 : k == kgpu::kSlotAff ? 1 : k == kgpu::kSlotAnti ? 2 : -1;
+    if (kind < 0) continue;
+    if (m == max_maps) return fail(c, KGPU_E_INVAL, "more histograms than max_maps");
+    const int64_t D = pl.slot_key[s] >= 0 ? c->key_n_values[(size_t)pl.slot_key[s]] : 0;
+    if (D > max_values) return fail(c, KGPU_E_INVAL, "a topology key has more values than max_values");
+    kinds[m] = kind;
+    keys[m] = pl.slot_key[s];
+    for (int64_t v = 0; v < max_values; ++v)
+      counts[(size_t)m * max_values + v] = v < D ? sc[(size_t)(pl.slot_off[s] + v)] : 0;
+    ++m;
+  }
+  *n_maps = m;
   return KGPU_OK;
 } catch (...) {
   return on_exception(c, false);

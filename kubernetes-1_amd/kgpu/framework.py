@@ -275,9 +275,12 @@ class GpuFramework:
             res[nn] = (vs, int(o["num_pdb_violations"]))
         return res, (self.order[chosen] if chosen >= 0 else "")
 
-    def preempt(self, pod, statuses, pdbs=(), now=0):
-        """genericScheduler.Preempt (generic_scheduler.go:252-315, no extenders) after a FitError whose
-        per-node statuses are `statuses` ({node: (code, plugin, reasons)}, CycleResult.statuses).
+    def preempt(self, pod, statuses, pdbs=(), now=0, extenders=()):
+        """genericScheduler.Preempt (generic_scheduler.go:252-315) after a FitError whose per-node
+        statuses are `statuses` ({node: (code, plugin, reasons)}, CycleResult.statuses).
+        extenders: the profile's scheduler extenders, objects with supports_preemption() /
+        is_interested(pod) / is_ignorable() / process_preemption(pod, {node: (victims,
+        numPDBViolations)}, node_of) (processPreemptionWithExtenders, :317-351).
         Returns (node name or "", victim pods, nominated pods whose nomination is cleared)."""
         if not self._eligible_to_preempt(pod):
             return "", [], []
@@ -286,6 +289,9 @@ class GpuFramework:
         if not potential:
             return "", [], [pod]
         n2v, node = self.select_nodes_for_preemption(pod, pdbs, now, nodes=potential)
+        if extenders and n2v:
+            n2v = process_preemption_with_extenders(pod, n2v, extenders, self.nodes.get)
+            node = pick_one_node_for_preemption(n2v, now, self.order)
         if not node:
             return "", [], []
         prio = _priority(pod)
@@ -303,6 +309,61 @@ class GpuFramework:
                 if api.meta(p).get("deletionTimestamp") is not None and _priority(p) < prio:
                     return False
         return True
+
+
+def process_preemption_with_extenders(pod, n2v, extenders, node_of):
+    """processPreemptionWithExtenders (generic_scheduler.go:317-351): each extender that supports
+    preemption and is interested in the pod replaces the candidate map in turn; an ignorable
+    extender's error is skipped, any other is raised; an empty map ends the walk."""
+    for ext in extenders:
+        if not (ext.supports_preemption() and ext.is_interested(pod)):
+            continue
+        try:
+            new = ext.process_preemption(pod, n2v, node_of)
+        except Exception:
+            if ext.is_ignorable():
+                continue
+            raise
+        n2v = new
+        if not n2v:
+            break
+    return n2v
+
+
+def pick_one_node_for_preemption(n2v, now, order):
+    """pickOneNodeForPreemption (generic_scheduler.go:718-843) on the host over an extender-edited
+    candidate map ({node: (victim pods, numPDBViolations)}), walked in Snapshot.List() order: the
+    device's own pick (kgpu_select_victims) covers the map before any extender edits it."""
+    if not n2v:
+        return ""
+    max_i32 = (1 << 31) - 1
+    rank = {nn: i for i, nn in enumerate(order)}
+    nodes = sorted(n2v, key=lambda nn: rank.get(nn, len(rank)))
+    for nn in nodes:
+        if not n2v[nn][0]:
+            return nn
+    lo = min(n2v[nn][1] for nn in nodes)
+    cand = [nn for nn in nodes if n2v[nn][1] == lo]
+    # victims are sorted MoreImportantPod first: the first one has the highest priority
+    for key in (lambda nn: _priority(n2v[nn][0][0]),
+                lambda nn: sum(_priority(p) + max_i32 + 1 for p in n2v[nn][0]),
+                lambda nn: len(n2v[nn][0])):
+        if len(cand) == 1:
+            return cand[0]
+        lo = min(key(nn) for nn in cand)
+        cand = [nn for nn in cand if key(nn) == lo]
+    if len(cand) == 1:
+        return cand[0]
+    # the latest "earliest start time" among the victims of each node (GetEarliestPodStartTime)
+    def earliest(nn):
+        vs = n2v[nn][0]
+        hp = max(_priority(p) for p in vs)
+        return min(_start_time(p, now) for p in vs if _priority(p) == hp)
+    best = cand[0]
+    for nn in cand[1:]:
+        if earliest(nn) > earliest(best):
+            best = nn
+    return best
 
 
 def _pod_key(pod):

@@ -21,7 +21,7 @@ EXPORTS = ["kgpu_abi_version", "kgpu_struct_sizes", "kgpu_create", "kgpu_destroy
            "kgpu_read_phase_trace", "kgpu_comm_unique_id", "kgpu_comm_init", "kgpu_apply_delta",
            "kgpu_set_nominated", "kgpu_select_victims", "kgpu_xgmi_handle", "kgpu_xgmi_init", "kgpu_xgmi_active",
            "kgpu_comm_info",
-           "kgpu_debug_fail_alloc", "kgpu_debug_pts_state", "kgpu_debug_broken_linear",
+           "kgpu_debug_fail_alloc", "kgpu_debug_pts_state", "kgpu_debug_ipa_state", "kgpu_debug_broken_linear",
            "kgpu_debug_wg_trace",
            "kgpu_next_slot", "kgpu_adopt_pod"]
 
@@ -67,6 +67,7 @@ def lib():
     L.kgpu_comm_info.argtypes = [vp, vp]
     L.kgpu_debug_fail_alloc.argtypes = [i32]
     L.kgpu_debug_pts_state.argtypes = [vp, vp, C.POINTER(abi.Pools), i32, i32, vp, vp, C.POINTER(i64)]
+    L.kgpu_debug_ipa_state.argtypes = [vp, vp, C.POINTER(abi.Pools), i32, i32, vp, vp, vp, C.POINTER(i32)]
     L.kgpu_debug_broken_linear.argtypes = [vp, vp, i32, vp, i32, vp]
     L.kgpu_debug_wg_trace.argtypes = [vp, vp, i64, C.POINTER(i32)]
     L.kgpu_next_slot.argtypes = [vp]
@@ -225,6 +226,18 @@ class Engine:
         self._check(lib().kgpu_debug_pts_state(self.h, q.ctypes.data, C.byref(pools), kind, constraint,
                                                 reg.ctypes.data, cnt.ctypes.data, C.byref(out)))
         return reg[:n_values].astype(bool), cnt[:n_values], int(out.value)
+
+    def ipa_state(self, query, pools, max_values, max_maps=32):
+        """kgpu_debug_ipa_state: [(kind, key id, counts[max_values] int64)] of one pod's InterPodAffinity
+        PreFilter maps on the device (kind 0 existing anti-affinity, 1 affinity, 2 anti-affinity)."""
+        q = np.ascontiguousarray(np.asarray(query, abi.QUERY).reshape(1))
+        kinds = np.zeros(max_maps, np.int32)
+        keys = np.zeros(max_maps, np.int32)
+        cnt = np.zeros((max_maps, max(max_values, 1)), np.int64)
+        n = C.c_int32(0)
+        self._check(lib().kgpu_debug_ipa_state(self.h, q.ctypes.data, C.byref(pools), max_maps, max(max_values, 1),
+                                                kinds.ctypes.data, keys.ctypes.data, cnt.ctypes.data, C.byref(n)))
+        return [(int(kinds[m]), int(keys[m]), cnt[m, :max_values]) for m in range(n.value)]
 
     def next_slot(self):
         """kgpu_next_slot: the slot the next pod assumed by kgpu_schedule_* gets."""

@@ -150,6 +150,51 @@ class Framework:
                 return pl.name, st
         return None, None
 
+    def run_filter_plugins(self, state, pod, ni, run_all_filters=False):
+        """framework.go:477-502 RunFilterPlugins: PluginToStatus {plugin name: Status}, the first
+        non-Unschedulable failure becoming the only entry, as an Error."""
+        statuses = {}
+        for pl in self.filters:
+            st = pl.filter(state, pod, ni)
+            if P.is_success(st):
+                continue
+            if st.code not in (P.UNSCHEDULABLE, P.UNRESOLVABLE):
+                return {pl.name: P.Status(P.ERROR, 'running "%s" filter plugin for pod "%s": %s'
+                                          % (pl.name, NI.name(pod), ", ".join(st.reasons)))}
+            statuses[pl.name] = st
+            if not run_all_filters:
+                return statuses
+        return statuses
+
+    def run_score_plugins(self, state, pod, nodes):
+        """framework.go:579-656 RunScorePlugins: ({plugin: [[node, score], ...]}, None) or (None, Error status)."""
+        out = {}
+        for pl, _ in self.scores:
+            lst = []
+            for n in nodes:
+                sc, st = pl.score(state, pod, NI.name(n))
+                if not P.is_success(st):
+                    return None, P.Status(P.ERROR, 'error while running score plugin for pod "%s": %s'
+                                          % (NI.name(pod), ", ".join(st.reasons)))
+                lst.append([NI.name(n), sc])
+            out[pl.name] = lst
+        for pl, _ in self.scores:
+            if hasattr(pl, "normalize"):
+                st = pl.normalize(state, pod, out[pl.name])
+                if not P.is_success(st):
+                    return None, P.Status(P.ERROR, 'error while running normalize score plugin for pod "%s": '
+                                          'normalize score plugin "%s" failed with error %s'
+                                          % (NI.name(pod), pl.name, ", ".join(st.reasons)))
+        for pl, w in self.scores:
+            for sc in out[pl.name]:
+                if sc[1] > P.MAX_NODE_SCORE or sc[1] < P.MIN_NODE_SCORE:
+                    return None, P.Status(P.ERROR, 'error while applying score defaultWeights for pod "%s": score '
+                                          'plugin "%s" returns an invalid score %d, it should in the range of '
+                                          '[%d, %d] after normalizing' % (NI.name(pod), pl.name, sc[1],
+                                                                          P.MIN_NODE_SCORE, P.MAX_NODE_SCORE))
+                sc[1] = sc[1] * w
+        return out, None
+
     def run_prescore(self, state, pod, nodes):
         for pl in self.prescores:
             st = pl.prescore(state, pod, nodes)
@@ -181,6 +226,25 @@ class Framework:
                     raise ScheduleError("score plugin %s returns an invalid score %d" % (pl.name, sc[1]))
                 sc[1] = sc[1] * w
         return out
+
+
+def merge_statuses(statuses):
+    """PluginToStatus.Merge (framework/v1alpha1/interface.go:161-191): precedence Error >
+    UnschedulableAndUnresolvable > Unschedulable, every reason appended (Go iterates the map in
+    random order; here in plugin order)."""
+    if not statuses:
+        return None
+    final = P.Status(P.SUCCESS)
+    codes = set()
+    for st in statuses.values():
+        codes.add(st.code)
+        final.code = st.code
+        final.reasons.extend(st.reasons)
+    for c in (P.ERROR, P.UNRESOLVABLE, P.UNSCHEDULABLE):
+        if c in codes:
+            final.code = c
+            break
+    return final
 
 
 class Result:

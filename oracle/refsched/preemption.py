@@ -359,9 +359,31 @@ def lower_priority_nominated_pods(nominator, pod, node_name):
     return [p for p in nominator.pods_for_node(node_name) if pod_priority(p) < pp]
 
 
-def preempt(gs, pod, fit_error, pdbs=(), nominator=None, now=0):
-    """generic_scheduler.go:252-315 Preempt (no extenders).  Returns (node, victims,
-    nominated pods to clear); node "" when preemption cannot help."""
+def process_preemption_with_extenders(pod, n2v, extenders, node_of):
+    """generic_scheduler.go:317-351: every extender that supports preemption and is interested in the
+    pod narrows (or extends) the candidates in turn; an ignorable extender's error is skipped, any
+    other aborts Preempt.  extenders: objects with supports_preemption / is_interested /
+    is_ignorable / process_preemption(pod, n2v, node_of) (tests/fake_plugins.FakeExtender)."""
+    if not n2v:
+        return n2v
+    for ext in extenders:
+        if not (ext.supports_preemption() and ext.is_interested(pod)):
+            continue
+        try:
+            new = ext.process_preemption(pod, n2v, node_of)
+        except Exception:
+            if ext.is_ignorable():
+                continue
+            raise
+        n2v = new
+        if not n2v:
+            break
+    return n2v
+
+
+def preempt(gs, pod, fit_error, pdbs=(), nominator=None, now=0, extenders=()):
+    """generic_scheduler.go:252-315 Preempt.  Returns (node, victims, nominated pods to clear); node
+    "" when preemption cannot help."""
     from .framework import FitError, ScheduleError
     if not isinstance(fit_error, FitError):
         return "", [], []
@@ -378,6 +400,7 @@ def preempt(gs, pod, fit_error, pdbs=(), nominator=None, now=0):
     if st is not None:
         raise ScheduleError(repr(st))
     n2v = select_nodes_for_preemption(gs.fw, nominator, state, pod, potential, list(pdbs), now)
+    n2v = process_preemption_with_extenders(pod, n2v, extenders, lambda nn: snap.map[nn].node)
     cand = pick_one_node_for_preemption(n2v, now)
     if not cand:
         return "", [], []

@@ -106,11 +106,109 @@ class _FalseMap:
         return 0, P.Status(P.ERROR, "priority map encounters an error")
 
 
+# ---- framework/v1alpha1/framework_test.go:142-170 TestPlugin.Filter and :2007-2039 the injected
+# score plugins (TestScorePlugin, TestScoreWithNormalizePlugin): outcomes set by the table's args
+class _InjectedFilter:
+    def __init__(self, name, code):
+        self.name, self.code = name, code
+
+    def filter(self, state, pod, ni):
+        return P.Status(self.code, "injected filter status")
+
+
+class _InjectedScore:
+    def __init__(self, name, inj):
+        self.name, self.inj = name, inj
+
+    def score(self, state, pod, node_name):   # setScoreRes
+        if self.inj.get("scoreStatus", 0) != P.SUCCESS:
+            return 0, P.Status(self.inj["scoreStatus"], "injecting failure.")
+        return self.inj.get("scoreRes", 0), None
+
+
+class _InjectedScoreNormalize(_InjectedScore):
+    def normalize(self, state, pod, scores):  # injectNormalizeRes
+        if self.inj.get("normalizeStatus", 0) != P.SUCCESS:
+            return P.Status(self.inj["normalizeStatus"], "injecting failure.")
+        for sc in scores:
+            sc[1] = self.inj.get("normalizeRes", 0)
+        return None
+
+
 def factories(spec):
-    """spec: {"FakeFilter": {node: code}} or plain names -> Profile.plugin_factories."""
+    """spec: {"FakeFilter": {node: code}, "injected_filters": {name: code}, "injected_scores":
+    {name: {"normalize": bool, injectedResult fields}}} -> Profile.plugin_factories."""
+    spec = spec or {}
     out = {"TrueFilter": true_filter, "FalseFilter": false_filter, "MatchFilter": match_filter,
            "NoPodsFilter": no_pods_filter, "NumericMap": _Numeric, "ReverseNumericMap": _ReverseNumeric,
            "TrueMap": _TrueMap, "FalseMap": _FalseMap}
-    if "FakeFilter" in (spec or {}):
+    if "FakeFilter" in spec:
         out["FakeFilter"] = fake_filter(spec["FakeFilter"])
+    for name, code in (spec.get("injected_filters") or {}).items():
+        out[name] = (lambda n, c: lambda _h: _InjectedFilter(n, c))(name, code)
+    for name, inj in (spec.get("injected_scores") or {}).items():
+        cls = _InjectedScoreNormalize if inj.get("normalize") else _InjectedScore
+        out[name] = (lambda n, i, k: lambda _h: k(n, i))(name, inj, cls)
     return out
+
+
+# ---- core/extender_test.go:56-80,135-356 FakeExtender (predicates only, no node cache): the
+# preemption verb keeps a node when every predicate passes on it (selectVictimsOnNodeByExtender
+# without cachedNodeNameToInfo) and adds no victims
+class ExtenderError(Exception):
+    pass
+
+
+def _pred_true(pod, node):
+    return True
+
+
+def _pred_false(pod, node):
+    return False
+
+
+def _pred_machine1(pod, node):
+    return NI.name(node) == "machine1"
+
+
+def _pred_error(pod, node):
+    raise ExtenderError("Some error")
+
+
+PREDICATES = {"true": _pred_true, "false": _pred_false, "machine1": _pred_machine1, "error": _pred_error}
+
+
+class FakeExtender:
+    def __init__(self, predicates=(), ignorable=False, uninterested=False):
+        self.predicates = [PREDICATES[p] for p in predicates]
+        self.ignorable, self.uninterested = ignorable, uninterested
+
+    def supports_preemption(self):
+        return True
+
+    def is_ignorable(self):
+        return self.ignorable
+
+    def is_interested(self, pod):
+        return not self.uninterested
+
+    def run_predicate(self, pod, node):
+        for pr in self.predicates:
+            if not pr(pod, node):
+                return False
+        return True
+
+    def process_preemption(self, pod, node_to_victims, node_of):
+        """node_to_victims: {node name: (victims, num_pdb_violations)} in iteration order;
+        node_of(name) -> v1.Node.  Raises ExtenderError."""
+        out = dict(node_to_victims)
+        for nn in list(out):
+            if not self.run_predicate(pod, node_of(nn)):
+                del out[nn]
+        return out
+
+
+def extenders(specs):
+    """[{"predicates": [...], "ignorable": bool, "uninterested": bool}] -> FakeExtender list."""
+    return [FakeExtender(s.get("predicates", ()), s.get("ignorable", False), s.get("uninterested", False))
+            for s in specs or ()]

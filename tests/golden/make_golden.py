@@ -16,7 +16,7 @@ REF = "/root/reference"
 GROUPS = ["noderesources", "tainttoleration", "nodeaffinity", "normalize", "generic", "node_tree",
           "podtopologyspread", "interpodaffinity", "defaultpodtopologyspread", "imagelocality",
           "nodepreferavoidpods", "nodeports", "nodename", "nodeunschedulable", "requestedtocapacityratio",
-          "resourcelimits", "preemption", "misc"]
+          "resourcelimits", "preemption", "framework", "misc"]
 
 
 def resolve(cases):

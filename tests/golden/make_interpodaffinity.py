@@ -1,6 +1,13 @@
 """Golden vectors transcribed from pkg/scheduler/framework/plugins/interpodaffinity/
 {scoring_test.go (TestPreferredAffinity, TestPreferredAffinityWithHardPodAffinitySymmetricWeight),
-filtering_test.go (TestRequiredAffinitySingleNode, TestRequiredAffinityMultipleNodes)}."""
+filtering_test.go (TestRequiredAffinitySingleNode, TestRequiredAffinityMultipleNodes,
+TestPreFilterStateAddRemovePod, TestGetTPMapMatchingIncomingAffinityAntiAffinity)}.
+
+The two state tables (kind ipa_state, expect_ipa) compare preFilterState's maps: topologyToMatchedAffinityTerms
+("aff") and topologyToMatchedAntiAffinityTerms ("anti") as sorted [key, value, count] triples.  Op
+"add_remove" is TestPreFilterStateAddRemovePod: the expected maps hold after AddPod(added pod); the
+state after AddPod must also equal the PreFilter state of a snapshot that already holds the pod, and
+the state after RemovePod must equal the original."""
 from gen_common import case
 
 SSRC = "pkg/scheduler/framework/plugins/interpodaffinity/scoring_test.go"
@@ -352,5 +359,81 @@ def multi_node_cases():
     return out
 
 
+def state_cases():
+    out = []
+
+    def sc(name, line, p, existing, nodes, aff, anti, added=None, services=()):
+        kw = {}
+        if added is not None:
+            kw.update(op="add_remove", op_pod=added, op_node=added["spec"]["nodeName"])
+        else:
+            kw.update(op="prefilter")
+        out.append(case(name, FSRC + ":%d" % line, kind="ipa_state", plugin="InterPodAffinity", args={}, pod=p,
+                        pods=existing, nodes=nodes, services=list(services),
+                        expect_ipa={"aff": sorted([list(x) for x in aff]), "anti": sorted([list(x) for x in anti])},
+                        **kw))
+
+    # ---- TestPreFilterStateAddRemovePod (filtering_test.go:1697)
+    l1, l2, l3 = {"region": "r1", "zone": "z11"}, {"region": "r1", "zone": "z12"}, {"region": "r2", "zone": "z21"}
+    sel1 = {"foo": "bar"}
+    anti_foobar = {"requiredDuringSchedulingIgnoredDuringExecution": [term([req("foo", "In", ["bar"])], "region")]}
+    complex_terms = [term([req("foo", "In", ["bar", "buzz"])], "region"),
+                     term([req("service", "NotIn", ["bar", "security", "test"])], "zone")]
+    anti_complex = {"requiredDuringSchedulingIgnoredDuringExecution": complex_terms}
+    aff_complex = {"requiredDuringSchedulingIgnoredDuringExecution": [dict(t) for t in complex_terms]}
+    abc = lambda: [node("nodeA", l1), node("nodeB", l2), node("nodeC", l3)]  # noqa: E731
+    svc = [{"spec": {"selector": dict(sel1)}}]
+    sc("no affinity exist", 1795, pod(sel1, name="pending"),
+       [pod(sel1, "nodeA", name="p1"), pod(None, "nodeC", name="p2")], abc(), [], [],
+       added=pod(sel1, "nodeB", name="addedPod"))
+    sc("preFilterState anti-affinity terms are updated correctly after adding and removing a pod", 1820,
+       pod(sel1, name="pending", affinity={"podAntiAffinity": anti_foobar}),
+       [pod(sel1, "nodeA", name="p1"), pod(None, "nodeC", name="p2", affinity={"podAntiAffinity": anti_foobar})],
+       abc(), [], [("region", "r1", 2)],
+       added=pod(sel1, "nodeB", name="addedPod", affinity={"podAntiAffinity": anti_foobar}))
+    sc("preFilterState anti-affinity terms are updated correctly after adding and removing a pod", 1862,
+       pod(sel1, name="pending", affinity={"podAntiAffinity": anti_complex}),
+       [pod(sel1, "nodeA", name="p1"), pod(None, "nodeC", name="p2", affinity={"podAntiAffinity": anti_foobar})],
+       abc(), [], [("region", "r1", 2), ("zone", "z11", 2), ("zone", "z21", 1)],
+       added=pod(sel1, "nodeA", name="addedPod", affinity={"podAntiAffinity": anti_complex}), services=svc)
+    sc("preFilterState matching pod affinity and anti-affinity are updated correctly after adding and removing a pod",
+       1907, pod(sel1, name="pending", affinity={"podAffinity": aff_complex}),
+       [pod(sel1, "nodeA", name="p1"),
+        pod(None, "nodeC", name="p2", affinity={"podAntiAffinity": anti_foobar, "podAffinity": aff_complex})],
+       abc(), [("region", "r1", 2), ("zone", "z11", 2)], [],
+       added=pod(sel1, "nodeA", name="addedPod", affinity={"podAntiAffinity": anti_complex}), services=svc)
+
+    # ---- TestGetTPMapMatchingIncomingAffinityAntiAffinity (filtering_test.go:2045)
+    def terms(*keys):
+        return [term([req(k, "Exists")], "hostname") for k in keys]
+
+    def normal(*labels):
+        return pod({lb: "" for lb in labels}, "nodeA", name="normal")
+
+    node_a = lambda: [node("nodeA", {"hostname": "nodeA"})]  # noqa: E731
+
+    def both(aff_keys, anti_keys, name):
+        return pod(None, name=name, affinity={"podAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": terms(*aff_keys)},
+                                              "podAntiAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": terms(*anti_keys)}})
+
+    hn = ("hostname", "nodeA")
+    sc("nil test", 2087, pod(None, name="aaa-normal"), [], node_a(), [], [])
+    sc("incoming pod without affinity/anti-affinity causes a no-op", 2096, pod(None, name="aaa-normal"),
+       [normal("aaa")], node_a(), [], [])
+    sc("no pod has label that violates incoming pod's affinity and anti-affinity", 2106,
+       both(["aaa"], ["aaa"], "aaa-anti"), [normal("bbb")], node_a(), [], [])
+    sc("existing pod matches incoming pod's affinity and anti-affinity - single term case", 2126,
+       both(["aaa"], ["aaa"], "affi-antiaffi"), [normal("aaa")], node_a(), [hn + (1,)], [hn + (1,)])
+    sc("existing pod matches incoming pod's affinity and anti-affinity - multiple terms case", 2150,
+       both(["aaa", "bbb"], ["aaa"], "affi-antiaffi"), [normal("aaa", "bbb")], node_a(), [hn + (2,)], [hn + (1,)])
+    sc("existing pod not match incoming pod's affinity but matches anti-affinity", 2174,
+       both(["aaa", "bbb"], ["aaa", "bbb"], "affi-antiaffi"), [normal("aaa")], node_a(), [], [hn + (1,)])
+    sc("incoming pod's anti-affinity has more than one term - existing pod violates partial term - case 1", 2196,
+       both(["aaa", "ccc"], ["aaa", "ccc"], "anaffi-antiaffiti"), [normal("aaa", "bbb")], node_a(), [], [hn + (1,)])
+    sc("incoming pod's anti-affinity has more than one term - existing pod violates partial term - case 2", 2218,
+       both(["aaa", "bbb"], ["aaa", "bbb"], "affi-antiaffi"), [normal("bbb")], node_a(), [], [hn + (1,)])
+    return out
+
+
 def all_cases():
-    return score_cases() + single_node_cases() + multi_node_cases()
+    return score_cases() + single_node_cases() + multi_node_cases() + state_cases()

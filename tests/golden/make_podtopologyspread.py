@@ -3,9 +3,10 @@
 TestSingleConstraint, TestMultipleConstraints), scoring_test.go (TestPreScoreStateEmptyNodes,
 TestPodTopologySpreadScore)}.
 
-The state tables compare cycle state (pairs, critical paths, constraints) and run on the oracle
-only: the device keeps no per-pod state object, and its domain counts are checked through the
-filter and score tables and the sequence parity tests."""
+The state tables (kind pts_state) compare cycle state (pairs, critical paths, constraints).  They run
+on the oracle (tests/test_oracle_golden.py) and on the device (tests/test_pts_state_device.py): the
+PreFilter / PreScore rows through kgpu_debug_pts_state, the AddPod / RemovePod rows as ADD_POD /
+REMOVE_POD deltas (kgpu_apply_delta) followed by the same export."""
 from gen_common import case
 from st import DO_NOT_SCHEDULE as DNS, HOSTNAME, LS, N, P, SCHEDULE_ANYWAY as SA
 

@@ -1,5 +1,6 @@
 """Golden vectors transcribed from pkg/scheduler/core/generic_scheduler_test.go: TestSelectNodesForPreemption
-(:1273), TestPickOneNodeForPreemption (:1652) and TestNodesWherePreemptionMightHelp (:1931).
+(:1273), TestPickOneNodeForPreemption (:1652), TestNodesWherePreemptionMightHelp (:1931) and TestPreempt
+(:2047).
 
 The preemption tables prepend a FakeFilter whose return code is the case's filterReturnCode (Success
 unless stated); with Success it is a no-op, so those cases also run through the HIP path
@@ -212,5 +213,70 @@ def might_help():
     return out
 
 
+def preempt_cases():
+    """TestPreempt (:2047): genericScheduler.Preempt after a FitError whose statuses are the table's
+    failedNodeToStatusMap (default: machine1..3 Unschedulable), with the table's extenders
+    (FakeExtender predicates, tests/fake_plugins.py).  Then the reference marks the victims deleted,
+    nominates the preemptor to the node and calls Preempt again: no more pods may be preempted."""
+    out = []
+    label_keys = ["hostname", "zone", "region"]
+    lower, never = "PreemptLowerPriority", "Never"
+
+    def pre(name, line, preemptor, pods, expected_node, expected, plugins=("NodeResourcesFit",), node_names=None,
+            statuses=None, extenders=()):
+        ns = []
+        for n in node_names or ["machine1", "machine2", "machine3"]:
+            lab = {label_keys[i]: part for i, part in enumerate(n.split("/"))}
+            ns.append(make_node(lab["hostname"], 1000 * 5, DEF_MEM * 5, labels=lab))
+        names = [n["metadata"]["name"] for n in ns]
+        st = statuses or {nm: U for nm in names[:3]}
+        prof = {"filters": list(plugins), "prefilters": list(plugins), "prescores": [], "scores": []}
+        out.append(case(name, SRC + ":%d" % line, kind="preempt", profile=prof, nodes=ns, pods=pods, pod=preemptor,
+                        statuses=st, extenders=list(extenders), pdbs=[], now=NOW, order="given",
+                        expect_preempt={"node": expected_node, "victims": sorted(expected)}))
+
+    def running(name, prio, nn, containers=None, labels=None):
+        o = p(name, prio, nn, containers, labels=labels)
+        o["status"]["phase"] = "Running"
+        return o
+
+    def pod1(policy=lower):
+        o = p("pod1", HIGH, containers=VLARGE)
+        if policy is not None:
+            o["spec"]["preemptionPolicy"] = policy
+        return o
+
+    base = lambda: [running("m1.1", LOW, "machine1", SMALL), running("m1.2", LOW, "machine1", SMALL),  # noqa: E731
+                    running("m2.1", HIGH, "machine2", LARGE), running("m3.1", MID, "machine3", MEDIUM)]
+    ext_pods = lambda: [running("m1.1", MID, "machine1", SMALL), running("m1.2", LOW, "machine1", SMALL),  # noqa: E731
+                        running("m2.1", MID, "machine2", LARGE)]
+    pre("basic preemption logic", 2074, pod1(), base(), "machine1", ["m1.1", "m1.2"])
+    pre("One node doesn't need any preemption", 2095, pod1(), base()[:3], "machine3", [])
+    foo = {"matchExpressions": [{"key": "foo", "operator": "Exists"}]}
+    tsc = [{"maxSkew": 1, "topologyKey": "zone", "whenUnsatisfiable": "DoNotSchedule", "labelSelector": foo},
+           {"maxSkew": 1, "topologyKey": "hostname", "whenUnsatisfiable": "DoNotSchedule", "labelSelector": foo}]
+    fl = {"foo": ""}
+    pre("preemption for topology spread constraints", 2116,
+        p("p", HIGH, uid=False, labels=fl, topologySpreadConstraints=tsc),
+        [running("pod-a1", HIGH, "node-a", labels=fl), running("pod-a2", HIGH, "node-a", labels=fl),
+         running("pod-b1", LOW, "node-b", labels=fl), running("pod-x1", HIGH, "node-x", labels=fl),
+         running("pod-x2", HIGH, "node-x", labels=fl)],
+        "node-b", ["pod-b1"], plugins=("PodTopologySpread",), node_names=["node-a/zone1", "node-b/zone1", "node-x/zone2"],
+        statuses={"node-a": U, "node-b": U, "node-x": U})
+    pre("Scheduler extenders allow only machine1, otherwise machine3 would have been chosen", 2201, pod1(), ext_pods(),
+        "machine1", ["m1.1", "m1.2"], extenders=[{"predicates": ["true"]}, {"predicates": ["machine1"]}])
+    pre("Scheduler extenders do not allow any preemption", 2230, pod1(), ext_pods(), "", [],
+        extenders=[{"predicates": ["false"]}])
+    pre("One scheduler extender allows only machine1, the other returns error but ignorable. Only machine1 would be "
+        "chosen", 2256, pod1(), ext_pods(), "machine1", ["m1.1", "m1.2"],
+        extenders=[{"predicates": ["error"], "ignorable": True}, {"predicates": ["machine1"]}])
+    pre("One scheduler extender allows only machine1, but it is not interested in given pod, otherwise machine1 would "
+        "have been chosen", 2286, pod1(), ext_pods(), "machine3", [],
+        extenders=[{"predicates": ["machine1"], "uninterested": True}, {"predicates": ["true"]}])
+    pre("no preempting in pod", 2316, pod1(never), base(), "", [])
+    pre("PreemptionPolicy is nil", 2337, pod1(None), base(), "machine1", ["m1.1", "m1.2"])
+    return out
+
+
 def all_cases():
-    return select_nodes() + pick_one() + might_help()
+    return select_nodes() + pick_one() + might_help() + preempt_cases()

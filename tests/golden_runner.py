@@ -131,6 +131,14 @@ def oracle_eval(c):
                                 lambda t, r: t.remove_node(r) is not None)
     if kind == "pts_state":
         return pts_state(c)
+    if kind == "ipa_state":
+        return ipa_state(c)
+    if kind == "run_score":
+        return run_score(c)
+    if kind == "run_filter":
+        return run_filter(c)
+    if kind == "preempt":
+        return preempt_full(c)
     if kind == "broken_linear":
         pl = P.RequestedToCapacityRatio(None, [], [])
         pl.shape = [tuple(x) for x in c["points"]]
@@ -222,6 +230,85 @@ def pts_state(c):
                       "paths": paths, "pairs": sorted([k, v, n] for (k, v), n in s["pairs"].items())}}
 
 
+RUNNER_NODES = [{"metadata": {"name": "node1"}}, {"metadata": {"name": "node2"}}]  # framework_test.go:338-341
+
+
+def run_score(c):
+    """RunScorePlugins (framework.go:579-656) with the table's injected score plugins."""
+    fw = F.Framework(profile_from_case(c), F.Handle(NI.Snapshot(RUNNER_NODES)))
+    out, st = fw.run_score_plugins({}, {"metadata": {"name": ""}}, RUNNER_NODES)
+    if st is not None:
+        return {"error": ", ".join(st.reasons)}
+    return {"run_scores": out}
+
+
+def run_filter(c):
+    """RunFilterPlugins + PluginToStatus.Merge (framework.go:477-502, interface.go:161-191)."""
+    fw = F.Framework(profile_from_case(c), F.Handle(NI.Snapshot(RUNNER_NODES)))
+    ni = NI.NodeInfo(RUNNER_NODES[0])
+    sm = fw.run_filter_plugins({}, {"metadata": {"name": ""}}, ni, run_all_filters=c.get("run_all_filters", False))
+    merged = F.merge_statuses(sm)
+    return {"status_map": {k: {"code": v.code, "reasons": list(v.reasons)} for k, v in sm.items()},
+            "merged": None if merged is None else {"code": merged.code, "reasons": list(merged.reasons)}}
+
+
+def preempt_full(c):
+    """genericScheduler.Preempt (generic_scheduler.go:252-351, extenders included) after a FitError with
+    the case's statuses, then the second call of TestPreempt (:2440-2460) with the victims marked
+    deleted and the preemptor nominated to the chosen node."""
+    import copy
+    import fake_plugins
+    from oracle.refsched import preemption as PR
+    c = copy.deepcopy(c)
+    prof = profile_from_case(c)
+    snap = NI.Snapshot(c["nodes"], c.get("pods", []), order=c.get("order", "given"))
+    gs = F.GenericScheduler(F.Framework(prof, F.Handle(snap)))
+    fe = F.FitError({n: (None, P.Status(code, "")) for n, code in c["statuses"].items()})
+    now = PR.pod_start_time({"status": {"startTime": c["now"]}}, 0)
+    pod = c["pod"]
+    ext = fake_plugins.extenders(c.get("extenders"))
+    node, victims, _ = PR.preempt(gs, pod, fe, c.get("pdbs", []), None, now, extenders=ext)
+    names = {NI.name(v) for v in victims}
+    for ni in snap.list:
+        for pi in ni.pods:
+            if NI.name(pi.pod) in names:
+                pi.pod.setdefault("metadata", {})["deletionTimestamp"] = c["now"]
+    pod.setdefault("status", {})["nominatedNodeName"] = node
+    node2, victims2, _ = PR.preempt(gs, pod, fe, c.get("pdbs", []), None, now, extenders=ext)
+    return {"preempt": {"node": node, "victims": sorted(names), "again": [node2, len(victims2)]}}
+
+
+def ipa_state(c):
+    """InterPodAffinity preFilterState maps after PreFilter, and for op add_remove after AddPod (with
+    the two DeepEqual checks of filtering_test.go:1990-2030: AddPod's state equals PreFilter over a
+    snapshot that holds the pod, RemovePod restores the original)."""
+    def prefilter(pods):
+        h = _handle(dict(c, pods=pods))
+        pl = make_plugin("InterPodAffinity", c.get("args"), h)
+        state = {}
+        st = pl.prefilter(state, c["pod"])
+        return pl, h, state, st
+
+    def maps(state):
+        s = state["PreFilterInterPodAffinity"]
+        return {k: sorted([a, b, n] for (a, b), n in s[k].items()) for k in ("existing_anti", "aff", "anti")}
+
+    pl, h, state, st = prefilter(c.get("pods", []))
+    if not P.is_success(st):
+        return {"error": repr(st)}
+    m = maps(state)
+    out = {"aff": m["aff"], "anti": m["anti"], "existing_anti": m["existing_anti"]}
+    if c["op"] == "add_remove":
+        ni = h.snapshot.get(c["op_node"])
+        pl.add_pod(state, c["pod"], c["op_pod"], ni)
+        added = maps(state)
+        _, _, all_state, _ = prefilter(list(c.get("pods", [])) + [c["op_pod"]])
+        pl.remove_pod(state, c["pod"], c["op_pod"], ni)
+        out = {"aff": added["aff"], "anti": added["anti"], "existing_anti": added["existing_anti"],
+               "add_equals_all": added == maps(all_state), "remove_restores": maps(state) == m}
+    return {"ipa": out}
+
+
 def profile_from_case(c):
     p = c.get("profile") or {}
     kw = {}
@@ -276,6 +363,29 @@ def check(c, got):
         bad.append(("num", c["expect_num"], got.get("num")))
     if "expect_state" in c:
         bad += _check_state(c["expect_state"], got.get("state") or {})
+    if "expect_run_scores" in c and got.get("run_scores") != c["expect_run_scores"]:
+        bad.append(("run_scores", c["expect_run_scores"], got.get("run_scores")))
+    if "expect_status_map" in c:
+        if got.get("status_map") != c["expect_status_map"]:
+            bad.append(("status_map", c["expect_status_map"], got.get("status_map")))
+        if got.get("merged") != c["expect_merged"]:
+            bad.append(("merged", c["expect_merged"], got.get("merged")))
+    if "expect_preempt" in c:
+        g = got.get("preempt") or {}
+        if g.get("node") != c["expect_preempt"]["node"] or g.get("victims") != c["expect_preempt"]["victims"]:
+            bad.append(("preempt", c["expect_preempt"], g))
+        again = g.get("again") or ["", 0]
+        if again[0] and again[1] > 0:  # generic_scheduler_test.go:2455-2457
+            bad.append(("preempted again", again))
+    if "expect_ipa" in c:
+        g = got.get("ipa") or {}
+        for f in ("aff", "anti"):
+            if g.get(f) != c["expect_ipa"][f]:
+                bad.append((f, c["expect_ipa"][f], g.get(f)))
+        if c.get("op") == "add_remove":
+            for f in ("add_equals_all", "remove_restores"):
+                if g.get(f) is not True:
+                    bad.append((f, True, g.get(f)))
     for f in ("output", "tree", "remove_errors"):
         if "expect_" + f in c and got.get(f) != c["expect_" + f]:
             bad.append((f, c["expect_" + f], got.get(f)))

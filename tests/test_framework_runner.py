@@ -1,0 +1,53 @@
+"""The reference's framework runner table TestFilterPlugins (framework_test.go:838, tests/golden/
+framework.json) on the device.
+
+The table's test plugins return injected codes.  The device evaluates real plugins, so each injected
+outcome is realised by a real filter plugin that yields exactly that code on the table's one node:
+Success -> NodeName (the pod names no node), Unschedulable -> NodeResourcesFit (the pod asks for more
+cpu than the node has: "Insufficient cpu"), UnschedulableAndUnresolvable -> NodeUnschedulable (an
+unschedulable node).  The device's status word must then name the same plugin position and code as
+RunFilterPlugins + Merge does for the test plugins.
+
+Not on the device, and why:
+  * rows injecting Error: the device's filters never return Error -- the Go runner turns any code
+    other than Unschedulable(AndUnresolvable) into an Error itself (framework.go:486-492), and that
+    code stays in the Go framework around the plugin;
+  * runAllFilters rows (WithRunAllFilters, alwaysCheckAllPredicates): the engine reports the FIRST
+    failing filter, as the default runner does; run-all merging is not implemented;
+  * TestRunScorePlugins: its plugins inject raw and normalized scores the device's plugins cannot
+    produce.  Weights, NormalizeScore and the sum run on the device for the real plugins and are
+    pinned by TestZeroRequest and every score table; the range check guards plugin bugs the
+    device's plugins cannot have.
+Those rows are pinned on the oracle's runner (tests/test_oracle_golden.py)."""
+import pytest
+
+from conftest import load_golden
+from kgpu.compile import Profile
+from kgpu.framework import GpuFramework
+
+REAL = {0: "NodeName", 2: "NodeResourcesFit", 3: "NodeUnschedulable"}
+ROWS = [c for c in load_golden("framework") if c["kind"] == "run_filter" and not c["run_all_filters"]
+        and all(code in REAL for code in c["profile"]["fake"]["injected_filters"].values())]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ROWS, ids=["%s:%s" % (c["src"].rsplit(":", 1)[1], c["name"]) for c in ROWS])
+def test_filter_runner_on_device(case):
+    fake = [(p, case["profile"]["fake"]["injected_filters"][p]) for p in case["profile"]["filters"]]
+    real = [REAL[code] for _, code in fake]
+    assert len(set(real)) == len(real)
+    node = {"metadata": {"name": "node1"}, "spec": {"unschedulable": True},
+            "status": {"allocatable": {"cpu": "1", "memory": "1Gi", "pods": "10"}}}
+    pod = {"metadata": {"name": "p", "namespace": "default", "uid": "p"},
+           "spec": {"containers": [{"name": "c", "resources": {"requests": {"cpu": "2"}}}]}}
+    fw = GpuFramework(Profile(filters=real, scores=[]), [node], [], pods_hint=[pod])
+    res = fw.cycle(pod)
+    want = case["expect_merged"]
+    if want is None:
+        assert res.statuses == {} and res.host == "node1", res.statuses
+    else:
+        code, plugin, _ = res.statuses["node1"]
+        first = next(i for i, (_, c) in enumerate(fake) if c != 0)
+        assert (code, plugin) == (want["code"], real[first]), (case["name"], code, plugin)
+        assert list(case["expect_status_map"]) == [fake[first][0]]
+    fw.engine.close()

@@ -250,3 +250,36 @@ def test_golden_nodes_where_preemption_might_help(case):
     from kgpu.framework import nodes_where_preemption_might_help
     got = nodes_where_preemption_might_help(case["node_names"], case["statuses"])
     assert sorted(got) == case["expect_set"], (case["name"], got)
+
+
+# ---------------------------------------------------------------- TestPreempt (generic_scheduler_test.go:2047)
+PREEMPT = [c for c in load_golden("preemption") if c["kind"] == "preempt"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", PREEMPT, ids=[c["src"].rsplit(":", 1)[1] for c in PREEMPT])
+def test_golden_preempt_gpu(case):
+    """genericScheduler.Preempt through the product (GpuFramework.preempt: nodesWherePreemptionMightHelp,
+    kgpu_select_victims on the device, the table's extenders), then the table's second call with the
+    victims marked deleted and the preemptor nominated to the node: nothing more may be preempted."""
+    import copy
+    import fake_plugins
+    case = copy.deepcopy(case)
+    fw = GpuFramework(_gpu_profile(case), case["nodes"], case["pods"], pods_hint=[case["pod"]])
+    now = PR.pod_start_time({"status": {"startTime": case["now"]}}, 0)
+    statuses = {nn: (code, None, []) for nn, code in case["statuses"].items()}
+    ext = fake_plugins.extenders(case.get("extenders"))
+    pod = case["pod"]
+    node, victims, _ = fw.preempt(pod, statuses, case.get("pdbs", []), now, extenders=ext)
+    want = case["expect_preempt"]
+    assert node == want["node"], (case["name"], node)
+    names = sorted(NI.name(v) for v in victims)
+    assert names == want["victims"], (case["name"], names)
+    for pods in fw.node_pods.values():
+        for p, _ in pods:
+            if NI.name(p) in names:
+                p["metadata"]["deletionTimestamp"] = case["now"]
+    pod.setdefault("status", {})["nominatedNodeName"] = node
+    node2, victims2, _ = fw.preempt(pod, statuses, case.get("pdbs", []), now, extenders=ext)
+    assert not (node2 and victims2), (case["name"], node2, victims2)
+    fw.engine.close()

@@ -1,41 +1,50 @@
-"""PodTopologySpread PreFilter / PreScore STATE on the device against the reference's own state tables
-(tests/golden/podtopologyspread.json, kind pts_state, transcribed from
-podtopologyspread/filtering_test.go:543 TestPreFilterState and scoring_test.go:38 TestPreScoreStateEmptyNodes).
+"""Topology-plugin PreFilter / PreScore STATE on the device against the reference's own state tables.
 
-kgpu_debug_pts_state exports what the device builds for one pod: per value of a constraint's key,
-whether the pair is registered and its count (TpPairToMatchNum / TopologyPairToPodCounts), and
-criticalPaths[0].MatchNum (PreFilter) or the topology size behind topologyNormalizingWeight (PreScore).
-The tables' AddPod / RemovePod cases (filtering_test.go:857,1146) update a PreFilter state in place;
-the device applies those updates only inside the nominated / preemption passes (k_victims), whose
-verdicts tests/test_preemption.py compares with the oracle's update_with_pod.  They run on the oracle
-(tests/test_oracle_golden.py)."""
+PodTopologySpread (tests/golden/podtopologyspread.json, kind pts_state): filtering_test.go:543
+TestPreFilterState, :857/:1146 TestPreFilterStateAddPod / RemovePod and scoring_test.go:38
+TestPreScoreStateEmptyNodes.  kgpu_debug_pts_state exports what the device builds for one pod: per value
+of a constraint's key, whether the pair is registered and its count (TpPairToMatchNum /
+TopologyPairToPodCounts), and criticalPaths[0].MatchNum (PreFilter) or the topology size behind
+topologyNormalizingWeight (PreScore).
+
+InterPodAffinity (tests/golden/interpodaffinity.json, kind ipa_state): filtering_test.go:1697
+TestPreFilterStateAddRemovePod and :2045 TestGetTPMapMatchingIncomingAffinityAntiAffinity through
+kgpu_debug_ipa_state (the three preFilterState maps).
+
+The AddPod / RemovePod rows run as what the device actually does when a pod lands on or leaves a
+node: a kgpu_apply_delta ADD_POD / REMOVE_POD through the host cache mirror (kgpu/cache.py, no
+re-upload), then the state export of the next cycle.  For the inter-pod affinity rows the state after
+the add must also equal the state of an engine uploaded with the pod already in place, and the
+remove must restore the original state, as the reference test's two DeepEqual checks require
+(filtering_test.go:1990-2030).  TestPreFilterStateRemovePod's "delete a non-existing pod" row has
+no pod to remove from a cache: its state is the unchanged one, which is what the table expects."""
+import numpy as np
 import pytest
 
 from conftest import load_golden
-from kgpu.compile import Cluster, Profile
+from kgpu.cache import SchedulerCache
+from kgpu.compile import Cluster, Pools, Profile
 from kgpu.framework import GpuFramework
 from oracle.refsched.golog import go_log
 
-CASES = [c for c in load_golden("podtopologyspread")
-         if c["kind"] == "pts_state" and c["op"] in ("prefilter", "prescore") and "expect_state" in c]
+PTS = [c for c in load_golden("podtopologyspread") if c["kind"] == "pts_state" and "expect_state" in c]
+IPA = [c for c in load_golden("interpodaffinity") if c["kind"] == "ipa_state"]
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("case", CASES, ids=["%s:%s" % (c["op"], c["name"][:50]) for c in CASES])
-def test_pts_state_on_device(case):
-    a = case.get("args") or {}
-    # PreFilter: the filter alone; PreScore over every node (the tables pass the whole list as filtered)
-    prefilter = case["op"] == "prefilter"
-    prof = Profile(filters=["PodTopologySpread"] if prefilter else [],
-                   scores=[] if prefilter else [("PodTopologySpread", 1)],
-                   pts_default_constraints=a.get("default_constraints", []))
-    cluster = Cluster(case.get("services", []), case.get("rcs", []), case.get("rss", []), case.get("sss", []))
-    fw = GpuFramework(prof, case["nodes"], case.get("pods", []), cluster=cluster, pods_hint=[case["pod"]])
-    q, pc, _, errs = fw.compile_pods([case["pod"]])
-    assert not errs
+def _cluster(case):
+    return Cluster(case.get("services", []), case.get("rcs", []), case.get("rss", []), case.get("sss", []))
+
+
+def _query(comp, pod):
+    pools = Pools()
+    q = comp.compile_pod(pod, pools)
+    pc, _ = pools.finalize()
+    return np.array([q]), pc
+
+
+def _pts_check(case, engine, comp, q, pc, kind):
     want = case["expect_state"]
-    kind = 0 if case["op"] == "prefilter" else 1
-    nk = fw.compiler.nkeys
+    nk = comp.nkeys
     pairs = {}
     for k, v, n in want["pairs"]:
         pairs.setdefault(k, {})[v] = n
@@ -47,7 +56,7 @@ def test_pts_state_on_device(case):
             checked += 1
             continue
         D = len(nk.vals[ki].items)
-        reg, cnt, scalar = fw.engine.pts_state(q[0], pc, kind, i, D)
+        reg, cnt, scalar = engine.pts_state(q[0], pc, kind, i, D)
         got = {nk.vals[ki].items[v]: int(cnt[v]) for v in range(D) if reg[v]}
         if kind == 1 and key == "kubernetes.io/hostname":
             # scoring.go:83-86,196-198: hostname pairs are never registered; counts are per node at Score
@@ -60,4 +69,80 @@ def test_pts_state_on_device(case):
             assert go_log(float(scalar + 2)) == want["weights"][i], (case["name"], key, scalar)
         checked += 1
     assert checked or not want["constraints"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", PTS, ids=["%s:%s" % (c["op"], c["name"][:50]) for c in PTS])
+def test_pts_state_on_device(case):
+    a = case.get("args") or {}
+    # PreFilter: the filter alone; PreScore over every node (the tables pass the whole list as filtered)
+    prescore = case["op"] == "prescore"
+    prof = Profile(filters=[] if prescore else ["PodTopologySpread"],
+                   scores=[("PodTopologySpread", 1)] if prescore else [],
+                   pts_default_constraints=a.get("default_constraints", []))
+    if case["op"] in ("add", "remove"):
+        hint = [case["pod"], case["op_pod"]]
+        cache = SchedulerCache(prof, case["nodes"], case.get("pods", []), cluster=_cluster(case), pods_hint=hint)
+        try:
+            if case["op"] == "add":
+                cache.add_pod(case["op_pod"])
+            elif any(p["metadata"]["name"] == case["op_pod"]["metadata"]["name"] and
+                     p["metadata"].get("namespace", "") == case["op_pod"]["metadata"].get("namespace", "")
+                     for p in case.get("pods", [])):
+                cache.remove_pod(case["op_pod"])
+            cache.sync()
+            assert cache.uploads == 1  # the change went through kgpu_apply_delta
+            q, pc = _query(cache.compiler, case["pod"])
+            _pts_check(case, cache.engine, cache.compiler, q, pc, 0)
+        finally:
+            cache.close()
+        return
+    fw = GpuFramework(prof, case["nodes"], case.get("pods", []), cluster=_cluster(case), pods_hint=[case["pod"]])
+    q, pc, _, errs = fw.compile_pods([case["pod"]])
+    assert not errs
+    _pts_check(case, fw.engine, fw.compiler, q, pc, 1 if prescore else 0)
     fw.engine.close()
+
+
+IPA_KINDS = ("existing_anti", "aff", "anti")
+
+
+def _ipa_maps(engine, comp, pod):
+    q, pc = _query(comp, pod)
+    nk = comp.nkeys
+    D = max([len(d.items) for d in nk.vals] + [1])
+    out = {k: {} for k in IPA_KINDS}
+    for kind, key, counts in engine.ipa_state(q[0], pc, D):
+        for v in np.nonzero(counts)[0]:
+            pair = (nk.keys.items[key], nk.vals[key].items[int(v)])
+            out[IPA_KINDS[kind]][pair] = out[IPA_KINDS[kind]].get(pair, 0) + int(counts[v])
+    return {k: sorted([a, b, n] for (a, b), n in m.items()) for k, m in out.items()}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", IPA, ids=["%s:%s" % (c["src"].rsplit(":", 1)[1], c["name"][:60]) for c in IPA])
+def test_ipa_state_on_device(case):
+    prof = Profile(filters=["InterPodAffinity"], scores=[])
+    hint = [case["pod"]] + ([case["op_pod"]] if case["op"] == "add_remove" else [])
+    cache = SchedulerCache(prof, case["nodes"], case.get("pods", []), cluster=_cluster(case), pods_hint=hint)
+    try:
+        before = _ipa_maps(cache.engine, cache.compiler, case["pod"])
+        want = case["expect_ipa"]
+        if case["op"] != "add_remove":
+            assert before["aff"] == want["aff"] and before["anti"] == want["anti"], (case["name"], before)
+            return
+        cache.add_pod(case["op_pod"])
+        cache.sync()
+        assert cache.uploads == 1  # the change went through kgpu_apply_delta
+        after = _ipa_maps(cache.engine, cache.compiler, case["pod"])
+        assert after["aff"] == want["aff"] and after["anti"] == want["anti"], (case["name"], after)
+        # DeepEqual(allPodsState, state): an engine uploaded with the pod already in place
+        fw = GpuFramework(prof, case["nodes"], list(case.get("pods", [])) + [case["op_pod"]], cluster=_cluster(case),
+                          pods_hint=hint)
+        assert _ipa_maps(fw.engine, fw.compiler, case["pod"]) == after, case["name"]
+        fw.engine.close()
+        cache.remove_pod(case["op_pod"])
+        cache.sync()
+        assert _ipa_maps(cache.engine, cache.compiler, case["pod"]) == before, case["name"]
+    finally:
+        cache.close()
