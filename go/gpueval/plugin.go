@@ -159,6 +159,7 @@ type GpuEval struct {
 	mir       *mirror
 	seq       int64
 	nominated bool     // the engine holds a non-empty nominator
+	nomLast   []string // nodes that held nominated pods at the last sync (preempt.go syncNominated)
 	ahead     *ahead   // batch-ahead (ahead.go; profileArgs.BatchAhead > 1, select mode)
 	track     *tracker // nodes whose NodeInfo may have moved since the last sync (track.go)
 	exact     bool     // compare every generation at every sync
@@ -560,6 +561,7 @@ func New(obj runtime.Object, h framework.FrameworkHandle) (framework.Plugin, err
 		g.ahead = &ahead{depth: prof.BatchAhead}
 	}
 	g.watch()
+	register(h, g) // genericScheduler.Preempt finds it by the profile's framework (preempt.go)
 	return g, nil
 }
 

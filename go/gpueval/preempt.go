@@ -4,12 +4,25 @@ package gpueval
 //
 // PreFilter copies the PreemptHandle's PodNominator into the engine (kgpu_set_nominated), so the
 // cycle's status words already hold podPassesFiltersOnNode's two-pass verdict
-// (generic_scheduler.go:526-615).  Preemption: this reference version runs genericScheduler.Preempt
-// in-tree before the PostFilter plugins (scheduler.go:543-562), and Preempt re-runs the Filter
-// plugins on NodeInfo clones with victims removed, which a status-word lookup cannot answer.  The
-// drop-in is SelectVictims: the body of Preempt after its eligibility checks
-// (generic_scheduler.go:263-301), called from a two-line patch of genericScheduler.Preempt or from
-// PostFilter once preemption moves there (the TODO at scheduler.go:548).
+// (generic_scheduler.go:526-615).
+//
+// Preemption.  This reference version runs genericScheduler.Preempt in-tree, before the PostFilter
+// plugins (scheduler.go:543-562), and only that path evicts: sched.preempt deletes the victims and
+// records the nomination.  A PostFilter plugin here can only return a NominatedNodeName, which would
+// nominate the pod to a node whose victims nobody deletes -- so this package ships no PostFilter.
+// Preempt's candidate search, selectNodesForPreemption (generic_scheduler.go:845-876), re-runs the
+// Filter plugins on NodeInfo clones with victims removed, which a status-word lookup cannot answer.
+// The drop-in replaces exactly that call (INTEGRATION.md section 9):
+//
+//	if gp := gpueval.ForFramework(prof.Framework); gp != nil {
+//		nodeNameToVictims, err = gp.SelectNodesForPreemption(ctx, pod, potentialNodes, pdbs)
+//	} else {
+//		nodeNameToVictims, err = selectNodesForPreemption(ctx, prof, g.podNominator, state, pod, potentialNodes, pdbs)
+//	}
+//
+// so Preempt keeps its own eligibility checks, the real PDB list (g.pdbLister), the extenders
+// (processPreemptionWithExtenders) and pickOneNodeForPreemption.  ForFramework finds the plugin by
+// the FrameworkHandle New received, which is the *framework profile.Profile embeds.
 
 /*
 #include "kgpu.h"
@@ -19,27 +32,78 @@ import "C"
 import (
 	"context"
 	"fmt"
+	"sync"
 
 	v1 "k8s.io/api/core/v1"
 	policy "k8s.io/api/policy/v1beta1"
 	metav1 "k8s.io/apimachinery/pkg/apis/meta/v1"
 	"k8s.io/apimachinery/pkg/labels"
+	extenderv1 "k8s.io/kube-scheduler/extender/v1"
 	podutil "k8s.io/kubernetes/pkg/api/v1/pod"
 	framework "k8s.io/kubernetes/pkg/scheduler/framework/v1alpha1"
 	"k8s.io/kubernetes/pkg/scheduler/util"
 )
 
-// syncNominated sends NominatedPodsForNode of every listed node to the engine.
+// The plugins New built, by the FrameworkHandle they were built with (one per profile).
+var (
+	registryMu sync.Mutex
+	registry   = map[framework.FrameworkHandle]*GpuEval{}
+)
+
+func register(h framework.FrameworkHandle, g *GpuEval) {
+	registryMu.Lock()
+	registry[h] = g
+	registryMu.Unlock()
+}
+
+// ForFramework returns the GpuEval of the profile whose framework is fw (profile.Profile.Framework),
+// or nil when that profile does not run one.
+func ForFramework(fw framework.FrameworkHandle) *GpuEval {
+	if fw == nil {
+		return nil
+	}
+	registryMu.Lock()
+	defer registryMu.Unlock()
+	return registry[fw]
+}
+
+// syncNominated sends the PodNominator's pods to the engine.  It asks NominatedPodsForNode only
+// about the nodes that may hold nominated pods (track.go: the informers' NominatedNodeName, the
+// candidates of this plugin's preemptions) and the nodes that held some at the last sync, so a cycle
+// costs O(nominated) map operations, not one per listed node.
 func (g *GpuEval) syncNominated(a *arena) error {
 	ph := g.h.PreemptHandle()
 	if ph == nil {
 		return nil
 	}
+	cand := map[string]struct{}{}
+	for _, n := range g.nomLast {
+		cand[n] = struct{}{}
+	}
+	for _, n := range g.track.nominations() {
+		cand[n] = struct{}{}
+	}
+	if len(cand) == 0 && !g.nominated {
+		return nil
+	}
+	idx := make([]int32, 0, len(cand))
+	for n := range cand {
+		if i, ok := g.mir.index[n]; ok {
+			idx = append(idx, i)
+		}
+	}
+	sortInt32s(idx) // Snapshot.List() order, as a walk over the list would send them
 	var noms []C.kgpu_nominated
 	var recs []C.kgpu_pod_query
 	p := &pools{}
-	for i, name := range g.mir.names {
-		for _, np := range ph.NominatedPodsForNode(name) {
+	g.nomLast = g.nomLast[:0]
+	for _, i := range idx {
+		name := g.mir.names[i]
+		pods := ph.NominatedPodsForNode(name)
+		if len(pods) > 0 {
+			g.nomLast = append(g.nomLast, name)
+		}
+		for _, np := range pods {
 			q, err := g.comp.compilePod(np, p)
 			if err != nil {
 				return err
@@ -53,6 +117,14 @@ func (g *GpuEval) syncNominated(a *arena) error {
 	}
 	g.nominated = len(noms) > 0
 	return g.eng.setNominated(noms, recs, p.toC(a))
+}
+
+func sortInt32s(x []int32) {
+	for i := 1; i < len(x); i++ {
+		for k := i; k > 0 && x[k] < x[k-1]; k-- {
+			x[k], x[k-1] = x[k-1], x[k]
+		}
+	}
 }
 
 // pdbsOf: indices of the PodDisruptionBudgets selecting the pod, in the caller's order
@@ -76,24 +148,47 @@ func pdbsOf(pod *v1.Pod, pdbs []*policy.PodDisruptionBudget) []int {
 	return out
 }
 
-// SelectVictims runs selectNodesForPreemption + pickOneNodeForPreemption for a pod whose cycle
-// ended in a FitError (its PreFilter ran on this snapshot).  Returns the node and the victims, in
-// Victims.Pods order; "" when no node can make room.
+// SelectNodesForPreemption replaces selectNodesForPreemption (generic_scheduler.go:845-876) for a pod
+// whose cycle ended in a FitError: every node of potentialNodes where the pod fits once lower-priority
+// pods are removed, with the victims selectVictimsOnNode keeps (Victims.Pods order) and the PDB
+// violations among them.  pdbs: the cluster's PodDisruptionBudgets, as Preempt lists them.
+func (g *GpuEval) SelectNodesForPreemption(ctx context.Context, pod *v1.Pod, potentialNodes []*framework.NodeInfo,
+	pdbs []*policy.PodDisruptionBudget) (map[string]*extenderv1.Victims, error) {
+	out, _, err := g.selectOnDevice(pod, potentialNodes, pdbs)
+	return out, err
+}
+
+// SelectVictims is SelectNodesForPreemption over every listed node followed by the device's
+// pickOneNodeForPreemption (ties in Snapshot.List() order): the node and its victims, "" when no
+// node can make room.  For callers that keep no extenders (tools, tests).
 func (g *GpuEval) SelectVictims(ctx context.Context, pod *v1.Pod, pdbs []*policy.PodDisruptionBudget) (string, []*v1.Pod, error) {
 	list, err := g.h.SnapshotSharedLister().NodeInfos().List()
 	if err != nil {
 		return "", nil, err
 	}
+	out, chosen, err := g.selectOnDevice(pod, list, pdbs)
+	if err != nil || chosen == "" {
+		return "", nil, err
+	}
+	return chosen, out[chosen].Pods, nil
+}
+
+// selectOnDevice: one kgpu_select_victims call over the lower-priority pods of `nodes`.  Nodes outside
+// `nodes` get no potential victims, so they keep failing the filters they failed this cycle and are
+// never candidates.  Returns the candidates and the device's pick.
+func (g *GpuEval) selectOnDevice(pod *v1.Pod, nodes []*framework.NodeInfo,
+	pdbs []*policy.PodDisruptionBudget) (map[string]*extenderv1.Victims, string, error) {
+	list := nodes
 	var a arena
 	defer a.free()
 	p := &pools{}
 	q, err := g.comp.compilePod(pod, p)
 	if err != nil {
-		return "", nil, err
+		return nil, "", err
 	}
 	if sel := g.defaultSelector(pod); sel != nil {
 		if q.dpts, err = g.comp.labelSelector(p, sel); err != nil {
-			return "", nil, err
+			return nil, "", err
 		}
 	}
 	prio := podutil.GetPodPriority(pod)
@@ -120,12 +215,12 @@ func (g *GpuEval) SelectVictims(ctx context.Context, pod *v1.Pod, pdbs []*policy
 				// a pod the device mirror does not hold: its effects would be read from another
 				// pod's slot; resync before preempting
 				g.mir = nil
-				return "", nil, fmt.Errorf("gpueval: pod %s/%s is not in the device mirror (resynced; retry)",
+				return nil, "", fmt.Errorf("gpueval: pod %s/%s is not in the device mirror (resynced; retry)",
 					pi.Pod.Namespace, pi.Pod.Name)
 			}
 			r, err := g.comp.compilePod(pi.Pod, p)
 			if err != nil {
-				return "", nil, err
+				return nil, "", err
 			}
 			js := pdbsOf(pi.Pod, pdbs)
 			for _, j := range js {
@@ -143,7 +238,7 @@ func (g *GpuEval) SelectVictims(ctx context.Context, pod *v1.Pod, pdbs []*policy
 	}
 	sortInts(usedOrder)
 	if len(usedOrder) > 64 {
-		return "", nil, fmt.Errorf("gpueval: %d PodDisruptionBudgets select potential victims (the engine takes 64)", len(usedOrder))
+		return nil, "", fmt.Errorf("gpueval: %d PodDisruptionBudgets select potential victims (the engine takes 64)", len(usedOrder))
 	}
 	allowed := make([]int32, 0, len(usedOrder))
 	for k, j := range usedOrder {
@@ -159,15 +254,30 @@ func (g *GpuEval) SelectVictims(ctx context.Context, pod *v1.Pod, pdbs []*policy
 	}
 	cq := cQueries(&a, []C.kgpu_pod_query{q})
 	out, vout, chosen, err := g.eng.selectVictims(cq, p.toC(&a), victims, recs, allowed, len(g.mir.names))
-	if err != nil || chosen < 0 {
-		return "", nil, err
+	if err != nil {
+		return nil, "", err
 	}
-	o := out[chosen]
-	res := make([]*v1.Pod, 0, int(o.n_victims))
-	for k := 0; k < int(o.n_victims); k++ {
-		res = append(res, pods[vout[int(o.first)+k]])
+	res := map[string]*extenderv1.Victims{}
+	for _, ni := range list {
+		idx, ok := g.mir.index[ni.Node().Name]
+		if !ok || out[idx].fits == 0 {
+			continue
+		}
+		o := out[idx]
+		vs := make([]*v1.Pod, 0, int(o.n_victims))
+		for k := 0; k < int(o.n_victims); k++ {
+			vs = append(vs, pods[vout[int(o.first)+k]])
+		}
+		res[ni.Node().Name] = &extenderv1.Victims{Pods: vs, NumPDBViolations: int64(o.num_pdb_violations)}
+		// the scheduler nominates the pod to one of these before the status update reaches the
+		// informer: the next cycles ask the PodNominator about all of them (syncNominated)
+		g.track.nominate(ni.Node().Name)
 	}
-	return g.mir.names[chosen], res, nil
+	name := ""
+	if chosen >= 0 {
+		name = g.mir.names[chosen]
+	}
+	return res, name, nil
 }
 
 func sortInts(x []int) {
@@ -176,19 +286,4 @@ func sortInts(x []int) {
 			x[k], x[k-1] = x[k-1], x[k]
 		}
 	}
-}
-
-// PostFilter (interface.go:276-290): the device's preemption choice as the nominated node.  In
-// this reference version it runs after the in-tree Preempt (scheduler.go:543-562); victims are
-// deleted by the caller that owns the client (sched.podPreemptor), as Preempt's caller does.
-func (g *GpuEval) PostFilter(ctx context.Context, cs *framework.CycleState, pod *v1.Pod,
-	m framework.NodeToStatusMap) (*framework.PostFilterResult, *framework.Status) {
-	node, _, err := g.SelectVictims(ctx, pod, nil)
-	if err != nil {
-		return nil, framework.NewStatus(framework.Error, err.Error())
-	}
-	if node == "" {
-		return nil, framework.NewStatus(framework.Unschedulable)
-	}
-	return &framework.PostFilterResult{NominatedNodeName: node}, nil
 }

@@ -274,7 +274,7 @@ func (g *GpuEval) deltaFromSnapshot(list []*framework.NodeInfo, a *arena) (*C.kg
 	same := len(list) == len(m.names) && (len(list) == 0 || unsafe.Pointer(&list[0]) == m.listData)
 	var order []int32
 	if same {
-		if g.exact || g.syncs%fullEvery == 0 {
+		if g.exact || g.syncs%fullEvery == 0 || g.track.takeFull() {
 			for i, ni := range list {
 				if int32(i) != m.index[ni.Node().Name] || ni.Generation == m.genAt[i] {
 					continue // an alias position, or unchanged

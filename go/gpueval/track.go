@@ -14,11 +14,20 @@ package gpueval
 //     informers): a pod's old and new nodeName, a node's name.
 //
 // A marked node is re-checked at every sync until its NodeInfo.Generation moves (an event can reach
-// this handler before the cache applied it) or markTTL syncs passed.  Nothing can reach the cache
-// without passing through one of these sources except an assumed pod's expiry
-// (cache.cleanupAssumedPods, cache.go:704-737) and an event whose handler ran late, so every
-// fullEvery syncs the whole list's generations are compared as well (a tight loop over positions:
-// no map operations).  ExactSync in the plugin args compares every generation at every sync.
+// this handler before the cache applied it) or markTTL syncs passed.  A mark that expires without
+// its generation moving forces a full generation scan at the next sync: the cache may simply be
+// later than markTTL syncs in applying the event (informer listeners run on their own goroutines),
+// and the scan then finds the change whenever it lands.  Nothing can reach the cache without passing
+// through one of these sources except an assumed pod's expiry (cache.cleanupAssumedPods,
+// cache.go:704-737) and an event whose handler ran late, so every fullEvery syncs the whole list's
+// generations are compared as well (a tight loop over positions: no map operations).  ExactSync in
+// the plugin args compares every generation at every sync.
+//
+// Nominations.  The same pod events record every node named by an unassigned pod's
+// Status.NominatedNodeName, and SelectNodesForPreemption records its candidate nodes (the one the
+// scheduler nominates is among them, before the status update reaches the informer).  PreFilter asks
+// the PodNominator only about those nodes and the ones that held nominated pods at the last sync:
+// O(nominated) instead of NominatedPodsForNode on every listed node (preempt.go syncNominated).
 
 import (
 	"sync"
@@ -35,9 +44,11 @@ const (
 type tracker struct {
 	mu    sync.Mutex
 	marks map[string]int // node name -> syncs left
+	full  bool           // a mark expired unsettled: compare every generation at the next sync
+	noms  map[string]struct{}
 }
 
-func newTracker() *tracker { return &tracker{marks: map[string]int{}} }
+func newTracker() *tracker { return &tracker{marks: map[string]int{}, noms: map[string]struct{}{}} }
 
 func (t *tracker) mark(node string) {
 	if node == "" {
@@ -58,9 +69,41 @@ func (t *tracker) take() []string {
 		out = append(out, n)
 		if left <= 1 {
 			delete(t.marks, n)
+			t.full = true
 		} else {
 			t.marks[n] = left - 1
 		}
+	}
+	return out
+}
+
+// takeFull reports (and clears) a pending full scan.
+func (t *tracker) takeFull() bool {
+	t.mu.Lock()
+	defer t.mu.Unlock()
+	f := t.full
+	t.full = false
+	return f
+}
+
+// nominate records a node that may hold nominated pods.
+func (t *tracker) nominate(node string) {
+	if node == "" {
+		return
+	}
+	t.mu.Lock()
+	t.noms[node] = struct{}{}
+	t.mu.Unlock()
+}
+
+// nominations returns the recorded nodes and clears the record.
+func (t *tracker) nominations() []string {
+	t.mu.Lock()
+	defer t.mu.Unlock()
+	out := make([]string, 0, len(t.noms))
+	for n := range t.noms {
+		out = append(out, n)
+		delete(t.noms, n)
 	}
 	return out
 }
@@ -120,6 +163,9 @@ func (g *GpuEval) watch() {
 		for _, o := range objs {
 			if p := podOf(o); p != nil {
 				t.mark(p.Spec.NodeName)
+				if p.Spec.NodeName == "" {
+					t.nominate(p.Status.NominatedNodeName)
+				}
 			}
 		}
 	}
