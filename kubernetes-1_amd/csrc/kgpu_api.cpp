@@ -31,6 +31,7 @@
 #include <vector>
 
 #include "kgpu_internal.h"
+#include "kgpu_staging.h"
 
 // ---- RCCL, loaded on first use.  Only node sharding (kgpu_comm_unique_id / kgpu_comm_init) needs
 // it, so a one-GPU process never maps librccl: RCCL's own exit-time teardown then cannot run after a
@@ -183,19 +184,17 @@ struct kgpu_ctx {
   DevBuf batch_ptrs;             // unsharded persistent runs: {gran, feas} per run
   DevBuf flags_buf;                                // DevState::port_overflow
   DevBuf d_stage, d_remap, d_from;
-  void* stage_host = nullptr;                      // pinned staging block of a delta launch
+  kgpu::HostStage delta_stage;                     // pinned staging block of a delta launch
   void* cyc_host = nullptr;                        // pinned staging of a short cycle: DevState + queries
   void* res_pin = nullptr;                         // pinned coherent block the short cycle's kernels
   kgpu_result* res_dev = nullptr;                  // write their result records into (its device address)
   // short-cycle arena (arena_put): bump offset and capacity in cyc_host / dstate, the byte range
-  // still to be copied, and whether a copy from cyc_host may still be pending on the stream
-  size_t ar_used = 0, ar_cap = 0, ar_lo = 0, ar_hi = 0;
-  bool ar_on = false, ar_inflight = false;
+  // still to be copied, and whether a copy from cyc_host may still be pending (kgpu_staging.h)
+  kgpu::Arena ar;
   bool tb_abort_mapped = false;                    // the last k_tbatch run wrote its abort word to res_pin
   size_t ar_limit = 1 << 20;                       // KGPU_OPT_ARENA_BYTES (bytes of arena items per cycle)
   DevState ds_last{};                              // the DevState image last uploaded by a short cycle
   const void* ds_ptr = nullptr;                    // ... into this dstate allocation (null: none)
-  size_t stage_cap = 0;
   bool last_diag = false;
   std::vector<int64_t> trace_wg_host;             // k_tbatch per-workgroup stamps of the last traced run
   int32_t trace_wg_groups = 0;
@@ -210,7 +209,6 @@ struct kgpu_ctx {
   int classes_init = 0;          // classes whose mcnt column is initialized on the device
   int Ccap = 0, TCcap = 0;
   DevBuf d_classes, d_citems, d_tclasses, d_creqs, d_cints, d_plans, d_aux, d_aux_terms, scratch, d_pods;
-  std::vector<int32_t> tcnt_host_init;  // unused placeholder for symmetry
   // host mirror of the pod table (snapshot pods, then assumed pods in slot order)
   struct PodRow {
     int32_t node, ns;
@@ -230,11 +228,9 @@ struct kgpu_ctx {
   bool coop = true;                 // KGPU_OPT_COOPERATIVE
   int batch_geo_first = 0;          // KGPU_OPT_BATCH_GEO
   DevBuf t_tables, t_zero, abort_buf;
-  void* t_stage_host = nullptr;  // pinned staging of the runs' tables (bump-allocated, wraps after a sync)
+  kgpu::HostStage table_stage;   // pinned staging of the runs' tables (bump-allocated, wraps after a sync)
   DevBuf pool_blk;               // the call's query pools, packed (upload_pools)
-  void* pool_host = nullptr;     // ... and their pinned staging
-  size_t pool_host_cap = 0;
-  size_t t_stage_cap = 0, t_stage_used = 0;
+  kgpu::HostStage pool_stage;    // ... and their pinned staging
   // ---- node sharding (kgpu_comm_init): this context holds one contiguous slice of the
   // snapshot; per pod the shard winners (and normalize maxima) are all-gathered over RCCL
   ncclComm_t comm = nullptr;
@@ -353,23 +349,36 @@ constexpr size_t kCycHostBytes = kDsQueryOff + sizeof(kgpu_pod_query) * kShortCy
 constexpr size_t kCycResBytes = sizeof(kgpu_result) * kShortCycle;
 constexpr size_t kCycAbortOff = kCycResBytes;  // int32 in res_pin
 
-void arena_mark(kgpu_ctx* c, size_t lo, size_t hi) {
-  if (c->ar_hi <= c->ar_lo) {
-    c->ar_lo = lo;
-    c->ar_hi = hi;
-  } else {
-    c->ar_lo = std::min(c->ar_lo, lo);
-    c->ar_hi = std::max(c->ar_hi, hi);
-  }
+// The context's stream synchronize: every pending copy from the staging blocks has run
+// (kgpu_staging.h), so they may be rewritten, regrown or freed.
+int sync_stream(kgpu_ctx* c) {
+  HIP_OK(c, hipStreamSynchronize(c->stream));
+  c->pool_stage.synced();
+  c->table_stage.synced();
+  c->delta_stage.synced();
+  c->ar.synced();
+  return KGPU_OK;
 }
+#define SYNC_OK(c)                 \
+  do {                             \
+    const int rs_ = sync_stream(c); \
+    if (rs_) return rs_;           \
+  } while (0)
+
+int stage_sync(void* self) { return sync_stream(static_cast<kgpu_ctx*>(self)); }
+int stage_alloc(void* self, void** p, size_t bytes) {
+  kgpu_ctx* c = static_cast<kgpu_ctx*>(self);
+  fail_point();
+  HIP_OK(c, hipHostMalloc(p, bytes, hipHostMallocDefault));
+  return KGPU_OK;
+}
+void stage_release(void*, void* p) { (void)hipHostFree(p); }
+kgpu::StageOps stage_ops(kgpu_ctx* c) { return kgpu::StageOps{c, stage_sync, stage_alloc, stage_release}; }
 
 // `bytes` of the arena: host and device addresses (false: no arena, or full)
 bool arena_reserve(kgpu_ctx* c, size_t bytes, char** host, char** dev) {
-  if (!c->ar_on) return false;
-  const size_t o = c->ar_used, sz = (std::max<size_t>(bytes, 16) + 15) & ~(size_t)15;
-  if (o + sz > c->ar_cap) return false;
-  c->ar_used = o + sz;
-  arena_mark(c, o, o + bytes);
+  size_t o;
+  if (!c->ar.reserve(bytes, &o)) return false;
   *host = static_cast<char*>(c->cyc_host) + o;
   *dev = static_cast<char*>(c->dstate.p) + o;
   return true;
@@ -385,21 +394,16 @@ void* arena_put(kgpu_ctx* c, const void* src, size_t bytes) {
 }
 
 int arena_flush(kgpu_ctx* c) {
-  if (c->ar_hi > c->ar_lo) {
-    HIP_OK(c, hipMemcpyAsync(static_cast<char*>(c->dstate.p) + c->ar_lo, static_cast<char*>(c->cyc_host) + c->ar_lo,
-                             c->ar_hi - c->ar_lo, hipMemcpyHostToDevice, c->stream));
-    c->ar_inflight = true;
-  }
-  c->ar_lo = c->ar_hi = 0;
+  size_t lo, hi;
+  if (c->ar.take_dirty(&lo, &hi))
+    HIP_OK(c, hipMemcpyAsync(static_cast<char*>(c->dstate.p) + lo, static_cast<char*>(c->cyc_host) + lo, hi - lo,
+                             hipMemcpyHostToDevice, c->stream));
   return KGPU_OK;
 }
 
 struct ArenaScope {
   kgpu_ctx* c;
-  ~ArenaScope() {
-    c->ar_on = false;
-    c->ar_lo = c->ar_hi = 0;
-  }
+  ~ArenaScope() { c->ar.end(); }
 };
 
 template <class T>
@@ -448,16 +452,12 @@ int upload_pools(kgpu_ctx* c, const kgpu_pools* p) {
                o_pd = place(nb(p->n_pod_terms, sizeof(kgpu_pod_term))), o_sc = place(nb(p->n_scalars, sizeof(kgpu_scalar_req))),
                o_po = place(nb(p->n_ports, sizeof(kgpu_port)));
   const size_t total = off;
-  if (total > c->pool_host_cap) {
-    HIP_OK(c, hipStreamSynchronize(c->stream));
-    if (c->pool_host) (void)hipHostFree(c->pool_host);
-    c->pool_host = nullptr;
-    c->pool_host_cap = 0;
-    const size_t cap = std::max<size_t>(total * 2, 64 * 1024);
-    HIP_OK(c, hipHostMalloc(&c->pool_host, cap, hipHostMallocDefault));
-    c->pool_host_cap = cap;
-  }
-  char* h = static_cast<char*>(c->pool_host);
+  // the block is rewritten from offset 0: a copy from its previous contents still pending (a call
+  // that left before its synchronize) is waited for first (kgpu_staging.h)
+  char* h = nullptr;
+  int rc0;
+  const kgpu::StageOps ops = stage_ops(c);
+  if ((rc0 = c->pool_stage.rewrite(ops, total, 64 * 1024, &h))) return rc0;
   std::memset(h, 0, total);
   auto put = [&](size_t o, const void* src, size_t bytes) {
     if (src && bytes) std::memcpy(h + o, src, bytes);
@@ -482,6 +482,7 @@ int upload_pools(kgpu_ctx* c, const kgpu_pools* p) {
       d = static_cast<const char*>(a);
     } else {
       HIP_OK(c, hipMemcpyAsync(c->pool_blk.p, h, total, hipMemcpyHostToDevice, c->stream));
+      c->pool_stage.enqueued();
       c->pool_blk.shadow.assign(h, h + total);
       c->pool_blk.shadow_p = c->pool_blk.p;
     }
@@ -532,7 +533,7 @@ int sync_prefer_union(kgpu_ctx* c) {
   }
   std::vector<uint64_t> all(TW * (size_t)c->nranks);
   if (TW) HIP_OK(c, hipMemcpyAsync(all.data(), d + TW, sizeof(uint64_t) * all.size(), hipMemcpyDeviceToHost, c->stream));
-  HIP_OK(c, hipStreamSynchronize(c->stream));
+  SYNC_OK(c);
   c->prefer_global.assign(TW, 0ull);
   for (int r = 0; r < c->nranks; ++r)
     for (size_t w = 0; w < TW; ++w) c->prefer_global[w] |= all[(size_t)r * TW + w];
@@ -866,7 +867,7 @@ int grow_columns(kgpu_ctx* c, int32_t** tab, int* cap, int need) {
   HIP_OK(c, hipMalloc(&t, sizeof(int32_t) * N * nc));
   HIP_OK(c, hipMemsetAsync(t, 0, sizeof(int32_t) * N * nc, c->stream));
   if (*tab && *cap) HIP_OK(c, hipMemcpyAsync(t, *tab, sizeof(int32_t) * N * (*cap), hipMemcpyDeviceToDevice, c->stream));
-  HIP_OK(c, hipStreamSynchronize(c->stream));
+  SYNC_OK(c);
   if (*tab) (void)hipFree(*tab);
   *tab = t;
   *cap = nc;
@@ -892,7 +893,7 @@ int upload_pod_table(kgpu_ctx* c) {
   int rc;
   if ((rc = ensure(c, c->d_pods, sizeof(int32_t) * buf.size()))) return rc;
   HIP_OK(c, hipMemcpyAsync(c->d_pods.p, buf.data(), sizeof(int32_t) * buf.size(), hipMemcpyHostToDevice, c->stream));
-  HIP_OK(c, hipStreamSynchronize(c->stream));
+  SYNC_OK(c);
   int32_t* b = static_cast<int32_t*>(c->d_pods.p);
   c->st.pod_node = b;
   c->st.pod_ns = b + R;
@@ -942,7 +943,7 @@ int reserve_ports(kgpu_ctx* c, int64_t extra) {
   HIP_OK(c, hipMalloc(&np, sizeof(kgpu_port) * std::max<size_t>((size_t)ps * N, 1)));
   HIP_OK(c, hipMemsetAsync(np, 0, sizeof(kgpu_port) * (size_t)ps * N, c->stream));
   if (N) HIP_OK(c, hipMemcpyAsync(np, st.ports, sizeof(kgpu_port) * (size_t)st.PS * N, hipMemcpyDeviceToDevice, c->stream));
-  HIP_OK(c, hipStreamSynchronize(c->stream));
+  SYNC_OK(c);
   swap_alloc(c->snap_allocs, st.ports, np);
   st.ports = np;
   st.PS = ps;
@@ -1440,19 +1441,7 @@ int run_tbatch(kgpu_ctx* c, TRun& tr, int first, int count, int64_t first_seq, i
   char* th = nullptr;
   char* tdev = nullptr;
   const bool t_arena = arena_reserve(c, tbytes, &th, &tdev);
-  if (!t_arena && c->t_stage_used + tbytes > c->t_stage_cap) {
-    HIP_OK(c, hipStreamSynchronize(c->stream));
-    c->t_stage_used = 0;
-    if (tbytes > c->t_stage_cap) {
-      if (c->t_stage_host) (void)hipHostFree(c->t_stage_host);
-      c->t_stage_host = nullptr;
-      c->t_stage_cap = 0;
-      const size_t cap = std::max<size_t>(tbytes * 2, 1 << 20);
-      HIP_OK(c, hipHostMalloc(&c->t_stage_host, cap, hipHostMallocDefault));
-      c->t_stage_cap = cap;
-    }
-  }
-  if (!t_arena) th = static_cast<char*>(c->t_stage_host) + c->t_stage_used;
+  if (!t_arena && (rc = c->table_stage.reserve(stage_ops(c), tbytes, 1 << 20, &th))) return rc;
   auto stage = [&](size_t o, const auto& v) {
     if (!v.empty()) std::memcpy(th + o, v.data(), sizeof(v[0]) * v.size());
   };
@@ -1468,7 +1457,7 @@ int run_tbatch(kgpu_ctx* c, TRun& tr, int first, int count, int64_t first_seq, i
   if (!t_arena) {
     if ((rc = ensure(c, c->t_tables, tbytes))) return rc;
     HIP_OK(c, hipMemcpyAsync(c->t_tables.p, th, tbytes, hipMemcpyHostToDevice, c->stream));
-    c->t_stage_used += tbytes;
+    c->table_stage.enqueued();
     tdev = static_cast<char*>(c->t_tables.p);
   }
   const char* td = tdev;
@@ -1755,7 +1744,7 @@ int stage_topology(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_
       if (c->has_alias && (rc = copy_to_aliases(c, c->st.mcnt + (size_t)c->classes_init * c->st.N,
                                                 (int)c->classes.size() - c->classes_init)))
         return rc;
-      HIP_OK(c, hipStreamSynchronize(c->stream));
+      SYNC_OK(c);
       c->classes_init = (int)c->classes.size();
     }
     const kgpu::QPlan* dpl;
@@ -1818,12 +1807,9 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
     }
     // the previous cycle's arena copy may still read cyc_host when that cycle failed before its
     // stream synchronize
-    if (c->ar_inflight) HIP_OK(c, hipStreamSynchronize(c->stream));
-    c->ar_inflight = false;
-    c->ar_used = (kDsQueryOff + sizeof(kgpu_pod_query) * (size_t)n + 255) & ~(size_t)255;
-    c->ar_cap = std::min(kCycHostBytes, c->ar_used + c->ar_limit);
-    c->ar_on = c->ar_limit > 0;
-    c->ar_lo = c->ar_hi = 0;
+    if (c->ar.inflight) SYNC_OK(c);
+    const size_t first = (kDsQueryOff + sizeof(kgpu_pod_query) * (size_t)n + 255) & ~(size_t)255;
+    c->ar.begin(first, c->ar_limit > 0 ? std::min(kCycHostBytes, first + c->ar_limit) : 0);
   }
   c->tb_abort_mapped = false;
   Staged sg;
@@ -1891,10 +1877,10 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
     if (!inline_q) {
       std::memcpy(h, &c->st_batch, sizeof(DevState));
       std::memcpy(h + kDsQueryOff, qs, sizeof(kgpu_pod_query) * (size_t)n);
-      arena_mark(c, 0, kDsQueryOff + sizeof(kgpu_pod_query) * (size_t)n);
+      c->ar.mark(0, kDsQueryOff + sizeof(kgpu_pod_query) * (size_t)n);
     } else if (!ds_same) {
       std::memcpy(h, &c->st_batch, sizeof(DevState));
-      arena_mark(c, 0, sizeof(DevState));
+      c->ar.mark(0, sizeof(DevState));
     }
     c->ds_last = c->st_batch;
     c->ds_ptr = c->dstate.p;
@@ -1969,7 +1955,7 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
                        : -1;
   // A one-pod persistent topology run (kgpu_schedule_one of a topology pod) keeps its abort word in
   // the arena, and k_tbatch copies it into res_pin at exit: no memset, no read-back copy.
-  const bool tb_arena = short_cycle && n == 1 && topo[0] && tgeo >= 0 && !xg && c->ar_on;
+  const bool tb_arena = short_cycle && n == 1 && topo[0] && tgeo >= 0 && !xg && c->ar.on;
   // zeroed only when a persistent run can start (a one-launch-per-pod cycle never reads it)
   if (kidx >= 0 || (tgeo >= 0 && !tb_arena)) HIP_OK(c, hipMemsetAsync(c->abort_buf.p, 0, 64, c->stream));
   std::deque<TRun> runs;
@@ -2206,8 +2192,7 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
     HIP_OK(c, hipMemcpyAsync(&c->abort_host, abort_word, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
   int32_t port_overflow = 0;
   if (batch_ports) HIP_OK(c, hipMemcpyAsync(&port_overflow, c->st.port_overflow, 4, hipMemcpyDeviceToHost, c->stream));
-  HIP_OK(c, hipStreamSynchronize(c->stream));
-  c->ar_inflight = false;
+  SYNC_OK(c);
   if (short_cycle) std::memcpy(results, res_host, sizeof(kgpu_result) * (size_t)n);
   if (used_persistent && c->tb_abort_mapped) {
     // k_tbatch's last workgroup wrote the abort word (-1 left by the host: the run never finished)
@@ -2436,19 +2421,14 @@ int launch_ops(kgpu_ctx* c, const DeltaBuild& b, const kgpu_pod_query* pods, int
     total += (parts[i].bytes + 63) & ~(size_t)63;
   }
   const size_t need = total + 64;  // + the overflow readback word
-  if (c->stage_cap < need) {
-    if (c->stage_host) (void)hipHostFree(c->stage_host);
-    c->stage_host = nullptr;
-    c->stage_cap = 0;
-    HIP_OK(c, hipHostMalloc(&c->stage_host, need * 2, hipHostMallocDefault));
-    c->stage_cap = need * 2;
-  }
   int rc;
+  char* h = nullptr;
+  if ((rc = c->delta_stage.rewrite(stage_ops(c), need, 64 * 1024, &h))) return rc;
   if ((rc = ensure(c, c->d_stage, total))) return rc;
-  char* h = static_cast<char*>(c->stage_host);
   for (int i = 0; i < kParts; ++i)
     if (parts[i].bytes && parts[i].src) std::memcpy(h + off[i], parts[i].src, parts[i].bytes);
   HIP_OK(c, hipMemcpyAsync(c->d_stage.p, h, total, hipMemcpyHostToDevice, c->stream));
+  c->delta_stage.enqueued();
   char* d = static_cast<char*>(c->d_stage.p);
   kgpu::DeltaArgs a{};
   a.n_ops = (int32_t)ops.size();
@@ -2466,7 +2446,7 @@ int launch_ops(kgpu_ctx* c, const DeltaBuild& b, const kgpu_pod_query* pods, int
     return fail(c, KGPU_E_DEVICE, "k_delta launch failed");
   int32_t* ov = reinterpret_cast<int32_t*>(h + total);
   HIP_OK(c, hipMemcpyAsync(ov, c->st.port_overflow, 4, hipMemcpyDeviceToHost, c->stream));
-  HIP_OK(c, hipStreamSynchronize(c->stream));
+  SYNC_OK(c);
   if (*ov) return fail(c, KGPU_E_DEVICE, "a node's host-port slots ran out while applying deltas");
   return KGPU_OK;
 }
@@ -2579,7 +2559,7 @@ int reorder_nodes(kgpu_ctx* c, const kgpu_delta_batch* b) {
     return rc;
   if (kgpu::launch_remap(ddesc, (int)desc.size(), dfrom, oldN, newN, c->stream))
     return fail(c, KGPU_E_DEVICE, "k_remap launch failed");
-  HIP_OK(c, hipStreamSynchronize(c->stream));
+  SYNC_OK(c);
   for (size_t i = 0; i < cols.size(); ++i) {
     if (cols[i].registered) swap_alloc(c->snap_allocs, *cols[i].field, fresh[i]);
     else if (*cols[i].field) (void)hipFree(*cols[i].field);
@@ -3004,10 +2984,13 @@ int kgpu_destroy(kgpu_ctx* c) try {
   for (void* q : c->xg_open)
     if (q) (void)hipIpcCloseMemHandle(q);
   if (c->xg_box.p) (void)hipFree(c->xg_box.p);
-  if (c->stage_host) (void)hipHostFree(c->stage_host);
+  {
+    const kgpu::StageOps ops = stage_ops(c);
+    c->delta_stage.release(ops);
+    c->table_stage.release(ops);
+    c->pool_stage.release(ops);
+  }
   if (c->cyc_host) (void)hipHostFree(c->cyc_host);
-  if (c->t_stage_host) (void)hipHostFree(c->t_stage_host);
-  if (c->pool_host) (void)hipHostFree(c->pool_host);
   if (c->res_pin) (void)hipHostFree(c->res_pin);
   if (c->st.mcnt) (void)hipFree(c->st.mcnt);
   if (c->st.tcnt) (void)hipFree(c->st.tcnt);
@@ -3073,7 +3056,7 @@ int kgpu_upload_snapshot(kgpu_ctx* c, const kgpu_snapshot* s, int64_t generation
                          !s->unschedulable || !s->image_off || !s->avoid_off || !s->zone_id || !s->port_count))
     return fail(c, KGPU_E_INVAL, "missing node column");
   HIP_OK(c, hipSetDevice(c->device));
-  HIP_OK(c, hipStreamSynchronize(c->stream));
+  SYNC_OK(c);
   free_all(c->snap_allocs);
   free_all(c->work_allocs);
   fail_point();
@@ -3449,7 +3432,7 @@ int kgpu_select_victims(kgpu_ctx* c, const kgpu_pod_query* q, const kgpu_pools* 
   if (!ps.veff.empty())
     HIP_OK(c, hipMemcpyAsync(vout.data(), c->pa_host.out_victims, sizeof(int32_t) * ps.veff.size(),
                              hipMemcpyDeviceToHost, c->stream));
-  HIP_OK(c, hipStreamSynchronize(c->stream));
+  SYNC_OK(c);
   // sorted positions -> the caller's victim indices; pick the node
   std::vector<int32_t> prio(std::max<int32_t>(args->n_victims, 1));
   for (int32_t i = 0; i < args->n_victims; ++i) prio[(size_t)i] = args->pods[args->victims[i].item].priority;
@@ -3507,7 +3490,7 @@ static int debug_topo_scratch(kgpu_ctx* c, const kgpu_pod_query* q, const kgpu_p
     return fail(c, KGPU_E_DEVICE, "topology phase launch failed");
   sc.assign((size_t)pl.scratch_len, 0);
   HIP_OK(c, hipMemcpyAsync(sc.data(), c->st.scratch, sizeof(int64_t) * sc.size(), hipMemcpyDeviceToHost, c->stream));
-  HIP_OK(c, hipStreamSynchronize(c->stream));
+  SYNC_OK(c);
   return KGPU_OK;
 }
 
@@ -3629,7 +3612,7 @@ int kgpu_get_scores(kgpu_ctx* c, int32_t plugin, int64_t* raw, int64_t* normaliz
 int kgpu_read_nodes(kgpu_ctx* c, int64_t* req_cpu, int64_t* req_mem, int64_t* req_eph, int64_t* nz_cpu,
                     int64_t* nz_mem, int32_t* num_pods) try {
   if (!c || !c->uploaded) return KGPU_E_INVAL;
-  HIP_OK(c, hipStreamSynchronize(c->stream));
+  SYNC_OK(c);
   const size_t N = (size_t)c->st.N;
   if (req_cpu) HIP_OK(c, hipMemcpy(req_cpu, c->st.req_cpu, 8 * N, hipMemcpyDeviceToHost));
   if (req_mem) HIP_OK(c, hipMemcpy(req_mem, c->st.req_mem, 8 * N, hipMemcpyDeviceToHost));
@@ -3703,7 +3686,7 @@ int kgpu_apply_delta(kgpu_ctx* c, const kgpu_delta_batch* b, int64_t generation,
       (b->n_pods && !b->pods) || (b->n_rows && !b->rows) || (b->n_order && !b->order))
     return fail(c, KGPU_E_INVAL, "malformed delta batch");
   if (hipSetDevice(c->device) != hipSuccess) return KGPU_E_DEVICE;
-  HIP_OK(c, hipStreamSynchronize(c->stream));
+  SYNC_OK(c);
   int rc = apply_delta(c, b, slots);
   if (!rc && c->comm) rc = sync_prefer_union(c);  // every rank applies the same batch
   if (rc) {
@@ -3868,14 +3851,14 @@ int kgpu_comm_init(kgpu_ctx* c, int32_t nranks, int32_t rank, const uint8_t id[1
     uint8_t* d = static_cast<uint8_t*>(tmp.p);
     HIP_OK(c, hipMemcpy(d, mine.data(), 64, hipMemcpyHostToDevice));
     ncclResult_t nr = rccl().AllGather(d, d + 64, 64, ncclUint8, comm, c->stream);
-    if (nr == ncclSuccess) HIP_OK(c, hipStreamSynchronize(c->stream));
+    if (nr == ncclSuccess) SYNC_OK(c);
     if (nr == ncclSuccess) HIP_OK(c, hipMemcpy(all.data(), d + 64, 64 * (size_t)nranks, hipMemcpyDeviceToHost));
     if (nr != ncclSuccess) ok = 0;
     if (ok && kgpu_xgmi_init(c, nranks, rank, all.data()) != KGPU_OK) ok = 0;
     int32_t* flag = reinterpret_cast<int32_t*>(d + 64 + 64 * (size_t)nranks);
     HIP_OK(c, hipMemcpy(flag, &ok, sizeof(int32_t), hipMemcpyHostToDevice));
     nr = rccl().AllReduce(flag, flag, 1, ncclInt32, ncclMin, comm, c->stream);
-    if (nr == ncclSuccess) HIP_OK(c, hipStreamSynchronize(c->stream));
+    if (nr == ncclSuccess) SYNC_OK(c);
     int32_t all_ok = 0;
     if (nr == ncclSuccess) HIP_OK(c, hipMemcpy(&all_ok, flag, sizeof(int32_t), hipMemcpyDeviceToHost));
     (void)hipFree(tmp.p);

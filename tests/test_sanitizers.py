@@ -58,7 +58,9 @@ def test_c_restatement_under_asan_ubsan(tmp_path):
     san_lib = os.path.join(ROOT, "oracle", "build", "libkgpu_ref_san.so")
     plain_lib = os.path.join(ROOT, "oracle", "build", "libkgpu_ref.so")
     got_p, want_p = str(tmp_path / "san.npz"), str(tmp_path / "plain.npz")
-    san = _run(san_lib, got_p, {"LD_PRELOAD": asan,
+    # the ASan runtime goes first; whatever the environment already preloads stays preloaded after it
+    pre = " ".join(x for x in (asan, os.environ.get("LD_PRELOAD", "")) if x)
+    san = _run(san_lib, got_p, {"LD_PRELOAD": pre,
                                 "ASAN_OPTIONS": "detect_leaks=0:abort_on_error=1:halt_on_error=1",
                                 "UBSAN_OPTIONS": "halt_on_error=1:print_stacktrace=1"})
     assert san.returncode == 0 and "sanitized run ok" in san.stdout, (san.stdout[-2000:], san.stderr[-4000:])
