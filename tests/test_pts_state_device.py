@@ -18,6 +18,8 @@ the add must also equal the state of an engine uploaded with the pod already in 
 remove must restore the original state, as the reference test's two DeepEqual checks require
 (filtering_test.go:1990-2030).  TestPreFilterStateRemovePod's "delete a non-existing pod" row has
 no pod to remove from a cache: its state is the unchanged one, which is what the table expects."""
+import copy
+
 import numpy as np
 import pytest
 
@@ -29,6 +31,14 @@ from oracle.refsched.golog import go_log
 
 PTS = [c for c in load_golden("podtopologyspread") if c["kind"] == "pts_state" and "expect_state" in c]
 IPA = [c for c in load_golden("interpodaffinity") if c["kind"] == "ipa_state"]
+
+
+def _uid(pod):
+    """The cache keys pods by UID (framework.GetPodKey); the tables' pods have none: ns/name."""
+    p = copy.deepcopy(pod)
+    m = p.setdefault("metadata", {})
+    m.setdefault("uid", "%s/%s" % (m.get("namespace", "") or "", m.get("name", "")))
+    return p
 
 
 def _cluster(case):
@@ -82,14 +92,15 @@ def test_pts_state_on_device(case):
                    pts_default_constraints=a.get("default_constraints", []))
     if case["op"] in ("add", "remove"):
         hint = [case["pod"], case["op_pod"]]
-        cache = SchedulerCache(prof, case["nodes"], case.get("pods", []), cluster=_cluster(case), pods_hint=hint)
+        cache = SchedulerCache(prof, case["nodes"], [_uid(p) for p in case.get("pods", [])], cluster=_cluster(case),
+                               pods_hint=hint)
         try:
             if case["op"] == "add":
-                cache.add_pod(case["op_pod"])
+                cache.add_pod(_uid(case["op_pod"]))
             elif any(p["metadata"]["name"] == case["op_pod"]["metadata"]["name"] and
                      p["metadata"].get("namespace", "") == case["op_pod"]["metadata"].get("namespace", "")
                      for p in case.get("pods", [])):
-                cache.remove_pod(case["op_pod"])
+                cache.remove_pod(_uid(case["op_pod"]))
             cache.sync()
             assert cache.uploads == 1  # the change went through kgpu_apply_delta
             q, pc = _query(cache.compiler, case["pod"])
@@ -124,14 +135,15 @@ def _ipa_maps(engine, comp, pod):
 def test_ipa_state_on_device(case):
     prof = Profile(filters=["InterPodAffinity"], scores=[])
     hint = [case["pod"]] + ([case["op_pod"]] if case["op"] == "add_remove" else [])
-    cache = SchedulerCache(prof, case["nodes"], case.get("pods", []), cluster=_cluster(case), pods_hint=hint)
+    cache = SchedulerCache(prof, case["nodes"], [_uid(p) for p in case.get("pods", [])], cluster=_cluster(case),
+                           pods_hint=hint)
     try:
         before = _ipa_maps(cache.engine, cache.compiler, case["pod"])
         want = case["expect_ipa"]
         if case["op"] != "add_remove":
             assert before["aff"] == want["aff"] and before["anti"] == want["anti"], (case["name"], before)
             return
-        cache.add_pod(case["op_pod"])
+        cache.add_pod(_uid(case["op_pod"]))
         cache.sync()
         assert cache.uploads == 1  # the change went through kgpu_apply_delta
         after = _ipa_maps(cache.engine, cache.compiler, case["pod"])
@@ -141,7 +153,7 @@ def test_ipa_state_on_device(case):
                           pods_hint=hint)
         assert _ipa_maps(fw.engine, fw.compiler, case["pod"]) == after, case["name"]
         fw.engine.close()
-        cache.remove_pod(case["op_pod"])
+        cache.remove_pod(_uid(case["op_pod"]))
         cache.sync()
         assert _ipa_maps(cache.engine, cache.compiler, case["pod"]) == before, case["name"]
     finally:
