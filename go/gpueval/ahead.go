@@ -8,7 +8,7 @@ package gpueval
 // per PreFilter.  A PreFilter that finds no batch in flight schedules its pod TOGETHER WITH the pods
 // the queue will pop next -- the scheduler's unassigned pods from the shared informer, in the order of
 // the default QueueSort (queuesort/priority_sort.go:41-50: priority, then the time the pod entered the
-// queue, approximated here by its creation time) -- in one kgpu_schedule_batch with on-device assume.
+// queue, which track.go's queue clock follows) -- in one kgpu_schedule_batch with on-device assume.
 // Pod k of the batch is evaluated with pods 0..k-1 assumed on their chosen nodes: exactly the state
 // the per-pod cycle of pod k sees when nothing else happens in between.  The next PreFilters are
 // served from the batch while that holds:
@@ -17,7 +17,8 @@ package gpueval
 //     batch chose: that node's NodeInfo differs from the mirror by exactly that pod, which the device
 //     already holds -- the mirror takes it over and kgpu_adopt_pod registers its UID for the pod's
 //     slot (no ADD_POD is sent);
-//   * the tracker marked no other node (no other pod or node event);
+//   * every other node the tracker marked still has the NodeInfo the mirror holds (a bind
+//     confirmation, cache.AddPod of an assumed pod, marks the node without changing it);
 //   * the cycle's pod is the next batch pod.
 //
 // Any deviation forgets the unconsumed speculative assumes (kgpu_forget_pod, newest first) and the
@@ -84,13 +85,35 @@ func (g *GpuEval) pendingPods(self *v1.Pod, max int) []*v1.Pod {
 		}
 		out = append(out, p)
 	}
-	sort.SliceStable(out, func(i, j int) bool {
-		pi, pj := podPriority(out[i]), podPriority(out[j])
-		if pi != pj {
-			return pi > pj
+	at, bad := g.track.queueKeys(out)
+	type ranked struct {
+		p   *v1.Pod
+		pri int32
+		at  int64
+	}
+	rs := make([]ranked, 0, len(out))
+	for i, p := range out {
+		if !bad[i] { // waits in backoff / unschedulable: not popped next
+			rs = append(rs, ranked{p, podPriority(p), at[i]})
 		}
-		return out[i].CreationTimestamp.Before(&out[j].CreationTimestamp)
+	}
+	sort.SliceStable(rs, func(i, j int) bool {
+		a, b := rs[i], rs[j]
+		if a.pri != b.pri {
+			return a.pri > b.pri
+		}
+		if (a.at < 0) != (b.at < 0) { // a pod the clock has not seen yet entered the queue last
+			return a.at >= 0
+		}
+		if a.at != b.at {
+			return a.at < b.at
+		}
+		return a.p.CreationTimestamp.Before(&b.p.CreationTimestamp)
 	})
+	out = out[:0]
+	for _, r := range rs {
+		out = append(out, r.p)
+	}
 	if len(out) > max {
 		out = out[:max]
 	}
@@ -105,16 +128,23 @@ func (g *GpuEval) adoptPrevious(list []*framework.NodeInfo) (bool, error) {
 	e := ah.adopt
 	ah.adopt = nil
 	marked := g.track.peek() // deltaFromSnapshot consumes the marks
-	clean := true
+	m := g.mir
+	clean := len(list) == len(m.genAt)
 	for _, nm := range marked {
-		if e == nil || nm != e.host {
+		if e != nil && nm == e.host {
+			continue
+		}
+		// a mark whose NodeInfo did not move (its event changed nothing, or has not reached the
+		// cache: the snapshot this cycle sees is the mirror's either way) leaves the batch valid
+		pos, ok := m.index[nm]
+		if !clean || !ok || int(pos) >= len(list) || list[pos].Node() == nil ||
+			list[pos].Node().Name != nm || list[pos].Generation != m.genAt[pos] {
 			clean = false
 		}
 	}
 	if e == nil {
 		return clean, nil
 	}
-	m := g.mir
 	pos, ok := m.index[e.host]
 	if !ok || int(pos) >= len(list) {
 		ah.spec = append([]aheadEntry{*e}, ah.spec...)

@@ -164,6 +164,9 @@ type GpuEval struct {
 	track     *tracker // nodes whose NodeInfo may have moved since the last sync (track.go)
 	exact     bool     // compare every generation at every sync
 	syncs     int
+	// the pod of the last PreFilter, and whether it reached Reserve (track.go queue clock)
+	lastPod types.UID
+	lastRes bool
 }
 
 func (g *GpuEval) Name() string { return Name }
@@ -421,6 +424,11 @@ func (g *GpuEval) snapshotSoA(list []*framework.NodeInfo, m *mirror, a *arena) (
 // batch-ahead the cycle may be served from (or start) a batch of the pods the queue pops next.
 func (g *GpuEval) PreFilter(ctx context.Context, cs *framework.CycleState, pod *v1.Pod) *framework.Status {
 	seq := atomic.AddInt64(&g.seq, 1) - 1
+	if g.lastPod != "" && !g.lastRes {
+		g.track.requeue(g.lastPod) // that cycle failed before Reserve (scheduler.go:535-576 recordSchedulingFailure)
+	}
+	g.lastPod, g.lastRes = pod.UID, false
+	g.track.popped(pod.UID)
 	if g.ahead != nil {
 		res, ok, err := g.serveAhead(pod, seq)
 		if err != nil {
@@ -544,10 +552,14 @@ func (g *GpuEval) ScoreExtensions() framework.ScoreExtensions { return nil }
 // that diff looks at it (track.go).
 func (g *GpuEval) Reserve(ctx context.Context, cs *framework.CycleState, pod *v1.Pod, node string) *framework.Status {
 	g.track.mark(node)
+	if pod.UID == g.lastPod {
+		g.lastRes = true
+	}
 	return nil
 }
 func (g *GpuEval) Unreserve(ctx context.Context, cs *framework.CycleState, pod *v1.Pod, node string) {
 	g.track.mark(node)
+	g.track.requeue(pod.UID) // the error func re-queues it (scheduler.go recordSchedulingFailure)
 }
 
 // New is the framework.PluginFactory (registry.go:28).

@@ -28,11 +28,21 @@ package gpueval
 // scheduler nominates is among them, before the status update reaches the informer).  PreFilter asks
 // the PodNominator only about those nodes and the ones that held nominated pods at the last sync:
 // O(nominated) instead of NominatedPodsForNode on every listed node (preempt.go syncNominated).
+//
+// Queue clock (batch-ahead's prediction of the pods the queue pops next, ahead.go pendingPods).
+// PrioritySort orders by priority, then QueuedPodInfo.Timestamp: set when the pod enters the queue
+// (scheduling_queue.go:248 Add, :458 Update of a pod in no queue, both through newQueuedPodInfo
+// :632) and reset when a cycle fails (AddUnschedulableIfNotPresent, :306); updates and moves between
+// the sub-queues keep it (updatePod :657).  The same informer events stamp a logical tick on every
+// unassigned pod; a cycle that did not reach Reserve, or an Unreserve, re-stamps its pod and marks it
+// failed: a failed pod waits in the backoff or unschedulable queue, so it is left out of the
+// prediction until its next cycle starts.
 
 import (
 	"sync"
 
 	v1 "k8s.io/api/core/v1"
+	"k8s.io/apimachinery/pkg/types"
 	"k8s.io/client-go/tools/cache"
 )
 
@@ -46,9 +56,66 @@ type tracker struct {
 	marks map[string]int // node name -> syncs left
 	full  bool           // a mark expired unsettled: compare every generation at the next sync
 	noms  map[string]struct{}
+
+	tick   int64                  // queue clock
+	queued map[types.UID]int64    // unassigned pod -> tick it entered the queue (Timestamp)
+	failed map[types.UID]struct{} // its last cycle failed: in backoff / unschedulable
 }
 
-func newTracker() *tracker { return &tracker{marks: map[string]int{}, noms: map[string]struct{}{}} }
+func newTracker() *tracker {
+	return &tracker{marks: map[string]int{}, noms: map[string]struct{}{},
+		queued: map[types.UID]int64{}, failed: map[types.UID]struct{}{}}
+}
+
+// enqueue stamps a pod entering the queue; a pod already queued keeps its stamp (updatePod).
+func (t *tracker) enqueue(uid types.UID) {
+	t.mu.Lock()
+	if _, ok := t.queued[uid]; !ok {
+		t.queued[uid] = t.tick
+		t.tick++
+	}
+	t.mu.Unlock()
+}
+
+// dequeue forgets a pod that was bound or deleted.
+func (t *tracker) dequeue(uid types.UID) {
+	t.mu.Lock()
+	delete(t.queued, uid)
+	delete(t.failed, uid)
+	t.mu.Unlock()
+}
+
+// requeue: the pod's cycle failed (AddUnschedulableIfNotPresent re-stamps it).
+func (t *tracker) requeue(uid types.UID) {
+	t.mu.Lock()
+	t.queued[uid] = t.tick
+	t.tick++
+	t.failed[uid] = struct{}{}
+	t.mu.Unlock()
+}
+
+// popped: the pod's cycle starts, so it left whichever sub-queue held it.
+func (t *tracker) popped(uid types.UID) {
+	t.mu.Lock()
+	delete(t.failed, uid)
+	t.mu.Unlock()
+}
+
+// queueKeys returns each pod's stamp (-1: not seen yet) and whether it waits after a failed cycle.
+func (t *tracker) queueKeys(pods []*v1.Pod) ([]int64, []bool) {
+	t.mu.Lock()
+	defer t.mu.Unlock()
+	at := make([]int64, len(pods))
+	bad := make([]bool, len(pods))
+	for i, p := range pods {
+		at[i] = -1
+		if v, ok := t.queued[p.UID]; ok {
+			at[i] = v
+		}
+		_, bad[i] = t.failed[p.UID]
+	}
+	return at, bad
+}
 
 func (t *tracker) mark(node string) {
 	if node == "" {
@@ -169,10 +236,20 @@ func (g *GpuEval) watch() {
 			}
 		}
 	}
+	// the queue clock follows the last object of each event
+	onQueue := func(o interface{}, deleted bool) {
+		if p := podOf(o); p != nil {
+			if deleted || p.Spec.NodeName != "" {
+				t.dequeue(p.UID)
+			} else {
+				t.enqueue(p.UID)
+			}
+		}
+	}
 	f.Core().V1().Pods().Informer().AddEventHandler(cache.ResourceEventHandlerFuncs{
-		AddFunc:    func(o interface{}) { onPod(o) },
-		UpdateFunc: func(o, n interface{}) { onPod(o, n) },
-		DeleteFunc: func(o interface{}) { onPod(o) },
+		AddFunc:    func(o interface{}) { onPod(o); onQueue(o, false) },
+		UpdateFunc: func(o, n interface{}) { onPod(o, n); onQueue(n, false) },
+		DeleteFunc: func(o interface{}) { onPod(o); onQueue(o, true) },
 	})
 	onNode := func(objs ...interface{}) {
 		for _, o := range objs {

@@ -6,7 +6,8 @@ events.  One schedules every pod with its own cycle (SchedulerCache.schedule: Up
 kgpu_schedule_one); the other through BatchAhead (one kgpu_schedule_batch with on-device assume for
 the pods the queue pops next, then adoption of each assume).  The scheduler loop pops pods in queue
 order and assumes each placed pod on its host (cache.AssumePod).  Deviations the batch must survive
-exactly: an external pod added and a node updated mid-stream, a placed pod the scheduler does not
+exactly: an external pod added and a node updated mid-stream, bind confirmations of assumed pods
+arriving two cycles late (the cache's AddPod of an assumed pod changes nothing), a placed pod the scheduler does not
 assume (a failed Reserve / Permit), a pod that jumps the queue, a pod deleted from the queue, and a
 batch pod that turns out unschedulable.  After the stream, every node row of both devices must be
 equal, and equal to the C restatement's rows of the final cluster."""
@@ -49,6 +50,7 @@ def _run(name, batched, depth=64):
     hosts = []
     seq = 0
     step = 0
+    unconfirmed = []
     while queue:
         if step == 90:
             queue.insert(0, jumper)             # pops before the pods the batch predicted
@@ -65,6 +67,9 @@ def _run(name, batched, depth=64):
             placed = copy.deepcopy(pod)
             placed["spec"]["nodeName"] = host
             cache.assume_pod(placed)
+            unconfirmed.append(placed)
+        if len(unconfirmed) > 2:                # the informer confirms the bind of an older assume
+            cache.add_pod(unconfirmed.pop(0))   # (cache.go:466-481): no change, the batch survives
         if step == 150:                         # an external pod lands on a node
             ext = copy.deepcopy(pods[0])
             ext["metadata"].update(uid="ext", name="ext")
