@@ -568,7 +568,15 @@ int kgpu_read_nodes(kgpu_ctx* ctx, int64_t* req_cpu, int64_t* req_mem, int64_t* 
  * plans, a one-pod persistent topology run's tables and zeroed words); items beyond it take copies of
  * their own.  0 = no staging beyond DevState and queries.  Default and maximum 1 MiB. */
 #define KGPU_OPT_ARENA_BYTES 12
+/* KGPU_OPT_TOPO_RESIDENT (13): 1 (default) = a persistent topology run starts from the histograms,
+ * pair registrations and eligibility bitmaps the previous run with the same tables left on the device
+ * (it writes its final bins back) when nothing else changed the mirror in between, instead of
+ * recomputing them in an init pass over every node; 0 = always recompute. */
+#define KGPU_OPT_TOPO_RESIDENT 13
 int kgpu_set_option(kgpu_ctx* ctx, int32_t option, int64_t value);
+/* Diagnostics of KGPU_OPT_TOPO_RESIDENT: out[0] = persistent topology runs that started from the
+ * resident state, out[1] = runs that recomputed it. */
+int kgpu_debug_topo_resident(const kgpu_ctx* ctx, int64_t out[2]);
 /* Phase stamps of the last persistent run (100 MHz s_memrealtime ticks), 16 per pipeline
  * iteration (pods + 1): workgroup 0's {start, evaluated, previous pod resolved, published, end, 0,
  * 0, 0}, then the last workgroup's.  Returns the number of iterations written (<= max_iters). */

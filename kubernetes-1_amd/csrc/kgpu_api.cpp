@@ -192,6 +192,19 @@ struct kgpu_ctx {
   // still to be copied, and whether a copy from cyc_host may still be pending (kgpu_staging.h)
   kgpu::Arena ar;
   bool tb_abort_mapped = false;                    // the last k_tbatch run wrote its abort word to res_pin
+  // Resident topology run state (TCache): the histograms, pair registrations, signature flags and
+  // eligibility bitmaps of the last persistent topology run, as that run left them (k_tbatch writes
+  // its final bins back).  The next run with the same tables starts from them instead of a
+  // k_tbatch_init pass -- valid only while nothing else changed the mirror since: every other
+  // writer of node state (upload, deltas, forget, the other evaluation paths' assumes, sharding)
+  // drops it.
+  struct TCache {
+    bool valid = false;
+    std::string key;     // the run's hists, signature programs, registrations and geometry
+    DevBuf buf;          // hist_init | tot_init | reg_init | sig_any | elig
+  } tc;
+  uint64_t tc_hits = 0, tc_misses = 0;
+  bool tc_on = true;                               // KGPU_OPT_TOPO_RESIDENT
   size_t ar_limit = 1 << 20;                       // KGPU_OPT_ARENA_BYTES (bytes of arena items per cycle)
   DevState ds_last{};                              // the DevState image last uploaded by a short cycle
   const void* ds_ptr = nullptr;                    // ... into this dstate allocation (null: none)
@@ -1421,6 +1434,28 @@ int run_tbatch(kgpu_ctx* c, TRun& tr, int first, int count, int64_t first_seq, i
   const size_t N = (size_t)c->st.N;
   const size_t ew = (N + 31) / 32;
   for (size_t s = 0; s < tr.sigs.size(); ++s) tr.sigs[s].elig_word = (int32_t)(s * ew);
+  // TCache: the init state of a run with these tables, left by the last run (unsharded engines; a
+  // node-sharded run sums every rank's partial instead)
+  const bool use_tc = !xg && c->tc_on;
+  std::string tkey;
+  if (use_tc) {
+    auto put = [&](const void* p, size_t n) { tkey.append(static_cast<const char*>(p), n); };
+    const int64_t geo[6] = {c->st.N, c->st.node_base, tr.lds_bins, tr.reg_words, (int64_t)tr.hists.size(),
+                            (int64_t)tr.regs.size()};
+    put(geo, sizeof(geo));
+    put(tr.hists.data(), sizeof(kgpu::THist) * tr.hists.size());
+    put(tr.regs.data(), sizeof(kgpu::TReg) * tr.regs.size());
+    // signatures by content (their programs; `rep` is only where the kernel reads the program)
+    std::vector<const std::vector<int64_t>*> progs(tr.sigs.size(), nullptr);
+    for (const auto& kv : tr.sig_ids) progs[(size_t)kv.second] = &kv.first;
+    for (const auto* pv : progs) {
+      const int64_t len = pv ? (int64_t)pv->size() : -1;
+      put(&len, sizeof(len));
+      if (pv) put(pv->data(), sizeof(int64_t) * pv->size());
+    }
+  }
+  const bool tc_hit = use_tc && c->tc.valid && c->tc.key == tkey;
+  c->tc.valid = false;  // until this run is launched
   // Every table of the run in one pinned block and ONE copy: a copy from pageable memory costs
   // microseconds each, and nine of them dominated a one-pod (kgpu_schedule_one) run.  The pinned
   // block is bump-allocated per run; it wraps only after a stream synchronize, so no staged bytes are
@@ -1484,7 +1519,15 @@ int run_tbatch(kgpu_ctx* c, TRun& tr, int first, int count, int64_t first_seq, i
   const size_t b_reg = a16((size_t)std::max(tr.reg_words, 1) * 4), b_sany = a16(std::max<size_t>(tr.sigs.size(), 1) * 4);
   const size_t b_elig = a16(std::max<size_t>(tr.sigs.size() * ew, 1) * 4);
   const size_t b_gran = (size_t)count * (size_t)(a.R + 1) * (size_t)groups * 8;
-  const size_t total = b_hist + b_tot + b_reg + b_sany + b_elig + b_gran;
+  const size_t b_init = b_hist + b_tot + b_reg + b_sany + b_elig;
+  char* zinit = nullptr;  // the init region in TCache's buffer (use_tc), else in the zeroed region
+  if (use_tc) {
+    if ((rc = ensure(c, c->tc.buf, b_init))) return rc;
+    zinit = static_cast<char*>(c->tc.buf.p);
+    if (!tc_hit) HIP_OK(c, hipMemsetAsync(zinit, 0, b_init, c->stream));
+    ++(tc_hit ? c->tc_hits : c->tc_misses);
+  }
+  const size_t total = (use_tc ? 0 : b_init) + b_gran;
   // abort_word null: a one-pod run of a short cycle -- its own abort word and workgroup counter after
   // the zeroed region, and the abort word copied to res_pin by the kernel (run_batch reads it there)
   const bool own_abort = abort_word == nullptr;
@@ -1499,12 +1542,14 @@ int run_tbatch(kgpu_ctx* c, TRun& tr, int first, int count, int64_t first_seq, i
       abort_word = static_cast<int32_t*>(c->abort_buf.p);
     }
   }
-  a.hist_init = reinterpret_cast<int32_t*>(z);
-  a.tot_init = reinterpret_cast<int32_t*>(z + b_hist);
-  a.reg_init = reinterpret_cast<uint32_t*>(z + b_hist + b_tot);
-  a.sig_any = reinterpret_cast<int32_t*>(z + b_hist + b_tot + b_reg);
-  a.elig = reinterpret_cast<uint32_t*>(z + b_hist + b_tot + b_reg + b_sany);
-  a.gran = reinterpret_cast<uint64_t*>(z + b_hist + b_tot + b_reg + b_sany + b_elig);
+  char* zi = use_tc ? zinit : z;
+  a.hist_init = reinterpret_cast<int32_t*>(zi);
+  a.tot_init = reinterpret_cast<int32_t*>(zi + b_hist);
+  a.reg_init = reinterpret_cast<uint32_t*>(zi + b_hist + b_tot);
+  a.sig_any = reinterpret_cast<int32_t*>(zi + b_hist + b_tot + b_reg);
+  a.elig = reinterpret_cast<uint32_t*>(zi + b_hist + b_tot + b_reg + b_sany);
+  a.gran = reinterpret_cast<uint64_t*>(use_tc ? z : z + b_init);
+  a.writeback = use_tc ? 1 : 0;
   if (c->tb_abort_mapped) {
     abort_word = reinterpret_cast<int32_t*>(z + total);
     a.done = abort_word + 1;
@@ -1528,7 +1573,7 @@ int run_tbatch(kgpu_ctx* c, TRun& tr, int first, int count, int64_t first_seq, i
   }
   if ((rc = arena_flush(c))) return rc;  // the short cycle's one copy: DevState, queries, pools, tables, zeros
   const DevState* dst = static_cast<const DevState*>(c->dstate.p);
-  if (kgpu::launch_tbatch_init(dst, a, groups, c->stream))
+  if (!tc_hit && kgpu::launch_tbatch_init(dst, a, groups, c->stream))
     return fail(c, KGPU_E_DEVICE, "k_tbatch_init launch failed");
   if (xg) {
     // node-sharded run: cluster-wide histograms from every rank's partial, then the
@@ -1553,6 +1598,10 @@ int run_tbatch(kgpu_ctx* c, TRun& tr, int first, int count, int64_t first_seq, i
   }
   if (kgpu::launch_tbatch(dst, a, groups, geo, c->spec, xg, c->coop, c->stream))
     return fail(c, KGPU_E_DEVICE, std::string("k_tbatch launch failed: ") + hipGetErrorString(hipGetLastError()));
+  if (use_tc) {
+    c->tc.valid = true;  // what this run leaves behind (an aborted run invalidates the mirror)
+    c->tc.key.swap(tkey);
+  }
   if (a.trace) {
     HIP_OK(c, hipMemcpyAsync(c->trace_host.data(), a.trace, sizeof(int64_t) * 16 * (size_t)(count + 1),
                              hipMemcpyDeviceToHost, c->stream));
@@ -1733,6 +1782,7 @@ int stage_topology(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_
     c->st.cints = dcint;
     if (c->classes_init < (int)c->classes.size()) {
       // fresh mcnt columns: counted on the device over the pod table (snapshot + assumed pods)
+      c->tc.valid = false;
       if (c->pod_rows_dev != (int)c->pod_rows.size() && (rc = upload_pod_table(c))) return rc;
       if ((rc = ensure(c, c->dstate, sizeof(DevState)))) return rc;
       c->st_batch = c->st;
@@ -1840,7 +1890,7 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
   st.results = short_cycle ? c->res_dev : static_cast<kgpu_result*>(c->results.p);
   // Per-plugin scores of a diagnostic cycle: every pod of a batch without topology pods goes
   // through k_eval, which then zeroes each node's rows itself; a one-pod persistent topology run's
-  // k_tbatch_init does too; otherwise one memset does, issued before the first launch that needs it.
+  // k_tbatch does too; otherwise one memset does, issued before the first launch that needs it.
   const bool zero_diag = diag && !topo_on && c->comm == nullptr;
   bool diag_zeroed = !diag || zero_diag;
   if (!diag) {
@@ -1974,7 +2024,7 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
         if ((rc = run_tbatch(c, tr, i, j - i, first_seq, assume, tper, tgroups, tgeo, tb_arena ? nullptr : abort_word, xg,
                              diag)))
           return rc;
-        if (diag) diag_zeroed = true;  // k_tbatch_init zeroed the rows (a diagnostic run is one pod)
+        if (diag) diag_zeroed = true;  // k_tbatch zeroed the rows (a diagnostic run is one pod)
         if (c->timing) HIP_OK(c, hipEventRecord(get_event(c, ev + 1), c->stream));
         ev += 2;
         timed_passes += j - i;
@@ -1984,6 +2034,7 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
       }
     }
     if ((rc = arena_flush(c))) return rc;  // every other launch reads DevState / queries / pools from it
+    c->tc.valid = false;                     // ... and may assume outside a persistent topology run
     if (topo[(size_t)i]) {
       if ((rc = zero_diag_rows())) return rc;
       const kgpu::QPlan& pl = plans[(size_t)i];
@@ -2387,6 +2438,7 @@ int launch_ops(kgpu_ctx* c, const DeltaBuild& b, const kgpu_pod_query* pods, int
                int n_rows, const int32_t* ints, int n_ints, const uint64_t* words, int n_words,
                const kgpu_scalar_req* scalars, int n_scalars, const kgpu_port* ports, int n_ports) {
   if (b.ops.empty()) return KGPU_OK;
+  c->tc.valid = false;  // node state changes outside a persistent topology run
   // group the ops by node (stable: batch order within a node), one workgroup per group
   std::vector<int32_t> idx(b.ops.size());
   for (size_t i = 0; i < idx.size(); ++i) idx[i] = (int32_t)i;
@@ -3017,6 +3069,13 @@ int kgpu_read_phase_trace(kgpu_ctx* c, int64_t* out, int32_t max_pods) try {
   return on_exception(c, false);
 }
 
+int kgpu_debug_topo_resident(const kgpu_ctx* c, int64_t out[2]) {
+  if (!c || !out) return KGPU_E_INVAL;
+  out[0] = (int64_t)c->tc_hits;
+  out[1] = (int64_t)c->tc_misses;
+  return KGPU_OK;
+}
+
 int kgpu_debug_wg_trace(kgpu_ctx* c, int64_t* out, int64_t max_words, int32_t* groups) try {
   if (!c || !out || !groups || max_words < 0) return KGPU_E_INVAL;
   const size_t n = std::min<size_t>((size_t)max_words, c->trace_wg_host.size());
@@ -3037,7 +3096,10 @@ int kgpu_set_option(kgpu_ctx* c, int32_t option, int64_t value) try {
   else if (option == KGPU_OPT_TOPO_PERSISTENT) c->tfast = value != 0;
   else if (option == KGPU_OPT_COOPERATIVE) c->coop = value != 0;
   else if (option == KGPU_OPT_BATCH_GEO) c->batch_geo_first = (int)std::max<int64_t>(0, value);
-  else if (option == KGPU_OPT_ARENA_BYTES) c->ar_limit = (size_t)std::min<int64_t>(std::max<int64_t>(0, value), (int64_t)kArenaBytes);
+  else if (option == KGPU_OPT_TOPO_RESIDENT) {
+    c->tc_on = value != 0;
+    c->tc.valid = false;
+  } else if (option == KGPU_OPT_ARENA_BYTES) c->ar_limit = (size_t)std::min<int64_t>(std::max<int64_t>(0, value), (int64_t)kArenaBytes);
   else if (option == KGPU_OPT_ABORT_AT) c->abort_at = value < 0 || value > INT32_MAX ? -1 : (int32_t)value;
   else if (option == KGPU_OPT_XGMI) c->xgmi = value != 0;
   else if (option == KGPU_OPT_SKIP_RELEASE_AT) c->skip_release_at = value < 0 || value > INT32_MAX ? -1 : (int32_t)value;
@@ -3049,6 +3111,7 @@ int kgpu_set_option(kgpu_ctx* c, int32_t option, int64_t value) try {
 
 int kgpu_upload_snapshot(kgpu_ctx* c, const kgpu_snapshot* s, int64_t generation) try {
   if (!c || !s) return KGPU_E_INVAL;
+  c->tc.valid = false;
   if (s->n_nodes < 0 || s->n_label_keys < 0 || s->n_scalar < 0 || s->taint_words < 0 || s->port_slots < 0)
     return fail(c, KGPU_E_INVAL, "negative snapshot dimension");
   if (s->n_nodes > 0 && (!s->alloc_cpu || !s->alloc_mem || !s->alloc_eph || !s->alloc_pods || !s->req_cpu ||
@@ -3748,6 +3811,7 @@ int kgpu_xgmi_handle(kgpu_ctx* c, int32_t nranks, uint8_t handle[64]) try {
 
 int kgpu_xgmi_init(kgpu_ctx* c, int32_t nranks, int32_t rank, const uint8_t* handles) try {
   if (!c || !handles || nranks < 2 || nranks > kgpu::kMaxRanks || rank < 0 || rank >= nranks) return KGPU_E_INVAL;
+  c->tc.valid = false;
   if (hipSetDevice(c->device) != hipSuccess) return KGPU_E_DEVICE;
   if (!c->xg_box.p || c->xg_GT != nranks * c->xg_groups)
     return fail(c, KGPU_E_STATE, "kgpu_xgmi_handle(nranks) must precede kgpu_xgmi_init");
@@ -3812,6 +3876,7 @@ int kgpu_comm_unique_id(uint8_t id[128]) try {
 
 int kgpu_comm_init(kgpu_ctx* c, int32_t nranks, int32_t rank, const uint8_t id[128]) try {
   if (!c || !id) return KGPU_E_INVAL;
+  c->tc.valid = false;
   if (nranks < 1 || nranks > kgpu::kMaxRanks || rank < 0 || rank >= nranks)
     return fail(c, KGPU_E_INVAL, "nranks must be in [1, 64] and 0 <= rank < nranks");
   if (c->comm) return fail(c, KGPU_E_STATE, "communicator already initialized");

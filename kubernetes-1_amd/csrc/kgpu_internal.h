@@ -396,7 +396,10 @@ struct TBatchArgs {
   int32_t lab_keys;       // node label keys cached in LDS per workgroup ([lab_keys][per] value ids)
   int32_t abort_at;       // KGPU_OPT_ABORT_AT test hook (-1: never), as in BatchArgs
   int32_t diag;           // kgpu_schedule_one: status word and per-plugin raw / normalized scores of every
-                          // node (the run is one pod; the host zeroed the diagnostic rows)
+                          // node (the run is one pod; every lane zeroes its nodes' diagnostic rows first)
+  int32_t writeback;      // workgroup 0 stores its final histogram bins and totals back into hist_init /
+                          // tot_init: the next run with the same tables starts from them without a
+                          // k_tbatch_init pass (kgpu_api.cpp TCache)
   int64_t* trace;        // null, or [count + 1][16] s_memrealtime stamps (KGPU_OPT_PHASE_TRACE): per pod
                           // and traced workgroup (0, last): start, PreFilter minima, rows evaluated,
                           // stats published, stats resolved, key published, winner resolved, end

@@ -2471,13 +2471,6 @@ __global__ void k_tbatch_init(const DevState* __restrict__ stp, TBatchArgs ta) {
       if (x) atomicAdd(b < ta.lds_bins ? gp(ta.hist_init) + b : gp(ta.tot_init) + (b - ta.lds_bins), x);
     }
   }
-  if (ta.diag && on) {
-    // a diagnostic (kgpu_schedule_one) run: this node's per-plugin raw / normalized rows start at 0
-    for (int sc = 0; sc < KGPU_NUM_SCORES; ++sc) {
-      gp(st.diag_raw)[(size_t)sc * st.N + n] = 0;
-      gp(st.diag_norm)[(size_t)sc * st.N + n] = 0;
-    }
-  }
 }
 
 // 63-bit order-preserving payloads of the statistics granules
@@ -2838,6 +2831,10 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int G = gridDim.x, g = blockIdx.x;
   const int lo = g * ta.per;
+  // run stamps (KGPU_OPT_PHASE_TRACE) in the trace's spare last row: entry, pod loop start, exit
+  const bool trun = ta.trace && tid == 0 && (g == 0 || g == G - 1);
+  int64_t* trun_row = ta.trace ? ta.trace + (size_t)ta.count * 16 + (g == 0 ? 0 : 8) : nullptr;
+  if (trun) trun_row[0] = (int64_t)__builtin_amdgcn_s_memrealtime();
 
   // LDS replicas and the workgroup's label values: eight independent loads in flight per thread
   // and round (a one-pod run pays this start-up in full; a strided loop would wait for each load)
@@ -2882,6 +2879,14 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
     r[j] = NodeRes{};
     sr[j] = TStatic{{0, 0}, {0, 0}, 0, -1};
     if (n < st.N) {
+      if (ta.diag) {
+        // a diagnostic (kgpu_schedule_one) run: this node's per-plugin raw / normalized rows start at
+        // 0 (this lane's later stores of them follow in program order)
+        for (int sc = 0; sc < KGPU_NUM_SCORES; ++sc) {
+          gp(st.diag_raw)[(size_t)sc * st.N + n] = 0;
+          gp(st.diag_norm)[(size_t)sc * st.N + n] = 0;
+        }
+      }
       r[j] = load_res(st, n);
       if constexpr (kDef) set_recips(r[j]);
       sr[j].unsched = gp(st.unsched)[n];
@@ -2902,6 +2907,7 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
   if (trc) trow[(size_t)i * 16 + (k)] = (int64_t)__builtin_amdgcn_s_memrealtime()
 #define KGPU_WSTAMP(k) \
   if (ta.trace_wg && tid == 0) ta.trace_wg[((size_t)i * G + g) * 8 + (k)] = (int64_t)__builtin_amdgcn_s_memrealtime()
+  if (trun) trun_row[1] = (int64_t)__builtin_amdgcn_s_memrealtime();
   for (int i = 0; i < ta.count; ++i) {
     KGPU_TSTAMP(0);
     KGPU_WSTAMP(0);
@@ -3327,6 +3333,14 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
   }
 #undef KGPU_TSTAMP
 #undef KGPU_WSTAMP
+  // The run's final histograms for the next run with the same tables (TCache): every workgroup loaded
+  // hist_init before it published pod 0's statistics, which workgroup 0 waited for, so nobody reads
+  // these words any more.  An aborted run leaves them (the host invalidates the mirror).
+  if (ta.writeback && g == 0 && !M.abort) {
+    for (int b = tid; b < ta.lds_bins; b += B) gp(ta.hist_init)[b] = H[b];
+    for (int h = tid; h < ta.n_hists; h += B) gp(ta.tot_init)[h] = TOT[h];
+  }
+  if (trun) trun_row[2] = (int64_t)__builtin_amdgcn_s_memrealtime();
   // every workgroup gets here, aborted or not (the pod loop only breaks): the last one to leave
   // copies the run's abort word into the caller's pinned block
   if (ta.abort_out && tid == 0) {

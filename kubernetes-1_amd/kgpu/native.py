@@ -22,7 +22,7 @@ EXPORTS = ["kgpu_abi_version", "kgpu_struct_sizes", "kgpu_create", "kgpu_destroy
            "kgpu_set_nominated", "kgpu_select_victims", "kgpu_xgmi_handle", "kgpu_xgmi_init", "kgpu_xgmi_active",
            "kgpu_comm_info",
            "kgpu_debug_fail_alloc", "kgpu_debug_pts_state", "kgpu_debug_ipa_state", "kgpu_debug_broken_linear",
-           "kgpu_debug_wg_trace",
+           "kgpu_debug_wg_trace", "kgpu_debug_topo_resident",
            "kgpu_next_slot", "kgpu_adopt_pod"]
 
 
@@ -70,6 +70,7 @@ def lib():
     L.kgpu_debug_ipa_state.argtypes = [vp, vp, C.POINTER(abi.Pools), i32, i32, vp, vp, vp, C.POINTER(i32)]
     L.kgpu_debug_broken_linear.argtypes = [vp, vp, i32, vp, i32, vp]
     L.kgpu_debug_wg_trace.argtypes = [vp, vp, i64, C.POINTER(i32)]
+    L.kgpu_debug_topo_resident.argtypes = [vp, vp]
     L.kgpu_next_slot.argtypes = [vp]
     L.kgpu_adopt_pod.argtypes = [vp, i32, i64]
     L.kgpu_select_victims.argtypes = [vp, vp, C.POINTER(abi.Pools), C.POINTER(abi.PreemptArgs), vp, vp,
@@ -255,6 +256,13 @@ class Engine:
         out = np.zeros(max(pods * g.value * 8, 1), np.int64)
         n = lib().kgpu_debug_wg_trace(self.h, out.ctypes.data, len(out), C.byref(g))
         return out[:n].reshape(-1, g.value, 8) if g.value else out[:0].reshape(0, 0, 8)
+
+    def topo_resident(self):
+        """kgpu_debug_topo_resident: (runs that started from the resident topology state, runs that
+        recomputed it)."""
+        out = np.zeros(2, np.int64)
+        self._check(lib().kgpu_debug_topo_resident(self.h, out.ctypes.data))
+        return int(out[0]), int(out[1])
 
     def broken_linear(self, points, utilizations):
         """kgpu_debug_broken_linear: the device's broken-linear shape function (the one

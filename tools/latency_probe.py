@@ -1,4 +1,4 @@
-"""Per-call latency of kgpu_schedule_one (the drop-in plugin's per-cycle call) on config (b).
+"""Per-call latency of kgpu_schedule_one (the drop-in plugin's per-cycle call) on configs (b), (c), (d).
 
 Run under `rocprofv3 --hip-trace --kernel-trace --stats` to see where a call's time goes
 (API calls, copies, launches, synchronisation)."""
@@ -23,8 +23,10 @@ def main():
     from kgpu.framework import GpuFramework
     if args.config == "b":
         nodes, existing, pods, prof = cluster.fit_least_balanced(n_nodes=args.nodes, n_pods=args.pods)
-    else:
+    elif args.config == "c":
         nodes, existing, pods, prof = cluster.taints_affinity_spread(n_nodes=args.nodes, n_pods=args.pods)
+    else:
+        nodes, existing, pods, prof = cluster.pod_affinity(n_nodes=args.nodes, n_existing=args.nodes, n_pods=args.pods)
     fw = GpuFramework(prof, nodes, existing, pods_hint=pods[:16])
     q, pc, _, errs = fw.compile_pods(pods)
     assert not errs
