@@ -573,6 +573,10 @@ int kgpu_read_nodes(kgpu_ctx* ctx, int64_t* req_cpu, int64_t* req_mem, int64_t* 
  * (it writes its final bins back) when nothing else changed the mirror in between, instead of
  * recomputing them in an init pass over every node; 0 = always recompute. */
 #define KGPU_OPT_TOPO_RESIDENT 13
+/* KGPU_OPT_BATCH_HELPER (14): 1 (default) = the persistent batch kernel of the NodeResourcesFit +
+ * BalancedAllocation + LeastAllocated profile on its one-row-wave geometry runs a helper wave that
+ * evaluates LeastAllocated and the tie-break ranks beside the row wave; 0 = the row wave alone. */
+#define KGPU_OPT_BATCH_HELPER 14
 int kgpu_set_option(kgpu_ctx* ctx, int32_t option, int64_t value);
 /* Diagnostics of KGPU_OPT_TOPO_RESIDENT: out[0] = persistent topology runs that started from the
  * resident state, out[1] = runs that recomputed it. */

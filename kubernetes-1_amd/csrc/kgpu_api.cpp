@@ -205,6 +205,7 @@ struct kgpu_ctx {
   } tc;
   uint64_t tc_hits = 0, tc_misses = 0;
   bool tc_on = true;                               // KGPU_OPT_TOPO_RESIDENT
+  bool batch_helper = true;                        // KGPU_OPT_BATCH_HELPER
   size_t ar_limit = 1 << 20;                       // KGPU_OPT_ARENA_BYTES (bytes of arena items per cycle)
   DevState ds_last{};                              // the DevState image last uploaded by a short cycle
   const void* ds_ptr = nullptr;                    // ... into this dstate allocation (null: none)
@@ -2171,7 +2172,7 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
         c->trace_host.assign((size_t)(cnt + 1) * 16, 0);
       }
       if (c->timing) HIP_OK(c, hipEventRecord(get_event(c, ev), c->stream));
-      if (kgpu::launch_batch(dst, ba, groups, kidx, c->spec, c->coop, c->stream))
+      if (kgpu::launch_batch(dst, ba, groups, kidx, c->spec, c->coop, c->batch_helper, c->stream))
         return fail(c, KGPU_E_DEVICE, "k_batch launch failed");
       if (c->timing) HIP_OK(c, hipEventRecord(get_event(c, ev + 1), c->stream));
       ev += 2;
@@ -3096,6 +3097,7 @@ int kgpu_set_option(kgpu_ctx* c, int32_t option, int64_t value) try {
   else if (option == KGPU_OPT_TOPO_PERSISTENT) c->tfast = value != 0;
   else if (option == KGPU_OPT_COOPERATIVE) c->coop = value != 0;
   else if (option == KGPU_OPT_BATCH_GEO) c->batch_geo_first = (int)std::max<int64_t>(0, value);
+  else if (option == KGPU_OPT_BATCH_HELPER) c->batch_helper = value != 0;
   else if (option == KGPU_OPT_TOPO_RESIDENT) {
     c->tc_on = value != 0;
     c->tc.valid = false;

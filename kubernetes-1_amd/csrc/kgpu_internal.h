@@ -506,7 +506,9 @@ int launch_shard_pack(const DevState* st, int parity, int blocks, int what, void
 // variant-B spare), -1 when N does not fit in max_groups workgroups.
 // first: the smallest geometry index considered (KGPU_OPT_BATCH_GEO; 0 = all)
 int batch_geometry(int N, int max_groups, int* per, int* groups, int first = 0);
-int launch_batch(const DevState* st, const BatchArgs& a, int groups, int kidx, int spec, bool coop, void* stream);
+// helper: config (b)'s profile on the one-row-wave geometry takes the helper-wave instantiation (HB)
+int launch_batch(const DevState* st, const BatchArgs& a, int groups, int kidx, int spec, bool coop, bool helper,
+                 void* stream);
 // Topology pipeline for one pod (PodArgs.pod): domain histograms, critical-path minima, filters,
 // scores, normalize + argmax, resolve + assume.  next_scratch: words of the next topology pod's
 // scratch to zero in the resolve launch (0 none).

@@ -649,40 +649,34 @@ __device__ __forceinline__ uint32_t wave_max32u(uint32_t x) {
   x = max(x, dpp32<0x143, 0xC>(x));
   return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
 }
+// Unsigned 64-bit wave max in two 32-bit passes: the high words' max, then the low words' max over
+// the lanes holding it.  A 32-bit DPP step is one max with a DPP operand; a 64-bit one is two DPP
+// moves, a 64-bit compare and two selects.
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t x) {
+  const uint32_t mh = wave_max32u((uint32_t)(x >> 32));
+  const uint32_t ml = wave_max32u((uint32_t)(x >> 32) == mh ? (uint32_t)x : 0u);
+  return ((uint64_t)mh << 32) | ml;
+}
 // signed 64-bit max / min through the order-preserving unsigned map
 __device__ __forceinline__ int64_t wave_max_i64(int64_t x) {
-  return (int64_t)(wave_red64((uint64_t)x ^ (1ull << 63), OpMaxU64{}) ^ (1ull << 63));
+  return (int64_t)(wave_max_u64((uint64_t)x ^ (1ull << 63)) ^ (1ull << 63));
 }
 __device__ __forceinline__ int64_t wave_min_i64(int64_t x) {
-  return (int64_t)(~wave_red64(~((uint64_t)x ^ (1ull << 63)), OpMaxU64{}) ^ (1ull << 63));
+  return (int64_t)(~wave_max_u64(~((uint64_t)x ^ (1ull << 63))) ^ (1ull << 63));
 }
 __device__ __forceinline__ int64_t wave_sum_i64(int64_t x) { return (int64_t)wave_red64((uint64_t)x, OpSumU64{}); }
 struct OpOrU64 {
   __device__ __forceinline__ uint64_t operator()(uint64_t a, uint64_t b) const { return a | b; }
 };
-// two independent unsigned max reductions in lockstep
+// two independent unsigned max reductions (the compiler interleaves the two pass chains)
 __device__ __forceinline__ void wave_red64x2(uint64_t& x, uint64_t& y) {
-#define KGPU_STEP2(C, R)              \
-  {                                   \
-    const uint64_t tx = dpp64<C, R>(x); \
-    const uint64_t ty = dpp64<C, R>(y); \
-    x = x > tx ? x : tx;              \
-    y = y > ty ? y : ty;              \
-  }
-  KGPU_STEP2(0xB1, 0xF)
-  KGPU_STEP2(0x4E, 0xF)
-  KGPU_STEP2(0x141, 0xF)
-  KGPU_STEP2(0x140, 0xF)
-  KGPU_STEP2(0x142, 0xA)
-  KGPU_STEP2(0x143, 0xC)
-#undef KGPU_STEP2
-  x = readlane64(x, 63);
-  y = readlane64(y, 63);
+  x = wave_max_u64(x);
+  y = wave_max_u64(y);
 }
 
 // argmax of unique keys: the maximum, then the one lane holding it
 __device__ __forceinline__ void wave_argmax(uint64_t& k, int& i) {
-  const uint64_t m = wave_red64(k, OpMaxU64{});
+  const uint64_t m = wave_max_u64(k);
   const uint64_t b = __ballot(k == m && m != 0);
   i = b ? __builtin_amdgcn_readlane(i, (int)__builtin_ctzll(b)) : -1;
   k = m;
@@ -1404,11 +1398,24 @@ __device__ __forceinline__ bool poll_row(const uint64_t* row, int G, const int32
   }
 }
 
+// HB (config (b)'s profile, one row wave): a helper wave beside the row wave evaluates the rows'
+// NodeResourcesLeastAllocated scores and tie-break ranks of each pod while the row wave evaluates
+// NodeResourcesFit and BalancedAllocation -- two instruction streams on two SIMDs instead of one
+// (the evaluation is issue-bound: DESIGN.md 4.3) -- and hands over ((least + 1) << 40) | rank40 per
+// row through LDS; the row wave's key adds balanced << 40 (the key's score field is the sum).
+struct HRow {
+  int64_t ac, am, zc, zm;
+  double ic, im;
+};
+
 // XG: the node-sharded instantiation (xGMI mailbox rings); the unsharded one carries none of its code.
-template <uint32_t FM, uint32_t SM, int K, int B, bool XG>
-__global__ __launch_bounds__(B + 64) void k_batch(const DevState* __restrict__ stp, BatchArgs pa) {
+template <uint32_t FM, uint32_t SM, int K, int B, bool XG, bool HB = false>
+__global__ __launch_bounds__(B + 64 + (HB ? B : 0)) void k_batch(const DevState* __restrict__ stp, BatchArgs pa) {
+  static_assert(!HB || (B == 64 && !XG &&
+                       SM == ((1u << KGPU_S_BALANCED_ALLOCATION) | (1u << KGPU_S_LEAST_ALLOCATED) | kDefRes)),
+                "the helper wave splits config (b)'s profile on the one-row-wave geometry");
   const DevState& st = *stp;
-  constexpr int W = B / 64;  // row waves; wave W communicates
+  constexpr int W = B / 64;  // row waves; wave W communicates; HB: wave W + 1 helps row wave 0
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int G = gridDim.x, g = blockIdx.x;
   const int lo = g * pa.per;
@@ -1416,6 +1423,8 @@ __global__ __launch_bounds__(B + 64) void k_batch(const DevState* __restrict__ s
   constexpr bool xg = XG;                       // xGMI mailbox ring (node-sharded run)
   const uint64_t tmask = xg ? (0xFull << 60) : kGValid;
   __shared__ BatchShared<B> sh;
+  __shared__ uint64_t sh_hk[HB ? 2 * K * B : 1];  // HB: [pod parity][slot][lane] helper's key part
+  __shared__ int sh_hready;                       // HB: i + 1 once pod i's helper parts are in sh_hk
   __shared__ uint64_t* sh_peer_g[XG ? kMaxRanks : 1];
   __shared__ int32_t* sh_peer_f[XG ? kMaxRanks : 1];
   if constexpr (XG) {
@@ -1427,6 +1436,7 @@ __global__ __launch_bounds__(B + 64) void k_batch(const DevState* __restrict__ s
   if (tid == 0) {
     sh.bready = 0;
     sh.cready = 0;
+    sh_hready = 0;
   }
   __syncthreads();
   auto ring_row = [&](int k) -> size_t { return xg ? (size_t)((pa.xseq0 + k) % pa.R) : (size_t)k; };
@@ -1456,6 +1466,100 @@ __global__ __launch_bounds__(B + 64) void k_batch(const DevState* __restrict__ s
 #define KGPU_STAMP(i, k) \
   if (tr && (tid == 0 || tid == B)) trow[(size_t)(i) * 16 + (k)] = (int64_t)__builtin_amdgcn_s_memrealtime()
 
+  if constexpr (HB) {
+    if (wave == W + 1) {
+      // ---- helper wave: Least + rank40 of every row of the row wave (same lanes, same nodes) and of
+      // its spare lane's variant-B row; it follows the candidate and the winner as the
+      // communication wave does, so its copies of the rows take the same assumes
+      HRow h[K];
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        const int n = lo + j * B + lane;
+        h[j] = HRow{0, 0, 0, 0, 0.0, 0.0};
+        if (!spare_slot(j, K, lane, B) && n < st.N) {
+          h[j].ac = gp(st.alloc_cpu)[n];
+          h[j].am = gp(st.alloc_mem)[n];
+          h[j].zc = gp(st.nz_cpu)[n];
+          h[j].zm = gp(st.nz_mem)[n];
+          h[j].ic = (h[j].ac > 0 && h[j].ac < (1ll << 52)) ? 1.0 / (double)h[j].ac : 0.0;
+          h[j].im = (h[j].am > 0 && h[j].am < (1ll << 52)) ? 1.0 / (double)h[j].am : 0.0;
+        }
+      }
+      __builtin_amdgcn_s_waitcnt(0);
+      const int64_t wl = st.w_of[KGPU_S_LEAST_ALLOCATED];
+      int cand = -1;
+      bool staged = false;
+      for (int i = 0; i <= pa.count; ++i) {
+        const bool have_prev = i > 0, have_cur = i < pa.count;
+        const int p = i & 1;
+        const kgpu_pod_query* qc = st.queries + pa.first + i;       // pod i (have_cur)
+        const kgpu_pod_query* qpp = st.queries + pa.first + i - 1;  // pod i-1 (have_prev)
+        const bool qmem = have_prev && (cp(qpp)->scalars.count | cp(qpp)->ports.count) != 0;
+        const bool fast_b = have_prev && cand >= 0 && staged && pa.assume && !qmem;
+        const int ob = cand >= 0 ? cand % B : -1, jb = cand >= 0 ? cand / B : -1;
+        if (have_cur) {
+          const uint64_t tk = pod_tie_key(st.seed, pa.seq0 + i);
+          if (fast_b) {
+            // the candidate row for pod i-1 with pod i-1 applied (assume_regs), in the spare lane
+            HRow t{};
+#pragma unroll
+            for (int j = 0; j < K; ++j)
+              if (j == jb) {
+                t.ac = lane64(h[j].ac, ob);
+                t.am = lane64(h[j].am, ob);
+                t.zc = lane64(h[j].zc, ob) + cp(qpp)->nz[0];
+                t.zm = lane64(h[j].zm, ob) + cp(qpp)->nz[1];
+                t.ic = __builtin_bit_cast(double, lane64(__builtin_bit_cast(int64_t, h[j].ic), ob));
+                t.im = __builtin_bit_cast(double, lane64(__builtin_bit_cast(int64_t, h[j].im), ob));
+              }
+            if (lane == B - 1) h[K - 1] = t;
+          }
+          kgpu_pod_query qh;
+          qh.score_req[0] = cp(qc)->score_req[0];
+          qh.score_req[1] = cp(qc)->score_req[1];
+#pragma unroll
+          for (int j = 0; j < K; ++j) {
+            const bool spare = spare_slot(j, K, lane, B);
+            const int n = spare ? lo + cand : lo + j * B + lane;
+            NodeRes nr{};
+            nr.ac = h[j].ac; nr.am = h[j].am; nr.zc = h[j].zc; nr.zm = h[j].zm; nr.ic = h[j].ic; nr.im = h[j].im;
+            const int64_t lv = least_score<true>(st, qh, nr, n) * wl;
+            sh_hk[(p * K + j) * B + lane] = ((uint64_t)(lv + 1) << 40) | rank40(tk, (uint64_t)(st.node_base + n), st.tie_mode);
+          }
+          if (lane == 0) lds_release(&sh_hready, i + 1);
+        }
+        __syncthreads();  // (c)
+        int wg = -1;
+        if (have_prev) {
+          if (sh.rabort[(i - 1) & 1]) break;
+          wg = sh.rwg[(i - 1) & 1];
+        }
+        const bool won = have_prev && wg == gme;
+        if (won && pa.assume && lane == ob) {
+#pragma unroll
+          for (int j = 0; j < K; ++j)
+            if (j == jb) {
+              h[j].zc += cp(qpp)->nz[0];
+              h[j].zm += cp(qpp)->nz[1];
+            }
+        }
+        const bool slow = have_cur && won && pa.assume && !fast_b;
+        int cn = -1;
+        if (have_cur && !slow) {
+          const Cand c = wg_combine<B>(sh, p, won && fast_b);
+          cn = c.key ? c.idx : -1;
+        }
+        if (slow) {
+          lds_wait(&sh.cready, i + 1, pa.abort);
+          cand = sh.cslow[p];
+        } else {
+          cand = cn;
+        }
+        staged = have_cur && !slow && cand >= 0;
+      }
+      return;
+    }
+  }
   if (wave == W) {
     // ---- communication wave: resolve pod i-1 while the row waves evaluate pod i, then combine
     //      their partials and publish pod i (variant B when this workgroup won pod i-1), and write
@@ -1590,11 +1694,32 @@ __global__ __launch_bounds__(B + 64) void k_batch(const DevState* __restrict__ s
         assume_regs(qp, t);
         if (tid == B - 1) r[K - 1] = t;
       }
+      if constexpr (HB) {
+        // Fit and BalancedAllocation here; Least and the rank from the helper wave
+        uint32_t fs[K];
+        bool any = false;
 #pragma unroll
-      for (int j = 0; j < K; ++j) {
-        const bool spare = spare_slot(j, K, tid, B);
-        const int n = spare ? lo + cand : lo + j * B + tid;
-        keys[j] = (spare ? fast_b : n < st.N) ? node_key<FM, SM>(st, q, r[j], n, tk) : 0;
+        for (int j = 0; j < K; ++j) {
+          const bool spare = spare_slot(j, K, tid, B);
+          const int n = spare ? lo + cand : lo + j * B + tid;
+          fs[j] = (spare ? fast_b : n < st.N) ? run_filters<FM>(st, q, r[j], n) : 1u;
+          any |= fs[j] == 0;
+        }
+        if (q.scalars.count | q.ports.count) vm_drain();
+        int64_t bw[K];
+        const bool wave_any = __ballot(any) != 0;
+#pragma unroll
+        for (int j = 0; j < K; ++j) bw[j] = wave_any ? balanced_score(q, r[j]) * st.w_of[KGPU_S_BALANCED_ALLOCATION] : 0;
+        lds_wait_ge(&sh_hready, i + 1, pa.abort);
+#pragma unroll
+        for (int j = 0; j < K; ++j) keys[j] = fs[j] ? 0 : sh_hk[(p * K + j) * B + tid] + ((uint64_t)bw[j] << 40);
+      } else {
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+          const bool spare = spare_slot(j, K, tid, B);
+          const int n = spare ? lo + cand : lo + j * B + tid;
+          keys[j] = (spare ? fast_b : n < st.N) ? node_key<FM, SM>(st, q, r[j], n, tk) : 0;
+        }
       }
       KGPU_STAMP(i, 5);
       wg_partials<K, B>(sh, p, keys, fast_b, ob, jb, cand, own_a, own_b);
@@ -2812,6 +2937,141 @@ __device__ __forceinline__ uint32_t trow_eval(const DevState& st, const TBatchAr
   return 0;
 }
 
+// trow_eval in two parts, for the pods of a run after its first (not diagnostic: only feasibility and
+// the raw scores matter, not the first failing filter's position).
+//  * trow_ind: every filter and score outside PodTopologySpread / InterPodAffinity (and DPTS).  These
+//    read the node's register row and node-static columns only, so k_tbatch evaluates them for pod
+//    i+1 while pod i's exchanges are in flight; pod i's assume changes them on one row (its winner),
+//    which is evaluated again -- on a copy of the candidate row with pod i applied -- before the key
+//    round ends.  False when a filter fails.
+//  * trow_topo: the topology filters and raw topology scores, after pod i's histogram deltas.
+template <uint32_t FM, uint32_t SM, bool kDef>
+__device__ __forceinline__ bool trow_ind(const DevState& st, const TBatchArgs& ta, const kgpu_pod_query& q,
+                                         const TPlan& tp, const NodeRes& r, int n, const TStatic& sr, TRow& o) {
+  auto one = [&](int f) -> bool {
+    if (f == KGPU_F_POD_TOPOLOGY_SPREAD || f == KGPU_F_INTER_POD_AFFINITY) return true;
+    if (f == KGPU_F_NODE_AFFINITY) return tb_elig(ta, tp.aff_sig, n);
+    if (f == KGPU_F_NODE_UNSCHEDULABLE) return !(sr.unsched && !(q.flags & KGPU_Q_TOLERATES_UNSCHEDULABLE));
+    if (f == KGPU_F_TAINT_TOLERATION && st.TW <= 2) {
+#pragma unroll
+      for (int w = 0; w < 2; ++w) {
+        if (w >= st.TW) break;
+        const uint64_t tol = w < q.tol_nosched.count ? cp(st.qp.words)[q.tol_nosched.begin + w] : 0ull;
+        if (sr.tns[w] & ~tol) return false;
+      }
+      return true;
+    }
+    return filter_one(f, st, q, r, n) == 0;
+  };
+  bool ok = true;
+  if constexpr (FM == kRuntime) {
+    for (int fi = 0; fi < st.n_filters && ok; ++fi) ok = one(cp(st.filters)[fi]);
+  } else {
+#pragma unroll
+    for (int f = 0; f < KGPU_NUM_FILTERS; ++f) {
+      if (!((FM >> f) & 1u)) continue;
+      if (ok) ok = one(f);
+    }
+  }
+  if (!ok) return false;
+  NodeEval e{0, 0, 0, 0};
+  tscores<SM, kDef>(st, q, r, n, e, st.TW <= 2, false);
+  if (st.TW <= 2 && st.w_of[KGPU_S_TAINT_TOLERATION] && st.any_prefer_taint) {  // taint_toleration.go:123-152
+#pragma unroll
+    for (int w = 0; w < 2; ++w) {
+      if (w >= st.TW) break;
+      const uint64_t tol = w < q.tol_prefer.count ? cp(st.qp.words)[q.tol_prefer.begin + w] : 0ull;
+      e.taint += __popcll(sr.tpr[w] & ~tol);
+    }
+  }
+  o.part = e.partial;
+  o.taint = e.taint;
+  o.na = e.na;
+  return true;
+}
+
+// The topology half: PodTopologySpread and InterPodAffinity Filter (podtopologyspread/filtering.go:276-328,
+// interpodaffinity/filtering.go:314-396), then the raw topology scores as in trow_eval.  False when a
+// filter fails.
+template <uint32_t FM>
+__device__ __forceinline__ bool trow_topo(const DevState& st, const TBatchArgs& ta, const TPlan& tp, int n,
+                                          const int32_t* H, const int64_t* PT, const TMisc& M, bool pany,
+                                          bool aff_any, const int32_t* LAB, int li, TRow& o) {
+  auto nval = [&](int key) -> int {
+    if (key < 0) return -1;
+    return key < ta.lab_keys ? LAB[key * ta.per + li] : gp(st.label_val)[(size_t)key * st.N + n];
+  };
+  bool has_pts = ((FM >> KGPU_F_POD_TOPOLOGY_SPREAD) & 1u) != 0, has_ipa = ((FM >> KGPU_F_INTER_POD_AFFINITY) & 1u) != 0;
+  if constexpr (FM == kRuntime) {
+    has_pts = has_ipa = false;
+    for (int fi = 0; fi < st.n_filters; ++fi) {
+      has_pts |= st.filters[fi] == KGPU_F_POD_TOPOLOGY_SPREAD;
+      has_ipa |= st.filters[fi] == KGPU_F_INTER_POD_AFFINITY;
+    }
+  }
+  if (has_pts && pany) {
+    for (int c = 0; c < tp.n_hard; ++c) {
+      const THard hc = tp.hard[c];
+      const int v = nval(hc.key);
+      if (v < 0) return false;
+      if (PT[hc.pt_off + v] + hc.self_match - M.pmin[hc.tab] > hc.max_skew) return false;
+    }
+  }
+  if (has_ipa) {
+    bool exist = true;
+    for (int a = 0; a < tp.n_aff; ++a) {
+      const TLook t = tp.aff[a];
+      const int v = nval(t.key);
+      if (v < 0) return false;
+      if (tval(st, H, t, v, n) <= 0) exist = false;
+    }
+    if (!exist && !(!aff_any && tp.self_all)) return false;
+    for (int a = 0; a < tp.n_anti; ++a) {
+      const TLook t = tp.anti[a];
+      const int v = nval(t.key);
+      if (v >= 0 && tval(st, H, t, v, n) > 0) return false;
+    }
+    for (int k = 0; k < tp.n_exa_tabs; ++k) {
+      const TTab tb = cp(ta.tabs)[tp.tabs.begin + tp.tabs.count - tp.n_exa_tabs + k];
+      const int v = nval(tb.key);
+      if (v >= 0 && PT[tb.off + v] > 0) return false;
+    }
+    for (int e = 0; e < tp.exa_u.count; ++e) {
+      const TLook t = cp(ta.looks)[tp.exa_u.begin + e];
+      if (nval(t.key) >= 0 && tcol(st, t, n) > 0) return false;
+    }
+  }
+  o.adj = 0;
+  if (tp.n_soft) {
+    const int v = nval(tp.soft_key);
+    if (v < 0) {
+      o.adj = INT64_MIN;
+    } else {
+      int64_t cnt;
+      if (tp.soft_mode == 0) cnt = H[tp.soft_off + v];
+      else if (tp.soft_mode == 1) cnt = gp(st.mcnt)[(size_t)tp.soft_col * st.N + n];
+      else cnt = tb_elig(ta, tp.soft_sig, n) ? gp(st.mcnt)[(size_t)tp.soft_col * st.N + n] : 0;
+      o.adj = cnt < tp.soft_max_skew ? tp.soft_max_skew - 1 : cnt;  // adjustForMaxSkew
+    }
+  }
+  int64_t is = 0;
+  if (tp.need_ipa) {
+    for (int k = 0; k < tp.tabs.count - tp.n_exa_tabs; ++k) {
+      const TTab tb = cp(ta.tabs)[tp.tabs.begin + k];
+      if (tb.kind != 2) continue;
+      const int v = nval(tb.key);
+      if (v >= 0) is += PT[tb.off + v];
+    }
+    for (int e2 = 0; e2 < tp.score_u.count; ++e2) {
+      const TLook t = cp(ta.looks)[tp.score_u.begin + e2];
+      if (nval(t.key) >= 0) is += (int64_t)t.weight * tcol(st, t, n);
+    }
+  }
+  o.ipa = is;
+  o.ds = tp.dpts_cls >= 0 ? gp(st.mcnt)[(size_t)tp.dpts_cls * st.N + n] : 0;
+  return true;
+}
+
 template <int B, int K, uint32_t FM, uint32_t SM, bool kDef, bool XG>
 __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, TBatchArgs ta) {
   const DevState& st = *stp;
@@ -2907,18 +3167,25 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
   if (trc) trow[(size_t)i * 16 + (k)] = (int64_t)__builtin_amdgcn_s_memrealtime()
 #define KGPU_WSTAMP(k) \
   if (ta.trace_wg && tid == 0) ta.trace_wg[((size_t)i * G + g) * 8 + (k)] = (int64_t)__builtin_amdgcn_s_memrealtime()
+  // Evaluation ahead (one row per lane): the next pod's non-topology filters and scores (trow_ind) run
+  // while this pod's statistics round is in flight; the candidate lane evaluates them again on its row
+  // with this pod applied while the key round is in flight, for the case its workgroup wins.
+  constexpr bool kAhead = K == 1;
+  bool ind_have = false;                     // (uniform) ind_* hold this pod's trow_ind of the lane's row
+  bool ind_next = false;                     // (uniform) ... and nx_* the next pod's
+  bool ind_ok = false, nx_ok = false, vb_ok = false;
+  TRow ind_o{}, nx_o{}, vb_o{};              // part / taint / na only
   if (trun) trun_row[1] = (int64_t)__builtin_amdgcn_s_memrealtime();
   for (int i = 0; i < ta.count; ++i) {
     KGPU_TSTAMP(0);
     KGPU_WSTAMP(0);
     if (i == ta.abort_at && g == 0 && tid == 0) __hip_atomic_store(ta.abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int pod = ta.first + i;
-    if (wave == W - 1 && i + 1 < ta.count && lane < (int)(sizeof(kgpu_pod_query) / 16)) {
-      // warm the next pod's query record (its first touch would otherwise put a memory round
-      // trip at the head of the next pod)
-      const uint4 x = reinterpret_cast<const GAS uint4*>(gp(st.queries + pod + 1))[lane];
-      asm volatile("" ::"v"(x.x));
-    }
+    // warm the next pod's query record (its first touch would otherwise put a memory round trip at
+    // the head of the next pod); the load is consumed at the end of this pod, so nothing waits for it
+    uint4 qwarm{};
+    if (wave == W - 1 && i + 1 < ta.count && lane < (int)(sizeof(kgpu_pod_query) / 16))
+      qwarm = reinterpret_cast<const GAS uint4*>(gp(st.queries + pod + 1))[lane];
     const kgpu_pod_query& q = *cp(st.queries + pod);
     const TPlan& tp = *cp(ta.plans + cp(ta.plan_of)[i]);
     const uint64_t tk = pod_tie_key(st.seed, ta.seq0 + i);
@@ -2946,6 +3213,7 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
         PT[tb.off + v] = x;
       }
     }
+    KGPU_WSTAMP(7);
     const bool pany = tp.n_hard > 0 && SANY[tp.hard_sig] != 0;
     bool aff_any = false;
     for (int a = 0; a < tp.n_aff; ++a) aff_any |= tp.aff_hist[a] >= 0 && TOT[tp.aff_hist[a]] > 0;
@@ -2963,10 +3231,17 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
       const int n = lo + j * B + tid;
       feas[j] = false;
       if (n >= st.N) continue;
-      const uint32_t sw =
-          trow_eval<FM, SM, kDef>(st, ta, q, tp, r[j], n, H, PT, M, pany, aff_any, LAB, j * B + tid, sr[j], o[j], ta.diag);
-      if (ta.diag) gp(st.status)[n] = sw;  // kgpu_schedule_one: the cycle's Filter verdicts
-      if (sw) continue;
+      if (kAhead && ind_have) {
+        // the non-topology half was evaluated ahead; the topology half reads this pod's tables
+        if (!ind_ok) continue;
+        o[j] = ind_o;
+        if (!trow_topo<FM>(st, ta, tp, n, H, PT, M, pany, aff_any, LAB, j * B + tid, o[j])) continue;
+      } else {
+        const uint32_t sw =
+            trow_eval<FM, SM, kDef>(st, ta, q, tp, r[j], n, H, PT, M, pany, aff_any, LAB, j * B + tid, sr[j], o[j], ta.diag);
+        if (ta.diag) gp(st.status)[n] = sw;  // kgpu_schedule_one: the cycle's Filter verdicts
+        if (sw) continue;
+      }
       feas[j] = true;
       ++sf;
       smaxT = max(smaxT, (uint32_t)o[j].taint);
@@ -3051,6 +3326,16 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
     }
     KGPU_TSTAMP(3);
     KGPU_WSTAMP(2);
+    // the next pod's non-topology half while the statistics travel (the polls below start after it;
+    // the round trip they wait for is longer than the evaluation)
+    const bool ahead = kAhead && !ta.diag && i + 1 < ta.count;
+    const kgpu_pod_query& qn = *cp(st.queries + pod + (ahead ? 1 : 0));
+    const TPlan& tpn = *cp(ta.plans + cp(ta.plan_of)[ahead ? i + 1 : i]);
+    if (ahead) {
+      const int n = lo + tid;
+      nx_ok = n < st.N && trow_ind<FM, SM, kDef>(st, ta, qn, tpn, r[0], n, sr[0], nx_o);
+    }
+    ind_next = ahead;
     // ---- NormalizeScore of every plugin under statistics S, weights, and the packed key of this
     // lane's best row; with write_diag, the cycle's per-plugin scores (as k_topo_score / k_topo_final)
     auto best_under = [&](const int64_t* S, bool write_diag, uint64_t& bkey, int& bidx) {
@@ -3204,8 +3489,17 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
     int bidx0, bi;
     best_under(STAT, ta.diag != 0, bkey0, bidx0);
     wg_best(bkey0, bidx0, bk, bi);
+    if (wave == 0 && lane == 0) store_sc1(arow + g, kGValid | bk);
+    // the candidate row with this pod applied, for the next pod (used when this workgroup wins; a pod
+    // with host ports or extended resources changes memory columns: its winner is evaluated again
+    // after the assume instead)
+    const bool vb_fast = q.scalars.count == 0 && q.ports.count == 0;
+    if (ind_next && ta.assume && bk != 0 && vb_fast && tid == bi) {
+      NodeRes t = r[0];
+      assume_regs(q, t);
+      vb_ok = trow_ind<FM, SM, kDef>(st, ta, qn, tpn, t, lo + tid, sr[0], vb_o);
+    }
     if (wave == 0) {
-      if (lane == 0) store_sc1(arow + g, kGValid | bk);
       KGPU_TSTAMP(5);
       KGPU_WSTAMP(3);
       uint64_t wkey = 0;
@@ -3325,9 +3619,21 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
               gp(st.mcnt)[(size_t)cp(ta.aux)[tp.assume_cls.begin + a] * st.N + wl] += 1;
             for (int a = 0; a < tp.own_tcls.count; ++a)
               gp(st.tcnt)[(size_t)cp(ta.aux)[tp.own_tcls.begin + a] * st.N + wl] += 1;
+            if (kAhead && ind_next) {
+              if (vb_fast) {
+                nx_ok = vb_ok;
+                nx_o = vb_o;
+              } else {
+                nx_ok = trow_ind<FM, SM, kDef>(st, ta, qn, tpn, r[0], wl, sr[0], nx_o);
+              }
+            }
           }
       }
     }
+    ind_have = ind_next;
+    ind_ok = nx_ok;
+    ind_o = nx_o;
+    asm volatile("" ::"v"(qwarm.x));
     __syncthreads();
     KGPU_TSTAMP(7);
   }
@@ -3555,6 +3861,21 @@ struct BatchRow {
                                       k_batch<FM, SM, 1, 960, true>, k_batch<FM, SM, 4, 512, true>};
 };
 using BatchFn = void (*)(const DevState*, BatchArgs);
+// the helper-wave instantiation (HB) of config (b)'s profile on the one-row-wave geometry
+template <uint32_t FM, uint32_t SM, bool E>
+struct HelperFn {
+  static constexpr BatchFn fn = nullptr;
+};
+template <uint32_t FM, uint32_t SM>
+struct HelperFn<FM, SM, true> {
+  static constexpr BatchFn fn = k_batch<FM, SM, 1, 64, false, true>;
+};
+static const BatchFn kBatchHelper[] = {
+    nullptr,
+    HelperFn<kFitFM, kFitSM, true>::fn,
+    nullptr,
+    nullptr,
+};
 static const BatchFn* const kBatch[] = {
     BatchRow<kRuntime, kRuntime>::fn,
     BatchRow<kFitFM, kFitSM>::fn,
@@ -3582,19 +3903,23 @@ int batch_geometry(int N, int max_groups, int* per, int* groups, int first) {
   return -1;
 }
 
-int launch_batch(const DevState* st, const BatchArgs& a, int groups, int geo, int spec, bool coop, void* stream) {
+int launch_batch(const DevState* st, const BatchArgs& a, int groups, int geo, int spec, bool coop, bool helper,
+                 void* stream) {
   if (spec < 0 || spec >= kNumSpecs) spec = 0;
   if (geo < 0 || geo >= kNumGeo) return -1;
   // One workgroup per CU: a dynamic LDS reservation above half a CU's 160 KB keeps the dispatcher
   // from stacking two persistent workgroups on one CU (they would share its SIMDs).
   const int x = a.R > 0 ? 1 : 0;  // node-sharded over xGMI mailboxes
-  const BatchFn fn = (x ? kBatchX : kBatch)[spec][geo];
-  static bool attr_set[2][kNumSpecs][kNumGeo] = {};
-  if (!attr_set[x][spec][geo]) {
+  const bool hb = helper && !x && geo == 0 && kBatchHelper[spec] != nullptr;
+  const BatchFn fn = hb ? kBatchHelper[spec] : (x ? kBatchX : kBatch)[spec][geo];
+  const int threads = kGeo[geo].B + 64 + (hb ? kGeo[geo].B : 0);
+  static bool attr_set[3][kNumSpecs][kNumGeo] = {};
+  const int ai = hb ? 2 : x;
+  if (!attr_set[ai][spec][geo]) {
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
                             kBatchLdsPad) != hipSuccess)
       return -1;
-    attr_set[x][spec][geo] = true;
+    attr_set[ai][spec][geo] = true;
   }
   // Cooperative: the runtime refuses a grid whose workgroups cannot all be resident at once, so
   // the granule exchange never waits on a workgroup that has not started.
@@ -3605,9 +3930,9 @@ int launch_batch(const DevState* st, const BatchArgs& a, int groups, int geo, in
   // CU on an otherwise idle device, so every workgroup is resident; were one not, the spins time out
   // into the abort word rather than hang)
   if (!coop) {
-    hipLaunchKernelGGL(fn, dim3(groups), dim3(kGeo[geo].B + 64), (unsigned)kBatchLdsPad, (hipStream_t)stream, sp, arg);
+    hipLaunchKernelGGL(fn, dim3(groups), dim3(threads), (unsigned)kBatchLdsPad, (hipStream_t)stream, sp, arg);
     if (hipGetLastError() != hipSuccess) return -1;
-  } else if (hipLaunchCooperativeKernel(reinterpret_cast<const void*>(fn), dim3(groups), dim3(kGeo[geo].B + 64),
+  } else if (hipLaunchCooperativeKernel(reinterpret_cast<const void*>(fn), dim3(groups), dim3(threads),
                                         args, (unsigned)kBatchLdsPad, (hipStream_t)stream) != hipSuccess) {
     return -1;
   }

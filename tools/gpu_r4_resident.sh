@@ -7,7 +7,7 @@ O=$R/gpurun_out/${1:-resident}
 mkdir -p $O
 cd $R && export TMPDIR=/tmp
 step() { local name=$1; shift; "$@" > $O/$name.log 2>&1; local rc=$?; echo "$name rc=$rc" >> $O/status.txt; return $rc; }
-step pytest timeout -k 10 600 python -u -m pytest tests/test_topo_resident.py tests/test_arena.py tests/test_schedule_one.py tests/test_delta.py tests/test_abort.py tests/test_topology_parity.py -x -v -m gpu --timeout 300 --timeout-method thread || exit 1
+step pytest timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread || exit 1
 step cyc_c timeout -k 10 180 python -u tools/cycle_trace.py --config c --nodes 5000 || exit 1
 step cyc_d timeout -k 10 180 python -u tools/cycle_trace.py --config d --nodes 5000 || exit 1
 step trace_b timeout -k 10 120 python -u tools/phase_trace.py --config b --nodes 5000 --pods 1000 || exit 1

@@ -55,6 +55,7 @@ def main():
         rows, spub, kpub = wt[:, :, 1] - t0, wt[:, :, 2] - t0, wt[:, :, 3] - t0
         G = wt.shape[1]
         print("per-workgroup medians over pods (ns after the earliest pod start), %d workgroups:" % G)
+        print("  tables built  " + " ".join("%5.0f" % x for x in np.median(wt[:, :, 7] - t0, axis=0)))
         print("  rows done     " + " ".join("%5.0f" % x for x in np.median(rows, axis=0)))
         print("  stats reduced " + " ".join("%5.0f" % x for x in np.median(wt[:, :, 4] - t0, axis=0)))
         print("  stats pub     " + " ".join("%5.0f" % x for x in np.median(spub, axis=0)))
