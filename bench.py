@@ -150,6 +150,10 @@ def measure(args, cfg, n_nodes_per_gpu, B, K, W, cpu_sample, cpu_threads, latenc
         eng.set_option(abi.OPT_COOPERATIVE, 0)
     if args.batch_geo is not None:
         eng.set_option(abi.OPT_BATCH_GEO, args.batch_geo)
+    if args.batch_helper is not None:
+        eng.set_option(abi.OPT_BATCH_HELPER, args.batch_helper)
+    if args.topo_resident is not None:
+        eng.set_option(abi.OPT_TOPO_RESIDENT, args.topo_resident)
     if args.topo_fused is not None:
         eng.set_option(abi.OPT_TOPO_FUSED, args.topo_fused)
     if args.no_topo_persistent:
@@ -411,6 +415,10 @@ def main():
                          "on N > 1; '' for none" % (DEFAULT_EXTRAS_1GPU, DEFAULT_EXTRAS_NGPU))
     ap.add_argument("--extra-cpu-sample", type=int, default=1000, help="pods of each extra record's CPU baseline")
     ap.add_argument("--reset-at-exit", action="store_true", help="hipDeviceReset() before exiting (profiling runs)")
+    ap.add_argument("--batch-helper", type=int, default=None,
+                    help="KGPU_OPT_BATCH_HELPER (default: the library's, 1 = config (b)'s helper wave)")
+    ap.add_argument("--topo-resident", type=int, default=None,
+                    help="KGPU_OPT_TOPO_RESIDENT (default: the library's, 1 = resident topology state)")
     ap.add_argument("--batch-geo", type=int, default=None,
                     help="smallest k_batch geometry index considered (KGPU_OPT_BATCH_GEO; 0 = 64 row threads)")
     ap.add_argument("--no-coop", action="store_true",

@@ -13,3 +13,9 @@ step cyc_d timeout -k 10 180 python -u tools/cycle_trace.py --config d --nodes 5
 step trace_b timeout -k 10 120 python -u tools/phase_trace.py --config b --nodes 5000 --pods 1000 || exit 1
 step trace_c timeout -k 10 120 python -u tools/phase_trace_topo.py --config c --nodes 5000 --pods 1000 || exit 1
 step trace_d timeout -k 10 120 python -u tools/phase_trace_topo.py --config d --nodes 5000 --pods 1000 || exit 1
+for k in 1 2; do
+  step bench_on$k timeout -k 10 200 python -u bench.py --config b --steps 20 --warmup 5 --cpu-sample 0 --latency-pods 0 --batch-helper 1 || exit 1
+  step bench_off$k timeout -k 10 200 python -u bench.py --config b --steps 20 --warmup 5 --cpu-sample 0 --latency-pods 0 --batch-helper 0 || exit 1
+done
+step bench_c timeout -k 10 200 python -u bench.py --config c --steps 10 --warmup 3 --cpu-sample 0 --latency-pods 100 || exit 1
+step bench_d timeout -k 10 200 python -u bench.py --config d --steps 10 --warmup 3 --cpu-sample 0 --latency-pods 100 || exit 1
