@@ -154,6 +154,8 @@ def measure(args, cfg, n_nodes_per_gpu, B, K, W, cpu_sample, cpu_threads, latenc
         eng.set_option(abi.OPT_BATCH_HELPER, args.batch_helper)
     if args.topo_resident is not None:
         eng.set_option(abi.OPT_TOPO_RESIDENT, args.topo_resident)
+    if args.topo_ahead is not None:
+        eng.set_option(abi.OPT_TOPO_AHEAD, args.topo_ahead)
     if args.topo_fused is not None:
         eng.set_option(abi.OPT_TOPO_FUSED, args.topo_fused)
     if args.no_topo_persistent:
@@ -419,6 +421,8 @@ def main():
                     help="KGPU_OPT_BATCH_HELPER (default: the library's, 1 = config (b)'s helper wave)")
     ap.add_argument("--topo-resident", type=int, default=None,
                     help="KGPU_OPT_TOPO_RESIDENT (default: the library's, 1 = resident topology state)")
+    ap.add_argument("--topo-ahead", type=int, default=None,
+                    help="KGPU_OPT_TOPO_AHEAD (default: the library's, 1 = next pod's non-topology half ahead)")
     ap.add_argument("--batch-geo", type=int, default=None,
                     help="smallest k_batch geometry index considered (KGPU_OPT_BATCH_GEO; 0 = 64 row threads)")
     ap.add_argument("--no-coop", action="store_true",

@@ -577,6 +577,10 @@ int kgpu_read_nodes(kgpu_ctx* ctx, int64_t* req_cpu, int64_t* req_mem, int64_t* 
  * BalancedAllocation + LeastAllocated profile on its one-row-wave geometry runs a helper wave that
  * evaluates LeastAllocated and the tie-break ranks beside the row wave; 0 = the row wave alone. */
 #define KGPU_OPT_BATCH_HELPER 14
+/* KGPU_OPT_TOPO_AHEAD (15): 1 (default) = the persistent topology kernel evaluates the next pod's
+ * filters and scores outside PodTopologySpread / InterPodAffinity while the current pod's statistics
+ * and key travel; 0 = every pod's rows are evaluated after the previous pod's assume. */
+#define KGPU_OPT_TOPO_AHEAD 15
 int kgpu_set_option(kgpu_ctx* ctx, int32_t option, int64_t value);
 /* Diagnostics of KGPU_OPT_TOPO_RESIDENT: out[0] = persistent topology runs that started from the
  * resident state, out[1] = runs that recomputed it. */

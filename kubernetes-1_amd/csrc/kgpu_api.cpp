@@ -206,6 +206,7 @@ struct kgpu_ctx {
   uint64_t tc_hits = 0, tc_misses = 0;
   bool tc_on = true;                               // KGPU_OPT_TOPO_RESIDENT
   bool batch_helper = true;                        // KGPU_OPT_BATCH_HELPER
+  bool topo_ahead = true;                          // KGPU_OPT_TOPO_AHEAD
   size_t ar_limit = 1 << 20;                       // KGPU_OPT_ARENA_BYTES (bytes of arena items per cycle)
   DevState ds_last{};                              // the DevState image last uploaded by a short cycle
   const void* ds_ptr = nullptr;                    // ... into this dstate allocation (null: none)
@@ -1551,6 +1552,7 @@ int run_tbatch(kgpu_ctx* c, TRun& tr, int first, int count, int64_t first_seq, i
   a.elig = reinterpret_cast<uint32_t*>(zi + b_hist + b_tot + b_reg + b_sany);
   a.gran = reinterpret_cast<uint64_t*>(use_tc ? z : z + b_init);
   a.writeback = use_tc ? 1 : 0;
+  a.ahead = c->topo_ahead ? 1 : 0;
   if (c->tb_abort_mapped) {
     abort_word = reinterpret_cast<int32_t*>(z + total);
     a.done = abort_word + 1;
@@ -3098,6 +3100,7 @@ int kgpu_set_option(kgpu_ctx* c, int32_t option, int64_t value) try {
   else if (option == KGPU_OPT_COOPERATIVE) c->coop = value != 0;
   else if (option == KGPU_OPT_BATCH_GEO) c->batch_geo_first = (int)std::max<int64_t>(0, value);
   else if (option == KGPU_OPT_BATCH_HELPER) c->batch_helper = value != 0;
+  else if (option == KGPU_OPT_TOPO_AHEAD) c->topo_ahead = value != 0;
   else if (option == KGPU_OPT_TOPO_RESIDENT) {
     c->tc_on = value != 0;
     c->tc.valid = false;

@@ -397,6 +397,7 @@ struct TBatchArgs {
   int32_t abort_at;       // KGPU_OPT_ABORT_AT test hook (-1: never), as in BatchArgs
   int32_t diag;           // kgpu_schedule_one: status word and per-plugin raw / normalized scores of every
                           // node (the run is one pod; every lane zeroes its nodes' diagnostic rows first)
+  int32_t ahead;          // evaluate the next pod's non-topology half during the exchanges (KGPU_OPT_TOPO_AHEAD)
   int32_t writeback;      // workgroup 0 stores its final histogram bins and totals back into hist_init /
                           // tot_init: the next run with the same tables starts from them without a
                           // k_tbatch_init pass (kgpu_api.cpp TCache)

@@ -3328,7 +3328,7 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
     KGPU_WSTAMP(2);
     // the next pod's non-topology half while the statistics travel (the polls below start after it;
     // the round trip they wait for is longer than the evaluation)
-    const bool ahead = kAhead && !ta.diag && i + 1 < ta.count;
+    const bool ahead = kAhead && ta.ahead && !ta.diag && i + 1 < ta.count;
     const kgpu_pod_query& qn = *cp(st.queries + pod + (ahead ? 1 : 0));
     const TPlan& tpn = *cp(ta.plans + cp(ta.plan_of)[ahead ? i + 1 : i]);
     if (ahead) {
@@ -3336,6 +3336,10 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
       nx_ok = n < st.N && trow_ind<FM, SM, kDef>(st, ta, qn, tpn, r[0], n, sr[0], nx_o);
     }
     ind_next = ahead;
+    // this pod's tie-break ranks, for the keys formed once the statistics are in
+    uint64_t rk[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) rk[j] = rank40(tk, (uint64_t)(st.node_base + lo + j * B + tid), st.tie_mode);
     // ---- NormalizeScore of every plugin under statistics S, weights, and the packed key of this
     // lane's best row; with write_diag, the cycle's per-plugin scores (as k_topo_score / k_topo_final)
     auto best_under = [&](const int64_t* S, bool write_diag, uint64_t& bkey, int& bidx) {
@@ -3401,7 +3405,7 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
                         vp * st.w_of[KGPU_S_POD_TOPOLOGY_SPREAD] + vi * st.w_of[KGPU_S_INTER_POD_AFFINITY] +
                         vd * st.w_of[KGPU_S_DEFAULT_POD_TOPOLOGY_SPREAD];
         if (st.n_scores == 0) total = 1;
-        const uint64_t key = ((uint64_t)(total + 1) << 40) | rank40(tk, (uint64_t)(st.node_base + n), st.tie_mode);
+        const uint64_t key = ((uint64_t)(total + 1) << 40) | rk[j];
         if (key > bkey) {
           bkey = key;
           bidx = j * B + tid;

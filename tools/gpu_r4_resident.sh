@@ -17,5 +17,9 @@ for k in 1 2; do
   step bench_on$k timeout -k 10 200 python -u bench.py --config b --steps 20 --warmup 5 --cpu-sample 0 --latency-pods 0 --batch-helper 1 || exit 1
   step bench_off$k timeout -k 10 200 python -u bench.py --config b --steps 20 --warmup 5 --cpu-sample 0 --latency-pods 0 --batch-helper 0 || exit 1
 done
-step bench_c timeout -k 10 200 python -u bench.py --config c --steps 10 --warmup 3 --cpu-sample 0 --latency-pods 100 || exit 1
-step bench_d timeout -k 10 200 python -u bench.py --config d --steps 10 --warmup 3 --cpu-sample 0 --latency-pods 100 || exit 1
+for k in 1 2; do
+  step bench_c_ahead$k timeout -k 10 200 python -u bench.py --config c --steps 10 --warmup 3 --cpu-sample 0 --latency-pods 100 --topo-ahead 1 || exit 1
+  step bench_c_noahead$k timeout -k 10 200 python -u bench.py --config c --steps 10 --warmup 3 --cpu-sample 0 --latency-pods 0 --topo-ahead 0 || exit 1
+done
+step bench_d_ahead timeout -k 10 200 python -u bench.py --config d --steps 10 --warmup 3 --cpu-sample 0 --latency-pods 100 --topo-ahead 1 || exit 1
+step bench_d_noahead timeout -k 10 200 python -u bench.py --config d --steps 10 --warmup 3 --cpu-sample 0 --latency-pods 0 --topo-ahead 0 || exit 1
