@@ -727,7 +727,7 @@ __device__ __forceinline__ Winner wave_winner(const BlkKey* kb, int nb) {
 
 // NodeInfo.AddPod on the chosen row (types.go:456-480): applied by the thread that owns the row,
 // on its register copy (written back) plus the rarely used scalar and host-port columns.
-__device__ void assume_row(const DevState& st, const kgpu_pod_query& q, NodeRes& r, int n) {
+__device__ __forceinline__ void assume_row(const DevState& st, const kgpu_pod_query& q, NodeRes& r, int n) {
   r.rc += q.req[0];
   r.rm += q.req[1];
   r.re += q.req[2];
