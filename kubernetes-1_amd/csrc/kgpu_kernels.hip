@@ -2805,13 +2805,34 @@ struct TRow {
 struct TStatic {
   uint64_t tns[2], tpr[2];
   int32_t unsched, zone;
+  uint64_t em;  // eligibility of the node under each of the run's signatures (bit s), from ta.elig
 };
+// The node's own match counts a pod reads from the columns (the ScheduleAnyway count of a node-unique
+// key, the DefaultPodTopologySpread count), kept in registers across the run: only this lane's assume
+// changes them (k_tbatch owns the columns during the run), so a column read once is exact after.
+struct TCnt {
+  int32_t col[2];  // cached column (class id) per purpose: 0 ScheduleAnyway, 1 DPTS; -1 none
+  int32_t v[2];
+};
+__device__ __forceinline__ int32_t tcnt_get(const DevState& st, TCnt& c, int slot, int col, int n) {
+  if (c.col[slot] != col) {
+    c.col[slot] = col;
+    c.v[slot] = gp(st.mcnt)[(size_t)col * st.N + n];
+  }
+  return c.v[slot];
+}
+// criticalPaths[0].MatchNum of a kind-0 table (MaxInt32 when no registered pair; filtering.go:93-121)
+__device__ __forceinline__ int64_t pmin_of(const TMisc& M, int tab) {
+  const int64_t x = M.pmin[tab];
+  return x == INT64_MAX ? 2147483647 : x;
+}
 
 template <uint32_t FM, uint32_t SM, bool kDef>
 __device__ __forceinline__ uint32_t trow_eval(const DevState& st, const TBatchArgs& ta, const kgpu_pod_query& q,
                                          const TPlan& tp, const NodeRes& r, int n, const int32_t* H,
                                          const int64_t* PT, const TMisc& M, bool pany, bool aff_any,
-                                         const int32_t* LAB, int li, const TStatic& sr, TRow& o, bool diag) {
+                                         const int32_t* LAB, int li, const TStatic& sr, TCnt& cc, TRow& o,
+                                         bool diag) {
   // node label value ids from the workgroup's LDS copy (keys < lab_keys), else from the column
   auto nval = [&](int key) -> int {
     if (key < 0) return -1;
@@ -2823,7 +2844,7 @@ __device__ __forceinline__ uint32_t trow_eval(const DevState& st, const TBatchAr
       const THard hc = tp.hard[c];
       const int v = nval(hc.key);
       if (v < 0) return KGPU_CODE_UNSCHEDULABLE << 8;
-      if (PT[hc.pt_off + v] + hc.self_match - M.pmin[hc.tab] > hc.max_skew) return KGPU_CODE_UNSCHEDULABLE << 8;
+      if (PT[hc.pt_off + v] + hc.self_match - pmin_of(M, hc.tab) > hc.max_skew) return KGPU_CODE_UNSCHEDULABLE << 8;
     }
     return 0;
   };
@@ -2857,7 +2878,7 @@ __device__ __forceinline__ uint32_t trow_eval(const DevState& st, const TBatchAr
   auto one = [&](int f) -> uint32_t {
     if (f == KGPU_F_POD_TOPOLOGY_SPREAD) return pts();
     if (f == KGPU_F_INTER_POD_AFFINITY) return ipa();
-    if (f == KGPU_F_NODE_AFFINITY) return tb_elig(ta, tp.aff_sig, n) ? 0 : KGPU_CODE_UNRESOLVABLE << 8;
+    if (f == KGPU_F_NODE_AFFINITY) return ((sr.em >> tp.aff_sig) & 1u) ? 0 : KGPU_CODE_UNRESOLVABLE << 8;
     if (f == KGPU_F_NODE_UNSCHEDULABLE)  // node_unschedulable.go:51-65
       return (sr.unsched && !(q.flags & KGPU_Q_TOLERATES_UNSCHEDULABLE)) ? KGPU_CODE_UNRESOLVABLE << 8 : 0;
     if (f == KGPU_F_TAINT_TOLERATION && st.TW <= 2) {  // taint_toleration.go:54-72
@@ -2913,8 +2934,8 @@ __device__ __forceinline__ uint32_t trow_eval(const DevState& st, const TBatchAr
     } else {
       int64_t cnt;
       if (tp.soft_mode == 0) cnt = H[tp.soft_off + v];
-      else if (tp.soft_mode == 1) cnt = gp(st.mcnt)[(size_t)tp.soft_col * st.N + n];
-      else cnt = tb_elig(ta, tp.soft_sig, n) ? gp(st.mcnt)[(size_t)tp.soft_col * st.N + n] : 0;
+      else if (tp.soft_mode == 1) cnt = tcnt_get(st, cc, 0, tp.soft_col, n);
+      else cnt = ((sr.em >> tp.soft_sig) & 1u) ? tcnt_get(st, cc, 0, tp.soft_col, n) : 0;
       o.adj = cnt < tp.soft_max_skew ? tp.soft_max_skew - 1 : cnt;  // adjustForMaxSkew
     }
   }
@@ -2933,7 +2954,7 @@ __device__ __forceinline__ uint32_t trow_eval(const DevState& st, const TBatchAr
     }
   }
   o.ipa = is;
-  o.ds = tp.dpts_cls >= 0 ? gp(st.mcnt)[(size_t)tp.dpts_cls * st.N + n] : 0;
+  o.ds = tp.dpts_cls >= 0 ? tcnt_get(st, cc, 1, tp.dpts_cls, n) : 0;
   return 0;
 }
 
@@ -2950,7 +2971,7 @@ __device__ __forceinline__ bool trow_ind(const DevState& st, const TBatchArgs& t
                                          const TPlan& tp, const NodeRes& r, int n, const TStatic& sr, TRow& o) {
   auto one = [&](int f) -> bool {
     if (f == KGPU_F_POD_TOPOLOGY_SPREAD || f == KGPU_F_INTER_POD_AFFINITY) return true;
-    if (f == KGPU_F_NODE_AFFINITY) return tb_elig(ta, tp.aff_sig, n);
+    if (f == KGPU_F_NODE_AFFINITY) return ((sr.em >> tp.aff_sig) & 1u) != 0;
     if (f == KGPU_F_NODE_UNSCHEDULABLE) return !(sr.unsched && !(q.flags & KGPU_Q_TOLERATES_UNSCHEDULABLE));
     if (f == KGPU_F_TAINT_TOLERATION && st.TW <= 2) {
 #pragma unroll
@@ -2996,7 +3017,8 @@ __device__ __forceinline__ bool trow_ind(const DevState& st, const TBatchArgs& t
 template <uint32_t FM>
 __device__ __forceinline__ bool trow_topo(const DevState& st, const TBatchArgs& ta, const TPlan& tp, int n,
                                           const int32_t* H, const int64_t* PT, const TMisc& M, bool pany,
-                                          bool aff_any, const int32_t* LAB, int li, TRow& o) {
+                                          bool aff_any, const int32_t* LAB, int li, const TStatic& sr, TCnt& cc,
+                                          TRow& o) {
   auto nval = [&](int key) -> int {
     if (key < 0) return -1;
     return key < ta.lab_keys ? LAB[key * ta.per + li] : gp(st.label_val)[(size_t)key * st.N + n];
@@ -3014,7 +3036,7 @@ __device__ __forceinline__ bool trow_topo(const DevState& st, const TBatchArgs& 
       const THard hc = tp.hard[c];
       const int v = nval(hc.key);
       if (v < 0) return false;
-      if (PT[hc.pt_off + v] + hc.self_match - M.pmin[hc.tab] > hc.max_skew) return false;
+      if (PT[hc.pt_off + v] + hc.self_match - pmin_of(M, hc.tab) > hc.max_skew) return false;
     }
   }
   if (has_ipa) {
@@ -3049,8 +3071,8 @@ __device__ __forceinline__ bool trow_topo(const DevState& st, const TBatchArgs& 
     } else {
       int64_t cnt;
       if (tp.soft_mode == 0) cnt = H[tp.soft_off + v];
-      else if (tp.soft_mode == 1) cnt = gp(st.mcnt)[(size_t)tp.soft_col * st.N + n];
-      else cnt = tb_elig(ta, tp.soft_sig, n) ? gp(st.mcnt)[(size_t)tp.soft_col * st.N + n] : 0;
+      else if (tp.soft_mode == 1) cnt = tcnt_get(st, cc, 0, tp.soft_col, n);
+      else cnt = ((sr.em >> tp.soft_sig) & 1u) ? tcnt_get(st, cc, 0, tp.soft_col, n) : 0;
       o.adj = cnt < tp.soft_max_skew ? tp.soft_max_skew - 1 : cnt;  // adjustForMaxSkew
     }
   }
@@ -3068,7 +3090,7 @@ __device__ __forceinline__ bool trow_topo(const DevState& st, const TBatchArgs& 
     }
   }
   o.ipa = is;
-  o.ds = tp.dpts_cls >= 0 ? gp(st.mcnt)[(size_t)tp.dpts_cls * st.N + n] : 0;
+  o.ds = tp.dpts_cls >= 0 ? tcnt_get(st, cc, 1, tp.dpts_cls, n) : 0;
   return true;
 }
 
@@ -3133,11 +3155,26 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
   const int64_t txw = XG ? tx_row_words(ta.nranks) : 0;
   NodeRes r[K];
   TStatic sr[K];
+  TCnt cc[K];
 #pragma unroll
   for (int j = 0; j < K; ++j) {
     const int n = lo + j * B + tid;
     r[j] = NodeRes{};
-    sr[j] = TStatic{{0, 0}, {0, 0}, 0, -1};
+    sr[j] = TStatic{{0, 0}, {0, 0}, 0, -1, 0};
+    cc[j] = TCnt{{-1, -1}, {0, 0}};
+    if (n < st.N) {
+      // the node's eligibility bits (k_tbatch_init's bitmaps): one load per signature, all in flight
+      uint64_t em = 0;
+      for (int s0 = 0; s0 < ta.n_sigs; s0 += 8) {
+        uint32_t w[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          w[u] = s0 + u < ta.n_sigs ? gp(ta.elig)[cp(ta.sigs)[s0 + u].elig_word + (n >> 5)] : 0u;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) em |= (uint64_t)((w[u] >> (n & 31)) & 1u) << (s0 + u);
+      }
+      sr[j].em = em;
+    }
     if (n < st.N) {
       if (ta.diag) {
         // a diagnostic (kgpu_schedule_one) run: this node's per-plugin raw / normalized rows start at
@@ -3217,9 +3254,7 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
     const bool pany = tp.n_hard > 0 && SANY[tp.hard_sig] != 0;
     bool aff_any = false;
     for (int a = 0; a < tp.n_aff; ++a) aff_any |= tp.aff_hist[a] >= 0 && TOT[tp.aff_hist[a]] > 0;
-    __syncthreads();
-    if (tid < kTMaxTabs && M.pmin[tid] == INT64_MAX) M.pmin[tid] = 2147483647;  // criticalPaths init MaxInt32
-    __syncthreads();
+    __syncthreads();  // (readers map an unset minimum to MaxInt32: pmin_of)
     KGPU_TSTAMP(1);
     // ---- Filter + raw scores of this workgroup's rows
     bool feas[K];
@@ -3235,10 +3270,10 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
         // the non-topology half was evaluated ahead; the topology half reads this pod's tables
         if (!ind_ok) continue;
         o[j] = ind_o;
-        if (!trow_topo<FM>(st, ta, tp, n, H, PT, M, pany, aff_any, LAB, j * B + tid, o[j])) continue;
+        if (!trow_topo<FM>(st, ta, tp, n, H, PT, M, pany, aff_any, LAB, j * B + tid, sr[j], cc[j], o[j])) continue;
       } else {
-        const uint32_t sw =
-            trow_eval<FM, SM, kDef>(st, ta, q, tp, r[j], n, H, PT, M, pany, aff_any, LAB, j * B + tid, sr[j], o[j], ta.diag);
+        const uint32_t sw = trow_eval<FM, SM, kDef>(st, ta, q, tp, r[j], n, H, PT, M, pany, aff_any, LAB, j * B + tid,
+                                                    sr[j], cc[j], o[j], ta.diag);
         if (ta.diag) gp(st.status)[n] = sw;  // kgpu_schedule_one: the cycle's Filter verdicts
         if (sw) continue;
       }
@@ -3619,8 +3654,12 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
         for (int j = 0; j < K; ++j)
           if (local == j * B + tid) {
             assume_row(st, q, r[j], wl);
-            for (int a = 0; a < tp.assume_cls.count; ++a)
-              gp(st.mcnt)[(size_t)cp(ta.aux)[tp.assume_cls.begin + a] * st.N + wl] += 1;
+            for (int a = 0; a < tp.assume_cls.count; ++a) {
+              const int col = cp(ta.aux)[tp.assume_cls.begin + a];
+              gp(st.mcnt)[(size_t)col * st.N + wl] += 1;
+              cc[j].v[0] += cc[j].col[0] == col ? 1 : 0;
+              cc[j].v[1] += cc[j].col[1] == col ? 1 : 0;
+            }
             for (int a = 0; a < tp.own_tcls.count; ++a)
               gp(st.tcnt)[(size_t)cp(ta.aux)[tp.own_tcls.begin + a] * st.N + wl] += 1;
             if (kAhead && ind_next) {
