@@ -1138,7 +1138,7 @@ size_t a16(size_t x) { return (x + 15) & ~(size_t)15; }
 constexpr size_t kTMiscBytes = 1024;
 
 // LDS layout of a run (byte offsets into the dynamic region); returns the total
-size_t t_layout(const TRun& tr, kgpu::TBatchArgs* a, int B, int lab_keys = 0, int per = 0, bool cmp = false) {
+size_t t_layout(const TRun& tr, kgpu::TBatchArgs* a, int B, int lab_keys = 0, int per = 0) {
   size_t o = a16((size_t)tr.lds_bins * 4);
   const size_t o_reg = o;
   o = a16(o + (size_t)tr.reg_words * 4);
@@ -1159,10 +1159,7 @@ size_t t_layout(const TRun& tr, kgpu::TBatchArgs* a, int B, int lab_keys = 0, in
   o = a16(o + kTMiscBytes);
   const size_t o_lab = o;
   o = a16(o + (size_t)lab_keys * (size_t)per * 4);
-  const size_t o_cmp = o;  // the compacted feasible rows (k_tbatch normalize pass)
-  if (cmp) o = a16(o + (size_t)per * (4 * 8 + 5 * 4));
   if (a) {
-    a->o_cmp = cmp ? (int32_t)o_cmp : -1;
     a->o_lab = (int32_t)o_lab;
     a->lab_keys = lab_keys;
     a->o_reg = (int32_t)o_reg;
@@ -1431,11 +1428,9 @@ int run_tbatch(kgpu_ctx* c, TRun& tr, int first, int count, int64_t first_seq, i
                                 c->cfg.most[1].resource == 1 && c->cfg.most[1].weight == 1)
                   ? 1 : 0;
   // node labels of the workgroup's rows in LDS when they fit beside the histograms
-  // (and the compacted rows of the normalize pass, when they fit without any label keys)
-  const bool cmp = t_layout(tr, nullptr, 512, 0, per, true) <= (size_t)kgpu::kTLdsBudget;
   int lab_keys = std::min(c->st.K, 16);
-  while (lab_keys > 0 && t_layout(tr, nullptr, 512, lab_keys, per, cmp) > (size_t)kgpu::kTLdsBudget) --lab_keys;
-  size_t lds = t_layout(tr, &a, 512, lab_keys, per, cmp);
+  while (lab_keys > 0 && t_layout(tr, nullptr, 512, lab_keys, per) > (size_t)kgpu::kTLdsBudget) --lab_keys;
+  size_t lds = t_layout(tr, &a, 512, lab_keys, per);
   // at least half a CU's LDS: one persistent workgroup per CU (two would share its SIMDs)
   a.lds_bytes = (int32_t)std::max<size_t>(lds, 96 * 1024);
   const size_t N = (size_t)c->st.N;

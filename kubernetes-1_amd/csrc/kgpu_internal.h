@@ -393,8 +393,6 @@ struct TBatchArgs {
   int32_t n_keys;         // node label keys the run's deltas read (winner's labels staged in LDS)
   // byte offsets of the LDS regions (histogram bins start at 0)
   int32_t o_reg, o_tot, o_sany, o_stat, o_smask, o_zsum, o_misc, o_pt, o_lab;
-  int32_t o_cmp;          // feasible rows compacted for the normalize pass ([per] int64 part, adj, ipa, rank,
-                          // then [per] int32 taint, na, ds, zone, local index); -1: not laid out
   int32_t lab_keys;       // node label keys cached in LDS per workgroup ([lab_keys][per] value ids)
   int32_t abort_at;       // KGPU_OPT_ABORT_AT test hook (-1: never), as in BatchArgs
   int32_t diag;           // kgpu_schedule_one: status word and per-plugin raw / normalized scores of every

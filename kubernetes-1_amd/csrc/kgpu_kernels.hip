@@ -2637,7 +2637,7 @@ struct TMisc {
   int64_t pmin[kTMaxTabs];   // criticalPaths[0].MatchNum per kind-0 table (MaxInt32 when none)
   uint64_t wkey;             // winning key of the pod (0: no feasible node)
   int32_t wg, wnode;         // its workgroup, its global node index
-  int32_t abort, ncomp;      // ncomp: feasible rows compacted this pod (o_cmp)
+  int32_t abort, pad;
   uint64_t akey[16];         // per-wave argmax partials
   int32_t aidx[16];
   int32_t wlab[64];          // the winner's value of each key the run's deltas read (-1 absent)
@@ -3109,18 +3109,6 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
   int64_t* PT = reinterpret_cast<int64_t*>(lds_raw + ta.o_pt);
   int32_t* LAB = reinterpret_cast<int32_t*>(lds_raw + ta.o_lab);  // [lab_keys][per] label value ids
   TMisc& M = *reinterpret_cast<TMisc*>(lds_raw + ta.o_misc);
-  // the compacted feasible rows of the pod (o_cmp >= 0): the normalize pass runs over these only
-  const bool cmpon = ta.o_cmp >= 0;
-  const int cper = ta.per;
-  int64_t* C_part = reinterpret_cast<int64_t*>(lds_raw + (cmpon ? ta.o_cmp : 0));
-  int64_t* C_adj = C_part + cper;
-  int64_t* C_ipa = C_adj + cper;
-  uint64_t* C_rk = reinterpret_cast<uint64_t*>(C_ipa + cper);
-  int32_t* C_taint = reinterpret_cast<int32_t*>(C_rk + cper);
-  int32_t* C_na = C_taint + cper;
-  int32_t* C_ds = C_na + cper;
-  int32_t* C_zone = C_ds + cper;
-  int32_t* C_li = C_zone + cper;
   constexpr int W = B / 64;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int G = gridDim.x, g = blockIdx.x;
@@ -3244,7 +3232,6 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
     if (tid < kTMaxTabs) M.pmin[tid] = INT64_MAX;
     if (tid < 8) M.acc32[tid] = 0;
     if (tid < 2) M.acc64[tid] = tid == 0 ? INT64_MAX : INT64_MIN;
-    if (tid == 0) M.ncomp = 0;
     __syncthreads();
     for (int k = 0; k < tp.tabs.count; ++k) {
       const TTab tb = cp(ta.tabs)[tp.tabs.begin + k];
@@ -3310,29 +3297,6 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
       if (z >= 0) {
         szoned = 1;
         if (o[j].ds && z < ta.zones) atomicAdd(ZSUM + z, o[j].ds);
-      }
-    }
-    // the feasible rows into the compacted arrays (wave-aggregated slot allocation)
-    int moff[K];
-    if (cmpon) {
-#pragma unroll
-      for (int j = 0; j < K; ++j) {
-        const uint64_t fb = __ballot(feas[j]);
-        int base = 0;
-        if (lane == 0 && fb) base = atomicAdd(&M.ncomp, (int)__popcll(fb));
-        base = __builtin_amdgcn_readfirstlane(base);
-        moff[j] = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(fb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fb, 0u));
-        if (feas[j]) {
-          const int t = moff[j];
-          C_part[t] = o[j].part;
-          C_adj[t] = o[j].adj;
-          C_ipa[t] = o[j].ipa;
-          C_taint[t] = o[j].taint;
-          C_na[t] = o[j].na;
-          C_ds[t] = o[j].ds;
-          C_zone[t] = sr[j].zone;
-          C_li[t] = j * B + tid;
-        }
       }
     }
     KGPU_TSTAMP(2);
@@ -3410,10 +3374,7 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
     // this pod's tie-break ranks, for the keys formed once the statistics are in
     uint64_t rk[K];
 #pragma unroll
-    for (int j = 0; j < K; ++j) {
-      rk[j] = rank40(tk, (uint64_t)(st.node_base + lo + j * B + tid), st.tie_mode);
-      if (cmpon && feas[j]) C_rk[moff[j]] = rk[j];
-    }
+    for (int j = 0; j < K; ++j) rk[j] = rank40(tk, (uint64_t)(st.node_base + lo + j * B + tid), st.tie_mode);
     // ---- NormalizeScore of every plugin under statistics S, weights, and the packed key of this
     // lane's best row; with write_diag, the cycle's per-plugin scores (as k_topo_score / k_topo_final)
     auto best_under = [&](const int64_t* S, bool write_diag, uint64_t& bkey, int& bidx) {
@@ -3446,26 +3407,28 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
       const double invP = (pmx > 0 && pmx < (1ll << 52)) ? 1.0 / (double)pmx : 0.0;
       bkey = 0;
       bidx = -1;
-      auto one = [&](int64_t part, int64_t adj, int64_t ipa, int32_t taint, int32_t na, int32_t ds, int32_t z,
-                     uint64_t rkv, int li) {
-        const int n = lo + li;
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        if (!feas[j]) continue;
+        const int n = lo + j * B + tid;
         // DefaultNormalizeScore (helper/normalize_score.go:26-54): non-negative operands, exact
         // through div_nonneg
-        const int64_t ps = (adj != INT64_MIN && tp.n_soft) ? (int64_t)((double)adj * wsoft) : 0;
+        const int64_t ps = (o[j].adj != INT64_MIN && tp.n_soft) ? (int64_t)((double)o[j].adj * wsoft) : 0;
         bool s1 = false, s2 = false, s3 = false;
-        const int64_t qt = ratio100(100 * (int64_t)taint, maxT, invT, s1);
-        const int64_t qn = ratio100(100 * (int64_t)na, maxNA, invNA, s2);
+        const int64_t qt = ratio100(100 * (int64_t)o[j].taint, maxT, invT, s1);
+        const int64_t qn = ratio100(100 * (int64_t)o[j].na, maxNA, invNA, s2);
         // scoring.go:248-256; pmn <= ps <= pmx, so the dividend is non-negative
-        const bool pdiv = adj != INT64_MIN && pmx != 0;  // pmn is set whenever pmx is
+        const bool pdiv = o[j].adj != INT64_MIN && pmx != 0;  // pmn is set whenever pmx is
         const int64_t qp = ratio100(pdiv ? 100 * (pmx + pmn - ps) : 0, pmx, invP, s3);
-        const int64_t vt = maxT == 0 ? 100 : 100 - (s1 ? div_nonneg(100 * (int64_t)taint, maxT) : qt);
-        const int64_t vn = maxNA == 0 ? (int64_t)na : (s2 ? div_nonneg(100 * (int64_t)na, maxNA) : qn);
-        const int64_t vp = adj == INT64_MIN ? 0 : (pmx == 0 ? 100 : (s3 ? div_nonneg(100 * (pmx + pmn - ps), pmx) : qp));
-        const int64_t vi = idiff > 0 ? (int64_t)(Mx * ((double)(ipa - imn) / (double)idiff)) : 0;
+        const int64_t vt = maxT == 0 ? 100 : 100 - (s1 ? div_nonneg(100 * (int64_t)o[j].taint, maxT) : qt);
+        const int64_t vn = maxNA == 0 ? (int64_t)o[j].na : (s2 ? div_nonneg(100 * (int64_t)o[j].na, maxNA) : qn);
+        const int64_t vp = o[j].adj == INT64_MIN ? 0 : (pmx == 0 ? 100 : (s3 ? div_nonneg(100 * (pmx + pmn - ps), pmx) : qp));
+        const int64_t vi = idiff > 0 ? (int64_t)(Mx * ((double)(o[j].ipa - imn) / (double)idiff)) : 0;
         int64_t vd = 0;
         if (tp.dpts_cls != -2) {
           double f = Mx;
-          if (dmax_node > 0) f = Mx * ((double)(dmax_node - ds) / (double)dmax_node);
+          if (dmax_node > 0) f = Mx * ((double)(dmax_node - o[j].ds) / (double)dmax_node);
+          const int z = sr[j].zone;
           if (have_zones && z >= 0) {
             double zs = Mx;
             if (dmax_zone > 0) zs = Mx * ((double)(dmax_zone - S[kTFixed + ta.soft_words + z]) / (double)dmax_zone);
@@ -3473,21 +3436,21 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
           }
           vd = (int64_t)f;
         }
-        int64_t total = part + vt * st.w_of[KGPU_S_TAINT_TOLERATION] + vn * st.w_of[KGPU_S_NODE_AFFINITY] +
+        int64_t total = o[j].part + vt * st.w_of[KGPU_S_TAINT_TOLERATION] + vn * st.w_of[KGPU_S_NODE_AFFINITY] +
                         vp * st.w_of[KGPU_S_POD_TOPOLOGY_SPREAD] + vi * st.w_of[KGPU_S_INTER_POD_AFFINITY] +
                         vd * st.w_of[KGPU_S_DEFAULT_POD_TOPOLOGY_SPREAD];
         if (st.n_scores == 0) total = 1;
-        const uint64_t key = ((uint64_t)(total + 1) << 40) | rkv;
+        const uint64_t key = ((uint64_t)(total + 1) << 40) | rk[j];
         if (key > bkey) {
           bkey = key;
-          bidx = li;
+          bidx = j * B + tid;
         }
         if (write_diag) {
           const size_t N = (size_t)st.N;
           gp(st.diag_raw)[KGPU_S_POD_TOPOLOGY_SPREAD * N + n] =
-              (adj == INT64_MIN || !tp.n_soft) ? 0 : (int64_t)((double)adj * wsoft);
-          gp(st.diag_raw)[KGPU_S_INTER_POD_AFFINITY * N + n] = ipa;
-          gp(st.diag_raw)[KGPU_S_DEFAULT_POD_TOPOLOGY_SPREAD * N + n] = tp.dpts_cls == -2 ? 0 : ds;
+              (o[j].adj == INT64_MIN || !tp.n_soft) ? 0 : (int64_t)((double)o[j].adj * wsoft);
+          gp(st.diag_raw)[KGPU_S_INTER_POD_AFFINITY * N + n] = o[j].ipa;
+          gp(st.diag_raw)[KGPU_S_DEFAULT_POD_TOPOLOGY_SPREAD * N + n] = tp.dpts_cls == -2 ? 0 : o[j].ds;
           for (int si = 0; si < st.n_scores; ++si) {
             const int s = cp(st.scores)[si];
             int64_t v;
@@ -3502,15 +3465,6 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
             gp(st.diag_norm)[(size_t)s * N + n] = v;
           }
         }
-      };
-      if (cmpon) {
-        // the feasible rows only, packed: waves past them skip the pass
-        const int F = M.ncomp;
-        for (int t = tid; t < F; t += B) one(C_part[t], C_adj[t], C_ipa[t], C_taint[t], C_na[t], C_ds[t], C_zone[t], C_rk[t], C_li[t]);
-      } else {
-#pragma unroll
-        for (int j = 0; j < K; ++j)
-          if (feas[j]) one(o[j].part, o[j].adj, o[j].ipa, o[j].taint, o[j].na, o[j].ds, sr[j].zone, rk[j], j * B + tid);
       }
     };
     // the workgroup's best key: wave partials through LDS, combined by wave 0 (every wave calls it)
