@@ -2942,6 +2942,7 @@ int kgpu_create(const kgpu_config* cfg, kgpu_ctx** out) try {
     if (e[0] == '1') signal(SIGSEGV, segv_trace);
   *out = nullptr;
   if (cfg->abi_version != KGPU_ABI_VERSION) return KGPU_E_INVAL;
+  if (kgpu::kernel_layout_sig() != kgpu::layout_sig_of()) return KGPU_E_STATE;  // mixed-revision build
   if (cfg->n_filters < 0 || cfg->n_filters > KGPU_NUM_FILTERS || cfg->n_scores < 0 ||
       cfg->n_scores > KGPU_NUM_SCORES || cfg->n_least < 0 || cfg->n_least > 8 || cfg->n_most < 0 || cfg->n_most > 8)
     return KGPU_E_INVAL;

@@ -530,6 +530,13 @@ int launch_topo_phase(const DevState* st, const PodArgs& a, int phase, int block
 // Persistent topology run: signature bitmaps + pair registrations and histogram
 // initialization from the match-count columns (k_tbatch_init), then k_tbatch.  kidx: geometry.
 int tbatch_geometry(int N, int max_groups, int* per, int* groups);
+// The launch-argument layouts as the kernel translation unit saw them: a library linked from a host
+// object and a kernel object of different revisions refuses to start (kgpu_create).
+constexpr int64_t layout_sig_of() {
+  return (int64_t)sizeof(TBatchArgs) * 1000003 + (int64_t)sizeof(BatchArgs) * 10007 + (int64_t)sizeof(DevState) * 101 +
+         (int64_t)sizeof(PodArgs) + (int64_t)sizeof(TPlan) * 7919;
+}
+int64_t kernel_layout_sig();
 // k_tbatch_init over the local nodes (a.per * groups >= N); then, on a node-sharded
 // engine, launch_xreduce over the init region; then launch_tbatch (xg: the XG instantiation).
 int launch_tbatch_init(const DevState* st, const TBatchArgs& a, int groups, void* stream);

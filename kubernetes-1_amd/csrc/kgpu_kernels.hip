@@ -3798,6 +3798,8 @@ static const TBatchFn* const kTBatch[2][4] = {
     {TBatchRow<kRuntime, kRuntime, false, true>::fn, TBatchRow<kRuntime, kRuntime, true, true>::fn,
      TBatchRow<kDefaultFM, kDefaultSM, true, true>::fn, TBatchRow<kDefaultFM, kAutoscalerSM, true, true>::fn}};
 
+int64_t kernel_layout_sig() { return layout_sig_of(); }
+
 int tbatch_geometry(int N, int max_groups, int* per, int* groups) {
   for (int gi = 0; gi < kNumTGeo; ++gi) {
     const int p = kTGeo[gi].B * kTGeo[gi].K;

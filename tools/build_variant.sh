@@ -4,11 +4,15 @@
 set -e
 R=$(cd "$(dirname "$0")/.." && pwd)
 SRC=$1; OUT=$2
-API=$(ls -t $R/build/obj/kgpu_api.cpp.*.o | head -1)
+# the host object compiled from the CURRENT tree (an object of another revision would disagree with
+# the variant about the launch-argument layouts)
+API=$(mktemp /tmp/kapi.XXXXXX.o)
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -ffp-contract=off -Wall -Wno-unused-result \
+  -I$R/include -c $R/kubernetes-1_amd/csrc/kgpu_api.cpp -o $API
 TMPO=$(mktemp /tmp/kvar.XXXXXX.o)
 cp "$SRC" $R/kubernetes-1_amd/csrc/.variant_$$.hip
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -ffp-contract=off -mllvm -amdgpu-kernarg-preload-count=16 \
   -Wall -Wno-unused-result -I$R/include -c $R/kubernetes-1_amd/csrc/.variant_$$.hip -o $TMPO
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$OUT.tmp" $TMPO $API -ldl
 mv "$OUT.tmp" "$OUT"
-rm -f $TMPO $R/kubernetes-1_amd/csrc/.variant_$$.hip
+rm -f $TMPO $API $R/kubernetes-1_amd/csrc/.variant_$$.hip
