@@ -299,6 +299,14 @@ __device__ __forceinline__ int64_t ratio100(int64_t x, int64_t cap, double inv, 
   q += r < 0 ? -1 : (r >= cap ? 1 : 0);
   return q;
 }
+// floor(x / cap) for 0 <= x <= 100 * cap < 2^31 (cap > 0, inv ~ 1/cap): 32-bit operands, one
+// conversion each way and the remainder correction
+__device__ __forceinline__ int32_t ratio100_32(int32_t x, int32_t cap, double inv) {
+  int32_t q = (int32_t)((double)x * inv);
+  const int32_t r = x - q * cap;
+  q += r < 0 ? -1 : (r >= cap ? 1 : 0);
+  return q;
+}
 __device__ __forceinline__ int64_t least_one(int64_t cap, int64_t req, double inv, bool& slow) {
   const bool zero = cap == 0 || req > cap;
   bool s;
@@ -2645,7 +2653,10 @@ struct TMisc {
   // statistics accumulated across the waves (LDS atomics), kTFixed slots
   int32_t acc32[8];          // kTFeas, kTMaxT, kTMaxNA, kTNonIgn, kTAdjMin (as ~min), kTAdjMax, kTDptsMax, kTZoned
   int64_t acc64[2];          // kTIpaMin, kTIpaMax
+  double logw[8];            // math.Log table entries logb .. logb + 7, loaded while the statistics travel
+  int32_t logb, pad2;
 };
+static_assert(sizeof(TMisc) <= 1024, "kTMiscBytes (kgpu_api.cpp) holds TMisc");
 
 __device__ __forceinline__ int tslot_op(int rr, int soft_words) {
   return rr < kTFixed ? tstat_op(rr) : (rr < kTFixed + soft_words ? kOpOr : kOpSum);
@@ -3211,6 +3222,7 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
   bool ind_have = false;                     // (uniform) ind_* hold this pod's trow_ind of the lane's row
   bool ind_next = false;                     // (uniform) ... and nx_* the next pod's
   bool ind_ok = false, nx_ok = false, vb_ok = false;
+  int log_guess = 2;                         // (uniform) math.Log index of the last pod's topology size
   TRow ind_o{}, nx_o{}, vb_o{};              // part / taint / na only
   if (trun) trun_row[1] = (int64_t)__builtin_amdgcn_s_memrealtime();
   for (int i = 0; i < ta.count; ++i) {
@@ -3363,6 +3375,15 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
     KGPU_WSTAMP(2);
     // the next pod's non-topology half while the statistics travel (the polls below start after it;
     // the round trip they wait for is longer than the evaluation)
+    // the math.Log entries around the previous pod's topology size, issued before the evaluation
+    // below and staged in LDS after it
+    double logw_pre = 0.0;
+    int logb_pre = 0;
+    if (tp.n_soft && wave == W - 1 && lane < 8) {
+      const int nl = st.n_total + 3;
+      logb_pre = max(0, min(log_guess - 3, nl - 8));
+      logw_pre = lane < nl ? st.log_table[logb_pre + lane] : 0.0;
+    }
     const bool ahead = kAhead && ta.ahead && !ta.diag && i + 1 < ta.count;
     const kgpu_pod_query& qn = *cp(st.queries + pod + (ahead ? 1 : 0));
     const TPlan& tpn = *cp(ta.plans + cp(ta.plan_of)[ahead ? i + 1 : i]);
@@ -3371,6 +3392,12 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
       nx_ok = n < st.N && trow_ind<FM, SM, kDef>(st, ta, qn, tpn, r[0], n, sr[0], nx_o);
     }
     ind_next = ahead;
+    // the math.Log entries around the previous pod's topology size (it changes by a few per pod): the
+    // normalize pass reads its weight from LDS instead of a dependent global load
+    if (tp.n_soft && wave == W - 1 && lane < 8) {
+      M.logw[lane] = logw_pre;  // loaded before the evaluation above
+      if (lane == 0) M.logb = logb_pre;
+    }
     // this pod's tie-break ranks, for the keys formed once the statistics are in
     uint64_t rk[K];
 #pragma unroll
@@ -3387,7 +3414,10 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
           size = 0;
           for (int w = 0; w < tp.soft_words; ++w) size += __popc((uint32_t)S[kTFixed + w]);
         }
-        wsoft = st.log_table[size + 2];  // topologyNormalizingWeight (scoring.go:286-288)
+        // topologyNormalizingWeight (scoring.go:286-288): math.Log(size + 2)
+        const int64_t li = size + 2 - M.logb;
+        wsoft = (li >= 0 && li < 8) ? M.logw[li] : st.log_table[size + 2];
+        log_guess = (int)(size + 2);
         if (S[kTNonIgn] > 0) {
           // int64(cnt * w) does not decrease with cnt: the extremes come from the extreme counts
           pmn = (int64_t)((double)S[kTAdjMin] * wsoft);
@@ -3405,6 +3435,8 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
       // as divisors: one reciprocal each, and ratio100's exact quotient per node
       const double invT = maxT > 0 ? 1.0 / (double)maxT : 0.0, invNA = maxNA > 0 ? 1.0 / (double)maxNA : 0.0;
       const double invP = (pmx > 0 && pmx < (1ll << 52)) ? 1.0 / (double)pmx : 0.0;
+      // the 32-bit quotients apply (maxima below 2^24: every quotient's dividend is below 2^31)
+      const bool small = maxT >= 0 && maxT < (1 << 24) && maxNA >= 0 && maxNA < (1 << 24) && pmx >= 0 && pmx < (1 << 24);
       bkey = 0;
       bidx = -1;
 #pragma unroll
@@ -3415,11 +3447,19 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
         // through div_nonneg
         const int64_t ps = (o[j].adj != INT64_MIN && tp.n_soft) ? (int64_t)((double)o[j].adj * wsoft) : 0;
         bool s1 = false, s2 = false, s3 = false;
-        const int64_t qt = ratio100(100 * (int64_t)o[j].taint, maxT, invT, s1);
-        const int64_t qn = ratio100(100 * (int64_t)o[j].na, maxNA, invNA, s2);
         // scoring.go:248-256; pmn <= ps <= pmx, so the dividend is non-negative
         const bool pdiv = o[j].adj != INT64_MIN && pmx != 0;  // pmn is set whenever pmx is
-        const int64_t qp = ratio100(pdiv ? 100 * (pmx + pmn - ps) : 0, pmx, invP, s3);
+        int64_t qt, qn, qp;
+        if (small) {
+          // every dividend below 2^31 (0 <= taint <= maxT, na <= maxNA, pmx + pmn - ps <= pmx < 2^24)
+          qt = ratio100_32(100 * o[j].taint, maxT > 0 ? maxT : 1, invT);
+          qn = ratio100_32(100 * o[j].na, maxNA > 0 ? maxNA : 1, invNA);
+          qp = ratio100_32(pdiv ? 100 * (int32_t)(pmx + pmn - ps) : 0, pmx > 0 ? (int32_t)pmx : 1, invP);
+        } else {
+          qt = ratio100(100 * (int64_t)o[j].taint, maxT, invT, s1);
+          qn = ratio100(100 * (int64_t)o[j].na, maxNA, invNA, s2);
+          qp = ratio100(pdiv ? 100 * (pmx + pmn - ps) : 0, pmx, invP, s3);
+        }
         const int64_t vt = maxT == 0 ? 100 : 100 - (s1 ? div_nonneg(100 * (int64_t)o[j].taint, maxT) : qt);
         const int64_t vn = maxNA == 0 ? (int64_t)o[j].na : (s2 ? div_nonneg(100 * (int64_t)o[j].na, maxNA) : qn);
         const int64_t vp = o[j].adj == INT64_MIN ? 0 : (pmx == 0 ? 100 : (s3 ? div_nonneg(100 * (pmx + pmn - ps), pmx) : qp));
