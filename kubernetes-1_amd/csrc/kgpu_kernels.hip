@@ -562,7 +562,12 @@ __device__ __forceinline__ void run_scores(const DevState& st, const kgpu_pod_qu
     for (int i = 0; i < st.n_scores; ++i) {
       const int s = cp(st.scores)[i];
       const int64_t v = score_one<false>(s, st, q, r, n, e);
-      if (diag) gp(st.diag_raw)[(size_t)s * st.N + n] = v;
+      if (diag) {
+        gp(st.diag_raw)[(size_t)s * st.N + n] = v;
+        // a plugin without NormalizeScore: its normalized score is the raw one (the normalize
+        // passes write only the normalized plugins, with no read-back of these rows)
+        if (!normalized(s)) gp(st.diag_norm)[(size_t)s * st.N + n] = v;
+      }
       if (!normalized(s)) part += v * cp(st.w_of)[s];
     }
     e.partial = part;
@@ -571,7 +576,10 @@ __device__ __forceinline__ void run_scores(const DevState& st, const kgpu_pod_qu
   } else {
     if constexpr ((SM >> S) & 1u) {
       const int64_t v = score_one<(SM & kDefRes) != 0>(S, st, q, r, n, e);
-      if (diag) gp(st.diag_raw)[(size_t)S * st.N + n] = v;
+      if (diag) {
+        gp(st.diag_raw)[(size_t)S * st.N + n] = v;
+        if constexpr (!(S == KGPU_S_TAINT_TOLERATION || S == KGPU_S_NODE_AFFINITY)) gp(st.diag_norm)[(size_t)S * st.N + n] = v;
+      }
       if constexpr (!(S == KGPU_S_TAINT_TOLERATION || S == KGPU_S_NODE_AFFINITY)) e.partial += v * st.w_of[S];
     }
     run_scores<SM, S + 1>(st, q, r, n, e, diag);
@@ -928,12 +936,16 @@ __global__ __launch_bounds__(kBlock) void k_final(const DevState* __restrict__ s
     const uint64_t key = ((uint64_t)total << 40) | rank40(tk, (uint64_t)(st.node_base + n), st.tie_mode);
     key_max(best, best_i, key, n);
     if (a.diag) {
+      // the normalized plugins only (run_scores wrote the others' normalized rows)
       for (int i = 0; i < st.n_scores; ++i) {
         const int s = st.scores[i];
-        int64_t v = gp(st.diag_raw)[(size_t)s * st.N + n];
-        if (s == KGPU_S_TAINT_TOLERATION) v = maxT == 0 ? 100 : 100 - (100 * v) / maxT;
-        if (s == KGPU_S_NODE_AFFINITY) v = maxNA == 0 ? v : (100 * v) / maxNA;
-        gp(st.diag_norm)[(size_t)s * st.N + n] = v;
+        if (s == KGPU_S_TAINT_TOLERATION) {
+          const int64_t v = gp(st.raw_taint)[n];
+          gp(st.diag_norm)[(size_t)s * st.N + n] = maxT == 0 ? 100 : 100 - (100 * v) / maxT;
+        } else if (s == KGPU_S_NODE_AFFINITY) {
+          const int64_t v = gp(st.raw_na)[n];
+          gp(st.diag_norm)[(size_t)s * st.N + n] = maxNA == 0 ? v : (100 * v) / maxNA;
+        }
       }
     }
   }
@@ -2062,7 +2074,10 @@ __device__ __forceinline__ void topo_filter(const DevState* __restrict__ stp, Po
             s == KGPU_S_DEFAULT_POD_TOPOLOGY_SPREAD)
           continue;  // k_topo_score / k_topo_final
         const int64_t v = score_one<false>(s, st, q, r, n, e);
-        if (a.diag) gp(st.diag_raw)[(size_t)s * st.N + n] = v;
+        if (a.diag) {
+          gp(st.diag_raw)[(size_t)s * st.N + n] = v;
+          if (!normalized(s)) gp(st.diag_norm)[(size_t)s * st.N + n] = v;  // topo_final writes the others
+        }
         if (!normalized(s)) part += v * cp(st.w_of)[s];
       }
       e.partial = part;
@@ -2238,14 +2253,16 @@ __device__ __forceinline__ void topo_final(const DevState* __restrict__ stp, Pod
     const uint64_t key = ((uint64_t)total << 40) | rank40(tk, (uint64_t)(st.node_base + n), st.tie_mode);
     key_max(best, best_i, key, n);
     if (a.diag) {
+      // the normalized and topology plugins only (run_scores wrote the others' normalized rows)
       for (int i = 0; i < st.n_scores; ++i) {
         const int s = st.scores[i];
-        int64_t v = gp(st.diag_raw)[(size_t)s * st.N + n];
+        int64_t v;
         if (s == KGPU_S_TAINT_TOLERATION) v = vt;
-        if (s == KGPU_S_NODE_AFFINITY) v = vn;
-        if (s == KGPU_S_POD_TOPOLOGY_SPREAD) v = vp;
-        if (s == KGPU_S_INTER_POD_AFFINITY) v = vi;
-        if (s == KGPU_S_DEFAULT_POD_TOPOLOGY_SPREAD) v = vd;
+        else if (s == KGPU_S_NODE_AFFINITY) v = vn;
+        else if (s == KGPU_S_POD_TOPOLOGY_SPREAD) v = vp;
+        else if (s == KGPU_S_INTER_POD_AFFINITY) v = vi;
+        else if (s == KGPU_S_DEFAULT_POD_TOPOLOGY_SPREAD) v = vd;
+        else continue;
         gp(st.diag_norm)[(size_t)s * st.N + n] = v;
       }
     }
@@ -2795,7 +2812,10 @@ __device__ __forceinline__ void tscores(const DevState& st, const kgpu_pod_query
       if ((kTopoSM >> s) & 1u) continue;
       if (s == KGPU_S_TAINT_TOLERATION && reg_taint) continue;
       const int64_t v = score_one<kDef>(s, st, q, r, n, e);
-      if (diag) gp(st.diag_raw)[(size_t)s * st.N + n] = v;
+      if (diag) {
+        gp(st.diag_raw)[(size_t)s * st.N + n] = v;
+        if (!normalized(s)) gp(st.diag_norm)[(size_t)s * st.N + n] = v;
+      }
       if (!normalized(s)) p += v * cp(st.w_of)[s];
     }
     e.partial = p;
@@ -3491,6 +3511,7 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
               (o[j].adj == INT64_MIN || !tp.n_soft) ? 0 : (int64_t)((double)o[j].adj * wsoft);
           gp(st.diag_raw)[KGPU_S_INTER_POD_AFFINITY * N + n] = o[j].ipa;
           gp(st.diag_raw)[KGPU_S_DEFAULT_POD_TOPOLOGY_SPREAD * N + n] = tp.dpts_cls == -2 ? 0 : o[j].ds;
+          // the normalized and topology plugins only (tscores wrote the others' normalized rows)
           for (int si = 0; si < st.n_scores; ++si) {
             const int s = cp(st.scores)[si];
             int64_t v;
@@ -3500,7 +3521,7 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
               case KGPU_S_POD_TOPOLOGY_SPREAD: v = vp; break;
               case KGPU_S_INTER_POD_AFFINITY: v = vi; break;
               case KGPU_S_DEFAULT_POD_TOPOLOGY_SPREAD: v = vd; break;
-              default: v = gp(st.diag_raw)[(size_t)s * N + n];
+              default: continue;
             }
             gp(st.diag_norm)[(size_t)s * N + n] = v;
           }
