@@ -1418,11 +1418,11 @@ __device__ __forceinline__ bool poll_row(const uint64_t* row, int G, const int32
   }
 }
 
-// HB (config (b)'s profile, one row wave): a helper wave beside the row wave evaluates the rows'
-// NodeResourcesLeastAllocated scores and tie-break ranks of each pod while the row wave evaluates
-// NodeResourcesFit and BalancedAllocation -- two instruction streams on two SIMDs instead of one
-// (the evaluation is issue-bound: DESIGN.md 4.3) -- and hands over ((least + 1) << 40) | rank40 per
-// row through LDS; the row wave's key adds balanced << 40 (the key's score field is the sum).
+// HB (config (b)'s profile, one row wave): two helper waves beside the row wave evaluate the rows'
+// NodeResourcesLeastAllocated (helper 1) and BalancedAllocation (helper 2) weighted scores of each pod
+// while the row wave evaluates NodeResourcesFit and the tie-break ranks -- three instruction streams on
+// three SIMDs instead of one (the evaluation is issue-bound: DESIGN.md 4.3) -- and hand them over
+// through LDS; the row wave forms ((least + balanced + 1) << 40) | rank40.
 struct HRow {
   int64_t ac, am, zc, zm;
   double ic, im;
@@ -1430,12 +1430,12 @@ struct HRow {
 
 // XG: the node-sharded instantiation (xGMI mailbox rings); the unsharded one carries none of its code.
 template <uint32_t FM, uint32_t SM, int K, int B, bool XG, bool HB = false>
-__global__ __launch_bounds__(B + 64 + (HB ? B : 0)) void k_batch(const DevState* __restrict__ stp, BatchArgs pa) {
+__global__ __launch_bounds__(B + 64 + (HB ? 2 * B : 0)) void k_batch(const DevState* __restrict__ stp, BatchArgs pa) {
   static_assert(!HB || (B == 64 && !XG &&
                        SM == ((1u << KGPU_S_BALANCED_ALLOCATION) | (1u << KGPU_S_LEAST_ALLOCATED) | kDefRes)),
                 "the helper wave splits config (b)'s profile on the one-row-wave geometry");
   const DevState& st = *stp;
-  constexpr int W = B / 64;  // row waves; wave W communicates; HB: wave W + 1 helps row wave 0
+  constexpr int W = B / 64;  // row waves; wave W communicates; HB: waves W + 1, W + 2 help row wave 0
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int G = gridDim.x, g = blockIdx.x;
   const int lo = g * pa.per;
@@ -1443,8 +1443,8 @@ __global__ __launch_bounds__(B + 64 + (HB ? B : 0)) void k_batch(const DevState*
   constexpr bool xg = XG;                       // xGMI mailbox ring (node-sharded run)
   const uint64_t tmask = xg ? (0xFull << 60) : kGValid;
   __shared__ BatchShared<B> sh;
-  __shared__ uint64_t sh_hk[HB ? 2 * K * B : 1];  // HB: [pod parity][slot][lane] helper's key part
-  __shared__ int sh_hready;                       // HB: i + 1 once pod i's helper parts are in sh_hk
+  __shared__ int64_t sh_hk[HB ? 2 * 2 * K * B : 1];  // HB: [helper][pod parity][slot][lane] weighted score
+  __shared__ int sh_hready[2];                       // HB: i + 1 once pod i's parts of helper h are in sh_hk
   __shared__ uint64_t* sh_peer_g[XG ? kMaxRanks : 1];
   __shared__ int32_t* sh_peer_f[XG ? kMaxRanks : 1];
   if constexpr (XG) {
@@ -1456,7 +1456,8 @@ __global__ __launch_bounds__(B + 64 + (HB ? B : 0)) void k_batch(const DevState*
   if (tid == 0) {
     sh.bready = 0;
     sh.cready = 0;
-    sh_hready = 0;
+    sh_hready[0] = 0;
+    sh_hready[1] = 0;
   }
   __syncthreads();
   auto ring_row = [&](int k) -> size_t { return xg ? (size_t)((pa.xseq0 + k) % pa.R) : (size_t)k; };
@@ -1487,10 +1488,11 @@ __global__ __launch_bounds__(B + 64 + (HB ? B : 0)) void k_batch(const DevState*
   if (tr && (tid == 0 || tid == B)) trow[(size_t)(i) * 16 + (k)] = (int64_t)__builtin_amdgcn_s_memrealtime()
 
   if constexpr (HB) {
-    if (wave == W + 1) {
-      // ---- helper wave: Least + rank40 of every row of the row wave (same lanes, same nodes) and of
-      // its spare lane's variant-B row; it follows the candidate and the winner as the
-      // communication wave does, so its copies of the rows take the same assumes
+    if (wave == W + 1 || wave == W + 2) {
+      // ---- helper waves: Least (helper 0) or Balanced (helper 1) of every row of the row wave (same
+      // lanes, same nodes) and of its spare lane's variant-B row; each follows the candidate and the
+      // winner as the communication wave does, so its copies of the rows take the same assumes
+      const int hw = wave - W - 1;
       HRow h[K];
 #pragma unroll
       for (int j = 0; j < K; ++j) {
@@ -1506,7 +1508,7 @@ __global__ __launch_bounds__(B + 64 + (HB ? B : 0)) void k_batch(const DevState*
         }
       }
       __builtin_amdgcn_s_waitcnt(0);
-      const int64_t wl = st.w_of[KGPU_S_LEAST_ALLOCATED];
+      const int64_t wl = st.w_of[KGPU_S_LEAST_ALLOCATED], wbal = st.w_of[KGPU_S_BALANCED_ALLOCATION];
       int cand = -1;
       bool staged = false;
       for (int i = 0; i <= pa.count; ++i) {
@@ -1518,7 +1520,6 @@ __global__ __launch_bounds__(B + 64 + (HB ? B : 0)) void k_batch(const DevState*
         const bool fast_b = have_prev && cand >= 0 && staged && pa.assume && !qmem;
         const int ob = cand >= 0 ? cand % B : -1, jb = cand >= 0 ? cand / B : -1;
         if (have_cur) {
-          const uint64_t tk = pod_tie_key(st.seed, pa.seq0 + i);
           if (fast_b) {
             // the candidate row for pod i-1 with pod i-1 applied (assume_regs), in the spare lane
             HRow t{};
@@ -1543,10 +1544,10 @@ __global__ __launch_bounds__(B + 64 + (HB ? B : 0)) void k_batch(const DevState*
             const int n = spare ? lo + cand : lo + j * B + lane;
             NodeRes nr{};
             nr.ac = h[j].ac; nr.am = h[j].am; nr.zc = h[j].zc; nr.zm = h[j].zm; nr.ic = h[j].ic; nr.im = h[j].im;
-            const int64_t lv = least_score<true>(st, qh, nr, n) * wl;
-            sh_hk[(p * K + j) * B + lane] = ((uint64_t)(lv + 1) << 40) | rank40(tk, (uint64_t)(st.node_base + n), st.tie_mode);
+            sh_hk[((hw * 2 + p) * K + j) * B + lane] =
+                hw == 0 ? least_score<true>(st, qh, nr, n) * wl : balanced_score(qh, nr) * wbal;
           }
-          if (lane == 0) lds_release(&sh_hready, i + 1);
+          if (lane == 0) lds_release(&sh_hready[hw], i + 1);
         }
         __syncthreads();  // (c)
         int wg = -1;
@@ -1715,24 +1716,24 @@ __global__ __launch_bounds__(B + 64 + (HB ? B : 0)) void k_batch(const DevState*
         if (tid == B - 1) r[K - 1] = t;
       }
       if constexpr (HB) {
-        // Fit and BalancedAllocation here; Least and the rank from the helper wave
+        // Fit and the tie-break rank here; Least and Balanced from the helper waves
         uint32_t fs[K];
-        bool any = false;
+        uint64_t rkj[K];
 #pragma unroll
         for (int j = 0; j < K; ++j) {
           const bool spare = spare_slot(j, K, tid, B);
           const int n = spare ? lo + cand : lo + j * B + tid;
           fs[j] = (spare ? fast_b : n < st.N) ? run_filters<FM>(st, q, r[j], n) : 1u;
-          any |= fs[j] == 0;
+          rkj[j] = rank40(tk, (uint64_t)(st.node_base + n), st.tie_mode);
         }
         if (q.scalars.count | q.ports.count) vm_drain();
-        int64_t bw[K];
-        const bool wave_any = __ballot(any) != 0;
+        lds_wait_ge(&sh_hready[0], i + 1, pa.abort);
+        lds_wait_ge(&sh_hready[1], i + 1, pa.abort);
 #pragma unroll
-        for (int j = 0; j < K; ++j) bw[j] = wave_any ? balanced_score(q, r[j]) * st.w_of[KGPU_S_BALANCED_ALLOCATION] : 0;
-        lds_wait_ge(&sh_hready, i + 1, pa.abort);
-#pragma unroll
-        for (int j = 0; j < K; ++j) keys[j] = fs[j] ? 0 : sh_hk[(p * K + j) * B + tid] + ((uint64_t)bw[j] << 40);
+        for (int j = 0; j < K; ++j) {
+          const int64_t tot = sh_hk[((0 * 2 + p) * K + j) * B + tid] + sh_hk[((1 * 2 + p) * K + j) * B + tid];
+          keys[j] = fs[j] ? 0 : (((uint64_t)(tot + 1) << 40) | rkj[j]);
+        }
       } else {
 #pragma unroll
         for (int j = 0; j < K; ++j) {
@@ -4018,7 +4019,7 @@ int launch_batch(const DevState* st, const BatchArgs& a, int groups, int geo, in
   const int x = a.R > 0 ? 1 : 0;  // node-sharded over xGMI mailboxes
   const bool hb = helper && !x && geo == 0 && kBatchHelper[spec] != nullptr;
   const BatchFn fn = hb ? kBatchHelper[spec] : (x ? kBatchX : kBatch)[spec][geo];
-  const int threads = kGeo[geo].B + 64 + (hb ? kGeo[geo].B : 0);
+  const int threads = kGeo[geo].B + 64 + (hb ? 2 * kGeo[geo].B : 0);
   static bool attr_set[3][kNumSpecs][kNumGeo] = {};
   const int ai = hb ? 2 : x;
   if (!attr_set[ai][spec][geo]) {
