@@ -1509,30 +1509,14 @@ __global__ __launch_bounds__(B + 64 + (HB ? 2 * B : 0)) void k_batch(const DevSt
       }
       __builtin_amdgcn_s_waitcnt(0);
       const int64_t wl = st.w_of[KGPU_S_LEAST_ALLOCATED], wbal = st.w_of[KGPU_S_BALANCED_ALLOCATION];
-      // The query words a helper reads (score_req[0..1] of pod i, nz[0..1], scalars / ports counts of
-      // pod i-1), one pod ahead through a vector load (lane l: the struct's 8-byte word l): a scalar
-      // load of a query's fields at the head of its pod would put a memory round trip there.
-      constexpr int kQW = (int)(sizeof(kgpu_pod_query) / 8);
-      static_assert(kQW <= 64, "one query per wave load");
-      auto qwords = [&](int k) -> uint64_t {
-        return (k < pa.count && lane < kQW) ? reinterpret_cast<const GAS uint64_t*>(gp(st.queries + pa.first + k))[lane] : 0ull;
-      };
-      auto qword = [&](uint64_t v, size_t off) -> int64_t { return (int64_t)readlane64(v, (int)(off / 8)); };
-      auto qhalf = [&](uint64_t v, size_t off) -> int32_t {
-        const uint64_t w = readlane64(v, (int)(off / 8));
-        return (int32_t)(off % 8 ? (w >> 32) : w);
-      };
-      uint64_t qv_cur = qwords(0), qv_prev = 0;
       int cand = -1;
       bool staged = false;
       for (int i = 0; i <= pa.count; ++i) {
         const bool have_prev = i > 0, have_cur = i < pa.count;
         const int p = i & 1;
-        const uint64_t qv_next = qwords(i + 1);  // consumed an iteration later
-        const int64_t pnz0 = have_prev ? qword(qv_prev, offsetof(kgpu_pod_query, nz)) : 0;
-        const int64_t pnz1 = have_prev ? qword(qv_prev, offsetof(kgpu_pod_query, nz) + 8) : 0;
-        const bool qmem = have_prev && (qhalf(qv_prev, offsetof(kgpu_pod_query, scalars) + 4) |
-                                        qhalf(qv_prev, offsetof(kgpu_pod_query, ports) + 4)) != 0;
+        const kgpu_pod_query* qc = st.queries + pa.first + i;       // pod i (have_cur)
+        const kgpu_pod_query* qpp = st.queries + pa.first + i - 1;  // pod i-1 (have_prev)
+        const bool qmem = have_prev && (cp(qpp)->scalars.count | cp(qpp)->ports.count) != 0;
         const bool fast_b = have_prev && cand >= 0 && staged && pa.assume && !qmem;
         const int ob = cand >= 0 ? cand % B : -1, jb = cand >= 0 ? cand / B : -1;
         if (have_cur) {
@@ -1544,16 +1528,16 @@ __global__ __launch_bounds__(B + 64 + (HB ? 2 * B : 0)) void k_batch(const DevSt
               if (j == jb) {
                 t.ac = lane64(h[j].ac, ob);
                 t.am = lane64(h[j].am, ob);
-                t.zc = lane64(h[j].zc, ob) + pnz0;
-                t.zm = lane64(h[j].zm, ob) + pnz1;
+                t.zc = lane64(h[j].zc, ob) + cp(qpp)->nz[0];
+                t.zm = lane64(h[j].zm, ob) + cp(qpp)->nz[1];
                 t.ic = __builtin_bit_cast(double, lane64(__builtin_bit_cast(int64_t, h[j].ic), ob));
                 t.im = __builtin_bit_cast(double, lane64(__builtin_bit_cast(int64_t, h[j].im), ob));
               }
             if (lane == B - 1) h[K - 1] = t;
           }
           kgpu_pod_query qh;
-          qh.score_req[0] = qword(qv_cur, offsetof(kgpu_pod_query, score_req));
-          qh.score_req[1] = qword(qv_cur, offsetof(kgpu_pod_query, score_req) + 8);
+          qh.score_req[0] = cp(qc)->score_req[0];
+          qh.score_req[1] = cp(qc)->score_req[1];
 #pragma unroll
           for (int j = 0; j < K; ++j) {
             const bool spare = spare_slot(j, K, lane, B);
@@ -1576,8 +1560,8 @@ __global__ __launch_bounds__(B + 64 + (HB ? 2 * B : 0)) void k_batch(const DevSt
 #pragma unroll
           for (int j = 0; j < K; ++j)
             if (j == jb) {
-              h[j].zc += pnz0;
-              h[j].zm += pnz1;
+              h[j].zc += cp(qpp)->nz[0];
+              h[j].zm += cp(qpp)->nz[1];
             }
         }
         const bool slow = have_cur && won && pa.assume && !fast_b;
@@ -1593,8 +1577,6 @@ __global__ __launch_bounds__(B + 64 + (HB ? 2 * B : 0)) void k_batch(const DevSt
           cand = cn;
         }
         staged = have_cur && !slow && cand >= 0;
-        qv_prev = qv_cur;
-        qv_cur = qv_next;
       }
       return;
     }
