@@ -207,6 +207,7 @@ struct kgpu_ctx {
   bool tc_on = true;                               // KGPU_OPT_TOPO_RESIDENT
   bool batch_helper = true;                        // KGPU_OPT_BATCH_HELPER
   bool topo_ahead = true;                          // KGPU_OPT_TOPO_AHEAD
+  int tbatch_geo_first = 0;                        // KGPU_OPT_TBATCH_GEO
   size_t ar_limit = 1 << 20;                       // KGPU_OPT_ARENA_BYTES (bytes of arena items per cycle)
   DevState ds_last{};                              // the DevState image last uploaded by a short cycle
   const void* ds_ptr = nullptr;                    // ... into this dstate allocation (null: none)
@@ -2004,7 +2005,7 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
   // runs as a one-pod persistent run too
   const int tgeo = (topo_on && c->tfast && (!diag || n == 1) && (!sharded || xg) && !cut && !nom_dev && st.K <= 64)
                        ? kgpu::tbatch_geometry(st.N, std::min(c->max_groups > 0 ? std::min(c->max_groups, c->n_cus) : c->n_cus, 256),
-                                               &tper, &tgroups)
+                                               &tper, &tgroups, c->tbatch_geo_first)
                        : -1;
   // A one-pod persistent topology run (kgpu_schedule_one of a topology pod) keeps its abort word in
   // the arena, and k_tbatch copies it into res_pin at exit: no memset, no read-back copy.
@@ -3102,6 +3103,7 @@ int kgpu_set_option(kgpu_ctx* c, int32_t option, int64_t value) try {
   else if (option == KGPU_OPT_BATCH_GEO) c->batch_geo_first = (int)std::max<int64_t>(0, value);
   else if (option == KGPU_OPT_BATCH_HELPER) c->batch_helper = value != 0;
   else if (option == KGPU_OPT_TOPO_AHEAD) c->topo_ahead = value != 0;
+  else if (option == KGPU_OPT_TBATCH_GEO) c->tbatch_geo_first = (int)std::min<int64_t>(std::max<int64_t>(value, 0), 2);
   else if (option == KGPU_OPT_TOPO_RESIDENT) {
     c->tc_on = value != 0;
     c->tc.valid = false;

@@ -529,7 +529,8 @@ int launch_debug_broken_linear(const kgpu_shape_point* pts, int n_pts, const int
 int launch_topo_phase(const DevState* st, const PodArgs& a, int phase, int blocks, int64_t extra, void* stream);
 // Persistent topology run: signature bitmaps + pair registrations and histogram
 // initialization from the match-count columns (k_tbatch_init), then k_tbatch.  kidx: geometry.
-int tbatch_geometry(int N, int max_groups, int* per, int* groups);
+// first: the smallest geometry index considered (KGPU_OPT_TBATCH_GEO)
+int tbatch_geometry(int N, int max_groups, int* per, int* groups, int first);
 // The launch-argument layouts as the kernel translation unit saw them: a library linked from a host
 // object and a kernel object of different revisions refuses to start (kgpu_create).
 constexpr int64_t layout_sig_of() {

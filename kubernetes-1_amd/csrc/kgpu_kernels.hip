@@ -3845,12 +3845,15 @@ struct TGeo {
 };
 // 512 threads x 1 or 2 rows per lane (two waves per SIMD, no VGPR spills): up to 262,144 nodes per
 // GPU in 256 workgroups; larger shards take the per-pod topology launches.
-constexpr TGeo kTGeo[] = {{512, 1}, {512, 2}};
-constexpr int kNumTGeo = 2;
+// 256 x 1: one wave per SIMD (the per-pod phases are latency chains that two waves per SIMD
+// stretch), up to 65,536 nodes per GPU.
+constexpr TGeo kTGeo[] = {{256, 1}, {512, 1}, {512, 2}};
+constexpr int kNumTGeo = 3;
 using TBatchFn = void (*)(const DevState*, TBatchArgs);
 template <uint32_t FM, uint32_t SM, bool kDef, bool XG>
 struct TBatchRow {
-  static constexpr TBatchFn fn[kNumTGeo] = {k_tbatch<512, 1, FM, SM, kDef, XG>, k_tbatch<512, 2, FM, SM, kDef, XG>};
+  static constexpr TBatchFn fn[kNumTGeo] = {k_tbatch<256, 1, FM, SM, kDef, XG>, k_tbatch<512, 1, FM, SM, kDef, XG>,
+                                            k_tbatch<512, 2, FM, SM, kDef, XG>};
 };
 // rows: 0 generic, 1 generic with Least/Most over {cpu:1, memory:1}, 2 default provider,
 // 3 ClusterAutoscaler provider; [1]: the node-sharded (xGMI) instantiations
@@ -3862,8 +3865,8 @@ static const TBatchFn* const kTBatch[2][4] = {
 
 int64_t kernel_layout_sig() { return layout_sig_of(); }
 
-int tbatch_geometry(int N, int max_groups, int* per, int* groups) {
-  for (int gi = 0; gi < kNumTGeo; ++gi) {
+int tbatch_geometry(int N, int max_groups, int* per, int* groups, int first) {
+  for (int gi = first < 0 ? 0 : first; gi < kNumTGeo; ++gi) {
     const int p = kTGeo[gi].B * kTGeo[gi].K;
     const int g = (N + p - 1) / p;
     if (g <= max_groups) {
