@@ -207,7 +207,7 @@ struct kgpu_ctx {
   bool tc_on = true;                               // KGPU_OPT_TOPO_RESIDENT
   bool batch_helper = true;                        // KGPU_OPT_BATCH_HELPER
   bool topo_ahead = true;                          // KGPU_OPT_TOPO_AHEAD
-  int tbatch_geo_first = 0;                        // KGPU_OPT_TBATCH_GEO
+  int tbatch_geo_first = 1;                        // KGPU_OPT_TBATCH_GEO (256 x 1 measured equal: 512 x 1 stays)
   size_t ar_limit = 1 << 20;                       // KGPU_OPT_ARENA_BYTES (bytes of arena items per cycle)
   DevState ds_last{};                              // the DevState image last uploaded by a short cycle
   const void* ds_ptr = nullptr;                    // ... into this dstate allocation (null: none)

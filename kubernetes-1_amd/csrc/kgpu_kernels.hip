@@ -3845,8 +3845,9 @@ struct TGeo {
 };
 // 512 threads x 1 or 2 rows per lane (two waves per SIMD, no VGPR spills): up to 262,144 nodes per
 // GPU in 256 workgroups; larger shards take the per-pod topology launches.
-// 256 x 1: one wave per SIMD (the per-pod phases are latency chains that two waves per SIMD
-// stretch), up to 65,536 nodes per GPU.
+// 256 x 1: one wave per SIMD, up to 65,536 nodes per GPU (KGPU_OPT_TBATCH_GEO 0; it measured equal
+// to 512 x 1 at 5k nodes -- the per-pod phases are latency chains, not issue-bound -- so the default
+// starts at 512 x 1).
 constexpr TGeo kTGeo[] = {{256, 1}, {512, 1}, {512, 2}};
 constexpr int kNumTGeo = 3;
 using TBatchFn = void (*)(const DevState*, TBatchArgs);

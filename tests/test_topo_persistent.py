@@ -19,7 +19,7 @@ def _big(seed, n_nodes=1500, n_existing=600, n_pods=80):
     return nodes, ex, pods, services, rss
 
 
-def _run(args, tfast=1, groups=0, threads=4):
+def _run(args, tfast=1, groups=0, threads=4, geo=None):
     from oracle.cref import RefEngine
     nodes, ex, pods, services, rss = args
     fw = GpuFramework(Profile(), nodes, ex, cluster=Cluster(services=services, rss=rss), pods_hint=pods)
@@ -30,6 +30,8 @@ def _run(args, tfast=1, groups=0, threads=4):
     fw.engine.set_option(abi.OPT_TOPO_PERSISTENT, tfast)
     if groups:
         fw.engine.set_option(abi.OPT_PERSIST_GROUPS, groups)
+    if geo is not None:
+        fw.engine.set_option(abi.OPT_TBATCH_GEO, geo)
     got, _ = fw.engine.schedule_batch(q, pc)
     return fw, w, got, want.read_nodes(), fw.engine.read_nodes(fw.snap.n_nodes)
 
@@ -68,6 +70,15 @@ def test_gpu_tbatch_bench_configs_3000(cfg, groups):
     else:
         nodes, ex, pods, _ = cluster.pod_affinity(n_nodes=3000, n_existing=3000, n_pods=320)
     fw, w, got, rw, rg = _run((nodes, ex, pods, [], []), tfast=1, groups=groups, threads=8)
+    _check(w, got, rw, rg)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [1, 4])
+def test_gpu_tbatch_geometry_256(seed):
+    """KGPU_OPT_TBATCH_GEO 0: 256 threads x 1 row per lane (four waves, one per SIMD; six
+    workgroups at 1,500 nodes)."""
+    fw, w, got, rw, rg = _run(_big(seed), tfast=1, geo=0)
     _check(w, got, rw, rg)
 
 
