@@ -2976,7 +2976,12 @@ int kgpu_create(const kgpu_config* cfg, kgpu_ctx** out) try {
   if (cfg->device < 0 || cfg->device >= ndev) return KGPU_E_INVAL;
   c->cfg = *cfg;
   c->device = cfg->device;
-  if (hipSetDevice(c->device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
+  // KGPU_SYNC_SPIN=1 (experiment): the synchronize of every cycle spins instead of yielding.  Only
+  // takes effect before the device's context exists in this process (a failure is ignored).
+  if (hipSetDevice(c->device) != hipSuccess) return KGPU_E_DEVICE;
+  if (const char* e = std::getenv("KGPU_SYNC_SPIN"))
+    if (e[0] == '1') (void)hipSetDeviceFlags(hipDeviceScheduleSpin);
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
     return KGPU_E_DEVICE;
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, c->device) != hipSuccess) {
