@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <array>
+#include <chrono>
 #include <atomic>
 #include <exception>
 #include <memory>
@@ -204,6 +205,12 @@ struct kgpu_ctx {
     DevBuf buf;          // hist_init | tot_init | reg_init | sig_any | elig
   } tc;
   uint64_t tc_hits = 0, tc_misses = 0;
+  // KGPU_HOST_TRACE=1 (diagnostics): host time of a short cycle's steps, summed over cycles and printed
+  // to stderr by kgpu_destroy (stamp k closes step k)
+  bool htrace = false;
+  static constexpr int kHt = 12;
+  int64_t ht_last = 0, ht_sum[kHt] = {}, ht_n = 0;
+  int ht_seen = 0;
   bool tc_on = true;                               // KGPU_OPT_TOPO_RESIDENT
   bool batch_helper = true;                        // KGPU_OPT_BATCH_HELPER
   bool topo_ahead = true;                          // KGPU_OPT_TOPO_AHEAD
@@ -392,6 +399,19 @@ void stage_release(void*, void* p) { (void)hipHostFree(p); }
 kgpu::StageOps stage_ops(kgpu_ctx* c) { return kgpu::StageOps{c, stage_sync, stage_alloc, stage_release}; }
 
 // `bytes` of the arena: host and device addresses (false: no arena, or full)
+int64_t now_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+// host trace stamp k of the current short cycle (k = 0 opens it)
+inline void ht(kgpu_ctx* c, int k) {
+  if (!c->htrace) return;
+  const int64_t t = now_ns();
+  if (k > 0) c->ht_sum[k] += t - c->ht_last;
+  c->ht_last = t;
+  c->ht_seen |= 1 << k;
+}
+
 bool arena_reserve(kgpu_ctx* c, size_t bytes, char** host, char** dev) {
   size_t o;
   if (!c->ar.reserve(bytes, &o)) return false;
@@ -1575,7 +1595,9 @@ int run_tbatch(kgpu_ctx* c, TRun& tr, int first, int count, int64_t first_seq, i
     c->trace_wg_host.assign(ww, 0);
     c->trace_wg_groups = groups;
   }
+  if (c->ar.on) ht(c, 5);  // 5: tables staged, resident-state key, layout
   if ((rc = arena_flush(c))) return rc;  // the short cycle's one copy: DevState, queries, pools, tables, zeros
+  if (c->ar.on) ht(c, 6);  // 6: the copy (API call)
   const DevState* dst = static_cast<const DevState*>(c->dstate.p);
   if (!tc_hit && kgpu::launch_tbatch_init(dst, a, groups, c->stream))
     return fail(c, KGPU_E_DEVICE, "k_tbatch_init launch failed");
@@ -1602,6 +1624,7 @@ int run_tbatch(kgpu_ctx* c, TRun& tr, int first, int count, int64_t first_seq, i
   }
   if (kgpu::launch_tbatch(dst, a, groups, geo, c->spec, xg, c->coop, c->stream))
     return fail(c, KGPU_E_DEVICE, std::string("k_tbatch launch failed: ") + hipGetErrorString(hipGetLastError()));
+  if (c->ar.on) ht(c, 7);  // 7: the launch (API call)
   if (use_tc) {
     c->tc.valid = true;  // what this run leaves behind (an aborted run invalidates the mirror)
     c->tc.key.swap(tkey);
@@ -1866,8 +1889,10 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
     c->ar.begin(first, c->ar_limit > 0 ? std::min(kCycHostBytes, first + c->ar_limit) : 0);
   }
   c->tb_abort_mapped = false;
+  if (short_cycle) ht(c, 0);
   Staged sg;
   if ((rc = stage_topology(c, qs, n, pools, sg))) return rc;
+  if (short_cycle) ht(c, 1);  // 1: topology staging (QPlan, classes)
   std::vector<kgpu::QPlan>& plans = sg.plans;
   std::vector<int32_t>& aux = sg.aux;
   std::vector<kgpu::TTerm>& aux_terms = sg.aux_terms;
@@ -1877,6 +1902,7 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
     for (int32_t i = 0; i < n; ++i) batch_ports += qs[i].ports.count;
   if ((rc = reserve_ports(c, batch_ports))) return rc;
   if ((rc = upload_pools(c, pools))) return rc;
+  if (short_cycle) ht(c, 2);  // 2: ports, pools
   if (!short_cycle) {
     if ((rc = ensure(c, c->queries, sizeof(kgpu_pod_query) * (size_t)n))) return rc;
     HIP_OK(c, hipMemcpyAsync(c->queries.p, qs, sizeof(kgpu_pod_query) * (size_t)n, hipMemcpyHostToDevice, c->stream));
@@ -2022,7 +2048,9 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
       TRun& tr = runs.back();
       kgpu_pools empty{};
       const kgpu_pools* pp = pools ? pools : &empty;
+      if (short_cycle) ht(c, 3);  // 3: DevState / queries staged, geometry
       while (j < n && topo[(size_t)j] && t_add(tr, c, qs[j], plans[(size_t)j], pp, aux, aux_terms, j)) ++j;
+      if (short_cycle) ht(c, 4);  // 4: the run's tables planned (t_add)
       if (j > i) {
         if (c->timing) HIP_OK(c, hipEventRecord(get_event(c, ev), c->stream));
         if ((rc = run_tbatch(c, tr, i, j - i, first_seq, assume, tper, tgroups, tgeo, tb_arena ? nullptr : abort_word, xg,
@@ -2240,6 +2268,7 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
     i = j;
   }
   if (timed) HIP_OK(c, hipEventRecord(t1, c->stream));
+  if (short_cycle) ht(c, 8);  // 8: launches issued (after run_tbatch's 5-7)
   kgpu_result* res_host = short_cycle ? static_cast<kgpu_result*>(c->res_pin) : results;
   if (!short_cycle)
     HIP_OK(c, hipMemcpyAsync(res_host, st.results, sizeof(kgpu_result) * (size_t)n, hipMemcpyDeviceToHost, c->stream));
@@ -2248,6 +2277,7 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
   int32_t port_overflow = 0;
   if (batch_ports) HIP_OK(c, hipMemcpyAsync(&port_overflow, c->st.port_overflow, 4, hipMemcpyDeviceToHost, c->stream));
   SYNC_OK(c);
+  if (short_cycle) ht(c, 9);  // 9: synchronize
   if (short_cycle) std::memcpy(results, res_host, sizeof(kgpu_result) * (size_t)n);
   if (used_persistent && c->tb_abort_mapped) {
     // k_tbatch's last workgroup wrote the abort word (-1 left by the host: the run never finished)
@@ -2320,6 +2350,10 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
     }
   }
   c->last_diag = diag;
+  if (short_cycle && c->htrace) {
+    ht(c, 10);  // 10: records, assumed-pod bookkeeping
+    ++c->ht_n;
+  }
   return KGPU_OK;
 }
 
@@ -2981,6 +3015,7 @@ int kgpu_create(const kgpu_config* cfg, kgpu_ctx** out) try {
   if (hipSetDevice(c->device) != hipSuccess) return KGPU_E_DEVICE;
   if (const char* e = std::getenv("KGPU_SYNC_SPIN"))
     if (e[0] == '1') (void)hipSetDeviceFlags(hipDeviceScheduleSpin);
+  if (const char* e = std::getenv("KGPU_HOST_TRACE")) c->htrace = e[0] == '1';
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
     return KGPU_E_DEVICE;
   hipDeviceProp_t prop;
@@ -3029,6 +3064,15 @@ int kgpu_create(const kgpu_config* cfg, kgpu_ctx** out) try {
 
 int kgpu_destroy(kgpu_ctx* c) try {
   if (!c) return KGPU_OK;
+  if (c->htrace && c->ht_n > 0) {
+    static const char* names[kgpu_ctx::kHt] = {"", "topology staging", "ports+pools", "state staged+geometry",
+                                               "tables planned", "tables staged+key", "copy API", "launch API",
+                                               "to end of issue", "synchronize", "records+bookkeeping", ""};
+    std::fprintf(stderr, "kgpu host trace over %lld short cycles (mean ns per cycle, steps seen in the last):\n",
+                 (long long)c->ht_n);
+    for (int k = 1; k < kgpu_ctx::kHt; ++k)
+      if (c->ht_seen & (1 << k)) std::fprintf(stderr, "  %2d %-24s %9.0f\n", k, names[k], (double)c->ht_sum[k] / c->ht_n);
+  }
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   free_all(c->snap_allocs);
