@@ -209,8 +209,9 @@ struct kgpu_ctx {
   // to stderr by kgpu_destroy (stamp k closes step k)
   bool htrace = false;
   static constexpr int kHt = 12;
-  int64_t ht_last = 0, ht_sum[kHt] = {}, ht_n = 0;
+  int64_t ht_last = 0, ht_cur[kHt] = {}, ht_n = 0;
   int ht_seen = 0;
+  std::vector<std::array<int64_t, kHt>> ht_cycles;  // per cycle: ns of each step (medians at destroy)
   bool tc_on = true;                               // KGPU_OPT_TOPO_RESIDENT
   bool batch_helper = true;                        // KGPU_OPT_BATCH_HELPER
   bool topo_ahead = true;                          // KGPU_OPT_TOPO_AHEAD
@@ -407,7 +408,8 @@ int64_t now_ns() {
 inline void ht(kgpu_ctx* c, int k) {
   if (!c->htrace) return;
   const int64_t t = now_ns();
-  if (k > 0) c->ht_sum[k] += t - c->ht_last;
+  if (k == 0) std::fill(c->ht_cur, c->ht_cur + kgpu_ctx::kHt, 0);
+  if (k > 0) c->ht_cur[k] += t - c->ht_last;
   c->ht_last = t;
   c->ht_seen |= 1 << k;
 }
@@ -2353,6 +2355,9 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
   if (short_cycle && c->htrace) {
     ht(c, 10);  // 10: records, assumed-pod bookkeeping
     ++c->ht_n;
+    std::array<int64_t, kgpu_ctx::kHt> row{};
+    std::copy(c->ht_cur, c->ht_cur + kgpu_ctx::kHt, row.begin());
+    c->ht_cycles.push_back(row);
   }
   return KGPU_OK;
 }
@@ -3068,10 +3073,14 @@ int kgpu_destroy(kgpu_ctx* c) try {
     static const char* names[kgpu_ctx::kHt] = {"", "topology staging", "ports+pools", "state staged+geometry",
                                                "tables planned", "tables staged+key", "copy API", "launch API",
                                                "to end of issue", "synchronize", "records+bookkeeping", ""};
-    std::fprintf(stderr, "kgpu host trace over %lld short cycles (mean ns per cycle, steps seen in the last):\n",
-                 (long long)c->ht_n);
-    for (int k = 1; k < kgpu_ctx::kHt; ++k)
-      if (c->ht_seen & (1 << k)) std::fprintf(stderr, "  %2d %-24s %9.0f\n", k, names[k], (double)c->ht_sum[k] / c->ht_n);
+    std::fprintf(stderr, "kgpu host trace over %lld short cycles (median ns per cycle):\n", (long long)c->ht_n);
+    for (int k = 1; k < kgpu_ctx::kHt; ++k) {
+      if (!(c->ht_seen & (1 << k))) continue;
+      std::vector<int64_t> v;
+      for (const auto& r : c->ht_cycles) v.push_back(r[(size_t)k]);
+      std::nth_element(v.begin(), v.begin() + (long)(v.size() / 2), v.end());
+      std::fprintf(stderr, "  %2d %-24s %9lld\n", k, names[k], (long long)v[v.size() / 2]);
+    }
   }
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
