@@ -1624,7 +1624,13 @@ int run_tbatch(kgpu_ctx* c, TRun& tr, int first, int count, int64_t first_seq, i
     x.abort = abort_word;
     if (kgpu::launch_xreduce(x, c->stream)) return fail(c, KGPU_E_DEVICE, "cross-rank histogram reduction launch failed");
   }
-  if (kgpu::launch_tbatch(dst, a, groups, geo, c->spec, xg, c->coop, c->stream))
+  // A one-pod run (a kgpu_schedule_one cycle) launches as an ordinary dispatch: the cooperative
+  // launch's residency check costs the cycle tens of microseconds of host wall time (the synchronize
+  // returned 57 us after the launch against a 24 us run), and the grid -- at most one workgroup per
+  // CU (the LDS reservation), at most 256 -- is resident on an idle device either way; were it not,
+  // the spin timeouts raise the abort word instead of hanging.
+  const bool coop = c->coop && !(count == 1 && !xg);
+  if (kgpu::launch_tbatch(dst, a, groups, geo, c->spec, xg, coop, c->stream))
     return fail(c, KGPU_E_DEVICE, std::string("k_tbatch launch failed: ") + hipGetErrorString(hipGetLastError()));
   if (c->ar.on) ht(c, 7);  // 7: the launch (API call)
   if (use_tc) {
