@@ -1451,7 +1451,9 @@ int run_tbatch(kgpu_ctx* c, TRun& tr, int first, int count, int64_t first_seq, i
                                 c->cfg.most[1].resource == 1 && c->cfg.most[1].weight == 1)
                   ? 1 : 0;
   // node labels of the workgroup's rows in LDS when they fit beside the histograms
-  int lab_keys = std::min(c->st.K, 16);
+  // (a one-pod run reads each label it needs once: copying the workgroup's label values into LDS first
+  // would only add a round of loads to its start)
+  int lab_keys = count == 1 ? 0 : std::min(c->st.K, 16);
   while (lab_keys > 0 && t_layout(tr, nullptr, 512, lab_keys, per) > (size_t)kgpu::kTLdsBudget) --lab_keys;
   size_t lds = t_layout(tr, &a, 512, lab_keys, per);
   // at least half a CU's LDS: one persistent workgroup per CU (two would share its SIMDs)
