@@ -554,9 +554,11 @@ __device__ __forceinline__ bool normalized(int s) {
   return s == KGPU_S_TAINT_TOLERATION || s == KGPU_S_NODE_AFFINITY;
 }
 
+// dv (compile-time profiles only): a diagnostic evaluation collects each plugin's raw score in dv[S]
+// (registers) instead of storing its rows; the caller stores them later.
 template <uint32_t SM, int S = 0>
 __device__ __forceinline__ void run_scores(const DevState& st, const kgpu_pod_query& q, const NodeRes& r, int n,
-                                           NodeEval& e, bool diag) {
+                                           NodeEval& e, bool diag, int64_t* dv = nullptr) {
   if constexpr (SM == kRuntime) {
     int64_t part = 0;
     for (int i = 0; i < st.n_scores; ++i) {
@@ -576,13 +578,15 @@ __device__ __forceinline__ void run_scores(const DevState& st, const kgpu_pod_qu
   } else {
     if constexpr ((SM >> S) & 1u) {
       const int64_t v = score_one<(SM & kDefRes) != 0>(S, st, q, r, n, e);
-      if (diag) {
+      if (diag && dv) {
+        dv[S] = v;
+      } else if (diag) {
         gp(st.diag_raw)[(size_t)S * st.N + n] = v;
         if constexpr (!(S == KGPU_S_TAINT_TOLERATION || S == KGPU_S_NODE_AFFINITY)) gp(st.diag_norm)[(size_t)S * st.N + n] = v;
       }
       if constexpr (!(S == KGPU_S_TAINT_TOLERATION || S == KGPU_S_NODE_AFFINITY)) e.partial += v * st.w_of[S];
     }
-    run_scores<SM, S + 1>(st, q, r, n, e, diag);
+    run_scores<SM, S + 1>(st, q, r, n, e, diag, dv);
   }
 }
 
@@ -2805,7 +2809,7 @@ constexpr uint32_t kTopoSM = (1u << KGPU_S_POD_TOPOLOGY_SPREAD) | (1u << KGPU_S_
 // caller adds it), not from the columns.
 template <uint32_t SM, bool kDef>
 __device__ __forceinline__ void tscores(const DevState& st, const kgpu_pod_query& q, const NodeRes& r, int n, NodeEval& e,
-                                        bool reg_taint, bool diag) {
+                                        bool reg_taint, bool diag, int64_t* dv = nullptr) {
   if constexpr (SM == kRuntime) {
     int64_t p = 0;
     for (int si = 0; si < st.n_scores; ++si) {
@@ -2821,8 +2825,8 @@ __device__ __forceinline__ void tscores(const DevState& st, const kgpu_pod_query
     }
     e.partial = p;
   } else {
-    if (reg_taint) run_scores<SM & ~kTopoSM & ~(1u << KGPU_S_TAINT_TOLERATION)>(st, q, r, n, e, diag);
-    else run_scores<SM & ~kTopoSM>(st, q, r, n, e, diag);
+    if (reg_taint) run_scores<SM & ~kTopoSM & ~(1u << KGPU_S_TAINT_TOLERATION)>(st, q, r, n, e, diag, dv);
+    else run_scores<SM & ~kTopoSM>(st, q, r, n, e, diag, dv);
   }
 }
 
@@ -2864,7 +2868,7 @@ __device__ __forceinline__ uint32_t trow_eval(const DevState& st, const TBatchAr
                                          const TPlan& tp, const NodeRes& r, int n, const int32_t* H,
                                          const int64_t* PT, const TMisc& M, bool pany, bool aff_any,
                                          const int32_t* LAB, int li, const TStatic& sr, TCnt& cc, TRow& o,
-                                         bool diag) {
+                                         bool diag, int64_t* dv = nullptr) {
   // node label value ids from the workgroup's LDS copy (keys < lab_keys), else from the column
   auto nval = [&](int key) -> int {
     if (key < 0) return -1;
@@ -2944,7 +2948,7 @@ __device__ __forceinline__ uint32_t trow_eval(const DevState& st, const TBatchAr
   }
   if (status) return status;
   NodeEval e{0, 0, 0, 0};
-  tscores<SM, kDef>(st, q, r, n, e, st.TW <= 2, diag);
+  tscores<SM, kDef>(st, q, r, n, e, st.TW <= 2, diag, dv);
   if (st.TW <= 2 && st.w_of[KGPU_S_TAINT_TOLERATION] && st.any_prefer_taint) {  // taint_toleration.go:123-152
 #pragma unroll
     for (int w = 0; w < 2; ++w) {
@@ -2952,7 +2956,8 @@ __device__ __forceinline__ uint32_t trow_eval(const DevState& st, const TBatchAr
       const uint64_t tol = w < q.tol_prefer.count ? cp(st.qp.words)[q.tol_prefer.begin + w] : 0ull;
       e.taint += __popcll(sr.tpr[w] & ~tol);
     }
-    if (diag) gp(st.diag_raw)[(size_t)KGPU_S_TAINT_TOLERATION * st.N + n] = e.taint;
+    if (diag && dv) dv[KGPU_S_TAINT_TOLERATION] = e.taint;
+    else if (diag) gp(st.diag_raw)[(size_t)KGPU_S_TAINT_TOLERATION * st.N + n] = e.taint;
   }
   o.part = e.partial;
   o.taint = e.taint;
@@ -3208,9 +3213,10 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
       sr[j].em = em;
     }
     if (n < st.N) {
-      if (ta.diag) {
+      if (ta.diag && !(K == 1 && SM != kRuntime)) {
         // a diagnostic (kgpu_schedule_one) run: this node's per-plugin raw / normalized rows start at
-        // 0 (this lane's later stores of them follow in program order)
+        // 0 (this lane's later stores of them follow in program order; kDefer runs store every row
+        // once at the end instead)
         for (int sc = 0; sc < KGPU_NUM_SCORES; ++sc) {
           gp(st.diag_raw)[(size_t)sc * st.N + n] = 0;
           gp(st.diag_norm)[(size_t)sc * st.N + n] = 0;
@@ -3240,6 +3246,14 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
   // while this pod's statistics round is in flight; the candidate lane evaluates them again on its row
   // with this pod applied while the key round is in flight, for the case its workgroup wins.
   constexpr bool kAhead = K == 1;
+  // kDefer (diagnostic runs of a compile-time profile, one row per lane): the cycle's status word, raw
+  // and normalized scores stay in registers until the pod is resolved, then every row of the lane's
+  // node is stored once -- stores issued during the pod would hold every later load and the exchanges'
+  // polls behind them (vmcnt counts stores too)
+  constexpr bool kDefer = K == 1 && SM != kRuntime;
+  int64_t dv[KGPU_NUM_SCORES];
+  int64_t dn[5], dt[3];  // normalized TT, NA, PTS, IPA, DPTS; raw PTS, IPA, DPTS
+  uint32_t dstat = 0;
   bool ind_have = false;                     // (uniform) ind_* hold this pod's trow_ind of the lane's row
   bool ind_next = false;                     // (uniform) ... and nx_* the next pod's
   bool ind_ok = false, nx_ok = false, vb_ok = false;
@@ -3251,6 +3265,14 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
     KGPU_WSTAMP(0);
     if (i == ta.abort_at && g == 0 && tid == 0) __hip_atomic_store(ta.abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int pod = ta.first + i;
+    if (kDefer && ta.diag) {
+#pragma unroll
+      for (int k = 0; k < KGPU_NUM_SCORES; ++k) dv[k] = 0;
+#pragma unroll
+      for (int k = 0; k < 5; ++k) dn[k] = 0;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) dt[k] = 0;
+    }
     // warm the next pod's query record (its first touch would otherwise put a memory round trip at
     // the head of the next pod); the load is consumed at the end of this pod, so nothing waits for it
     uint4 qwarm{};
@@ -3306,8 +3328,9 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
         if (!trow_topo<FM>(st, ta, tp, n, H, PT, M, pany, aff_any, LAB, j * B + tid, sr[j], cc[j], o[j])) continue;
       } else {
         const uint32_t sw = trow_eval<FM, SM, kDef>(st, ta, q, tp, r[j], n, H, PT, M, pany, aff_any, LAB, j * B + tid,
-                                                    sr[j], cc[j], o[j], ta.diag);
-        if (ta.diag) gp(st.status)[n] = sw;  // kgpu_schedule_one: the cycle's Filter verdicts
+                                                    sr[j], cc[j], o[j], ta.diag, kDefer ? dv : (int64_t*)nullptr);
+        if (kDefer && ta.diag) dstat = sw;
+        else if (ta.diag) gp(st.status)[n] = sw;  // kgpu_schedule_one: the cycle's Filter verdicts
         if (sw) continue;
       }
       feas[j] = true;
@@ -3506,7 +3529,12 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
           bkey = key;
           bidx = j * B + tid;
         }
-        if (write_diag) {
+        if (write_diag && kDefer) {
+          dn[0] = vt; dn[1] = vn; dn[2] = vp; dn[3] = vi; dn[4] = vd;
+          dt[0] = (o[j].adj == INT64_MIN || !tp.n_soft) ? 0 : (int64_t)((double)o[j].adj * wsoft);
+          dt[1] = o[j].ipa;
+          dt[2] = tp.dpts_cls == -2 ? 0 : o[j].ds;
+        } else if (write_diag) {
           const size_t N = (size_t)st.N;
           gp(st.diag_raw)[KGPU_S_POD_TOPOLOGY_SPREAD * N + n] =
               (o[j].adj == INT64_MIN || !tp.n_soft) ? 0 : (int64_t)((double)o[j].adj * wsoft);
@@ -3741,6 +3769,29 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
     asm volatile("" ::"v"(qwarm.x));
     __syncthreads();
     KGPU_TSTAMP(7);
+    if (kDefer && ta.diag) {
+      // the cycle's rows of this lane's node, once (zeros for plugins outside the profile and for a
+      // node that failed a filter)
+      const int n = lo + tid;
+      if (n < st.N) {
+        const size_t N = (size_t)st.N;
+        gp(st.status)[n] = dstat;
+#pragma unroll
+        for (int k = 0; k < KGPU_NUM_SCORES; ++k) {
+          int64_t raw = 0, nrm = 0;
+          if ((SM >> k) & 1u) {
+            if (k == KGPU_S_POD_TOPOLOGY_SPREAD) { raw = dt[0]; nrm = dn[2]; }
+            else if (k == KGPU_S_INTER_POD_AFFINITY) { raw = dt[1]; nrm = dn[3]; }
+            else if (k == KGPU_S_DEFAULT_POD_TOPOLOGY_SPREAD) { raw = dt[2]; nrm = dn[4]; }
+            else if (k == KGPU_S_TAINT_TOLERATION) { raw = dv[k]; nrm = dn[0]; }
+            else if (k == KGPU_S_NODE_AFFINITY) { raw = dv[k]; nrm = dn[1]; }
+            else { raw = dv[k]; nrm = dv[k]; }
+          }
+          gp(st.diag_raw)[(size_t)k * N + n] = raw;
+          gp(st.diag_norm)[(size_t)k * N + n] = nrm;
+        }
+      }
+    }
   }
 #undef KGPU_TSTAMP
 #undef KGPU_WSTAMP
