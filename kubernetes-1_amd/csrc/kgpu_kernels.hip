@@ -2716,9 +2716,8 @@ __device__ __forceinline__ bool tpoll_slot(const uint64_t* row, int G, const int
 // NJ granules per lane and slot (G <= 64 * NJ).
 template <int MS, int NJ>
 __device__ __forceinline__ bool tpoll_slots(const uint64_t* srow, int G, int R, int W, int soft_words,
-                                            const int32_t* abort_word, int64_t* STAT, int wave0 = 0) {
-  // polling waves wave0 .. wave0 + W - 1
-  const int lane = threadIdx.x & 63, wave = (threadIdx.x >> 6) - wave0;
+                                            const int32_t* abort_word, int64_t* STAT) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   for (;;) {
     uint64_t v[MS][NJ];
@@ -3424,7 +3423,7 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
     // below and staged in LDS after it
     double logw_pre = 0.0;
     int logb_pre = 0;
-    if (tp.n_soft && wave == 0 && lane < 8) {
+    if (tp.n_soft && wave == W - 1 && lane < 8) {
       const int nl = st.n_total + 3;
       logb_pre = max(0, min(log_guess - 3, nl - 8));
       logw_pre = lane < nl ? st.log_table[logb_pre + lane] : 0.0;
@@ -3432,18 +3431,14 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
     const bool ahead = kAhead && ta.ahead && !ta.diag && i + 1 < ta.count;
     const kgpu_pod_query& qn = *cp(st.queries + pod + (ahead ? 1 : 0));
     const TPlan& tpn = *cp(ta.plans + cp(ta.plan_of)[ahead ? i + 1 : i]);
-    // split: the first half of the waves evaluates ahead here while the second half polls the
-    // statistics, and the second half evaluates during the key round (which wave 0 polls alone), so
-    // neither round's polls start late
-    const bool split = ahead && !XG && W >= 2 && G <= 64 && R <= 4 * (W / 2);
-    if (ahead && !(split && wave >= W / 2)) {
+    if (ahead) {
       const int n = lo + tid;
       nx_ok = n < st.N && trow_ind<FM, SM, kDef>(st, ta, qn, tpn, r[0], n, sr[0], nx_o);
     }
     ind_next = ahead;
     // the math.Log entries around the previous pod's topology size (it changes by a few per pod): the
     // normalize pass reads its weight from LDS instead of a dependent global load
-    if (tp.n_soft && wave == 0 && lane < 8) {
+    if (tp.n_soft && wave == W - 1 && lane < 8) {
       M.logw[lane] = logw_pre;  // loaded before the evaluation above
       if (lane == 0) M.logb = logb_pre;
     }
@@ -3582,9 +3577,7 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
       txrow = sh_ptx[ta.rank] + (size_t)((ta.xseq0 + i) % kTXRing) * txw;
       txtag = kGValid | ((uint64_t)(((ta.xseq0 + i) / kTXRing) & 7) << 60);
     }
-    if (split) {
-      if (wave >= W / 2) ok = tpoll_slots<4, 1>(srow, G, R, W / 2, ta.soft_words, ta.abort, STAT, W / 2);
-    } else if (!XG && G <= 64 && R <= 4 * W) {
+    if (!XG && G <= 64 && R <= 4 * W) {
       ok = tpoll_slots<4, 1>(srow, G, R, W, ta.soft_words, ta.abort, STAT);
     } else if (!XG && G <= 256 && R <= 2 * W) {
       ok = tpoll_slots<2, 4>(srow, G, R, W, ta.soft_words, ta.abort, STAT);
@@ -3634,10 +3627,6 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
       NodeRes t = r[0];
       assume_regs(q, t);
       vb_ok = trow_ind<FM, SM, kDef>(st, ta, qn, tpn, t, lo + tid, sr[0], vb_o);
-    }
-    if (split && wave >= W / 2) {
-      const int n = lo + tid;
-      nx_ok = n < st.N && trow_ind<FM, SM, kDef>(st, ta, qn, tpn, r[0], n, sr[0], nx_o);
     }
     if (wave == 0) {
       KGPU_TSTAMP(5);
