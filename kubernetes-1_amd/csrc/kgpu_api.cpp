@@ -199,10 +199,15 @@ struct kgpu_ctx {
   // k_tbatch_init pass -- valid only while nothing else changed the mirror since: every other
   // writer of node state (upload, deltas, forget, the other evaluation paths' assumes, sharding)
   // drops it.
+  // Two buffers: the run uses buf[cur] (a hit) or the other one (a miss), and zeroes the buffer it
+  // does not use at kernel entry, so a miss finds its buffer zeroed without a memset (one stream
+  // operation less per cycle where every pod brings other tables, config (d)).
   struct TCache {
     bool valid = false;
     std::string key;     // the run's hists, signature programs, registrations and geometry
-    DevBuf buf;          // hist_init | tot_init | reg_init | sig_any | elig
+    DevBuf buf[2];       // hist_init | tot_init | reg_init | sig_any | elig
+    size_t dirty[2] = {0, 0};  // leading bytes of buf[i] that may be non-zero
+    int cur = 0;
   } tc;
   uint64_t tc_hits = 0, tc_misses = 0;
   // KGPU_HOST_TRACE=1 (diagnostics): host time of a short cycle's steps, summed over cycles and printed
@@ -1548,10 +1553,17 @@ int run_tbatch(kgpu_ctx* c, TRun& tr, int first, int count, int64_t first_seq, i
   const size_t b_gran = (size_t)count * (size_t)(a.R + 1) * (size_t)groups * 8;
   const size_t b_init = b_hist + b_tot + b_reg + b_sany + b_elig;
   char* zinit = nullptr;  // the init region in TCache's buffer (use_tc), else in the zeroed region
+  int tc_use = 0;  // the TCache buffer this run uses; the other is zeroed by the kernel
   if (use_tc) {
-    if ((rc = ensure(c, c->tc.buf, b_init))) return rc;
-    zinit = static_cast<char*>(c->tc.buf.p);
-    if (!tc_hit) HIP_OK(c, hipMemsetAsync(zinit, 0, b_init, c->stream));
+    tc_use = tc_hit ? c->tc.cur : 1 - c->tc.cur;
+    DevBuf& tb = c->tc.buf[tc_use];
+    if (tb.bytes < b_init) {
+      if ((rc = ensure(c, tb, b_init))) return rc;
+      c->tc.dirty[tc_use] = tb.bytes;  // fresh memory: zeroed below
+    }
+    zinit = static_cast<char*>(tb.p);
+    if (!tc_hit && c->tc.dirty[tc_use]) HIP_OK(c, hipMemsetAsync(zinit, 0, c->tc.dirty[tc_use], c->stream));
+    c->tc.dirty[tc_use] = std::max(tc_hit ? c->tc.dirty[tc_use] : 0, b_init);
     ++(tc_hit ? c->tc_hits : c->tc_misses);
   }
   const size_t total = (use_tc ? 0 : b_init) + b_gran;
@@ -1577,6 +1589,12 @@ int run_tbatch(kgpu_ctx* c, TRun& tr, int first, int count, int64_t first_seq, i
   a.elig = reinterpret_cast<uint32_t*>(zi + b_hist + b_tot + b_reg + b_sany);
   a.gran = reinterpret_cast<uint64_t*>(use_tc ? z : z + b_init);
   a.writeback = use_tc ? 1 : 0;
+  a.zero_n16 = 0;
+  a.zero_buf = nullptr;
+  if (use_tc && c->tc.dirty[1 - tc_use]) {
+    a.zero_n16 = (int32_t)((c->tc.dirty[1 - tc_use] + 15) / 16);
+    a.zero_buf = static_cast<kgpu::TBatchArgs::Z16*>(c->tc.buf[1 - tc_use].p);
+  }
   a.ahead = c->topo_ahead ? 1 : 0;
   if (c->tb_abort_mapped) {
     abort_word = reinterpret_cast<int32_t*>(z + total);
@@ -1638,6 +1656,8 @@ int run_tbatch(kgpu_ctx* c, TRun& tr, int first, int count, int64_t first_seq, i
   if (use_tc) {
     c->tc.valid = true;  // what this run leaves behind (an aborted run invalidates the mirror)
     c->tc.key.swap(tkey);
+    c->tc.cur = tc_use;
+    c->tc.dirty[1 - tc_use] = 0;  // zeroed by this run
   }
   if (a.trace) {
     HIP_OK(c, hipMemcpyAsync(c->trace_host.data(), a.trace, sizeof(int64_t) * 16 * (size_t)(count + 1),

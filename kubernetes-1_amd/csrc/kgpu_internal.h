@@ -253,7 +253,7 @@ struct BatchArgs {
   uint64_t* gran;       // [count][groups] granules, zeroed before the launch
   int32_t* feas;        // [count][groups] feasible count of each published variant
   int32_t* abort;       // raised (1) by a workgroup that lost co-residency; zeroed before the launch
-  int64_t* trace;       // null, or [count + 1][16] s_memrealtime stamps, 8 per traced workgroup
+  int64_t* trace;        // null, or [count + 1][16] s_memrealtime stamps, 8 per traced workgroup
                         // (0 and last): iteration start, evaluated, previous pod resolved,
                         // granule published, iteration end
   int32_t abort_at;     // KGPU_OPT_ABORT_AT test hook: workgroup 0 raises the abort word at this
@@ -401,6 +401,11 @@ struct TBatchArgs {
   int32_t writeback;      // workgroup 0 stores its final histogram bins and totals back into hist_init /
                           // tot_init: the next run with the same tables starts from them without a
                           // k_tbatch_init pass (kgpu_api.cpp TCache)
+  int32_t zero_n16;       // the other resident-state buffer: its first zero_n16 16-byte words are zeroed by
+                          // the grid at kernel entry, so the next miss starts from zeros without a memset
+  int32_t pad_z;
+  struct alignas(16) Z16 { uint64_t lo, hi; };
+  Z16* zero_buf;
   int64_t* trace;        // null, or [count + 1][16] s_memrealtime stamps (KGPU_OPT_PHASE_TRACE): per pod
                           // and traced workgroup (0, last): start, PreFilter minima, rows evaluated,
                           // stats published, stats resolved, key published, winner resolved, end

@@ -2582,11 +2582,15 @@ __global__ void k_tbatch_init(const DevState* __restrict__ stp, TBatchArgs ta) {
   }
   uint64_t em = 0;
   for (int s = 0; s < ta.n_sigs; ++s) {
-    const TSig sg = cp(ta.sigs)[s];
-    bool ok = on && sg.n_keys >= 0 && node_affinity_ok(st, *cp(st.queries + sg.rep), n);
-    for (int k = 0; k < sg.n_keys && ok; ++k) ok = sg.keys[k] >= 0 && gp(st.label_val)[(size_t)sg.keys[k] * st.N + n] >= 0;
+    // through the constant pointer: a local copy's keys[k] at a run-time k lived in scratch
+    const CAS TSig* sg = cp(ta.sigs) + s;
+    bool ok = on && sg->n_keys >= 0 && node_affinity_ok(st, *cp(st.queries + sg->rep), n);
+    for (int k = 0; k < sg->n_keys && ok; ++k) {
+      const int key = sg->keys[k];
+      ok = key >= 0 && gp(st.label_val)[(size_t)key * st.N + n] >= 0;
+    }
     if (ok) em |= 1ull << s;
-    or_agg(gp(ta.elig) + sg.elig_word, n >> 5, 1u << (n & 31), ok);
+    or_agg(gp(ta.elig) + sg->elig_word, n >> 5, 1u << (n & 31), ok);
     const uint64_t any = __ballot(ok);
     if (any && lane == (int)__builtin_ctzll(any))
       __hip_atomic_store(gp(ta.sig_any) + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -3154,6 +3158,8 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
   const bool trun = ta.trace && tid == 0 && (g == 0 || g == G - 1);
   int64_t* trun_row = ta.trace ? ta.trace + (size_t)ta.count * 16 + (g == 0 ? 0 : 8) : nullptr;
   if (trun) trun_row[0] = (int64_t)__builtin_amdgcn_s_memrealtime();
+  // the resident state's spare buffer, zeroed for the next miss (nothing in this run reads it)
+  for (int i = g * B + tid; i < ta.zero_n16; i += G * B) gp(ta.zero_buf)[i] = TBatchArgs::Z16{0, 0};
 
   // LDS replicas and the workgroup's label values: eight independent loads in flight per thread
   // and round (a one-pod run pays this start-up in full; a strided loop would wait for each load)
