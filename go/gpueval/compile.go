@@ -351,6 +351,17 @@ func scoreRequest(p *v1.Pod, r v1.ResourceName) int64 {
 	return v
 }
 
+// scalarNames: a pod's scalar requests in query order (kgpu_pod_query.scalars; the names
+// kgpu_filter_reasons quotes in "Insufficient <name>").
+func scalarNames(sc map[string]int64) []string {
+	names := make([]string, 0, len(sc))
+	for r := range sc {
+		names = append(names, r)
+	}
+	sort.Strings(names)
+	return names
+}
+
 // ---------------------------------------------------------------- pod query
 func toleratesTaint(t v1.Toleration, k taintKey) bool {
 	tt := v1.Taint{Key: k.key, Value: k.value, Effect: v1.TaintEffect(k.effect)}
@@ -373,11 +384,7 @@ func (c *compiler) compilePod(pod *v1.Pod, p *pools) (C.kgpu_pod_query, error) {
 	if cpu == 0 && mem == 0 && eph == 0 && len(sc) == 0 {
 		flags |= C.KGPU_Q_FIT_ALL_ZERO
 	}
-	names := make([]string, 0, len(sc))
-	for r := range sc {
-		names = append(names, r)
-	}
-	sort.Strings(names)
+	names := scalarNames(sc)
 	b := len(p.scalars)
 	for _, r := range names {
 		col := c.scalars.get(r)

@@ -100,44 +100,86 @@ func toExprs(ls *metav1.LabelSelector) []metav1.LabelSelectorRequirement {
 	return out
 }
 
-// filterReasons rebuilds the plugins' status reasons from the device's status-word detail
-// (mirror of kubernetes-1_amd/kgpu/framework.py reasons).
-func filterReasons(plugin string, detail uint32) []string {
-	switch plugin {
-	case "NodeUnschedulable":
-		return []string{"node(s) were unschedulable"}
-	case "NodeName":
-		return []string{"node(s) didn't match the requested hostname"}
-	case "NodePorts":
-		return []string{"node(s) didn't have free ports for the requested pod ports"}
-	case "NodeAffinity":
-		return []string{"node(s) didn't match node selector"}
-	case "PodTopologySpread":
-		return []string{"node(s) didn't match pod topology spread constraints"}
-	case "TaintToleration":
-		return []string{"node(s) had taints that the pod didn't tolerate"}
-	case "NodeResourcesFit":
-		// fit.go:194-267 order: pods, cpu, memory, ephemeral-storage
-		var out []string
-		if detail&1 != 0 {
-			out = append(out, "Too many pods")
+// reasonQuery is the C copy of one cycle's pod query, pools and scalar request names, kept from
+// PreFilter until the next PreFilter so that Filter can have its status reasons formatted.
+type reasonQuery struct {
+	a     arena
+	q     *C.kgpu_pod_query
+	pools *C.kgpu_pools
+	names **C.char
+}
+
+func newReasonQuery(q C.kgpu_pod_query, p *pools, pod *v1.Pod) *reasonQuery {
+	r := &reasonQuery{}
+	r.q = cQueries(&r.a, []C.kgpu_pod_query{q})
+	r.pools = p.toC(&r.a)
+	_, _, _, sc := podRequest(pod)
+	names := scalarNames(sc)
+	if len(names) > 0 {
+		arr := (*[1 << 20]*C.char)(r.a.alloc(len(names) * int(unsafe.Sizeof((*C.char)(nil)))))
+		for i, n := range names {
+			cs := C.CString(n)
+			r.a.ptrs = append(r.a.ptrs, unsafe.Pointer(cs))
+			arr[i] = cs
 		}
-		for i, r := range []string{"cpu", "memory", "ephemeral-storage"} {
-			if detail&(2<<uint(i)) != 0 {
-				out = append(out, "Insufficient "+r)
+		r.names = &arr[0]
+	}
+	return r
+}
+
+func (r *reasonQuery) free() {
+	if r != nil {
+		r.a.free()
+	}
+}
+
+// filterReasons: the failing plugin's status reasons for node `node`'s status word, formatted by
+// kgpu_filter_reasons -- the formatter the Python mirror calls too (kgpu/framework.py
+// status_reasons), pinned by the reference's filter tables under -m gpu.  The node's Spec.Taints
+// go in spec order with their dictionary ids (TaintToleration names the first untolerated one,
+// taint_toleration.go:59-71).
+func (g *GpuEval) filterReasons(rq *reasonQuery, node int32, w uint32, n *v1.Node) ([]string, error) {
+	if rq == nil {
+		return nil, fmt.Errorf("gpueval: no compiled query for this cycle's status reasons")
+	}
+	var a arena
+	defer a.free()
+	var args C.kgpu_reason_args
+	args.q, args.pools, args.node, args.word = rq.q, rq.pools, C.int32_t(node), C.uint32_t(w)
+	args.scalar_names = rq.names
+	if n != nil && len(n.Spec.Taints) > 0 {
+		tr := (*[1 << 20]C.kgpu_taint_ref)(a.alloc(len(n.Spec.Taints) * int(unsafe.Sizeof(C.kgpu_taint_ref{}))))
+		for i, t := range n.Spec.Taints {
+			id, ok := g.comp.taints[taintKey{t.Key, t.Value, string(t.Effect)}]
+			if !ok {
+				id = -1
+			}
+			k, v, e := C.CString(t.Key), C.CString(t.Value), C.CString(string(t.Effect))
+			a.ptrs = append(a.ptrs, unsafe.Pointer(k), unsafe.Pointer(v), unsafe.Pointer(e))
+			tr[i] = C.kgpu_taint_ref{key: k, value: v, effect: e, id: C.int32_t(id)}
+		}
+		args.taints, args.n_taints = &tr[0], C.int32_t(len(n.Spec.Taints))
+	}
+	buf := make([]byte, 512)
+	for {
+		var need C.int64_t
+		cb := a.alloc(len(buf))
+		rc := C.kgpu_filter_reasons(g.eng.ctx, &args, (*C.char)(cb), C.int64_t(len(buf)), &need)
+		if rc == C.KGPU_E_CAPACITY {
+			buf = make([]byte, int(need))
+			continue
+		}
+		if rc < 0 {
+			return nil, kerr(g.eng.ctx, rc)
+		}
+		raw := C.GoBytes(cb, C.int(need))
+		out := make([]string, 0, int(rc))
+		for start, i := 0, 0; i < len(raw) && len(out) < int(rc); i++ {
+			if raw[i] == 0 {
+				out = append(out, string(raw[start:i]))
+				start = i + 1
 			}
 		}
-		return out
-	case "InterPodAffinity":
-		base := "node(s) didn't match pod affinity/anti-affinity"
-		switch detail {
-		case 1:
-			return []string{base, "node(s) didn't match pod affinity rules"}
-		case 2:
-			return []string{base, "node(s) didn't match pod anti-affinity rules"}
-		case 3:
-			return []string{base, "node(s) didn't satisfy existing pods anti-affinity rules"}
-		}
+		return out, nil
 	}
-	return nil
 }

@@ -147,6 +147,7 @@ type cycle struct {
 	norm   map[int32][]int64  // shadow mode: per score plugin id, the device-normalized 0-100 value per node
 	index  map[string]int32   // node name -> node index of this cycle's mirror
 	chosen int32              // device-selected node index, -1 = FitError
+	rq     *reasonQuery       // the pod's C query for kgpu_filter_reasons (owned by GpuEval.rq)
 }
 
 func (c *cycle) Clone() framework.StateData { return c }
@@ -167,6 +168,7 @@ type GpuEval struct {
 	// the pod of the last PreFilter, and whether it reached Reserve (track.go queue clock)
 	lastPod types.UID
 	lastRes bool
+	rq      *reasonQuery // the last diagnostic cycle's query, freed by the next PreFilter
 }
 
 func (g *GpuEval) Name() string { return Name }
@@ -479,8 +481,9 @@ func (g *GpuEval) PreFilter(ctx context.Context, cs *framework.CycleState, pod *
 			}
 		}
 	}
-	cq := cQueries(&a, []C.kgpu_pod_query{q})
-	res, _, err := g.eng.scheduleOne(cq, p.toC(&a), seq, false)
+	g.rq.free()
+	g.rq = newReasonQuery(q, p, pod)
+	res, _, err := g.eng.scheduleOne(g.rq.q, g.rq.pools, seq, false)
 	if err != nil {
 		return framework.NewStatus(framework.Error, err.Error())
 	}
@@ -489,7 +492,7 @@ func (g *GpuEval) PreFilter(ctx context.Context, cs *framework.CycleState, pod *
 	if err != nil {
 		return framework.NewStatus(framework.Error, err.Error())
 	}
-	c := &cycle{words: words, chosen: int32(res.node), index: g.mir.index}
+	c := &cycle{words: words, chosen: int32(res.node), index: g.mir.index, rq: g.rq}
 	if g.prof.Mode == "shadow" {
 		// every replaced score plugin's normalized (unweighted) value per node: the shadow plugins
 		// return them, the framework weights and sums them (framework.go:632-648)
@@ -523,11 +526,16 @@ func (g *GpuEval) Filter(ctx context.Context, cs *framework.CycleState, pod *v1.
 		}
 		return framework.NewStatus(framework.Unschedulable, "node(s) were not chosen by the batched cycle")
 	}
-	w := c.words[g.mir.index[ni.Node().Name]]
+	i := g.mir.index[ni.Node().Name]
+	w := c.words[i]
 	if w == 0 || w == C.KGPU_FS_NOT_EVALUATED {
 		return nil
 	}
-	return framework.NewStatus(framework.Code((w>>8)&3), reasons(g.prof.Filters, w)...)
+	rs, err := g.filterReasons(c.rq, i, w, ni.Node())
+	if err != nil {
+		return framework.NewStatus(framework.Error, err.Error())
+	}
+	return framework.NewStatus(framework.Code((w>>8)&3), rs...)
 }
 
 func (g *GpuEval) Score(ctx context.Context, cs *framework.CycleState, pod *v1.Pod, node string) (int64, *framework.Status) {
@@ -562,6 +570,20 @@ func (g *GpuEval) Unreserve(ctx context.Context, cs *framework.CycleState, pod *
 	g.track.requeue(pod.UID) // the error func re-queues it (scheduler.go recordSchedulingFailure)
 }
 
+// Close releases the plugin: it leaves the ForFramework registry (which otherwise keeps it, and its
+// device context, alive for the life of the process) and destroys its engine.  Call it when the
+// scheduler that built the profile is torn down or rebuilt.
+func (g *GpuEval) Close() {
+	unregister(g)
+	g.rq.free()
+	g.rq = nil
+	if g.eng != nil {
+		g.eng.close()
+		g.eng = nil
+	}
+	g.mir = nil
+}
+
 // New is the framework.PluginFactory (registry.go:28).
 func New(obj runtime.Object, h framework.FrameworkHandle) (framework.Plugin, error) {
 	prof, err := argsFrom(obj)
@@ -583,14 +605,6 @@ func (g *GpuEval) defaultSelector(pod *v1.Pod) *metav1LabelSelector {
 }
 
 // ---------------------------------------------------------------- small helpers
-func reasons(filters []string, w uint32) []string {
-	pos := int(w & 0xFF)
-	if pos == 0 || pos > len(filters) {
-		return nil
-	}
-	return filterReasons(filters[pos-1], w>>16)
-}
-
 func labelsSet(m map[string]string) labels.Set { return labels.Set(m) }
 
 func parseInt64(s string) (int64, uint8) {

@@ -56,6 +56,16 @@ func register(h framework.FrameworkHandle, g *GpuEval) {
 	registryMu.Unlock()
 }
 
+func unregister(g *GpuEval) {
+	registryMu.Lock()
+	for h, x := range registry {
+		if x == g {
+			delete(registry, h)
+		}
+	}
+	registryMu.Unlock()
+}
+
 // ForFramework returns the GpuEval of the profile whose framework is fw (profile.Profile.Framework),
 // or nil when that profile does not run one.
 func ForFramework(fw framework.FrameworkHandle) *GpuEval {

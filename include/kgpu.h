@@ -413,6 +413,39 @@ int kgpu_schedule_batch(kgpu_ctx* ctx, const kgpu_pod_query* qs, int32_t n, cons
  * normalized (unweighted) scores of one score plugin over the feasible nodes (others: 0). */
 int kgpu_get_filter(kgpu_ctx* ctx, uint32_t* status_words);
 int kgpu_get_scores(kgpu_ctx* ctx, int32_t plugin, int64_t* raw, int64_t* normalized);
+
+/* ---- Filter status reasons (kgpu_filter_reasons).  A node taint as the caller's NodeInfo holds it. */
+typedef struct kgpu_taint_ref {
+  const char* key;
+  const char* value;
+  const char* effect;   /* v1.TaintEffect: "NoSchedule", "PreferNoSchedule", "NoExecute" */
+  int32_t id;           /* taint dictionary id (the bit of the query's toleration masks) */
+  int32_t pad;
+} kgpu_taint_ref;
+
+typedef struct kgpu_reason_args {
+  const kgpu_pod_query* q;          /* the pod the word was computed for, and its pools */
+  const kgpu_pools* pools;
+  int32_t node;                     /* local node index of the word (Snapshot.List() position) */
+  uint32_t word;                    /* that node's status word (kgpu_get_filter) */
+  const kgpu_taint_ref* taints;     /* the node's Spec.Taints, in spec order */
+  int32_t n_taints;
+  int32_t n_filters;                /* ctx == NULL only: the profile's filter order (KGPU_F_*) */
+  const int32_t* filters;
+  const char* const* scalar_names;  /* resource name of each of q's scalar requests, in q->scalars order */
+} kgpu_reason_args;
+
+/* The reasons of a failed node's Filter status (framework.Status.Reasons()), formatted exactly as the
+ * failing plugin formats them: they become the FitError's per-node reasons and the pod's
+ * FailedScheduling event (replaces the plugins' NewStatus calls: node_unschedulable.go:61-63,
+ * node_name.go:50-52, node_ports.go:107-109, node_affinity.go:58-60, taint_toleration.go:59-71 with
+ * apis/core/v1/helper/helpers.go:448-471, noderesources/fit.go:159-176,194-267,
+ * podtopologyspread/filtering.go:297-324, interpodaffinity/filtering.go:372-396).
+ * Writes the reasons into buf as consecutive NUL-terminated strings and returns how many there are
+ * (0 for a feasible or unevaluated word); *bytes = the bytes they need.  KGPU_E_CAPACITY when that
+ * exceeds len (buf untouched).  ctx may be NULL (pure formatting: args.filters gives the profile's
+ * order); with a ctx, a pod with more than 12 scalar requests reads the node's scalar columns. */
+int kgpu_filter_reasons(kgpu_ctx* ctx, const kgpu_reason_args* args, char* buf, int64_t len, int64_t* bytes);
 /* Diagnostics (parity against the reference's PodTopologySpread state tables,
  * podtopologyspread/filtering_test.go:543 and scoring_test.go:38): the state the device builds for one
  * pod, for its constraint `constraint` (0-based, in kgpu_pod_query.pts_hard / pts_soft order), per

@@ -33,6 +33,7 @@
 
 #include "kgpu_internal.h"
 #include "kgpu_staging.h"
+#include "kgpu_reasons.h"
 
 // ---- RCCL, loaded on first use.  Only node sharding (kgpu_comm_unique_id / kgpu_comm_init) needs
 // it, so a one-GPU process never maps librccl: RCCL's own exit-time teardown then cannot run after a
@@ -2830,6 +2831,10 @@ int update_csr(kgpu_ctx* c, const kgpu_delta_batch* b) {
 int apply_delta(kgpu_ctx* c, const kgpu_delta_batch* b, int32_t* slots) {
   DevState& st = c->st;
   int rc;
+  // Any delta batch may change what the resident topology state was computed from -- a reorder moves
+  // rows without a single op, key metadata and CSR updates change no row either -- so it is dropped
+  // before anything is touched (an order-only batch kept it valid).
+  c->tc.valid = false;
   if (b->n_order > 0 && (rc = reorder_nodes(c, b))) return rc;
   fail_point();
   if ((rc = update_key_meta(c, b))) return rc;
@@ -2988,7 +2993,8 @@ int kgpu_struct_sizes(int32_t* out, int32_t n) {
                        (int32_t)sizeof(kgpu_node_row),  (int32_t)sizeof(kgpu_delta_batch),
                        (int32_t)sizeof(kgpu_shape_point), (int32_t)sizeof(kgpu_nominated),
                        (int32_t)sizeof(kgpu_victim),    (int32_t)sizeof(kgpu_preempt_args),
-                       (int32_t)sizeof(kgpu_node_victims)};
+                       (int32_t)sizeof(kgpu_node_victims), (int32_t)sizeof(kgpu_taint_ref),
+                       (int32_t)sizeof(kgpu_reason_args)};
   const int32_t m = (int32_t)(sizeof(s) / sizeof(s[0]));
   for (int32_t i = 0; i < n && i < m; ++i) out[i] = s[i];
   return m;
@@ -3766,6 +3772,35 @@ int kgpu_get_scores(kgpu_ctx* c, int32_t plugin, int64_t* raw, int64_t* normaliz
   if (normalized)
     HIP_OK(c, hipMemcpy(normalized, c->st.diag_norm + plugin * N, sizeof(int64_t) * N, hipMemcpyDeviceToHost));
   return KGPU_OK;
+} catch (...) {
+  return on_exception(c, false);
+}
+
+int kgpu_filter_reasons(kgpu_ctx* c, const kgpu_reason_args* a, char* buf, int64_t len, int64_t* bytes) try {
+  if (!a || len < 0 || (a->n_taints > 0 && !a->taints) || a->n_taints < 0) return KGPU_E_INVAL;
+  if (bytes) *bytes = 0;
+  const uint32_t pos = a->word & 0xFFu;
+  if (pos == 0 || a->word == KGPU_FS_NOT_EVALUATED) return 0;  // feasible / never examined: no status
+  const int32_t nf = c ? c->cfg.n_filters : a->n_filters;
+  const int32_t* fl = c ? c->cfg.filters : a->filters;
+  if (!fl || (int32_t)pos > nf) return c ? fail(c, KGPU_E_INVAL, "status word names no filter of the profile") : KGPU_E_INVAL;
+  kgpu::ScalarRead read;
+  if (c) {
+    read = [c, a](int32_t col, int64_t* alloc, int64_t* used) {
+      if (!c->uploaded || a->node < 0 || a->node >= c->st.N || col < 0 || col >= c->st.S) return false;
+      const size_t at = (size_t)col * (size_t)c->st.N + (size_t)a->node;
+      return hipStreamSynchronize(c->stream) == hipSuccess &&
+             hipMemcpy(alloc, c->st.alloc_scalar + at, 8, hipMemcpyDeviceToHost) == hipSuccess &&
+             hipMemcpy(used, c->st.req_scalar + at, 8, hipMemcpyDeviceToHost) == hipSuccess;
+    };
+  }
+  std::vector<std::string> rs;
+  const int rc = kgpu::filter_reasons(fl[pos - 1], a->word, *a, read, &rs);
+  if (rc != KGPU_OK) return c ? fail(c, rc, "status word cannot be formatted from these arguments") : rc;
+  const int64_t need = kgpu::pack_reasons(rs, buf, len);
+  if (bytes) *bytes = need;
+  if (need > len) return KGPU_E_CAPACITY;
+  return (int)rs.size();
 } catch (...) {
   return on_exception(c, false);
 }

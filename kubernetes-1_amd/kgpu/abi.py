@@ -148,6 +148,17 @@ class PreemptArgs(C.Structure):
     _fields_ = [("n_victims", C.c_int32), ("n_pdbs", C.c_int32), ("victims", vp), ("pdb_allowed", vp), ("pods", vp)]
 
 
+class TaintRef(C.Structure):
+    _fields_ = [("key", C.c_char_p), ("value", C.c_char_p), ("effect", C.c_char_p), ("id", C.c_int32),
+                ("pad", C.c_int32)]
+
+
+class ReasonArgs(C.Structure):
+    _fields_ = [("q", vp), ("pools", C.POINTER(Pools)), ("node", C.c_int32), ("word", C.c_uint32),
+                ("taints", C.POINTER(TaintRef)), ("n_taints", C.c_int32), ("n_filters", C.c_int32),
+                ("filters", C.POINTER(C.c_int32)), ("scalar_names", C.POINTER(C.c_char_p))]
+
+
 # declaration order of kgpu_struct_sizes
 STRUCT_SIZES = [("kgpu_range", RANGE.itemsize), ("kgpu_req", REQ.itemsize), ("kgpu_selector", SELECTOR.itemsize),
                 ("kgpu_node_term", NODE_TERM.itemsize), ("kgpu_pref_term", PREF_TERM.itemsize),
@@ -160,7 +171,8 @@ STRUCT_SIZES = [("kgpu_range", RANGE.itemsize), ("kgpu_req", REQ.itemsize), ("kg
                 ("kgpu_node_row", NODE_ROW.itemsize), ("kgpu_delta_batch", C.sizeof(DeltaBatch)),
                 ("kgpu_shape_point", C.sizeof(ShapePoint)), ("kgpu_nominated", NOMINATED.itemsize),
                 ("kgpu_victim", VICTIM.itemsize), ("kgpu_preempt_args", C.sizeof(PreemptArgs)),
-                ("kgpu_node_victims", NODE_VICTIMS.itemsize)]
+                ("kgpu_node_victims", NODE_VICTIMS.itemsize), ("kgpu_taint_ref", C.sizeof(TaintRef)),
+                ("kgpu_reason_args", C.sizeof(ReasonArgs))]
 
 
 def ptr(a):

@@ -791,6 +791,27 @@ class Compiler:
         return out
 
     # -------------------------------------------------- pod query
+    def _scalar_requests(self, res, pod):
+        """[(resource name, kgpu_scalar_req)] of a pod in query order: its scalar requests (Fit checks
+        them unless ignored, fit.go:247-264), then the scorers' scalar resources it does not request."""
+        prof = self.profile
+        out = []
+        seen = set()
+        for r, v in res.scalars.items():
+            check = 0 if (api.is_extended(r) and r in prof.ignored_resources) else 1
+            out.append((r, (self.scalars.get(r), check, v, api.PodResources._score(res, r, pod))))
+            seen.add(r)
+        for r, _ in list(prof.least_resources) + list(prof.most_resources):
+            if r not in ("cpu", "memory", "ephemeral-storage") and r not in seen and api.is_scalar(r):
+                out.append((r, (self.scalars.get(r), 0, 0, api.PodResources._score(res, r, pod))))
+                seen.add(r)
+        return out
+
+    def scalar_names(self, pod):
+        """The resource name of each scalar request compile_pod writes for `pod`, in query order (what
+        kgpu_filter_reasons quotes in "Insufficient <name>")."""
+        return [r for r, _ in self._scalar_requests(api.PodResources(pod), pod)]
+
     def compile_pod(self, pod, pools):
         q = np.zeros((), abi.QUERY)
         prof = self.profile
@@ -802,16 +823,7 @@ class Compiler:
         q["score_req"] = (res.score["cpu"], res.score["memory"], res.score["ephemeral-storage"])
         if res.fit_all_zero:
             flags |= abi.Q_FIT_ALL_ZERO
-        sc = []
-        seen = set()
-        for r, v in res.scalars.items():
-            check = 0 if (api.is_extended(r) and r in prof.ignored_resources) else 1
-            sc.append((self.scalars.get(r), check, v, api.PodResources._score(res, r, pod)))
-            seen.add(r)
-        for r, _ in list(prof.least_resources) + list(prof.most_resources):
-            if r not in ("cpu", "memory", "ephemeral-storage") and r not in seen and api.is_scalar(r):
-                sc.append((self.scalars.get(r), 0, 0, api.PodResources._score(res, r, pod)))
-                seen.add(r)
+        sc = [rec for _, rec in self._scalar_requests(res, pod)]
         q["scalars"] = pools._rng(pools.scalars, sc)
         nn = api.spec(pod).get("nodeName", "") or ""
         q["node_name"] = -1 if nn == "" else self.node_index.get(nn, -2)

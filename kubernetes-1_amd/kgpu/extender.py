@@ -107,7 +107,7 @@ class GpuExtender:
             totals[:] = 1  # no score plugins: every feasible node scores 1 (generic_scheduler.go:631-640)
         node = int(res["node"])
         cyc = {"words": words, "totals": totals, "winner": self.cache.list[node] if node >= 0 else None,
-               "error": node == -2, "seq": seq}
+               "error": node == -2, "seq": seq, "compiled": (q, pc)}
         if uid:
             self._memo = (uid, gen, cyc)
             self._remember(uid, pod)
@@ -184,7 +184,9 @@ class GpuExtender:
                     if w == abi.STATUS_NOT_EVALUATED:
                         failed[nm] = "node not evaluated (percentageOfNodesToScore)"
                         continue
-                    st = status_reasons(filters, self.cache.nodes, pod, nm, w)
+                    st = status_reasons(filters, self.cache.compiler, self.cache.nodes, pod, nm, w,
+                                        handle=self.cache.engine.h, node=self.cache.index[nm],
+                                        compiled=cyc["compiled"])
                     failed[nm] = ", ".join(st[2]) if st and st[2] else (st[1] if st else "")
         except ExtenderError as e:
             return {"Nodes": None, "NodeNames": None, "FailedNodes": None, "Error": str(e)}

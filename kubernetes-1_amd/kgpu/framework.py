@@ -9,8 +9,8 @@ it holds the compiled, device-resident snapshot (cache.UpdateSnapshot), compiles
                      scores (RunScorePlugins, framework.go:579-656) + the selected host
   schedule(pods)  -> the scheduleOne loop (scheduler.go:509-593) with on-device assume
 
-Status reasons are rebuilt on the host from the device's status word, exactly as the plugins
-format them (file:line at each message).
+Status reasons are rebuilt from the device's status word by libkgpu's kgpu_filter_reasons, exactly
+as the plugins format them (file:line at each message in csrc/kgpu_reasons.h).
 """
 import numpy as np
 
@@ -20,54 +20,40 @@ from .compile import CompileError, Compiler, Pools
 from . import native
 from .native import Engine
 
-REASON = {
-    "NodeUnschedulable": "node(s) were unschedulable",             # node_unschedulable.go:39
-    "NodeName": "node(s) didn't match the requested hostname",      # node_name.go:38
-    "NodePorts": "node(s) didn't have free ports for the requested pod ports",  # node_ports.go:41
-    "NodeAffinity": "node(s) didn't match node selector",           # node_affinity.go:44
-    "PodTopologySpread": "node(s) didn't match pod topology spread constraints",  # plugin.go:33
-}
-IPA_REASONS = {1: ["node(s) didn't match pod affinity/anti-affinity", "node(s) didn't match pod affinity rules"],
-               2: ["node(s) didn't match pod affinity/anti-affinity", "node(s) didn't match pod anti-affinity rules"],
-               3: ["node(s) didn't match pod affinity/anti-affinity",
-                   "node(s) didn't satisfy existing pods anti-affinity rules"]}
+def node_taints(compiler, node):
+    """A node's Spec.Taints in spec order as kgpu_filter_reasons takes them: (key, value, effect,
+    taint dictionary id)."""
+    out = []
+    if node is None:
+        return out
+    for t in api.spec(node).get("taints") or []:
+        k, v, e = t.get("key", "") or "", t.get("value", "") or "", t.get("effect", "") or ""
+        out.append((k, v, e, compiler.taints.get((k, v, e))))
+    return out
 
 
-def status_reasons(filters, nodes, pod, node_name, word):
-    """(code, plugin, reasons) of a node's device status word, formatted as the failing plugin
-    formats them; None for a feasible node.  filters: the profile's filter plugins in order;
-    nodes: name -> v1.Node."""
+def status_reasons(filters, compiler, nodes, pod, node_name, word, handle=None, node=-1, compiled=None):
+    """(code, plugin, reasons) of a node's device status word, None for a feasible node.  The reasons
+    come from libkgpu's kgpu_filter_reasons, the formatter the Go shim's Filter calls too, which
+    writes them exactly as the failing plugin does (file:line at each message in kgpu_reasons.h).
+    filters: the profile's filter plugins in order; nodes: name -> v1.Node; handle: the engine that
+    produced the word (None: pure formatting); node: the word's local node index; compiled: the pod's
+    (query, pools) when the caller holds them."""
     pos = word & 0xFF
-    if pos == 0:
+    if pos == 0 or word == abi.STATUS_NOT_EVALUATED:
         return None
     plugin = filters[pos - 1]
     code = (word >> 8) & 3
-    detail = word >> 16
-    if plugin == "NodeResourcesFit":  # fit.go:159-176, 194-267
-        res = api.PodResources(pod)
-        out = []
-        if detail & 1:
-            out.append("Too many pods")
-        for bit, r in ((2, "cpu"), (4, "memory"), (8, "ephemeral-storage")):
-            if detail & bit:
-                out.append("Insufficient " + r)
-        for i, r in enumerate(res.scalars):
-            if detail & (16 << min(i, 11)):
-                out.append("Insufficient " + r)
-        return code, plugin, out
-    if plugin == "TaintToleration":  # taint_toleration.go:54-72
-        from .compile import _tolerates
-        tols = api.spec(pod).get("tolerations") or []
-        for t in api.spec(nodes[node_name]).get("taints") or []:
-            if t.get("effect") not in ("NoSchedule", "NoExecute"):
-                continue
-            k, v, e = t.get("key", "") or "", t.get("value", "") or "", t.get("effect")
-            if not any(_tolerates(x, k, v, e) for x in tols):
-                return code, plugin, ["node(s) had taint {%s: %s}, that the pod didn't tolerate" % (k, v)]
-        return code, plugin, []
-    if plugin == "InterPodAffinity":
-        return code, plugin, list(IPA_REASONS.get(detail, []))
-    return code, plugin, [REASON[plugin]]
+    if compiled is None:
+        pools = Pools()
+        q = compiler.compile_pod(pod, pools)
+        pc, _ = pools.finalize()
+    else:
+        q, pc = compiled
+    reasons = native.filter_reasons(handle, q, pc, node, word, node_taints(compiler, nodes.get(node_name)),
+                                    compiler.scalar_names(pod),
+                                    filters=None if handle else [abi.FILTER_IDS[f] for f in filters])
+    return code, plugin, reasons
 
 
 class CycleResult:
@@ -147,8 +133,10 @@ class GpuFramework:
         return q, pc, pnp, errors
 
     # ------------------------------------------------------------------ reasons
-    def reasons(self, pod, node_name, word):
-        return status_reasons(self.filters, self.nodes, pod, node_name, word)
+    def reasons(self, pod, node_name, word, compiled=None, node=-1):
+        h = self.engine.h if self.engine is not None else None
+        return status_reasons(self.filters, self.compiler, self.nodes, pod, node_name, word, handle=h, node=node,
+                              compiled=compiled)
 
     # ------------------------------------------------------------------ cycles
     def cycle(self, pod, assume=False, seq=None):
@@ -166,7 +154,7 @@ class GpuFramework:
             if int(words[i]) == abi.STATUS_NOT_EVALUATED:
                 continue  # never examined: percentageOfNodesToScore stopped the search before it
             nm = self.order[self.snap.node_base + int(i)]
-            statuses[nm] = self.reasons(pod, nm, int(words[i]))
+            statuses[nm] = self.reasons(pod, nm, int(words[i]), compiled=(q[0], pc), node=int(i))
         scores = {}
         feas = np.nonzero(words == 0)[0]
         for name, w in self.profile.scores:

@@ -23,7 +23,7 @@ EXPORTS = ["kgpu_abi_version", "kgpu_struct_sizes", "kgpu_create", "kgpu_destroy
            "kgpu_comm_info",
            "kgpu_debug_fail_alloc", "kgpu_debug_pts_state", "kgpu_debug_ipa_state", "kgpu_debug_broken_linear",
            "kgpu_debug_wg_trace", "kgpu_debug_topo_resident",
-           "kgpu_next_slot", "kgpu_adopt_pod"]
+           "kgpu_next_slot", "kgpu_adopt_pod", "kgpu_filter_reasons"]
 
 
 class KgpuError(RuntimeError):
@@ -75,6 +75,7 @@ def lib():
     L.kgpu_adopt_pod.argtypes = [vp, i32, i64]
     L.kgpu_select_victims.argtypes = [vp, vp, C.POINTER(abi.Pools), C.POINTER(abi.PreemptArgs), vp, vp,
                                       C.POINTER(i32)]
+    L.kgpu_filter_reasons.argtypes = [vp, C.POINTER(abi.ReasonArgs), vp, i64, C.POINTER(i64)]
     if L.kgpu_abi_version() != abi.ABI_VERSION:
         raise KgpuError(abi.E_STATE, "ABI version mismatch")
     _lib = L
@@ -299,6 +300,35 @@ def comm_unique_id():
     if rc != 0:
         raise KgpuError(rc, "kgpu_comm_unique_id failed")
     return bytes(buf)
+
+
+def filter_reasons(handle, query, pools, node, word, taints, scalar_names, filters=None):
+    """kgpu_filter_reasons: the failing plugin's reasons for one node's status word, formatted by the
+    library.  handle: an engine context, or None with `filters` (the profile's KGPU_F_* order) for
+    pure formatting.  taints: the node's Spec.Taints as [(key, value, effect, dictionary id)] in spec
+    order; scalar_names: the resource name of each of the query's scalar requests, in order."""
+    q = np.ascontiguousarray(np.asarray(query, abi.QUERY).reshape(1))
+    tr = (abi.TaintRef * max(len(taints), 1))()
+    keep = []
+    for i, (k, v, e, tid) in enumerate(taints):
+        b = [x.encode() for x in (k, v, e)]
+        keep.append(b)
+        tr[i].key, tr[i].value, tr[i].effect, tr[i].id = b[0], b[1], b[2], int(tid)
+    names = (C.c_char_p * max(len(scalar_names), 1))(*[n.encode() for n in scalar_names])
+    fl = (C.c_int32 * max(len(filters or ()), 1))(*(filters or ()))
+    a = abi.ReasonArgs(q.ctypes.data, C.pointer(pools), int(node), int(word) & 0xFFFFFFFF, tr, len(taints),
+                       len(filters or ()), fl, names)
+    need = C.c_int64(0)
+    buf = C.create_string_buffer(512)
+    L = lib()
+    n = L.kgpu_filter_reasons(handle, C.byref(a), buf, len(buf), C.byref(need))
+    if n == abi.E_CAPACITY:
+        buf = C.create_string_buffer(need.value)
+        n = L.kgpu_filter_reasons(handle, C.byref(a), buf, len(buf), C.byref(need))
+    if n < 0:
+        msg = L.kgpu_last_error(handle) if handle else b""
+        raise KgpuError(n, (msg or b"kgpu_filter_reasons").decode())
+    return [x.decode() for x in buf.raw[:need.value].split(b"\0")[:n]]
 
 
 def debug_fail_alloc(countdown):

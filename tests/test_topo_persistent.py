@@ -19,7 +19,7 @@ def _big(seed, n_nodes=1500, n_existing=600, n_pods=80):
     return nodes, ex, pods, services, rss
 
 
-def _run(args, tfast=1, groups=0, threads=4, geo=None):
+def _run(args, tfast=1, groups=0, threads=4, geo=None, ahead=None):
     from oracle.cref import RefEngine
     nodes, ex, pods, services, rss = args
     fw = GpuFramework(Profile(), nodes, ex, cluster=Cluster(services=services, rss=rss), pods_hint=pods)
@@ -32,6 +32,8 @@ def _run(args, tfast=1, groups=0, threads=4, geo=None):
         fw.engine.set_option(abi.OPT_PERSIST_GROUPS, groups)
     if geo is not None:
         fw.engine.set_option(abi.OPT_TBATCH_GEO, geo)
+    if ahead is not None:
+        fw.engine.set_option(abi.OPT_TOPO_AHEAD, ahead)
     got, _ = fw.engine.schedule_batch(q, pc)
     return fw, w, got, want.read_nodes(), fw.engine.read_nodes(fw.snap.n_nodes)
 
@@ -57,6 +59,16 @@ def test_gpu_tbatch_random_matches_c_restatement(seed, groups):
 def test_gpu_tbatch_small_clusters(seed):
     """One workgroup, most lanes idle, every plugin input of gen_random.topo_cluster."""
     fw, w, got, rw, rg = _run(gen_random.topo_cluster(seed, n_nodes=40, n_existing=60, n_pods=60), tfast=1)
+    _check(w, got, rw, rg)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ahead", [0, 1])
+@pytest.mark.parametrize("seed", [2, 5])
+def test_gpu_tbatch_ahead_switch(seed, ahead):
+    """KGPU_OPT_TOPO_AHEAD 0 (every pod evaluated after the previous assume) and 1 (the next pod's
+    non-topology half evaluated while the statistics travel): both against the C restatement."""
+    fw, w, got, rw, rg = _run(_big(seed, n_nodes=900, n_existing=400, n_pods=60), tfast=1, ahead=ahead)
     _check(w, got, rw, rg)
 
 
