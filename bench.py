@@ -31,7 +31,11 @@ for p in (ROOT, os.path.join(ROOT, "kubernetes-1_amd")):
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md chip table)
 BYTES_PER_NODE_EVAL = {"b": 72, "a": 73, "c": 121, "d": 84, "e": 121}  # SURVEY.md 8(d) algorithmic bytes per node-eval
-BYTES_PER_EXISTING_POD = {"d": 24}  # IPA reads {node, ns, label bitset} per existing pod per pod
+BYTES_PER_EXISTING_POD = {"d": 24}
+# the plugin profile of each workload (kgpu/cluster.py): "default" = the default provider's filters and
+# scores (algorithmprovider/registry.go:92-133)
+PROFILES = {"a": "default", "b": "Fit+LeastAllocated+BalancedAllocation", "c": "default", "d": "default",
+            "e": "default"}  # IPA reads {node, ns, label bitset} per existing pod per pod
 
 
 def log(*a):
@@ -263,42 +267,47 @@ def measure(args, cfg, n_nodes_per_gpu, B, K, W, cpu_sample, cpu_threads, latenc
         host = host_info()
         rates = {}
         best = None
-        counts = cpu_thread_counts or sorted({1, cpu_threads, host["affinity_cpus"]})
+        counts = cpu_thread_counts or sorted({1, 4, 8, cpu_threads, host["affinity_cpus"]})
+        samples = {}
         for th in counts:
+            # one worker on a large cluster: a shorter sample (SINGLE_WORKER_SAMPLE pods), so the parallel
+            # efficiency of the baseline is in the line without a minute of CPU time
+            St = min(S, SINGLE_WORKER_SAMPLE) if th == 1 and n_local > 10000 else S
             ref = RefEngine(fw.config, fw.snap, threads=th)
             if len(q_init):
                 ref.schedule(q_init, pc)   # untimed, like the GPU's
             tc = time.perf_counter()
-            rres = ref.schedule(q[:S], pc, first_seq=len(q_init))
+            rres = ref.schedule(q[:St], pc, first_seq=len(q_init))
             tcpu = time.perf_counter() - tc
             ref.close()
-            ok = bool(np.array_equal(rres["node"], res_all["node"][:S]))
-            rates[str(th)] = round(S / tcpu, 2)
-            log("cpu baseline %s: %d thread(s): %.1f pods/s (placements %s)"
-                % (cfg, th, S / tcpu, "match" if ok else "DIFFER"))
-            if best is None or S / tcpu > best[0]:
-                best = (S / tcpu, th, tcpu, ok)
-        rate, th, tcpu, ok = best
+            ok = bool(np.array_equal(rres["node"], res_all["node"][:St]))
+            rates[str(th)] = round(St / tcpu, 2)
+            samples[str(th)] = St
+            log("cpu baseline %s: %d thread(s): %.1f pods/s over %d pods (placements %s)"
+                % (cfg, th, St / tcpu, St, "match" if ok else "DIFFER"))
+            if best is None or St / tcpu > best[0]:
+                best = (St / tcpu, th, tcpu, ok, St)
+        rate, th, tcpu, ok, St = best
         cpu = {"value": round(rate, 2), "unit": "pods/s", "cores": th, "kind": "port",
                "nproc": host["nproc"], "affinity_cpus": host["affinity_cpus"], "cpu_model": host["cpu_model"],
                "rates_by_threads": rates,
-               "sample": "C restatement (oracle/c) of the reference algorithm over %s (%d pods) of the same workload "
-                         "on a fresh snapshot, %.2fs at %d thread(s) (fastest of %s workers); placements %s the GPU's"
-                         % ("the whole workload" if S == n_pods else "the first %d pods" % S, S, tcpu, th,
-                            "/".join(sorted(rates, key=int)), "identical to" if ok else "DIFFERENT from")}
+               "sample": "oracle/c over %s %d pods, %.2fs at %d thread(s); placements %s"
+                         % ("all" if St == n_pods else "the first", St, tcpu, th, "match" if ok else "DIFFER")}
+        if len(set(samples.values())) > 1:
+            cpu["pods_by_threads"] = samples
 
     traffic = pmc_traffic(cfg, n_local, launch_pods, kname)
     rec = {
         "metric": "pods scheduled/sec", "value": round(pods_per_s, 2), "unit": "pods/s", "n_gpus": world,
         "steps": K, "warmup": W, "ms_per_step": round(1e3 * elapsed / K, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "int64", "data": "synthetic",
-        "config": {"workload": "config(%s): %d nodes / %d pods, %s" % (cfg, n_cluster, n_pods,
-                                                                        "+".join(prof.filters + [s for s, _ in prof.scores])),
+        "config": {"workload": "(%s) %d nodes / %d pods" % (cfg, n_cluster, n_pods), "profile": PROFILES[cfg],
                    "nodes": n_cluster, "nodes_per_gpu": fw.snap.n_nodes, "pods": n_pods, "pods_per_step": B,
                    "percentage_of_nodes_to_score": 100,
                    "parallelism": ("node shards x%d, %s" % (world, "granules through xGMI peer stores (persistent kernel)"
                                                               if xgmi else "RCCL all-gather per pod"))
                    if sharded else "1 GPU"},
+        "series": "%s:%d" % (cfg, n_nodes_per_gpu),
         "node_evals_per_s": round(pods_per_s * n_cluster, 1),
         "comm": comm,
         "placed": placed,
@@ -319,6 +328,10 @@ def measure(args, cfg, n_nodes_per_gpu, B, K, W, cpu_sample, cpu_threads, latenc
 
 
 DEFAULT_EXTRAS_1GPU = "b:100000,c:5000,d:5000,c:100000,d:100000,e:125000"
+# the workload every N of the driver's 1/2/4/8 sweep runs: config (e)'s 125k-node shard per GPU (an
+# extra record at N = 1, the headline at N > 1)
+SCALING_SERIES = ("e", 125000)
+SINGLE_WORKER_SAMPLE = 200
 DEFAULT_EXTRAS_NGPU = "b:5000"
 
 
@@ -469,9 +482,15 @@ def main():
         # workers (the reference's parallelize.Until width) up to 10k nodes, at 16 above
         recs.append(measure(args, xcfg, xn, args.pods_per_step, args.steps, args.warmup, args.extra_cpu_sample,
                             args.cpu_threads, args.latency_pods, rank, world, local, dist_on,
-                            cpu_thread_counts=[1, args.cpu_threads] if xn <= 10000 else [args.cpu_threads]))
+                            cpu_thread_counts=sorted({1, 4, 8, args.cpu_threads} if xn <= 10000 else
+                                                     {1, 8, args.cpu_threads})))
     if recs:
         line["extra"] = recs
+    # the record of the driver's 1/2/4/8 sweep's common workload (config (e)'s shard per GPU), by name
+    key = "%s:%d" % SCALING_SERIES
+    ser = [r for r in [line] + recs if r.get("series") == key]
+    line["scaling_series"] = {"series": key, "value": ser[0]["value"] if ser else None,
+                              "n_gpus": world, "unit": "pods/s"}
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist_on:

@@ -9,6 +9,7 @@
 #include <rccl/rccl.h>
 #include <dlfcn.h>
 #include <execinfo.h>
+#include <fcntl.h>
 #include <signal.h>
 #include <unistd.h>
 
@@ -3002,10 +3003,42 @@ int kgpu_struct_sizes(int32_t* out, int32_t n) {
 
 // KGPU_SEGV_TRACE=1 (diagnostics): a host SIGSEGV prints this library's native backtrace to stderr
 // before the default action (a Python faulthandler shows only the interpreter's frames).
-static void segv_trace(int sig) {
+// Each frame is printed with dladdr's library, symbol and offset from the library's load base, and the
+// /proc/self/maps line that holds it, so a fault inside another library's exit handler names that
+// library (diagnostics: formatting in a signal handler is not async-signal-safe).
+static void segv_maps_line(const void* addr) {
+  static char buf[1 << 17];
+  const int fd = open("/proc/self/maps", O_RDONLY);
+  if (fd < 0) return;
+  const ssize_t n = read(fd, buf, sizeof(buf) - 1);
+  close(fd);
+  if (n <= 0) return;
+  buf[n] = 0;
+  char* save = nullptr;
+  for (char* line = strtok_r(buf, "\n", &save); line; line = strtok_r(nullptr, "\n", &save)) {
+    unsigned long lo = 0, hi = 0;
+    if (std::sscanf(line, "%lx-%lx", &lo, &hi) == 2 && (unsigned long)addr >= lo && (unsigned long)addr < hi) {
+      std::fprintf(stderr, "      maps: %s\n", line);
+      return;
+    }
+  }
+}
+
+static void segv_trace(int sig, siginfo_t* si, void*) {
   void* fr[64];
   const int n = backtrace(fr, 64);
-  backtrace_symbols_fd(fr, n, 2);
+  std::fprintf(stderr, "kgpu: signal %d, fault address %p, %d frames\n", sig, si ? si->si_addr : nullptr, n);
+  for (int i = 0; i < n; ++i) {
+    Dl_info d{};
+    if (dladdr(fr[i], &d) && d.dli_fname)
+      std::fprintf(stderr, "  #%d %p %s (%s+0x%lx) load base %p, offset 0x%lx\n", i, fr[i], d.dli_fname,
+                   d.dli_sname ? d.dli_sname : "?",
+                   d.dli_saddr ? (unsigned long)((const char*)fr[i] - (const char*)d.dli_saddr) : 0ul, d.dli_fbase,
+                   (unsigned long)((const char*)fr[i] - (const char*)d.dli_fbase));
+    else
+      std::fprintf(stderr, "  #%d %p (no library)\n", i, fr[i]);
+    segv_maps_line(fr[i]);
+  }
   signal(sig, SIG_DFL);
   raise(sig);
 }
@@ -3013,7 +3046,12 @@ static void segv_trace(int sig) {
 int kgpu_create(const kgpu_config* cfg, kgpu_ctx** out) try {
   if (!cfg || !out) return KGPU_E_INVAL;
   if (const char* e = std::getenv("KGPU_SEGV_TRACE"))
-    if (e[0] == '1') signal(SIGSEGV, segv_trace);
+    if (e[0] == '1') {
+      struct sigaction sa {};
+      sa.sa_sigaction = segv_trace;
+      sa.sa_flags = SA_SIGINFO;
+      sigaction(SIGSEGV, &sa, nullptr);
+    }
   *out = nullptr;
   if (cfg->abi_version != KGPU_ABI_VERSION) return KGPU_E_INVAL;
   if (kgpu::kernel_layout_sig() != kgpu::layout_sig_of()) return KGPU_E_STATE;  // mixed-revision build

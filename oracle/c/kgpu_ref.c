@@ -20,6 +20,8 @@
  * atomic counter; DESIGN.md "Determinism contract").  Build: oracle/c/Makefile.
  */
 #include <math.h>
+#include <stdio.h>
+#include <time.h>
 #include <pthread.h>
 #include <sched.h>
 #include <stdatomic.h>
@@ -1096,6 +1098,7 @@ typedef struct {
   int phase; /* 0 filter, 1 score */
   int n, chunk;
   _Atomic int next;
+  _Atomic int done;  /* items processed (parallel_until's join) */
   uint32_t* status;
   const int* feasible;
   int nf;
@@ -1134,12 +1137,24 @@ static void process(work_t* w, int i) {
 /* A persistent pool of (threads - 1) workers plus the calling thread.  Go's ParallelizeUntil
  * starts 16 goroutines per call and hands out chunks through a channel; goroutine start and
  * channel receive cost well under a microsecond, so a faithful (and strong) baseline must not pay
- * an OS sleep/wake per parallel section.  Workers therefore spin on a generation word (yielding
- * after a bounded spin) and take chunks with an atomic fetch-add; the caller spins on the busy
- * count.  A condition-variable pool measured 2.7x SLOWER at 16 threads than 1 thread on 5k nodes
- * (two futex wake-ups of 15 threads per pod dominate a 70 us cycle). */
+ * an OS sleep/wake per parallel section.  Workers therefore spin on a sequence word (yielding
+ * after a bounded spin) and take chunks with an atomic fetch-add.  A condition-variable pool
+ * measured 2.7x SLOWER at 16 threads than 1 thread on 5k nodes (two futex wake-ups of 15 threads
+ * per pod dominate a 70 us cycle).
+ *
+ * The join waits for the ITEMS, not for the workers: until round 4 the caller waited for every
+ * worker to check in, so one worker the OS had descheduled (16 spinning threads on a 16-CPU share
+ * beside the interpreter's and the runtime's threads) held the whole section for a scheduler quantum
+ * even when it took no chunk -- the reason 16 workers were slower than one at 5k nodes
+ * (KGPU_REF_PHASES: the filter section 63 us at 1 thread, 1.3 ms at 8).  Now:
+ *   seq is odd while a job is open (2k+1) and even after it (2k+2);
+ *   a worker that sees an open job registers in `active`, then re-checks seq: only if the job is
+ *   still open does it touch the job, else it unregisters;
+ *   the caller, once every item is done, closes the job (seq + 1) and waits for `active` to drain --
+ *   only workers already inside run_chunks, each of which finds no chunk left. */
 struct pool_s {
-  _Atomic int gen, busy, quit;
+  _Atomic long seq;
+  _Atomic int active, quit;
   work_t* _Atomic job;
   int nthreads;
   pthread_t tid[256];
@@ -1151,21 +1166,25 @@ static void run_chunks(work_t* w) {
     if (start >= w->n) return;
     int end = start + w->chunk < w->n ? start + w->chunk : w->n;
     for (int i = start; i < end; ++i) process(w, i);
+    atomic_fetch_add_explicit(&w->done, end - start, memory_order_release);
   }
 }
 
 static void* pool_worker(void* arg) {
   pool_t* p = (pool_t*)arg;
-  int seen = 0;
+  long seen = 0;
   for (;;) {
     int spins = 0;
-    while (atomic_load_explicit(&p->gen, memory_order_acquire) == seen) {
+    long s;
+    while ((s = atomic_load_explicit(&p->seq, memory_order_acquire)) == seen || !(s & 1)) {
       if (atomic_load_explicit(&p->quit, memory_order_relaxed)) return NULL;
       if (++spins > 4096) { sched_yield(); spins = 0; }
     }
-    seen = atomic_load_explicit(&p->gen, memory_order_acquire);
-    run_chunks(atomic_load_explicit(&p->job, memory_order_acquire));
-    atomic_fetch_sub_explicit(&p->busy, 1, memory_order_release);
+    seen = s;
+    atomic_fetch_add_explicit(&p->active, 1, memory_order_seq_cst);
+    if (atomic_load_explicit(&p->seq, memory_order_seq_cst) == s)
+      run_chunks(atomic_load_explicit(&p->job, memory_order_acquire));
+    atomic_fetch_sub_explicit(&p->active, 1, memory_order_release);
   }
 }
 
@@ -1191,15 +1210,19 @@ static void parallel_until(pool_t* pool, work_t* w, int n) {
   w->n = n;
   w->chunk = chunk;
   atomic_store_explicit(&w->next, 0, memory_order_relaxed);
+  atomic_store_explicit(&w->done, 0, memory_order_relaxed);
   if (!pool || pool->nthreads <= 1 || n < 2) {
     for (int i = 0; i < n; ++i) process(w, i);
     return;
   }
   atomic_store_explicit(&pool->job, w, memory_order_relaxed);
-  atomic_store_explicit(&pool->busy, pool->nthreads - 1, memory_order_relaxed);
-  atomic_fetch_add_explicit(&pool->gen, 1, memory_order_release);
+  const long open = atomic_load_explicit(&pool->seq, memory_order_relaxed) + 1;  /* odd: job open */
+  atomic_store_explicit(&pool->seq, open, memory_order_seq_cst);
   run_chunks(w);
-  while (atomic_load_explicit(&pool->busy, memory_order_acquire) > 0) {
+  while (atomic_load_explicit(&w->done, memory_order_acquire) < n) {
+  }
+  atomic_store_explicit(&pool->seq, open + 1, memory_order_seq_cst);  /* closed: late workers stay out */
+  while (atomic_load_explicit(&pool->active, memory_order_acquire) > 0) {
   }
 }
 
@@ -1236,7 +1259,20 @@ int kgpu_ref_schedule(ref_state* r, const kgpu_pod_query* qs, int nq, const kgpu
   int* feasible = (int*)malloc(sizeof(int) * (N ? N : 1));
   int64_t* scores = (int64_t*)malloc(sizeof(int64_t) * (size_t)(N ? N : 1) * (r->cfg.n_scores ? r->cfg.n_scores : 1));
   int64_t* totals = (int64_t*)malloc(sizeof(int64_t) * (N ? N : 1));
+  /* KGPU_REF_PHASES=1: wall time per pod of each phase to stderr (where a parallel baseline's time goes) */
+  const int phases = getenv("KGPU_REF_PHASES") != NULL;
+  double ph[5] = {0, 0, 0, 0, 0};
+  struct timespec t0, t1;
+#define PHASE(k)                                                                                       \
+  do {                                                                                                 \
+    if (phases) {                                                                                      \
+      clock_gettime(CLOCK_MONOTONIC, &t1);                                                             \
+      ph[k] += (double)(t1.tv_sec - t0.tv_sec) * 1e6 + (double)(t1.tv_nsec - t0.tv_nsec) / 1e3;       \
+      t0 = t1;                                                                                         \
+    }                                                                                                  \
+  } while (0)
   for (int qi = 0; qi < nq; ++qi) {
+    if (phases) clock_gettime(CLOCK_MONOTONIC, &t0);
     const kgpu_pod_query* q = &qs[qi];
     work_t w;
     memset(&w, 0, sizeof(w));
@@ -1250,7 +1286,9 @@ int kgpu_ref_schedule(ref_state* r, const kgpu_pod_query* qs, int nq, const kgpu
     if (has_filter(r, KGPU_F_POD_TOPOLOGY_SPREAD)) pts_prefilter(&qst, r, p, q);
     if (has_filter(r, KGPU_F_INTER_POD_AFFINITY)) ipa_prefilter(&qst, r);
     w.qs = &qst;
+    PHASE(0);
     parallel_until((pool_t*)r->pool, &w, N);
+    PHASE(1);
     int nf = 0;
     int evaluated = r->total;
     if (r->to_find < N && r->total == N) {
@@ -1307,7 +1345,9 @@ int kgpu_ref_schedule(ref_state* r, const kgpu_pod_query* qs, int nq, const kgpu
         w.feasible = feasible;
         w.nf = nf;
         w.scores = scores;
+        PHASE(2);
         parallel_until((pool_t*)r->pool, &w, nf);
+        PHASE(3);
         for (int i = 0; i < nf; ++i) totals[i] = 0;
         for (int k = 0; k < r->cfg.n_scores; ++k) {
           int64_t* s = scores + (size_t)k * nf;
@@ -1339,6 +1379,7 @@ int kgpu_ref_schedule(ref_state* r, const kgpu_pod_query* qs, int nq, const kgpu
         res.score = totals[bi];
         add_pod(r, p, q, feasible[bi]);
         add_pod_record(r, q, p, feasible[bi]);
+        PHASE(4);
       }
     }
     qstate_free(&qst, r);
@@ -1348,6 +1389,11 @@ int kgpu_ref_schedule(ref_state* r, const kgpu_pod_query* qs, int nq, const kgpu
   free(feasible);
   free(scores);
   free(totals);
+  if (phases && nq > 0)
+    fprintf(stderr, "kgpu_ref %d thread(s), us/pod: prefilter %.1f, filter (parallel) %.1f, feasible list %.1f, "
+            "score (parallel) %.1f, normalize+totals+selectHost+assume %.1f\n", r->threads, ph[0] / nq, ph[1] / nq,
+            ph[2] / nq, ph[3] / nq, ph[4] / nq);
+#undef PHASE
   return 0;
 }
 
