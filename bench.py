@@ -150,8 +150,8 @@ def measure(args, cfg, n_nodes_per_gpu, B, K, W, cpu_sample, cpu_threads, latenc
     eng = fw.engine
     if args.no_persistent:
         eng.set_option(abi.OPT_PERSISTENT, 0)
-    if args.no_coop:
-        eng.set_option(abi.OPT_COOPERATIVE, 0)
+    if args.coop:
+        eng.set_option(abi.OPT_COOPERATIVE, 1)
     if args.batch_geo is not None:
         eng.set_option(abi.OPT_BATCH_GEO, args.batch_geo)
     if args.batch_helper is not None:
@@ -442,8 +442,10 @@ def main():
                     help="KGPU_OPT_TBATCH_GEO (smallest k_tbatch geometry index; 0 = 256 threads x 1 row)")
     ap.add_argument("--batch-geo", type=int, default=None,
                     help="smallest k_batch geometry index considered (KGPU_OPT_BATCH_GEO; 0 = 64 row threads)")
-    ap.add_argument("--no-coop", action="store_true",
-                    help="KGPU_OPT_COOPERATIVE = 0: ordinary launches of the persistent kernels (profiling runs)")
+    ap.add_argument("--coop", action="store_true",
+                    help="KGPU_OPT_COOPERATIVE = 1: every persistent launch through hipLaunchCooperativeKernel "
+                         "(default: ordinary launches of a co-resident grid)")
+    ap.add_argument("--no-coop", action="store_true", help=argparse.SUPPRESS)  # the default since round 5
     ap.add_argument("--os-exit", action="store_true",
                     help="leave through os._exit(0) after printing (profiling runs: see DESIGN.md, rocprofv3 exit)")
     ap.add_argument("--probe-launch", action="store_true",

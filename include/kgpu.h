@@ -587,10 +587,14 @@ int kgpu_read_nodes(kgpu_ctx* ctx, int64_t* req_cpu, int64_t* req_mem, int64_t* 
  * the next pod's wait on it times out (the path a lost LDS release would take): the batch fails with
  * KGPU_E_DEVICE and the mirror is invalidated (-1, the default: never). */
 #define KGPU_OPT_SKIP_RELEASE_AT 9
-/* KGPU_OPT_COOPERATIVE (10): 1 (default) = persistent kernels go through hipLaunchCooperativeKernel,
- * which refuses a grid that cannot be co-resident; 0 = an ordinary launch of the same grid (one
- * workgroup per CU on an idle device; a workgroup that never starts turns into KGPU_E_DEVICE through
- * the spin timeouts).  For tools whose exit path faults after cooperative launches (rocprofv3). */
+/* KGPU_OPT_COOPERATIVE (10): 0 (default) = the persistent kernels go out as ordinary launches of a grid
+ * the engine sized to be co-resident (at most one workgroup per CU: an LDS reservation above half a CU,
+ * and an occupancy query per kernel instantiation at its first launch); 1 = every persistent launch goes
+ * through hipLaunchCooperativeKernel (+15-19 us of host time per launch, MI355X_MICROARCH.md coop-launch).
+ * A workgroup that does not start on time makes the others' spins time out: when that happens before the
+ * run resolved its first pod, nothing on the device changed, and a call whose only state-changing launch
+ * was that run is issued again once with a cooperative launch (kgpu_debug_counters out[0]); any later
+ * abort fails the call with KGPU_E_DEVICE and invalidates the mirror. */
 #define KGPU_OPT_COOPERATIVE 10
 /* KGPU_OPT_BATCH_GEO (11): the smallest k_batch geometry considered (index into the geometry table
  * of kgpu_kernels.hip: 0 = 64 row threads, 1 = 128, 2 = 192, 3 = 448, 4 = 960, 5 = 512 x 4 rows per
@@ -618,7 +622,14 @@ int kgpu_read_nodes(kgpu_ctx* ctx, int64_t* req_cpu, int64_t* req_mem, int64_t* 
  * threads x 1 row per lane, 1 = 512 x 1, 2 = 512 x 2); the first whose workgroups fit the GPU is used.
  * Default 1 (256 x 1 measured equal at 5k nodes, with twice the exchange traffic). */
 #define KGPU_OPT_TBATCH_GEO 16
+/* KGPU_OPT_HOLD_GROUP (17): test hook -- on an ordinary (non-cooperative) persistent launch, workgroup
+ * `value` leaves at once, as a workgroup that never became resident (-1, the default: none). */
+#define KGPU_OPT_HOLD_GROUP 17
 int kgpu_set_option(kgpu_ctx* ctx, int32_t option, int64_t value);
+/* Engine counters: out[0] = calls issued again with a cooperative launch after a persistent run's
+ * workgroups were not all resident before its first pod (KGPU_OPT_COOPERATIVE); out[1] = persistent
+ * launches; out[2] = cooperative persistent launches.  Returns how many counters exist. */
+int kgpu_debug_counters(const kgpu_ctx* ctx, int64_t* out, int32_t n);
 /* Diagnostics of KGPU_OPT_TOPO_RESIDENT: out[0] = persistent topology runs that started from the
  * resident state, out[1] = runs that recomputed it. */
 int kgpu_debug_topo_resident(const kgpu_ctx* ctx, int64_t out[2]);

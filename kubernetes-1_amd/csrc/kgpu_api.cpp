@@ -256,7 +256,12 @@ struct kgpu_ctx {
   int64_t max_key_values = 1;
   // persistent topology runs (k_tbatch)
   bool tfast = true;                // KGPU_OPT_TOPO_PERSISTENT
-  bool coop = true;                 // KGPU_OPT_COOPERATIVE
+  bool coop = false;                // KGPU_OPT_COOPERATIVE (ordinary launches of a co-resident grid)
+  bool force_coop = false;          // a call issued again after a clean abort (every persistent launch
+                                    // of it cooperative)
+  int32_t hold_group = -1;          // KGPU_OPT_HOLD_GROUP test hook
+  int64_t n_coop_retry = 0, n_persist = 0, n_coop = 0;  // kgpu_debug_counters
+  int state_launches = 0;           // launches of the current call that may change device state
   int batch_geo_first = 0;          // KGPU_OPT_BATCH_GEO
   DevBuf t_tables, t_zero, abort_buf;
   kgpu::HostStage table_stage;   // pinned staging of the runs' tables (bump-allocated, wraps after a sync)
@@ -1646,12 +1651,16 @@ int run_tbatch(kgpu_ctx* c, TRun& tr, int first, int count, int64_t first_seq, i
     x.abort = abort_word;
     if (kgpu::launch_xreduce(x, c->stream)) return fail(c, KGPU_E_DEVICE, "cross-rank histogram reduction launch failed");
   }
-  // A one-pod run (a kgpu_schedule_one cycle) launches as an ordinary dispatch: the cooperative
-  // launch's residency check costs the cycle tens of microseconds of host wall time (the synchronize
-  // returned 57 us after the launch against a 24 us run), and the grid -- at most one workgroup per
-  // CU (the LDS reservation), at most 256 -- is resident on an idle device either way; were it not,
-  // the spin timeouts raise the abort word instead of hanging.
-  const bool coop = c->coop && !(count == 1 && !xg);
+  // Ordinary dispatch unless KGPU_OPT_COOPERATIVE (or the retry of a clean abort) asks otherwise: the
+  // cooperative launch's residency check costs tens of microseconds of host wall time (a one-pod run's
+  // synchronize returned 57 us after the launch against a 24 us run), and the grid -- at most one
+  // workgroup per CU (the LDS reservation), at most 256 -- is resident on an idle device either way;
+  // were it not, the spin timeouts raise the abort word instead of hanging.
+  const bool coop = (c->coop && !(count == 1 && !xg)) || c->force_coop;
+  a.hold = coop ? -1 : c->hold_group;
+  ++c->n_persist;
+  c->n_coop += coop ? 1 : 0;
+  ++c->state_launches;
   if (kgpu::launch_tbatch(dst, a, groups, geo, c->spec, xg, coop, c->stream))
     return fail(c, KGPU_E_DEVICE, std::string("k_tbatch launch failed: ") + hipGetErrorString(hipGetLastError()));
   if (c->ar.on) ht(c, 7);  // 7: the launch (API call)
@@ -1874,7 +1883,14 @@ int stage_topology(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_
 }
 
 int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools* pools, int64_t first_seq,
-              kgpu_result* results, kgpu_stats* stats, bool diag, int32_t assume) {
+              kgpu_result* results, kgpu_stats* stats, bool diag, int32_t assume);
+
+// internal: run_batch_once's persistent run aborted before resolving any pod and was the call's only
+// state-changing launch (never returned to a caller)
+constexpr int kCleanAbort = 1000;
+
+int run_batch_once(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools* pools, int64_t first_seq,
+                   kgpu_result* results, kgpu_stats* stats, bool diag, int32_t assume) {
   if (!c->uploaded) return fail(c, KGPU_E_STATE, "no snapshot uploaded");
   if (n <= 0) return KGPU_OK;
   int rc;
@@ -2099,6 +2115,7 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
     }
     if ((rc = arena_flush(c))) return rc;  // every other launch reads DevState / queries / pools from it
     c->tc.valid = false;                     // ... and may assume outside a persistent topology run
+    ++c->state_launches;
     if (topo[(size_t)i]) {
       if ((rc = zero_diag_rows())) return rc;
       const kgpu::QPlan& pl = plans[(size_t)i];
@@ -2235,7 +2252,12 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
         c->trace_host.assign((size_t)(cnt + 1) * 16, 0);
       }
       if (c->timing) HIP_OK(c, hipEventRecord(get_event(c, ev), c->stream));
-      if (kgpu::launch_batch(dst, ba, groups, kidx, c->spec, c->coop, c->batch_helper, c->stream))
+      const bool coop = c->coop || c->force_coop;
+      ba.hold = coop ? -1 : c->hold_group;
+      ++c->n_persist;
+      c->n_coop += coop ? 1 : 0;
+      ++c->state_launches;
+      if (kgpu::launch_batch(dst, ba, groups, kidx, c->spec, coop, c->batch_helper, c->stream))
         return fail(c, KGPU_E_DEVICE, "k_batch launch failed");
       if (c->timing) HIP_OK(c, hipEventRecord(get_event(c, ev + 1), c->stream));
       ev += 2;
@@ -2270,6 +2292,7 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
           a.q = qs[k];
         }
         if ((rc = zero_diag_rows())) return rc;
+        ++c->state_launches;
         if (c->timing) HIP_OK(c, hipEventRecord(get_event(c, ev), c->stream));
         if (nom_dev && kgpu::launch_victims(dst, nom_dev, st.N, c->stream))
           return fail(c, KGPU_E_DEVICE, "k_victims launch failed");
@@ -2315,7 +2338,15 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
     // k_tbatch's last workgroup wrote the abort word (-1 left by the host: the run never finished)
     const int32_t w = __atomic_load_n(reinterpret_cast<int32_t*>(static_cast<char*>(c->res_pin) + kCycAbortOff),
                                       __ATOMIC_ACQUIRE);
-    c->abort_host = w != 0 ? 1 : 0;
+    c->abort_host = w == -1 ? kgpu::kAbortDirty : w;
+  }
+  if (used_persistent && c->abort_host == kgpu::kAbortClean && c->state_launches == 1 && !c->force_coop && !xg) {
+    // A workgroup never started before the run resolved its first pod, and that run was the call's
+    // only state-changing launch: nothing on the device changed.  The resident topology state's spare
+    // buffer may be half zeroed: both buffers are recomputed from zeros by the next run.
+    c->tc.valid = false;
+    for (int k = 0; k < 2; ++k) c->tc.dirty[k] = c->tc.buf[k].bytes;
+    return kCleanAbort;
   }
   c->port_bound += batch_ports;
   if (port_overflow) {
@@ -2975,6 +3006,27 @@ int assume_via_delta(kgpu_ctx* c, const kgpu_pod_query& q, const kgpu_pools* poo
                     (int)r.ports.size());
 }
 
+// One scheduling call.  Its persistent kernels go out as ordinary launches; when a run's workgroups were
+// not all resident before it resolved its first pod and nothing else of the call touched the device
+// (kCleanAbort), the call is issued once more with cooperative launches, which wait for the whole grid
+// (KGPU_OPT_COOPERATIVE, ADVICE r4: transient contention no longer forces a full re-upload).
+int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools* pools, int64_t first_seq,
+              kgpu_result* results, kgpu_stats* stats, bool diag, int32_t assume) {
+  c->state_launches = 0;
+  int rc = run_batch_once(c, qs, n, pools, first_seq, results, stats, diag, assume);
+  if (rc != kCleanAbort) return rc;
+  ++c->n_coop_retry;
+  c->force_coop = true;
+  c->state_launches = 0;
+  rc = run_batch_once(c, qs, n, pools, first_seq, results, stats, diag, assume);
+  c->force_coop = false;
+  if (rc == kCleanAbort) {  // unreachable: a forced cooperative call never reports a clean abort
+    c->uploaded = false;
+    return fail(c, KGPU_E_DEVICE, "persistent run aborted twice before its first pod");
+  }
+  return rc;
+}
+
 }  // namespace
 
 extern "C" {
@@ -3208,6 +3260,13 @@ int kgpu_read_phase_trace(kgpu_ctx* c, int64_t* out, int32_t max_pods) try {
   return on_exception(c, false);
 }
 
+int kgpu_debug_counters(const kgpu_ctx* c, int64_t* out, int32_t n) {
+  if (!c || (n > 0 && !out)) return KGPU_E_INVAL;
+  const int64_t v[3] = {c->n_coop_retry, c->n_persist, c->n_coop};
+  for (int32_t i = 0; i < n && i < 3; ++i) out[i] = v[i];
+  return 3;
+}
+
 int kgpu_debug_topo_resident(const kgpu_ctx* c, int64_t out[2]) {
   if (!c || !out) return KGPU_E_INVAL;
   out[0] = (int64_t)c->tc_hits;
@@ -3244,6 +3303,7 @@ int kgpu_set_option(kgpu_ctx* c, int32_t option, int64_t value) try {
   } else if (option == KGPU_OPT_ARENA_BYTES) c->ar_limit = (size_t)std::min<int64_t>(std::max<int64_t>(0, value), (int64_t)kArenaBytes);
   else if (option == KGPU_OPT_ABORT_AT) c->abort_at = value < 0 || value > INT32_MAX ? -1 : (int32_t)value;
   else if (option == KGPU_OPT_XGMI) c->xgmi = value != 0;
+  else if (option == KGPU_OPT_HOLD_GROUP) c->hold_group = value < 0 || value > INT32_MAX ? -1 : (int32_t)value;
   else if (option == KGPU_OPT_SKIP_RELEASE_AT) c->skip_release_at = value < 0 || value > INT32_MAX ? -1 : (int32_t)value;
   else return KGPU_E_INVAL;
   return KGPU_OK;

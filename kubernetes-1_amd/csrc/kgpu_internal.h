@@ -252,7 +252,9 @@ struct BatchArgs {
   int64_t seq0;         // tie-break sequence number of query `first`
   uint64_t* gran;       // [count][groups] granules, zeroed before the launch
   int32_t* feas;        // [count][groups] feasible count of each published variant
-  int32_t* abort;       // raised (1) by a workgroup that lost co-residency; zeroed before the launch
+  int32_t* abort;       // zeroed before the launch; OR-ed by a workgroup whose spin gave up: 2 (kAbortClean)
+                        // before the run resolved any pod -- no device state changed, the call may be
+                        // issued again -- else 1
   int64_t* trace;        // null, or [count + 1][16] s_memrealtime stamps, 8 per traced workgroup
                         // (0 and last): iteration start, evaluated, previous pod resolved,
                         // granule published, iteration end
@@ -261,6 +263,9 @@ struct BatchArgs {
   int32_t skip_release_at;  // KGPU_OPT_SKIP_RELEASE_AT test hook: at this iteration the candidate lane
                             // stages its row but never releases the hand-off, so the next pod's LDS
                             // wait times out (-1: never)
+  int32_t hold;         // KGPU_OPT_HOLD_GROUP test hook: this workgroup leaves at once (an ordinary launch
+                        // whose workgroup never became resident; -1: none)
+  int32_t pad_h;
   // Node sharding over xGMI (kgpu_xgmi_init): every workgroup of every rank publishes its granule
   // and feasible count into every rank's mailbox ring; each rank polls its own.  Unsharded:
   // nranks 1, pgran[0] = gran, pfeas[0] = feas, GT = groups, R = 0 (rows are this launch's pods,
@@ -274,6 +279,9 @@ struct BatchArgs {
   int32_t R;               // ring rows, 0 = linear rows
   int64_t xseq0;
 };
+// abort word codes (OR-ed): a spin gave up before the run resolved its first pod (nothing on the device
+// changed) / after it
+constexpr int32_t kAbortDirty = 1, kAbortClean = 2;
 constexpr int kXgmiRing = 4096;      // mailbox ring rows (a persistent run holds at most half)
 constexpr int kXgmiMaxGT = 1024;     // granules per row the poll sweeps (16 per lane)
 
@@ -403,7 +411,7 @@ struct TBatchArgs {
                           // k_tbatch_init pass (kgpu_api.cpp TCache)
   int32_t zero_n16;       // the other resident-state buffer: its first zero_n16 16-byte words are zeroed by
                           // the grid at kernel entry, so the next miss starts from zeros without a memset
-  int32_t pad_z;
+  int32_t hold;           // KGPU_OPT_HOLD_GROUP test hook, as in BatchArgs
   struct alignas(16) Z16 { uint64_t lo, hi; };
   Z16* zero_buf;
   int64_t* trace;        // null, or [count + 1][16] s_memrealtime stamps (KGPU_OPT_PHASE_TRACE): per pod

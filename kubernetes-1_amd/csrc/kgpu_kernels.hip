@@ -32,6 +32,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <map>
+#include <mutex>
+#include <tuple>
 
 #include "kgpu_internal.h"
 
@@ -1442,6 +1445,7 @@ __global__ __launch_bounds__(B + 64 + (HB ? 2 * B : 0)) void k_batch(const DevSt
   constexpr int W = B / 64;  // row waves; wave W communicates; HB: waves W + 1, W + 2 help row wave 0
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int G = gridDim.x, g = blockIdx.x;
+  if (g == pa.hold) return;  // KGPU_OPT_HOLD_GROUP: a workgroup that never became resident
   const int lo = g * pa.per;
   const int GT = pa.GT, gme = pa.rank * G + g;  // this workgroup's granule in every row
   constexpr bool xg = XG;                       // xGMI mailbox ring (node-sharded run)
@@ -1639,7 +1643,9 @@ __global__ __launch_bounds__(B + 64 + (HB ? 2 * B : 0)) void k_batch(const DevSt
           gp(st.results)[pa.first + i - 1] = res;
         }
       } else if (lane == 0) {
-        __hip_atomic_store(pa.abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // pod 0's granules never came (i == 1): no workgroup resolved a pod of this run
+        __hip_atomic_fetch_or(pa.abort, (i <= 1 && !XG) ? kAbortClean : kAbortDirty, __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_AGENT);
       }
       if (lane == 0 && have_prev) {
         sh.rwg[(i - 1) & 1] = wg;
@@ -3153,6 +3159,21 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
   constexpr int W = B / 64;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int G = gridDim.x, g = blockIdx.x;
+  // every workgroup leaves through here, aborted or not (the pod loop only breaks): the last one to
+  // leave copies the run's abort word into the caller's pinned block
+  auto leave = [&]() {
+    if (ta.abort_out && tid == 0) {
+      __threadfence();
+      if (atomicAdd(ta.done, 1) == G - 1) {
+        __threadfence();
+        __hip_atomic_store(ta.abort_out, load_sc1(ta.abort), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+  };
+  if (g == ta.hold) {  // KGPU_OPT_HOLD_GROUP: a workgroup that never became resident
+    leave();
+    return;
+  }
   const int lo = g * ta.per;
   // run stamps (KGPU_OPT_PHASE_TRACE) in the trace's spare last row: entry, pod loop start, exit
   const bool trun = ta.trace && tid == 0 && (g == 0 || g == G - 1);
@@ -3609,8 +3630,10 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
         if (lane == 0) STAT[rr] = x;
       }
     }
+    // pod 0's statistics never came: no workgroup resolved a pod of this run
+    const int32_t acode = (i == 0 && !XG) ? kAbortClean : kAbortDirty;
     if (!ok && lane == 0) {
-      __hip_atomic_store(ta.abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_or(ta.abort, acode, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       M.abort = 1;
     }
     __syncthreads();
@@ -3701,7 +3724,7 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
         }
       } else if (lane == 0) {
         if (!pok) {
-          __hip_atomic_store(ta.abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_fetch_or(ta.abort, acode, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           M.abort = 1;
         }
         M.wkey = wkey;
@@ -3809,15 +3832,7 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
     for (int h = tid; h < ta.n_hists; h += B) gp(ta.tot_init)[h] = TOT[h];
   }
   if (trun) trun_row[2] = (int64_t)__builtin_amdgcn_s_memrealtime();
-  // every workgroup gets here, aborted or not (the pod loop only breaks): the last one to leave
-  // copies the run's abort word into the caller's pinned block
-  if (ta.abort_out && tid == 0) {
-    __threadfence();
-    if (atomicAdd(ta.done, 1) == G - 1) {
-      __threadfence();
-      __hip_atomic_store(ta.abort_out, load_sc1(ta.abort), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  }
+  leave();
 }
 
 // ---------------------------------------------------------------- cross-rank init reduction
@@ -3936,6 +3951,27 @@ int tbatch_geometry(int N, int max_groups, int* per, int* groups, int first) {
   return -1;
 }
 
+// An ordinary launch of a persistent grid is only as good as its residency: the grid must fit the GPU at
+// once (MI355X_MICROARCH.md coop-launch: a plain launch of a grid the cooperative check would accept has
+// the same residency).  Queried once per kernel instantiation and block shape; false sends the launch
+// through hipLaunchCooperativeKernel, which refuses a grid that cannot be co-resident.
+static bool grid_fits(const void* fn, int threads, size_t lds, int groups) {
+  static std::mutex mu;
+  static std::map<std::tuple<const void*, int, size_t>, int> cap;  // workgroups the device holds at once
+  std::lock_guard<std::mutex> lock(mu);
+  auto key = std::make_tuple(fn, threads, lds);
+  auto it = cap.find(key);
+  if (it == cap.end()) {
+    int per_cu = 0, dev = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, threads, lds) != hipSuccess) per_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 0;
+    it = cap.emplace(key, per_cu * cus).first;
+  }
+  return groups <= it->second;
+}
+
 int launch_tbatch_init(const DevState* st, const TBatchArgs& a, int groups, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const int N = a.per * groups;  // >= st->N
@@ -3966,10 +4002,11 @@ int launch_tbatch(const DevState* st, const TBatchArgs& a, int groups, int geo, 
   TBatchArgs arg = a;
   const DevState* sp = st;
   void* args[] = {(void*)&sp, (void*)&arg};
-  if (!coop) {  // KGPU_OPT_COOPERATIVE off: as launch_batch
+  if (!coop && grid_fits(reinterpret_cast<const void*>(fn), kTGeo[geo].B, (size_t)a.lds_bytes, groups)) {
     hipLaunchKernelGGL(fn, dim3(groups), dim3(kTGeo[geo].B), (unsigned)a.lds_bytes, s, sp, arg);
     return hipGetLastError() == hipSuccess ? 0 : -1;
   }
+  arg.hold = -1;
   return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(fn), dim3(groups), dim3(kTGeo[geo].B), args,
                                     (unsigned)a.lds_bytes, s) == hipSuccess
              ? 0
@@ -4097,12 +4134,14 @@ int launch_batch(const DevState* st, const BatchArgs& a, int groups, int geo, in
   // (coop false, KGPU_OPT_COOPERATIVE: an ordinary launch of the same grid -- at most one workgroup per
   // CU on an otherwise idle device, so every workgroup is resident; were one not, the spins time out
   // into the abort word rather than hang)
-  if (!coop) {
+  if (!coop && grid_fits(reinterpret_cast<const void*>(fn), threads, (size_t)kBatchLdsPad, groups)) {
     hipLaunchKernelGGL(fn, dim3(groups), dim3(threads), (unsigned)kBatchLdsPad, (hipStream_t)stream, sp, arg);
     if (hipGetLastError() != hipSuccess) return -1;
-  } else if (hipLaunchCooperativeKernel(reinterpret_cast<const void*>(fn), dim3(groups), dim3(threads),
-                                        args, (unsigned)kBatchLdsPad, (hipStream_t)stream) != hipSuccess) {
-    return -1;
+  } else {
+    arg.hold = -1;  // every workgroup of a cooperative launch is resident
+    if (hipLaunchCooperativeKernel(reinterpret_cast<const void*>(fn), dim3(groups), dim3(threads), args,
+                                   (unsigned)kBatchLdsPad, (hipStream_t)stream) != hipSuccess)
+      return -1;
   }
   hipLaunchKernelGGL(k_batch_fixup, dim3((a.count + 255) / 256), dim3(256), 0, (hipStream_t)stream, st, a, groups);
   return hipGetLastError() == hipSuccess ? 0 : -1;

@@ -23,7 +23,7 @@ EXPORTS = ["kgpu_abi_version", "kgpu_struct_sizes", "kgpu_create", "kgpu_destroy
            "kgpu_comm_info",
            "kgpu_debug_fail_alloc", "kgpu_debug_pts_state", "kgpu_debug_ipa_state", "kgpu_debug_broken_linear",
            "kgpu_debug_wg_trace", "kgpu_debug_topo_resident",
-           "kgpu_next_slot", "kgpu_adopt_pod", "kgpu_filter_reasons"]
+           "kgpu_next_slot", "kgpu_adopt_pod", "kgpu_filter_reasons", "kgpu_debug_counters"]
 
 
 class KgpuError(RuntimeError):
@@ -75,6 +75,7 @@ def lib():
     L.kgpu_adopt_pod.argtypes = [vp, i32, i64]
     L.kgpu_select_victims.argtypes = [vp, vp, C.POINTER(abi.Pools), C.POINTER(abi.PreemptArgs), vp, vp,
                                       C.POINTER(i32)]
+    L.kgpu_debug_counters.argtypes = [vp, vp, i32]
     L.kgpu_filter_reasons.argtypes = [vp, C.POINTER(abi.ReasonArgs), vp, i64, C.POINTER(i64)]
     if L.kgpu_abi_version() != abi.ABI_VERSION:
         raise KgpuError(abi.E_STATE, "ABI version mismatch")
@@ -264,6 +265,14 @@ class Engine:
         out = np.zeros(2, np.int64)
         self._check(lib().kgpu_debug_topo_resident(self.h, out.ctypes.data))
         return int(out[0]), int(out[1])
+
+    def counters(self):
+        """kgpu_debug_counters: {coop_retries, persistent_launches, coop_launches}."""
+        out = np.zeros(8, np.int64)
+        n = lib().kgpu_debug_counters(self.h, out.ctypes.data, len(out))
+        if n < 0:
+            self._check(n)
+        return dict(zip(["coop_retries", "persistent_launches", "coop_launches"], [int(x) for x in out[:n]]))
 
     def broken_linear(self, points, utilizations):
         """kgpu_debug_broken_linear: the device's broken-linear shape function (the one

@@ -158,3 +158,59 @@ def test_lds_handoff_timeout_recovers(at):
     e.upload(fw.snap, fw.arrays)
     got, _ = e.schedule_batch(q, pc)
     _same(_ref(fw, q, pc), got)
+
+
+def _hold_case(kind):
+    if kind == "batch":
+        nodes, existing, pods, prof = cluster.fit_least_balanced(n_nodes=700, n_pods=160)
+    else:
+        nodes, existing, pods, prof = cluster.taints_affinity_spread(n_nodes=600, n_pods=60)
+    fw = GpuFramework(prof, nodes, existing, pods_hint=pods)
+    q, pc, _, errs = fw.compile_pods(pods)
+    assert not errs
+    return fw, q, pc
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["batch", "tbatch"])
+def test_missing_workgroup_retried_cooperatively(kind):
+    """Persistent kernels go out as ordinary launches (KGPU_OPT_COOPERATIVE 0).  A workgroup that never
+    starts (KGPU_OPT_HOLD_GROUP: it leaves at once) makes the others' pod-0 spins time out before any
+    pod resolved -- a clean abort: the call is issued again with a cooperative launch, returns the C
+    restatement's placements, and the mirror stays valid (the next call needs no re-upload)."""
+    fw, q, pc = _hold_case(kind)
+    e = fw.engine
+    want = _ref(fw, q, pc)
+    e.set_option(abi.OPT_HOLD_GROUP, 1)
+    got1, _ = e.schedule_batch(q[:80], pc, first_seq=0)
+    e.set_option(abi.OPT_HOLD_GROUP, -1)
+    c = e.counters()
+    assert c["coop_retries"] == 1 and c["coop_launches"] >= 1, c
+    got2, _ = e.schedule_batch(q[80:], pc, first_seq=80)
+    assert e.counters()["coop_retries"] == 1
+    _same(want, np.concatenate([got1, got2]))
+
+
+@pytest.mark.gpu
+def test_missing_workgroup_one_pod_cycle():
+    """The same for a kgpu_schedule_one cycle of a topology pod (a one-pod k_tbatch run whose abort word
+    travels through the pinned result block), in the middle of a sequence of cycles with assume and the
+    resident topology state on: every placement and the final node rows equal the C restatement's."""
+    from oracle.cref import RefEngine
+    fw, q, pc = _hold_case("tbatch_one")
+    e = fw.engine
+    got = []
+    for i in range(len(q)):
+        if i == 7:
+            e.set_option(abi.OPT_HOLD_GROUP, 0)
+        res, _ = e.schedule_one(q[i], pc, seq=i, assume=True)
+        if i == 7:
+            e.set_option(abi.OPT_HOLD_GROUP, -1)
+        got.append(res)
+    assert e.counters()["coop_retries"] == 1
+    ref = RefEngine(fw.config, fw.snap, threads=4)
+    want = ref.schedule(q, pc)
+    _same(want, np.array(got, dtype=abi.RESULT))
+    rows_w, rows_g = ref.read_nodes(), e.read_nodes(fw.snap.n_nodes)
+    for k in rows_w:
+        np.testing.assert_array_equal(rows_w[k], rows_g[k], err_msg=k)
