@@ -96,7 +96,7 @@ def _object_workload(cfg, n_nodes, n_pods):
 def pmc_traffic(cfg, n_local, launch_pods, kname):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3 --pmc passes of this
     exact workload (the newest profiles/r*_pmc_traffic.json holding it; tools/pmc_summary.py), or None."""
-    for fname in ("r04_pmc_traffic.json", "r03_pmc_traffic.json", "r02_pmc_traffic.json", "r01_pmc_traffic.json"):
+    for fname in ("r05_pmc_traffic.json", "r04_pmc_traffic.json", "r03_pmc_traffic.json", "r02_pmc_traffic.json", "r01_pmc_traffic.json"):
         try:
             with open(os.path.join(ROOT, "profiles", fname)) as fh:
                 pmc = json.load(fh).get("%s:%d:%d" % (cfg, n_local, launch_pods))
@@ -493,6 +493,14 @@ def main():
     ser = [r for r in [line] + recs if r.get("series") == key]
     line["scaling_series"] = {"series": key, "value": ser[0]["value"] if ser else None,
                               "n_gpus": world, "unit": "pods/s"}
+    # the same records in brief, last in the line: the driver keeps the tail of the output
+    def brief(r):
+        rf, cb, lt = r["roofline"], r.get("cpu_baseline") or {}, r.get("latency") or {}
+        return {"s": r["series"], "pods_s": round(r["value"]), "us_pod": rf["us_per_pod"], "GBs": rf["achieved"],
+                "frac": rf["frac"], "traffic": rf["traffic"], "cpu": cb.get("value"), "cpu_th": cb.get("cores"),
+                "cpu_1th": (cb.get("rates_by_threads") or {}).get("1"),
+                "one_p50_p99": [lt.get("p50_us"), lt.get("p99_us")] if lt else None}
+    line["summary"] = [brief(r) for r in [line] + recs]
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist_on:

@@ -218,7 +218,8 @@ struct kgpu_ctx {
   static constexpr int kHt = 12;
   int64_t ht_last = 0, ht_cur[kHt] = {}, ht_n = 0;
   int ht_seen = 0;
-  std::vector<std::array<int64_t, kHt>> ht_cycles;  // per cycle: ns of each step (medians at destroy)
+  std::vector<std::array<int64_t, kHt>> ht_cycles;  // per short cycle: ns of each step (p50 / p99 at destroy)
+  std::vector<std::array<int64_t, kHt>> ht_batches; // the same for longer calls (kgpu_schedule_batch)
   bool tc_on = true;                               // KGPU_OPT_TOPO_RESIDENT
   bool batch_helper = true;                        // KGPU_OPT_BATCH_HELPER
   bool topo_ahead = true;                          // KGPU_OPT_TOPO_AHEAD
@@ -1935,12 +1936,15 @@ int run_batch_once(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_
     if (c->ar.inflight) SYNC_OK(c);
     const size_t first = (kDsQueryOff + sizeof(kgpu_pod_query) * (size_t)n + 255) & ~(size_t)255;
     c->ar.begin(first, c->ar_limit > 0 ? std::min(kCycHostBytes, first + c->ar_limit) : 0);
+    if (c->htrace)  // the host trace's "record landed" step: every record the kernels write overwrites this
+      for (int32_t i = 0; i < n; ++i)
+        __atomic_store_n(&static_cast<kgpu_result*>(c->res_pin)[i].evaluated, INT32_MIN, __ATOMIC_RELAXED);
   }
   c->tb_abort_mapped = false;
-  if (short_cycle) ht(c, 0);
+  ht(c, 0);
   Staged sg;
   if ((rc = stage_topology(c, qs, n, pools, sg))) return rc;
-  if (short_cycle) ht(c, 1);  // 1: topology staging (QPlan, classes)
+  ht(c, 1);  // 1: topology staging (QPlan, classes)
   std::vector<kgpu::QPlan>& plans = sg.plans;
   std::vector<int32_t>& aux = sg.aux;
   std::vector<kgpu::TTerm>& aux_terms = sg.aux_terms;
@@ -1950,7 +1954,7 @@ int run_batch_once(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_
     for (int32_t i = 0; i < n; ++i) batch_ports += qs[i].ports.count;
   if ((rc = reserve_ports(c, batch_ports))) return rc;
   if ((rc = upload_pools(c, pools))) return rc;
-  if (short_cycle) ht(c, 2);  // 2: ports, pools
+  ht(c, 2);  // 2: ports, pools
   if (!short_cycle) {
     if ((rc = ensure(c, c->queries, sizeof(kgpu_pod_query) * (size_t)n))) return rc;
     HIP_OK(c, hipMemcpyAsync(c->queries.p, qs, sizeof(kgpu_pod_query) * (size_t)n, hipMemcpyHostToDevice, c->stream));
@@ -2015,6 +2019,7 @@ int run_batch_once(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_
   } else {
     c->ds_ptr = nullptr;
     HIP_OK(c, hipMemcpyAsync(c->dstate.p, &c->st_batch, sizeof(DevState), hipMemcpyHostToDevice, c->stream));
+    ht(c, 3);  // 3: queries and DevState copies (API calls)
   }
   const DevState* dst = static_cast<const DevState*>(c->dstate.p);
   const int blocks = kgpu::eval_blocks(st.N);
@@ -2096,9 +2101,9 @@ int run_batch_once(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_
       TRun& tr = runs.back();
       kgpu_pools empty{};
       const kgpu_pools* pp = pools ? pools : &empty;
-      if (short_cycle) ht(c, 3);  // 3: DevState / queries staged, geometry
+      ht(c, 3);  // 3: DevState / queries staged, geometry
       while (j < n && topo[(size_t)j] && t_add(tr, c, qs[j], plans[(size_t)j], pp, aux, aux_terms, j)) ++j;
-      if (short_cycle) ht(c, 4);  // 4: the run's tables planned (t_add)
+      ht(c, 4);  // 4: the run's tables planned (t_add)
       if (j > i) {
         if (c->timing) HIP_OK(c, hipEventRecord(get_event(c, ev), c->stream));
         if ((rc = run_tbatch(c, tr, i, j - i, first_seq, assume, tper, tgroups, tgeo, tb_arena ? nullptr : abort_word, xg,
@@ -2115,8 +2120,8 @@ int run_batch_once(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_
     }
     if ((rc = arena_flush(c))) return rc;  // every other launch reads DevState / queries / pools from it
     c->tc.valid = false;                     // ... and may assume outside a persistent topology run
-    ++c->state_launches;
     if (topo[(size_t)i]) {
+      ++c->state_launches;  // the per-pod topology pipeline
       if ((rc = zero_diag_rows())) return rc;
       const kgpu::QPlan& pl = plans[(size_t)i];
       // the previous pod's resolve launch zeroes this pod's scratch only when it went through this
@@ -2323,7 +2328,7 @@ int run_batch_once(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_
     i = j;
   }
   if (timed) HIP_OK(c, hipEventRecord(t1, c->stream));
-  if (short_cycle) ht(c, 8);  // 8: launches issued (after run_tbatch's 5-7)
+  ht(c, 8);  // 8: launches issued (after run_tbatch's 5-7)
   kgpu_result* res_host = short_cycle ? static_cast<kgpu_result*>(c->res_pin) : results;
   if (!short_cycle)
     HIP_OK(c, hipMemcpyAsync(res_host, st.results, sizeof(kgpu_result) * (size_t)n, hipMemcpyDeviceToHost, c->stream));
@@ -2331,8 +2336,18 @@ int run_batch_once(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_
     HIP_OK(c, hipMemcpyAsync(&c->abort_host, abort_word, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
   int32_t port_overflow = 0;
   if (batch_ports) HIP_OK(c, hipMemcpyAsync(&port_overflow, c->st.port_overflow, 4, hipMemcpyDeviceToHost, c->stream));
+  if (short_cycle && c->htrace) {
+    // 11: until the kernels' records are visible in pinned memory (bounded: 2 s); the synchronize after it
+    // is then the completion signal's own latency
+    const int64_t t_end = now_ns() + 2000000000ll;
+    for (int32_t i = 0; i < n; ++i)
+      while (__atomic_load_n(&static_cast<kgpu_result*>(c->res_pin)[i].evaluated, __ATOMIC_ACQUIRE) == INT32_MIN &&
+             now_ns() < t_end) {
+      }
+    ht(c, 11);
+  }
   SYNC_OK(c);
-  if (short_cycle) ht(c, 9);  // 9: synchronize
+  ht(c, 9);  // 9: synchronize
   if (short_cycle) std::memcpy(results, res_host, sizeof(kgpu_result) * (size_t)n);
   if (used_persistent && c->tb_abort_mapped) {
     // k_tbatch's last workgroup wrote the abort word (-1 left by the host: the run never finished)
@@ -2413,12 +2428,12 @@ int run_batch_once(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_
     }
   }
   c->last_diag = diag;
-  if (short_cycle && c->htrace) {
+  if (c->htrace) {
     ht(c, 10);  // 10: records, assumed-pod bookkeeping
-    ++c->ht_n;
     std::array<int64_t, kgpu_ctx::kHt> row{};
     std::copy(c->ht_cur, c->ht_cur + kgpu_ctx::kHt, row.begin());
-    c->ht_cycles.push_back(row);
+    (short_cycle ? c->ht_cycles : c->ht_batches).push_back(row);
+    c->ht_n += short_cycle ? 1 : 0;
   }
   return KGPU_OK;
 }
@@ -3139,14 +3154,15 @@ int kgpu_create(const kgpu_config* cfg, kgpu_ctx** out) try {
   if (cfg->device < 0 || cfg->device >= ndev) return KGPU_E_INVAL;
   c->cfg = *cfg;
   c->device = cfg->device;
-  // The synchronize that ends every cycle spins instead of yielding (the device's context is
-  // created with hipDeviceScheduleSpin): kgpu_schedule_one of a topology pod 66.4 -> 63.4 us p50 at 5k
-  // nodes (profiles/r04_sync_spin_latency.txt).  KGPU_SYNC_SPIN=0 keeps the runtime's default.  Only
-  // takes effect before the device's context exists in this process (a failure is ignored).
+  // KGPU_SYNC_SPIN=1: synchronizes spin instead of yielding (hipDeviceScheduleSpin: kgpu_schedule_one of a
+  // topology pod 66.4 -> 63.4 us p50 at 5k nodes, profiles/r04_sync_spin_latency.txt).  Opt-in: the flag
+  // is the device's, for every context and library of the process (a PyTorch or Go caller included), and
+  // a spinning synchronize holds a CPU core for the length of a 100k-node batch.  It takes effect only if
+  // no HIP context exists on the device yet (hipSetDeviceFlags fails otherwise; the failure is ignored).
   if (hipSetDevice(c->device) != hipSuccess) return KGPU_E_DEVICE;
   {
     const char* e = std::getenv("KGPU_SYNC_SPIN");
-    if (!(e && e[0] == '0')) (void)hipSetDeviceFlags(hipDeviceScheduleSpin);
+    if (e && e[0] == '1') (void)hipSetDeviceFlags(hipDeviceScheduleSpin);
   }
   if (const char* e = std::getenv("KGPU_HOST_TRACE")) c->htrace = e[0] == '1';
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
@@ -3197,17 +3213,40 @@ int kgpu_create(const kgpu_config* cfg, kgpu_ctx** out) try {
 
 int kgpu_destroy(kgpu_ctx* c) try {
   if (!c) return KGPU_OK;
-  if (c->htrace && c->ht_n > 0) {
+  if (c->htrace) {
     static const char* names[kgpu_ctx::kHt] = {"", "topology staging", "ports+pools", "state staged+geometry",
                                                "tables planned", "tables staged+key", "copy API", "launch API",
-                                               "to end of issue", "synchronize", "records+bookkeeping", ""};
-    std::fprintf(stderr, "kgpu host trace over %lld short cycles (median ns per cycle):\n", (long long)c->ht_n);
-    for (int k = 1; k < kgpu_ctx::kHt; ++k) {
-      if (!(c->ht_seen & (1 << k))) continue;
-      std::vector<int64_t> v;
-      for (const auto& r : c->ht_cycles) v.push_back(r[(size_t)k]);
-      std::nth_element(v.begin(), v.begin() + (long)(v.size() / 2), v.end());
-      std::fprintf(stderr, "  %2d %-24s %9lld\n", k, names[k], (long long)v[v.size() / 2]);
+                                               "to end of issue", "synchronize", "records+bookkeeping", "record landed"};
+    // p50 and p99 of each step, and of the whole call, over the short cycles and over the longer calls
+    auto pct = [](std::vector<int64_t> v, double q) {
+      const size_t i = std::min(v.size() - 1, (size_t)(q * (double)(v.size() - 1) + 0.5));
+      std::nth_element(v.begin(), v.begin() + (long)i, v.end());
+      return (long long)v[i];
+    };
+    const std::vector<std::array<int64_t, kgpu_ctx::kHt>>* sets[2] = {&c->ht_cycles, &c->ht_batches};
+    for (int si = 0; si < 2; ++si) {
+      const auto& rows = *sets[si];
+      if (rows.empty()) continue;
+      std::fprintf(stderr, "kgpu host trace over %zu %s (ns per call: p50, p99, and the median over the calls at "
+                   "or above the whole call's p99 -- what holds the tail):\n", rows.size(),
+                   si == 0 ? "short cycles" : "batch calls");
+      std::vector<int64_t> tot;
+      for (const auto& r : rows) {
+        int64_t t = 0;
+        for (int k = 1; k < kgpu_ctx::kHt; ++k) t += r[(size_t)k];
+        tot.push_back(t);
+      }
+      const long long t99 = pct(tot, 0.99);
+      for (int k = 1; k < kgpu_ctx::kHt; ++k) {
+        if (!(c->ht_seen & (1 << k))) continue;
+        std::vector<int64_t> v, tail;
+        for (size_t i = 0; i < rows.size(); ++i) {
+          v.push_back(rows[i][(size_t)k]);
+          if (tot[i] >= t99) tail.push_back(rows[i][(size_t)k]);
+        }
+        std::fprintf(stderr, "  %2d %-24s %9lld %9lld %9lld\n", k, names[k], pct(v, 0.5), pct(v, 0.99), pct(tail, 0.5));
+      }
+      std::fprintf(stderr, "     %-24s %9lld %9lld\n", "whole call", pct(tot, 0.5), t99);
     }
   }
   (void)hipSetDevice(c->device);

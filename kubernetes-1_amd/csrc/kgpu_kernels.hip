@@ -1251,7 +1251,7 @@ struct BatchShared {
 __device__ __forceinline__ void lds_release(int* f, int v) {
   __hip_atomic_store(f, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-// LDS hand-offs between the waves of a workgroup.  A wait that outlives kSpinTimeout (a protocol
+// LDS hand-offs between the waves of a workgroup.  A wait that outlives 2 x kSpinTimeout (a protocol
 // fault, never expected) raises the run's abort word instead of hanging the workgroup: the
 // communication wave's next sweep sees it, every wave leaves the pod loop, and the host reports
 // KGPU_E_DEVICE and invalidates the mirror.
@@ -1268,8 +1268,10 @@ __device__ __forceinline__ void lds_wait_t(int* f, int v, int32_t* abort_word) {
       const uint64_t now = __builtin_amdgcn_s_memrealtime();
       if (it == 0) {
         t0 = now;
-      } else if (now - t0 > kSpinTimeout) {
-        __hip_atomic_store(abort_word, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else if (now - t0 > 2 * kSpinTimeout) {
+        // twice the global polls' limit: when a workgroup never started, the communication wave's poll
+        // gives up first and reports the clean abort this wave would otherwise hide
+        __hip_atomic_fetch_or(abort_word, kAbortDirty, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return;
       }
     }
