@@ -266,6 +266,7 @@ struct kgpu_ctx {
   int batch_geo_first = 0;          // KGPU_OPT_BATCH_GEO
   DevBuf t_tables, t_zero, abort_buf;
   kgpu::HostStage table_stage;   // pinned staging of the runs' tables (bump-allocated, wraps after a sync)
+  kgpu::HostStage batch_stage;   // pinned staging of a long batch's queries, DevState, run pointers and results
   DevBuf pool_blk;               // the call's query pools, packed (upload_pools)
   kgpu::HostStage pool_stage;    // ... and their pinned staging
   // ---- node sharding (kgpu_comm_init): this context holds one contiguous slice of the
@@ -392,6 +393,7 @@ int sync_stream(kgpu_ctx* c) {
   HIP_OK(c, hipStreamSynchronize(c->stream));
   c->pool_stage.synced();
   c->table_stage.synced();
+  c->batch_stage.synced();
   c->delta_stage.synced();
   c->ar.synced();
   return KGPU_OK;
@@ -1886,6 +1888,19 @@ int stage_topology(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_
 int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools* pools, int64_t first_seq,
               kgpu_result* results, kgpu_stats* stats, bool diag, int32_t assume);
 
+// A long batch's host-to-device copy through the pinned batch block: a copy from pageable memory is
+// staged by the runtime itself and costs the call far more (the queries of a 1000-pod batch are
+// 0.3 MB).
+int stage_h2d(kgpu_ctx* c, void* dst, const void* src, size_t bytes) {
+  char* h = nullptr;
+  int rc;
+  if ((rc = c->batch_stage.reserve(stage_ops(c), bytes, 1 << 20, &h))) return rc;
+  std::memcpy(h, src, bytes);
+  HIP_OK(c, hipMemcpyAsync(dst, h, bytes, hipMemcpyHostToDevice, c->stream));
+  c->batch_stage.enqueued();
+  return KGPU_OK;
+}
+
 // internal: run_batch_once's persistent run aborted before resolving any pod and was the call's only
 // state-changing launch (never returned to a caller)
 constexpr int kCleanAbort = 1000;
@@ -1957,7 +1972,7 @@ int run_batch_once(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_
   ht(c, 2);  // 2: ports, pools
   if (!short_cycle) {
     if ((rc = ensure(c, c->queries, sizeof(kgpu_pod_query) * (size_t)n))) return rc;
-    HIP_OK(c, hipMemcpyAsync(c->queries.p, qs, sizeof(kgpu_pod_query) * (size_t)n, hipMemcpyHostToDevice, c->stream));
+    if ((rc = stage_h2d(c, c->queries.p, qs, sizeof(kgpu_pod_query) * (size_t)n))) return rc;
     if ((rc = ensure(c, c->results, sizeof(kgpu_result) * (size_t)n))) return rc;
   }
   if (!c->ticket.p) {
@@ -2018,7 +2033,7 @@ int run_batch_once(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_
     c->ds_ptr = c->dstate.p;
   } else {
     c->ds_ptr = nullptr;
-    HIP_OK(c, hipMemcpyAsync(c->dstate.p, &c->st_batch, sizeof(DevState), hipMemcpyHostToDevice, c->stream));
+    if ((rc = stage_h2d(c, c->dstate.p, &c->st_batch, sizeof(DevState)))) return rc;
     ht(c, 3);  // 3: queries and DevState copies (API calls)
   }
   const DevState* dst = static_cast<const DevState*>(c->dstate.p);
@@ -2233,7 +2248,7 @@ int run_batch_once(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_
         ba.feas = reinterpret_cast<int32_t*>(ba.gran + cells);
         run_ptrs.push_back({ba.gran, ba.feas});
         void** slot = static_cast<void**>(c->batch_ptrs.p) + 2 * (run_ptrs.size() - 1);
-        HIP_OK(c, hipMemcpyAsync(slot, run_ptrs.back().data(), sizeof(void*) * 2, hipMemcpyHostToDevice, c->stream));
+        if ((rc = stage_h2d(c, slot, run_ptrs.back().data(), sizeof(void*) * 2))) return rc;
         ba.pgran = reinterpret_cast<uint64_t* const*>(slot);
         ba.pfeas = reinterpret_cast<int32_t* const*>(slot + 1);
         ba.nranks = 1;
@@ -2329,9 +2344,16 @@ int run_batch_once(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_
   }
   if (timed) HIP_OK(c, hipEventRecord(t1, c->stream));
   ht(c, 8);  // 8: launches issued (after run_tbatch's 5-7)
-  kgpu_result* res_host = short_cycle ? static_cast<kgpu_result*>(c->res_pin) : results;
-  if (!short_cycle)
+  // a long batch's records land in the pinned batch block (read back after the synchronize, before the
+  // block can be reused)
+  kgpu_result* res_host = static_cast<kgpu_result*>(c->res_pin);
+  if (!short_cycle) {
+    char* h = nullptr;
+    if ((rc = c->batch_stage.reserve(stage_ops(c), sizeof(kgpu_result) * (size_t)n, 1 << 20, &h))) return rc;
+    res_host = reinterpret_cast<kgpu_result*>(h);
     HIP_OK(c, hipMemcpyAsync(res_host, st.results, sizeof(kgpu_result) * (size_t)n, hipMemcpyDeviceToHost, c->stream));
+    c->batch_stage.enqueued();
+  }
   if (used_persistent && !c->tb_abort_mapped)
     HIP_OK(c, hipMemcpyAsync(&c->abort_host, abort_word, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
   int32_t port_overflow = 0;
@@ -2348,7 +2370,7 @@ int run_batch_once(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_
   }
   SYNC_OK(c);
   ht(c, 9);  // 9: synchronize
-  if (short_cycle) std::memcpy(results, res_host, sizeof(kgpu_result) * (size_t)n);
+  std::memcpy(results, res_host, sizeof(kgpu_result) * (size_t)n);
   if (used_persistent && c->tb_abort_mapped) {
     // k_tbatch's last workgroup wrote the abort word (-1 left by the host: the run never finished)
     const int32_t w = __atomic_load_n(reinterpret_cast<int32_t*>(static_cast<char*>(c->res_pin) + kCycAbortOff),
@@ -3271,6 +3293,7 @@ int kgpu_destroy(kgpu_ctx* c) try {
     c->delta_stage.release(ops);
     c->table_stage.release(ops);
     c->pool_stage.release(ops);
+    c->batch_stage.release(ops);
   }
   if (c->cyc_host) (void)hipHostFree(c->cyc_host);
   if (c->res_pin) (void)hipHostFree(c->res_pin);

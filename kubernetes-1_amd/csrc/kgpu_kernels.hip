@@ -1834,21 +1834,27 @@ __global__ __launch_bounds__(B + 64 + (HB ? 2 * B : 0)) void k_batch(const DevSt
 
 // FeasibleNodes and the scored flag of every pod of a persistent run (generic_scheduler.go:184-191:
 // a single feasible node is returned without scoring).
-__global__ void k_batch_fixup(const DevState* __restrict__ stp, BatchArgs pa, int G) {
+__global__ __launch_bounds__(256) void k_batch_fixup(const DevState* __restrict__ stp, BatchArgs pa, int G) {
+  // one wave per pod: its lanes sum the pod's per-workgroup feasible counts (coalesced), where one thread
+  // per pod looping over G counts took 12.7 us per 1000-pod launch at 5k nodes (profiles/r05_*)
   const DevState& st = *stp;
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (i >= pa.count) return;
-  int f = 0;
   const size_t row = pa.R > 0 ? (size_t)((pa.xseq0 + i) % pa.R) : (size_t)i;
-  for (int g = 0; g < pa.GT; ++g) f += pa.feas[row * pa.GT + g];
+  int f = 0;
+  for (int g = lane; g < pa.GT; g += 64) f += pa.feas[row * pa.GT + g];
+  f = (int)wave_sum32((uint32_t)f);
   (void)G;
-  kgpu_result& r = gp(st.results)[pa.first + i];
-  r.feasible = f;
-  if (r.node >= 0 && f >= 2) {
-    r.scored = 1;
-  } else {
-    r.scored = 0;
-    r.score = 0;
+  if (lane == 0) {
+    kgpu_result& r = gp(st.results)[pa.first + i];
+    r.feasible = f;
+    if (r.node >= 0 && f >= 2) {
+      r.scored = 1;
+    } else {
+      r.scored = 0;
+      r.score = 0;
+    }
   }
 }
 
@@ -4145,7 +4151,7 @@ int launch_batch(const DevState* st, const BatchArgs& a, int groups, int geo, in
                                    (unsigned)kBatchLdsPad, (hipStream_t)stream) != hipSuccess)
       return -1;
   }
-  hipLaunchKernelGGL(k_batch_fixup, dim3((a.count + 255) / 256), dim3(256), 0, (hipStream_t)stream, st, a, groups);
+  hipLaunchKernelGGL(k_batch_fixup, dim3((a.count + 3) / 4), dim3(256), 0, (hipStream_t)stream, st, a, groups);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
