@@ -214,3 +214,26 @@ def test_missing_workgroup_one_pod_cycle():
     rows_w, rows_g = ref.read_nodes(), e.read_nodes(fw.snap.n_nodes)
     for k in rows_w:
         np.testing.assert_array_equal(rows_w[k], rows_g[k], err_msg=k)
+
+
+@pytest.mark.gpu
+def test_abort_one_pod_cycle_recovers():
+    """A one-pod topology cycle (kgpu_schedule_one's k_tbatch run, abort word through the pinned result
+    block) that aborts after its workgroups started (KGPU_OPT_ABORT_AT): KGPU_E_DEVICE, the mirror is
+    invalid until the next upload, and after it the cycles match the C restatement."""
+    from oracle.cref import RefEngine
+    fw, q, pc = _hold_case("tbatch_one")
+    e = fw.engine
+    for i in range(5):
+        e.schedule_one(q[i], pc, seq=i, assume=True)
+    e.set_option(abi.OPT_ABORT_AT, 0)
+    with pytest.raises(KgpuError) as ex:
+        e.schedule_one(q[5], pc, seq=5, assume=True)
+    assert ex.value.code == abi.E_DEVICE and "re-upload" in str(ex.value)
+    e.set_option(abi.OPT_ABORT_AT, -1)
+    assert e.counters()["coop_retries"] == 0  # a run that started everywhere is not issued again
+    with pytest.raises(KgpuError):
+        e.schedule_one(q[5], pc, seq=5, assume=True)
+    e.upload(fw.snap, fw.arrays)
+    got = [e.schedule_one(q[i], pc, seq=i, assume=True)[0] for i in range(len(q))]
+    _same(RefEngine(fw.config, fw.snap, threads=4).schedule(q, pc), np.array(got, dtype=abi.RESULT))
