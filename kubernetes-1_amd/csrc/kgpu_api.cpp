@@ -263,6 +263,8 @@ struct kgpu_ctx {
   int32_t hold_group = -1;          // KGPU_OPT_HOLD_GROUP test hook
   int64_t n_coop_retry = 0, n_persist = 0, n_coop = 0;  // kgpu_debug_counters
   int state_launches = 0;           // launches of the current call that may change device state
+  bool unsettled = false;           // a short cycle returned on its completion word, before the stream's
+                                    // own completion: settle() before anything that is not stream-ordered
   int batch_geo_first = 0;          // KGPU_OPT_BATCH_GEO
   DevBuf t_tables, t_zero, abort_buf;
   kgpu::HostStage table_stage;   // pinned staging of the runs' tables (bump-allocated, wraps after a sync)
@@ -386,6 +388,7 @@ constexpr size_t kDsQueryOff = (sizeof(DevState) + 255) & ~(size_t)255;
 constexpr size_t kCycHostBytes = kDsQueryOff + sizeof(kgpu_pod_query) * kShortCycle + kArenaBytes;
 constexpr size_t kCycResBytes = sizeof(kgpu_result) * kShortCycle;
 constexpr size_t kCycAbortOff = kCycResBytes;  // int32 in res_pin
+constexpr size_t kCycDoneOff = kCycResBytes + 4;  // int32 in res_pin: k_final's completion word (PodArgs.done_out)
 
 // The context's stream synchronize: every pending copy from the staging blocks has run
 // (kgpu_staging.h), so they may be rewritten, regrown or freed.
@@ -405,6 +408,13 @@ int sync_stream(kgpu_ctx* c) {
   } while (0)
 
 int stage_sync(void* self) { return sync_stream(static_cast<kgpu_ctx*>(self)); }
+
+// The stream's own completion of a short cycle that returned on its completion word.
+int settle(kgpu_ctx* c) {
+  if (!c->unsettled) return KGPU_OK;
+  c->unsettled = false;
+  return sync_stream(c);
+}
 int stage_alloc(void* self, void** p, size_t bytes) {
   kgpu_ctx* c = static_cast<kgpu_ctx*>(self);
   fail_point();
@@ -1951,9 +1961,10 @@ int run_batch_once(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_
     if (c->ar.inflight) SYNC_OK(c);
     const size_t first = (kDsQueryOff + sizeof(kgpu_pod_query) * (size_t)n + 255) & ~(size_t)255;
     c->ar.begin(first, c->ar_limit > 0 ? std::min(kCycHostBytes, first + c->ar_limit) : 0);
-    if (c->htrace)  // the host trace's "record landed" step: every record the kernels write overwrites this
-      for (int32_t i = 0; i < n; ++i)
-        __atomic_store_n(&static_cast<kgpu_result*>(c->res_pin)[i].evaluated, INT32_MIN, __ATOMIC_RELAXED);
+    // every record the kernels write overwrites this: the host trace's "record landed" step, and the
+    // second half of a one-pod cycle's completion (its word and its record)
+    for (int32_t i = 0; i < n; ++i)
+      __atomic_store_n(&static_cast<kgpu_result*>(c->res_pin)[i].evaluated, INT32_MIN, __ATOMIC_RELAXED);
   }
   c->tb_abort_mapped = false;
   ht(c, 0);
@@ -2088,6 +2099,7 @@ int run_batch_once(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_
     return KGPU_OK;
   };
   bool used_persistent = false;
+  int32_t* done_word = nullptr;  // the pinned completion word of the call's last kernel (one-pod cycles)
   // one abort word for every persistent run of this batch (OR-ed on the device)
   int rc_abort = ensure(c, c->abort_buf, 64);
   if (rc_abort) return rc_abort;
@@ -2124,6 +2136,11 @@ int run_batch_once(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_
         if ((rc = run_tbatch(c, tr, i, j - i, first_seq, assume, tper, tgroups, tgeo, tb_arena ? nullptr : abort_word, xg,
                              diag)))
           return rc;
+        // the one-pod run's last workgroup copies the abort word into pinned memory after everything is
+        // written back: the call's completion word
+        done_word = (c->tb_abort_mapped && !c->timing && !c->phase_trace)
+                        ? reinterpret_cast<int32_t*>(static_cast<char*>(c->res_pin) + kCycAbortOff)
+                        : nullptr;
         if (diag) diag_zeroed = true;  // k_tbatch zeroed the rows (a diagnostic run is one pod)
         if (c->timing) HIP_OK(c, hipEventRecord(get_event(c, ev + 1), c->stream));
         ev += 2;
@@ -2311,6 +2328,14 @@ int run_batch_once(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_
           a.q_inline = 1;
           a.q = qs[k];
         }
+        // a one-pod diagnostic cycle ends on k_final's resolving workgroup: it raises a pinned completion
+        // word once everything is written back, and the host returns on it
+        if (a.resolve_self && short_cycle && n == 1 && !sharded && !c->timing && !c->phase_trace) {
+          int32_t* dw = reinterpret_cast<int32_t*>(static_cast<char*>(c->res_pin) + kCycDoneOff);
+          __atomic_store_n(dw, -1, __ATOMIC_RELEASE);
+          a.done_out = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(c->res_dev) + kCycDoneOff);
+          done_word = dw;
+        }
         if ((rc = zero_diag_rows())) return rc;
         ++c->state_launches;
         if (c->timing) HIP_OK(c, hipEventRecord(get_event(c, ev), c->stream));
@@ -2358,7 +2383,22 @@ int run_batch_once(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_
     HIP_OK(c, hipMemcpyAsync(&c->abort_host, abort_word, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
   int32_t port_overflow = 0;
   if (batch_ports) HIP_OK(c, hipMemcpyAsync(&port_overflow, c->st.port_overflow, 4, hipMemcpyDeviceToHost, c->stream));
-  if (short_cycle && c->htrace) {
+  // A one-pod cycle whose last kernel raises a completion word, with no stream operation after it,
+  // returns once the word lands (bounded: 2 s, then the synchronize below): the stream's own completion
+  // signal reaches the host about 8 us later (profiles/r05_host_trace.txt).  The copies that fed the
+  // kernel ran before it, so the staging blocks are free; settle() synchronizes before any operation
+  // that is not ordered on the stream.
+  bool landed = false;
+  if (done_word && short_cycle && n == 1 && !batch_ports && !timed && (!used_persistent || c->tb_abort_mapped)) {
+    const int64_t t_end = now_ns() + 2000000000ll;
+    const int32_t* ev = &static_cast<kgpu_result*>(c->res_pin)[0].evaluated;
+    while (!(landed = __atomic_load_n(done_word, __ATOMIC_ACQUIRE) != -1 &&
+                      __atomic_load_n(ev, __ATOMIC_ACQUIRE) != INT32_MIN) &&
+           now_ns() < t_end) {
+    }
+  }
+  if (landed && c->htrace) ht(c, 11);
+  if (!landed && short_cycle && c->htrace) {
     // 11: until the kernels' records are visible in pinned memory (bounded: 2 s); the synchronize after it
     // is then the completion signal's own latency
     const int64_t t_end = now_ns() + 2000000000ll;
@@ -2368,7 +2408,16 @@ int run_batch_once(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_
       }
     ht(c, 11);
   }
-  SYNC_OK(c);
+  if (landed) {
+    c->pool_stage.synced();
+    c->table_stage.synced();
+    c->delta_stage.synced();
+    c->batch_stage.synced();
+    c->ar.synced();
+    c->unsettled = true;
+  } else {
+    SYNC_OK(c);
+  }
   ht(c, 9);  // 9: synchronize
   std::memcpy(results, res_host, sizeof(kgpu_result) * (size_t)n);
   if (used_persistent && c->tb_abort_mapped) {
@@ -3314,6 +3363,10 @@ const char* kgpu_last_error(const kgpu_ctx* c) { return c ? c->err.c_str() : "nu
 int64_t kgpu_generation(const kgpu_ctx* c) { return c ? c->generation : -1; }
 
 int kgpu_read_phase_trace(kgpu_ctx* c, int64_t* out, int32_t max_pods) try {
+  if (c && c->unsettled) {  // a short cycle returned on its completion word: the stream first
+    const int rs_ = settle(c);
+    if (rs_) return rs_;
+  }
   if (!c || !out || max_pods < 0) return KGPU_E_INVAL;
   const int32_t n = std::min<int32_t>(max_pods, (int32_t)(c->trace_host.size() / 16));
   std::memcpy(out, c->trace_host.data(), sizeof(int64_t) * 16 * (size_t)n);
@@ -3337,6 +3390,10 @@ int kgpu_debug_topo_resident(const kgpu_ctx* c, int64_t out[2]) {
 }
 
 int kgpu_debug_wg_trace(kgpu_ctx* c, int64_t* out, int64_t max_words, int32_t* groups) try {
+  if (c && c->unsettled) {  // a short cycle returned on its completion word: the stream first
+    const int rs_ = settle(c);
+    if (rs_) return rs_;
+  }
   if (!c || !out || !groups || max_words < 0) return KGPU_E_INVAL;
   const size_t n = std::min<size_t>((size_t)max_words, c->trace_wg_host.size());
   std::memcpy(out, c->trace_wg_host.data(), sizeof(int64_t) * n);
@@ -3374,6 +3431,10 @@ int kgpu_set_option(kgpu_ctx* c, int32_t option, int64_t value) try {
 }
 
 int kgpu_upload_snapshot(kgpu_ctx* c, const kgpu_snapshot* s, int64_t generation) try {
+  if (c && c->unsettled) {  // a short cycle returned on its completion word: the stream first
+    const int rs_ = settle(c);
+    if (rs_) return rs_;
+  }
   if (!c || !s) return KGPU_E_INVAL;
   c->tc.valid = false;
   if (s->n_nodes < 0 || s->n_label_keys < 0 || s->n_scalar < 0 || s->taint_words < 0 || s->port_slots < 0)
@@ -3536,6 +3597,10 @@ int kgpu_upload_snapshot(kgpu_ctx* c, const kgpu_snapshot* s, int64_t generation
 
 int kgpu_schedule_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools* pools, int64_t first_seq,
                         kgpu_result* results, kgpu_stats* stats) try {
+  if (c && c->unsettled) {  // a short cycle returned on its completion word: the stream first
+    const int rs_ = settle(c);
+    if (rs_) return rs_;
+  }
   if (!c || (n > 0 && (!qs || !results))) return KGPU_E_INVAL;
   if (hipSetDevice(c->device) != hipSuccess) return KGPU_E_DEVICE;
   return run_batch(c, qs, n, pools, first_seq, results, stats, false, 1);
@@ -3558,6 +3623,10 @@ int kgpu_schedule_one(kgpu_ctx* c, const kgpu_pod_query* q, const kgpu_pools* po
 
 int kgpu_set_nominated(kgpu_ctx* c, const kgpu_nominated* noms, int32_t n, const kgpu_pod_query* pods,
                        const kgpu_pools* pools) try {
+  if (c && c->unsettled) {  // a short cycle returned on its completion word: the stream first
+    const int rs_ = settle(c);
+    if (rs_) return rs_;
+  }
   if (!c || n < 0 || (n > 0 && (!noms || !pods))) return KGPU_E_INVAL;
   kgpu_ctx::Nominator nm;
   int32_t n_items = 0;
@@ -3664,6 +3733,10 @@ static int32_t pick_one_node(const std::vector<int32_t>& cand, const kgpu_node_v
 
 int kgpu_select_victims(kgpu_ctx* c, const kgpu_pod_query* q, const kgpu_pools* pools, const kgpu_preempt_args* args,
                         kgpu_node_victims* nodes_out, int32_t* victims_out, int32_t* chosen) try {
+  if (c && c->unsettled) {  // a short cycle returned on its completion word: the stream first
+    const int rs_ = settle(c);
+    if (rs_) return rs_;
+  }
   if (!c || !q || !args || !nodes_out || (args->n_victims > 0 && (!args->victims || !args->pods || !victims_out)))
     return KGPU_E_INVAL;
   if (args->n_victims < 0 || args->n_pdbs < 0 || (args->n_pdbs > 0 && !args->pdb_allowed)) return KGPU_E_INVAL;
@@ -3831,6 +3904,10 @@ static int debug_topo_check(kgpu_ctx* c) {
 
 int kgpu_debug_pts_state(kgpu_ctx* c, const kgpu_pod_query* q, const kgpu_pools* pools, int32_t kind,
                          int32_t constraint, uint8_t* registered, int64_t* counts, int64_t* scalar) try {
+  if (c && c->unsettled) {  // a short cycle returned on its completion word: the stream first
+    const int rs_ = settle(c);
+    if (rs_) return rs_;
+  }
   if (!c || !q || !registered || !counts || !scalar || (kind != 0 && kind != 1) || constraint < 0) return KGPU_E_INVAL;
   int rc;
   if ((rc = debug_topo_check(c))) return rc;
@@ -3865,6 +3942,10 @@ int kgpu_debug_pts_state(kgpu_ctx* c, const kgpu_pod_query* q, const kgpu_pools*
 
 int kgpu_debug_ipa_state(kgpu_ctx* c, const kgpu_pod_query* q, const kgpu_pools* pools, int32_t max_maps,
                          int32_t max_values, int32_t* kinds, int32_t* keys, int64_t* counts, int32_t* n_maps) try {
+  if (c && c->unsettled) {  // a short cycle returned on its completion word: the stream first
+    const int rs_ = settle(c);
+    if (rs_) return rs_;
+  }
   if (!c || !q || !kinds || !keys || !counts || !n_maps || max_maps < 0 || max_values < 0) return KGPU_E_INVAL;
   int rc;
   if ((rc = debug_topo_check(c))) return rc;
@@ -3898,6 +3979,10 @@ int kgpu_debug_ipa_state(kgpu_ctx* c, const kgpu_pod_query* q, const kgpu_pools*
 
 int kgpu_debug_broken_linear(kgpu_ctx* c, const kgpu_shape_point* points, int32_t n_points, const int64_t* p,
                              int32_t n, int64_t* out) try {
+  if (c && c->unsettled) {  // a short cycle returned on its completion word: the stream first
+    const int rs_ = settle(c);
+    if (rs_) return rs_;
+  }
   if (!c || !points || !p || !out || n_points <= 0 || n_points > 16 || n <= 0) return KGPU_E_INVAL;
   if (hipSetDevice(c->device) != hipSuccess) return KGPU_E_DEVICE;
   fail_point();
@@ -3967,6 +4052,10 @@ int kgpu_filter_reasons(kgpu_ctx* c, const kgpu_reason_args* a, char* buf, int64
 
 int kgpu_read_nodes(kgpu_ctx* c, int64_t* req_cpu, int64_t* req_mem, int64_t* req_eph, int64_t* nz_cpu,
                     int64_t* nz_mem, int32_t* num_pods) try {
+  if (c && c->unsettled) {  // a short cycle returned on its completion word: the stream first
+    const int rs_ = settle(c);
+    if (rs_) return rs_;
+  }
   if (!c || !c->uploaded) return KGPU_E_INVAL;
   SYNC_OK(c);
   const size_t N = (size_t)c->st.N;
@@ -3982,6 +4071,10 @@ int kgpu_read_nodes(kgpu_ctx* c, int64_t* req_cpu, int64_t* req_mem, int64_t* re
 }
 
 int kgpu_forget_pod(kgpu_ctx* c, int32_t slot) try {
+  if (c && c->unsettled) {  // a short cycle returned on its completion word: the stream first
+    const int rs_ = settle(c);
+    if (rs_) return rs_;
+  }
   if (!c) return KGPU_E_INVAL;
   if (!c->uploaded) return fail(c, KGPU_E_STATE, "no snapshot uploaded");
   if (slot < 0 || slot >= (int32_t)c->recs.size() || !c->recs[(size_t)slot].active)
@@ -4018,6 +4111,10 @@ int kgpu_forget_pod(kgpu_ctx* c, int32_t slot) try {
 int kgpu_next_slot(const kgpu_ctx* c) { return c ? (int)std::min<size_t>(c->recs.size(), INT32_MAX) : -1; }
 
 int kgpu_adopt_pod(kgpu_ctx* c, int32_t slot, int64_t uid) try {
+  if (c && c->unsettled) {  // a short cycle returned on its completion word: the stream first
+    const int rs_ = settle(c);
+    if (rs_) return rs_;
+  }
   if (!c) return KGPU_E_INVAL;
   if (!c->uploaded) return fail(c, KGPU_E_STATE, "no snapshot uploaded");
   if (slot < 0 || slot >= (int32_t)c->recs.size() || !c->recs[(size_t)slot].active || !c->recs[(size_t)slot].has_res)
@@ -4036,6 +4133,10 @@ int kgpu_adopt_pod(kgpu_ctx* c, int32_t slot, int64_t uid) try {
 }
 
 int kgpu_apply_delta(kgpu_ctx* c, const kgpu_delta_batch* b, int64_t generation, int32_t* slots) try {
+  if (c && c->unsettled) {  // a short cycle returned on its completion word: the stream first
+    const int rs_ = settle(c);
+    if (rs_) return rs_;
+  }
   if (!c || !b) return KGPU_E_INVAL;
   if (!c->uploaded) return fail(c, KGPU_E_STATE, "no snapshot uploaded");
   if (b->n_deltas < 0 || b->n_pods < 0 || b->n_rows < 0 || b->n_order < 0 || (b->n_deltas && !b->deltas) ||
@@ -4067,6 +4168,10 @@ static int xgmi_geometry(kgpu_ctx* c, int32_t nranks) {
 }
 
 int kgpu_xgmi_handle(kgpu_ctx* c, int32_t nranks, uint8_t handle[64]) try {
+  if (c && c->unsettled) {  // a short cycle returned on its completion word: the stream first
+    const int rs_ = settle(c);
+    if (rs_) return rs_;
+  }
   if (!c || !handle || nranks < 2 || nranks > kgpu::kMaxRanks) return KGPU_E_INVAL;
   if (hipSetDevice(c->device) != hipSuccess) return KGPU_E_DEVICE;
   if (!c->uploaded) return fail(c, KGPU_E_STATE, "upload this rank's shard before kgpu_xgmi_handle");
@@ -4103,6 +4208,10 @@ int kgpu_xgmi_handle(kgpu_ctx* c, int32_t nranks, uint8_t handle[64]) try {
 }
 
 int kgpu_xgmi_init(kgpu_ctx* c, int32_t nranks, int32_t rank, const uint8_t* handles) try {
+  if (c && c->unsettled) {  // a short cycle returned on its completion word: the stream first
+    const int rs_ = settle(c);
+    if (rs_) return rs_;
+  }
   if (!c || !handles || nranks < 2 || nranks > kgpu::kMaxRanks || rank < 0 || rank >= nranks) return KGPU_E_INVAL;
   c->tc.valid = false;
   if (hipSetDevice(c->device) != hipSuccess) return KGPU_E_DEVICE;
@@ -4168,6 +4277,10 @@ int kgpu_comm_unique_id(uint8_t id[128]) try {
 }
 
 int kgpu_comm_init(kgpu_ctx* c, int32_t nranks, int32_t rank, const uint8_t id[128]) try {
+  if (c && c->unsettled) {  // a short cycle returned on its completion word: the stream first
+    const int rs_ = settle(c);
+    if (rs_) return rs_;
+  }
   if (!c || !id) return KGPU_E_INVAL;
   c->tc.valid = false;
   if (nranks < 1 || nranks > kgpu::kMaxRanks || rank < 0 || rank >= nranks)

@@ -240,6 +240,9 @@ struct PodArgs {
   int32_t resolve_self; // 1: k_final's last workgroup resolves and assumes `pod` (no k_resolve launch)
   int32_t q_inline;     // 1: `pod`'s query is `q` below (a one-pod cycle: no query upload)
   int64_t seq;          // tie-break sequence number of `pod`
+  int32_t* done_out;    // null, or (resolve_self) the pinned host word the resolving workgroup sets to 0 once
+                        // every store of the cycle is written back: the host returns on it without waiting
+                        // for the stream's completion signal (~8 us later, profiles/r05_host_trace.txt)
   kgpu_pod_query q;
 };
 

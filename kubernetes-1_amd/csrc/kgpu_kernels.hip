@@ -964,6 +964,10 @@ __global__ __launch_bounds__(kBlock) void k_final(const DevState* __restrict__ s
     // assume -- in place of a k_resolve launch (the end of a short cycle).  Release / acquire
     // fences around the ticket make every workgroup's partial visible to it across XCDs.
     __shared__ int last;
+    // a cycle the host completes on done_out: every wave writes its stores back (the diagnostic rows
+    // included) before the ticket, not only wave 0's partial
+    if (a.done_out) __threadfence();
+    __syncthreads();
     if (threadIdx.x == 0) {
       __threadfence();
       last = atomicAdd(st.ticket, 1) == (int)gridDim.x - 1;
@@ -988,6 +992,11 @@ __global__ __launch_bounds__(kBlock) void k_final(const DevState* __restrict__ s
           assume_counts(st, a.pod, idx);
         }
         __hip_atomic_store(st.ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // for the next cycle
+      }
+      if (a.done_out) {
+        __threadfence();  // the record, the assume and the last workgroup's rows, written back
+        __syncthreads();
+        if (threadIdx.x == 0) __hip_atomic_store(a.done_out, 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
       }
     }
   }
@@ -3170,6 +3179,12 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
   // every workgroup leaves through here, aborted or not (the pod loop only breaks): the last one to
   // leave copies the run's abort word into the caller's pinned block
   auto leave = [&]() {
+    if (ta.abort_out) {
+      // the host completes a one-pod cycle on abort_out: every wave's stores (records, diagnostic rows,
+      // the resident state's write-back) are written back before the workgroup counts itself out
+      __threadfence();
+      __syncthreads();
+    }
     if (ta.abort_out && tid == 0) {
       __threadfence();
       if (atomicAdd(ta.done, 1) == G - 1) {
