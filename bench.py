@@ -190,9 +190,19 @@ def measure(args, cfg, n_nodes_per_gpu, B, K, W, cpu_sample, cpu_threads, latenc
         stats = abi.Stats()
         t0 = time.perf_counter()
         results = []
-        for k in range(K):
-            res, stats = eng.schedule_batch(q[k * B:(k + 1) * B], pc, first_seq=len(q_init) + k * B, stats=stats)
-            results.append(res)
+        if args.no_pipeline:
+            for k in range(K):
+                res, stats = eng.schedule_batch(q[k * B:(k + 1) * B], pc, first_seq=len(q_init) + k * B, stats=stats)
+                results.append(res)
+        else:
+            # pipelined steps (kgpu_schedule_batch_submit / _wait): step k+1's host work overlaps step k's
+            # device run; a step the pipeline does not carry (topology pods) runs synchronously in submit
+            for k in range(K):
+                eng.schedule_batch_submit(q[k * B:(k + 1) * B], pc, first_seq=len(q_init) + k * B, stats=stats)
+                if eng.pipelined() > 1:
+                    results.append(eng.schedule_batch_wait()[0])
+            while eng.pipelined():
+                results.append(eng.schedule_batch_wait()[0])
         torch.cuda.synchronize()
         if dist_on:
             dist.barrier()
@@ -419,6 +429,8 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--latency-pods", type=int, default=200, help="pods timed one at a time through kgpu_schedule_one")
     ap.add_argument("--no-persistent", action="store_true", help="one evaluation launch per pod")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="synchronous kgpu_schedule_batch per step instead of pipelined submit / wait")
     ap.add_argument("--topo-fused", type=int, default=None, help="KGPU_OPT_TOPO_FUSED (default: the library's)")
     ap.add_argument("--no-topo-persistent", action="store_true",
                     help="topology pods through the per-pod topology launches instead of k_tbatch")

@@ -409,6 +409,20 @@ int kgpu_schedule_one(kgpu_ctx* ctx, const kgpu_pod_query* q, const kgpu_pools* 
 int kgpu_schedule_batch(kgpu_ctx* ctx, const kgpu_pod_query* qs, int32_t n, const kgpu_pools* pools,
                         int64_t first_seq, kgpu_result* results, kgpu_stats* stats);
 
+/* Pipelined batches: the scheduleOne loop over consecutive batches, each batch's host work (the caller's
+ * compile, staging, the launch) overlapped with the previous batch's device run.  _submit stages and
+ * launches a batch and returns; `results` and `stats` must stay valid until the batch is completed by
+ * _wait, which completes the OLDEST batch in flight and returns its status.  Two batches are kept in
+ * flight (a third submit first completes the oldest).  A batch the pipeline does not carry (topology
+ * pods, normalize pods, host ports, nominated pods, node sharding, percentageOfNodesToScore < 100,
+ * short batches) runs synchronously inside _submit after the batches in flight; its _wait returns its
+ * status.  Every other call on the context fails with KGPU_E_STATE while batches are in flight.
+ * kgpu_pipelined returns the number of batches submitted and not yet waited for. */
+int kgpu_schedule_batch_submit(kgpu_ctx* ctx, const kgpu_pod_query* qs, int32_t n, const kgpu_pools* pools,
+                               int64_t first_seq, kgpu_result* results, kgpu_stats* stats);
+int kgpu_schedule_batch_wait(kgpu_ctx* ctx);
+int kgpu_pipelined(const kgpu_ctx* ctx);
+
 /* Diagnostics for the last kgpu_schedule_one: per-node filter status words, and per-node raw /
  * normalized (unweighted) scores of one score plugin over the feasible nodes (others: 0). */
 int kgpu_get_filter(kgpu_ctx* ctx, uint32_t* status_words);

@@ -263,6 +263,32 @@ struct kgpu_ctx {
   int32_t hold_group = -1;          // KGPU_OPT_HOLD_GROUP test hook
   int64_t n_coop_retry = 0, n_persist = 0, n_coop = 0;  // kgpu_debug_counters
   int state_launches = 0;           // launches of the current call that may change device state
+  // pipelined batches (kgpu_schedule_batch_submit / _wait): two slots, each with its pinned staging block,
+  // device block (DevState | queries | run pointers | abort word), granules and pinned result records
+  struct PipeSlot {
+    void* host = nullptr;         // pinned staging of the device block
+    size_t host_cap = 0;
+    DevBuf dev, gran;
+    void* res = nullptr;          // pinned, mapped: the records and the abort word, written by k_batch_fixup
+    void* res_dev = nullptr;
+    size_t res_cap = 0;
+    size_t gran_zeroed = 0;       // leading bytes of `gran` known to be zero
+    hipEvent_t done = nullptr, t0 = nullptr, t1 = nullptr;
+  };
+  struct PipeBatch {
+    int slot = 0;
+    int32_t n = 0;
+    kgpu_result* results = nullptr;
+    kgpu_stats* stats = nullptr;
+    std::vector<kgpu_pod_query> qs;           // for the assumed pods' records (ForgetPod)
+    std::vector<int32_t> ints;                // the pools' label pairs ...
+    std::vector<kgpu_scalar_req> scalars;     // ... and scalar requests those records keep
+    int rc = KGPU_OK;                         // a batch the pipeline does not carry: ran in submit
+    bool timed = false;
+  };
+  PipeSlot pipe[2];
+  std::deque<PipeBatch> pipe_q;
+  int pipe_next = 0;
   bool unsettled = false;           // a short cycle returned on its completion word, before the stream's
                                     // own completion: settle() before anything that is not stream-ordered
   int batch_geo_first = 0;          // KGPU_OPT_BATCH_GEO
@@ -364,6 +390,8 @@ void free_all(std::vector<void*>& reg) {
 int ensure(kgpu_ctx* c, DevBuf& b, size_t bytes) {
   if (bytes == 0) bytes = 8;
   if (b.bytes >= bytes) return KGPU_OK;
+  // a pipelined batch in flight may still read the old buffer (kgpu_schedule_batch_submit)
+  if (b.p && !c->pipe_q.empty()) HIP_OK(c, hipStreamSynchronize(c->stream));
   if (b.p) (void)hipFree(b.p);
   b.p = nullptr;
   b.bytes = 0;
@@ -3113,6 +3141,212 @@ int run_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools
   return rc;
 }
 
+// ---------------------------------------------------------------- pipelined batches
+// kgpu_schedule_batch_submit stages and launches a batch and returns; kgpu_schedule_batch_wait completes
+// the oldest one.  Batch k+1's host work (the caller's, staging, the launch) then runs while batch k's
+// kernel does, and the stream carries three operations per batch -- one copy (DevState, queries, run
+// pointers, a zeroed abort word), k_batch, k_batch_fixup (records and abort word into pinned memory, the
+// other slot's granules zeroed) -- where a synchronous call pays a staging gap, six operations and a
+// synchronize (0.19 ms of each 1.75 ms config-(b) step outside the kernel).  Batches alternate
+// between two slots; slot s is reused by batch k+2 only after batch k completed.
+bool pipe_eligible(const kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools* pools) {
+  if (!c->uploaded || !c->persistent || n <= kShortCycle || c->comm || c->xg_nranks > 1 || c->has_alias ||
+      !c->nom.list.empty() || c->st.cut_state || topo_profile(c) || c->phase_trace || c->abort_at >= 0 ||
+      c->skip_release_at >= 0 || c->hold_group >= 0)
+    return false;
+  for (int32_t i = 0; i < n; ++i)
+    if (qs[i].ports.count || needs_norm(c, qs[i], pools) || (qs[i].flags & KGPU_Q_SCORE_ERROR)) return false;
+  return true;
+}
+
+int pipe_complete(kgpu_ctx* c);
+
+int pipe_submit(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools* pools, int64_t first_seq,
+                kgpu_result* results, kgpu_stats* stats) {
+  int rc;
+  if (!pipe_eligible(c, qs, n, pools)) {
+    // not carried: complete what is in flight, run it synchronously, queue its outcome for its wait
+    while (!c->pipe_q.empty())
+      if ((rc = pipe_complete(c))) return rc;
+    kgpu_ctx::PipeBatch b;
+    b.rc = run_batch(c, qs, n, pools, first_seq, results, stats, false, 1);
+    b.n = -1;
+    c->pipe_q.push_back(std::move(b));
+    return KGPU_OK;
+  }
+  if (c->pipe_q.size() >= 2 && (rc = pipe_complete(c))) return rc;
+  int per = 0, groups = 0;
+  const int kidx = kgpu::batch_geometry(c->st.N, std::min(c->max_groups > 0 ? std::min(c->max_groups, c->n_cus) : c->n_cus, 256),
+                                        &per, &groups, c->batch_geo_first);
+  if (kidx < 0) return fail(c, KGPU_E_UNSUPPORTED, "no persistent geometry for this node count");
+  // the pools ride on the stream like every other copy (ordered after the batch in flight)
+  if ((rc = upload_pools(c, pools))) return rc;
+  if (!c->ticket.p) {
+    if ((rc = ensure(c, c->ticket, 64))) return rc;
+    HIP_OK(c, hipMemset(c->ticket.p, 0, 64));
+  }
+  const int s = c->pipe_next;
+  c->pipe_next ^= 1;
+  kgpu_ctx::PipeSlot& ps = c->pipe[s];
+  // device block: DevState | queries | [gran, feas] run pointers | abort word
+  const size_t q_off = kDsQueryOff, q_bytes = sizeof(kgpu_pod_query) * (size_t)n;
+  const size_t p_off = (q_off + q_bytes + 15) & ~(size_t)15, a_off = p_off + 16 * 2;
+  const size_t bytes = a_off + 64;
+  if ((rc = ensure(c, ps.dev, bytes))) return rc;
+  if (ps.host_cap < bytes) {
+    if (ps.host) HIP_OK(c, hipHostFree(ps.host));
+    ps.host = nullptr;
+    ps.host_cap = 0;
+    HIP_OK(c, hipHostMalloc(&ps.host, bytes * 2, hipHostMallocDefault));
+    ps.host_cap = bytes * 2;
+  }
+  const size_t cells = (size_t)n * (size_t)groups;
+  const size_t gbytes = (sizeof(uint64_t) + sizeof(int32_t)) * cells;
+  if (ps.gran.bytes < gbytes) {
+    if ((rc = ensure(c, ps.gran, gbytes))) return rc;
+    ps.gran_zeroed = 0;
+  }
+  if (ps.gran_zeroed < gbytes) {
+    HIP_OK(c, hipMemsetAsync(ps.gran.p, 0, ps.gran.bytes, c->stream));
+    ps.gran_zeroed = ps.gran.bytes;
+  }
+  const size_t rbytes = sizeof(kgpu_result) * (size_t)n + 64;
+  if (ps.res_cap < rbytes) {
+    if (ps.res) HIP_OK(c, hipHostFree(ps.res));
+    ps.res = nullptr;
+    ps.res_cap = 0;
+    HIP_OK(c, hipHostMalloc(&ps.res, rbytes * 2, hipHostMallocCoherent | hipHostMallocMapped));
+    HIP_OK(c, hipHostGetDevicePointer(&ps.res_dev, ps.res, 0));
+    ps.res_cap = rbytes * 2;
+  }
+  for (hipEvent_t* e : {&ps.done, &ps.t0, &ps.t1})
+    if (!*e) HIP_OK(c, hipEventCreateWithFlags(e, e == &ps.done ? hipEventDisableTiming : hipEventDefault));
+  char* h = static_cast<char*>(ps.host);
+  char* d = static_cast<char*>(ps.dev.p);
+  DevState st = c->st;
+  st.ticket = static_cast<int32_t*>(c->ticket.p);
+  st.queries = reinterpret_cast<const kgpu_pod_query*>(d + q_off);
+  if ((rc = ensure(c, c->results, sizeof(kgpu_result) * (size_t)n))) return rc;
+  st.results = static_cast<kgpu_result*>(c->results.p);
+  st.diag_raw = nullptr;
+  st.diag_norm = nullptr;
+  uint64_t* gran = static_cast<uint64_t*>(ps.gran.p);
+  int32_t* feas = reinterpret_cast<int32_t*>(gran + cells);
+  std::memcpy(h, &st, sizeof(DevState));
+  std::memcpy(h + q_off, qs, q_bytes);
+  void* ptrs[2] = {gran, feas};
+  std::memcpy(h + p_off, ptrs, sizeof(ptrs));
+  std::memset(h + a_off, 0, 64);
+  HIP_OK(c, hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, c->stream));
+  c->tc.valid = false;  // the batch assumes outside a persistent topology run
+  kgpu::BatchArgs ba{};
+  ba.gran = gran;
+  ba.feas = feas;
+  ba.pgran = reinterpret_cast<uint64_t* const*>(d + p_off);
+  ba.pfeas = reinterpret_cast<int32_t* const*>(d + p_off + sizeof(void*));
+  ba.nranks = 1;
+  ba.rank = 0;
+  ba.GT = groups;
+  ba.R = 0;
+  ba.first = 0;
+  ba.count = n;
+  ba.per = per;
+  ba.assume = 1;
+  ba.seq0 = first_seq;
+  ba.abort = reinterpret_cast<int32_t*>(d + a_off);
+  ba.abort_at = -1;
+  ba.skip_release_at = -1;
+  ba.trace = nullptr;
+  ba.res_out = static_cast<kgpu_result*>(ps.res_dev);
+  ba.abort_out = reinterpret_cast<int32_t*>(static_cast<char*>(ps.res_dev) + sizeof(kgpu_result) * (size_t)n);
+  // the other slot's granules, zeroed by this batch's fixup for the batch after next
+  kgpu_ctx::PipeSlot& po = c->pipe[s ^ 1];
+  ba.zero_buf = static_cast<uint64_t*>(po.gran.p);
+  ba.zero_n16 = po.gran.p ? (int64_t)(po.gran.bytes / 16) : 0;
+  const bool coop = c->coop;
+  ba.hold = -1;
+  ++c->n_persist;
+  c->n_coop += coop ? 1 : 0;
+  *reinterpret_cast<int32_t*>(static_cast<char*>(ps.res) + sizeof(kgpu_result) * (size_t)n) = -1;
+  const bool timed = stats != nullptr;
+  if (timed) HIP_OK(c, hipEventRecord(ps.t0, c->stream));
+  if (kgpu::launch_batch(reinterpret_cast<const DevState*>(d), ba, groups, kidx, c->spec, coop, c->batch_helper,
+                         c->stream))
+    return fail(c, KGPU_E_DEVICE, "k_batch launch failed");
+  if (timed) HIP_OK(c, hipEventRecord(ps.t1, c->stream));
+  HIP_OK(c, hipEventRecord(ps.done, c->stream));
+  ps.gran_zeroed = 0;                 // this batch dirties its slot ...
+  if (po.gran.p) po.gran_zeroed = po.gran.bytes;  // ... and its fixup zeroes the other
+  kgpu_ctx::PipeBatch b;
+  b.slot = s;
+  b.n = n;
+  b.results = results;
+  b.stats = stats;
+  b.timed = timed;
+  b.qs.assign(qs, qs + n);
+  if (pools) {
+    if (pools->ints && pools->n_ints > 0) b.ints.assign(pools->ints, pools->ints + pools->n_ints);
+    if (pools->scalars && pools->n_scalars > 0) b.scalars.assign(pools->scalars, pools->scalars + pools->n_scalars);
+  }
+  c->pipe_q.push_back(std::move(b));
+  return KGPU_OK;
+}
+
+// Completes the oldest batch in flight: its records, the assumed pods' bookkeeping, its stats.
+int pipe_complete(kgpu_ctx* c) {
+  if (c->pipe_q.empty()) return fail(c, KGPU_E_STATE, "no pipelined batch in flight");
+  kgpu_ctx::PipeBatch b = std::move(c->pipe_q.front());
+  c->pipe_q.pop_front();
+  if (b.n < 0) return b.rc;  // ran synchronously in submit
+  kgpu_ctx::PipeSlot& ps = c->pipe[b.slot];
+  HIP_OK(c, hipEventSynchronize(ps.done));
+  const kgpu_result* res = static_cast<const kgpu_result*>(ps.res);
+  const int32_t abort = __atomic_load_n(reinterpret_cast<const int32_t*>(res + b.n), __ATOMIC_ACQUIRE);
+  if (abort != 0) {
+    // no re-issue here: the next batch already ran on top of this one
+    c->uploaded = false;
+    c->pipe_q.clear();
+    (void)sync_stream(c);
+    return fail(c, KGPU_E_DEVICE, "pipelined persistent run gave up waiting for a workgroup; the device mirror is "
+                                  "invalid: re-upload the snapshot");
+  }
+  std::memcpy(b.results, res, sizeof(kgpu_result) * (size_t)b.n);
+  if (b.stats) {
+    float ms = 0.f;
+    HIP_OK(c, hipEventElapsedTime(&ms, ps.t0, ps.t1));
+    b.stats->pods += b.n;
+    b.stats->device_ms += ms;
+    int64_t placed = 0;
+    for (int32_t i = 0; i < b.n; ++i) placed += b.results[i].node >= 0;
+    b.stats->scheduled += placed;
+    if (c->timing) {
+      b.stats->eval_kernel_ms += ms;
+      b.stats->eval_launches += b.n;
+    }
+  }
+  for (int32_t i = 0; i < b.n; ++i) {
+    if (b.results[i].node < 0) continue;
+    const kgpu_pod_query& q = b.qs[(size_t)i];
+    kgpu_ctx::PodRow row;
+    row.node = b.results[i].node;
+    row.ns = q.ns;
+    row.flags = query_pod_flags(q);
+    if (q.labels.count && q.labels.begin + q.labels.count <= (int32_t)b.ints.size())
+      row.pairs.assign(b.ints.begin() + q.labels.begin, b.ints.begin() + q.labels.begin + q.labels.count);
+    c->pod_rows.push_back(std::move(row));
+    kgpu_ctx::PodRec a;
+    a.node = b.results[i].node;
+    a.q = q;
+    a.active = true;
+    a.has_res = true;
+    if (q.scalars.count && q.scalars.begin + q.scalars.count <= (int32_t)b.scalars.size())
+      a.sc.assign(b.scalars.begin() + q.scalars.begin, b.scalars.begin() + q.scalars.begin + q.scalars.count);
+    c->recs.push_back(std::move(a));
+  }
+  c->last_diag = false;
+  return KGPU_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -3344,6 +3578,14 @@ int kgpu_destroy(kgpu_ctx* c) try {
     c->pool_stage.release(ops);
     c->batch_stage.release(ops);
   }
+  for (auto& ps : c->pipe) {
+    if (ps.host) (void)hipHostFree(ps.host);
+    if (ps.res) (void)hipHostFree(ps.res);
+    if (ps.dev.p) (void)hipFree(ps.dev.p);
+    if (ps.gran.p) (void)hipFree(ps.gran.p);
+    for (hipEvent_t e : {ps.done, ps.t0, ps.t1})
+      if (e) (void)hipEventDestroy(e);
+  }
   if (c->cyc_host) (void)hipHostFree(c->cyc_host);
   if (c->res_pin) (void)hipHostFree(c->res_pin);
   if (c->st.mcnt) (void)hipFree(c->st.mcnt);
@@ -3363,6 +3605,8 @@ const char* kgpu_last_error(const kgpu_ctx* c) { return c ? c->err.c_str() : "nu
 int64_t kgpu_generation(const kgpu_ctx* c) { return c ? c->generation : -1; }
 
 int kgpu_read_phase_trace(kgpu_ctx* c, int64_t* out, int32_t max_pods) try {
+  if (c && !c->pipe_q.empty())
+    return fail(c, KGPU_E_STATE, "pipelined batches in flight: complete them with kgpu_schedule_batch_wait first");
   if (c && c->unsettled) {  // a short cycle returned on its completion word: the stream first
     const int rs_ = settle(c);
     if (rs_) return rs_;
@@ -3390,6 +3634,8 @@ int kgpu_debug_topo_resident(const kgpu_ctx* c, int64_t out[2]) {
 }
 
 int kgpu_debug_wg_trace(kgpu_ctx* c, int64_t* out, int64_t max_words, int32_t* groups) try {
+  if (c && !c->pipe_q.empty())
+    return fail(c, KGPU_E_STATE, "pipelined batches in flight: complete them with kgpu_schedule_batch_wait first");
   if (c && c->unsettled) {  // a short cycle returned on its completion word: the stream first
     const int rs_ = settle(c);
     if (rs_) return rs_;
@@ -3404,6 +3650,8 @@ int kgpu_debug_wg_trace(kgpu_ctx* c, int64_t* out, int64_t max_words, int32_t* g
 }
 
 int kgpu_set_option(kgpu_ctx* c, int32_t option, int64_t value) try {
+  if (c && !c->pipe_q.empty())
+    return fail(c, KGPU_E_STATE, "pipelined batches in flight: complete them with kgpu_schedule_batch_wait first");
   if (!c) return KGPU_E_INVAL;
   if (option == KGPU_OPT_KERNEL_TIMING) c->timing = value != 0;
   else if (option == KGPU_OPT_PERSISTENT) c->persistent = value != 0;
@@ -3431,6 +3679,8 @@ int kgpu_set_option(kgpu_ctx* c, int32_t option, int64_t value) try {
 }
 
 int kgpu_upload_snapshot(kgpu_ctx* c, const kgpu_snapshot* s, int64_t generation) try {
+  if (c && !c->pipe_q.empty())
+    return fail(c, KGPU_E_STATE, "pipelined batches in flight: complete them with kgpu_schedule_batch_wait first");
   if (c && c->unsettled) {  // a short cycle returned on its completion word: the stream first
     const int rs_ = settle(c);
     if (rs_) return rs_;
@@ -3597,6 +3847,8 @@ int kgpu_upload_snapshot(kgpu_ctx* c, const kgpu_snapshot* s, int64_t generation
 
 int kgpu_schedule_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools* pools, int64_t first_seq,
                         kgpu_result* results, kgpu_stats* stats) try {
+  if (c && !c->pipe_q.empty())
+    return fail(c, KGPU_E_STATE, "pipelined batches in flight: complete them with kgpu_schedule_batch_wait first");
   if (c && c->unsettled) {  // a short cycle returned on its completion word: the stream first
     const int rs_ = settle(c);
     if (rs_) return rs_;
@@ -3608,8 +3860,35 @@ int kgpu_schedule_batch(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const 
   return on_exception(c, true);
 }
 
+int kgpu_schedule_batch_submit(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools* pools,
+                               int64_t first_seq, kgpu_result* results, kgpu_stats* stats) try {
+  if (!c || (n > 0 && (!qs || !results))) return KGPU_E_INVAL;
+  if (c->unsettled) {
+    const int rs_ = settle(c);
+    if (rs_) return rs_;
+  }
+  if (hipSetDevice(c->device) != hipSuccess) return KGPU_E_DEVICE;
+  return pipe_submit(c, qs, n, pools, first_seq, results, stats);
+} catch (...) {
+  c->pipe_q.clear();
+  return on_exception(c, true);
+}
+
+int kgpu_schedule_batch_wait(kgpu_ctx* c) try {
+  if (!c) return KGPU_E_INVAL;
+  if (hipSetDevice(c->device) != hipSuccess) return KGPU_E_DEVICE;
+  return pipe_complete(c);
+} catch (...) {
+  c->pipe_q.clear();
+  return on_exception(c, true);
+}
+
+int kgpu_pipelined(const kgpu_ctx* c) { return c ? (int)c->pipe_q.size() : 0; }
+
 int kgpu_schedule_one(kgpu_ctx* c, const kgpu_pod_query* q, const kgpu_pools* pools, int64_t pod_seq, int32_t assume,
                       kgpu_result* res, int32_t* assumed_slot) try {
+  if (c && !c->pipe_q.empty())
+    return fail(c, KGPU_E_STATE, "pipelined batches in flight: complete them with kgpu_schedule_batch_wait first");
   if (!c || !q || !res) return KGPU_E_INVAL;
   if (hipSetDevice(c->device) != hipSuccess) return KGPU_E_DEVICE;
   size_t before = c->recs.size();
@@ -3623,6 +3902,8 @@ int kgpu_schedule_one(kgpu_ctx* c, const kgpu_pod_query* q, const kgpu_pools* po
 
 int kgpu_set_nominated(kgpu_ctx* c, const kgpu_nominated* noms, int32_t n, const kgpu_pod_query* pods,
                        const kgpu_pools* pools) try {
+  if (c && !c->pipe_q.empty())
+    return fail(c, KGPU_E_STATE, "pipelined batches in flight: complete them with kgpu_schedule_batch_wait first");
   if (c && c->unsettled) {  // a short cycle returned on its completion word: the stream first
     const int rs_ = settle(c);
     if (rs_) return rs_;
@@ -3733,6 +4014,8 @@ static int32_t pick_one_node(const std::vector<int32_t>& cand, const kgpu_node_v
 
 int kgpu_select_victims(kgpu_ctx* c, const kgpu_pod_query* q, const kgpu_pools* pools, const kgpu_preempt_args* args,
                         kgpu_node_victims* nodes_out, int32_t* victims_out, int32_t* chosen) try {
+  if (c && !c->pipe_q.empty())
+    return fail(c, KGPU_E_STATE, "pipelined batches in flight: complete them with kgpu_schedule_batch_wait first");
   if (c && c->unsettled) {  // a short cycle returned on its completion word: the stream first
     const int rs_ = settle(c);
     if (rs_) return rs_;
@@ -3904,6 +4187,8 @@ static int debug_topo_check(kgpu_ctx* c) {
 
 int kgpu_debug_pts_state(kgpu_ctx* c, const kgpu_pod_query* q, const kgpu_pools* pools, int32_t kind,
                          int32_t constraint, uint8_t* registered, int64_t* counts, int64_t* scalar) try {
+  if (c && !c->pipe_q.empty())
+    return fail(c, KGPU_E_STATE, "pipelined batches in flight: complete them with kgpu_schedule_batch_wait first");
   if (c && c->unsettled) {  // a short cycle returned on its completion word: the stream first
     const int rs_ = settle(c);
     if (rs_) return rs_;
@@ -3942,6 +4227,8 @@ int kgpu_debug_pts_state(kgpu_ctx* c, const kgpu_pod_query* q, const kgpu_pools*
 
 int kgpu_debug_ipa_state(kgpu_ctx* c, const kgpu_pod_query* q, const kgpu_pools* pools, int32_t max_maps,
                          int32_t max_values, int32_t* kinds, int32_t* keys, int64_t* counts, int32_t* n_maps) try {
+  if (c && !c->pipe_q.empty())
+    return fail(c, KGPU_E_STATE, "pipelined batches in flight: complete them with kgpu_schedule_batch_wait first");
   if (c && c->unsettled) {  // a short cycle returned on its completion word: the stream first
     const int rs_ = settle(c);
     if (rs_) return rs_;
@@ -3979,6 +4266,8 @@ int kgpu_debug_ipa_state(kgpu_ctx* c, const kgpu_pod_query* q, const kgpu_pools*
 
 int kgpu_debug_broken_linear(kgpu_ctx* c, const kgpu_shape_point* points, int32_t n_points, const int64_t* p,
                              int32_t n, int64_t* out) try {
+  if (c && !c->pipe_q.empty())
+    return fail(c, KGPU_E_STATE, "pipelined batches in flight: complete them with kgpu_schedule_batch_wait first");
   if (c && c->unsettled) {  // a short cycle returned on its completion word: the stream first
     const int rs_ = settle(c);
     if (rs_) return rs_;
@@ -4001,6 +4290,8 @@ int kgpu_debug_broken_linear(kgpu_ctx* c, const kgpu_shape_point* points, int32_
 }
 
 int kgpu_get_filter(kgpu_ctx* c, uint32_t* words) try {
+  if (c && !c->pipe_q.empty())
+    return fail(c, KGPU_E_STATE, "pipelined batches in flight: complete them with kgpu_schedule_batch_wait first");
   if (!c || !words) return KGPU_E_INVAL;
   if (!c->last_diag) return fail(c, KGPU_E_STATE, "no kgpu_schedule_one cycle to report");
   HIP_OK(c, hipMemcpy(words, c->st.status, sizeof(uint32_t) * (size_t)c->st.N, hipMemcpyDeviceToHost));
@@ -4010,6 +4301,8 @@ int kgpu_get_filter(kgpu_ctx* c, uint32_t* words) try {
 }
 
 int kgpu_get_scores(kgpu_ctx* c, int32_t plugin, int64_t* raw, int64_t* normalized) try {
+  if (c && !c->pipe_q.empty())
+    return fail(c, KGPU_E_STATE, "pipelined batches in flight: complete them with kgpu_schedule_batch_wait first");
   if (!c || plugin < 0 || plugin >= KGPU_NUM_SCORES) return KGPU_E_INVAL;
   if (!c->last_diag) return fail(c, KGPU_E_STATE, "no kgpu_schedule_one cycle to report");
   const size_t N = (size_t)c->st.N;
@@ -4052,6 +4345,8 @@ int kgpu_filter_reasons(kgpu_ctx* c, const kgpu_reason_args* a, char* buf, int64
 
 int kgpu_read_nodes(kgpu_ctx* c, int64_t* req_cpu, int64_t* req_mem, int64_t* req_eph, int64_t* nz_cpu,
                     int64_t* nz_mem, int32_t* num_pods) try {
+  if (c && !c->pipe_q.empty())
+    return fail(c, KGPU_E_STATE, "pipelined batches in flight: complete them with kgpu_schedule_batch_wait first");
   if (c && c->unsettled) {  // a short cycle returned on its completion word: the stream first
     const int rs_ = settle(c);
     if (rs_) return rs_;
@@ -4071,6 +4366,8 @@ int kgpu_read_nodes(kgpu_ctx* c, int64_t* req_cpu, int64_t* req_mem, int64_t* re
 }
 
 int kgpu_forget_pod(kgpu_ctx* c, int32_t slot) try {
+  if (c && !c->pipe_q.empty())
+    return fail(c, KGPU_E_STATE, "pipelined batches in flight: complete them with kgpu_schedule_batch_wait first");
   if (c && c->unsettled) {  // a short cycle returned on its completion word: the stream first
     const int rs_ = settle(c);
     if (rs_) return rs_;
@@ -4111,6 +4408,8 @@ int kgpu_forget_pod(kgpu_ctx* c, int32_t slot) try {
 int kgpu_next_slot(const kgpu_ctx* c) { return c ? (int)std::min<size_t>(c->recs.size(), INT32_MAX) : -1; }
 
 int kgpu_adopt_pod(kgpu_ctx* c, int32_t slot, int64_t uid) try {
+  if (c && !c->pipe_q.empty())
+    return fail(c, KGPU_E_STATE, "pipelined batches in flight: complete them with kgpu_schedule_batch_wait first");
   if (c && c->unsettled) {  // a short cycle returned on its completion word: the stream first
     const int rs_ = settle(c);
     if (rs_) return rs_;
@@ -4133,6 +4432,8 @@ int kgpu_adopt_pod(kgpu_ctx* c, int32_t slot, int64_t uid) try {
 }
 
 int kgpu_apply_delta(kgpu_ctx* c, const kgpu_delta_batch* b, int64_t generation, int32_t* slots) try {
+  if (c && !c->pipe_q.empty())
+    return fail(c, KGPU_E_STATE, "pipelined batches in flight: complete them with kgpu_schedule_batch_wait first");
   if (c && c->unsettled) {  // a short cycle returned on its completion word: the stream first
     const int rs_ = settle(c);
     if (rs_) return rs_;
@@ -4168,6 +4469,8 @@ static int xgmi_geometry(kgpu_ctx* c, int32_t nranks) {
 }
 
 int kgpu_xgmi_handle(kgpu_ctx* c, int32_t nranks, uint8_t handle[64]) try {
+  if (c && !c->pipe_q.empty())
+    return fail(c, KGPU_E_STATE, "pipelined batches in flight: complete them with kgpu_schedule_batch_wait first");
   if (c && c->unsettled) {  // a short cycle returned on its completion word: the stream first
     const int rs_ = settle(c);
     if (rs_) return rs_;
@@ -4208,6 +4511,8 @@ int kgpu_xgmi_handle(kgpu_ctx* c, int32_t nranks, uint8_t handle[64]) try {
 }
 
 int kgpu_xgmi_init(kgpu_ctx* c, int32_t nranks, int32_t rank, const uint8_t* handles) try {
+  if (c && !c->pipe_q.empty())
+    return fail(c, KGPU_E_STATE, "pipelined batches in flight: complete them with kgpu_schedule_batch_wait first");
   if (c && c->unsettled) {  // a short cycle returned on its completion word: the stream first
     const int rs_ = settle(c);
     if (rs_) return rs_;
@@ -4277,6 +4582,8 @@ int kgpu_comm_unique_id(uint8_t id[128]) try {
 }
 
 int kgpu_comm_init(kgpu_ctx* c, int32_t nranks, int32_t rank, const uint8_t id[128]) try {
+  if (c && !c->pipe_q.empty())
+    return fail(c, KGPU_E_STATE, "pipelined batches in flight: complete them with kgpu_schedule_batch_wait first");
   if (c && c->unsettled) {  // a short cycle returned on its completion word: the stream first
     const int rs_ = settle(c);
     if (rs_) return rs_;

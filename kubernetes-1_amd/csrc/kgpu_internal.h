@@ -269,6 +269,13 @@ struct BatchArgs {
   int32_t hold;         // KGPU_OPT_HOLD_GROUP test hook: this workgroup leaves at once (an ordinary launch
                         // whose workgroup never became resident; -1: none)
   int32_t pad_h;
+  // pipelined batches (kgpu_schedule_batch_submit): k_batch_fixup also writes every record into pinned host
+  // memory (res_out), copies the run's abort word there (abort_out), and zeroes the other pipeline slot's
+  // granule area for the batch after next (zero_buf, zero_n16 16-byte words); all null / 0 otherwise
+  kgpu_result* res_out;
+  int32_t* abort_out;
+  uint64_t* zero_buf;
+  int64_t zero_n16;
   // Node sharding over xGMI (kgpu_xgmi_init): every workgroup of every rank publishes its granule
   // and feasible count into every rank's mailbox ring; each rank polls its own.  Unsharded:
   // nranks 1, pgran[0] = gran, pfeas[0] = feas, GT = groups, R = 0 (rows are this launch's pods,

@@ -964,9 +964,10 @@ __global__ __launch_bounds__(kBlock) void k_final(const DevState* __restrict__ s
     // assume -- in place of a k_resolve launch (the end of a short cycle).  Release / acquire
     // fences around the ticket make every workgroup's partial visible to it across XCDs.
     __shared__ int last;
-    // a cycle the host completes on done_out: every wave writes its stores back (the diagnostic rows
-    // included) before the ticket, not only wave 0's partial
-    if (a.done_out) __threadfence();
+    // a cycle the host completes on done_out: every wave's stores (the diagnostic rows included) reach L2
+    // before thread 0's release writes the L2 back (one write-back per workgroup: a fence in every wave
+    // cost a 100k-node cycle 5 us, profiles/r05_host_trace.txt)
+    if (a.done_out) __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
     if (threadIdx.x == 0) {
       __threadfence();
@@ -994,9 +995,12 @@ __global__ __launch_bounds__(kBlock) void k_final(const DevState* __restrict__ s
         __hip_atomic_store(st.ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // for the next cycle
       }
       if (a.done_out) {
-        __threadfence();  // the record, the assume and the last workgroup's rows, written back
+        __builtin_amdgcn_s_waitcnt(0);  // the record, the assume and the last workgroup's rows in L2 ...
         __syncthreads();
-        if (threadIdx.x == 0) __hip_atomic_store(a.done_out, 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (threadIdx.x == 0) {
+          __threadfence();  // ... written back, then the completion word
+          __hip_atomic_store(a.done_out, 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
       }
     }
   }
@@ -1849,6 +1853,14 @@ __global__ __launch_bounds__(256) void k_batch_fixup(const DevState* __restrict_
   const DevState& st = *stp;
   const int lane = threadIdx.x & 63;
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  // pipelined batches: the other slot's granules, zeroed for the batch after next (its last reader, that
+  // slot's previous fixup, finished before this run's k_batch started)
+  for (int64_t z = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; z < pa.zero_n16; z += (int64_t)gridDim.x * blockDim.x) {
+    uint4* zp = reinterpret_cast<uint4*>(pa.zero_buf) + z;
+    *zp = uint4{0, 0, 0, 0};
+  }
+  if (pa.abort_out && blockIdx.x == 0 && threadIdx.x == 0)
+    __hip_atomic_store(pa.abort_out, load_sc1(pa.abort), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   if (i >= pa.count) return;
   const size_t row = pa.R > 0 ? (size_t)((pa.xseq0 + i) % pa.R) : (size_t)i;
   int f = 0;
@@ -1864,6 +1876,7 @@ __global__ __launch_bounds__(256) void k_batch_fixup(const DevState* __restrict_
       r.scored = 0;
       r.score = 0;
     }
+    if (pa.res_out) pa.res_out[pa.first + i] = r;
   }
 }
 
@@ -3181,8 +3194,9 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
   auto leave = [&]() {
     if (ta.abort_out) {
       // the host completes a one-pod cycle on abort_out: every wave's stores (records, diagnostic rows,
-      // the resident state's write-back) are written back before the workgroup counts itself out
-      __threadfence();
+      // the resident state's write-back) reach L2 before thread 0's release writes it back and counts the
+      // workgroup out (one write-back per workgroup: a fence in every wave cost a 100k-node cycle 38 us)
+      __builtin_amdgcn_s_waitcnt(0);
       __syncthreads();
     }
     if (ta.abort_out && tid == 0) {

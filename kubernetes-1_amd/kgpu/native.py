@@ -23,7 +23,8 @@ EXPORTS = ["kgpu_abi_version", "kgpu_struct_sizes", "kgpu_create", "kgpu_destroy
            "kgpu_comm_info",
            "kgpu_debug_fail_alloc", "kgpu_debug_pts_state", "kgpu_debug_ipa_state", "kgpu_debug_broken_linear",
            "kgpu_debug_wg_trace", "kgpu_debug_topo_resident",
-           "kgpu_next_slot", "kgpu_adopt_pod", "kgpu_filter_reasons", "kgpu_debug_counters"]
+           "kgpu_next_slot", "kgpu_adopt_pod", "kgpu_filter_reasons", "kgpu_debug_counters",
+           "kgpu_schedule_batch_submit", "kgpu_schedule_batch_wait", "kgpu_pipelined"]
 
 
 class KgpuError(RuntimeError):
@@ -76,6 +77,9 @@ def lib():
     L.kgpu_select_victims.argtypes = [vp, vp, C.POINTER(abi.Pools), C.POINTER(abi.PreemptArgs), vp, vp,
                                       C.POINTER(i32)]
     L.kgpu_debug_counters.argtypes = [vp, vp, i32]
+    L.kgpu_schedule_batch_submit.argtypes = [vp, vp, i32, C.POINTER(abi.Pools), i64, vp, vp]
+    L.kgpu_schedule_batch_wait.argtypes = [vp]
+    L.kgpu_pipelined.argtypes = [vp]
     L.kgpu_filter_reasons.argtypes = [vp, C.POINTER(abi.ReasonArgs), vp, i64, C.POINTER(i64)]
     if L.kgpu_abi_version() != abi.ABI_VERSION:
         raise KgpuError(abi.E_STATE, "ABI version mismatch")
@@ -139,6 +143,29 @@ class Engine:
         self._check(lib().kgpu_schedule_batch(self.h, q.ctypes.data, len(q), C.byref(pools), first_seq,
                                               res.ctypes.data, C.byref(st)))
         return res, st
+
+    def schedule_batch_submit(self, queries, pools, first_seq=0, stats=None):
+        """kgpu_schedule_batch_submit: stage and launch a batch, return at once; schedule_batch_wait
+        completes the oldest batch in flight and returns its (results, stats).  The arrays handed to the
+        library stay referenced here until then."""
+        q = np.ascontiguousarray(queries, dtype=abi.QUERY)
+        res = np.zeros(len(q), abi.RESULT)
+        if not hasattr(self, "_inflight"):
+            self._inflight = []
+        self._inflight.append((q, res, stats, pools))
+        rc = lib().kgpu_schedule_batch_submit(self.h, q.ctypes.data, len(q), C.byref(pools), first_seq, res.ctypes.data,
+                                              C.byref(stats) if stats is not None else None)
+        if rc != 0:
+            self._inflight.pop()
+            self._check(rc)
+
+    def schedule_batch_wait(self):
+        q, res, stats, pools = self._inflight.pop(0)
+        self._check(lib().kgpu_schedule_batch_wait(self.h))
+        return res, stats
+
+    def pipelined(self):
+        return int(lib().kgpu_pipelined(self.h))
 
     def schedule_one(self, query, pools, seq=0, assume=True):
         q = np.ascontiguousarray(np.atleast_1d(query), dtype=abi.QUERY)
