@@ -283,7 +283,8 @@ struct kgpu_ctx {
     std::vector<kgpu_pod_query> qs;           // for the assumed pods' records (ForgetPod)
     std::vector<int32_t> ints;                // the pools' label pairs ...
     std::vector<kgpu_scalar_req> scalars;     // ... and scalar requests those records keep
-    int rc = KGPU_OK;                         // a batch the pipeline does not carry: ran in submit
+    int rc = KGPU_OK;                         // its outcome once done
+    bool done = false;                        // completed (a batch the pipeline does not carry: in submit)
     bool timed = false;
   };
   PipeSlot pipe[2];
@@ -3159,22 +3160,35 @@ bool pipe_eligible(const kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const
   return true;
 }
 
-int pipe_complete(kgpu_ctx* c);
+int pipe_finish(kgpu_ctx* c, kgpu_ctx::PipeBatch& b);
+int pipe_in_flight(const kgpu_ctx* c) {
+  int k = 0;
+  for (const auto& b : c->pipe_q) k += b.done ? 0 : 1;
+  return k;
+}
 
 int pipe_submit(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools* pools, int64_t first_seq,
                 kgpu_result* results, kgpu_stats* stats) {
   int rc;
   if (!pipe_eligible(c, qs, n, pools)) {
-    // not carried: complete what is in flight, run it synchronously, queue its outcome for its wait
-    while (!c->pipe_q.empty())
-      if ((rc = pipe_complete(c))) return rc;
+    // not carried: complete what is in flight (each keeps its outcome for its own wait), run it
+    // synchronously, queue its outcome for its wait
+    for (auto& b : c->pipe_q)
+      if (!b.done) pipe_finish(c, b);
     kgpu_ctx::PipeBatch b;
-    b.rc = run_batch(c, qs, n, pools, first_seq, results, stats, false, 1);
-    b.n = -1;
+    b.rc = c->uploaded ? run_batch(c, qs, n, pools, first_seq, results, stats, false, 1)
+                       : fail(c, KGPU_E_STATE, "no snapshot uploaded");
+    b.done = true;
     c->pipe_q.push_back(std::move(b));
     return KGPU_OK;
   }
-  if (c->pipe_q.size() >= 2 && (rc = pipe_complete(c))) return rc;
+  if (pipe_in_flight(c) >= 2) {
+    for (auto& b : c->pipe_q)
+      if (!b.done) {
+        pipe_finish(c, b);
+        break;
+      }
+  }
   int per = 0, groups = 0;
   const int kidx = kgpu::batch_geometry(c->st.N, std::min(c->max_groups > 0 ? std::min(c->max_groups, c->n_cus) : c->n_cus, 256),
                                         &per, &groups, c->batch_geo_first);
@@ -3292,28 +3306,29 @@ int pipe_submit(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_poo
   return KGPU_OK;
 }
 
-// Completes the oldest batch in flight: its records, the assumed pods' bookkeeping, its stats.
-int pipe_complete(kgpu_ctx* c) {
-  if (c->pipe_q.empty()) return fail(c, KGPU_E_STATE, "no pipelined batch in flight");
-  kgpu_ctx::PipeBatch b = std::move(c->pipe_q.front());
-  c->pipe_q.pop_front();
-  if (b.n < 0) return b.rc;  // ran synchronously in submit
+// Completes a batch in flight in place: its records, the assumed pods' bookkeeping, its stats; its
+// outcome waits for its own kgpu_schedule_batch_wait.
+int pipe_finish(kgpu_ctx* c, kgpu_ctx::PipeBatch& b) {
+  b.done = true;
+  b.rc = KGPU_OK;
   kgpu_ctx::PipeSlot& ps = c->pipe[b.slot];
-  HIP_OK(c, hipEventSynchronize(ps.done));
+  if (hipEventSynchronize(ps.done) != hipSuccess) {
+    c->uploaded = false;
+    return b.rc = fail(c, KGPU_E_DEVICE, "pipelined batch: event synchronize failed");
+  }
+  if (!c->uploaded) return b.rc = fail(c, KGPU_E_STATE, "the device mirror was invalidated by an earlier batch");
   const kgpu_result* res = static_cast<const kgpu_result*>(ps.res);
   const int32_t abort = __atomic_load_n(reinterpret_cast<const int32_t*>(res + b.n), __ATOMIC_ACQUIRE);
   if (abort != 0) {
     // no re-issue here: the next batch already ran on top of this one
     c->uploaded = false;
-    c->pipe_q.clear();
-    (void)sync_stream(c);
-    return fail(c, KGPU_E_DEVICE, "pipelined persistent run gave up waiting for a workgroup; the device mirror is "
-                                  "invalid: re-upload the snapshot");
+    return b.rc = fail(c, KGPU_E_DEVICE, "pipelined persistent run gave up waiting for a workgroup; the device "
+                                         "mirror is invalid: re-upload the snapshot");
   }
   std::memcpy(b.results, res, sizeof(kgpu_result) * (size_t)b.n);
   if (b.stats) {
     float ms = 0.f;
-    HIP_OK(c, hipEventElapsedTime(&ms, ps.t0, ps.t1));
+    if (hipEventElapsedTime(&ms, ps.t0, ps.t1) != hipSuccess) ms = 0.f;
     b.stats->pods += b.n;
     b.stats->device_ms += ms;
     int64_t placed = 0;
@@ -3345,6 +3360,15 @@ int pipe_complete(kgpu_ctx* c) {
   }
   c->last_diag = false;
   return KGPU_OK;
+}
+
+// kgpu_schedule_batch_wait: the oldest batch submitted and not yet waited for.
+int pipe_complete(kgpu_ctx* c) {
+  if (c->pipe_q.empty()) return fail(c, KGPU_E_STATE, "no pipelined batch in flight");
+  if (!c->pipe_q.front().done) pipe_finish(c, c->pipe_q.front());
+  const int rc = c->pipe_q.front().rc;
+  c->pipe_q.pop_front();
+  return rc;
 }
 
 }  // namespace
