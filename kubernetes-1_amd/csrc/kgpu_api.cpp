@@ -1215,7 +1215,7 @@ size_t a16(size_t x) { return (x + 15) & ~(size_t)15; }
 constexpr size_t kTMiscBytes = 1024;
 
 // LDS layout of a run (byte offsets into the dynamic region); returns the total
-size_t t_layout(const TRun& tr, kgpu::TBatchArgs* a, int B, int lab_keys = 0, int per = 0) {
+size_t t_layout(const TRun& tr, kgpu::TBatchArgs* a, int B, int lab_keys = 0, int per = 0, size_t wlab_n = 0) {
   size_t o = a16((size_t)tr.lds_bins * 4);
   const size_t o_reg = o;
   o = a16(o + (size_t)tr.reg_words * 4);
@@ -1236,7 +1236,11 @@ size_t t_layout(const TRun& tr, kgpu::TBatchArgs* a, int B, int lab_keys = 0, in
   o = a16(o + kTMiscBytes);
   const size_t o_lab = o;
   o = a16(o + (size_t)lab_keys * (size_t)per * 4);
+  const size_t o_wlab = o;
+  o = a16(o + wlab_n * 4);
   if (a) {
+    a->o_wlab = (int32_t)o_wlab;
+    a->wlab = wlab_n > 0 ? 1 : 0;
     a->o_lab = (int32_t)o_lab;
     a->lab_keys = lab_keys;
     a->o_reg = (int32_t)o_reg;
@@ -1509,7 +1513,10 @@ int run_tbatch(kgpu_ctx* c, TRun& tr, int first, int count, int64_t first_seq, i
   // would only add a round of loads to its start)
   int lab_keys = count == 1 ? 0 : std::min(c->st.K, 16);
   while (lab_keys > 0 && t_layout(tr, nullptr, 512, lab_keys, per) > (size_t)kgpu::kTLdsBudget) --lab_keys;
-  size_t lds = t_layout(tr, &a, 512, lab_keys, per);
+  // every node's label values of the delta keys, for the winner's (a batch run, when they fit too)
+  size_t wlab_n = (count > 1 && !xg && c->st.K > 0) ? (size_t)c->st.K * (size_t)c->st.N : 0;
+  if (wlab_n && t_layout(tr, nullptr, 512, lab_keys, per, wlab_n) > (size_t)kgpu::kTLdsBudget) wlab_n = 0;
+  size_t lds = t_layout(tr, &a, 512, lab_keys, per, wlab_n);
   // at least half a CU's LDS: one persistent workgroup per CU (two would share its SIMDs)
   a.lds_bytes = (int32_t)std::max<size_t>(lds, 96 * 1024);
   const size_t N = (size_t)c->st.N;

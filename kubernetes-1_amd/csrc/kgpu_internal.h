@@ -412,6 +412,9 @@ struct TBatchArgs {
   // byte offsets of the LDS regions (histogram bins start at 0)
   int32_t o_reg, o_tot, o_sany, o_stat, o_smask, o_zsum, o_misc, o_pt, o_lab;
   int32_t lab_keys;       // node label keys cached in LDS per workgroup ([lab_keys][per] value ids)
+  int32_t wlab;           // 1: every node's values of the n_keys keys in LDS at o_wlab ([n_keys][N]): the assume
+                          // phase reads the winner's labels there instead of a dependent global load
+  int32_t o_wlab;
   int32_t abort_at;       // KGPU_OPT_ABORT_AT test hook (-1: never), as in BatchArgs
   int32_t diag;           // kgpu_schedule_one: status word and per-plugin raw / normalized scores of every
                           // node (the run is one pod; every lane zeroes its nodes' diagnostic rows first)

@@ -3249,6 +3249,22 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
     for (int u = 0; u < kU; ++u)
       if (base + u * B + tid < nlab) LAB[base + u * B + tid] = v[u];
   }
+  // every node's delta-key labels (ta.wlab): the winner's come from here in the assume phase
+  int32_t* WLAB = reinterpret_cast<int32_t*>(lds_raw + ta.o_wlab);
+  if (!XG && ta.wlab) {
+    const int nw = ta.n_keys * st.N;
+    for (int base = 0; base < nw; base += kU * B) {
+      int32_t v[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int i = base + u * B + tid;
+        v[u] = i < nw ? gp(st.label_val)[i] : -1;  // label_val is [K][N]: the same layout
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u)
+        if (base + u * B + tid < nw) WLAB[base + u * B + tid] = v[u];
+    }
+  }
   if (tid == 0) M.abort = 0;
   if constexpr (XG) {
     if (tid < ta.nranks) sh_ptx[tid] = ta.ptx[tid];
@@ -3793,7 +3809,7 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
       // the winner's label values and signature bits, staged once for every delta (XG: from the
       // winning rank's record, staged by wave 0)
       if constexpr (!XG) {
-        if (tid < ta.n_keys) M.wlab[tid] = gp(st.label_val)[(size_t)tid * st.N + wl];
+        if (tid < ta.n_keys) M.wlab[tid] = ta.wlab ? WLAB[tid * st.N + wl] : gp(st.label_val)[(size_t)tid * st.N + wl];
         else if (tid >= 64 && tid - 64 < ta.n_sigs) M.welig[tid - 64] = tb_elig(ta, tid - 64, wl) ? 1 : 0;
         __syncthreads();
       }
