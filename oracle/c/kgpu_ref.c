@@ -1097,8 +1097,9 @@ typedef struct {
   const kgpu_pod_query* q;
   int phase; /* 0 filter, 1 score */
   int n, chunk;
-  _Atomic int next;
-  _Atomic int done;  /* items processed (parallel_until's join) */
+  _Alignas(64) _Atomic int next;
+  _Alignas(64) _Atomic int done;  /* items processed (parallel_until's join), on a line of its own */
+  _Alignas(64) char pad_;
   uint32_t* status;
   const int* feasible;
   int nf;
