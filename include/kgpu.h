@@ -639,6 +639,10 @@ int kgpu_read_nodes(kgpu_ctx* ctx, int64_t* req_cpu, int64_t* req_mem, int64_t* 
 /* KGPU_OPT_HOLD_GROUP (17): test hook -- on an ordinary (non-cooperative) persistent launch, workgroup
  * `value` leaves at once, as a workgroup that never became resident (-1, the default: none). */
 #define KGPU_OPT_HOLD_GROUP 17
+/* KGPU_OPT_TBATCH_WLAB (18): 1 (default) = a persistent topology batch run keeps every node's label values
+ * of the delta keys in LDS when they fit, so the assume phase reads the winner's labels there; 0 = a global
+ * load per pod (A/B switch). */
+#define KGPU_OPT_TBATCH_WLAB 18
 int kgpu_set_option(kgpu_ctx* ctx, int32_t option, int64_t value);
 /* Engine counters: out[0] = calls issued again with a cooperative launch after a persistent run's
  * workgroups were not all resident before its first pod (KGPU_OPT_COOPERATIVE); out[1] = persistent

@@ -261,6 +261,7 @@ struct kgpu_ctx {
   bool force_coop = false;          // a call issued again after a clean abort (every persistent launch
                                     // of it cooperative)
   int32_t hold_group = -1;          // KGPU_OPT_HOLD_GROUP test hook
+  bool tbatch_wlab = true;          // KGPU_OPT_TBATCH_WLAB
   int64_t n_coop_retry = 0, n_persist = 0, n_coop = 0;  // kgpu_debug_counters
   int state_launches = 0;           // launches of the current call that may change device state
   // pipelined batches (kgpu_schedule_batch_submit / _wait): two slots, each with its pinned staging block,
@@ -1514,7 +1515,7 @@ int run_tbatch(kgpu_ctx* c, TRun& tr, int first, int count, int64_t first_seq, i
   int lab_keys = count == 1 ? 0 : std::min(c->st.K, 16);
   while (lab_keys > 0 && t_layout(tr, nullptr, 512, lab_keys, per) > (size_t)kgpu::kTLdsBudget) --lab_keys;
   // every node's label values of the delta keys, for the winner's (a batch run, when they fit too)
-  size_t wlab_n = (count > 1 && !xg && c->st.K > 0) ? (size_t)c->st.K * (size_t)c->st.N : 0;
+  size_t wlab_n = (count > 1 && !xg && c->st.K > 0 && c->tbatch_wlab) ? (size_t)c->st.K * (size_t)c->st.N : 0;
   if (wlab_n && t_layout(tr, nullptr, 512, lab_keys, per, wlab_n) > (size_t)kgpu::kTLdsBudget) wlab_n = 0;
   size_t lds = t_layout(tr, &a, 512, lab_keys, per, wlab_n);
   // at least half a CU's LDS: one persistent workgroup per CU (two would share its SIMDs)
@@ -3701,6 +3702,7 @@ int kgpu_set_option(kgpu_ctx* c, int32_t option, int64_t value) try {
   } else if (option == KGPU_OPT_ARENA_BYTES) c->ar_limit = (size_t)std::min<int64_t>(std::max<int64_t>(0, value), (int64_t)kArenaBytes);
   else if (option == KGPU_OPT_ABORT_AT) c->abort_at = value < 0 || value > INT32_MAX ? -1 : (int32_t)value;
   else if (option == KGPU_OPT_XGMI) c->xgmi = value != 0;
+  else if (option == KGPU_OPT_TBATCH_WLAB) c->tbatch_wlab = value != 0;
   else if (option == KGPU_OPT_HOLD_GROUP) c->hold_group = value < 0 || value > INT32_MAX ? -1 : (int32_t)value;
   else if (option == KGPU_OPT_SKIP_RELEASE_AT) c->skip_release_at = value < 0 || value > INT32_MAX ? -1 : (int32_t)value;
   else return KGPU_E_INVAL;

@@ -19,7 +19,7 @@ def _big(seed, n_nodes=1500, n_existing=600, n_pods=80):
     return nodes, ex, pods, services, rss
 
 
-def _run(args, tfast=1, groups=0, threads=4, geo=None, ahead=None):
+def _run(args, tfast=1, groups=0, threads=4, geo=None, ahead=None, wlab=None):
     from oracle.cref import RefEngine
     nodes, ex, pods, services, rss = args
     fw = GpuFramework(Profile(), nodes, ex, cluster=Cluster(services=services, rss=rss), pods_hint=pods)
@@ -34,6 +34,8 @@ def _run(args, tfast=1, groups=0, threads=4, geo=None, ahead=None):
         fw.engine.set_option(abi.OPT_TBATCH_GEO, geo)
     if ahead is not None:
         fw.engine.set_option(abi.OPT_TOPO_AHEAD, ahead)
+    if wlab is not None:
+        fw.engine.set_option(abi.OPT_TBATCH_WLAB, wlab)
     got, _ = fw.engine.schedule_batch(q, pc)
     return fw, w, got, want.read_nodes(), fw.engine.read_nodes(fw.snap.n_nodes)
 
@@ -59,6 +61,16 @@ def test_gpu_tbatch_random_matches_c_restatement(seed, groups):
 def test_gpu_tbatch_small_clusters(seed):
     """One workgroup, most lanes idle, every plugin input of gen_random.topo_cluster."""
     fw, w, got, rw, rg = _run(gen_random.topo_cluster(seed, n_nodes=40, n_existing=60, n_pods=60), tfast=1)
+    _check(w, got, rw, rg)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("wlab", [0, 1])
+@pytest.mark.parametrize("seed", [3])
+def test_gpu_tbatch_winner_labels_switch(seed, wlab):
+    """KGPU_OPT_TBATCH_WLAB 0 / 1: the winner's label values from global memory or from the run's LDS
+    copy of every node's: both against the C restatement."""
+    fw, w, got, rw, rg = _run(_big(seed, n_nodes=1200, n_existing=500, n_pods=70), tfast=1, wlab=wlab)
     _check(w, got, rw, rg)
 
 
