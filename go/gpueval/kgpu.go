@@ -254,6 +254,19 @@ func (e *engine) filterWords(n int) ([]uint32, error) {
 	return w[:n], kerr(e.ctx, rc)
 }
 
+// filterWordsAll copies the last scheduleOne's per-plugin status words under KGPU_OPT_RUN_ALL_FILTERS:
+// [filter position][node], each in filterWords' format (0: the plugin passed the node).
+func (e *engine) filterWordsAll(nf, n int) ([]uint32, error) {
+	w := make([]uint32, nf*n+1)
+	rc := C.kgpu_get_filter_all(e.ctx, (*C.uint32_t)(unsafe.Pointer(&w[0])))
+	return w[:nf*n], kerr(e.ctx, rc)
+}
+
+// setOption is kgpu_set_option.
+func (e *engine) setOption(opt C.int32_t, v int64) error {
+	return kerr(e.ctx, C.kgpu_set_option(e.ctx, opt, C.int64_t(v)))
+}
+
 // scores returns one score plugin's raw and normalized (unweighted) values per node.
 func (e *engine) scores(plugin int, n int) (raw, norm []int64, err error) {
 	raw, norm = make([]int64, n+1), make([]int64, n+1)

@@ -57,6 +57,11 @@ type profileArgs struct {
 	Mode                   string // "select" or "shadow"
 	ExactSync              bool   // compare every NodeInfo generation at every sync (track.go)
 	BatchAhead             int    // > 1: schedule the pod with the next BatchAhead-1 queued pods (ahead.go)
+	// RunAllFilters mirrors the framework's runAllFilters (framework.go:90,155-160,494), which the
+	// scheduler sets from the legacy Policy's AlwaysCheckAllPredicates (factory.go:107,278-281): every
+	// filter plugin runs on every node and Filter returns the merged status with every failing
+	// plugin's reasons (KGPU_OPT_RUN_ALL_FILTERS).  Set it together with that Policy field.
+	RunAllFilters          bool
 	ignoredResources       map[string]struct{}
 }
 
@@ -144,6 +149,7 @@ func (c *compiler) config() *C.kgpu_config {
 // cycle is the per-pod state read by Filter and Score (and by the shadow score plugins).
 type cycle struct {
 	words  []uint32           // per-node filter status words (node index order)
+	all    []uint32           // RunAllFilters: [filter position][node] each plugin's own word
 	norm   map[int32][]int64  // shadow mode: per score plugin id, the device-normalized 0-100 value per node
 	index  map[string]int32   // node name -> node index of this cycle's mirror
 	chosen int32              // device-selected node index, -1 = FitError
@@ -238,6 +244,12 @@ func (g *GpuEval) upload(list []*framework.NodeInfo, a *arena) error {
 		eng, err := newEngine(c.config())
 		if err != nil {
 			return err
+		}
+		if g.prof.RunAllFilters {
+			if err := eng.setOption(C.KGPU_OPT_RUN_ALL_FILTERS, 1); err != nil {
+				eng.close()
+				return err
+			}
 		}
 		g.eng = eng
 	}
@@ -493,6 +505,17 @@ func (g *GpuEval) PreFilter(ctx context.Context, cs *framework.CycleState, pod *
 		return framework.NewStatus(framework.Error, err.Error())
 	}
 	c := &cycle{words: words, chosen: int32(res.node), index: g.mir.index, rq: g.rq}
+	if g.prof.RunAllFilters {
+		nf := 0 // the profile's device filters (compiler.config's kgpu_config.filters)
+		for _, f := range g.prof.Filters {
+			if _, ok := filterIDs[f]; ok {
+				nf++
+			}
+		}
+		if c.all, err = g.eng.filterWordsAll(nf, n); err != nil {
+			return framework.NewStatus(framework.Error, err.Error())
+		}
+	}
 	if g.prof.Mode == "shadow" {
 		// every replaced score plugin's normalized (unweighted) value per node: the shadow plugins
 		// return them, the framework weights and sums them (framework.go:632-648)
@@ -531,9 +554,25 @@ func (g *GpuEval) Filter(ctx context.Context, cs *framework.CycleState, pod *v1.
 	if w == 0 || w == C.KGPU_FS_NOT_EVALUATED {
 		return nil
 	}
-	rs, err := g.filterReasons(c.rq, i, w, ni.Node())
-	if err != nil {
-		return framework.NewStatus(framework.Error, err.Error())
+	if c.all == nil {
+		rs, err := g.filterReasons(c.rq, i, w, ni.Node())
+		if err != nil {
+			return framework.NewStatus(framework.Error, err.Error())
+		}
+		return framework.NewStatus(framework.Code((w>>8)&3), rs...)
+	}
+	// runAllFilters: PluginToStatus.Merge (interface.go:162-191) of every failing plugin's status --
+	// the merged code is w's, the reasons every failing plugin's in profile order
+	n := len(c.words)
+	var rs []string
+	for p := 0; p*n < len(c.all); p++ {
+		if wp := c.all[p*n+int(i)]; wp != 0 {
+			r, err := g.filterReasons(c.rq, i, wp, ni.Node())
+			if err != nil {
+				return framework.NewStatus(framework.Error, err.Error())
+			}
+			rs = append(rs, r...)
+		}
 	}
 	return framework.NewStatus(framework.Code((w>>8)&3), rs...)
 }

@@ -15,6 +15,7 @@
  *   kgpu_schedule_batch             scheduleOne loop (scheduler.go:509-593) with on-device assume
  *                                   (cache.AssumePod cache.go:338 -> NodeInfo.AddPod types.go:456)
  *   kgpu_get_filter                 per-node PluginToStatus.Merge code (framework.go:477-502)
+ *   kgpu_get_filter_all             runAllFilters: every plugin's status per node (framework.go:484-499)
  *   kgpu_get_scores                 PluginToNodeScores (framework.go:579-656), raw and normalized
  *   kgpu_forget_pod                 cache.ForgetPod (cache.go:383-410) -> NodeInfo.RemovePod (types.go:484)
  *   kgpu_apply_delta                the NodeInfo side of the informer / cache event stream between two
@@ -426,6 +427,13 @@ int kgpu_pipelined(const kgpu_ctx* ctx);
 /* Diagnostics for the last kgpu_schedule_one: per-node filter status words, and per-node raw /
  * normalized (unweighted) scores of one score plugin over the feasible nodes (others: 0). */
 int kgpu_get_filter(kgpu_ctx* ctx, uint32_t* status_words);
+/* KGPU_OPT_RUN_ALL_FILTERS: the last kgpu_schedule_one cycle's per-plugin status words,
+ * [n_filters][N] in profile filter order -- row i holds filter i's word for every node (0: it passed),
+ * each word in kgpu_get_filter's format with its own position; PluginToStatus {plugin: Status} of a
+ * node is the non-zero words of its column, and kgpu_filter_reasons formats each of them.
+ * Replaces framework.go:484-499's statuses map under runAllFilters.  KGPU_E_STATE when the last cycle
+ * did not run with the option. */
+int kgpu_get_filter_all(kgpu_ctx* ctx, uint32_t* status_words);
 int kgpu_get_scores(kgpu_ctx* ctx, int32_t plugin, int64_t* raw, int64_t* normalized);
 
 /* ---- Filter status reasons (kgpu_filter_reasons).  A node taint as the caller's NodeInfo holds it. */
@@ -643,6 +651,17 @@ int kgpu_read_nodes(kgpu_ctx* ctx, int64_t* req_cpu, int64_t* req_mem, int64_t* 
  * of the delta keys in LDS when they fit, so the assume phase reads the winner's labels there; 0 = a global
  * load per pod (A/B switch). */
 #define KGPU_OPT_TBATCH_WLAB 18
+/* KGPU_OPT_TBATCH_OWN (19): 1 = in the persistent topology kernel's exchanges a workgroup takes its own
+ * statistics and key granules from LDS / registers instead of loading its own stores back; 0 (default) =
+ * every granule loaded (1 measured 1-3 % slower; A/B switch). */
+#define KGPU_OPT_TBATCH_OWN 19
+/* KGPU_OPT_RUN_ALL_FILTERS (20): the framework's runAllFilters (framework.go:90,155-160,484-499; set from
+ * the legacy Policy's AlwaysCheckAllPredicates, factory.go:107,278-281).  1 = a kgpu_schedule_one cycle
+ * runs every filter plugin on every node: kgpu_get_filter's word becomes PluginToStatus.Merge's
+ * (interface.go:162-191: UnschedulableAndUnresolvable over Unschedulable; the position and detail bits
+ * stay the first failing plugin's) and kgpu_get_filter_all returns each plugin's own word; preemption's
+ * nodesWherePreemptionMightHelp reads the merged code.  Placements do not change.  Default 0. */
+#define KGPU_OPT_RUN_ALL_FILTERS 20
 int kgpu_set_option(kgpu_ctx* ctx, int32_t option, int64_t value);
 /* Engine counters: out[0] = calls issued again with a cooperative launch after a persistent run's
  * workgroups were not all resident before its first pod (KGPU_OPT_COOPERATIVE); out[1] = persistent

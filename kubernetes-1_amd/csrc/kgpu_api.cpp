@@ -262,6 +262,9 @@ struct kgpu_ctx {
                                     // of it cooperative)
   int32_t hold_group = -1;          // KGPU_OPT_HOLD_GROUP test hook
   bool tbatch_wlab = true;          // KGPU_OPT_TBATCH_WLAB
+  bool tbatch_own = false;          // KGPU_OPT_TBATCH_OWN (measured slower: DESIGN.md 4.4)
+  bool run_all = false;             // KGPU_OPT_RUN_ALL_FILTERS
+  bool last_run_all = false;        // the last diagnostic cycle wrote status_all
   int64_t n_coop_retry = 0, n_persist = 0, n_coop = 0;  // kgpu_debug_counters
   int state_launches = 0;           // launches of the current call that may change device state
   // pipelined batches (kgpu_schedule_batch_submit / _wait): two slots, each with its pinned staging block,
@@ -1708,6 +1711,7 @@ int run_tbatch(kgpu_ctx* c, TRun& tr, int first, int count, int64_t first_seq, i
   // were it not, the spin timeouts raise the abort word instead of hanging.
   const bool coop = (c->coop && !(count == 1 && !xg)) || c->force_coop;
   a.hold = coop ? -1 : c->hold_group;
+  a.own_gran = c->tbatch_own ? 1 : 0;
   ++c->n_persist;
   c->n_coop += coop ? 1 : 0;
   ++c->state_launches;
@@ -2029,6 +2033,9 @@ int run_batch_once(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_
   }
   DevState st = c->st;
   st.ticket = static_cast<int32_t*>(c->ticket.p);
+  // runAllFilters: a diagnostic cycle's statuses merge every failing plugin (k_eval's runtime profile,
+  // k_topo_filter, k_victims' nominated pass); placements do not depend on it
+  st.run_all = (diag && c->run_all) ? 1 : 0;
   st.queries = short_cycle ? reinterpret_cast<const kgpu_pod_query*>(static_cast<char*>(c->dstate.p) + kDsQueryOff)
                            : static_cast<const kgpu_pod_query*>(c->queries.p);
   // a short cycle's records go straight to pinned host memory (no read-back copy)
@@ -2146,7 +2153,8 @@ int run_batch_once(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_
   // instantiation); without them, the per-pod RCCL pipeline
   // a diagnostic cycle (kgpu_schedule_one: status words and per-plugin scores) of one topology pod
   // runs as a one-pod persistent run too
-  const int tgeo = (topo_on && c->tfast && (!diag || n == 1) && (!sharded || xg) && !cut && !nom_dev && st.K <= 64)
+  const int tgeo = (topo_on && c->tfast && (!diag || (n == 1 && !st.run_all)) && (!sharded || xg) && !cut && !nom_dev &&
+                    st.K <= 64)
                        ? kgpu::tbatch_geometry(st.N, std::min(c->max_groups > 0 ? std::min(c->max_groups, c->n_cus) : c->n_cus, 256),
                                                &tper, &tgroups, c->tbatch_geo_first)
                        : -1;
@@ -2378,7 +2386,7 @@ int run_batch_once(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_
         if (c->timing) HIP_OK(c, hipEventRecord(get_event(c, ev), c->stream));
         if (nom_dev && kgpu::launch_victims(dst, nom_dev, st.N, c->stream))
           return fail(c, KGPU_E_DEVICE, "k_victims launch failed");
-        if (kgpu::launch_eval(dst, a, blocks, c->spec, c->stream))
+        if (kgpu::launch_eval(dst, a, blocks, st.run_all ? 0 : c->spec, c->stream))  // run-all: the runtime profile
           return fail(c, KGPU_E_DEVICE, "k_eval launch failed");
         if (cut && kgpu::launch_cut(dst, a, blocks, c->cfg.n_filters, c->stream))
           return fail(c, KGPU_E_DEVICE, "k_cut launch failed");
@@ -2536,6 +2544,7 @@ int run_batch_once(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_
     }
   }
   c->last_diag = diag;
+  c->last_run_all = diag && c->run_all;
   if (c->htrace) {
     ht(c, 10);  // 10: records, assumed-pod bookkeeping
     std::array<int64_t, kgpu_ctx::kHt> row{};
@@ -2555,6 +2564,7 @@ int alloc_node_work(kgpu_ctx* c) {
   auto& W = c->work_allocs;
   int rc;
   if ((rc = dalloc(c, W, &st.status, N))) return rc;
+  if ((rc = dalloc(c, W, &st.status_all, (size_t)KGPU_NUM_FILTERS * N))) return rc;
   if ((rc = dalloc(c, W, &st.raw_taint, N))) return rc;
   if ((rc = dalloc(c, W, &st.raw_na, N))) return rc;
   if ((rc = dalloc(c, W, &st.partial, N))) return rc;
@@ -3703,6 +3713,8 @@ int kgpu_set_option(kgpu_ctx* c, int32_t option, int64_t value) try {
   else if (option == KGPU_OPT_ABORT_AT) c->abort_at = value < 0 || value > INT32_MAX ? -1 : (int32_t)value;
   else if (option == KGPU_OPT_XGMI) c->xgmi = value != 0;
   else if (option == KGPU_OPT_TBATCH_WLAB) c->tbatch_wlab = value != 0;
+  else if (option == KGPU_OPT_TBATCH_OWN) c->tbatch_own = value != 0;
+  else if (option == KGPU_OPT_RUN_ALL_FILTERS) c->run_all = value != 0;
   else if (option == KGPU_OPT_HOLD_GROUP) c->hold_group = value < 0 || value > INT32_MAX ? -1 : (int32_t)value;
   else if (option == KGPU_OPT_SKIP_RELEASE_AT) c->skip_release_at = value < 0 || value > INT32_MAX ? -1 : (int32_t)value;
   else return KGPU_E_INVAL;
@@ -4072,6 +4084,8 @@ int kgpu_select_victims(kgpu_ctx* c, const kgpu_pod_query* q, const kgpu_pools* 
   st.queries = static_cast<const kgpu_pod_query*>(c->queries.p);
   st.diag_raw = nullptr;
   st.diag_norm = nullptr;
+  // nodesWherePreemptionMightHelp reads the cycle's merged code (framework.go:494 runAllFilters)
+  st.run_all = c->run_all ? 1 : 0;
   // potential victims per local node, MoreImportantPod order (stable over the caller's order)
   PreemptStage ps;
   std::vector<int32_t> pos_of;  // sorted position -> caller's victim index
@@ -4328,6 +4342,19 @@ int kgpu_get_filter(kgpu_ctx* c, uint32_t* words) try {
   if (!c || !words) return KGPU_E_INVAL;
   if (!c->last_diag) return fail(c, KGPU_E_STATE, "no kgpu_schedule_one cycle to report");
   HIP_OK(c, hipMemcpy(words, c->st.status, sizeof(uint32_t) * (size_t)c->st.N, hipMemcpyDeviceToHost));
+  return KGPU_OK;
+} catch (...) {
+  return on_exception(c, false);
+}
+
+int kgpu_get_filter_all(kgpu_ctx* c, uint32_t* words) try {
+  if (c && !c->pipe_q.empty())
+    return fail(c, KGPU_E_STATE, "pipelined batches in flight: complete them with kgpu_schedule_batch_wait first");
+  if (!c || !words) return KGPU_E_INVAL;
+  if (!c->last_diag || !c->last_run_all)
+    return fail(c, KGPU_E_STATE, "no kgpu_schedule_one cycle under KGPU_OPT_RUN_ALL_FILTERS to report");
+  const size_t nf = (size_t)c->cfg.n_filters, N = (size_t)c->st.N;
+  if (nf * N) HIP_OK(c, hipMemcpy(words, c->st.status_all, sizeof(uint32_t) * nf * N, hipMemcpyDeviceToHost));
   return KGPU_OK;
 } catch (...) {
   return on_exception(c, false);

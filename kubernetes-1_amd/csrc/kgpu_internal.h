@@ -219,6 +219,12 @@ struct DevState {
   const uint32_t* nom_status;
   // zeroed word: k_final's last workgroup ticket when it resolves its own pod (PodArgs.resolve_self)
   int32_t* ticket;
+  // ---- runAllFilters (framework.go:90,494; KGPU_OPT_RUN_ALL_FILTERS): a diagnostic cycle runs every
+  // filter plugin on every node, status[n] becomes PluginToStatus.Merge's word (the first failing
+  // plugin's position and detail, the merged code) and status_all[i][n] the i-th plugin's own word
+  uint32_t* status_all;                 // [KGPU_NUM_FILTERS][N]
+  int32_t run_all;
+  int32_t pad3;
 };
 // Filter status word of a node the cycle never examined (findNodesThatPassFilters stopped before
 // it), or of the feasible node whose discovery cancelled the search: not in `filtered` and not in
@@ -425,6 +431,8 @@ struct TBatchArgs {
   int32_t zero_n16;       // the other resident-state buffer: its first zero_n16 16-byte words are zeroed by
                           // the grid at kernel entry, so the next miss starts from zeros without a memset
   int32_t hold;           // KGPU_OPT_HOLD_GROUP test hook, as in BatchArgs
+  int32_t own_gran;       // 1: a workgroup's own statistics / key granules are taken from LDS / registers in
+                          // its polls instead of loaded back (KGPU_OPT_TBATCH_OWN)
   struct alignas(16) Z16 { uint64_t lo, hi; };
   Z16* zero_buf;
   int64_t* trace;        // null, or [count + 1][16] s_memrealtime stamps (KGPU_OPT_PHASE_TRACE): per pod

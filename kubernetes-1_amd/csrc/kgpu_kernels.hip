@@ -509,11 +509,35 @@ __device__ __forceinline__ uint32_t filter_one(int f, const DevState& st, const 
   }
 }
 
+// PluginToStatus.Merge (interface.go:162-191) of the words so far and the next failing plugin's word:
+// UnschedulableAndUnresolvable wins over Unschedulable (the device's filters return no Error); the
+// first failing plugin keeps the position and detail bits (its reasons come first).
+__device__ __forceinline__ uint32_t merge_status(uint32_t acc, uint32_t w) {
+  if (!acc) return w;
+  const uint32_t ca = (acc >> 8) & 3u, cw = (w >> 8) & 3u;
+  return cw > ca ? (acc & ~(3u << 8)) | (cw << 8) : acc;
+}
+
+// runAllFilters (framework.go:484-499 without the early exit): every plugin of the profile, each word
+// in status_all, the merged word returned.
+__device__ __noinline__ uint32_t run_filters_all(const DevState& st, const kgpu_pod_query& q, const NodeRes& r, int n,
+                                                 const QPlan* pl) {
+  uint32_t acc = 0;
+  for (int i = 0; i < st.n_filters; ++i) {
+    const uint32_t c = filter_one(cp(st.filters)[i], st, q, r, n, pl);
+    const uint32_t w = c ? c | (uint32_t)(i + 1) : 0u;
+    gp(st.status_all)[(size_t)i * st.N + n] = w;
+    acc = w ? merge_status(acc, w) : acc;
+  }
+  return acc;
+}
+
 // Filters in profile order; the first failure's 1-based position goes in the low byte.
 template <uint32_t FM, int F = 0>
 __device__ __forceinline__ uint32_t run_filters(const DevState& st, const kgpu_pod_query& q, const NodeRes& r, int n,
                                                 const QPlan* pl = nullptr) {
   if constexpr (FM == kRuntime) {
+    if (st.run_all) return run_filters_all(st, q, r, n, pl);
     for (int i = 0; i < st.n_filters; ++i) {
       const uint32_t c = filter_one(cp(st.filters)[i], st, q, r, n, pl);
       if (c) return c | (uint32_t)(i + 1);
@@ -1385,15 +1409,19 @@ struct Sweep {
   uint64_t v[NJ];
   int abort;
 };
+// Granule `own` (-1: none) is the caller's own, value `ownv`: not loaded.
 template <int NJ, bool SYS>
-__device__ __forceinline__ Sweep<NJ> sweep(const uint64_t* row, int G, const int32_t* abort_word, uint64_t fill) {
+__device__ __forceinline__ Sweep<NJ> sweep(const uint64_t* row, int G, const int32_t* abort_word, uint64_t fill,
+                                           int own = -1, uint64_t ownv = 0) {
   const int lane = threadIdx.x & 63;
   Sweep<NJ> s;
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     uint64_t* p = const_cast<uint64_t*>(row + lane + 64 * j);
-    s.v[j] = (lane + 64 * j < G) ? (SYS ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : load_sc1(p))
-                                 : fill;  // a valid granule with key 0
+    const int gg = lane + 64 * j;
+    s.v[j] = gg == own ? ownv
+                       : (gg < G ? (SYS ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : load_sc1(p))
+                                 : fill);  // a valid granule with key 0
   }
   s.abort = load_sc1(abort_word);
   return s;
@@ -1426,14 +1454,14 @@ __device__ __forceinline__ bool row_done(const Sweep<NJ>& cur, uint64_t tmask, u
 }
 template <int NJ, bool SYS>
 __device__ __forceinline__ bool poll_row(const uint64_t* row, int G, const int32_t* abort_word, uint64_t tmask,
-                                         uint64_t expect, uint64_t& wkey, int& wg) {
+                                         uint64_t expect, uint64_t& wkey, int& wg, int own = -1, uint64_t ownv = 0) {
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  Sweep<NJ> a = sweep<NJ, SYS>(row, G, abort_word, expect);
+  Sweep<NJ> a = sweep<NJ, SYS>(row, G, abort_word, expect, own, ownv);
   for (;;) {
-    const Sweep<NJ> b = sweep<NJ, SYS>(row, G, abort_word, expect);
+    const Sweep<NJ> b = sweep<NJ, SYS>(row, G, abort_word, expect, own, ownv);
     if (a.abort != 0) return false;
     if (row_done<NJ>(a, tmask, expect, wkey, wg)) return true;
-    a = sweep<NJ, SYS>(row, G, abort_word, expect);
+    a = sweep<NJ, SYS>(row, G, abort_word, expect, own, ownv);
     if (b.abort != 0) return false;
     if (row_done<NJ>(b, tmask, expect, wkey, wg)) return true;
     if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinTimeout) return false;
@@ -2754,10 +2782,18 @@ __device__ __forceinline__ bool tpoll_slot(const uint64_t* row, int G, const int
 // granule of every slot is there.  Polling the slots one after another costs a wave with two slots a
 // second memory round trip after the data has landed.  Writes STAT[rr]; false on timeout / abort.
 // NJ granules per lane and slot (G <= 64 * NJ).
-template <int MS, int NJ>
+// Granule `own` of every slot (-1: none) is the caller's own: its value is enc_stat(own_stat(rr)), not
+// loaded.
+template <int MS, int NJ, class OwnStat>
 __device__ __forceinline__ bool tpoll_slots(const uint64_t* srow, int G, int R, int W, int soft_words,
-                                            const int32_t* abort_word, int64_t* STAT) {
+                                            const int32_t* abort_word, int64_t* STAT, int own, const OwnStat& own_stat) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint64_t ov[MS];
+#pragma unroll
+  for (int k = 0; k < MS; ++k) {
+    const int rr = wave + k * W;
+    ov[k] = (own >= 0 && rr < R && lane == (own & 63)) ? enc_stat(own_stat(rr)) : kGValid;
+  }
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   for (;;) {
     uint64_t v[MS][NJ];
@@ -2768,7 +2804,7 @@ __device__ __forceinline__ bool tpoll_slots(const uint64_t* srow, int G, int R, 
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         const int gg = lane + 64 * j;
-        v[k][j] = (rr < R && gg < G) ? load_sc1(srow + (size_t)rr * G + gg) : kGValid;
+        v[k][j] = gg == own ? ov[k] : ((rr < R && gg < G) ? load_sc1(srow + (size_t)rr * G + gg) : kGValid);
         if (!(v[k][j] & kGValid)) all = false;
       }
     }
@@ -3475,10 +3511,29 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
     __syncthreads();
     KGPU_WSTAMP(4);
     uint64_t* srow = ta.gran + (size_t)i * (R + 1) * G;  // [R][G] statistics granules | [G] keys
+    // this workgroup's value of statistics slot `rr` (LDS after the barrier above), for the polls below
+    // (own_gran).  Every candidate word is read first -- clamped addresses, one LDS round trip -- and then
+    // selected: a switch over the slot puts an LDS read and its wait in each of a dozen divergent
+    // branches, which the wave runs one after another (0.7 us per pod).
+    auto stat_of = [&](int rr) -> int64_t {
+      const int i32 = rr < 6 ? rr : (rr == kTDptsMax ? 6 : 7);
+      const uint32_t w32 = (uint32_t)M.acc32[i32];
+      const int64_t w64 = M.acc64[rr == kTIpaMax ? 1 : 0];
+      const int vi = rr - kTFixed;
+      const int voff = vi < 0 ? ta.o_smask : (vi < ta.soft_words ? ta.o_smask + 4 * vi : ta.o_zsum + 4 * (vi - ta.soft_words));
+      const int32_t wv = *reinterpret_cast<const int32_t*>(lds_raw + voff);
+      if (rr >= kTFixed) return vi < ta.soft_words ? (int64_t)(uint32_t)wv : (int64_t)wv;  // SMASK bits / ZSUM
+      if (rr == kTIpaMin) return w64 == INT64_MAX ? tident(kOpMin) : w64;
+      if (rr == kTIpaMax) return w64 == INT64_MIN ? tident(kOpMax) : w64;
+      if (rr == kTAdjMin) return tp.n_soft ? (int64_t)(uint32_t)~w32 : tident(kOpMin);
+      if (rr == kTAdjMax) return tp.n_soft ? (int64_t)w32 : tident(kOpMax);
+      if (rr == kTFeas || rr == kTNonIgn) return (int32_t)w32;
+      return (int64_t)w32;  // kTMaxT, kTMaxNA, kTDptsMax, kTZoned
+    };
+    // one slot per thread, the same selection written out: the publisher calling stat_of(tid) published
+    // wrong statistics on this compiler (placements off against the C restatement in 31 of 32 persistent
+    // topology test clusters, tools/own_probe.py), the expanded form below does not
     if (tid < R) {
-      // one slot per thread.  Every thread reads its candidate words first -- clamped addresses, one
-      // LDS round trip -- and then selects: a switch over the slot puts an LDS read and its wait in
-      // each of a dozen divergent branches, which the wave runs one after another (0.7 us per pod).
       const int i32 = tid < 6 ? tid : (tid == kTDptsMax ? 6 : 7);
       const uint32_t w32 = (uint32_t)M.acc32[i32];
       const int64_t w64 = M.acc64[tid == kTIpaMax ? 1 : 0];
@@ -3657,10 +3712,14 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
       txrow = sh_ptx[ta.rank] + (size_t)((ta.xseq0 + i) % kTXRing) * txw;
       txtag = kGValid | ((uint64_t)(((ta.xseq0 + i) / kTXRing) & 7) << 60);
     }
+    // own_gran (KGPU_OPT_TBATCH_OWN, off by default): this workgroup's own granules come from LDS, not
+    // from the round trip of its own store (another wave made it) -- measured 1-3 % slower per pod, the
+    // statistics wait longer
+    const int own = ta.own_gran ? g : -1;
     if (!XG && G <= 64 && R <= 4 * W) {
-      ok = tpoll_slots<4, 1>(srow, G, R, W, ta.soft_words, ta.abort, STAT);
+      ok = tpoll_slots<4, 1>(srow, G, R, W, ta.soft_words, ta.abort, STAT, own, stat_of);
     } else if (!XG && G <= 256 && R <= 2 * W) {
-      ok = tpoll_slots<2, 4>(srow, G, R, W, ta.soft_words, ta.abort, STAT);
+      ok = tpoll_slots<2, 4>(srow, G, R, W, ta.soft_words, ta.abort, STAT, own, stat_of);
     } else for (int rr = wave; rr < R; rr += W) {
       const int op = tslot_op(rr, ta.soft_words);
       int64_t x;
@@ -3715,7 +3774,7 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
       KGPU_WSTAMP(3);
       uint64_t wkey = 0;
       int wg = -1;
-      bool pok = poll_row<4, false>(arow, G, ta.abort, kGValid, kGValid, wkey, wg);
+      bool pok = poll_row<4, false>(arow, G, ta.abort, kGValid, kGValid, wkey, wg, own, kGValid | bk);
       if constexpr (XG) {
         // this rank's best: its local winner publishes the record -- the winning node's label values
         // and signature bits first, then (after a system-scope release) the key; workgroup 0 publishes
@@ -4630,10 +4689,13 @@ __device__ uint32_t ipa_adj(const VCtx& c) {
   return 0;
 }
 
-// RunFilterPlugins + Merge on the adjusted view, profile order, first failure wins.
-__device__ uint32_t eval_adj(const VCtx& c) {
+// RunFilterPlugins + Merge on the adjusted view, profile order, first failure wins -- or, with
+// runAllFilters, every plugin's word merged (and, with `all`, stored in status_all: the nominated pass
+// 1 that becomes the cycle's verdict on the node).
+__device__ uint32_t eval_adj(const VCtx& c, bool all = false) {
   const DevState& st = *c.st;
   const NodeRes r0 = load_res(st, c.n);
+  uint32_t acc = 0;
   for (int i = 0; i < st.n_filters; ++i) {
     const int f = st.filters[i];
     uint32_t code;
@@ -4644,9 +4706,15 @@ __device__ uint32_t eval_adj(const VCtx& c) {
       case KGPU_F_INTER_POD_AFFINITY: code = c.pl ? ipa_adj(c) : 0; break;
       default: code = filter_one(f, st, *c.q, r0, c.n); break;  // NodeInfo-independent of pods
     }
-    if (code) return code | (uint32_t)(i + 1);
+    const uint32_t w = code ? code | (uint32_t)(i + 1) : 0u;
+    if (!st.run_all) {
+      if (w) return w;
+      continue;
+    }
+    if (all) gp(st.status_all)[(size_t)i * st.N + c.n] = w;
+    acc = w ? merge_status(acc, w) : acc;
   }
-  return 0;
+  return acc;
 }
 
 // podPassesFiltersOnNode: pass 1 with the nominated pods (only when some were added), pass 2 without.
@@ -4682,7 +4750,7 @@ __global__ __launch_bounds__(64) void k_victims(const DevState* __restrict__ stp
   if (!a.preempt) {  // nominated pass 1 of a scheduling cycle
     if (c.m1 > c.m0) {
       c.pass1 = true;
-      a.nom_status[n] = eval_adj(c);
+      a.nom_status[n] = eval_adj(c, true);
     }
     return;
   }

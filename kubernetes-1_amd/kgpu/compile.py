@@ -251,9 +251,12 @@ class Profile:
     def __init__(self, filters=None, scores=None, least_resources=(("cpu", 1), ("memory", 1)),
                  most_resources=(("cpu", 1), ("memory", 1)), hard_pod_affinity_weight=1, ignored_resources=(),
                  pts_default_constraints=(), percentage_of_nodes_to_score=100, tie_break_mode=0, seed=0x7B,
-                 rtcr_resources=(("cpu", 1), ("memory", 1)), rtcr_shape=((0, 10), (100, 0))):
+                 rtcr_resources=(("cpu", 1), ("memory", 1)), rtcr_shape=((0, 10), (100, 0)), run_all_filters=False):
         """rtcr_*: RequestedToCapacityRatioArgs (apis/config/types_pluginargs.go): Resources as
-        (name, weight), Shape as (utilization, score 0-10)."""
+        (name, weight), Shape as (utilization, score 0-10).  run_all_filters: the framework's
+        runAllFilters (framework.go:90,155-160; the legacy Policy's AlwaysCheckAllPredicates,
+        factory.go:278-281)."""
+        self.run_all_filters = bool(run_all_filters)
         self.filters = list(self.DEFAULT_FILTERS if filters is None else filters)
         self.scores = [tuple(s) for s in (self.DEFAULT_SCORES if scores is None else scores)]
         self.least_resources = [tuple(r) for r in least_resources]

@@ -57,11 +57,15 @@ def status_reasons(filters, compiler, nodes, pod, node_name, word, handle=None, 
 
 
 class CycleResult:
-    def __init__(self, host, result, statuses, scores):
+    def __init__(self, host, result, statuses, scores, plugin_statuses=None):
         self.host = host            # node name or None
         self.result = result        # kgpu_result record
         self.statuses = statuses    # {node: (code, plugin, reasons)} for infeasible nodes
         self.scores = scores        # {plugin: {node: (raw, normalized)}} over feasible nodes
+        # runAllFilters: {node: {plugin: (code, reasons)}} -- RunFilterPlugins' PluginToStatus, whose
+        # Merge is `statuses` (code merged, reasons of every failing plugin in profile order; the plugin
+        # named there is the first failing one)
+        self.plugin_statuses = plugin_statuses
 
 
 def nodes_where_preemption_might_help(order, codes):
@@ -111,6 +115,8 @@ class GpuFramework:
         self.engine = None
         if create_engine:
             self.engine = Engine(self.config)
+            if getattr(profile, "run_all_filters", False):
+                self.engine.set_option(abi.OPT_RUN_ALL_FILTERS, 1)
             self.engine.upload(self.snap, self.arrays)
 
     def init_comm(self, rank, world, uid):
@@ -149,12 +155,25 @@ class GpuFramework:
         self.seq = s + 1
         n = self.snap.n_nodes
         words = self.engine.filter_words(n)
-        statuses = {}
+        run_all = getattr(self.profile, "run_all_filters", False)
+        every = self.engine.filter_words_all(len(self.filters), n) if run_all else None
+        statuses, plugin_statuses = {}, ({} if run_all else None)
         for i in np.nonzero(words)[0]:
             if int(words[i]) == abi.STATUS_NOT_EVALUATED:
                 continue  # never examined: percentageOfNodesToScore stopped the search before it
             nm = self.order[self.snap.node_base + int(i)]
-            statuses[nm] = self.reasons(pod, nm, int(words[i]), compiled=(q[0], pc), node=int(i))
+            if not run_all:
+                statuses[nm] = self.reasons(pod, nm, int(words[i]), compiled=(q[0], pc), node=int(i))
+                continue
+            per = {}
+            for p in range(len(self.filters)):
+                wp = int(every[p, i])
+                if wp:
+                    code, plugin, rs = self.reasons(pod, nm, wp, compiled=(q[0], pc), node=int(i))
+                    per[plugin] = (code, rs)
+            plugin_statuses[nm] = per
+            w = int(words[i])
+            statuses[nm] = ((w >> 8) & 3, self.filters[(w & 0xFF) - 1], [r for _, rs in per.values() for r in rs])
         scores = {}
         feas = np.nonzero(words == 0)[0]
         for name, w in self.profile.scores:
@@ -163,7 +182,7 @@ class GpuFramework:
         host = self.order[res["node"]] if res["node"] >= 0 else None
         if assume and host is not None:
             self._placed(pod, host)
-        return CycleResult(host, res, statuses, scores)
+        return CycleResult(host, res, statuses, scores, plugin_statuses)
 
     def _placed(self, pod, host):
         """Record an assumed pod on its node (NodeInfo.AddPod) and drop it from the nominator

@@ -17,7 +17,7 @@ _lib = None
 
 EXPORTS = ["kgpu_abi_version", "kgpu_struct_sizes", "kgpu_create", "kgpu_destroy", "kgpu_last_error",
            "kgpu_upload_snapshot", "kgpu_generation", "kgpu_schedule_one", "kgpu_schedule_batch",
-           "kgpu_get_filter", "kgpu_get_scores", "kgpu_forget_pod", "kgpu_read_nodes", "kgpu_set_option",
+           "kgpu_get_filter", "kgpu_get_filter_all", "kgpu_get_scores", "kgpu_forget_pod", "kgpu_read_nodes", "kgpu_set_option",
            "kgpu_read_phase_trace", "kgpu_comm_unique_id", "kgpu_comm_init", "kgpu_apply_delta",
            "kgpu_set_nominated", "kgpu_select_victims", "kgpu_xgmi_handle", "kgpu_xgmi_init", "kgpu_xgmi_active",
            "kgpu_comm_info",
@@ -53,6 +53,7 @@ def lib():
     L.kgpu_schedule_one.argtypes = [vp, vp, C.POINTER(abi.Pools), i64, i32, vp, C.POINTER(i32)]
     L.kgpu_schedule_batch.argtypes = [vp, vp, i32, C.POINTER(abi.Pools), i64, vp, C.POINTER(abi.Stats)]
     L.kgpu_get_filter.argtypes = [vp, vp]
+    L.kgpu_get_filter_all.argtypes = [vp, vp]
     L.kgpu_get_scores.argtypes = [vp, i32, vp, vp]
     L.kgpu_forget_pod.argtypes = [vp, i32]
     L.kgpu_read_nodes.argtypes = [vp, vp, vp, vp, vp, vp, vp]
@@ -178,6 +179,12 @@ class Engine:
     def filter_words(self, n):
         out = np.zeros(n, np.uint32)
         self._check(lib().kgpu_get_filter(self.h, out.ctypes.data))
+        return out
+
+    def filter_words_all(self, n_filters, n):
+        """KGPU_OPT_RUN_ALL_FILTERS: the last cycle's per-plugin words, [n_filters][n]."""
+        out = np.zeros((n_filters, n), np.uint32)
+        self._check(lib().kgpu_get_filter_all(self.h, out.ctypes.data))
         return out
 
     def scores(self, plugin, n):

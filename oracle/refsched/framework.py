@@ -45,7 +45,7 @@ class Profile:
                  least_resources=(("cpu", 1), ("memory", 1)), most_resources=(("cpu", 1), ("memory", 1)),
                  hard_pod_affinity_weight=1, ignored_resources=(), pts_default_constraints=(),
                  percentage_of_nodes_to_score=100, tie_break_mode=tiebreak.MODE_HASH, seed=0x7B,
-                 plugin_factories=None):
+                 plugin_factories=None, run_all_filters=False):
         self.filters = list(DEFAULT_FILTERS if filters is None else filters)
         self.prefilters = list(DEFAULT_PREFILTERS if prefilters is None else prefilters)
         self.prescores = list(DEFAULT_PRESCORES if prescores is None else prescores)
@@ -61,6 +61,9 @@ class Profile:
         # extra plugin constructors, name -> factory(handle): the fake plugins of the reference's
         # generic_scheduler_test.go (tests/fake_plugins.py)
         self.plugin_factories = dict(plugin_factories or {})
+        # WithRunAllFilters (framework.go:155-160), set from the legacy Policy's AlwaysCheckAllPredicates
+        # (factory.go:107,278-281)
+        self.run_all_filters = bool(run_all_filters)
 
 
 def cluster_autoscaler_profile(**kw):
@@ -141,7 +144,14 @@ class Framework:
         return None
 
     def run_filters(self, state, pod, ni):
-        """Returns (plugin_name or None, status) with early exit (runAllFilters=false)."""
+        """Returns (plugin_name or None, status): RunFilterPlugins + PluginToStatus.Merge.  Without
+        runAllFilters the first failure (early exit); with it the Merge of every failing plugin's
+        status, named after the first (merge_statuses)."""
+        if self.profile.run_all_filters:
+            statuses = self.run_filter_plugins(state, pod, ni, run_all_filters=True)
+            if not statuses:
+                return None, None
+            return next(iter(statuses)), merge_statuses(statuses)
         for pl in self.filters:
             st = pl.filter(state, pod, ni)
             if not P.is_success(st):

@@ -13,8 +13,8 @@ Not on the device, and why:
   * rows injecting Error: the device's filters never return Error -- the Go runner turns any code
     other than Unschedulable(AndUnresolvable) into an Error itself (framework.go:486-492), and that
     code stays in the Go framework around the plugin (INTEGRATION.md);
-  * runAllFilters rows (WithRunAllFilters, alwaysCheckAllPredicates): the engine reports the FIRST
-    failing filter, as the default runner does; run-all merging is not implemented (DESIGN.md 8);
+  * runAllFilters rows run on the device too (KGPU_OPT_RUN_ALL_FILTERS): the merged code and the map of
+    every failing plugin (tests/test_run_all_filters.py holds the cluster-level cases);
   * TestRunScorePlugins: its plugins inject raw and normalized scores the device's plugins cannot
     produce.  Weights, NormalizeScore and the sum run on the device for the real plugins and are
     pinned by TestZeroRequest and every score table; the range check guards plugin bugs the
@@ -27,7 +27,7 @@ from kgpu.compile import Profile
 from kgpu.framework import GpuFramework
 
 REAL = {0: ["NodeName", "NodePorts"], 2: ["NodeResourcesFit"], 3: ["NodeUnschedulable"]}
-ROWS = [c for c in load_golden("framework") if c["kind"] == "run_filter" and not c["run_all_filters"]
+ROWS = [c for c in load_golden("framework") if c["kind"] == "run_filter"
         and all(code in REAL for code in c["profile"]["fake"]["injected_filters"].values())]
 
 
@@ -44,7 +44,8 @@ def test_filter_runner_on_device(case):
             "status": {"allocatable": {"cpu": "1", "memory": "1Gi", "pods": "10"}}}
     pod = {"metadata": {"name": "p", "namespace": "default", "uid": "p"},
            "spec": {"containers": [{"name": "c", "resources": {"requests": {"cpu": "2"}}}]}}
-    fw = GpuFramework(Profile(filters=real, scores=[]), [node], [], pods_hint=[pod])
+    run_all = case["run_all_filters"]
+    fw = GpuFramework(Profile(filters=real, scores=[], run_all_filters=run_all), [node], [], pods_hint=[pod])
     res = fw.cycle(pod)
     want = case["expect_merged"]
     if want is None:
@@ -53,5 +54,10 @@ def test_filter_runner_on_device(case):
         code, plugin, _ = res.statuses["node1"]
         first = next(i for i, (_, c) in enumerate(fake) if c != 0)
         assert (code, plugin) == (want["code"], real[first]), (case["name"], code, plugin)
-        assert list(case["expect_status_map"]) == [fake[first][0]]
+        if not run_all:
+            assert list(case["expect_status_map"]) == [fake[first][0]]
+        else:  # the PluginToStatus map: every failing plugin with its own code
+            to_fake = dict(zip(real, (f for f, _ in fake)))
+            got = {to_fake[pl]: c for pl, (c, _) in res.plugin_statuses["node1"].items()}
+            assert got == {f: st["code"] for f, st in case["expect_status_map"].items()}, (case["name"], got)
     fw.engine.close()
