@@ -164,8 +164,8 @@ def measure(args, cfg, n_nodes_per_gpu, B, K, W, cpu_sample, cpu_threads, latenc
         eng.set_option(abi.OPT_TBATCH_GEO, args.tbatch_geo)
     if args.tbatch_wlab is not None:
         eng.set_option(abi.OPT_TBATCH_WLAB, args.tbatch_wlab)
-    if args.tbatch_own is not None:
-        eng.set_option(abi.OPT_TBATCH_OWN, args.tbatch_own)
+    if args.tbatch_poll_sleep is not None:
+        eng.set_option(abi.OPT_TBATCH_POLL_SLEEP, args.tbatch_poll_sleep)
     if args.topo_fused is not None:
         eng.set_option(abi.OPT_TOPO_FUSED, args.topo_fused)
     if args.no_topo_persistent:
@@ -456,8 +456,8 @@ def main():
                     help="KGPU_OPT_TOPO_AHEAD (default: the library's, 1 = next pod's non-topology half ahead)")
     ap.add_argument("--tbatch-geo", type=int, default=None,
                     help="KGPU_OPT_TBATCH_GEO (smallest k_tbatch geometry index; 0 = 256 threads x 1 row)")
-    ap.add_argument("--tbatch-own", type=int, default=None,
-                    help="KGPU_OPT_TBATCH_OWN (default: the library's, 0; 1 = own granules not loaded back)")
+    ap.add_argument("--tbatch-poll-sleep", type=int, default=None,
+                    help="KGPU_OPT_TBATCH_POLL_SLEEP (default: the library's, 1 = sleep between statistics sweeps)")
     ap.add_argument("--tbatch-wlab", type=int, default=None,
                     help="KGPU_OPT_TBATCH_WLAB (default: the library's, 1 = every node's delta-key labels in LDS)")
     ap.add_argument("--batch-geo", type=int, default=None,

@@ -586,7 +586,8 @@ int kgpu_read_nodes(kgpu_ctx* ctx, int64_t* req_cpu, int64_t* req_mem, int64_t* 
  * lower cap gives each lane more node rows (tests use it to cover every rows-per-lane variant). */
 #define KGPU_OPT_PERSIST_GROUPS 3
 /* KGPU_OPT_PHASE_TRACE (4): record per-pod phase timestamps of the persistent kernel (diagnostics;
- * read with kgpu_read_phase_trace). */
+ * read with kgpu_read_phase_trace).  2: the topology kernel's stamps 1 and 2 mark the end of its
+ * normalize + key pass and of the workgroup argmax instead of PreFilter and the rows. */
 #define KGPU_OPT_PHASE_TRACE 4
 /* KGPU_OPT_TOPO_FUSED (5): 1 = run a topology pod's six phases (histograms, critical-path minima,
  * filters, scores, normalize + argmax, resolve + assume) in one cooperative launch with grid
@@ -651,10 +652,7 @@ int kgpu_read_nodes(kgpu_ctx* ctx, int64_t* req_cpu, int64_t* req_mem, int64_t* 
  * of the delta keys in LDS when they fit, so the assume phase reads the winner's labels there; 0 = a global
  * load per pod (A/B switch). */
 #define KGPU_OPT_TBATCH_WLAB 18
-/* KGPU_OPT_TBATCH_OWN (19): 1 = in the persistent topology kernel's exchanges a workgroup takes its own
- * statistics and key granules from LDS / registers instead of loading its own stores back; 0 (default) =
- * every granule loaded (1 measured 1-3 % slower; A/B switch). */
-#define KGPU_OPT_TBATCH_OWN 19
+/* 19: unused (KGPU_OPT_TBATCH_OWN in round 5, removed after its A/B: DESIGN.md 4.4) */
 /* KGPU_OPT_RUN_ALL_FILTERS (20): the framework's runAllFilters (framework.go:90,155-160,484-499; set from
  * the legacy Policy's AlwaysCheckAllPredicates, factory.go:107,278-281).  1 = a kgpu_schedule_one cycle
  * runs every filter plugin on every node: kgpu_get_filter's word becomes PluginToStatus.Merge's
@@ -662,6 +660,9 @@ int kgpu_read_nodes(kgpu_ctx* ctx, int64_t* req_cpu, int64_t* req_mem, int64_t* 
  * stay the first failing plugin's) and kgpu_get_filter_all returns each plugin's own word; preemption's
  * nodesWherePreemptionMightHelp reads the merged code.  Placements do not change.  Default 0. */
 #define KGPU_OPT_RUN_ALL_FILTERS 20
+/* KGPU_OPT_TBATCH_POLL_SLEEP (21): 1 (default) = the persistent topology kernel's statistics polls sleep
+ * briefly between sweeps; 0 = back to back (A/B switch). */
+#define KGPU_OPT_TBATCH_POLL_SLEEP 21
 int kgpu_set_option(kgpu_ctx* ctx, int32_t option, int64_t value);
 /* Engine counters: out[0] = calls issued again with a cooperative launch after a persistent run's
  * workgroups were not all resident before its first pod (KGPU_OPT_COOPERATIVE); out[1] = persistent

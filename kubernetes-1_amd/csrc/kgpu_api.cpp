@@ -113,6 +113,7 @@ struct kgpu_ctx {
   int32_t abort_at = -1;  // KGPU_OPT_ABORT_AT: batch query index at which a persistent run aborts
   int32_t skip_release_at = -1;  // KGPU_OPT_SKIP_RELEASE_AT: batch query whose LDS hand-off is never released
   bool phase_trace = false;
+  int phase_trace_mode = 0;         // the KGPU_OPT_PHASE_TRACE value
   DevBuf trace;
   std::vector<int64_t> trace_host;
   int spec = 0;      // k_eval instantiation for the profile (kgpu::select_spec)
@@ -262,7 +263,7 @@ struct kgpu_ctx {
                                     // of it cooperative)
   int32_t hold_group = -1;          // KGPU_OPT_HOLD_GROUP test hook
   bool tbatch_wlab = true;          // KGPU_OPT_TBATCH_WLAB
-  bool tbatch_own = false;          // KGPU_OPT_TBATCH_OWN (measured slower: DESIGN.md 4.4)
+  bool tbatch_sleep = true;         // KGPU_OPT_TBATCH_POLL_SLEEP
   bool run_all = false;             // KGPU_OPT_RUN_ALL_FILTERS
   bool last_run_all = false;        // the last diagnostic cycle wrote status_all
   int64_t n_coop_retry = 0, n_persist = 0, n_coop = 0;  // kgpu_debug_counters
@@ -1673,6 +1674,7 @@ int run_tbatch(kgpu_ctx* c, TRun& tr, int first, int count, int64_t first_seq, i
     HIP_OK(c, hipMemsetAsync(c->trace.p, 0, sizeof(int64_t) * (tw + ww), c->stream));
     a.trace = static_cast<int64_t*>(c->trace.p);
     a.trace_wg = a.trace + tw;
+    a.trace_mode = c->phase_trace_mode;
     c->trace_host.assign(tw, 0);
     c->trace_wg_host.assign(ww, 0);
     c->trace_wg_groups = groups;
@@ -1711,7 +1713,7 @@ int run_tbatch(kgpu_ctx* c, TRun& tr, int first, int count, int64_t first_seq, i
   // were it not, the spin timeouts raise the abort word instead of hanging.
   const bool coop = (c->coop && !(count == 1 && !xg)) || c->force_coop;
   a.hold = coop ? -1 : c->hold_group;
-  a.own_gran = c->tbatch_own ? 1 : 0;
+  a.poll_sleep = c->tbatch_sleep ? 1 : 0;
   ++c->n_persist;
   c->n_coop += coop ? 1 : 0;
   ++c->state_launches;
@@ -2360,21 +2362,26 @@ int run_batch_once(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_
         a.prev_blocks = blocks;
         a.prev_parity = (k - 1) & 1;
         a.parity = k & 1;
-        a.norm = (diag || cut || needs_norm(c, qs[k], pools)) ? 1 : 0;
+        // a one-pod diagnostic cycle of a pod without a normalize pass takes one launch: k_eval's last
+        // workgroup resolves it (resolve_tail) and writes the normalized rows k_final would
+        const bool one_launch = short_cycle && n == 1 && diag && !sharded && !cut &&
+                                !(qs[k].flags & KGPU_Q_SCORE_ERROR) && !needs_norm(c, qs[k], pools);
+        a.norm = (!one_launch && (diag || cut || needs_norm(c, qs[k], pools))) ? 1 : 0;
         a.assume = assume;
         a.diag = diag ? 1 : 0;
         a.zero_diag = zero_diag ? 1 : 0;
         a.cut = cut ? 1 : 0;
         a.seq = first_seq + k;
-        // the chain's last pod with a normalize pass: k_final's last workgroup resolves it
-        a.resolve_self = (k == j - 1 && a.norm && !sharded) ? 1 : 0;
+        // the chain's last pod with a normalize pass: k_final's last workgroup resolves it (k_eval's, for a
+        // one-launch cycle)
+        a.resolve_self = (k == j - 1 && (a.norm || one_launch) && !sharded) ? 1 : 0;
         resolved_in_final = a.resolve_self != 0;
         if (inline_q) {
           a.q_inline = 1;
           a.q = qs[k];
         }
-        // a one-pod diagnostic cycle ends on k_final's resolving workgroup: it raises a pinned completion
-        // word once everything is written back, and the host returns on it
+        // a one-pod diagnostic cycle ends on k_final's (k_eval's) resolving workgroup: it raises a pinned
+        // completion word once everything is written back, and the host returns on it
         if (a.resolve_self && short_cycle && n == 1 && !sharded && !c->timing && !c->phase_trace) {
           int32_t* dw = reinterpret_cast<int32_t*>(static_cast<char*>(c->res_pin) + kCycDoneOff);
           __atomic_store_n(dw, -1, __ATOMIC_RELEASE);
@@ -3698,7 +3705,10 @@ int kgpu_set_option(kgpu_ctx* c, int32_t option, int64_t value) try {
   if (option == KGPU_OPT_KERNEL_TIMING) c->timing = value != 0;
   else if (option == KGPU_OPT_PERSISTENT) c->persistent = value != 0;
   else if (option == KGPU_OPT_PERSIST_GROUPS) c->max_groups = (int)std::max<int64_t>(value, 0);
-  else if (option == KGPU_OPT_PHASE_TRACE) c->phase_trace = value != 0;
+  else if (option == KGPU_OPT_PHASE_TRACE) {
+    c->phase_trace = value != 0;
+    c->phase_trace_mode = (int)std::min<int64_t>(std::max<int64_t>(value, 0), 2);
+  }
   else if (option == KGPU_OPT_TOPO_FUSED) c->topo_fused = value != 0;
   else if (option == KGPU_OPT_TOPO_PERSISTENT) c->tfast = value != 0;
   else if (option == KGPU_OPT_COOPERATIVE) c->coop = value != 0;
@@ -3713,7 +3723,7 @@ int kgpu_set_option(kgpu_ctx* c, int32_t option, int64_t value) try {
   else if (option == KGPU_OPT_ABORT_AT) c->abort_at = value < 0 || value > INT32_MAX ? -1 : (int32_t)value;
   else if (option == KGPU_OPT_XGMI) c->xgmi = value != 0;
   else if (option == KGPU_OPT_TBATCH_WLAB) c->tbatch_wlab = value != 0;
-  else if (option == KGPU_OPT_TBATCH_OWN) c->tbatch_own = value != 0;
+  else if (option == KGPU_OPT_TBATCH_POLL_SLEEP) c->tbatch_sleep = value != 0;
   else if (option == KGPU_OPT_RUN_ALL_FILTERS) c->run_all = value != 0;
   else if (option == KGPU_OPT_HOLD_GROUP) c->hold_group = value < 0 || value > INT32_MAX ? -1 : (int32_t)value;
   else if (option == KGPU_OPT_SKIP_RELEASE_AT) c->skip_release_at = value < 0 || value > INT32_MAX ? -1 : (int32_t)value;

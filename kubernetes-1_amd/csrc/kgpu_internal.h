@@ -431,8 +431,8 @@ struct TBatchArgs {
   int32_t zero_n16;       // the other resident-state buffer: its first zero_n16 16-byte words are zeroed by
                           // the grid at kernel entry, so the next miss starts from zeros without a memset
   int32_t hold;           // KGPU_OPT_HOLD_GROUP test hook, as in BatchArgs
-  int32_t own_gran;       // 1: a workgroup's own statistics / key granules are taken from LDS / registers in
-                          // its polls instead of loaded back (KGPU_OPT_TBATCH_OWN)
+  int32_t poll_sleep;     // 1: a short sleep between statistics sweeps (KGPU_OPT_TBATCH_POLL_SLEEP)
+  int32_t trace_mode;     // KGPU_OPT_PHASE_TRACE value: 2 moves stamps 1 / 2 into the normalize phase
   struct alignas(16) Z16 { uint64_t lo, hi; };
   Z16* zero_buf;
   int64_t* trace;        // null, or [count + 1][16] s_memrealtime stamps (KGPU_OPT_PHASE_TRACE): per pod

@@ -520,7 +520,7 @@ __device__ __forceinline__ uint32_t merge_status(uint32_t acc, uint32_t w) {
 
 // runAllFilters (framework.go:484-499 without the early exit): every plugin of the profile, each word
 // in status_all, the merged word returned.
-__device__ __noinline__ uint32_t run_filters_all(const DevState& st, const kgpu_pod_query& q, const NodeRes& r, int n,
+__device__ __forceinline__ uint32_t run_filters_all(const DevState& st, const kgpu_pod_query& q, const NodeRes& r, int n,
                                                  const QPlan* pl) {
   uint32_t acc = 0;
   for (int i = 0; i < st.n_filters; ++i) {
@@ -866,6 +866,53 @@ __device__ __forceinline__ void chunk_of(int N, int& lo, int& hi) {
 // ---------------------------------------------------------------- kernels
 // One workgroup = one wave64: the workgroup argmax is a pure shuffle reduction (no LDS, no
 // barrier), and every wave resolves the previous pod's winner on its own.
+// The last workgroup of a one-pod launch to finish resolves the pod -- selectHost, the result record and
+// the assume -- in place of a k_resolve launch (PodArgs.resolve_self: the end of a short cycle, after
+// k_final, or after k_eval when the pod needs no normalize pass).  Release / acquire fences around the
+// ticket make every workgroup's partial visible to it across XCDs.
+__device__ __forceinline__ void resolve_tail(const DevState& st, const PodArgs& a) {
+  __shared__ int last;
+  // a cycle the host completes on done_out: every wave's stores (the diagnostic rows included) reach L2
+  // before thread 0's release writes the L2 back (one write-back per workgroup: a fence in every wave
+  // cost a 100k-node cycle 5 us, profiles/r05_host_trace.txt)
+  if (a.done_out) __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    last = atomicAdd(st.ticket, 1) == (int)gridDim.x - 1;
+  }
+  __syncthreads();
+  if (last) {
+    __threadfence();
+    PodArgs r{};
+    r.prev = a.pod;
+    r.prev_blocks = (int32_t)gridDim.x;
+    r.prev_parity = a.parity;
+    r.assume = a.assume;
+    r.cut = a.cut;
+    int gidx;
+    const Winner w = prev_winner(st, r, &gidx);
+    const kgpu_pod_query pq = a.q_inline ? a.q : (kgpu_pod_query)*cp(st.queries + a.pod);
+    const int idx = settle_prev(st, r, pq, w, gidx, threadIdx.x == 0);
+    if (threadIdx.x == 0) {
+      if (idx >= 0) {
+        NodeRes row = load_res(st, idx);
+        assume_row(st, pq, row, idx);
+        assume_counts(st, a.pod, idx);
+      }
+      __hip_atomic_store(st.ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // for the next cycle
+    }
+    if (a.done_out) {
+      __builtin_amdgcn_s_waitcnt(0);  // the record, the assume and the last workgroup's rows in L2 ...
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        __threadfence();  // ... written back, then the completion word
+        __hip_atomic_store(a.done_out, 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+  }
+}
+
 template <uint32_t FM, uint32_t SM>
 __global__ __launch_bounds__(kBlock) void k_eval(const DevState* __restrict__ stp, PodArgs a) {
   const DevState& st = *stp;
@@ -911,6 +958,15 @@ __global__ __launch_bounds__(kBlock) void k_eval(const DevState* __restrict__ st
     e.status = s1 ? s1 : run_filters<FM>(st, q, r, n);
     if (e.status == 0) {
       run_scores<SM>(st, q, r, n, e, a.diag);
+      if (a.diag && !a.norm) {
+        // the normalized rows k_final would write: without a normalize pass every raw TaintToleration /
+        // NodeAffinity score is 0 (needs_norm), so DefaultNormalizeScore gives 100 / 0
+        for (int si = 0; si < st.n_scores; ++si) {
+          const int s = st.scores[si];
+          if (s == KGPU_S_TAINT_TOLERATION) gp(st.diag_norm)[(size_t)s * st.N + n] = 100;
+          else if (s == KGPU_S_NODE_AFFINITY) gp(st.diag_norm)[(size_t)s * st.N + n] = e.na;
+        }
+      }
       ++feas;
       maxT = max(maxT, e.taint);
       maxNA = max(maxNA, e.na);
@@ -936,6 +992,8 @@ __global__ __launch_bounds__(kBlock) void k_eval(const DevState* __restrict__ st
     gp(st.sbuf)[(size_t)a.parity * kMaxBlocks + blockIdx.x] = BlkStat{feas, maxT, maxNA, 0};
     if (!a.norm) gp(st.kbuf)[(size_t)a.parity * kMaxBlocks + blockIdx.x] = BlkKey{best, best_i, feas};
   }
+  // a one-pod diagnostic cycle without a normalize pass resolves here: no k_final / k_resolve launch
+  if (a.resolve_self && !a.norm) resolve_tail(st, a);
 }
 
 // Normalize pass: DefaultNormalizeScore maxima over the feasible set are known only after the
@@ -983,51 +1041,7 @@ __global__ __launch_bounds__(kBlock) void k_final(const DevState* __restrict__ s
   wave_reduce_key(best, best_i);
   bf = wave_reduce_sum(bf);
   if (threadIdx.x == 0) gp(st.kbuf)[(size_t)a.parity * kMaxBlocks + blockIdx.x] = BlkKey{best, best_i, bf};
-  if (a.resolve_self) {
-    // The last workgroup to finish resolves this pod -- selectHost, the result record and the
-    // assume -- in place of a k_resolve launch (the end of a short cycle).  Release / acquire
-    // fences around the ticket make every workgroup's partial visible to it across XCDs.
-    __shared__ int last;
-    // a cycle the host completes on done_out: every wave's stores (the diagnostic rows included) reach L2
-    // before thread 0's release writes the L2 back (one write-back per workgroup: a fence in every wave
-    // cost a 100k-node cycle 5 us, profiles/r05_host_trace.txt)
-    if (a.done_out) __builtin_amdgcn_s_waitcnt(0);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      __threadfence();
-      last = atomicAdd(st.ticket, 1) == (int)gridDim.x - 1;
-    }
-    __syncthreads();
-    if (last) {
-      __threadfence();
-      PodArgs r{};
-      r.prev = a.pod;
-      r.prev_blocks = (int32_t)gridDim.x;
-      r.prev_parity = a.parity;
-      r.assume = a.assume;
-      r.cut = a.cut;
-      int gidx;
-      const Winner w = prev_winner(st, r, &gidx);
-      const kgpu_pod_query pq = a.q_inline ? a.q : (kgpu_pod_query)*cp(st.queries + a.pod);
-      const int idx = settle_prev(st, r, pq, w, gidx, threadIdx.x == 0);
-      if (threadIdx.x == 0) {
-        if (idx >= 0) {
-          NodeRes row = load_res(st, idx);
-          assume_row(st, pq, row, idx);
-          assume_counts(st, a.pod, idx);
-        }
-        __hip_atomic_store(st.ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // for the next cycle
-      }
-      if (a.done_out) {
-        __builtin_amdgcn_s_waitcnt(0);  // the record, the assume and the last workgroup's rows in L2 ...
-        __syncthreads();
-        if (threadIdx.x == 0) {
-          __threadfence();  // ... written back, then the completion word
-          __hip_atomic_store(a.done_out, 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-      }
-    }
-  }
+  if (a.resolve_self) resolve_tail(st, a);
 }
 
 // Resolve-only launch (end of a batch / single cycle), with the evaluation grid's chunk mapping
@@ -1409,19 +1423,15 @@ struct Sweep {
   uint64_t v[NJ];
   int abort;
 };
-// Granule `own` (-1: none) is the caller's own, value `ownv`: not loaded.
 template <int NJ, bool SYS>
-__device__ __forceinline__ Sweep<NJ> sweep(const uint64_t* row, int G, const int32_t* abort_word, uint64_t fill,
-                                           int own = -1, uint64_t ownv = 0) {
+__device__ __forceinline__ Sweep<NJ> sweep(const uint64_t* row, int G, const int32_t* abort_word, uint64_t fill) {
   const int lane = threadIdx.x & 63;
   Sweep<NJ> s;
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     uint64_t* p = const_cast<uint64_t*>(row + lane + 64 * j);
-    const int gg = lane + 64 * j;
-    s.v[j] = gg == own ? ownv
-                       : (gg < G ? (SYS ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : load_sc1(p))
-                                 : fill);  // a valid granule with key 0
+    s.v[j] = (lane + 64 * j < G) ? (SYS ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : load_sc1(p))
+                                 : fill;  // a valid granule with key 0
   }
   s.abort = load_sc1(abort_word);
   return s;
@@ -1454,14 +1464,14 @@ __device__ __forceinline__ bool row_done(const Sweep<NJ>& cur, uint64_t tmask, u
 }
 template <int NJ, bool SYS>
 __device__ __forceinline__ bool poll_row(const uint64_t* row, int G, const int32_t* abort_word, uint64_t tmask,
-                                         uint64_t expect, uint64_t& wkey, int& wg, int own = -1, uint64_t ownv = 0) {
+                                         uint64_t expect, uint64_t& wkey, int& wg) {
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  Sweep<NJ> a = sweep<NJ, SYS>(row, G, abort_word, expect, own, ownv);
+  Sweep<NJ> a = sweep<NJ, SYS>(row, G, abort_word, expect);
   for (;;) {
-    const Sweep<NJ> b = sweep<NJ, SYS>(row, G, abort_word, expect, own, ownv);
+    const Sweep<NJ> b = sweep<NJ, SYS>(row, G, abort_word, expect);
     if (a.abort != 0) return false;
     if (row_done<NJ>(a, tmask, expect, wkey, wg)) return true;
-    a = sweep<NJ, SYS>(row, G, abort_word, expect, own, ownv);
+    a = sweep<NJ, SYS>(row, G, abort_word, expect);
     if (b.abort != 0) return false;
     if (row_done<NJ>(b, tmask, expect, wkey, wg)) return true;
     if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinTimeout) return false;
@@ -2769,11 +2779,12 @@ __device__ __forceinline__ bool tpoll_slot(const uint64_t* row, int G, const int
         else acc = tcombine(op, acc, dec_stat(v));
       }
     }
+    const int ab = load_sc1(abort_word);  // with the sweep: one round trip per retry
     if (__all(all)) {
       out = wave_op_i64(op, acc);
       return true;
     }
-    if (load_sc1(abort_word) != 0 || __builtin_amdgcn_s_memrealtime() - t0 > kSpinTimeout) return false;
+    if (ab != 0 || __builtin_amdgcn_s_memrealtime() - t0 > kSpinTimeout) return false;
   }
 }
 
@@ -2782,18 +2793,18 @@ __device__ __forceinline__ bool tpoll_slot(const uint64_t* row, int G, const int
 // granule of every slot is there.  Polling the slots one after another costs a wave with two slots a
 // second memory round trip after the data has landed.  Writes STAT[rr]; false on timeout / abort.
 // NJ granules per lane and slot (G <= 64 * NJ).
-// Granule `own` of every slot (-1: none) is the caller's own: its value is enc_stat(own_stat(rr)), not
-// loaded.
-template <int MS, int NJ, class OwnStat>
+// Wave `wave` polls ALL of its statistics slots (wave, wave + W, ... below R, at most MS of them) in
+// one sweep, NJ granules per lane and slot (G <= 64 * NJ), and reduces each slot once every granule of
+// every slot is there.  Polling the slots one after another costs a wave with two slots a second memory
+// round trip after the data has landed.  The abort word is loaded with each sweep (loaded only after a
+// failed sweep, it made every retry two round trips).  SLEEP (KGPU_OPT_TBATCH_POLL_SLEEP): a short
+// s_sleep between sweeps -- every wave of every workgroup polls the same few granule lines, and less
+// polling traffic measured 0.5-1 % faster per pod (more -- two sweeps in flight -- 1.5-2 % slower;
+// DESIGN.md 4.4).  Writes STAT[rr]; false on timeout / abort.
+template <int MS, int NJ, bool SLEEP>
 __device__ __forceinline__ bool tpoll_slots(const uint64_t* srow, int G, int R, int W, int soft_words,
-                                            const int32_t* abort_word, int64_t* STAT, int own, const OwnStat& own_stat) {
+                                            const int32_t* abort_word, int64_t* STAT) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  uint64_t ov[MS];
-#pragma unroll
-  for (int k = 0; k < MS; ++k) {
-    const int rr = wave + k * W;
-    ov[k] = (own >= 0 && rr < R && lane == (own & 63)) ? enc_stat(own_stat(rr)) : kGValid;
-  }
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   for (;;) {
     uint64_t v[MS][NJ];
@@ -2804,10 +2815,11 @@ __device__ __forceinline__ bool tpoll_slots(const uint64_t* srow, int G, int R, 
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         const int gg = lane + 64 * j;
-        v[k][j] = gg == own ? ov[k] : ((rr < R && gg < G) ? load_sc1(srow + (size_t)rr * G + gg) : kGValid);
+        v[k][j] = (rr < R && gg < G) ? load_sc1(srow + (size_t)rr * G + gg) : kGValid;
         if (!(v[k][j] & kGValid)) all = false;
       }
     }
+    const int ab = load_sc1(abort_word);
     if (__all(all)) {
 #pragma unroll
       for (int k = 0; k < MS; ++k) {
@@ -2823,7 +2835,8 @@ __device__ __forceinline__ bool tpoll_slots(const uint64_t* srow, int G, int R, 
       }
       return true;
     }
-    if (load_sc1(abort_word) != 0 || __builtin_amdgcn_s_memrealtime() - t0 > kSpinTimeout) return false;
+    if (ab != 0 || __builtin_amdgcn_s_memrealtime() - t0 > kSpinTimeout) return false;
+    if constexpr (SLEEP) __builtin_amdgcn_s_sleep(2);
   }
 }
 
@@ -3426,7 +3439,7 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
     bool aff_any = false;
     for (int a = 0; a < tp.n_aff; ++a) aff_any |= tp.aff_hist[a] >= 0 && TOT[tp.aff_hist[a]] > 0;
     __syncthreads();  // (readers map an unset minimum to MaxInt32: pmin_of)
-    KGPU_TSTAMP(1);
+    if (ta.trace_mode != 2) KGPU_TSTAMP(1);
     // ---- Filter + raw scores of this workgroup's rows
     bool feas[K];
     TRow o[K];
@@ -3471,7 +3484,7 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
         if (o[j].ds && z < ta.zones) atomicAdd(ZSUM + z, o[j].ds);
       }
     }
-    KGPU_TSTAMP(2);
+    if (ta.trace_mode != 2) KGPU_TSTAMP(2);
     KGPU_WSTAMP(1);
     // ---- statistics round: wave reductions (DPP), workgroup (LDS atomics), granules, every workgroup
     sf = wave_sum32(sf);
@@ -3511,28 +3524,11 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
     __syncthreads();
     KGPU_WSTAMP(4);
     uint64_t* srow = ta.gran + (size_t)i * (R + 1) * G;  // [R][G] statistics granules | [G] keys
-    // this workgroup's value of statistics slot `rr` (LDS after the barrier above), for the polls below
-    // (own_gran).  Every candidate word is read first -- clamped addresses, one LDS round trip -- and then
-    // selected: a switch over the slot puts an LDS read and its wait in each of a dozen divergent
-    // branches, which the wave runs one after another (0.7 us per pod).
-    auto stat_of = [&](int rr) -> int64_t {
-      const int i32 = rr < 6 ? rr : (rr == kTDptsMax ? 6 : 7);
-      const uint32_t w32 = (uint32_t)M.acc32[i32];
-      const int64_t w64 = M.acc64[rr == kTIpaMax ? 1 : 0];
-      const int vi = rr - kTFixed;
-      const int voff = vi < 0 ? ta.o_smask : (vi < ta.soft_words ? ta.o_smask + 4 * vi : ta.o_zsum + 4 * (vi - ta.soft_words));
-      const int32_t wv = *reinterpret_cast<const int32_t*>(lds_raw + voff);
-      if (rr >= kTFixed) return vi < ta.soft_words ? (int64_t)(uint32_t)wv : (int64_t)wv;  // SMASK bits / ZSUM
-      if (rr == kTIpaMin) return w64 == INT64_MAX ? tident(kOpMin) : w64;
-      if (rr == kTIpaMax) return w64 == INT64_MIN ? tident(kOpMax) : w64;
-      if (rr == kTAdjMin) return tp.n_soft ? (int64_t)(uint32_t)~w32 : tident(kOpMin);
-      if (rr == kTAdjMax) return tp.n_soft ? (int64_t)w32 : tident(kOpMax);
-      if (rr == kTFeas || rr == kTNonIgn) return (int32_t)w32;
-      return (int64_t)w32;  // kTMaxT, kTMaxNA, kTDptsMax, kTZoned
-    };
-    // one slot per thread, the same selection written out: the publisher calling stat_of(tid) published
-    // wrong statistics on this compiler (placements off against the C restatement in 31 of 32 persistent
-    // topology test clusters, tools/own_probe.py), the expanded form below does not
+    // one slot per thread.  Every thread reads its candidate words first -- clamped addresses, one LDS
+    // round trip -- and then selects: a switch over the slot puts an LDS read and its wait in each of a
+    // dozen divergent branches, which the wave runs one after another (0.7 us per pod).  (Written out:
+    // the same selection called as a lambda or function, stat_of(tid), published wrong statistics on this
+    // compiler -- profiles/r05_stat_publish_probe.txt.)
     if (tid < R) {
       const int i32 = tid < 6 ? tid : (tid == kTDptsMax ? 6 : 7);
       const uint32_t w32 = (uint32_t)M.acc32[i32];
@@ -3712,14 +3708,12 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
       txrow = sh_ptx[ta.rank] + (size_t)((ta.xseq0 + i) % kTXRing) * txw;
       txtag = kGValid | ((uint64_t)(((ta.xseq0 + i) / kTXRing) & 7) << 60);
     }
-    // own_gran (KGPU_OPT_TBATCH_OWN, off by default): this workgroup's own granules come from LDS, not
-    // from the round trip of its own store (another wave made it) -- measured 1-3 % slower per pod, the
-    // statistics wait longer
-    const int own = ta.own_gran ? g : -1;
     if (!XG && G <= 64 && R <= 4 * W) {
-      ok = tpoll_slots<4, 1>(srow, G, R, W, ta.soft_words, ta.abort, STAT, own, stat_of);
+      ok = ta.poll_sleep ? tpoll_slots<4, 1, true>(srow, G, R, W, ta.soft_words, ta.abort, STAT)
+                         : tpoll_slots<4, 1, false>(srow, G, R, W, ta.soft_words, ta.abort, STAT);
     } else if (!XG && G <= 256 && R <= 2 * W) {
-      ok = tpoll_slots<2, 4>(srow, G, R, W, ta.soft_words, ta.abort, STAT, own, stat_of);
+      ok = ta.poll_sleep ? tpoll_slots<2, 4, true>(srow, G, R, W, ta.soft_words, ta.abort, STAT)
+                         : tpoll_slots<2, 4, false>(srow, G, R, W, ta.soft_words, ta.abort, STAT);
     } else for (int rr = wave; rr < R; rr += W) {
       const int op = tslot_op(rr, ta.soft_words);
       int64_t x;
@@ -3758,7 +3752,9 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
     uint64_t bkey0, bk;
     int bidx0, bi;
     best_under(STAT, ta.diag != 0, bkey0, bidx0);
+    if (ta.trace_mode == 2) KGPU_TSTAMP(1);  // trace mode 2: normalize + keys of the lane's rows done
     wg_best(bkey0, bidx0, bk, bi);
+    if (ta.trace_mode == 2) KGPU_TSTAMP(2);  // ... and the workgroup's best key known
     if (wave == 0 && lane == 0) store_sc1(arow + g, kGValid | bk);
     // the candidate row with this pod applied, for the next pod (used when this workgroup wins; a pod
     // with host ports or extended resources changes memory columns: its winner is evaluated again
@@ -3774,7 +3770,7 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
       KGPU_WSTAMP(3);
       uint64_t wkey = 0;
       int wg = -1;
-      bool pok = poll_row<4, false>(arow, G, ta.abort, kGValid, kGValid, wkey, wg, own, kGValid | bk);
+      bool pok = poll_row<4, false>(arow, G, ta.abort, kGValid, kGValid, wkey, wg);
       if constexpr (XG) {
         // this rank's best: its local winner publishes the record -- the winning node's label values
         // and signature bits first, then (after a system-scope release) the key; workgroup 0 publishes

@@ -19,7 +19,7 @@ def _big(seed, n_nodes=1500, n_existing=600, n_pods=80):
     return nodes, ex, pods, services, rss
 
 
-def _run(args, tfast=1, groups=0, threads=4, geo=None, ahead=None, wlab=None, own=None):
+def _run(args, tfast=1, groups=0, threads=4, geo=None, ahead=None, wlab=None, poll_sleep=None):
     from oracle.cref import RefEngine
     nodes, ex, pods, services, rss = args
     fw = GpuFramework(Profile(), nodes, ex, cluster=Cluster(services=services, rss=rss), pods_hint=pods)
@@ -36,8 +36,8 @@ def _run(args, tfast=1, groups=0, threads=4, geo=None, ahead=None, wlab=None, ow
         fw.engine.set_option(abi.OPT_TOPO_AHEAD, ahead)
     if wlab is not None:
         fw.engine.set_option(abi.OPT_TBATCH_WLAB, wlab)
-    if own is not None:
-        fw.engine.set_option(abi.OPT_TBATCH_OWN, own)
+    if poll_sleep is not None:
+        fw.engine.set_option(abi.OPT_TBATCH_POLL_SLEEP, poll_sleep)
     got, _ = fw.engine.schedule_batch(q, pc)
     return fw, w, got, want.read_nodes(), fw.engine.read_nodes(fw.snap.n_nodes)
 
@@ -77,17 +77,13 @@ def test_gpu_tbatch_winner_labels_switch(seed, wlab):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("own", [0, 1])
-@pytest.mark.parametrize("cfg", ["c", "d"])
-def test_gpu_tbatch_own_granules_switch(cfg, own):
-    """KGPU_OPT_TBATCH_OWN 0 / 1: a workgroup's own exchange granules loaded back or taken from LDS:
-    both against the C restatement, over 5,000 nodes (10 workgroups) and the bench's pod mix."""
-    from kgpu import cluster
-    if cfg == "c":
-        nodes, ex, pods, _ = cluster.taints_affinity_spread(n_nodes=5000, n_pods=300)
-    else:
-        nodes, ex, pods, _ = cluster.pod_affinity(n_nodes=5000, n_existing=5000, n_pods=240)
-    fw, w, got, rw, rg = _run((nodes, ex, pods, [], []), tfast=1, threads=8, own=own)
+@pytest.mark.parametrize("poll_sleep", [0, 1])
+@pytest.mark.parametrize("groups", [0, 2])
+@pytest.mark.parametrize("seed", [1, 6])
+def test_gpu_tbatch_poll_sleep_switch(seed, groups, poll_sleep):
+    """KGPU_OPT_TBATCH_POLL_SLEEP 0 / 1: statistics sweeps back to back or with a sleep between, against
+    the C restatement."""
+    fw, w, got, rw, rg = _run(_big(seed), tfast=1, groups=groups, poll_sleep=poll_sleep)
     _check(w, got, rw, rg)
 
 

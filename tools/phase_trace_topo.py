@@ -19,6 +19,8 @@ def main():
     ap.add_argument("--pods", type=int, default=1000)
     ap.add_argument("--config", default="c")
     ap.add_argument("--groups", type=int, default=0)
+    ap.add_argument("--mode", type=int, default=1,
+                    help="KGPU_OPT_PHASE_TRACE value: 2 splits the normalize phase (stamps 1 / 2 move there)")
     args = ap.parse_args()
     import numpy as np
     from kgpu import abi, cluster
@@ -34,11 +36,20 @@ def main():
         eng.set_option(abi.OPT_PERSIST_GROUPS, args.groups)
     eng.schedule_batch(q[:32], pc)
     eng.upload(fw.snap, fw.arrays)
-    eng.set_option(abi.OPT_PHASE_TRACE, 1)
+    eng.set_option(abi.OPT_PHASE_TRACE, args.mode)
     eng.schedule_batch(q, pc)
     t = eng.phase_trace(len(q) + 1).astype(np.float64) * 10.0  # ns
     t = t[1:len(q) - 1]
     names = ["prefilter", "rows", "stats_pub", "stats_wait", "score_pub", "key_wait", "assume"]
+    if args.mode == 2:  # stamps 1 / 2: normalize + keys done, workgroup argmax done (after stamp 4)
+        for w, name in ((0, "wg0"), (1, "wglast")):
+            a = t[:, w, :]
+            print("config %s %d nodes %s normalize split: per-pod %.0f ns | prefilter+rows+stats_pub %.0f  "
+                  "stats_wait %.0f  normalize+keys %.0f  wg_argmax %.0f  key_store %.0f  key_wait %.0f  assume %.0f"
+                  % (args.config, args.nodes, name, np.median(np.diff(a[:, 0])), np.median(a[:, 3] - a[:, 0]),
+                     np.median(a[:, 4] - a[:, 3]), np.median(a[:, 1] - a[:, 4]), np.median(a[:, 2] - a[:, 1]),
+                     np.median(a[:, 5] - a[:, 2]), np.median(a[:, 6] - a[:, 5]), np.median(a[:, 7] - a[:, 6])))
+        return
     for w, name in ((0, "wg0"), (1, "wglast")):
         a = t[:, w, :]
         per = np.diff(a[:, 0])
