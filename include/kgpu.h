@@ -587,7 +587,8 @@ int kgpu_read_nodes(kgpu_ctx* ctx, int64_t* req_cpu, int64_t* req_mem, int64_t* 
 #define KGPU_OPT_PERSIST_GROUPS 3
 /* KGPU_OPT_PHASE_TRACE (4): record per-pod phase timestamps of the persistent kernel (diagnostics;
  * read with kgpu_read_phase_trace).  2: the topology kernel's stamps 1 and 2 mark the end of its
- * normalize + key pass and of the workgroup argmax instead of PreFilter and the rows. */
+ * normalize + key pass and of the workgroup argmax instead of PreFilter and the rows; 3: the end of its
+ * per-pod record loads + accumulator reset and of its lookup tables (PreFilter split). */
 #define KGPU_OPT_PHASE_TRACE 4
 /* KGPU_OPT_TOPO_FUSED (5): 1 = run a topology pod's six phases (histograms, critical-path minima,
  * filters, scores, normalize + argmax, resolve + assume) in one cooperative launch with grid

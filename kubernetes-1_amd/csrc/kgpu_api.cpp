@@ -3707,7 +3707,7 @@ int kgpu_set_option(kgpu_ctx* c, int32_t option, int64_t value) try {
   else if (option == KGPU_OPT_PERSIST_GROUPS) c->max_groups = (int)std::max<int64_t>(value, 0);
   else if (option == KGPU_OPT_PHASE_TRACE) {
     c->phase_trace = value != 0;
-    c->phase_trace_mode = (int)std::min<int64_t>(std::max<int64_t>(value, 0), 2);
+    c->phase_trace_mode = (int)std::min<int64_t>(std::max<int64_t>(value, 0), 3);
   }
   else if (option == KGPU_OPT_TOPO_FUSED) c->topo_fused = value != 0;
   else if (option == KGPU_OPT_TOPO_PERSISTENT) c->tfast = value != 0;

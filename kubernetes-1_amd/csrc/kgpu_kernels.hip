@@ -1343,30 +1343,36 @@ __device__ __forceinline__ void wg_partials(BatchShared<B>& sh, int p, const uin
                                             int jb, int cand, Cand& ra, Cand& rb) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   Cand a{0, -1, 0}, b{0, -1, 0};
+  if (!vb) {
 #pragma unroll
-  for (int j = 0; j < K; ++j) {
-    const int l = j * B + tid;
-    const bool spare = spare_slot(j, K, tid, B);
-    const uint64_t k = spare ? 0 : keys[j];
-    a.feas += __popcll(__ballot(k != 0));
-    if (k > a.key) { a.key = k; a.idx = l; }
-    if (vb) {
-      const uint64_t kv = spare ? keys[j] : ((tid == ob && j == jb) ? 0 : k);
-      b.feas += __popcll(__ballot(kv != 0));
-      if (kv > b.key) { b.key = kv; b.idx = spare ? cand : l; }
+    for (int j = 0; j < K; ++j) {
+      const uint64_t k = spare_slot(j, K, tid, B) ? 0 : keys[j];
+      a.feas += __popcll(__ballot(k != 0));
+      if (k > a.key) { a.key = k; a.idx = j * B + tid; }
     }
-  }
-  if (vb) {
-    // the two max chains interleaved (independent DPP sequences overlap)
-    uint64_t ma = a.key, mb = b.key;
-    wave_red64x2(ma, mb);
-    const uint64_t ba = __ballot(a.key == ma && ma != 0), bb = __ballot(b.key == mb && mb != 0);
-    a.idx = ba ? __builtin_amdgcn_readlane(a.idx, (int)__builtin_ctzll(ba)) : -1;
-    b.idx = bb ? __builtin_amdgcn_readlane(b.idx, (int)__builtin_ctzll(bb)) : -1;
-    a.key = ma;
-    b.key = mb;
-  } else {
     wave_argmax(a.key, a.idx);
+  } else {
+    // Variant A (the rows as they are) and variant B (the candidate's slot replaced by the spare) share
+    // every row but those two slots: one max chain over the shared rows, then each variant's own slot
+    // from its lane -- one 64-bit DPP reduction per pod instead of two (the row wave is issue-bound).
+    uint64_t m = 0, kc = 0, ks = 0;
+    int mi = -1, f0 = 0;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      const bool spare = spare_slot(j, K, tid, B), isc = tid == ob && j == jb;
+      const uint64_t k = (spare || isc) ? 0 : keys[j];
+      f0 += __popcll(__ballot(k != 0));
+      if (k > m) { m = k; mi = j * B + tid; }
+      if (isc) kc = keys[j];
+      if (spare) ks = keys[j];
+    }
+    wave_argmax(m, mi);
+    const uint64_t kcu = (ob >> 6) == wave ? (uint64_t)lane64((int64_t)kc, ob & 63) : 0;        // A's own slot
+    const uint64_t ksu = ((B - 1) >> 6) == wave ? (uint64_t)lane64((int64_t)ks, (B - 1) & 63) : 0;  // B's
+    a = Cand{m, mi, f0 + (kcu != 0 ? 1 : 0)};
+    if (kcu > m) { a.key = kcu; a.idx = jb * B + ob; }
+    b = Cand{m, mi, f0 + (ksu != 0 ? 1 : 0)};
+    if (ksu > m) { b.key = ksu; b.idx = cand; }
   }
   if (lane == 0) {
     sh.ka[p][wave] = a.key; sh.ia[p][wave] = a.idx; sh.fa[p][wave] = a.feas;
@@ -3417,6 +3423,7 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
     if (tid < 8) M.acc32[tid] = 0;
     if (tid < 2) M.acc64[tid] = tid == 0 ? INT64_MAX : INT64_MIN;
     __syncthreads();
+    if (ta.trace_mode == 3) KGPU_TSTAMP(1);  // trace mode 3: the pod's records loaded, LDS accumulators reset
     for (int k = 0; k < tp.tabs.count; ++k) {
       const TTab tb = cp(ta.tabs)[tp.tabs.begin + k];
       for (int v = tid; v < tb.D; v += B) {
@@ -3435,11 +3442,12 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
       }
     }
     KGPU_WSTAMP(7);
+    if (ta.trace_mode == 3) KGPU_TSTAMP(2);  // ... and its lookup tables built (before the barrier)
     const bool pany = tp.n_hard > 0 && SANY[tp.hard_sig] != 0;
     bool aff_any = false;
     for (int a = 0; a < tp.n_aff; ++a) aff_any |= tp.aff_hist[a] >= 0 && TOT[tp.aff_hist[a]] > 0;
     __syncthreads();  // (readers map an unset minimum to MaxInt32: pmin_of)
-    if (ta.trace_mode != 2) KGPU_TSTAMP(1);
+    if (ta.trace_mode < 2) KGPU_TSTAMP(1);
     // ---- Filter + raw scores of this workgroup's rows
     bool feas[K];
     TRow o[K];
@@ -3484,7 +3492,7 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
         if (o[j].ds && z < ta.zones) atomicAdd(ZSUM + z, o[j].ds);
       }
     }
-    if (ta.trace_mode != 2) KGPU_TSTAMP(2);
+    if (ta.trace_mode < 2) KGPU_TSTAMP(2);
     KGPU_WSTAMP(1);
     // ---- statistics round: wave reductions (DPP), workgroup (LDS atomics), granules, every workgroup
     sf = wave_sum32(sf);

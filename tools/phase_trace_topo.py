@@ -20,7 +20,8 @@ def main():
     ap.add_argument("--config", default="c")
     ap.add_argument("--groups", type=int, default=0)
     ap.add_argument("--mode", type=int, default=1,
-                    help="KGPU_OPT_PHASE_TRACE value: 2 splits the normalize phase (stamps 1 / 2 move there)")
+                    help="KGPU_OPT_PHASE_TRACE value: 2 splits the normalize phase, 3 the PreFilter phase "
+                         "(stamps 1 / 2 move there)")
     args = ap.parse_args()
     import numpy as np
     from kgpu import abi, cluster
@@ -49,6 +50,15 @@ def main():
                   % (args.config, args.nodes, name, np.median(np.diff(a[:, 0])), np.median(a[:, 3] - a[:, 0]),
                      np.median(a[:, 4] - a[:, 3]), np.median(a[:, 1] - a[:, 4]), np.median(a[:, 2] - a[:, 1]),
                      np.median(a[:, 5] - a[:, 2]), np.median(a[:, 6] - a[:, 5]), np.median(a[:, 7] - a[:, 6])))
+        return
+    if args.mode == 3:  # stamps 1 / 2: records loaded + reset, tables built (before the barrier)
+        for w, name in ((0, "wg0"), (1, "wglast")):
+            a = t[:, w, :]
+            print("config %s %d nodes %s prefilter split: per-pod %.0f ns | records+reset+barrier %.0f  tables %.0f  "
+                  "barrier+rows+stats_pub %.0f  stats_wait %.0f  score_pub %.0f  key_wait %.0f  assume %.0f"
+                  % (args.config, args.nodes, name, np.median(np.diff(a[:, 0])), np.median(a[:, 1] - a[:, 0]),
+                     np.median(a[:, 2] - a[:, 1]), np.median(a[:, 3] - a[:, 2]), np.median(a[:, 4] - a[:, 3]),
+                     np.median(a[:, 5] - a[:, 4]), np.median(a[:, 6] - a[:, 5]), np.median(a[:, 7] - a[:, 6])))
         return
     for w, name in ((0, "wg0"), (1, "wglast")):
         a = t[:, w, :]
