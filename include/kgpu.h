@@ -664,6 +664,11 @@ int kgpu_read_nodes(kgpu_ctx* ctx, int64_t* req_cpu, int64_t* req_mem, int64_t* 
 /* KGPU_OPT_TBATCH_POLL_SLEEP (21): 1 (default) = the persistent topology kernel's statistics polls sleep
  * briefly between sweeps; 0 = back to back (A/B switch). */
 #define KGPU_OPT_TBATCH_POLL_SLEEP 21
+/* 22: unused (a register cache of table records in round 5, removed after its A/B) */
+/* KGPU_OPT_ZEROCOPY_POOLS (23): 1 (default) = a kgpu_schedule_one cycle whose only kernel is k_eval reads
+ * the pod's query pools from pinned host memory (no copy on the stream); 0 = they ride in the cycle's
+ * copy (A/B switch). */
+#define KGPU_OPT_ZEROCOPY_POOLS 23
 int kgpu_set_option(kgpu_ctx* ctx, int32_t option, int64_t value);
 /* Engine counters: out[0] = calls issued again with a cooperative launch after a persistent run's
  * workgroups were not all resident before its first pod (KGPU_OPT_COOPERATIVE); out[1] = persistent

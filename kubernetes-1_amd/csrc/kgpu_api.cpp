@@ -192,6 +192,11 @@ struct kgpu_ctx {
   void* cyc_host = nullptr;                        // pinned staging of a short cycle: DevState + queries
   void* res_pin = nullptr;                         // pinned coherent block the short cycle's kernels
   kgpu_result* res_dev = nullptr;                  // write their result records into (its device address)
+  // pinned coherent block a one-launch cycle's k_eval reads the pod's query pools from (zero-copy: no copy
+  // on the stream for pools that change with every pod), and its device address
+  void* pool_pin = nullptr;
+  const char* pool_pin_dev = nullptr;
+  bool zc_pools = true;                            // KGPU_OPT_ZEROCOPY_POOLS
   // short-cycle arena (arena_put): bump offset and capacity in cyc_host / dstate, the byte range
   // still to be copied, and whether a copy from cyc_host may still be pending (kgpu_staging.h)
   kgpu::Arena ar;
@@ -532,7 +537,15 @@ int upload_pool(kgpu_ctx* c, DevBuf& b, const T* src, int32_t n, const T** dst) 
 // the bytes equal the last upload): a pageable copy per pool cost microseconds each on the per-pod
 // (kgpu_schedule_one) path.  The staging block is rewritten only by the next call, after this call's
 // stream synchronize.
-int upload_pools(kgpu_ctx* c, const kgpu_pools* p) {
+constexpr size_t kPoolPinBytes = 64 * 1024;
+
+// zero_copy: a one-pod cycle whose only kernel is k_eval (kgpu_schedule_one's one-launch and normalize
+// cycles without topology state): pools that are not on the device already are read by the kernel from
+// pinned host memory (each wave's reads are uniform: one transaction per wave and word) instead of
+// riding in the cycle's arena copy -- the copy was one hipMemcpyAsync and one copyBuffer dispatch per
+// cycle (profiles/r05_b5000_cycle_hip_stats.txt).  The block is rewritten only by the next cycle, after
+// this one's kernel finished (the cycle returns on its completion word or its stream synchronize).
+int upload_pools(kgpu_ctx* c, const kgpu_pools* p, bool zero_copy = false) {
   kgpu_pools empty{};
   if (!p) p = &empty;
   kgpu::DevPools& q = c->st.qp;
@@ -573,7 +586,16 @@ int upload_pools(kgpu_ctx* c, const kgpu_pools* p) {
   const bool current = c->pool_blk.shadow_p == c->pool_blk.p && c->pool_blk.shadow.size() == total &&
                        std::memcmp(c->pool_blk.shadow.data(), h, total) == 0;
   const char* d = static_cast<const char*>(c->pool_blk.p);
-  if (!current) {
+  if (!current && zero_copy && c->zc_pools && total <= kPoolPinBytes) {
+    if (!c->pool_pin) {
+      HIP_OK(c, hipHostMalloc(&c->pool_pin, kPoolPinBytes, hipHostMallocCoherent | hipHostMallocMapped));
+      void* dp = nullptr;
+      HIP_OK(c, hipHostGetDevicePointer(&dp, c->pool_pin, 0));
+      c->pool_pin_dev = static_cast<const char*>(dp);
+    }
+    std::memcpy(c->pool_pin, h, total);
+    d = c->pool_pin_dev;
+  } else if (!current) {
     // a short cycle's changed pools ride in its arena copy (pool_blk and its shadow stay as they were)
     if (const void* a = arena_put(c, h, total)) {
       d = static_cast<const char*>(a);
@@ -2022,7 +2044,10 @@ int run_batch_once(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_
   if (assume)
     for (int32_t i = 0; i < n; ++i) batch_ports += qs[i].ports.count;
   if ((rc = reserve_ports(c, batch_ports))) return rc;
-  if ((rc = upload_pools(c, pools))) return rc;
+  // the cycles whose only kernel is k_eval (inline_q below): their pools may stay in pinned memory
+  const bool zc = short_cycle && n == 1 && diag && !topo_on && c->comm == nullptr && !(c->xg_nranks > 1) &&
+                  c->st.cut_state == nullptr && c->nom.list.empty() && !c->timing && !c->phase_trace;
+  if ((rc = upload_pools(c, pools, zc))) return rc;
   ht(c, 2);  // 2: ports, pools
   if (!short_cycle) {
     if ((rc = ensure(c, c->queries, sizeof(kgpu_pod_query) * (size_t)n))) return rc;
@@ -3637,6 +3662,7 @@ int kgpu_destroy(kgpu_ctx* c) try {
   }
   if (c->cyc_host) (void)hipHostFree(c->cyc_host);
   if (c->res_pin) (void)hipHostFree(c->res_pin);
+  if (c->pool_pin) (void)hipHostFree(c->pool_pin);
   if (c->st.mcnt) (void)hipFree(c->st.mcnt);
   if (c->st.tcnt) (void)hipFree(c->st.tcnt);
   if (c->shard.p) (void)hipFree(c->shard.p);
@@ -3724,6 +3750,7 @@ int kgpu_set_option(kgpu_ctx* c, int32_t option, int64_t value) try {
   else if (option == KGPU_OPT_XGMI) c->xgmi = value != 0;
   else if (option == KGPU_OPT_TBATCH_WLAB) c->tbatch_wlab = value != 0;
   else if (option == KGPU_OPT_TBATCH_POLL_SLEEP) c->tbatch_sleep = value != 0;
+  else if (option == KGPU_OPT_ZEROCOPY_POOLS) c->zc_pools = value != 0;
   else if (option == KGPU_OPT_RUN_ALL_FILTERS) c->run_all = value != 0;
   else if (option == KGPU_OPT_HOLD_GROUP) c->hold_group = value < 0 || value > INT32_MAX ? -1 : (int32_t)value;
   else if (option == KGPU_OPT_SKIP_RELEASE_AT) c->skip_release_at = value < 0 || value > INT32_MAX ? -1 : (int32_t)value;

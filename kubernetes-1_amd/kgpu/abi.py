@@ -24,6 +24,7 @@ OPT_HOLD_GROUP = 17
 OPT_TBATCH_WLAB = 18
 OPT_RUN_ALL_FILTERS = 20
 OPT_TBATCH_POLL_SLEEP = 21
+OPT_ZEROCOPY_POOLS = 23
 CODE_SUCCESS, CODE_ERROR, CODE_UNSCHEDULABLE, CODE_UNRESOLVABLE = 0, 1, 2, 3
 STATUS_NOT_EVALUATED = 0xFF  # KGPU_FS_NOT_EVALUATED: percentageOfNodesToScore stopped before the node
 

@@ -57,6 +57,33 @@ def test_schedule_one_sequence_matches_oracle(name):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("zc", [0, 1])
+@pytest.mark.parametrize("name", ["fit", "random0", "random7"])
+def test_schedule_one_per_pod_pools(name, zc):
+    """The Go shim's shape: every cycle's pod compiled on its own (its own pools block, different from the
+    last cycle's).  KGPU_OPT_ZEROCOPY_POOLS 1: a one-launch cycle's k_eval reads them from pinned host
+    memory, rewritten every cycle; 0: they ride in the cycle's copy.  Both against the C restatement of
+    the same sequence (compiled as one batch), placements and node rows."""
+    nodes, existing, pods, prof = _case(name)
+    fw = GpuFramework(prof, nodes, existing, pods_hint=pods)
+    q, pc, _, errs = fw.compile_pods(pods)
+    assert not errs
+    want, want_rows = _ref(fw, q, pc)
+    fw.engine.upload(fw.snap, fw.arrays)
+    fw.engine.set_option(abi.OPT_ZEROCOPY_POOLS, zc)
+    got = np.zeros(len(q), abi.RESULT)
+    for i, pod in enumerate(pods):
+        qi, pci, _, errs = fw.compile_pods([pod])
+        assert not errs
+        got[i], _ = fw.engine.schedule_one(qi[0], pci, seq=i, assume=True)
+    for f in ("node", "feasible", "scored", "score"):
+        np.testing.assert_array_equal(want[f], got[f], err_msg="%s: %s" % (name, f))
+    rows = fw.engine.read_nodes(fw.snap.n_nodes)
+    for k in ROW_KEYS:
+        np.testing.assert_array_equal(want_rows[k], rows[k], err_msg="%s: %s" % (name, k))
+
+
+@pytest.mark.gpu
 def test_schedule_one_without_assume_leaves_rows():
     nodes, existing, pods, prof = _case("fit")
     fw = GpuFramework(prof, nodes, existing, pods_hint=pods)

@@ -18,6 +18,7 @@ def main():
     ap.add_argument("--nodes", type=int, default=5000)
     ap.add_argument("--pods", type=int, default=300)
     ap.add_argument("--config", default="b")
+    ap.add_argument("--zc", type=int, default=None, help="KGPU_OPT_ZEROCOPY_POOLS (default: the library's, 1)")
     args = ap.parse_args()
     from kgpu import cluster
     from kgpu.framework import GpuFramework
@@ -31,6 +32,9 @@ def main():
     q, pc, _, errs = fw.compile_pods(pods)
     assert not errs
     eng = fw.engine
+    if args.zc is not None:
+        from kgpu import abi
+        eng.set_option(abi.OPT_ZEROCOPY_POOLS, args.zc)
     for i in range(20):  # warm
         eng.schedule_one(q[i], pc, seq=i, assume=False)
     lat = []
