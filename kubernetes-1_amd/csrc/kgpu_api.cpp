@@ -2605,6 +2605,9 @@ int alloc_node_work(kgpu_ctx* c) {
   // raw | normalized in one block: a diagnostic cycle zeroes both with one memset
   if ((rc = dalloc(c, W, &st.diag_raw, (size_t)2 * KGPU_NUM_SCORES * N))) return rc;
   st.diag_norm = st.diag_raw + (size_t)KGPU_NUM_SCORES * N;
+  // the rows of plugins outside the profile are never written: zero from here on (the kernels zero only
+  // the profile's rows per diagnostic cycle)
+  if (N) HIP_OK(c, hipMemset(st.diag_raw, 0, sizeof(int64_t) * 2 * KGPU_NUM_SCORES * N));
   HIP_OK(c, hipMemset(st.status, 0, sizeof(uint32_t) * std::max<size_t>(N, 1)));
   if ((rc = dalloc(c, W, &st.raw_pts, N))) return rc;
   if ((rc = dalloc(c, W, &st.raw_ipa, N))) return rc;

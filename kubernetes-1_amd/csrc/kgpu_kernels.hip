@@ -943,10 +943,11 @@ __global__ __launch_bounds__(kBlock) void k_eval(const DevState* __restrict__ st
       assume_counts(st, a.prev, n);
     }
     if (a.zero_diag) {
-      // a diagnostic cycle without memsets: this node's rows start at 0 (a plugin outside the
-      // profile, or a node that fails a filter, reads 0 as after hipMemset)
-#pragma unroll
-      for (int s = 0; s < KGPU_NUM_SCORES; ++s) {
+      // a diagnostic cycle without memsets: this node's rows of the profile's plugins start at 0 (a node
+      // that fails a filter reads 0 as after hipMemset); a plugin outside the profile has rows no kernel
+      // writes, zeroed once when they were allocated
+      for (int si = 0; si < st.n_scores; ++si) {
+        const int s = st.scores[si];
         gp(st.diag_raw)[(size_t)s * st.N + n] = 0;
         gp(st.diag_norm)[(size_t)s * st.N + n] = 0;
       }
@@ -3352,7 +3353,8 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
         // a diagnostic (kgpu_schedule_one) run: this node's per-plugin raw / normalized rows start at
         // 0 (this lane's later stores of them follow in program order; kDefer runs store every row
         // once at the end instead)
-        for (int sc = 0; sc < KGPU_NUM_SCORES; ++sc) {
+        for (int si = 0; si < st.n_scores; ++si) {  // the profile's plugins (the others stay 0)
+          const int sc = cp(st.scores)[si];
           gp(st.diag_raw)[(size_t)sc * st.N + n] = 0;
           gp(st.diag_norm)[(size_t)sc * st.N + n] = 0;
         }
@@ -3923,15 +3925,14 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
         gp(st.status)[n] = dstat;
 #pragma unroll
         for (int k = 0; k < KGPU_NUM_SCORES; ++k) {
+          if (!((SM >> k) & 1u)) continue;  // outside the profile: rows no kernel writes, zero since allocation
           int64_t raw = 0, nrm = 0;
-          if ((SM >> k) & 1u) {
-            if (k == KGPU_S_POD_TOPOLOGY_SPREAD) { raw = dt[0]; nrm = dn[2]; }
-            else if (k == KGPU_S_INTER_POD_AFFINITY) { raw = dt[1]; nrm = dn[3]; }
-            else if (k == KGPU_S_DEFAULT_POD_TOPOLOGY_SPREAD) { raw = dt[2]; nrm = dn[4]; }
-            else if (k == KGPU_S_TAINT_TOLERATION) { raw = dv[k]; nrm = dn[0]; }
-            else if (k == KGPU_S_NODE_AFFINITY) { raw = dv[k]; nrm = dn[1]; }
-            else { raw = dv[k]; nrm = dv[k]; }
-          }
+          if (k == KGPU_S_POD_TOPOLOGY_SPREAD) { raw = dt[0]; nrm = dn[2]; }
+          else if (k == KGPU_S_INTER_POD_AFFINITY) { raw = dt[1]; nrm = dn[3]; }
+          else if (k == KGPU_S_DEFAULT_POD_TOPOLOGY_SPREAD) { raw = dt[2]; nrm = dn[4]; }
+          else if (k == KGPU_S_TAINT_TOLERATION) { raw = dv[k]; nrm = dn[0]; }
+          else if (k == KGPU_S_NODE_AFFINITY) { raw = dv[k]; nrm = dn[1]; }
+          else { raw = dv[k]; nrm = dv[k]; }
           gp(st.diag_raw)[(size_t)k * N + n] = raw;
           gp(st.diag_norm)[(size_t)k * N + n] = nrm;
         }
