@@ -418,7 +418,11 @@ int kgpu_schedule_batch(kgpu_ctx* ctx, const kgpu_pod_query* qs, int32_t n, cons
  * pods, normalize pods, host ports, nominated pods, node sharding, percentageOfNodesToScore < 100,
  * short batches) runs synchronously inside _submit after the batches in flight; its _wait returns its
  * status.  Every other call on the context fails with KGPU_E_STATE while batches are in flight.
- * kgpu_pipelined returns the number of batches submitted and not yet waited for. */
+ * kgpu_pipelined returns the number of batches submitted and not yet waited for.
+ * A pipelined batch is never re-issued: if one of its persistent workgroups starts late (the ordinary
+ * launch of KGPU_OPT_COOPERATIVE 0 under transient contention), its _wait fails with KGPU_E_DEVICE and
+ * the mirror must be uploaded again, even when the abort was clean (a later batch may already be queued
+ * behind it).  Callers that cannot afford a re-upload set KGPU_OPT_COOPERATIVE to 1. */
 int kgpu_schedule_batch_submit(kgpu_ctx* ctx, const kgpu_pod_query* qs, int32_t n, const kgpu_pools* pools,
                                int64_t first_seq, kgpu_result* results, kgpu_stats* stats);
 int kgpu_schedule_batch_wait(kgpu_ctx* ctx);

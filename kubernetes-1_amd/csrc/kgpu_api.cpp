@@ -2469,9 +2469,16 @@ int run_batch_once(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_
   if (done_word && short_cycle && n == 1 && !batch_ports && !timed && (!used_persistent || c->tb_abort_mapped)) {
     const int64_t t_end = now_ns() + 2000000000ll;
     const int32_t* ev = &static_cast<kgpu_result*>(c->res_pin)[0].evaluated;
-    while (!(landed = __atomic_load_n(done_word, __ATOMIC_ACQUIRE) != -1 &&
-                      __atomic_load_n(ev, __ATOMIC_ACQUIRE) != INT32_MIN) &&
-           now_ns() < t_end) {
+    // a non-zero word is an abort code: the run wrote no record, so stop at once and let the
+    // synchronize below complete the stream (an aborted cycle used to spin the full 2 s)
+    for (;;) {
+      const int32_t w = __atomic_load_n(done_word, __ATOMIC_ACQUIRE);
+      if (w > 0) break;
+      if (w == 0 && __atomic_load_n(ev, __ATOMIC_ACQUIRE) != INT32_MIN) {
+        landed = true;
+        break;
+      }
+      if (now_ns() >= t_end) break;
     }
   }
   if (landed && c->htrace) ht(c, 11);
@@ -4379,6 +4386,10 @@ int kgpu_debug_broken_linear(kgpu_ctx* c, const kgpu_shape_point* points, int32_
 int kgpu_get_filter(kgpu_ctx* c, uint32_t* words) try {
   if (c && !c->pipe_q.empty())
     return fail(c, KGPU_E_STATE, "pipelined batches in flight: complete them with kgpu_schedule_batch_wait first");
+  if (c && c->unsettled) {  // a short cycle returned on its completion word: the stream first
+    const int rs_ = settle(c);
+    if (rs_) return rs_;
+  }
   if (!c || !words) return KGPU_E_INVAL;
   if (!c->last_diag) return fail(c, KGPU_E_STATE, "no kgpu_schedule_one cycle to report");
   HIP_OK(c, hipMemcpy(words, c->st.status, sizeof(uint32_t) * (size_t)c->st.N, hipMemcpyDeviceToHost));
@@ -4390,6 +4401,10 @@ int kgpu_get_filter(kgpu_ctx* c, uint32_t* words) try {
 int kgpu_get_filter_all(kgpu_ctx* c, uint32_t* words) try {
   if (c && !c->pipe_q.empty())
     return fail(c, KGPU_E_STATE, "pipelined batches in flight: complete them with kgpu_schedule_batch_wait first");
+  if (c && c->unsettled) {  // a short cycle returned on its completion word: the stream first
+    const int rs_ = settle(c);
+    if (rs_) return rs_;
+  }
   if (!c || !words) return KGPU_E_INVAL;
   if (!c->last_diag || !c->last_run_all)
     return fail(c, KGPU_E_STATE, "no kgpu_schedule_one cycle under KGPU_OPT_RUN_ALL_FILTERS to report");
@@ -4403,6 +4418,10 @@ int kgpu_get_filter_all(kgpu_ctx* c, uint32_t* words) try {
 int kgpu_get_scores(kgpu_ctx* c, int32_t plugin, int64_t* raw, int64_t* normalized) try {
   if (c && !c->pipe_q.empty())
     return fail(c, KGPU_E_STATE, "pipelined batches in flight: complete them with kgpu_schedule_batch_wait first");
+  if (c && c->unsettled) {  // a short cycle returned on its completion word: the stream first
+    const int rs_ = settle(c);
+    if (rs_) return rs_;
+  }
   if (!c || plugin < 0 || plugin >= KGPU_NUM_SCORES) return KGPU_E_INVAL;
   if (!c->last_diag) return fail(c, KGPU_E_STATE, "no kgpu_schedule_one cycle to report");
   const size_t N = (size_t)c->st.N;

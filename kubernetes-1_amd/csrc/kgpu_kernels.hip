@@ -3842,7 +3842,9 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
         }
       } else if (lane == 0) {
         if (!pok) {
-          __hip_atomic_fetch_or(ta.abort, acode, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          // a key-poll timeout is never clean: a workgroup that published its key late may still see
+          // every key, resolve the pod and assume it (only the statistics phase of pod 0 is clean)
+          __hip_atomic_fetch_or(ta.abort, kAbortDirty, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           M.abort = 1;
         }
         M.wkey = wkey;

@@ -267,11 +267,10 @@ def sharded_spread_compiled(n_nodes=1_000_000, n_pods=10000, shard=None, n_hint=
     nz = min(N, n_zones)
     for i in range(nz):
         comp.nkeys.add(ZONE, "zone%d" % i)
+    names = ["node%d" % i for i in range(N)]
     if N:
-        comp.nkeys.add_key(HOSTNAME)
-        hv = comp.nkeys.vals[1]
-        hv.items = ["node%d" % i for i in range(N)]
-        hv.ids = dict(zip(hv.items, range(N)))
+        hk = comp.nkeys.add_key(HOSTNAME)
+        comp.nkeys.vals[hk].add_many(names)
     t_ded = ("dedicated", "infra", "NoSchedule")
     t_spot = ("spot", "true", "PreferNoSchedule")
     f_ded = int(np.argmax(ded)) if ded.any() else None
@@ -287,8 +286,7 @@ def sharded_spread_compiled(n_nodes=1_000_000, n_pods=10000, shard=None, n_hint=
     comp.ns.add("")
     # Snapshot.List(): node i sits in zone i % n_zones at position i // n_zones of that zone, so the
     # zone round robin (node_tree.go:147-170) lists the nodes in insertion order
-    comp.order = hv.items if N else []
-    comp.node_index = hv.ids if N else {}
+    comp.set_order(names, first_wins=False)
     A = comp.empty_columns(N)
     A["alloc_cpu"][:] = cpu * 1000
     A["alloc_mem"][:] = mem * GI
@@ -303,8 +301,7 @@ def sharded_spread_compiled(n_nodes=1_000_000, n_pods=10000, shard=None, n_hint=
         tid = comp.taints.get(t)
         if tid >= 0:
             A[col][tid // 64][mask] |= np.uint64(1 << (tid % 64))
-    empty = [[] for _ in range(N)]
-    compiled = comp.finish_snapshot(A, empty, empty, (), shard)
+    compiled = comp.snapshot_from_columns(A, shard)
     return comp, compiled, pods, prof
 
 

@@ -1,21 +1,29 @@
 """Compile k8s-v1-shaped objects into the engine's dictionary-encoded SoA inputs (include/kgpu.h).
 
-This is the host half of PreFilter: everything that is per-pod or per-object string work happens
-here once (label keys/values, namespaces, taints, images and controller UIDs become dense ids;
-selectors become requirement programs; tolerations become bit masks over the cluster's taint
-dictionary), so that the device only ever compares integers.
+The compile itself is libkgpu's (include/kgpu_compile.h, csrc/kgpu_compile.cpp): the one implementation
+of the PreFilter-time string work that the Go shim calls too.  This module marshals dicts into its
+descriptors (cdesc.py), holds the handles, and copies the results into numpy arrays:
 
-Semantics follow the reference files cited at each step; the device and the C restatement
-consume exactly these arrays.
+  Compiler           kgpu_compiler: the cluster dictionaries of one upload epoch (label keys / values,
+                     namespaces, taints, images, controller UIDs become dense ids)
+  Pools              kgpu_pool_set: the records kgpu_range fields point into, interned by content
+  compile_pod        kgpu_compile_pod -> kgpu_pod_query
+  compile_snapshot   kgpu_compile_snapshot -> kgpu_snapshot columns (existing pods folded in)
+  node_row / key_meta / node_lists   the delta stream's records (kgpu_apply_delta)
+
+What stays host-side here is lister work the Go shim gets from the reference's own helpers:
+helper.DefaultSelector (default_selector below, helper/spread.go:29-72) and the PodDisruptionBudget
+selector check of preemption (label_selector_matches).
 """
+import ctypes as C
+
 import numpy as np
 
 from . import abi
 from . import api
+from . import cdesc
 
 HOSTNAME = api.LABEL_HOSTNAME
-_PROTO = {"TCP": 0, "UDP": 1, "SCTP": 2}
-
 
 class StrDict:
     __slots__ = ("ids", "items")
@@ -71,133 +79,70 @@ class NeedsUpload(Exception):
     """A cluster change the device columns cannot absorb as a delta: upload the snapshot again."""
 
 
-class Pools:
-    """Growable pools referenced by kgpu_range fields.
+_POOL_FIELDS = (("reqs", abi.REQ), ("ints", np.dtype("<i4")), ("words", np.dtype("<u8")),
+                ("node_terms", abi.NODE_TERM), ("pref_terms", abi.PREF_TERM), ("spreads", abi.SPREAD),
+                ("pod_terms", abi.POD_TERM), ("scalars", abi.SCALAR_REQ), ("ports", abi.PORT))
 
-    Ranges are interned by content: pods compiled from one template (a Deployment's replicas)
-    share every record, so the device reads one cache-hot copy instead of a fresh line per pod."""
+
+def _copy(ptr, dtype, count, shape=None):
+    """A numpy copy of `count` records at a C pointer (owned by the compiler)."""
+    dtype = np.dtype(dtype)
+    if not count:
+        out = np.zeros(0, dtype)
+    else:
+        buf = (C.c_char * (dtype.itemsize * int(count))).from_address(ptr)
+        out = np.frombuffer(buf, dtype).copy()
+    return out.reshape(shape) if shape is not None else out
+
+
+def pools_numpy(view):
+    """Numpy copies of a kgpu_pools view's records, by pool name."""
+    return {f: _copy(getattr(view, f), dt, getattr(view, "n_" + f)) for f, dt in _POOL_FIELDS}
+
+
+def pools_struct(P):
+    """An abi.Pools pointing at the numpy arrays P (the struct keeps them alive)."""
+    c = abi.Pools()
+    for k, a in P.items():
+        setattr(c, k, abi.ptr(a))
+        setattr(c, "n_" + k, len(a))
+    c._keep = P
+    return c
+
+
+class Pools:
+    """A kgpu_pool_set: growable pools referenced by kgpu_range fields, interned by content (pods compiled
+    from one template, a Deployment's replicas, share every record)."""
 
     def __init__(self):
-        self.reqs, self.ints, self.words = [], [], []
-        self.node_terms, self.pref_terms, self.spreads, self.pod_terms = [], [], [], []
-        self.scalars, self.ports = [], []
-        self._cache = {}
-        self._np = None
+        self._L = cdesc.lib()
+        h = C.c_void_p()
+        rc = self._L.kgpu_pools_create(C.byref(h))
+        if rc != 0:
+            raise MemoryError("kgpu_pools_create failed")
+        self.h = h
 
-    def _rng(self, lst, items):
-        items = list(items)
-        if not items:
-            return (0, 0)
-        key = (id(lst), tuple(items))
-        r = self._cache.get(key)
-        if r is None:
-            r = self._cache[key] = (len(lst), len(items))
-            lst.extend(items)
-        return r
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h is not None and h.value:
+            self._L.kgpu_pools_destroy(h)
+            self.h = None
 
-    def truncate(self, lst, n):
-        """Drop records appended after position n (a compile step that failed half-way)."""
-        del lst[n:]
-        for k in [k for k, v in self._cache.items() if k[0] == id(lst) and v[0] + v[1] > n]:
-            del self._cache[k]
+    def view(self):
+        v = abi.Pools()
+        self._L.kgpu_pools_view(self.h, C.byref(v))
+        return v
 
-    def ints_range(self, xs):
-        return self._rng(self.ints, [int(x) for x in xs])
-
-    def words_range(self, ws):
-        return self._rng(self.words, [int(w) for w in ws])
+    def scalar_name(self, i):
+        s = cdesc.Str()
+        if self._L.kgpu_pools_scalar_name(self.h, int(i), C.byref(s)) != 0:
+            raise IndexError(i)
+        return C.string_at(s.p, s.n).decode() if s.n else ""
 
     def finalize(self):
-        P = {}
-        P["reqs"] = np.array(self.reqs, dtype=abi.REQ) if self.reqs else np.zeros(0, abi.REQ)
-        P["ints"] = np.array(self.ints, dtype=np.int32)
-        P["words"] = np.array(self.words, dtype=np.uint64)
-        P["node_terms"] = np.array(self.node_terms, dtype=abi.NODE_TERM) if self.node_terms else np.zeros(0, abi.NODE_TERM)
-        P["pref_terms"] = np.array(self.pref_terms, dtype=abi.PREF_TERM) if self.pref_terms else np.zeros(0, abi.PREF_TERM)
-        P["spreads"] = np.array(self.spreads, dtype=abi.SPREAD) if self.spreads else np.zeros(0, abi.SPREAD)
-        P["pod_terms"] = np.array(self.pod_terms, dtype=abi.POD_TERM) if self.pod_terms else np.zeros(0, abi.POD_TERM)
-        P["scalars"] = np.array(self.scalars, dtype=abi.SCALAR_REQ) if self.scalars else np.zeros(0, abi.SCALAR_REQ)
-        P["ports"] = np.array(self.ports, dtype=abi.PORT) if self.ports else np.zeros(0, abi.PORT)
-        self._np = P
-        c = abi.Pools()
-        for k, a in P.items():
-            setattr(c, k, abi.ptr(a))
-            setattr(c, "n_" + k, len(a))
-        c._keep = P  # the struct holds raw pointers: the arrays live as long as it does
-        return c, P
-
-
-# ----------------------------------------------------------------- selector compilation
-_LSEL = {"In": abi.OP_IN, "NotIn": abi.OP_NOTIN, "Exists": abi.OP_EXISTS, "DoesNotExist": abi.OP_DNE}
-_NSEL = dict(_LSEL, Gt=abi.OP_GT, Lt=abi.OP_LT)
-
-
-def _validate_req(key, op, vals):
-    """labels.NewRequirement validation (selector.go:140-190); raises CompileError."""
-    if not api.qualified_name_ok(key):
-        raise CompileError("invalid label key %r" % key)
-    if op in (abi.OP_IN, abi.OP_NOTIN) and len(vals) == 0:
-        raise CompileError("values set can't be empty")
-    if op in (abi.OP_EXISTS, abi.OP_DNE) and len(vals) != 0:
-        raise CompileError("values set must be empty")
-    if op in (abi.OP_GT, abi.OP_LT):
-        if len(vals) != 1 or api.parse_int64(vals[0]) is None:
-            raise CompileError("Gt/Lt needs one integer value")
-    for v in vals:
-        if not api.label_value_ok(v):
-            raise CompileError("invalid label value %r" % v)
-
-
-def _req_rec(ks, pools, key, op, vals, register=False):
-    """register: pod label selectors add their key and values to the pod key space, so that a pod
-    compiled later with that label gets the ids the selector already holds (node selectors run
-    against the fixed node set of the snapshot and drop unknown values instead)."""
-    if register:
-        ki = ks.add_key(key)
-        for v in vals if op in (abi.OP_IN, abi.OP_NOTIN) else ():
-            ks.add(key, v)
-    else:
-        ki = ks.key(key)
-    vids = []
-    if op in (abi.OP_IN, abi.OP_NOTIN) and ki >= 0:
-        vids = sorted({ks.val(ki, v) for v in vals} - {-1})
-    imm = api.parse_int64(vals[0]) if op in (abi.OP_GT, abi.OP_LT) else 0
-    return (ki, op, pools.ints_range(vids), imm)
-
-
-def compile_label_selector(ks, pools, ps):
-    """metav1.LabelSelectorAsSelector (apis/meta/v1/helpers.go:34-70) -> kgpu_selector tuple."""
-    if ps is None:
-        return (abi.SEL_NOTHING, 0, (0, 0))
-    ml = ps.get("matchLabels") or {}
-    me = ps.get("matchExpressions") or []
-    recs = []
-    for k in sorted(ml):
-        _validate_req(k, abi.OP_IN, [ml[k]])
-        recs.append(_req_rec(ks, pools, k, abi.OP_IN, [ml[k]], register=True))
-    for e in me:
-        op = _LSEL.get(e.get("operator"))
-        if op is None:
-            raise CompileError("invalid pod selector operator %r" % e.get("operator"))
-        vals = list(e.get("values") or [])
-        _validate_req(e.get("key", ""), op, vals)
-        recs.append(_req_rec(ks, pools, e.get("key", ""), op, vals, register=True))
-    return (abi.SEL_AND, 0, pools._rng(pools.reqs, recs))
-
-
-def compile_node_reqs(ks, pools, nsm, validate=True):
-    """NodeSelectorRequirementsAsSelector (helpers.go:237-267) body; returns a reqs range."""
-    recs = []
-    for e in nsm:
-        op = _NSEL.get(e.get("operator"))
-        if op is None:
-            raise CompileError("invalid node selector operator %r" % e.get("operator"))
-        vals = list(e.get("values") or [])
-        if validate:
-            _validate_req(e.get("key", ""), op, vals)
-        recs.append(_req_rec(ks, pools, e.get("key", ""), op, vals))
-    return pools._rng(pools.reqs, recs)
-
+        """(abi.Pools over numpy copies of the records, {pool name: numpy array})."""
+        P = pools_numpy(self.view())
+        return pools_struct(P), P
 
 def label_selector_matches(ps, labels):
     """Host-side evaluation of a LabelSelector against a label map (used for self-matches)."""
@@ -222,21 +167,6 @@ def label_selector_matches(ps, labels):
 
 def set_selector_matches(sel_map, labels):
     return all(labels.get(k) == v for k, v in sel_map.items())
-
-
-# ----------------------------------------------------------------- taints / tolerations
-def _tolerates(t, key, value, effect):
-    """v1.Toleration.ToleratesTaint (staging/src/k8s.io/api/core/v1/toleration.go:37-56)."""
-    te = t.get("effect", "") or ""
-    if te and te != effect:
-        return False
-    tk = t.get("key", "") or ""
-    if tk and tk != key:
-        return False
-    op = t.get("operator", "") or ""
-    if op in ("", "Equal"):
-        return (t.get("value", "") or "") == value
-    return op == "Exists"
 
 
 class Profile:
@@ -324,7 +254,7 @@ def default_selector(pod, cluster):
                 try:
                     if ps is not None:
                         for e in ps.get("matchExpressions") or []:
-                            if e.get("operator") not in _LSEL:
+                            if e.get("operator") not in ("In", "NotIn", "Exists", "DoesNotExist"):
                                 raise CompileError("bad op")
                 except CompileError:
                     failed = True
@@ -345,65 +275,169 @@ def default_selector(pod, cluster):
 
 
 # ----------------------------------------------------------------- the compiler
+class CDict:
+    """One of the compiler's dictionaries (kgpu_dict_*): ids in first-seen order.  Taints are (key, value,
+    effect) tuples and controllers (kind, uid) tuples, the others strings."""
+
+    def __init__(self, comp, d, key=0):
+        self.comp, self.d, self.key = comp, d, key
+        self.parts = 3 if d == cdesc.DICT_TAINT else (2 if d == cdesc.DICT_CONTROLLER else 1)
+
+    def _parts(self, x):
+        xs = tuple(x) if self.parts > 1 else (x,)
+        return (cdesc.Str * len(xs))(*[cdesc.s_(p if p is not None else "") for p in xs]), len(xs)
+
+    def add(self, x):
+        arr, n = self._parts(x)
+        i = self.comp._L.kgpu_dict_add(self.comp._cc, self.d, self.key, arr, n)
+        if i < 0:
+            raise ValueError("kgpu_dict_add(%d): %d %s" % (self.d, i, self.comp._err()))
+        return i
+
+    def get(self, x):
+        arr, n = self._parts(x)
+        return self.comp._L.kgpu_dict_get(self.comp._cc, self.d, self.key, arr, n)
+
+    def add_many(self, xs):
+        """Single-part items in order, in one call (a columnar generator's million hostnames)."""
+        bs = [x.encode() for x in xs]
+        off = np.zeros(len(bs) + 1, np.int64)
+        np.cumsum([len(b) for b in bs], out=off[1:])
+        rc = self.comp._L.kgpu_dict_add_many(self.comp._cc, self.d, self.key, b"".join(bs), off.ctypes.data,
+                                             len(bs), None)
+        if rc != 0:
+            raise ValueError("kgpu_dict_add_many: %d %s" % (rc, self.comp._err()))
+
+    def __len__(self):
+        return max(0, self.comp._L.kgpu_dict_size(self.comp._cc, self.d, self.key))
+
+    def item(self, i):
+        L = self.comp._L
+        n = L.kgpu_dict_item(self.comp._cc, self.d, self.key, i, None, 0)
+        buf = C.create_string_buffer(max(1, n))
+        L.kgpu_dict_item(self.comp._cc, self.d, self.key, i, buf, n)
+        s = buf.raw[:n].decode()
+        return tuple(s.split("\0")) if self.parts > 1 else s
+
+    @property
+    def items(self):
+        return [self.item(i) for i in range(len(self))]
+
+    @property
+    def ids(self):
+        return {x: i for i, x in enumerate(self.items)}
+
+
+class CKeySpace:
+    """Label keys, each with its own value dictionary (values are topology domains)."""
+
+    class _Vals:
+        def __init__(self, ks):
+            self.ks = ks
+
+        def __getitem__(self, k):
+            if k < 0 or k >= len(self):
+                raise IndexError(k)
+            return CDict(self.ks.comp, self.ks.vald, k)
+
+        def __len__(self):
+            return len(self.ks.keys)
+
+        def __iter__(self):
+            return (self[k] for k in range(len(self)))
+
+    def __init__(self, comp, keyd, vald):
+        self.comp, self.vald = comp, vald
+        self.keys = CDict(comp, keyd)
+        self.vals = CKeySpace._Vals(self)
+
+    def add_key(self, k):
+        return self.keys.add(k)
+
+    def add(self, k, v):
+        ki = self.keys.add(k)
+        return ki, CDict(self.comp, self.vald, ki).add(v)
+
+    def key(self, k):
+        return self.keys.get(k)
+
+    def val(self, ki, v):
+        return -1 if ki < 0 else CDict(self.comp, self.vald, ki).get(v)
+
+
+_SNAP_1D = (("alloc_cpu", "<i8"), ("alloc_mem", "<i8"), ("alloc_eph", "<i8"), ("alloc_pods", "<i4"),
+            ("req_cpu", "<i8"), ("req_mem", "<i8"), ("req_eph", "<i8"), ("nz_cpu", "<i8"), ("nz_mem", "<i8"),
+            ("num_pods", "<i4"), ("unschedulable", "u1"), ("zone_id", "<i4"), ("port_count", "<i4"))
+
+
 class Compiler:
+    """A kgpu_compiler: the cluster dictionaries of one upload epoch, and the compile of pods, snapshots and
+    delta records against them (csrc/kgpu_compile.cpp)."""
+
     def __init__(self, profile, cluster=None):
         self.profile = profile
         self.cluster = cluster or Cluster()
-        self.nkeys = KeySpace()       # node label keys / values
-        self.pkeys = KeySpace()       # pod label keys / values
-        self.ns = StrDict()
-        self.taints = StrDict()       # (key, value, effect)
-        self.scalars = StrDict()
-        self.images = StrDict()
-        self.controllers = StrDict()  # (kind, uid)
-        self.uids = StrDict()         # pod UIDs (kgpu_pod_query.uid = id + 1; 0: none)
-        self.ips = StrDict()
-        self.ips.add("0.0.0.0")
-        self.protos = StrDict()
-        for p in ("TCP", "UDP", "SCTP"):
-            self.protos.add(p)
-        self.zones = StrDict()
-        self.node_index = {}
+        self._L = cdesc.lib()
+        p, keep = cdesc.profile_desc(profile)
+        h = C.c_void_p()
+        rc = self._L.kgpu_compiler_create(C.byref(p), C.byref(h))
+        if rc != 0:
+            raise MemoryError("kgpu_compiler_create failed")
+        self._cc = h
+        self.nkeys = CKeySpace(self, cdesc.DICT_NODE_KEY, cdesc.DICT_NODE_VALUE)
+        self.pkeys = CKeySpace(self, cdesc.DICT_POD_KEY, cdesc.DICT_POD_VALUE)
+        for attr, d in (("ns", cdesc.DICT_NAMESPACE), ("taints", cdesc.DICT_TAINT), ("scalars", cdesc.DICT_SCALAR),
+                        ("images", cdesc.DICT_IMAGE), ("controllers", cdesc.DICT_CONTROLLER),
+                        ("uids", cdesc.DICT_UID), ("ips", cdesc.DICT_IP), ("protos", cdesc.DICT_PROTOCOL),
+                        ("zones", cdesc.DICT_ZONE)):
+            setattr(self, attr, CDict(self, d))
         self.order = []
-        for r, _ in list(profile.least_resources) + list(profile.most_resources) + list(profile.rtcr_resources):
-            if r not in ("cpu", "memory", "ephemeral-storage"):
-                self.scalars.add(r)
+        self.node_index = {}
+
+    def __del__(self):
+        h = getattr(self, "_cc", None)
+        if h is not None and h.value:
+            self._L.kgpu_compiler_destroy(h)
+            self._cc = None
+
+    def _err(self):
+        m = self._L.kgpu_compiler_last_error(self._cc)
+        return m.decode() if m else ""
+
+    @property
+    def dims(self):
+        d = np.zeros(3, np.int32)
+        self._L.kgpu_compiler_dims(self._cc, d.ctypes.data)
+        return {"S": int(d[0]), "K": int(d[1]), "TW": int(d[2])}
+
+    def set_order(self, names, first_wins=True):
+        """The node list node names resolve against (Snapshot.List() order)."""
+        names = list(names)
+        bs = [n.encode() for n in names]
+        off = np.zeros(len(bs) + 1, np.int64)
+        np.cumsum([len(b) for b in bs], out=off[1:])
+        rc = self._L.kgpu_compiler_set_order(self._cc, b"".join(bs), off.ctypes.data, len(bs), 1 if first_wins else 0)
+        if rc != 0:
+            raise ValueError(self._err())
+        self.order = names
+        idx = {}
+        if first_wins:
+            for i, nm in enumerate(names):
+                idx.setdefault(nm, i)
+        else:
+            idx = {nm: i for i, nm in enumerate(names)}
+        self.node_index = idx
 
     # -------------------------------------------------- dictionaries
     def register_node(self, n):
-        for k, v in api.labels_of(n).items():
-            self.nkeys.add(k, v)
-        for t in api.spec(n).get("taints") or []:
-            self.taints.add((t.get("key", "") or "", t.get("value", "") or "", t.get("effect", "") or ""))
-        for r in ((n.get("status") or {}).get("allocatable") or {}):
-            if api.is_scalar(r):
-                self.scalars.add(r)
-        for im in (n.get("status") or {}).get("images") or []:
-            for nm in im.get("names") or []:
-                self.images.add(nm)
-        for a in api.avoid_pods(n):
-            self.controllers.add(a)
-        z = api.zone_key(n)
-        if z:
-            self.zones.add(z)
+        cdesc.clear_cache()
+        d = cdesc.node_desc(n)
+        self._L.kgpu_compiler_register_node(self._cc, C.byref(d))
 
     def register_pod(self, p):
-        for k, v in api.labels_of(p).items():
-            self.pkeys.add(k, v)
-        self.ns.add(api.ns_of(p))
-        for c in api.containers(p) + api.init_containers(p):
-            for r in api.requests_of(c):
-                if api.is_scalar(r):
-                    self.scalars.add(r)
-        oh = api.spec(p).get("overhead") or {}
-        for r in oh:
-            if api.is_scalar(r):
-                self.scalars.add(r)
-        for c in api.containers(p):
-            for pt in c.get("ports") or []:
-                if int(pt.get("hostPort", 0) or 0) > 0:
-                    self.ips.add(pt.get("hostIP", "") or "0.0.0.0")
-                    self.protos.add(pt.get("protocol", "") or "TCP")
+        cdesc.clear_cache()
+        d = cdesc.pod_desc(p)
+        self._L.kgpu_compiler_register_pod(self._cc, C.byref(d))
 
     def register(self, nodes, existing=(), pods=()):
         for n in nodes:
@@ -418,68 +452,57 @@ class Compiler:
         Snapshot.List() order).  shard=(base, count) keeps only that slice of node rows.
         ordered: the node objects already in Snapshot.List() order (a cache mirror's nodeTree pass);
         uid_of(pod) -> int64: fills kgpu_snapshot.pod_uid so that deltas can address the pods."""
+        cdesc.clear_cache()
         ordered = api.snapshot_order(nodes) if ordered is None else list(ordered)
-        self.order = [api.name_of(n) for n in ordered]
-        self.node_index = {nm: i for i, nm in enumerate(self.order)}
-        N = len(ordered)
-        A = self.empty_columns(N)
-        img_lists, avoid_lists = [], []
-        name_to_nodes = {}
-        for n in ordered:
-            for im in (n.get("status") or {}).get("images") or []:
-                for nm in im.get("names") or []:
-                    name_to_nodes.setdefault(nm, set()).add(api.name_of(n))
-        for i, n in enumerate(ordered):
-            al = (n.get("status") or {}).get("allocatable") or {}
-            cpu = mem = eph = pods = 0
-            for r, q in al.items():
-                if r == "cpu":
-                    cpu += api.q_milli(q)
-                elif r == "memory":
-                    mem += api.q_value(q)
-                elif r == "pods":
-                    pods += api.q_value(q)
-                elif r == "ephemeral-storage":
-                    eph += api.q_value(q)
-                elif api.is_scalar(r):
-                    A["alloc_scalar"][self.scalars.get(r), i] += api.q_value(q)
-            A["alloc_cpu"][i], A["alloc_mem"][i], A["alloc_eph"][i], A["alloc_pods"][i] = cpu, mem, eph, pods
-            A["unschedulable"][i] = 1 if api.spec(n).get("unschedulable") else 0
-            for k, v in api.labels_of(n).items():
-                ki = self.nkeys.key(k)
-                A["label_val"][ki, i] = self.nkeys.val(ki, v)
-            for t in api.spec(n).get("taints") or []:
-                key = (t.get("key", "") or "", t.get("value", "") or "", t.get("effect", "") or "")
-                tid = self.taints.get(key)
-                w, b = divmod(tid, 64)
-                if key[2] in ("NoSchedule", "NoExecute"):
-                    A["taint_nosched"][w, i] |= np.uint64(1 << b)
-                elif key[2] == "PreferNoSchedule":
-                    A["taint_prefer"][w, i] |= np.uint64(1 << b)
-            z = api.zone_key(n)
-            A["zone_id"][i] = self.zones.get(z) if z else -1
-            ims = {}
-            for im in (n.get("status") or {}).get("images") or []:
-                for nm in im.get("names") or []:
-                    spread = float(len(name_to_nodes[nm])) / float(N)
-                    ims[self.images.get(nm)] = int(float(int(im.get("sizeBytes", 0))) * spread)
-            img_lists.append(sorted(ims.items()))
-            av = set()
-            for a in api.avoid_pods(n):
-                av.add(self.controllers.get(a))
-            avoid_lists.append(sorted(av))
-        return self.finish_snapshot(A, img_lists, avoid_lists, existing, shard, uid_of)
+        names = [api.name_of(n) for n in ordered]
+        self.order, self.node_index = names, {nm: i for i, nm in enumerate(names)}
+        nd = [cdesc.node_desc(n) for n in ordered]
+        ex = list(existing)
+        ed = [cdesc.pod_desc(p) for p in ex]
+        uids = None
+        if uid_of is not None:
+            uids = np.array([uid_of(p) if (api.spec(p).get("nodeName", "") or "") in self.node_index else 0
+                             for p in ex], np.int64)
+        out = abi.Snapshot()
+        base, cnt = (0, -1) if shard is None else shard
+        rc = self._L.kgpu_compile_snapshot(self._cc, cdesc._arr(cdesc.NodeDesc, nd), len(nd),
+                                           cdesc._arr(cdesc.PodDesc, ed), len(ed),
+                                           uids.ctypes.data if uids is not None and len(uids) else None,
+                                           base, cnt, C.byref(out))
+        if rc != 0:
+            raise CompileError(self._err())
+        return self._take_snapshot(out, uids is not None)
+
+    def snapshot_from_columns(self, A, shard=None):
+        """The snapshot of node columns a columnar generator filled against the current dictionaries
+        (A: alloc_*, unschedulable, label_val, taint_nosched / taint_prefer, zone_id, alloc_scalar in the
+        order set by set_order), no existing pods (kgpu_compile_snapshot_columns)."""
+        cols = abi.Snapshot()
+        N = len(self.order)
+        cols.n_nodes, cols.n_total_nodes = N, N
+        keep = {}
+        for f in ("alloc_cpu", "alloc_mem", "alloc_eph", "alloc_pods", "unschedulable", "zone_id", "alloc_scalar",
+                  "label_val", "taint_nosched", "taint_prefer"):
+            keep[f] = np.ascontiguousarray(A[f])
+            setattr(cols, f, abi.ptr(keep[f]))
+        cols.n_scalar = A["alloc_scalar"].shape[0]
+        cols.n_label_keys = A["label_val"].shape[0]
+        cols.taint_words = A["taint_nosched"].shape[0]
+        out = abi.Snapshot()
+        base, cnt = (0, -1) if shard is None else shard
+        rc = self._L.kgpu_compile_snapshot_columns(self._cc, C.byref(cols), None, 0, None, base, cnt, C.byref(out))
+        if rc != 0:
+            raise CompileError(self._err())
+        return self._take_snapshot(out, False)
 
     def empty_columns(self, N):
-        """The node columns of an N-node snapshot against the current dictionaries, zeroed."""
+        """The node columns of an N-node snapshot against the current dictionaries, zeroed (for
+        snapshot_from_columns)."""
         A = {}
-        for f in ("alloc_cpu", "alloc_mem", "alloc_eph", "req_cpu", "req_mem", "req_eph", "nz_cpu", "nz_mem"):
+        for f in ("alloc_cpu", "alloc_mem", "alloc_eph"):
             A[f] = np.zeros(N, np.int64)
         A["alloc_pods"] = np.zeros(N, np.int32)
-        A["num_pods"] = np.zeros(N, np.int32)
-        S = len(self.scalars)
-        A["alloc_scalar"] = np.zeros((S, N), np.int64)
-        A["req_scalar"] = np.zeros((S, N), np.int64)
+        A["alloc_scalar"] = np.zeros((len(self.scalars), N), np.int64)
         A["unschedulable"] = np.zeros(N, np.uint8)
         A["label_val"] = np.full((len(self.nkeys.keys), N), -1, np.int32)
         TW = max(1, (len(self.taints) + 63) // 64)
@@ -488,519 +511,139 @@ class Compiler:
         A["zone_id"] = np.full(N, -1, np.int32)
         return A
 
-    def finish_snapshot(self, A, img_lists, avoid_lists, existing=(), shard=None, uid_of=None):
-        """Everything after the per-node columns: existing pods, label-value metadata, the image /
-        avoid CSRs, the shard slice and the kgpu_snapshot struct.  self.order / self.node_index
-        hold Snapshot.List(); A holds empty_columns(N) filled in that order."""
-        N = len(self.order)
-        base, cnt = (0, N) if shard is None else shard
-        S = len(self.scalars)
-        K = len(self.nkeys.keys)
-        TW = max(1, (len(self.taints) + 63) // 64)
-        # existing pods -> node rows + pod table
-        A.update(self._compile_existing(existing, A, uid_of))
-        # label value metadata
-        A["key_n_values"] = np.array([len(d) for d in self.nkeys.vals], np.int32) if K else np.zeros(0, np.int32)
-        off = [0]
-        ints, oks = [], []
-        empty = []
-        for ki in range(K):
-            d = self.nkeys.vals[ki]
-            for v in d.items:
-                iv = api.parse_int64(v)
-                ints.append(0 if iv is None else iv)
-                oks.append(0 if iv is None else 1)
-            off.append(len(ints))
-            empty.append(d.get(""))
-        A["value_off"] = np.array(off, np.int32)
-        A["value_int"] = np.array(ints, np.int64)
-        A["value_int_ok"] = np.array(oks, np.uint8)
-        A["key_empty_value"] = np.array(empty, np.int32)
-        A["key_unique"] = self.key_unique(A["label_val"])
-        # images / avoid CSR
-        A["image_off"], A["image_id"], A["image_score"] = self._csr(img_lists, True)
-        A["avoid_off"], A["avoid_id"], _ = self._csr([[(a, 0) for a in lst] for lst in avoid_lists], False)
-        # shard slice
-        if shard is not None:
-            A = self._slice(A, base, cnt)
+    def _take_snapshot(self, s, with_uids):
+        """Numpy copies of the compiler's kgpu_snapshot arrays and an abi.Snapshot over them."""
+        n, S, K, TW = s.n_nodes, s.n_scalar, s.n_label_keys, s.taint_words
+        A = {}
+        for f, dt in _SNAP_1D:
+            A[f] = _copy(getattr(s, f), dt, n)
+        A["alloc_scalar"] = _copy(s.alloc_scalar, "<i8", S * n, (S, n))
+        A["req_scalar"] = _copy(s.req_scalar, "<i8", S * n, (S, n))
+        A["label_val"] = _copy(s.label_val, "<i4", K * n, (K, n))
+        A["key_n_values"] = _copy(s.key_n_values, "<i4", K)
+        A["value_off"] = _copy(s.value_off, "<i4", K + 1)
+        nv = int(A["value_off"][-1])
+        A["value_int"] = _copy(s.value_int, "<i8", nv)
+        A["value_int_ok"] = _copy(s.value_int_ok, "u1", nv)
+        A["key_empty_value"] = _copy(s.key_empty_value, "<i4", K)
+        A["key_unique"] = _copy(s.key_unique, "u1", K)
+        A["taint_nosched"] = _copy(s.taint_nosched, "<u8", TW * n, (TW, n))
+        A["taint_prefer"] = _copy(s.taint_prefer, "<u8", TW * n, (TW, n))
+        A["port_slots"] = s.port_slots
+        A["ports"] = _copy(s.ports, abi.PORT, s.port_slots * n, (s.port_slots, n))
+        A["image_off"] = _copy(s.image_off, "<i4", n + 1)
+        A["image_id"] = _copy(s.image_id, "<i4", int(A["image_off"][-1]))
+        A["image_score"] = _copy(s.image_score, "<i8", int(A["image_off"][-1]))
+        A["avoid_off"] = _copy(s.avoid_off, "<i4", n + 1)
+        A["avoid_id"] = _copy(s.avoid_id, "<i4", int(A["avoid_off"][-1]))
+        P, PK = s.n_pods, s.n_pod_label_keys
+        A["pod_node"] = _copy(s.pod_node, "<i4", P)
+        A["pod_ns"] = _copy(s.pod_ns, "<i4", P)
+        A["pod_flags"] = _copy(s.pod_flags, "<u4", P)
+        A["pod_label_val"] = _copy(s.pod_label_val, "<i4", PK * P, (PK, P))
+        A["terms"] = _copy(s.terms, abi.TERM, s.n_terms)
+        A["pod_uid"] = _copy(s.pod_uid, "<i8", P) if with_uids else None
         snap = abi.Snapshot()
-        snap.n_nodes, snap.node_base, snap.n_total_nodes = cnt, base, N
-        for f in ("alloc_cpu", "alloc_mem", "alloc_eph", "alloc_pods", "req_cpu", "req_mem", "req_eph", "nz_cpu",
-                  "nz_mem", "num_pods", "alloc_scalar", "req_scalar", "unschedulable", "label_val", "key_n_values",
-                  "value_off", "value_int", "value_int_ok", "key_empty_value", "taint_nosched", "taint_prefer",
-                  "port_count", "ports", "image_off", "image_id", "image_score", "avoid_off", "avoid_id",
-                  "zone_id", "pod_node", "pod_ns", "pod_flags", "pod_label_val", "terms", "pod_uid", "key_unique"):
-            if A.get(f) is None:
-                continue
-            A[f] = np.ascontiguousarray(A[f])
-            setattr(snap, f, abi.ptr(A[f]))
-        self.dims = {"S": S, "K": K, "TW": TW}  # device column counts fixed by this upload
-        snap.n_scalar = S
-        snap.n_label_keys = K
-        snap.taint_words = TW
-        snap.port_slots = A["port_slots"]
-        snap.n_zones = len(self.zones)
-        snap.n_pods = len(A["pod_node"])
-        snap.n_pod_label_keys = A["pod_label_val"].shape[0]  # keys registered later have no snapshot pod
-        snap.n_terms = len(A["terms"])
-        snap.pools, A["_pools_np"] = A["_pools"].finalize()
+        for f in ("n_nodes", "node_base", "n_total_nodes", "n_scalar", "n_label_keys", "taint_words", "port_slots",
+                  "n_zones", "n_pods", "n_pod_label_keys", "n_terms"):
+            setattr(snap, f, getattr(s, f))
+        for f, a in A.items():
+            if isinstance(a, np.ndarray):
+                setattr(snap, f, abi.ptr(a))
+        A["_pools_np"] = pools_numpy(s.pools)
+        snap.pools = pools_struct(A["_pools_np"])
         A["_snap"] = snap
         return snap, A, self.order
 
-    @staticmethod
-    def key_unique(label_val):
-        """kgpu_snapshot.key_unique over the WHOLE list (before any shard slice): per node label key,
-        1 when no value labels two nodes -- the engine's hostname-like keys, whose counts a sharded
-        topology run reads from the node's own column."""
-        K = label_val.shape[0]
-        out = np.zeros(K, np.uint8)
-        for k in range(K):
-            v = label_val[k][label_val[k] >= 0]
-            out[k] = 1 if len(np.unique(v)) == len(v) else 0
-        return out
-
-    @staticmethod
-    def _csr(lists, with_val):
-        off = np.zeros(len(lists) + 1, np.int32)
-        ids, vals = [], []
-        for i, lst in enumerate(lists):
-            off[i + 1] = off[i] + len(lst)
-            for a, v in lst:
-                ids.append(a)
-                vals.append(v)
-        return off, np.array(ids, np.int32), np.array(vals, np.int64)
-
-    @staticmethod
-    def _slice(A, base, cnt):
-        out = dict(A)
-        for f in ("alloc_cpu", "alloc_mem", "alloc_eph", "alloc_pods", "req_cpu", "req_mem", "req_eph", "nz_cpu",
-                  "nz_mem", "num_pods", "unschedulable", "zone_id", "port_count"):
-            out[f] = A[f][base:base + cnt]
-        for f in ("alloc_scalar", "req_scalar", "label_val", "taint_nosched", "taint_prefer", "ports"):
-            out[f] = A[f][:, base:base + cnt]
-        for fo, fi, fv in (("image_off", "image_id", "image_score"), ("avoid_off", "avoid_id", None)):
-            off = A[fo]
-            lo, hi = off[base], off[base + cnt]
-            out[fo] = off[base:base + cnt + 1] - lo
-            out[fi] = A[fi][lo:hi]
-            if fv:
-                out[fv] = A[fv][lo:hi]
-        return out
-
-    def _compile_existing(self, existing, A, uid_of=None):
-        N = len(self.order)
-        pools = Pools()
-        pod_node, pod_ns, pod_flags, pod_uid = [], [], [], []
-        PK = len(self.pkeys.keys)
-        plab = []
-        terms = []
-        used_ports = [[] for _ in range(N)]
-        for p in existing:
-            nn = api.spec(p).get("nodeName", "") or ""
-            ni = self.node_index.get(nn)
-            if ni is None:
-                continue  # NewSnapshot keeps such pods on node-less NodeInfos: never scheduled onto
-            res = api.PodResources(p)
-            A["req_cpu"][ni] += res.cpu
-            A["req_mem"][ni] += res.mem
-            A["req_eph"][ni] += res.eph
-            for r, v in res.scalars.items():
-                A["req_scalar"][self.scalars.get(r), ni] += v
-            A["nz_cpu"][ni] += res.nz_cpu
-            A["nz_mem"][ni] += res.nz_mem
-            A["num_pods"][ni] += 1
-            for c in api.containers(p):
-                for pt in c.get("ports") or []:
-                    port = int(pt.get("hostPort", 0) or 0)
-                    if port > 0:
-                        used_ports[ni].append((self.ips.get(pt.get("hostIP", "") or "0.0.0.0"),
-                                               self.protos.get(pt.get("protocol", "") or "TCP"), port))
-            slot = len(pod_node)
-            pod_node.append(ni)
-            if uid_of is not None:
-                pod_uid.append(uid_of(p))
-            pod_ns.append(self.ns.get(api.ns_of(p)))
-            fl = abi.PF_ACTIVE
-            if api.meta(p).get("deletionTimestamp") is not None:
-                fl |= abi.PF_TERMINATING
-            a = api.spec(p).get("affinity")
-            if a is not None and (a.get("podAffinity") is not None or a.get("podAntiAffinity") is not None):
-                fl |= abi.PF_WITH_AFFINITY
-            pod_flags.append(fl)
-            row = [-1] * PK
-            for k, v in api.labels_of(p).items():
-                ki = self.pkeys.key(k)
-                row[ki] = self.pkeys.val(ki, v)
-            plab.append(row)
-            for kind, t in self.pod_terms(p, pools):
-                terms.append((slot, kind, t))
-        P = len(pod_node)
-        slots = max([len(u) for u in used_ports] + [1])
-        port_count = np.array([len(u) for u in used_ports], np.int32)
-        ports = np.zeros((slots, N), abi.PORT)
-        for i, u in enumerate(used_ports):
-            for s, (ip, pr, port) in enumerate(sorted(set(u))):
-                ports[s, i] = (ip, pr, port, 0)
-            port_count[i] = len(set(u))
-        out = {"pod_node": np.array(pod_node, np.int32), "pod_ns": np.array(pod_ns, np.int32),
-               "pod_flags": np.array(pod_flags, np.uint32),
-               "pod_label_val": (np.array(plab, np.int32).T.copy() if P and PK else np.zeros((PK, P), np.int32)),
-               "terms": np.array(terms, dtype=abi.TERM) if terms else np.zeros(0, abi.TERM),
-               "port_count": port_count, "ports": ports, "port_slots": slots, "_pools": pools,
-               "pod_uid": np.array(pod_uid, np.int64) if uid_of is not None else None}
-        return out
-
     # -------------------------------------------------- node rows for deltas (kgpu_node_row)
     def node_row(self, n, pools):
-        """kgpu_node_row of a v1.Node against the dictionaries of the last upload.  Raises
-        NeedsUpload when the node brings a label key, taint word or scalar resource the device
-        columns have no room for; new values of known keys grow the dictionaries (key_meta)."""
-        dims = self.dims
+        """kgpu_node_row of a v1.Node against the dictionaries of the last upload.  Raises NeedsUpload when
+        the node brings a label key, taint word or scalar resource the device columns have no room for;
+        new values of known keys grow the dictionaries (key_meta)."""
+        cdesc.clear_cache()
         r = np.zeros((), abi.NODE_ROW)
-        al = (n.get("status") or {}).get("allocatable") or {}
-        cpu = mem = eph = pods = 0
-        sc = [0] * dims["S"]
-        for res, q in al.items():
-            if res == "cpu":
-                cpu += api.q_milli(q)
-            elif res == "memory":
-                mem += api.q_value(q)
-            elif res == "pods":
-                pods += api.q_value(q)
-            elif res == "ephemeral-storage":
-                eph += api.q_value(q)
-            elif api.is_scalar(res):
-                col = self.scalars.add(res)
-                if col >= dims["S"]:
-                    raise NeedsUpload("new scalar resource %r" % res)
-                sc[col] += api.q_value(q)
-        r["alloc_cpu"], r["alloc_mem"], r["alloc_eph"], r["alloc_pods"] = cpu, mem, eph, pods
-        r["unschedulable"] = 1 if api.spec(n).get("unschedulable") else 0
-        z = api.zone_key(n)
-        r["zone_id"] = self.zones.add(z) if z else -1
-        pairs = []
-        for k, v in sorted(api.labels_of(n).items()):
-            ki = self.nkeys.key(k)
-            if ki < 0 or ki >= dims["K"]:
-                raise NeedsUpload("new node label key %r" % k)
-            pairs += [ki, self.nkeys.add(k, v)[1]]
-        r["labels"] = pools.ints_range(pairs)
-        TW = dims["TW"]
-        words = [0] * (2 * TW)
-        for t in api.spec(n).get("taints") or []:
-            key = (t.get("key", "") or "", t.get("value", "") or "", t.get("effect", "") or "")
-            tid = self.taints.add(key)
-            w, b = divmod(tid, 64)
-            if w >= TW:
-                raise NeedsUpload("taint dictionary outgrew %d words" % TW)
-            if key[2] in ("NoSchedule", "NoExecute"):
-                words[w] |= 1 << b
-            elif key[2] == "PreferNoSchedule":
-                words[TW + w] |= 1 << b
-        r["taints"] = pools.words_range(words) if any(words) else (0, 0)
-        r["alloc_scalar"] = pools.words_range([v & 0xFFFFFFFFFFFFFFFF for v in sc]) if any(sc) else (0, 0)
-        for im in (n.get("status") or {}).get("images") or []:
-            for nm in im.get("names") or []:
-                self.images.add(nm)
-        for a in api.avoid_pods(n):
-            self.controllers.add(a)
+        d = cdesc.node_desc(n)
+        rc = self._L.kgpu_compile_node_row(self._cc, pools.h, C.byref(d), r.ctypes.data)
+        if rc == abi.E_CAPACITY:
+            raise NeedsUpload(self._err())
+        if rc != 0:
+            raise CompileError(self._err())
         return r
 
     def key_meta(self):
         """key_n_values / value_off / value_int / value_int_ok / key_empty_value of the node keys."""
-        K = self.dims["K"]
-        off, ints, oks, empty = [0], [], [], []
-        for ki in range(K):
-            d = self.nkeys.vals[ki]
-            for v in d.items:
-                iv = api.parse_int64(v)
-                ints.append(0 if iv is None else iv)
-                oks.append(0 if iv is None else 1)
-            off.append(len(ints))
-            empty.append(d.get(""))
-        return {"key_n_values": np.array([len(self.nkeys.vals[k]) for k in range(K)], np.int32),
-                "value_off": np.array(off, np.int32), "value_int": np.array(ints, np.int64),
-                "value_int_ok": np.array(oks, np.uint8), "key_empty_value": np.array(empty, np.int32)}
+        m = cdesc.KeyMeta()
+        rc = self._L.kgpu_compiler_key_meta(self._cc, C.byref(m))
+        if rc != 0:
+            raise CompileError(self._err())
+        K = m.n_keys
+        return {"key_n_values": _copy(m.key_n_values, "<i4", K), "value_off": _copy(m.value_off, "<i4", K + 1),
+                "value_int": _copy(m.value_int, "<i8", m.n_values),
+                "value_int_ok": _copy(m.value_int_ok, "u1", m.n_values),
+                "key_empty_value": _copy(m.key_empty_value, "<i4", K)}
 
     def node_lists(self, ordered, all_nodes=None):
-        """ImageLocality scaledImageScore CSR (image_locality.go:100-113: NumNodes of the image over
-        the cache's nodes, spread over len(NodeInfos().List())) and the NodePreferAvoidPods CSR, in
-        list order."""
-        N = len(ordered)
-        name_to_nodes = {}
-        for n in (ordered if all_nodes is None else all_nodes):
-            for im in (n.get("status") or {}).get("images") or []:
-                for nm in im.get("names") or []:
-                    name_to_nodes.setdefault(nm, set()).add(api.name_of(n))
-        img_lists, avoid_lists = [], []
-        for n in ordered:
-            ims = {}
-            for im in (n.get("status") or {}).get("images") or []:
-                for nm in im.get("names") or []:
-                    spread = float(len(name_to_nodes[nm])) / float(N)
-                    ims[self.images.add(nm)] = int(float(int(im.get("sizeBytes", 0))) * spread)
-            img_lists.append(sorted(ims.items()))
-            avoid_lists.append(sorted({self.controllers.add(a) for a in api.avoid_pods(n)}))
-        out = {}
-        out["image_off"], out["image_id"], out["image_score"] = self._csr(img_lists, True)
-        out["avoid_off"], out["avoid_id"], _ = self._csr([[(a, 0) for a in lst] for lst in avoid_lists], False)
-        return out
+        """ImageLocality scaledImageScore CSR (image_locality.go:100-113: NumNodes of the image over the
+        cache's nodes, spread over len(NodeInfos().List())) and the NodePreferAvoidPods CSR, in list
+        order."""
+        cdesc.clear_cache()
+        ordered = list(ordered)
+        al = ordered if all_nodes is None else list(all_nodes)
+        od = [cdesc.node_desc(n) for n in ordered]
+        ad = od if all_nodes is None else [cdesc.node_desc(n) for n in al]
+        out = cdesc.NodeLists()
+        rc = self._L.kgpu_compile_node_lists(self._cc, cdesc._arr(cdesc.NodeDesc, od), len(od),
+                                             cdesc._arr(cdesc.NodeDesc, ad), len(ad), C.byref(out))
+        if rc != 0:
+            raise CompileError(self._err())
+        n = out.n_nodes
+        return {"image_off": _copy(out.image_off, "<i4", n + 1), "image_id": _copy(out.image_id, "<i4", out.n_images),
+                "image_score": _copy(out.image_score, "<i8", out.n_images),
+                "avoid_off": _copy(out.avoid_off, "<i4", n + 1), "avoid_id": _copy(out.avoid_id, "<i4", out.n_avoid)}
 
-    # -------------------------------------------------- pod terms (framework/v1alpha1/types.go:92-160)
-    def _pod_term(self, pod, term, pools, weight=0):
-        ns = term.get("namespaces") or []
-        names = ns if ns else [api.ns_of(pod)]
-        sel = compile_label_selector(self.pkeys, pools, term.get("labelSelector"))
-        nsr = pools.ints_range([self.ns.add(x) for x in sorted(set(names))])
-        tk = term.get("topologyKey", "") or ""
-        return (weight, self.nkeys.key(tk), nsr, sel)
+    # -------------------------------------------------- pod queries
+    def pod_desc(self, pod):
+        """kgpu_pod_desc of a pod, with its DefaultSelector from this compiler's cluster listers."""
+        return cdesc.pod_desc(pod, default_selector(pod, self.cluster))
 
-    def _terms(self, pod, v1terms, pools, weighted):
-        """getAffinityTerms / getWeightedAffinityTerms: any selector error drops the whole list."""
-        if not v1terms:
-            return []
-        out = []
-        save = (len(pools.reqs), len(pools.ints))
-        try:
-            for t in v1terms:
-                if weighted:
-                    out.append(self._pod_term(pod, t.get("podAffinityTerm") or {}, pools, int(t.get("weight", 0))))
-                else:
-                    out.append(self._pod_term(pod, t, pools))
-        except CompileError:
-            pools.truncate(pools.reqs, save[0])
-            pools.truncate(pools.ints, save[1])
-            return []
-        return out
+    def compile_pod(self, pod, pools):
+        cdesc.clear_cache()
+        q = np.zeros((), abi.QUERY)
+        d = self.pod_desc(pod)
+        rc = self._L.kgpu_compile_pod(self._cc, pools.h, C.byref(d), q.ctypes.data)
+        if rc != 0:
+            raise CompileError(self._err())
+        return q
 
-    def pod_terms(self, pod, pools):
-        a = api.spec(pod).get("affinity")
-        out = []
-        if a is None:
-            return out
-        pa, paa = a.get("podAffinity"), a.get("podAntiAffinity")
-        if pa is not None:
-            for t in self._terms(pod, pa.get("requiredDuringSchedulingIgnoredDuringExecution"), pools, False):
-                out.append((abi.TERM_REQ_AFF, t))
-        if paa is not None:
-            for t in self._terms(pod, paa.get("requiredDuringSchedulingIgnoredDuringExecution"), pools, False):
-                out.append((abi.TERM_REQ_ANTI, t))
-        if pa is not None:
-            for t in self._terms(pod, pa.get("preferredDuringSchedulingIgnoredDuringExecution"), pools, True):
-                out.append((abi.TERM_PREF_AFF, t))
-        if paa is not None:
-            for t in self._terms(pod, paa.get("preferredDuringSchedulingIgnoredDuringExecution"), pools, True):
-                out.append((abi.TERM_PREF_ANTI, t))
-        return out
-
-    # -------------------------------------------------- pod query
-    def _scalar_requests(self, res, pod):
-        """[(resource name, kgpu_scalar_req)] of a pod in query order: its scalar requests (Fit checks
-        them unless ignored, fit.go:247-264), then the scorers' scalar resources it does not request."""
-        prof = self.profile
-        out = []
-        seen = set()
-        for r, v in res.scalars.items():
-            check = 0 if (api.is_extended(r) and r in prof.ignored_resources) else 1
-            out.append((r, (self.scalars.get(r), check, v, api.PodResources._score(res, r, pod))))
-            seen.add(r)
-        for r, _ in list(prof.least_resources) + list(prof.most_resources):
-            if r not in ("cpu", "memory", "ephemeral-storage") and r not in seen and api.is_scalar(r):
-                out.append((r, (self.scalars.get(r), 0, 0, api.PodResources._score(res, r, pod))))
-                seen.add(r)
-        return out
+    def compile_pods(self, pods, pools):
+        """kgpu_compile_pods over `pods` in one call: (queries, {index: error message})."""
+        cdesc.clear_cache()
+        pods = list(pods)
+        q = np.zeros(len(pods), abi.QUERY)
+        if not pods:
+            return q, {}
+        descs = cdesc._arr(cdesc.PodDesc, [self.pod_desc(p) for p in pods])
+        status = np.zeros(len(pods), np.int32)
+        rc = self._L.kgpu_compile_pods(self._cc, pools.h, descs, len(pods), q.ctypes.data, status.ctypes.data)
+        if rc < 0:
+            raise CompileError(self._err())
+        errors = {}
+        if rc:
+            # the messages: compile the failed pods again one at a time (the batch keeps the last only)
+            for i in np.nonzero(status)[0]:
+                try:
+                    self.compile_pod(pods[int(i)], pools)
+                except CompileError as e:
+                    errors[int(i)] = str(e)
+        return q, errors
 
     def scalar_names(self, pod):
         """The resource name of each scalar request compile_pod writes for `pod`, in query order (what
         kgpu_filter_reasons quotes in "Insufficient <name>")."""
-        return [r for r, _ in self._scalar_requests(api.PodResources(pod), pod)]
-
-    def compile_pod(self, pod, pools):
-        q = np.zeros((), abi.QUERY)
-        prof = self.profile
-        flags = 0
-        res = api.PodResources(pod)
-        q["ns"] = self.ns.add(api.ns_of(pod))
-        q["req"] = (res.cpu, res.mem, res.eph)
-        q["nz"] = (res.nz_cpu, res.nz_mem)
-        q["score_req"] = (res.score["cpu"], res.score["memory"], res.score["ephemeral-storage"])
-        if res.fit_all_zero:
-            flags |= abi.Q_FIT_ALL_ZERO
-        sc = [rec for _, rec in self._scalar_requests(res, pod)]
-        q["scalars"] = pools._rng(pools.scalars, sc)
-        nn = api.spec(pod).get("nodeName", "") or ""
-        q["node_name"] = -1 if nn == "" else self.node_index.get(nn, -2)
-        q["n_containers"] = len(api.containers(pod))
-        want = []
-        for c in api.containers(pod):
-            for pt in c.get("ports") or []:
-                port = int(pt.get("hostPort", 0) or 0)
-                if port > 0:
-                    want.append((self.ips.add(pt.get("hostIP", "") or "0.0.0.0"),
-                                 self.protos.add(pt.get("protocol", "") or "TCP"), port, 0))
-        q["ports"] = pools._rng(pools.ports, want)
-        tols = api.spec(pod).get("tolerations") or []
-        TW = max(1, (len(self.taints) + 63) // 64)
-        m_ns = [0] * TW
-        m_pr = [0] * TW
-        prefer_tols = [t for t in tols if not t.get("effect") or t.get("effect") == "PreferNoSchedule"]
-        for tid, (k, v, e) in enumerate(self.taints.items):
-            w, b = divmod(tid, 64)
-            if e in ("NoSchedule", "NoExecute") and any(_tolerates(t, k, v, e) for t in tols):
-                m_ns[w] |= 1 << b
-            if e == "PreferNoSchedule" and any(_tolerates(t, k, v, e) for t in prefer_tols):
-                m_pr[w] |= 1 << b
-        q["tol_nosched"] = pools.words_range(m_ns)
-        q["tol_prefer"] = pools.words_range(m_pr)
-        if any(_tolerates(t, "node.kubernetes.io/unschedulable", "", "NoSchedule") for t in tols):
-            flags |= abi.Q_TOLERATES_UNSCHED
-        # nodeSelector map (labels.SelectorFromSet: no validation, helper/node_affinity.go:30-36)
-        nsel = api.spec(pod).get("nodeSelector") or {}
-        q["node_selector"] = compile_node_reqs(self.nkeys, pools, [{"key": k, "operator": "In", "values": [v]}
-                                                                   for k, v in sorted(nsel.items())],
-                                               validate=False)
-        aff = api.spec(pod).get("affinity")
-        na = aff.get("nodeAffinity") if aff is not None else None
-        if na is not None and na.get("requiredDuringSchedulingIgnoredDuringExecution") is not None:
-            flags |= abi.Q_REQ_NODE_AFFINITY
-            terms = (na["requiredDuringSchedulingIgnoredDuringExecution"].get("nodeSelectorTerms")) or []
-            recs = [self._node_term(t, pools) for t in terms]
-            q["req_terms"] = pools._rng(pools.node_terms, recs)
-        prefs = []
-        if na is not None and na.get("preferredDuringSchedulingIgnoredDuringExecution") is not None:
-            for t in na["preferredDuringSchedulingIgnoredDuringExecution"]:
-                w = int(t.get("weight", 0))
-                if w == 0:
-                    continue
-                me = ((t.get("preference") or {}).get("matchExpressions")) or []
-                if not me:
-                    prefs.append((w, 0, (abi.SEL_NOTHING, 0, (0, 0))))
-                    continue
-                try:
-                    r = compile_node_reqs(self.nkeys, pools, me)
-                except CompileError:
-                    flags |= abi.Q_SCORE_ERROR
-                    continue
-                prefs.append((w, 0, (abi.SEL_AND, 0, r)))
-        q["pref_terms"] = pools._rng(pools.pref_terms, prefs)
-        imgs = [self.images.get(api.normalized_image_name(c.get("image", "") or "")) for c in api.containers(pod)]
-        q["images"] = pools.ints_range(imgs)
-        if all(i < 0 for i in imgs):
-            flags |= abi.Q_NO_KNOWN_IMAGE  # image_locality.go:53-79: sumScores 0 -> score 0
-        ref = api.controller_ref(pod)
-        q["avoid_id"] = -1
-        if ref is not None and ref.get("kind") in ("ReplicationController", "ReplicaSet"):
-            q["avoid_id"] = self.controllers.get((ref.get("kind"), ref.get("uid")))
-        # PodTopologySpread (common.go:44-99)
-        tsc = api.spec(pod).get("topologySpreadConstraints") or []
-        if tsc:
-            flags |= abi.Q_HAS_TSC
-        q["pts_hard"] = self._spreads(pod, tsc, "DoNotSchedule", pools)
-        q["pts_soft"] = self._spreads(pod, tsc, "ScheduleAnyway", pools)
-        # DefaultPodTopologySpread selector (default_pod_topology_spread.go:191-205)
-        ds = default_selector(pod, self.cluster)
-        q["dpts"] = (abi.SEL_AND, 0, (0, 0)) if ds is None else compile_label_selector(self.pkeys, pools, ds)
-        if ds is None:
-            q["dpts"]["kind"] = 2  # empty selector: countMatchingPods returns 0 (Empty())
-        # InterPodAffinity (types.go:92-160)
-        if aff is not None:
-            if aff.get("podAffinity") is not None:
-                flags |= abi.Q_HAS_POD_AFFINITY
-            if aff.get("podAntiAffinity") is not None:
-                flags |= abi.Q_HAS_POD_ANTI
-        byk = {abi.TERM_REQ_AFF: [], abi.TERM_REQ_ANTI: [], abi.TERM_PREF_AFF: [], abi.TERM_PREF_ANTI: []}
-        for kind, t in self.pod_terms(pod, pools):
-            byk[kind].append(t)
-        q["ipa_req_aff"] = pools._rng(pools.pod_terms, byk[abi.TERM_REQ_AFF])
-        q["ipa_req_anti"] = pools._rng(pools.pod_terms, byk[abi.TERM_REQ_ANTI])
-        q["ipa_pref_aff"] = pools._rng(pools.pod_terms, byk[abi.TERM_PREF_AFF])
-        q["ipa_pref_anti"] = pools._rng(pools.pod_terms, byk[abi.TERM_PREF_ANTI])
-        if byk[abi.TERM_REQ_AFF] and self._self_match_all(pod):
-            flags |= abi.Q_SELF_MATCH_ALL_AFF
-        pairs = []
-        for k, v in sorted(api.labels_of(pod).items()):
-            ki, vi = self.pkeys.add(k, v)
-            pairs += [ki, vi]
-        q["labels"] = pools.ints_range(pairs)
-        if api.meta(pod).get("deletionTimestamp") is not None:
-            flags |= abi.Q_TERMINATING
-        q["flags"] = flags
-        q["limits"] = api.pod_limits(pod)
-        pr = api.spec(pod).get("priority")
-        q["priority"] = 0 if pr is None else int(pr)  # podutil.GetPodPriority
-        q["uid"] = 1 + self.uids.add(api.meta(pod).get("uid", "") or "%s/%s" % (api.ns_of(pod), api.name_of(pod)))
-        return q
-
-    def _self_match_all(self, pod):
-        a = api.spec(pod).get("affinity") or {}
-        terms = ((a.get("podAffinity") or {}).get("requiredDuringSchedulingIgnoredDuringExecution")) or []
-        pl = api.labels_of(pod)
-        for t in terms:
-            ns = t.get("namespaces") or [api.ns_of(pod)]
-            if api.ns_of(pod) not in ns or not label_selector_matches(t.get("labelSelector"), pl):
-                return False
-        return True
-
-    def _node_term(self, t, pools):
-        """One NodeSelectorTerm (helpers.go:317-346) -> kgpu_node_term tuple."""
-        me = t.get("matchExpressions") or []
-        mf = t.get("matchFields") or []
-        never = (0, 0), -1, -1, 1, 0
-        if not me and not mf:
-            return never
-        reqs = (0, 0)
-        if me:
-            try:
-                reqs = compile_node_reqs(self.nkeys, pools, me)
-            except CompileError:
-                return never
-        fop, fnode = -1, -1
-        if mf:
-            ins, notins = set(), set()
-            for e in mf:
-                op, vals = e.get("operator"), e.get("values") or []
-                if op not in ("In", "NotIn") or len(vals) != 1:
-                    return never
-                key = e.get("key", "")
-                if key != "metadata.name":
-                    got = ""  # fields.Set{"metadata.name": ...}.Get(other) == ""
-                    if (op == "In") != (got == vals[0]):
-                        return never
-                    continue
-                (ins if op == "In" else notins).add(vals[0])
-            if len(ins) > 1 or (ins & notins):
-                return never
-            if ins:
-                fop, fnode = abi.OP_IN, self.node_index.get(next(iter(ins)), -1)
-            elif notins:
-                idx = [self.node_index[x] for x in notins if x in self.node_index]
-                if len(idx) > 1:
-                    raise CompileError("more than one metadata.name NotIn requirement in a term")
-                if idx:
-                    fop, fnode = abi.OP_NOTIN, idx[0]
-            if me == [] and fop == -1:
-                fop, fnode = abi.OP_NOTIN, -1  # fields only, all satisfied: matches every node
-        return reqs, fop, fnode, 0, 0
-
-    def _spreads(self, pod, tsc, action, pools):
-        pl = api.labels_of(pod)
-        cons = []
-        if tsc:
-            for c in tsc:
-                if c.get("whenUnsatisfiable") == action:
-                    cons.append((int(c.get("maxSkew", 0)), c.get("topologyKey", ""), c.get("labelSelector")))
-        else:
-            dflt = [c for c in self.profile.pts_default_constraints if c.get("whenUnsatisfiable") == action]
-            if dflt:
-                ds = default_selector(pod, self.cluster)
-                if ds is not None:
-                    cons = [(int(c.get("maxSkew", 0)), c.get("topologyKey", ""), ds) for c in dflt]
-        recs = []
-        for ms, key, ps in cons:
-            sel = compile_label_selector(self.pkeys, pools, ps)
-            recs.append((ms, self.nkeys.key(key), 1 if key == HOSTNAME else 0,
-                         1 if label_selector_matches(ps, pl) else 0, sel))
-        return pools._rng(pools.spreads, recs)
+        pools = Pools()
+        q = self.compile_pod(pod, pools)
+        b, c = int(q["scalars"]["begin"]), int(q["scalars"]["count"])
+        return [pools.scalar_name(b + i) for i in range(c)]
 
     # -------------------------------------------------- config
     def config(self, device=0, node_capacity=0, pod_capacity=0, term_capacity=0):

@@ -4,6 +4,8 @@ that, after re-upload, schedules exactly as the C restatement does.
 
 The hook raises the abort word from workgroup 0 at a chosen pod, which is what a workgroup that
 lost co-residency does after kSpinTimeout (kgpu_kernels.hip, poll_row / tpoll_slot)."""
+import time
+
 import numpy as np
 import pytest
 
@@ -203,9 +205,13 @@ def test_missing_workgroup_one_pod_cycle():
     for i in range(len(q)):
         if i == 7:
             e.set_option(abi.OPT_HOLD_GROUP, 0)
+        t0 = time.perf_counter()
         res, _ = e.schedule_one(q[i], pc, seq=i, assume=True)
         if i == 7:
             e.set_option(abi.OPT_HOLD_GROUP, -1)
+            # the spin timeout (0.5 s) and the cooperative re-issue; the host stops waiting on the completion
+            # word as soon as it holds the abort code (it used to spin out its 2 s bound first: ADVICE r5)
+            assert time.perf_counter() - t0 < 1.5
         got.append(res)
     assert e.counters()["coop_retries"] == 1
     ref = RefEngine(fw.config, fw.snap, threads=4)
@@ -227,8 +233,10 @@ def test_abort_one_pod_cycle_recovers():
     for i in range(5):
         e.schedule_one(q[i], pc, seq=i, assume=True)
     e.set_option(abi.OPT_ABORT_AT, 0)
+    t0 = time.perf_counter()
     with pytest.raises(KgpuError) as ex:
         e.schedule_one(q[5], pc, seq=5, assume=True)
+    assert time.perf_counter() - t0 < 1.5  # no 2 s spin on a completion word that holds an abort code
     assert ex.value.code == abi.E_DEVICE and "re-upload" in str(ex.value)
     e.set_option(abi.OPT_ABORT_AT, -1)
     assert e.counters()["coop_retries"] == 0  # a run that started everywhere is not issued again
