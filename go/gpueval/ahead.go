@@ -51,6 +51,10 @@ type aheadEntry struct {
 	res  C.kgpu_result
 	slot int32 // pod-table slot of the speculative assume (-1: not placed)
 	host string
+	// the assume delta the device applied (kgpu_pod_query.req / .nz): adoption checks that the
+	// scheduler's own NodeInfo.AddPod moved the node's sums by exactly this much
+	req [3]int64
+	nz  [2]int64
 }
 
 type ahead struct {
@@ -163,8 +167,19 @@ func (g *GpuEval) adoptPrevious(list []*framework.NodeInfo) (bool, error) {
 			same = false
 		}
 	}
-	if assumed == nil || !same || m.nodes[e.host] != ni.Node() {
-		// not (only) this pod's assume: the speculative assume is undone and the node diffed
+	// the device row is the mirror's last sums plus the assume delta it applied; the NodeInfo's sums
+	// after cache.AssumePod (NodeInfo.AddPod, types.go:549-581: Requested with overhead CPU as
+	// MilliValue, NonZeroRequested with the non-zero defaults) must equal them
+	want := m.res[e.host]
+	for k := 0; k < 3; k++ {
+		want.req[k] += e.req[k]
+	}
+	for k := 0; k < 2; k++ {
+		want.nz[k] += e.nz[k]
+	}
+	if assumed == nil || !same || m.nodes[e.host] != ni.Node() || resOf(ni) != want {
+		// not (only) this pod's assume, or sums the device does not hold: the speculative assume is
+		// undone and the node diffed
 		ah.spec = append([]aheadEntry{*e}, ah.spec...)
 		g.track.mark(e.host)
 		return false, nil
@@ -178,6 +193,7 @@ func (g *GpuEval) adoptPrevious(list []*framework.NodeInfo) (bool, error) {
 	}
 	m.pods[e.host] = cur
 	m.gens[e.host] = ni.Generation
+	m.res[e.host] = want
 	m.genAt[pos] = ni.Generation
 	m.slots[e.uid] = e.slot
 	g.track.settle(e.host) // the mirror matches that NodeInfo again
@@ -231,7 +247,7 @@ func (g *GpuEval) serveAhead(pod *v1.Pod, seq int64) (C.kgpu_result, bool, error
 
 // startBatch runs after this cycle's sync: the pod and the pods the queue pops next in one
 // kgpu_schedule_batch with on-device assume.  Returns the pod's own result.
-func (g *GpuEval) startBatch(pod *v1.Pod, q C.kgpu_pod_query, p *pools, seq int64) (C.kgpu_result, bool, error) {
+func (g *GpuEval) startBatch(pod *v1.Pod, q C.kgpu_pod_query, ps *poolSet, seq int64) (C.kgpu_result, bool, error) {
 	var zero C.kgpu_result
 	ah := g.ahead
 	if g.nominated || ah.depth <= 1 {
@@ -240,14 +256,9 @@ func (g *GpuEval) startBatch(pod *v1.Pod, q C.kgpu_pod_query, p *pools, seq int6
 	pods := []*v1.Pod{pod}
 	qs := []C.kgpu_pod_query{q}
 	for _, np := range g.pendingPods(pod, ah.depth-1) {
-		nq, err := g.comp.compilePod(np, p)
+		nq, err := g.comp.compilePod(np, g.defaultSelector(np), ps)
 		if err != nil {
 			break // that pod's own cycle reports it
-		}
-		if sel := g.defaultSelector(np); sel != nil {
-			if nq.dpts, err = g.comp.labelSelector(p, sel); err != nil {
-				break
-			}
 		}
 		pods = append(pods, np)
 		qs = append(qs, nq)
@@ -258,7 +269,7 @@ func (g *GpuEval) startBatch(pod *v1.Pod, q C.kgpu_pod_query, p *pools, seq int6
 	var a arena
 	defer a.free()
 	slot := g.eng.nextSlot()
-	res, err := g.eng.scheduleBatch(qs, p.toC(&a), seq)
+	res, err := g.eng.scheduleBatch(qs, ps.toC(&a), seq)
 	if err != nil {
 		g.mir = nil
 		return zero, false, err
@@ -266,7 +277,9 @@ func (g *GpuEval) startBatch(pod *v1.Pod, q C.kgpu_pod_query, p *pools, seq int6
 	ah.spec = ah.spec[:0]
 	var first aheadEntry
 	for k := range pods {
-		e := aheadEntry{uid: pods[k].UID, seq: seq + int64(k), res: res[k], slot: -1}
+		e := aheadEntry{uid: pods[k].UID, seq: seq + int64(k), res: res[k], slot: -1,
+			req: [3]int64{int64(qs[k].req[0]), int64(qs[k].req[1]), int64(qs[k].req[2])},
+			nz:  [2]int64{int64(qs[k].nz[0]), int64(qs[k].nz[1])}}
 		if res[k].node >= 0 {
 			e.slot = slot
 			e.host = g.mir.names[res[k].node]

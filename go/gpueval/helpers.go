@@ -100,25 +100,26 @@ func toExprs(ls *metav1.LabelSelector) []metav1.LabelSelectorRequirement {
 	return out
 }
 
-// reasonQuery is the C copy of one cycle's pod query, pools and scalar request names, kept from
-// PreFilter until the next PreFilter so that Filter can have its status reasons formatted.
+// reasonQuery is the C copy of one cycle's pod query, its pool set and its scalar request names,
+// kept from PreFilter until the next PreFilter so that Filter can have its status reasons formatted.
 type reasonQuery struct {
 	a     arena
+	ps    *poolSet
 	q     *C.kgpu_pod_query
 	pools *C.kgpu_pools
 	names **C.char
 }
 
-func newReasonQuery(q C.kgpu_pod_query, p *pools, pod *v1.Pod) *reasonQuery {
-	r := &reasonQuery{}
+// newReasonQuery takes ownership of ps (the set q was compiled into).
+func newReasonQuery(q C.kgpu_pod_query, ps *poolSet) *reasonQuery {
+	r := &reasonQuery{ps: ps}
 	r.q = cQueries(&r.a, []C.kgpu_pod_query{q})
-	r.pools = p.toC(&r.a)
-	_, _, _, sc := podRequest(pod)
-	names := scalarNames(sc)
-	if len(names) > 0 {
-		arr := (*[1 << 20]*C.char)(r.a.alloc(len(names) * int(unsafe.Sizeof((*C.char)(nil)))))
-		for i, n := range names {
-			cs := C.CString(n)
+	r.pools = ps.toC(&r.a)
+	// the names of the pod's scalar requests, in query order (what "Insufficient <name>" quotes)
+	if n := int(q.scalars.count); n > 0 {
+		arr := (*[1 << 20]*C.char)(r.a.alloc(n * int(unsafe.Sizeof((*C.char)(nil)))))
+		for i := 0; i < n; i++ {
+			cs := C.CString(ps.scalarName(int32(q.scalars.begin) + int32(i)))
 			r.a.ptrs = append(r.a.ptrs, unsafe.Pointer(cs))
 			arr[i] = cs
 		}
@@ -130,6 +131,7 @@ func newReasonQuery(q C.kgpu_pod_query, p *pools, pod *v1.Pod) *reasonQuery {
 func (r *reasonQuery) free() {
 	if r != nil {
 		r.a.free()
+		r.ps.free()
 	}
 }
 
@@ -150,10 +152,7 @@ func (g *GpuEval) filterReasons(rq *reasonQuery, node int32, w uint32, n *v1.Nod
 	if n != nil && len(n.Spec.Taints) > 0 {
 		tr := (*[1 << 20]C.kgpu_taint_ref)(a.alloc(len(n.Spec.Taints) * int(unsafe.Sizeof(C.kgpu_taint_ref{}))))
 		for i, t := range n.Spec.Taints {
-			id, ok := g.comp.taints[taintKey{t.Key, t.Value, string(t.Effect)}]
-			if !ok {
-				id = -1
-			}
+			id := g.comp.taintID(t) // -1: not in the dictionary
 			k, v, e := C.CString(t.Key), C.CString(t.Value), C.CString(string(t.Effect))
 			a.ptrs = append(a.ptrs, unsafe.Pointer(k), unsafe.Pointer(v), unsafe.Pointer(e))
 			tr[i] = C.kgpu_taint_ref{key: k, value: v, effect: e, id: C.int32_t(id)}

@@ -21,8 +21,14 @@ import (
 	"unsafe"
 )
 
-// arena owns C allocations made for one call.
-type arena struct{ ptrs []unsafe.Pointer }
+// arena owns C allocations made for one call, and the C objects (pool sets) that must outlive it.
+type arena struct {
+	ptrs []unsafe.Pointer
+	fns  []func()
+}
+
+// onFree runs f when the arena is freed (after its memory is released).
+func (a *arena) onFree(f func()) { a.fns = append(a.fns, f) }
 
 func (a *arena) alloc(bytes int) unsafe.Pointer {
 	if bytes <= 0 {
@@ -38,6 +44,10 @@ func (a *arena) free() {
 		C.free(p)
 	}
 	a.ptrs = nil
+	for _, f := range a.fns {
+		f()
+	}
+	a.fns = nil
 }
 
 // cmem copies n elements of elem bytes from a Go slice of plain values (no Go pointers inside)
@@ -70,75 +80,15 @@ func cu8(a *arena, s []uint8) *C.uint8_t {
 	return (*C.uint8_t)(cmem(a, unsafe.Pointer(&s[0]), len(s), 1))
 }
 
-func cu32(a *arena, s []uint32) *C.uint32_t {
-	if len(s) == 0 {
-		return nil
-	}
-	return (*C.uint32_t)(cmem(a, unsafe.Pointer(&s[0]), len(s), 4))
-}
 
-func cu64(a *arena, s []uint64) *C.uint64_t {
-	if len(s) == 0 {
-		return nil
-	}
-	return (*C.uint64_t)(cmem(a, unsafe.Pointer(&s[0]), len(s), 8))
-}
 
-func cReqs(a *arena, s []C.kgpu_req) *C.kgpu_req {
-	if len(s) == 0 {
-		return nil
-	}
-	return (*C.kgpu_req)(cmem(a, unsafe.Pointer(&s[0]), len(s), int(unsafe.Sizeof(s[0]))))
-}
 
-func cNodeTerms(a *arena, s []C.kgpu_node_term) *C.kgpu_node_term {
-	if len(s) == 0 {
-		return nil
-	}
-	return (*C.kgpu_node_term)(cmem(a, unsafe.Pointer(&s[0]), len(s), int(unsafe.Sizeof(s[0]))))
-}
 
-func cPrefTerms(a *arena, s []C.kgpu_pref_term) *C.kgpu_pref_term {
-	if len(s) == 0 {
-		return nil
-	}
-	return (*C.kgpu_pref_term)(cmem(a, unsafe.Pointer(&s[0]), len(s), int(unsafe.Sizeof(s[0]))))
-}
 
-func cSpreads(a *arena, s []C.kgpu_spread) *C.kgpu_spread {
-	if len(s) == 0 {
-		return nil
-	}
-	return (*C.kgpu_spread)(cmem(a, unsafe.Pointer(&s[0]), len(s), int(unsafe.Sizeof(s[0]))))
-}
 
-func cPodTerms(a *arena, s []C.kgpu_pod_term) *C.kgpu_pod_term {
-	if len(s) == 0 {
-		return nil
-	}
-	return (*C.kgpu_pod_term)(cmem(a, unsafe.Pointer(&s[0]), len(s), int(unsafe.Sizeof(s[0]))))
-}
 
-func cTerms(a *arena, s []C.kgpu_term) *C.kgpu_term {
-	if len(s) == 0 {
-		return nil
-	}
-	return (*C.kgpu_term)(cmem(a, unsafe.Pointer(&s[0]), len(s), int(unsafe.Sizeof(s[0]))))
-}
 
-func cScalars(a *arena, s []C.kgpu_scalar_req) *C.kgpu_scalar_req {
-	if len(s) == 0 {
-		return nil
-	}
-	return (*C.kgpu_scalar_req)(cmem(a, unsafe.Pointer(&s[0]), len(s), int(unsafe.Sizeof(s[0]))))
-}
 
-func cPorts(a *arena, s []C.kgpu_port) *C.kgpu_port {
-	if len(s) == 0 {
-		return nil
-	}
-	return (*C.kgpu_port)(cmem(a, unsafe.Pointer(&s[0]), len(s), int(unsafe.Sizeof(s[0]))))
-}
 
 func cQueries(a *arena, s []C.kgpu_pod_query) *C.kgpu_pod_query {
 	if len(s) == 0 {

@@ -26,12 +26,10 @@ import (
 	"context"
 	"fmt"
 	"sort"
-	"strconv"
 	"sync/atomic"
 	"unsafe"
 
 	v1 "k8s.io/api/core/v1"
-	"k8s.io/apimachinery/pkg/labels"
 	"k8s.io/apimachinery/pkg/runtime"
 	"k8s.io/apimachinery/pkg/types"
 	v1helper "k8s.io/kubernetes/pkg/apis/core/v1/helper"
@@ -57,6 +55,9 @@ type profileArgs struct {
 	Mode                   string // "select" or "shadow"
 	ExactSync              bool   // compare every NodeInfo generation at every sync (track.go)
 	BatchAhead             int    // > 1: schedule the pod with the next BatchAhead-1 queued pods (ahead.go)
+	// DefaultConstraints: PodTopologySpreadArgs.DefaultConstraints (apis/config/types_pluginargs.go),
+	// applied with the pod's DefaultSelector to a pod without constraints (podtopologyspread/common.go:44-72).
+	DefaultConstraints     []v1.TopologySpreadConstraint
 	// RunAllFilters mirrors the framework's runAllFilters (framework.go:90,155-160,494), which the
 	// scheduler sets from the legacy Policy's AlwaysCheckAllPredicates (factory.go:107,278-281): every
 	// filter plugin runs on every node and Filter returns the merged status with every failing
@@ -78,18 +79,16 @@ var scoreIDs = map[string]int32{"NodeResourcesBalancedAllocation": C.KGPU_S_BALA
 	"NodeResourcesMostAllocated": C.KGPU_S_MOST_ALLOCATED, "RequestedToCapacityRatio": C.KGPU_S_REQUESTED_TO_CAPACITY_RATIO,
 	"NodeResourceLimits": C.KGPU_S_RESOURCE_LIMITS}
 
-func (p *profileArgs) scalarResources() []string {
-	var out []string
-	for _, m := range []map[string]int64{p.LeastResources, p.MostResources, p.RTCRResources} {
-		for r := range m {
-			if r != "cpu" && r != "memory" && r != "ephemeral-storage" {
-				out = append(out, r)
-			}
-		}
+func sortedNames(m map[string]int64) []string {
+	out := make([]string, 0, len(m))
+	for r := range m {
+		out = append(out, r)
 	}
 	sort.Strings(out)
 	return out
 }
+
+func sortStrings(x []string) { sort.Strings(x) }
 
 // config builds kgpu_config (kubernetes-1_amd/kgpu/compile.py Compiler.config).
 func (c *compiler) config() *C.kgpu_config {
@@ -120,7 +119,10 @@ func (c *compiler) config() *C.kgpu_config {
 		case "ephemeral-storage":
 			return 2
 		}
-		return 3 + c.scalars.add(name)
+		if col := c.scalarColumn(name); col >= 0 && v1helper.IsScalarResourceName(v1.ResourceName(name)) {
+			return 3 + col // the compiler gave every profile resource a column up front
+		}
+		return -1
 	}
 	fill := func(m map[string]int64, arr *[8]C.kgpu_resource_weight, n *C.int32_t) {
 		names := make([]string, 0, len(m))
@@ -219,43 +221,47 @@ func (g *GpuEval) syncSnapshot() error {
 	return g.upload(list, &a)
 }
 
-// upload compiles the whole Snapshot.List() into kgpu_snapshot columns.
+// upload compiles the whole Snapshot.List() into kgpu_snapshot columns (a fresh compiler: the
+// dictionaries of a new upload epoch).
 func (g *GpuEval) upload(list []*framework.NodeInfo, a *arena) error {
-	c := newCompiler(g.prof)
+	c, err := newCompiler(g.prof)
+	if err != nil {
+		return err
+	}
 	for _, ni := range list {
-		c.registerNode(ni.Node())
+		if err := c.registerNode(ni.Node()); err != nil {
+			c.close()
+			return err
+		}
 		for _, pi := range ni.Pods {
-			c.registerPod(pi.Pod)
+			if err := c.registerPod(pi.Pod); err != nil {
+				c.close()
+				return err
+			}
 		}
 	}
-	for i, ni := range list {
-		if _, ok := c.nodeIndex[ni.Node().Name]; !ok {
-			c.nodeIndex[ni.Node().Name] = int32(i)
-		}
-	}
+	c.dictAdd(C.KGPU_DICT_NAMESPACE, 0, "")
 	g.track.take() // a full upload covers every mark
-	c.dims.K = len(c.nkeys.keys.items)
-	c.dims.S = len(c.scalars.items)
-	c.dims.TW = (len(c.taintList) + 63) / 64
-	if c.dims.TW == 0 {
-		c.dims.TW = 1
-	}
 	if g.eng == nil {
 		eng, err := newEngine(c.config())
 		if err != nil {
+			c.close()
 			return err
 		}
 		if g.prof.RunAllFilters {
 			if err := eng.setOption(C.KGPU_OPT_RUN_ALL_FILTERS, 1); err != nil {
 				eng.close()
+				c.close()
 				return err
 			}
 		}
 		g.eng = eng
 	}
+	g.comp.close()
 	g.comp = c
 	m := &mirror{index: map[string]int32{}, gens: map[string]int64{}, nodes: map[string]*v1.Node{},
-		pods: map[string]map[types.UID]*v1.Pod{}, uids: map[types.UID]int64{}, slots: map[types.UID]int32{}}
+		pods: map[string]map[types.UID]*v1.Pod{}, uids: map[types.UID]int64{}, slots: map[types.UID]int32{},
+		res: map[string]nodeRes{}}
 	m.genAt = make([]int64, len(list))
 	for i, ni := range list {
 		m.genAt[i] = ni.Generation
@@ -275,162 +281,47 @@ func (g *GpuEval) upload(list []*framework.NodeInfo, a *arena) error {
 	return g.eng.uploadSnapshot(s, m.gen)
 }
 
-// snapshotSoA fills kgpu_snapshot (one pass over the list; pods of every NodeInfo).  The list
-// is uploaded once per distinct node; a list holding a NodeInfo twice is aliased by the next
-// delta's order (kgpu_delta_batch.order).
+// snapshotSoA compiles the list's nodes and their NodeInfos' pods (kgpu_compile_snapshot: the node
+// columns, NodeInfo.AddPod of every pod, the pods' label rows and affinity terms).  The list is
+// uploaded once per distinct node; a list holding a NodeInfo twice is aliased by the next delta's
+// order (kgpu_delta_batch.order).  Pod-table slots follow the pods' order here.
 func (g *GpuEval) snapshotSoA(list []*framework.NodeInfo, m *mirror, a *arena) (*C.kgpu_snapshot, error) {
 	c := g.comp
 	seen := map[string]bool{}
-	var uniq []*framework.NodeInfo
+	var nodes []*v1.Node
+	var existing []*v1.Pod
+	var hosts []string
+	var uids []int64
 	for _, ni := range list {
-		if !seen[ni.Node().Name] {
-			seen[ni.Node().Name] = true
-			uniq = append(uniq, ni)
-		}
-	}
-	N, K, S, TW := len(uniq), c.dims.K, c.dims.S, c.dims.TW
-	i64 := func() []int64 { return make([]int64, N) }
-	allocCPU, allocMem, allocEph, reqCPU, reqMem, reqEph, nzCPU, nzMem := i64(), i64(), i64(), i64(), i64(), i64(), i64(), i64()
-	allocPods, numPods, zone, portCount := make([]int32, N), make([]int32, N), make([]int32, N), make([]int32, N)
-	unsched := make([]uint8, N)
-	labelVal := make([]int32, K*N)
-	for i := range labelVal {
-		labelVal[i] = -1
-	}
-	taintNo, taintPref := make([]uint64, TW*N), make([]uint64, TW*N)
-	allocSc, reqSc := make([]int64, S*N), make([]int64, S*N)
-	var podNode, podNs []int32
-	var podFlags []uint32
-	var podUID []int64
-	p := &pools{}
-	var terms []C.kgpu_term
-	var ports [][]C.kgpu_port
-	for i, ni := range uniq {
 		n := ni.Node()
+		if seen[n.Name] {
+			continue
+		}
+		seen[n.Name] = true
 		m.names = append(m.names, n.Name)
-		m.index[n.Name] = int32(i)
+		m.index[n.Name] = int32(len(nodes))
 		m.gens[n.Name] = ni.Generation
 		m.nodes[n.Name] = n
-		r, err := c.nodeRow(n, p)
-		if err != nil {
-			return nil, err
-		}
-		allocCPU[i], allocMem[i], allocEph[i], allocPods[i] = int64(r.alloc_cpu), int64(r.alloc_mem), int64(r.alloc_eph), int32(r.alloc_pods)
-		unsched[i], zone[i] = uint8(r.unschedulable), int32(r.zone_id)
-		for j := 0; j+1 < int(r.labels.count); j += 2 {
-			k, v := p.ints[int(r.labels.begin)+j], p.ints[int(r.labels.begin)+j+1]
-			labelVal[int(k)*N+i] = v
-			m.labels.add(k, v, 1)
-		}
-		if r.taints.count > 0 {
-			for w := 0; w < TW; w++ {
-				taintNo[w*N+i] = p.words[int(r.taints.begin)+w]
-				taintPref[w*N+i] = p.words[int(r.taints.begin)+TW+w]
-			}
-		}
-		for s := 0; s < int(r.alloc_scalar.count); s++ {
-			allocSc[s*N+i] = int64(p.words[int(r.alloc_scalar.begin)+s])
-		}
-		reqCPU[i], reqMem[i], reqEph[i] = ni.Requested.MilliCPU, ni.Requested.Memory, ni.Requested.EphemeralStorage
-		nzCPU[i], nzMem[i] = ni.NonZeroRequested.MilliCPU, ni.NonZeroRequested.Memory
-		for name, v := range ni.Requested.ScalarResources {
-			if col := c.scalars.get(string(name)); col >= 0 && int(col) < S {
-				reqSc[int(col)*N+i] = v
-			}
-		}
-		numPods[i] = int32(len(ni.Pods))
-		var used []C.kgpu_port
-		for ip, pp := range ni.UsedPorts {
-			for pr := range pp {
-				proto := map[string]int32{"TCP": 0, "UDP": 1, "SCTP": 2}[pr.Protocol]
-				used = append(used, C.kgpu_port{ip: C.int32_t(c.ips.add(ip)), proto: C.int32_t(proto), port: C.int32_t(pr.Port)})
-			}
-		}
-		ports = append(ports, used)
-		portCount[i] = int32(len(used))
+		m.res[n.Name] = resOf(ni)
 		m.pods[n.Name] = map[types.UID]*v1.Pod{}
+		nodes = append(nodes, n)
 		for _, pi := range ni.Pods {
-			slot := int32(len(podNode))
 			m.pods[n.Name][pi.Pod.UID] = pi.Pod
-			m.slots[pi.Pod.UID] = slot
-			podNode = append(podNode, int32(i))
-			podNs = append(podNs, c.ns.add(pi.Pod.Namespace))
-			fl := uint32(C.KGPU_PF_ACTIVE)
-			if pi.Pod.DeletionTimestamp != nil {
-				fl |= C.KGPU_PF_TERMINATING
-			}
-			if af := pi.Pod.Spec.Affinity; af != nil && (af.PodAffinity != nil || af.PodAntiAffinity != nil) {
-				fl |= C.KGPU_PF_WITH_AFFINITY
-			}
-			podFlags = append(podFlags, fl)
-			podUID = append(podUID, m.uid(pi.Pod.UID))
-			q, err := c.compilePod(pi.Pod, p) // the pod's terms (PodInfo, types.go:92-160)
-			if err != nil {
-				return nil, err
-			}
-			for kind, r := range []C.kgpu_range{q.ipa_req_aff, q.ipa_req_anti, q.ipa_pref_aff, q.ipa_pref_anti} {
-				for t := 0; t < int(r.count); t++ {
-					terms = append(terms, C.kgpu_term{pod: C.int32_t(slot), kind: C.int32_t(kind), t: p.podTerms[int(r.begin)+t]})
-				}
-			}
+			m.slots[pi.Pod.UID] = int32(len(existing))
+			existing = append(existing, pi.Pod)
+			hosts = append(hosts, n.Name)
+			uids = append(uids, m.uid(pi.Pod.UID))
 		}
 	}
-	PK := len(c.pkeys.keys.items)
-	P := len(podNode)
-	podLab := make([]int32, PK*P)
-	for i := range podLab {
-		podLab[i] = -1
+	s, err := c.snapshot(nodes, existing, hosts, uids, a)
+	if err != nil {
+		return nil, err
 	}
-	slot := 0
-	for _, ni := range uniq {
-		for _, pi := range ni.Pods {
-			for k, v := range pi.Pod.Labels {
-				ki, vi := c.pkeys.add(k, v)
-				if int(ki) < PK {
-					podLab[int(ki)*P+slot] = vi
-				}
-			}
-			slot++
+	for _, n := range nodes {
+		for _, kv := range c.nodeLabelIDs(n) {
+			m.labels.add(kv[0], kv[1], 1)
 		}
 	}
-	PS := 1
-	for _, u := range ports {
-		if len(u) > PS {
-			PS = len(u)
-		}
-	}
-	portTab := make([]C.kgpu_port, PS*N)
-	for i, u := range ports {
-		for s, pt := range u {
-			portTab[s*N+i] = pt
-		}
-	}
-	s := (*C.kgpu_snapshot)(a.alloc(int(unsafeSizeofSnapshot)))
-	s.n_nodes, s.node_base, s.n_total_nodes = C.int32_t(N), 0, C.int32_t(N)
-	s.alloc_cpu, s.alloc_mem, s.alloc_eph = ci64(a, allocCPU), ci64(a, allocMem), ci64(a, allocEph)
-	s.alloc_pods = ci32(a, allocPods)
-	s.req_cpu, s.req_mem, s.req_eph = ci64(a, reqCPU), ci64(a, reqMem), ci64(a, reqEph)
-	s.nz_cpu, s.nz_mem = ci64(a, nzCPU), ci64(a, nzMem)
-	s.num_pods = ci32(a, numPods)
-	s.n_scalar, s.alloc_scalar, s.req_scalar = C.int32_t(S), ci64(a, allocSc), ci64(a, reqSc)
-	s.unschedulable = cu8(a, unsched)
-	s.n_label_keys, s.label_val = C.int32_t(K), ci32(a, labelVal)
-	var b C.kgpu_delta_batch
-	g.keyMeta(&b, a)
-	s.key_n_values, s.value_off, s.value_int, s.value_int_ok, s.key_empty_value =
-		b.key_n_values, b.value_off, b.value_int, b.value_int_ok, b.key_empty_value
-	s.taint_words, s.taint_nosched, s.taint_prefer = C.int32_t(TW), cu64(a, taintNo), cu64(a, taintPref)
-	s.port_slots, s.port_count, s.ports = C.int32_t(PS), ci32(a, portCount), cPorts(a, portTab)
-	g.nodeLists(uniq, &b, a)
-	s.image_off, s.image_id, s.image_score, s.avoid_off, s.avoid_id = b.image_off, b.image_id, b.image_score, b.avoid_off, b.avoid_id
-	s.zone_id, s.n_zones = ci32(a, zone), C.int32_t(len(c.zones.items))
-	s.n_pods, s.pod_node, s.pod_ns = C.int32_t(P), ci32(a, podNode), ci32(a, podNs)
-	s.pod_flags = cu32(a, podFlags)
-	s.n_pod_label_keys, s.pod_label_val = C.int32_t(PK), ci32(a, podLab)
-	s.n_terms, s.terms = C.int32_t(len(terms)), cTerms(a, terms)
-	s.pools = *p.toC(a)
-	s.pod_uid = ci64(a, podUID)
-	s.key_unique = cu8(a, m.labels.unique(K)) // the whole Snapshot.List(): the cluster-wide view
 	return s, nil
 }
 
@@ -468,18 +359,22 @@ func (g *GpuEval) PreFilter(ctx context.Context, cs *framework.CycleState, pod *
 	if err := g.syncNominated(&a); err != nil {
 		return framework.NewStatus(framework.Error, err.Error())
 	}
-	p := &pools{}
-	q, err := g.comp.compilePod(pod, p)
+	ps, err := newPoolSet()
 	if err != nil {
 		return framework.NewStatus(framework.Error, err.Error())
 	}
-	if sel := g.defaultSelector(pod); sel != nil {
-		if q.dpts, err = g.comp.labelSelector(p, sel); err != nil {
-			return framework.NewStatus(framework.Error, err.Error())
+	kept := false // ps passes to the cycle's reasonQuery
+	defer func() {
+		if !kept {
+			ps.free()
 		}
+	}()
+	q, err := g.comp.compilePod(pod, g.defaultSelector(pod), ps)
+	if err != nil {
+		return framework.NewStatus(framework.Error, err.Error())
 	}
 	if g.ahead != nil && !g.nominated {
-		if res, ok, err := g.startBatch(pod, q, p, seq); err != nil {
+		if res, ok, err := g.startBatch(pod, q, ps, seq); err != nil {
 			return framework.NewStatus(framework.Error, err.Error())
 		} else if ok && res.node >= 0 {
 			cs.Write(stateKey, &cycle{chosen: int32(res.node), index: g.mir.index})
@@ -494,7 +389,8 @@ func (g *GpuEval) PreFilter(ctx context.Context, cs *framework.CycleState, pod *
 		}
 	}
 	g.rq.free()
-	g.rq = newReasonQuery(q, p, pod)
+	g.rq = newReasonQuery(q, ps)
+	kept = true
 	res, _, err := g.eng.scheduleOne(g.rq.q, g.rq.pools, seq, false)
 	if err != nil {
 		return framework.NewStatus(framework.Error, err.Error())
@@ -621,6 +517,8 @@ func (g *GpuEval) Close() {
 		g.eng = nil
 	}
 	g.mir = nil
+	g.comp.close()
+	g.comp = nil
 }
 
 // New is the framework.PluginFactory (registry.go:28).
@@ -642,32 +540,3 @@ func New(obj runtime.Object, h framework.FrameworkHandle) (framework.Plugin, err
 func (g *GpuEval) defaultSelector(pod *v1.Pod) *metav1LabelSelector {
 	return defaultSelectorFromListers(g.h, pod)
 }
-
-// ---------------------------------------------------------------- small helpers
-func labelsSet(m map[string]string) labels.Set { return labels.Set(m) }
-
-func parseInt64(s string) (int64, uint8) {
-	x, err := strconv.ParseInt(s, 10, 64)
-	if err != nil {
-		return 0, 0
-	}
-	return x, 1
-}
-
-func sortCSR(ids []int32, vals []int64) {
-	sort.Sort(csrSorter{ids, vals})
-}
-
-type csrSorter struct {
-	ids  []int32
-	vals []int64
-}
-
-func (s csrSorter) Len() int           { return len(s.ids) }
-func (s csrSorter) Less(i, j int) bool { return s.ids[i] < s.ids[j] }
-func (s csrSorter) Swap(i, j int) {
-	s.ids[i], s.ids[j] = s.ids[j], s.ids[i]
-	s.vals[i], s.vals[j] = s.vals[j], s.vals[i]
-}
-
-var _ = v1helper.IsScalarResourceName

@@ -105,7 +105,11 @@ func (g *GpuEval) syncNominated(a *arena) error {
 	sortInt32s(idx) // Snapshot.List() order, as a walk over the list would send them
 	var noms []C.kgpu_nominated
 	var recs []C.kgpu_pod_query
-	p := &pools{}
+	ps, err := newPoolSet()
+	if err != nil {
+		return err
+	}
+	a.onFree(ps.free)
 	g.nomLast = g.nomLast[:0]
 	for _, i := range idx {
 		name := g.mir.names[i]
@@ -114,7 +118,7 @@ func (g *GpuEval) syncNominated(a *arena) error {
 			g.nomLast = append(g.nomLast, name)
 		}
 		for _, np := range pods {
-			q, err := g.comp.compilePod(np, p)
+			q, err := g.comp.compilePod(np, nil, ps) // addNominatedPods reads no DefaultSelector
 			if err != nil {
 				return err
 			}
@@ -126,7 +130,7 @@ func (g *GpuEval) syncNominated(a *arena) error {
 		return nil
 	}
 	g.nominated = len(noms) > 0
-	return g.eng.setNominated(noms, recs, p.toC(a))
+	return g.eng.setNominated(noms, recs, ps.toC(a))
 }
 
 func sortInt32s(x []int32) {
@@ -191,15 +195,14 @@ func (g *GpuEval) selectOnDevice(pod *v1.Pod, nodes []*framework.NodeInfo,
 	list := nodes
 	var a arena
 	defer a.free()
-	p := &pools{}
-	q, err := g.comp.compilePod(pod, p)
+	ps, err := newPoolSet()
 	if err != nil {
 		return nil, "", err
 	}
-	if sel := g.defaultSelector(pod); sel != nil {
-		if q.dpts, err = g.comp.labelSelector(p, sel); err != nil {
-			return nil, "", err
-		}
+	a.onFree(ps.free)
+	q, err := g.comp.compilePod(pod, g.defaultSelector(pod), ps)
+	if err != nil {
+		return nil, "", err
 	}
 	prio := podutil.GetPodPriority(pod)
 	var victims []C.kgpu_victim
@@ -228,7 +231,7 @@ func (g *GpuEval) selectOnDevice(pod *v1.Pod, nodes []*framework.NodeInfo,
 				return nil, "", fmt.Errorf("gpueval: pod %s/%s is not in the device mirror (resynced; retry)",
 					pi.Pod.Namespace, pi.Pod.Name)
 			}
-			r, err := g.comp.compilePod(pi.Pod, p)
+			r, err := g.comp.compilePod(pi.Pod, nil, ps)
 			if err != nil {
 				return nil, "", err
 			}
@@ -263,7 +266,7 @@ func (g *GpuEval) selectOnDevice(pod *v1.Pod, nodes []*framework.NodeInfo,
 		victims[i].pdb_mask = C.uint64_t(m)
 	}
 	cq := cQueries(&a, []C.kgpu_pod_query{q})
-	out, vout, chosen, err := g.eng.selectVictims(cq, p.toC(&a), victims, recs, allowed, len(g.mir.names))
+	out, vout, chosen, err := g.eng.selectVictims(cq, ps.toC(&a), victims, recs, allowed, len(g.mir.names))
 	if err != nil {
 		return nil, "", err
 	}

@@ -1,7 +1,7 @@
 package gpueval
 
-// Device mirror of the scheduling Snapshot (mirror of kubernetes-1_amd/kgpu/compile.py
-// compile_snapshot and kgpu/cache.py sync):
+// Device mirror of the scheduling Snapshot (mirror of kubernetes-1_amd/kgpu/cache.py sync; the
+// records themselves come from libkgpu's compiler, compile.go):
 //
 //   * upload():   Snapshot.List() -> kgpu_snapshot SoA columns (node order = node index).
 //   * sync():     at PreFilter, the Snapshot was just refreshed by cache.UpdateSnapshot
@@ -22,9 +22,7 @@ import (
 
 	v1 "k8s.io/api/core/v1"
 	"k8s.io/apimachinery/pkg/types"
-	v1helper "k8s.io/kubernetes/pkg/apis/core/v1/helper"
 	framework "k8s.io/kubernetes/pkg/scheduler/framework/v1alpha1"
-	utilnode "k8s.io/kubernetes/pkg/util/node"
 )
 
 var errNeedsUpload = fmt.Errorf("gpueval: change needs a full upload")
@@ -44,6 +42,24 @@ type mirror struct {
 	genAt    []int64                     // NodeInfo.Generation last sent, by list position
 	listData unsafe.Pointer              // backing array of the Snapshot.List() last synced
 	labels   labelCounts                 // per key, nodes carrying each value (key_unique)
+	res      map[string]nodeRes          // NodeInfo.Requested / NonZeroRequested last sent, by node name
+}
+
+// nodeRes: the resource sums of a NodeInfo the device row holds (NodeInfo.AddPod, types.go:549-581).
+type nodeRes struct {
+	req [3]int64 // Requested: MilliCPU, Memory, EphemeralStorage
+	nz  [2]int64 // NonZeroRequested: MilliCPU, Memory
+}
+
+func resOf(ni *framework.NodeInfo) nodeRes {
+	var r nodeRes
+	if q := ni.Requested; q != nil {
+		r.req = [3]int64{q.MilliCPU, q.Memory, q.EphemeralStorage}
+	}
+	if q := ni.NonZeroRequested; q != nil {
+		r.nz = [2]int64{q.MilliCPU, q.Memory}
+	}
+	return r
 }
 
 // recordSlots keeps the pod-table slot of every pod the last delta batch added.
@@ -63,70 +79,6 @@ func (m *mirror) uid(u types.UID) int64 {
 	m.nextUID++
 	m.uids[u] = m.nextUID
 	return m.nextUID
-}
-
-// nodeRow compiles the node's own attributes (kgpu_node_row).
-func (c *compiler) nodeRow(n *v1.Node, p *pools) (C.kgpu_node_row, error) {
-	var r C.kgpu_node_row
-	al := n.Status.Allocatable
-	r.alloc_cpu = C.int64_t(al.Cpu().MilliValue())
-	r.alloc_mem = C.int64_t(al.Memory().Value())
-	r.alloc_eph = C.int64_t(al.StorageEphemeral().Value())
-	r.alloc_pods = C.int32_t(al.Pods().Value())
-	if n.Spec.Unschedulable {
-		r.unschedulable = 1
-	}
-	r.zone_id = -1
-	if z := utilnode.GetZoneKey(n); z != "" {
-		r.zone_id = C.int32_t(c.zones.add(z))
-	}
-	pairs := []int32{}
-	for k, v := range n.Labels {
-		ki := c.nkeys.key(k)
-		if ki < 0 || int(ki) >= c.dims.K {
-			return r, errNeedsUpload
-		}
-		_, vi := c.nkeys.add(k, v)
-		pairs = append(pairs, ki, vi)
-	}
-	r.labels = p.intsRange(pairs)
-	TW := c.dims.TW
-	words := make([]uint64, 2*TW)
-	any := false
-	for _, t := range n.Spec.Taints {
-		id := c.taintID(taintKey{t.Key, t.Value, string(t.Effect)})
-		if int(id)/64 >= TW {
-			return r, errNeedsUpload
-		}
-		switch t.Effect {
-		case v1.TaintEffectNoSchedule, v1.TaintEffectNoExecute:
-			words[id/64] |= 1 << (uint(id) % 64)
-			any = true
-		case v1.TaintEffectPreferNoSchedule:
-			words[TW+int(id)/64] |= 1 << (uint(id) % 64)
-			any = true
-		}
-	}
-	if any {
-		r.taints = p.wordsRange(words)
-	}
-	sc := make([]uint64, c.dims.S)
-	anyS := false
-	for res, q := range al {
-		if !v1helper.IsScalarResourceName(res) {
-			continue
-		}
-		col := c.scalars.add(string(res))
-		if int(col) >= c.dims.S {
-			return r, errNeedsUpload
-		}
-		sc[col] += uint64(q.Value())
-		anyS = true
-	}
-	if anyS {
-		r.alloc_scalar = p.wordsRange(sc)
-	}
-	return r, nil
 }
 
 // labelCounts: per node label key, how many listed nodes carry each value id; multi[k] counts the
@@ -164,22 +116,9 @@ func (lc *labelCounts) unique(K int) []uint8 {
 	return out
 }
 
-// nodeLabels: (key id, value id) pairs of a node against the compiler's dictionaries.
-func (c *compiler) nodeLabels(n *v1.Node) [][2]int32 {
-	var out [][2]int32
-	for k, v := range n.Labels {
-		ki := c.nkeys.key(k)
-		if ki < 0 {
-			continue
-		}
-		out = append(out, [2]int32{ki, c.nkeys.val(ki, v)})
-	}
-	return out
-}
-
 // deltaBuild accumulates one kgpu_delta_batch.
 type deltaBuild struct {
-	p          *pools
+	ps         *poolSet
 	deltas     []C.kgpu_delta
 	podsQ      []C.kgpu_pod_query
 	rows       []C.kgpu_node_row
@@ -194,7 +133,7 @@ func (g *GpuEval) diffNode(b *deltaBuild, ni *framework.NodeInfo, pos int32, was
 	nm := ni.Node().Name
 	if !wasListed || m.nodes[nm] != ni.Node() {
 		if _, done := b.rowOf[nm]; !done {
-			r, err := c.nodeRow(ni.Node(), b.p)
+			r, err := c.nodeRow(ni.Node(), b.ps)
 			if err != nil {
 				return err
 			}
@@ -202,18 +141,18 @@ func (g *GpuEval) diffNode(b *deltaBuild, ni *framework.NodeInfo, pos int32, was
 			b.rowOf[nm] = len(b.rows) - 1
 			b.deltas = append(b.deltas, C.kgpu_delta{op: C.KGPU_D_SET_NODE, node: C.int32_t(pos), item: C.int32_t(len(b.rows) - 1)})
 			if old := m.nodes[nm]; old != nil {
-				for _, kv := range c.nodeLabels(old) {
+				for _, kv := range c.nodeLabelIDs(old) {
 					m.labels.add(kv[0], kv[1], -1)
 				}
 			}
-			for _, kv := range c.nodeLabels(ni.Node()) {
+			for _, kv := range c.nodeLabelIDs(ni.Node()) {
 				m.labels.add(kv[0], kv[1], 1)
 			}
 			b.labelMoved = true
 		}
 	}
 	podDelta := func(pod *v1.Pod, op C.int32_t) error {
-		q, err := c.compilePod(pod, b.p)
+		q, err := c.compilePod(pod, nil, b.ps) // NodeInfo.AddPod / RemovePod read no DefaultSelector
 		if err != nil {
 			return err
 		}
@@ -253,6 +192,7 @@ func (g *GpuEval) diffNode(b *deltaBuild, ni *framework.NodeInfo, pos int32, was
 	m.pods[nm] = cur
 	m.gens[nm] = ni.Generation
 	m.nodes[nm] = ni.Node()
+	m.res[nm] = resOf(ni)
 	return nil
 }
 
@@ -269,7 +209,12 @@ func (g *GpuEval) diffNode(b *deltaBuild, ni *framework.NodeInfo, pos int32, was
 // full walk (node adds / removes are rare).
 func (g *GpuEval) deltaFromSnapshot(list []*framework.NodeInfo, a *arena) (*C.kgpu_delta_batch, error) {
 	m, c := g.mir, g.comp
-	b := &deltaBuild{p: &pools{}, rowOf: map[string]int{}}
+	ps, err := newPoolSet()
+	if err != nil {
+		return nil, err
+	}
+	a.onFree(ps.free) // the batch's queries and rows point into it until kgpu_apply_delta returns
+	b := &deltaBuild{ps: ps, rowOf: map[string]int{}}
 	g.syncs++
 	same := len(list) == len(m.names) && (len(list) == 0 || unsafe.Pointer(&list[0]) == m.listData)
 	var order []int32
@@ -339,12 +284,13 @@ func (g *GpuEval) deltaFromSnapshot(list []*framework.NodeInfo, a *arena) (*C.kg
 		// labels of the nodes that left the list
 		for nm, n := range m.nodes {
 			if _, ok := newIndex[nm]; !ok {
-				for _, kv := range c.nodeLabels(n) {
+				for _, kv := range c.nodeLabelIDs(n) {
 					m.labels.add(kv[0], kv[1], -1)
 				}
 				delete(m.nodes, nm)
 				delete(m.pods, nm)
 				delete(m.gens, nm)
+				delete(m.res, nm)
 				b.labelMoved = true
 			}
 		}
@@ -365,67 +311,28 @@ func (g *GpuEval) deltaFromSnapshot(list []*framework.NodeInfo, a *arena) (*C.kg
 		bt.n_order, bt.order = C.int32_t(len(order)), ci32(a, order)
 	}
 	if !same || len(b.rows) > 0 {
-		g.nodeLists(list, bt, a) // ImageLocality / NodePreferAvoidPods CSR over the new list
-		g.keyMeta(bt, a)         // label dictionaries may have grown
+		nodes := make([]*v1.Node, len(list))
+		for i, ni := range list {
+			nodes[i] = ni.Node()
+		}
+		// ImageLocality / NodePreferAvoidPods CSR over the new list; label dictionaries may have grown
+		if err := c.nodeLists(nodes, bt, a); err != nil {
+			return nil, err
+		}
+		if err := c.keyMeta(bt, a); err != nil {
+			return nil, err
+		}
 	}
 	if b.labelMoved {
 		bt.key_unique = cu8(a, m.labels.unique(c.dims.K))
 	}
-	bt.n_zones = C.int32_t(len(c.zones.items))
-	bt.pools = *b.p.toC(a)
+	bt.n_zones = C.int32_t(c.dictSize(C.KGPU_DICT_ZONE, 0))
+	bt.pools = *ps.toC(a)
+	if !same {
+		// node names (NodeName, matchFields) resolve against the new list from the next compile on
+		if err := c.setOrder(m.names); err != nil {
+			return nil, err
+		}
+	}
 	return bt, nil
-}
-
-// nodeLists fills the ImageLocality scaledImageScore and NodePreferAvoidPods CSR
-// (image_locality.go:100-113; node_prefer_avoid_pods.go:47-82).
-func (g *GpuEval) nodeLists(list []*framework.NodeInfo, b *C.kgpu_delta_batch, a *arena) {
-	c := g.comp
-	total := float64(len(list))
-	off, ids, scores := []int32{0}, []int32{}, []int64{}
-	aoff, aids := []int32{0}, []int32{}
-	for _, ni := range list {
-		for name, st := range ni.ImageStates {
-			ids = append(ids, c.images.add(name))
-			scores = append(scores, int64(float64(st.Size)*(float64(st.NumNodes)/total)))
-		}
-		sortCSR(ids[off[len(off)-1]:], scores[off[len(off)-1]:])
-		off = append(off, int32(len(ids)))
-		if avoids, err := v1helper.GetAvoidPodsFromNodeAnnotations(ni.Node().Annotations); err == nil {
-			for _, av := range avoids.PreferAvoidPods {
-				if pc := av.PodSignature.PodController; pc != nil {
-					aids = append(aids, c.controllers.add(pc.Kind+"/"+string(pc.UID)))
-				}
-			}
-		}
-		aoff = append(aoff, int32(len(aids)))
-	}
-	b.image_off = ci32(a, off)
-	b.image_id = ci32(a, append(ids, 0))
-	b.image_score = ci64(a, append(scores, 0))
-	b.avoid_off = ci32(a, aoff)
-	b.avoid_id = ci32(a, append(aids, 0))
-}
-
-// keyMeta sends the node label dictionaries (key_n_values / value_off / value_int ...).
-func (g *GpuEval) keyMeta(b *C.kgpu_delta_batch, a *arena) {
-	c := g.comp
-	K := c.dims.K
-	nv, off, empty := make([]int32, K), []int32{0}, make([]int32, K)
-	ints, oks := []int64{}, []uint8{}
-	for k := 0; k < K; k++ {
-		d := c.nkeys.vals[k]
-		nv[k] = int32(len(d.items))
-		for _, v := range d.items {
-			x, ok := parseInt64(v)
-			ints = append(ints, x)
-			oks = append(oks, ok)
-		}
-		off = append(off, int32(len(ints)))
-		empty[k] = d.get("")
-	}
-	b.key_n_values = ci32(a, append(nv, 0))
-	b.value_off = ci32(a, off)
-	b.value_int = ci64(a, append(ints, 0))
-	b.value_int_ok = cu8(a, append(oks, 0))
-	b.key_empty_value = ci32(a, append(empty, 0))
 }
