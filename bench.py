@@ -259,6 +259,19 @@ def measure(args, cfg, n_nodes_per_gpu, B, K, W, cpu_sample, cpu_threads, latenc
         la = np.array(lat)
         lat_rec = {"call": "kgpu_schedule_one", "pods": len(lat), "p50_us": round(float(np.percentile(la, 50)), 2),
                    "p99_us": round(float(np.percentile(la, 99)), 2), "mean_us": round(float(la.mean()), 2)}
+    # what a scheduleOne cycle costs through a product boundary (scheduler.go:509-593): the pod compile
+    # (PreFilter-time host work, libkgpu's C compile and the Python marshalling in front of it), the
+    # drop-in cycle (compile + kgpu_schedule_one per pod, the Go shim's PreFilter) and the HTTP extender's
+    # verbs (filter + prioritize + bind per pod, JSON in process)
+    comp_rec = dropin_rec = ext_rec = None
+    if rank == 0 and world == 1 and args.dropin_pods > 0:
+        from tools.compile_bench import compile_costs
+        comp_rec = compile_costs(fw, pods[:min(len(pods), 1000)], reps=2)
+        comp_rec["pods"] = min(len(pods), 1000)
+        reset()
+        dropin_rec = dropin_cycles(fw, eng, pods[:args.dropin_pods], len(q_init), comp_rec)
+        if nodes is not None and not init and n_cluster <= 10000 and args.extender_pods > 0:
+            ext_rec = extender_cycles(prof, nodes, existing, pods[:args.extender_pods], local)
     # eval_launches counts node-evaluation passes (one per pod); with the persistent kernel one
     # launch covers the whole batch, so the per-launch duration is kernel_ms / launches_made
     per_pod_s = kst.eval_kernel_ms / 1e3 / max(kst.eval_launches, 1)
@@ -334,11 +347,93 @@ def measure(args, cfg, n_nodes_per_gpu, B, K, W, cpu_sample, cpu_threads, latenc
                      "bytes_per_launch": pod_bytes * launch_pods},
         "cpu_baseline": cpu,
         "latency": lat_rec,
+        "compile_us_per_pod": comp_rec["c_us_per_pod"] if comp_rec else None,
+        "compile": comp_rec,
+        "dropin": dropin_rec,
+        "extender": ext_rec,
     }
     # release the device context before the next workload and before interpreter teardown (under
     # rocprofv3 the HIP runtime may be finalized before a garbage-collected engine would be)
     eng.close()
     return rec
+
+
+def dropin_cycles(fw, eng, pods, first_seq, comp_rec):
+    """The Go shim's PreFilter per pod, timed one pod at a time: kgpu_compile_pod from a descriptor built
+    beforehand (desc.go's marshalling is Go's cost, reported beside it from the Python twin) and
+    kgpu_schedule_one with assume.  pods/s of the whole loop."""
+    import ctypes as C
+
+    import numpy as np
+    from kgpu import abi, cdesc
+    from kgpu.compile import Pools
+    L = cdesc.lib()
+    comp = fw.compiler
+    descs = [comp.pod_desc(p) for p in pods]
+    pools = Pools()
+    q = np.zeros(1, abi.QUERY)
+    cu, cy = [], []
+    t_all = time.perf_counter()
+    for i, d in enumerate(descs):
+        t0 = time.perf_counter()
+        rc = L.kgpu_compile_pod(comp._cc, pools.h, C.byref(d), q.ctypes.data)
+        view = pools.view()
+        t1 = time.perf_counter()
+        if rc != 0:
+            raise RuntimeError("kgpu_compile_pod: %s" % comp._err())
+        eng.schedule_one(q[0], view, seq=first_seq + i, assume=True)
+        t2 = time.perf_counter()
+        cu.append((t1 - t0) * 1e6)
+        cy.append((t2 - t0) * 1e6)
+    total = time.perf_counter() - t_all
+    cu, cy = np.array(cu), np.array(cy)
+    pct = lambda a, p: round(float(np.percentile(a, p)), 2)  # noqa: E731
+    return {"call": "kgpu_compile_pod + kgpu_schedule_one (assume)", "pods": len(descs),
+            "pods_s": round(len(descs) / total, 1), "compile_us_p50": pct(cu, 50), "compile_us_p99": pct(cu, 99),
+            "cycle_us_p50": pct(cy, 50), "cycle_us_p99": pct(cy, 99),
+            "marshal_us_per_pod": comp_rec.get("marshal_us_per_pod"),
+            "note": "descriptors built outside the clock (the Go shim marshals in Go; the Python twin's "
+                    "marshal cost is marshal_us_per_pod)"}
+
+
+def extender_cycles(prof, nodes, existing, pods, device):
+    """The HTTP extender (kgpu/extender.py) per pod: filter -> prioritize -> bind with
+    ExtenderArgs JSON-encoded and decoded in process (the wire format, no socket), every node a candidate
+    (nodeCacheCapable: NodeNames), the selectHost pick among the prioritize scores bound.  Its own
+    scheduler-cache mirror and engine on the same cluster."""
+    import numpy as np
+    from kgpu import api
+    from kgpu.cache import SchedulerCache
+    from kgpu.extender import GpuExtender
+    cache = SchedulerCache(prof, nodes, existing, device=device)
+    ext = GpuExtender(cache)
+    names = [api.name_of(n) for n in nodes]
+    ts = []
+    placed = 0
+    try:
+        for k, pod in enumerate(pods):
+            t0 = time.perf_counter()
+            fr = json.loads(json.dumps(ext.filter(json.loads(json.dumps({"Pod": pod, "NodeNames": names})))))
+            if fr.get("Error"):
+                raise RuntimeError("extender filter: %s" % fr["Error"])
+            feasible = fr.get("NodeNames") or []
+            if feasible:
+                pr = json.loads(json.dumps(ext.prioritize(json.loads(json.dumps({"Pod": pod, "NodeNames": feasible})))))
+                best = max(pr, key=lambda h: h["Score"])["Host"]
+                md = api.meta(pod)
+                br = ext.bind(json.loads(json.dumps({"PodName": md.get("name", ""), "PodNamespace": md.get("namespace", ""),
+                                                     "PodUID": md.get("uid", ""), "Node": best})))
+                if br.get("Error"):
+                    raise RuntimeError("extender bind: %s" % br["Error"])
+                placed += 1
+            if k > 0:  # the first pod pays the mirror's first sync
+                ts.append((time.perf_counter() - t0) * 1e6)
+    finally:
+        cache.close()
+    a = np.array(ts)
+    return {"verbs": "filter + prioritize + bind (JSON in process, no socket)", "pods": len(ts), "placed": placed,
+            "pods_s": round(len(ts) / (a.sum() / 1e6), 1), "us_p50": round(float(np.percentile(a, 50)), 1),
+            "us_p99": round(float(np.percentile(a, 99)), 1)}
 
 
 DEFAULT_EXTRAS_1GPU = "b:100000,c:5000,d:5000,c:100000,d:100000,e:125000"
@@ -432,6 +527,11 @@ def main():
                     help="pods timed for the CPU baseline (-1: the whole workload, 0: skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--latency-pods", type=int, default=200, help="pods timed one at a time through kgpu_schedule_one")
+    ap.add_argument("--dropin-pods", type=int, default=200,
+                    help="pods timed through the drop-in cycle (C compile + kgpu_schedule_one); 0: skip the compile, "
+                         "drop-in and extender records")
+    ap.add_argument("--extender-pods", type=int, default=30,
+                    help="pods through the extender's filter / prioritize / bind (configs up to 10k nodes)")
     ap.add_argument("--no-persistent", action="store_true", help="one evaluation launch per pod")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="synchronous kgpu_schedule_batch per step instead of pipelined submit / wait")
@@ -516,10 +616,13 @@ def main():
     # the same records in brief, last in the line: the driver keeps the tail of the output
     def brief(r):
         rf, cb, lt = r["roofline"], r.get("cpu_baseline") or {}, r.get("latency") or {}
+        di, ex = r.get("dropin") or {}, r.get("extender") or {}
         return {"s": r["series"], "pods_s": round(r["value"]), "us_pod": rf["us_per_pod"], "GBs": rf["achieved"],
                 "frac": rf["frac"], "traffic": rf["traffic"], "cpu": cb.get("value"), "cpu_th": cb.get("cores"),
                 "cpu_1th": (cb.get("rates_by_threads") or {}).get("1"),
-                "one_p50_p99": [lt.get("p50_us"), lt.get("p99_us")] if lt else None}
+                "one_p50_p99": [lt.get("p50_us"), lt.get("p99_us")] if lt else None,
+                "compile_us": r.get("compile_us_per_pod"), "dropin_pods_s": di.get("pods_s"),
+                "extender_pods_s": ex.get("pods_s")}
     line["summary"] = [brief(r) for r in [line] + recs]
     if rank == 0:
         print(json.dumps(line), flush=True)

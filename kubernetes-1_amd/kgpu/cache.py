@@ -358,7 +358,8 @@ class SchedulerCache:
         if self.engine is not None:
             self.engine.apply_delta(batch, self.generation, len(d), keep)
         self.list, self.index = list(new_list), new_index
-        comp.set_order(new_list, first_wins=True)  # a node's first row addresses all of its rows
+        if reorder:
+            comp.set_order(new_list, first_wins=True)  # a node's first row addresses all of its rows
         self.dev_pods = dev
         self._log.clear()
         self._dirty_nodes.clear()

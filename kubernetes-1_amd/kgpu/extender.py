@@ -107,7 +107,8 @@ class GpuExtender:
             totals[:] = 1  # no score plugins: every feasible node scores 1 (generic_scheduler.go:631-640)
         node = int(res["node"])
         cyc = {"words": words, "totals": totals, "winner": self.cache.list[node] if node >= 0 else None,
-               "error": node == -2, "seq": seq, "compiled": (q, pc)}
+               "node": node, "error": node == -2, "seq": seq, "compiled": (q, pc),
+               "n_scalars": int(q["scalars"]["count"]), "scalar_names": None, "reasons": {}}
         if uid:
             self._memo = (uid, gen, cyc)
             self._remember(uid, pod)
@@ -121,25 +122,46 @@ class GpuExtender:
                                  now - next(iter(self._pending.values()))[1] > PENDING_TTL):
             self._pending.popitem(last=False)
 
-    def _winner(self, cyc, names):
+    def _winner(self, cyc, names, idx):
         """selectHost over the candidates the device found feasible: the maximum of
-        total << 40 | rank40 (the build's tie-break, kgpu/tiebreak.py)."""
+        total << 40 | rank40 (the build's tie-break, kgpu/tiebreak.py).  When the candidates hold every
+        node the device found feasible, that is the device's own selectHost pick."""
+        feas = idx[cyc["words"][idx] == 0]
+        if len(feas) == 0:
+            return None
+        if cyc["node"] >= 0 and len(np.unique(feas)) == int((cyc["words"] == 0).sum()):
+            return cyc["winner"]
         prof = self.cache.profile
-        seed = int(getattr(prof, "seed", 0x7B))
-        mode = int(getattr(prof, "tie_break_mode", tiebreak.MODE_HASH))
-        best, best_nm = -1, None
-        for nm in names:
-            i = self.cache.index[nm]
-            if int(cyc["words"][i]) != 0:
-                continue
-            k = tiebreak.key(int(cyc["totals"][i]), i, seed, cyc["seq"], mode)
-            if k > best:
-                best, best_nm = k, nm
-        return best_nm
+        keys = tiebreak.keys_np(cyc["totals"][feas], feas, int(getattr(prof, "seed", 0x7B)), cyc["seq"],
+                                int(getattr(prof, "tie_break_mode", tiebreak.MODE_HASH)))
+        return self.cache.list[int(feas[int(np.argmax(keys))])]
+
+    def _reasons(self, cyc, pod, nm, i, w, filters):
+        """The FailedNodes string of node nm (local index i, status word w).  Reasons depend on the word,
+        the pod and -- for TaintToleration -- the node's taints, and for NodeResourcesFit's scalar
+        resources on the node's columns: memoized per (word, taints) except in that last case."""
+        plugin = filters[(w & 0xFF) - 1]
+        memo = not (plugin == "NodeResourcesFit" and cyc["n_scalars"])
+        if memo:
+            taints = tuple((t.get("key", ""), t.get("value", ""), t.get("effect", ""))
+                           for t in api.spec(self.cache.nodes.get(nm) or {}).get("taints") or []) \
+                if plugin == "TaintToleration" else ()
+            hit = cyc["reasons"].get((w, taints))
+            if hit is not None:
+                return hit
+        if cyc["scalar_names"] is None:
+            cyc["scalar_names"] = self.cache.compiler.scalar_names(pod)
+        st = status_reasons(filters, self.cache.compiler, self.cache.nodes, pod, nm, w, handle=self.cache.engine.h,
+                            node=i, compiled=cyc["compiled"], scalar_names=cyc["scalar_names"])
+        out = ", ".join(st[2]) if st and st[2] else (st[1] if st else "")
+        if memo:
+            cyc["reasons"][(w, taints)] = out
+        return out
 
     def _candidates(self, args):
-        """ExtenderArgs -> (names, NodeList items or None).  NodeNames when the scheduler treats
-        the extender as node-cache capable, else the full Node objects (extender.go:293-304)."""
+        """ExtenderArgs -> (names, NodeList items or None, local node indices).  NodeNames when the
+        scheduler treats the extender as node-cache capable, else the full Node objects
+        (extender.go:293-304)."""
         names = args.get("NodeNames")
         items = None
         if names is None:
@@ -150,10 +172,16 @@ class GpuExtender:
             names = [api.name_of(n) for n in items]
             self._sync_nodes(items)
         self.cache.sync()
-        for nm in names:
-            if nm not in self.cache.index:
-                raise ExtenderError("node %r is not in the extender's node cache" % nm)
-        return names, items
+        try:
+            idx = self._indices(names)
+        except KeyError as e:
+            raise ExtenderError("node %r is not in the extender's node cache" % e.args[0])
+        return names, items, idx
+
+    def _indices(self, names):
+        """The candidates' local node indices (numpy)."""
+        ix = self.cache.index
+        return np.fromiter((ix[nm] for nm in names), np.int64, len(names))
 
     def _sync_nodes(self, items):
         """Node objects sent with each call (nodeCacheCapable false) refresh the mirror's copy."""
@@ -170,24 +198,20 @@ class GpuExtender:
         try:
             with self.lock:
                 pod = args.get("Pod") or {}
-                names, items = self._candidates(args)
+                names, items, idx = self._candidates(args)
                 cyc = self._cycle(pod)
                 if cyc["error"]:
                     raise ExtenderError("a score plugin failed for pod %s/%s" % (api.ns_of(pod), api.name_of(pod)))
-                keep, failed = [], {}
                 filters = [f for f in self.cache.profile.filters if f in abi.FILTER_IDS]
-                for k, nm in enumerate(names):
-                    w = int(cyc["words"][self.cache.index[nm]])
-                    if w == 0:
-                        keep.append(k)
-                        continue
+                w_all = cyc["words"][idx]
+                keep = np.nonzero(w_all == 0)[0].tolist()
+                failed = {}
+                for k in np.nonzero(w_all != 0)[0].tolist():
+                    nm, w = names[k], int(w_all[k])
                     if w == abi.STATUS_NOT_EVALUATED:
                         failed[nm] = "node not evaluated (percentageOfNodesToScore)"
-                        continue
-                    st = status_reasons(filters, self.cache.compiler, self.cache.nodes, pod, nm, w,
-                                        handle=self.cache.engine.h, node=self.cache.index[nm],
-                                        compiled=cyc["compiled"])
-                    failed[nm] = ", ".join(st[2]) if st and st[2] else (st[1] if st else "")
+                    else:
+                        failed[nm] = self._reasons(cyc, pod, nm, int(idx[k]), w, filters)
         except ExtenderError as e:
             return {"Nodes": None, "NodeNames": None, "FailedNodes": None, "Error": str(e)}
         out = {"Nodes": None, "NodeNames": None, "FailedNodes": failed, "Error": ""}
@@ -202,17 +226,13 @@ class GpuExtender:
         the scheduler ignores a failing prioritizer (generic_scheduler.go:686-688)."""
         with self.lock:
             pod = args.get("Pod") or {}
-            names, _ = self._candidates(args)
+            names, _, idx = self._candidates(args)
             cyc = self._cycle(pod)
-            winner = self._winner(cyc, names) if self.mode == "select" else None
-            out = []
-            for nm in names:
-                if self.mode == "select":
-                    s = MAX_EXTENDER_PRIORITY if nm == winner else 0
-                else:
-                    s = int(cyc["totals"][self.cache.index[nm]]) if cyc["words"][self.cache.index[nm]] == 0 else 0
-                out.append({"Host": nm, "Score": s})
-            return out
+            if self.mode == "select":
+                winner = self._winner(cyc, names, idx)
+                return [{"Host": nm, "Score": MAX_EXTENDER_PRIORITY if nm == winner else 0} for nm in names]
+            sc = np.where(cyc["words"][idx] == 0, cyc["totals"][idx], 0).tolist()
+            return [{"Host": nm, "Score": int(s)} for nm, s in zip(names, sc)]
 
     def bind(self, args):
         """ExtenderBindingArgs -> ExtenderBindingResult (extender.go:384-404)."""

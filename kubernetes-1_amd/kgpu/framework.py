@@ -32,13 +32,15 @@ def node_taints(compiler, node):
     return out
 
 
-def status_reasons(filters, compiler, nodes, pod, node_name, word, handle=None, node=-1, compiled=None):
+def status_reasons(filters, compiler, nodes, pod, node_name, word, handle=None, node=-1, compiled=None,
+                   scalar_names=None):
     """(code, plugin, reasons) of a node's device status word, None for a feasible node.  The reasons
     come from libkgpu's kgpu_filter_reasons, the formatter the Go shim's Filter calls too, which
     writes them exactly as the failing plugin does (file:line at each message in kgpu_reasons.h).
     filters: the profile's filter plugins in order; nodes: name -> v1.Node; handle: the engine that
     produced the word (None: pure formatting); node: the word's local node index; compiled: the pod's
-    (query, pools) when the caller holds them."""
+    (query, pools) when the caller holds them; scalar_names: compiler.scalar_names(pod) when the caller
+    holds them (a cycle formats many nodes' reasons for one pod)."""
     pos = word & 0xFF
     if pos == 0 or word == abi.STATUS_NOT_EVALUATED:
         return None
@@ -50,8 +52,10 @@ def status_reasons(filters, compiler, nodes, pod, node_name, word, handle=None, 
         pc, _ = pools.finalize()
     else:
         q, pc = compiled
+    if scalar_names is None:
+        scalar_names = compiler.scalar_names(pod)
     reasons = native.filter_reasons(handle, q, pc, node, word, node_taints(compiler, nodes.get(node_name)),
-                                    compiler.scalar_names(pod),
+                                    scalar_names,
                                     filters=None if handle else [abi.FILTER_IDS[f] for f in filters])
     return code, plugin, reasons
 

@@ -35,3 +35,23 @@ def rank(seed, seq, idx, mode=MODE_HASH):
 
 def key(score, idx, seed, seq, mode=MODE_HASH):
     return (score << 40) | rank(seed, seq, idx, mode)
+
+
+def keys_np(scores, idx, seed, seq, mode=MODE_HASH):
+    """key() over arrays of scores and node indices (numpy uint64; the 40-bit products wrap mod 2^64,
+    which keeps their low 40 bits exact)."""
+    import numpy as np
+    idx = np.asarray(idx, np.uint64)
+    if mode == MODE_FIRST:
+        r = np.uint64(MASK40) - idx
+    else:
+        k = _splitmix64((seed ^ ((seq * _PHI) & M64)) & M64)
+        m = np.uint64(MASK40)
+        with np.errstate(over="ignore"):
+            x = (idx & m) ^ np.uint64(k & MASK40)
+            x = (x * np.uint64(0xD6E8FEB865)) & m
+            x ^= x >> np.uint64(19)
+            x = (x * np.uint64(0x94D049BB13)) & m
+            x ^= x >> np.uint64(23)
+        r = x ^ np.uint64((k >> 24) & MASK40)
+    return (np.asarray(scores, np.uint64) << np.uint64(40)) | r

@@ -30,3 +30,19 @@ def test_rank40_inverse_round_trip():
             for i in idx:
                 x = (M - i) if mode == tiebreak.MODE_FIRST else tiebreak.rank40(k, i)
                 assert rank40_inv(k, x, mode) == i, (mode, seq, i)
+
+
+def test_tiebreak_keys_np_matches_scalar_keys():
+    """kgpu.tiebreak.keys_np (the extender's vectorized selectHost over candidates) equals key() per node."""
+    import random
+
+    import numpy as np
+    from kgpu import tiebreak as T
+    rng = random.Random(7)
+    for mode in (T.MODE_HASH, T.MODE_FIRST):
+        for _ in range(100):
+            seed, seq = rng.getrandbits(64), rng.getrandbits(24)
+            idx = np.array([rng.randrange(1 << 21) for _ in range(40)])
+            sc = np.array([rng.randrange(1 << 23) for _ in range(40)])
+            got = [int(x) for x in T.keys_np(sc, idx, seed, seq, mode)]
+            assert got == [T.key(int(s), int(i), seed, seq, mode) for s, i in zip(sc, idx)]
