@@ -1,4 +1,4 @@
-"""Node sharding with topology plugins on the CPU: world_size-2 gloo ranks.
+"""Node sharding with topology plugins on the CPU: world_size-2 and -4 gloo ranks.
 
 tests/test_shard_cpu.py pins the combine rule for pods whose only cross-node state is the
 DefaultNormalizeScore maxima.  This file pins the rule for PodTopologySpread, InterPodAffinity and
@@ -21,7 +21,9 @@ DefaultPodTopologySpread, whose PreFilter / PreScore state is a function of EVER
 * selectHost: the max packed key over the ranks' best keys (global node index) with the SUMmed
   feasible count must be the unsharded scheduleOne's choice, pod after pod.
 
-The expected side is the unsharded Python oracle (oracle/refsched framework.schedule_sequence)."""
+The expected side is the unsharded Python oracle (oracle/refsched framework.schedule_sequence) and,
+for the world-4 runs, the C restatement (oracle/c) over the whole cluster as well: its placements are
+the device's parity anchor, so the combine rule is pinned against both restatements."""
 import copy
 import os
 import socket
@@ -48,6 +50,8 @@ def _workload(name):
         nodes, existing, pods, _ = cluster.pod_affinity(n_nodes=48, n_existing=48, n_pods=32)
     elif name == "sharded_spread":  # config (e) generator, small: zone = i % 16, NodeAffinity admits zone1..zone4
         nodes, existing, pods, _ = cluster.sharded_spread(n_nodes=160, n_pods=36, n_zones=16)
+    elif name == "sharded_spread_e4":  # config (e) shape over four shards: zone = i % 64 as the bench's 125k shards
+        nodes, existing, pods, _ = cluster.sharded_spread(n_nodes=256, n_pods=40, n_zones=64)
     else:
         nodes, existing, pods, _ = cluster.uneven_zones()
     return nodes, existing, pods
@@ -98,6 +102,19 @@ def _rank_main(rank, world, port, name, out):
         nodes, existing, pods = _workload(name)
         prof = F.Profile()
         want = F.schedule_sequence(nodes, existing, pods, prof)
+        want_c = None
+        if world > 2:
+            # the C restatement over the whole cluster (default provider profile, like F.Profile())
+            from kgpu.compile import Profile
+            from kgpu.framework import GpuFramework
+            from oracle.cref import RefEngine
+            full = GpuFramework(Profile(), nodes, existing, pods_hint=pods, create_engine=False)
+            q, pc, _, errs = full.compile_pods(pods)
+            assert not errs, errs
+            ref = RefEngine(full.config, full.snap)
+            rc = ref.schedule(q, pc)
+            ref.close()
+            want_c = [full.order[int(x)] if int(x) >= 0 else None for x in rc["node"]]
 
         snap = NI.Snapshot(nodes, existing)
         N = len(snap.list)
@@ -155,6 +172,7 @@ def _rank_main(rank, world, port, name, out):
             w = want[k]
             if total == 0:
                 assert isinstance(w, F.FitError), "pod %d: shards found no node, unsharded %r" % (k, w)
+                assert want_c is None or want_c[k] is None, "pod %d: oracle/c placed it on %s" % (k, want_c[k])
                 continue
             assert not isinstance(w, F.ScheduleError), "pod %d: unsharded failed: %r" % (k, w)
             assert total == w.feasible, "pod %d: feasible %d vs %d" % (k, total, w.feasible)
@@ -282,6 +300,7 @@ def _rank_main(rank, world, port, name, out):
                 recs = _gather((best, host), world)
                 host = max(recs)[1]
             assert host == w.host, "pod %d: shards chose %s, unsharded %s" % (k, host, w.host)
+            assert want_c is None or host == want_c[k], "pod %d: shards chose %s, oracle/c %s" % (k, host, want_c[k])
             if host in mine:  # only the owning rank applies the assume (cache.go AssumePod)
                 placed = copy.deepcopy(pod)
                 placed["spec"]["nodeName"] = host
@@ -295,9 +314,7 @@ def _rank_main(rank, world, port, name, out):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("name", ["spread", "interpod", "sharded_spread", "uneven"])
-def test_shard_topology_combine_gloo_world2(name):
-    world = 2
+def _run(name, world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -307,5 +324,17 @@ def test_shard_topology_combine_gloo_world2(name):
     for p in procs:
         p.join(timeout=300)
     got = dict(q.get(timeout=5) for _ in range(world))
-    assert got == {0: "ok", 1: "ok"}, got
+    assert got == {r: "ok" for r in range(world)}, got
     assert all(p.exitcode == 0 for p in procs)
+
+
+@pytest.mark.parametrize("name", ["spread", "interpod", "sharded_spread", "uneven"])
+def test_shard_topology_combine_gloo_world2(name):
+    _run(name, 2)
+
+
+@pytest.mark.parametrize("name", ["sharded_spread_e4", "spread", "interpod"])
+def test_shard_topology_combine_gloo_world4(name):
+    """Four ranks (the combine's associativity beyond a pair; the (e) shape with 64 zones over four
+    shards), checked against the Python oracle and oracle/c on the whole cluster."""
+    _run(name, 4)
