@@ -225,6 +225,17 @@ func (e *engine) scores(plugin int, n int) (raw, norm []int64, err error) {
 	return raw[:n], norm[:n], kerr(e.ctx, rc)
 }
 
+// preparePods registers the topology pod classes of pods expected soon (kgpu_prepare_pods): their count
+// columns are filled now, not on the cycle of the first pod that needs them.
+func (e *engine) preparePods(qs []C.kgpu_pod_query, pools *C.kgpu_pools) error {
+	if len(qs) == 0 {
+		return nil
+	}
+	var a arena
+	defer a.free()
+	return kerr(e.ctx, C.kgpu_prepare_pods(e.ctx, cQueries(&a, qs), C.int32_t(len(qs)), pools))
+}
+
 func (e *engine) forget(slot int32) error { return kerr(e.ctx, C.kgpu_forget_pod(e.ctx, C.int32_t(slot))) }
 func (e *engine) generation() int64       { return int64(C.kgpu_generation(e.ctx)) }
 func (e *engine) close()                  { C.kgpu_destroy(e.ctx) }

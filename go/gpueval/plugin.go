@@ -30,6 +30,7 @@ import (
 	"unsafe"
 
 	v1 "k8s.io/api/core/v1"
+	"k8s.io/apimachinery/pkg/labels"
 	"k8s.io/apimachinery/pkg/runtime"
 	"k8s.io/apimachinery/pkg/types"
 	v1helper "k8s.io/kubernetes/pkg/apis/core/v1/helper"
@@ -278,7 +279,48 @@ func (g *GpuEval) upload(list []*framework.NodeInfo, a *arena) error {
 	}
 	m.gen++
 	g.mir = m
-	return g.eng.uploadSnapshot(s, m.gen)
+	if err := g.eng.uploadSnapshot(s, m.gen); err != nil {
+		return err
+	}
+	return g.prepareQueue()
+}
+
+// prepareQueue registers the pod classes of the unassigned pods the informer holds (at most
+// prepareMax): a new upload epoch starts with empty class tables, and the first cycle of each class
+// would otherwise pay its count (kgpu_prepare_pods).
+const prepareMax = 512
+
+func (g *GpuEval) prepareQueue() error {
+	f := g.h.SharedInformerFactory()
+	if f == nil {
+		return nil
+	}
+	all, err := f.Core().V1().Pods().Lister().List(labels.Everything())
+	if err != nil {
+		return nil
+	}
+	ps, err := newPoolSet()
+	if err != nil {
+		return err
+	}
+	defer ps.free()
+	var qs []C.kgpu_pod_query
+	for _, p := range all {
+		if p.Spec.NodeName != "" || p.DeletionTimestamp != nil {
+			continue
+		}
+		q, err := g.comp.compilePod(p, g.defaultSelector(p), ps)
+		if err != nil {
+			continue // that pod's own cycle reports it
+		}
+		qs = append(qs, q)
+		if len(qs) == prepareMax {
+			break
+		}
+	}
+	var a arena
+	defer a.free()
+	return g.eng.preparePods(qs, ps.toC(&a))
 }
 
 // snapshotSoA compiles the list's nodes and their NodeInfos' pods (kgpu_compile_snapshot: the node

@@ -499,6 +499,15 @@ int kgpu_forget_pod(kgpu_ctx* ctx, int32_t pod_slot);
 int kgpu_next_slot(const kgpu_ctx* ctx);
 int kgpu_adopt_pod(kgpu_ctx* ctx, int32_t pod_slot, int64_t uid);
 
+/* Register ahead of need the pod classes of pods the caller expects to schedule (the queue's pending pods,
+ * the templates of its workloads): the label-selector classes and term classes their topology plugins
+ * count (PodTopologySpread constraints, DefaultPodTopologySpread selectors, InterPodAffinity terms) are
+ * interned and their per-node count columns initialized now -- one launch over the pod table -- instead of
+ * on the cycle of the first pod that needs them.  Changes no placement: a class is a function of the
+ * cluster's pods, kept current by every assume, forget and delta from then on.  Pods whose plans the engine
+ * does not support are skipped (their own cycle reports it).  No-op outside a topology profile. */
+int kgpu_prepare_pods(kgpu_ctx* ctx, const kgpu_pod_query* qs, int32_t n, const kgpu_pools* pools);
+
 /* ---- delta stream (kgpu_apply_delta).  The caller keeps the scheduler cache's bookkeeping
  * (podStates / assumedPods / nodeTree, cache.go) and sends the NodeInfo changes it implies; the
  * engine applies them to the device mirror in one launch and de-duplicates pods by UID. */
@@ -676,7 +685,9 @@ int kgpu_read_nodes(kgpu_ctx* ctx, int64_t* req_cpu, int64_t* req_mem, int64_t* 
 int kgpu_set_option(kgpu_ctx* ctx, int32_t option, int64_t value);
 /* Engine counters: out[0] = calls issued again with a cooperative launch after a persistent run's
  * workgroups were not all resident before its first pod (KGPU_OPT_COOPERATIVE); out[1] = persistent
- * launches; out[2] = cooperative persistent launches.  Returns how many counters exist. */
+ * launches; out[2] = cooperative persistent launches; out[3] = k_class_init launches (pod classes met
+ * for the first time, kgpu_prepare_pods); out[4] = whole pod-table uploads (the table is otherwise sent
+ * incrementally).  Returns how many counters exist. */
 int kgpu_debug_counters(const kgpu_ctx* ctx, int64_t* out, int32_t n);
 /* Diagnostics of KGPU_OPT_TOPO_RESIDENT: out[0] = persistent topology runs that started from the
  * resident state, out[1] = runs that recomputed it. */

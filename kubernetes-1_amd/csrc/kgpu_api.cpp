@@ -255,7 +255,8 @@ struct kgpu_ctx {
     std::vector<int32_t> own_tcls;
   };
   std::vector<PodRow> pod_rows;
-  int pod_rows_dev = -1;         // rows present in the device pod table (-1: table never uploaded)
+  int pod_rows_dev = -1;         // rows present in the device pod table (-1: rebuild it whole)
+  std::vector<int32_t> pod_rows_dirty;  // slots below pod_rows_dev changed in place since (flags)
   std::vector<int32_t> key_n_values, key_empty;
   std::vector<uint8_t> key_unique;  // every value of the key sits on at most one node of THIS shard
   // kgpu_snapshot / kgpu_delta_batch.key_unique: the caller's cluster-wide view (empty: not given)
@@ -272,6 +273,7 @@ struct kgpu_ctx {
   bool run_all = false;             // KGPU_OPT_RUN_ALL_FILTERS
   bool last_run_all = false;        // the last diagnostic cycle wrote status_all
   int64_t n_coop_retry = 0, n_persist = 0, n_coop = 0;  // kgpu_debug_counters
+  int64_t n_class_init = 0, n_pod_table_full = 0;       // ... k_class_init launches, whole pod-table uploads
   int state_launches = 0;           // launches of the current call that may change device state
   // pipelined batches (kgpu_schedule_batch_submit / _wait): two slots, each with its pinned staging block,
   // device block (DevState | queries | run pointers | abort word), granules and pinned result records
@@ -993,22 +995,67 @@ int grow_columns(kgpu_ctx* c, int32_t** tab, int* cap, int need) {
   return KGPU_OK;
 }
 
-// Upload the host pod table (node, ns, flags, dense labels) for k_class_init.
+// A pod row changed in place (its flags): re-sent with the next table sync when already on the device.
+void pod_row_dirty(kgpu_ctx* c, int32_t slot) {
+  if (c->pod_rows_dev >= 0 && slot < c->pod_rows_dev) c->pod_rows_dirty.push_back(slot);
+}
+
+// The device pod table (node, ns, flags, dense labels; column-major with row capacity Pcap and key
+// capacity PKcap) that k_class_init walks.  Incremental: the rows appended since the last sync and the
+// rows changed in place go out as two strided copies (a new pod class on a cluster of 100k pods used to
+// rebuild and send the whole table, ~4 MB, on the cycle that met it); a full rebuild only when a
+// capacity is exceeded or the rows were renumbered (a node reorder).
 int upload_pod_table(kgpu_ctx* c) {
   const int rows = (int)c->pod_rows.size();
-  int pk = 0;
-  for (const auto& r : c->pod_rows)
-    for (size_t j = 0; j + 1 < r.pairs.size(); j += 2) pk = std::max(pk, r.pairs[j] + 1);
-  pk = std::max(pk, 1);
-  const size_t R = (size_t)std::max(rows, 1);
-  std::vector<int32_t> buf(R * (3 + (size_t)pk), -1);
-  for (int i = 0; i < rows; ++i) {
+  auto key_end = [&](int i) {
+    int pk = 0;
     const auto& r = c->pod_rows[(size_t)i];
-    buf[(size_t)i] = r.node;
-    buf[R + i] = r.ns;
-    buf[2 * R + i] = (int32_t)r.flags;
-    for (size_t j = 0; j + 1 < r.pairs.size(); j += 2) buf[(3 + (size_t)r.pairs[j]) * R + i] = r.pairs[j + 1];
+    for (size_t j = 0; j + 1 < r.pairs.size(); j += 2) pk = std::max(pk, r.pairs[j] + 1);
+    return pk;
+  };
+  auto fill = [&](int32_t* col0, size_t stride, int i, int pkc) {  // row i into a (3 + pkc) x stride block
+    const auto& r = c->pod_rows[(size_t)i];
+    col0[0] = r.node;
+    col0[stride] = r.ns;
+    col0[2 * stride] = (int32_t)r.flags;
+    for (int k = 0; k < pkc; ++k) col0[(3 + (size_t)k) * stride] = -1;
+    for (size_t j = 0; j + 1 < r.pairs.size(); j += 2)
+      if (r.pairs[j] >= 0 && r.pairs[j] < pkc) col0[(3 + (size_t)r.pairs[j]) * stride] = r.pairs[j + 1];
+  };
+  if (c->pod_rows_dev >= 0 && c->d_pods.p && rows <= c->st.Pcap) {
+    int pk = 0;
+    for (int i = c->pod_rows_dev; i < rows; ++i) pk = std::max(pk, key_end(i));
+    for (int32_t sl : c->pod_rows_dirty) pk = std::max(pk, key_end(sl));
+    if (pk <= c->st.PKcap) {
+      const size_t P = (size_t)c->st.Pcap, H = 3 + (size_t)c->st.PKcap;
+      int32_t* b = static_cast<int32_t*>(c->d_pods.p);
+      const int nnew = rows - c->pod_rows_dev;
+      std::vector<int32_t> buf(H * (size_t)std::max(nnew, 0) + H * c->pod_rows_dirty.size());
+      if (nnew > 0) {
+        for (int i = 0; i < nnew; ++i) fill(buf.data() + i, (size_t)nnew, c->pod_rows_dev + i, c->st.PKcap);
+        HIP_OK(c, hipMemcpy2DAsync(b + c->pod_rows_dev, P * 4, buf.data(), (size_t)nnew * 4, (size_t)nnew * 4, H,
+                                   hipMemcpyHostToDevice, c->stream));
+      }
+      int32_t* d = buf.data() + H * (size_t)std::max(nnew, 0);
+      for (int32_t sl : c->pod_rows_dirty) {
+        fill(d, 1, sl, c->st.PKcap);
+        HIP_OK(c, hipMemcpy2DAsync(b + sl, P * 4, d, 4, 4, H, hipMemcpyHostToDevice, c->stream));
+        d += H;
+      }
+      SYNC_OK(c);  // buf is pageable and local
+      c->pod_rows_dev = rows;
+      c->pod_rows_dirty.clear();
+      return KGPU_OK;
+    }
   }
+  int pk = 0;
+  for (int i = 0; i < rows; ++i) pk = std::max(pk, key_end(i));
+  // capacities with room for the pods the next cycles assume and the label keys they bring
+  const size_t R = (size_t)std::max(rows + rows / 2, 1024);
+  const int pkc = std::max(pk + 4, 8);
+  ++c->n_pod_table_full;
+  std::vector<int32_t> buf(R * (3 + (size_t)pkc), -1);
+  for (int i = 0; i < rows; ++i) fill(buf.data() + i, R, i, pkc);
   int rc;
   if ((rc = ensure(c, c->d_pods, sizeof(int32_t) * buf.size()))) return rc;
   HIP_OK(c, hipMemcpyAsync(c->d_pods.p, buf.data(), sizeof(int32_t) * buf.size(), hipMemcpyHostToDevice, c->stream));
@@ -1019,8 +1066,9 @@ int upload_pod_table(kgpu_ctx* c) {
   c->st.pod_flags = reinterpret_cast<uint32_t*>(b + 2 * R);
   c->st.pod_lab = b + 3 * R;
   c->st.Pcap = (int32_t)R;
-  c->st.PKcap = pk;
+  c->st.PKcap = pkc;
   c->pod_rows_dev = rows;
+  c->pod_rows_dirty.clear();
   return KGPU_OK;
 }
 
@@ -1890,6 +1938,50 @@ void drop_nominated(kgpu_ctx* c, int64_t uid) {
           l.end());
 }
 
+// The interned classes / term classes on the device: count columns grown, class tables re-sent when they
+// changed, and the columns of classes new since the last sync counted over the pod table (k_class_init).
+int sync_classes(kgpu_ctx* c) {
+  int rc;
+  if ((rc = grow_columns(c, &c->st.mcnt, &c->Ccap, (int)c->classes.size()))) return rc;
+  if ((rc = grow_columns(c, &c->st.tcnt, &c->TCcap, (int)c->tclasses.size()))) return rc;
+  const kgpu::ClassRec* dcl;
+  const kgpu::ClassItem* dci;
+  const kgpu::TermClassRec* dtc;
+  const kgpu_req* dcr;
+  const int32_t* dcint;
+  // the class tables only grow: re-sent when they changed since the last cycle (upload_pool)
+  auto up = [&](DevBuf& b, const auto& v, auto** d) { return upload_pool(c, b, v.data(), (int32_t)v.size(), d); };
+  if ((rc = up(c->d_classes, c->classes, &dcl)) || (rc = up(c->d_citems, c->citems, &dci)) ||
+      (rc = up(c->d_tclasses, c->tclasses, &dtc)) || (rc = up(c->d_creqs, c->creqs, &dcr)) ||
+      (rc = up(c->d_cints, c->cints, &dcint)))
+    return rc;
+  c->st.classes = dcl;
+  c->st.class_items = dci;
+  c->st.tclasses = dtc;
+  c->st.creqs = dcr;
+  c->st.cints = dcint;
+  if (c->classes_init < (int)c->classes.size()) {
+    // fresh mcnt columns: counted on the device over the pod table (snapshot + assumed pods)
+    c->tc.valid = false;
+    if ((c->pod_rows_dev != (int)c->pod_rows.size() || !c->pod_rows_dirty.empty()) && (rc = upload_pod_table(c)))
+      return rc;
+    if ((rc = ensure(c, c->dstate, sizeof(DevState)))) return rc;
+    c->st_batch = c->st;
+    c->ds_ptr = nullptr;  // the short cycle's cached DevState image is stale
+    HIP_OK(c, hipMemcpyAsync(c->dstate.p, &c->st_batch, sizeof(DevState), hipMemcpyHostToDevice, c->stream));
+    if (kgpu::launch_class_init(static_cast<const DevState*>(c->dstate.p), c->classes_init,
+                                (int)c->classes.size() - c->classes_init, (int)c->pod_rows.size(), c->stream))
+      return fail(c, KGPU_E_DEVICE, "k_class_init launch failed");
+    ++c->n_class_init;
+    if (c->has_alias && (rc = copy_to_aliases(c, c->st.mcnt + (size_t)c->classes_init * c->st.N,
+                                              (int)c->classes.size() - c->classes_init)))
+      return rc;
+    SYNC_OK(c);
+    c->classes_init = (int)c->classes.size();
+  }
+  return KGPU_OK;
+}
+
 // Topology plugins of a batch: plans, class columns, pools (kgpu_internal.h "topology plugins").
 struct Staged {
   std::vector<kgpu::QPlan> plans;
@@ -1908,41 +2000,7 @@ int stage_topology(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_
   if (sg.topo_on) {
     kgpu_pools empty{};
     if ((rc = build_plans(c, qs, n, pools ? pools : &empty, plans, aux, aux_terms, &max_scratch))) return rc;
-    if ((rc = grow_columns(c, &c->st.mcnt, &c->Ccap, (int)c->classes.size()))) return rc;
-    if ((rc = grow_columns(c, &c->st.tcnt, &c->TCcap, (int)c->tclasses.size()))) return rc;
-    const kgpu::ClassRec* dcl;
-    const kgpu::ClassItem* dci;
-    const kgpu::TermClassRec* dtc;
-    const kgpu_req* dcr;
-    const int32_t* dcint;
-    // the class tables only grow: re-sent when they changed since the last cycle (upload_pool)
-    auto up = [&](DevBuf& b, const auto& v, auto** d) { return upload_pool(c, b, v.data(), (int32_t)v.size(), d); };
-    if ((rc = up(c->d_classes, c->classes, &dcl)) || (rc = up(c->d_citems, c->citems, &dci)) ||
-        (rc = up(c->d_tclasses, c->tclasses, &dtc)) || (rc = up(c->d_creqs, c->creqs, &dcr)) ||
-        (rc = up(c->d_cints, c->cints, &dcint)))
-      return rc;
-    c->st.classes = dcl;
-    c->st.class_items = dci;
-    c->st.tclasses = dtc;
-    c->st.creqs = dcr;
-    c->st.cints = dcint;
-    if (c->classes_init < (int)c->classes.size()) {
-      // fresh mcnt columns: counted on the device over the pod table (snapshot + assumed pods)
-      c->tc.valid = false;
-      if (c->pod_rows_dev != (int)c->pod_rows.size() && (rc = upload_pod_table(c))) return rc;
-      if ((rc = ensure(c, c->dstate, sizeof(DevState)))) return rc;
-      c->st_batch = c->st;
-      c->ds_ptr = nullptr;  // the short cycle's cached DevState image is stale
-      HIP_OK(c, hipMemcpyAsync(c->dstate.p, &c->st_batch, sizeof(DevState), hipMemcpyHostToDevice, c->stream));
-      if (kgpu::launch_class_init(static_cast<const DevState*>(c->dstate.p), c->classes_init,
-                                  (int)c->classes.size() - c->classes_init, (int)c->pod_rows.size(), c->stream))
-        return fail(c, KGPU_E_DEVICE, "k_class_init launch failed");
-      if (c->has_alias && (rc = copy_to_aliases(c, c->st.mcnt + (size_t)c->classes_init * c->st.N,
-                                                (int)c->classes.size() - c->classes_init)))
-        return rc;
-      SYNC_OK(c);
-      c->classes_init = (int)c->classes.size();
-    }
+    if ((rc = sync_classes(c))) return rc;
     const kgpu::QPlan* dpl;
     const int32_t* dax;
     const kgpu::TTerm* dat;
@@ -2934,7 +2992,8 @@ int reorder_nodes(kgpu_ctx* c, const kgpu_delta_batch* b) {
     r.node = nn;
     c->pod_rows[sl].node = nn;
   }
-  c->pod_rows_dev = -1;
+  c->pod_rows_dev = -1;  // renumbered rows: the table is rebuilt
+  c->pod_rows_dirty.clear();
   c->row_canon.swap(canon);
   c->alias_rows.clear();
   c->has_alias = false;
@@ -3051,7 +3110,6 @@ int apply_delta(kgpu_ctx* c, const kgpu_delta_batch* b, int32_t* slots) {
   const kgpu_pools& P = b->pools;
   const bool topo = topo_profile(c);
   DeltaBuild db;
-  bool pods_changed = false;
   for (int i = 0; i < b->n_deltas; ++i) {
     const kgpu_delta& d = b->deltas[i];
     if (slots) slots[i] = -1;
@@ -3078,7 +3136,6 @@ int apply_delta(kgpu_ctx* c, const kgpu_delta_batch* b, int32_t* slots) {
     for (int k = 0; k < q.scalars.count; ++k)
       if (P.scalars[q.scalars.begin + k].col >= st.S)
         return fail(c, KGPU_E_INVAL, "pod scalar resource outside the snapshot's scalar columns: re-upload");
-    pods_changed = true;
     if (d.op == KGPU_D_ADD_POD) {
       if (d.node < 0 || d.node >= st.n_total) return fail(c, KGPU_E_INVAL, "ADD_POD on a node outside Snapshot.List()");
       if (c->uid_slot.count(d.uid)) return fail(c, KGPU_E_STATE, "ADD_POD: the pod uid is already on a node");
@@ -3126,10 +3183,10 @@ int apply_delta(kgpu_ctx* c, const kgpu_delta_batch* b, int32_t* slots) {
         for (int32_t r : node_rows(c, local)) pod_op(c, db, kgpu::kDRemovePod, r, d.item, slot);
       rec.active = false;
       c->pod_rows[(size_t)slot].flags &= ~KGPU_PF_ACTIVE;
+      pod_row_dirty(c, slot);
       c->uid_slot.erase(it);
     }
   }
-  if (pods_changed) c->pod_rows_dev = -1;
   return launch_ops(c, db, b->pods, b->n_pods, b->rows, b->n_rows, P.ints, P.n_ints, P.words, P.n_words, P.scalars,
                     P.n_scalars, P.ports, P.n_ports);
 }
@@ -3164,8 +3221,7 @@ int assume_via_delta(kgpu_ctx* c, const kgpu_pod_query& q, const kgpu_pools* poo
   rec.node = mine ? local + c->st.node_base : gnode;
   row.node = rec.node;
   c->recs.push_back(std::move(rec));
-  c->pod_rows.push_back(std::move(row));
-  c->pod_rows_dev = -1;
+  c->pod_rows.push_back(std::move(row));  // appended: the next table sync sends it
   if (!mine) return KGPU_OK;
   int rc;
   if (topo_profile(c) && (rc = grow_columns(c, &c->st.tcnt, &c->TCcap, (int)c->tclasses.size()))) return rc;
@@ -3706,9 +3762,9 @@ int kgpu_read_phase_trace(kgpu_ctx* c, int64_t* out, int32_t max_pods) try {
 
 int kgpu_debug_counters(const kgpu_ctx* c, int64_t* out, int32_t n) {
   if (!c || (n > 0 && !out)) return KGPU_E_INVAL;
-  const int64_t v[3] = {c->n_coop_retry, c->n_persist, c->n_coop};
-  for (int32_t i = 0; i < n && i < 3; ++i) out[i] = v[i];
-  return 3;
+  const int64_t v[5] = {c->n_coop_retry, c->n_persist, c->n_coop, c->n_class_init, c->n_pod_table_full};
+  for (int32_t i = 0; i < n && i < 5; ++i) out[i] = v[i];
+  return 5;
 }
 
 int kgpu_debug_topo_resident(const kgpu_ctx* c, int64_t out[2]) {
@@ -3875,6 +3931,7 @@ int kgpu_upload_snapshot(kgpu_ctx* c, const kgpu_snapshot* s, int64_t generation
   c->classes_init = 0;
   c->pod_rows.clear();
   c->pod_rows_dev = -1;
+  c->pod_rows_dirty.clear();
   for (int i = 0; i < s->n_pods; ++i) {
     kgpu_ctx::PodRec rec;
     rec.node = s->pod_node[i];
@@ -4517,7 +4574,7 @@ int kgpu_forget_pod(kgpu_ctx* c, int32_t slot) try {
   }
   a.active = false;
   c->pod_rows[(size_t)slot].flags &= ~KGPU_PF_ACTIVE;
-  c->pod_rows_dev = -1;
+  pod_row_dirty(c, slot);
   if (a.has_uid) c->uid_slot.erase(a.uid);
   return KGPU_OK;
 } catch (...) {
@@ -4546,6 +4603,29 @@ int kgpu_adopt_pod(kgpu_ctx* c, int32_t slot, int64_t uid) try {
   a.has_uid = true;
   c->uid_slot.emplace(uid, slot);
   return KGPU_OK;
+} catch (...) {
+  return on_exception(c, false);
+}
+
+int kgpu_prepare_pods(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_pools* pools) try {
+  if (c && !c->pipe_q.empty())
+    return fail(c, KGPU_E_STATE, "pipelined batches in flight: complete them with kgpu_schedule_batch_wait first");
+  if (c && c->unsettled) {  // a short cycle returned on its completion word: the stream first
+    const int rs_ = settle(c);
+    if (rs_) return rs_;
+  }
+  if (!c || n < 0 || (n > 0 && !qs)) return KGPU_E_INVAL;
+  if (!c->uploaded) return fail(c, KGPU_E_STATE, "no snapshot uploaded");
+  if (!topo_profile(c) || n == 0) return KGPU_OK;
+  std::vector<kgpu::QPlan> plans;
+  std::vector<int32_t> aux;
+  std::vector<kgpu::TTerm> aux_terms;
+  int64_t scratch = 0;
+  kgpu_pools empty{};
+  int rc = build_plans(c, qs, n, pools ? pools : &empty, plans, aux, aux_terms, &scratch);
+  if (rc == KGPU_E_UNSUPPORTED) return KGPU_OK;  // such a pod's own cycle reports it
+  if (rc) return rc;
+  return sync_classes(c);
 } catch (...) {
   return on_exception(c, false);
 }

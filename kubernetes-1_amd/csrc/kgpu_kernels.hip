@@ -3536,9 +3536,13 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
     uint64_t* srow = ta.gran + (size_t)i * (R + 1) * G;  // [R][G] statistics granules | [G] keys
     // one slot per thread.  Every thread reads its candidate words first -- clamped addresses, one LDS
     // round trip -- and then selects: a switch over the slot puts an LDS read and its wait in each of a
-    // dozen divergent branches, which the wave runs one after another (0.7 us per pod).  (Written out:
-    // the same selection called as a lambda or function, stat_of(tid), published wrong statistics on this
-    // compiler -- profiles/r05_stat_publish_probe.txt.)
+    // dozen divergent branches, which the wave runs one after another (0.7 us per pod).  The selection is
+    // a chain of selects, not an if / else chain: ROCm 7.2's gfx950 backend lowers the if / else chain (a
+    // switch whose default, the zero extension, is reached from both sides of a divergent branch) to code
+    // that never assigns the default's value to the lanes of slots kTDptsMax and kTZoned -- they publish
+    // stale registers.  The LLVM IR is right; the machine code is not (reproducer
+    // tools/repro/stat_select.hip).  Whether it shows depended on the surrounding code: the lambda form
+    // miscompiled inside k_tbatch, the written-out if / else chain did not, both do in the reproducer.
     if (tid < R) {
       const int i32 = tid < 6 ? tid : (tid == kTDptsMax ? 6 : 7);
       const uint32_t w32 = (uint32_t)M.acc32[i32];
@@ -3546,14 +3550,13 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
       const int vi = tid - kTFixed;
       const int voff = vi < 0 ? ta.o_smask : (vi < ta.soft_words ? ta.o_smask + 4 * vi : ta.o_zsum + 4 * (vi - ta.soft_words));
       const int32_t wv = *reinterpret_cast<const int32_t*>(lds_raw + voff);
-      int64_t x;
-      if (tid >= kTFixed) x = vi < ta.soft_words ? (int64_t)(uint32_t)wv : (int64_t)wv;  // SMASK bits / ZSUM
-      else if (tid == kTIpaMin) x = w64 == INT64_MAX ? tident(kOpMin) : w64;
-      else if (tid == kTIpaMax) x = w64 == INT64_MIN ? tident(kOpMax) : w64;
-      else if (tid == kTAdjMin) x = tp.n_soft ? (int64_t)(uint32_t)~w32 : tident(kOpMin);
-      else if (tid == kTAdjMax) x = tp.n_soft ? (int64_t)w32 : tident(kOpMax);
-      else if (tid == kTFeas || tid == kTNonIgn) x = (int32_t)w32;
-      else x = (int64_t)w32;  // kTMaxT, kTMaxNA, kTDptsMax, kTZoned
+      int64_t x = (int64_t)w32;  // kTMaxT, kTMaxNA, kTDptsMax, kTZoned
+      x = (tid == kTFeas || tid == kTNonIgn) ? (int64_t)(int32_t)w32 : x;
+      x = tid == kTAdjMax ? (tp.n_soft ? (int64_t)w32 : tident(kOpMax)) : x;
+      x = tid == kTAdjMin ? (tp.n_soft ? (int64_t)(uint32_t)~w32 : tident(kOpMin)) : x;
+      x = tid == kTIpaMax ? (w64 == INT64_MIN ? tident(kOpMax) : w64) : x;
+      x = tid == kTIpaMin ? (w64 == INT64_MAX ? tident(kOpMin) : w64) : x;
+      x = tid >= kTFixed ? (vi < ta.soft_words ? (int64_t)(uint32_t)wv : (int64_t)wv) : x;  // SMASK bits / ZSUM
       store_sc1(srow + (size_t)tid * G + g, enc_stat(x));
     }
     KGPU_TSTAMP(3);

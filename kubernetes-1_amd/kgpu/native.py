@@ -23,7 +23,7 @@ EXPORTS = ["kgpu_abi_version", "kgpu_struct_sizes", "kgpu_create", "kgpu_destroy
            "kgpu_comm_info",
            "kgpu_debug_fail_alloc", "kgpu_debug_pts_state", "kgpu_debug_ipa_state", "kgpu_debug_broken_linear",
            "kgpu_debug_wg_trace", "kgpu_debug_topo_resident",
-           "kgpu_next_slot", "kgpu_adopt_pod", "kgpu_filter_reasons", "kgpu_debug_counters",
+           "kgpu_next_slot", "kgpu_adopt_pod", "kgpu_prepare_pods", "kgpu_filter_reasons", "kgpu_debug_counters",
            "kgpu_schedule_batch_submit", "kgpu_schedule_batch_wait", "kgpu_pipelined"]
 
 
@@ -75,6 +75,7 @@ def lib():
     L.kgpu_debug_topo_resident.argtypes = [vp, vp]
     L.kgpu_next_slot.argtypes = [vp]
     L.kgpu_adopt_pod.argtypes = [vp, i32, i64]
+    L.kgpu_prepare_pods.argtypes = [vp, vp, i32, vp]
     L.kgpu_select_victims.argtypes = [vp, vp, C.POINTER(abi.Pools), C.POINTER(abi.PreemptArgs), vp, vp,
                                       C.POINTER(i32)]
     L.kgpu_debug_counters.argtypes = [vp, vp, i32]
@@ -280,6 +281,11 @@ class Engine:
         """kgpu_next_slot: the slot the next pod assumed by kgpu_schedule_* gets."""
         return int(lib().kgpu_next_slot(self.h))
 
+    def prepare_pods(self, queries, pools):
+        """kgpu_prepare_pods: intern the topology classes of pods expected soon and count their columns now."""
+        q = np.ascontiguousarray(np.atleast_1d(queries), dtype=abi.QUERY)
+        self._check(lib().kgpu_prepare_pods(self.h, q.ctypes.data, len(q), C.byref(pools)))
+
     def adopt_pod(self, slot, uid):
         """kgpu_adopt_pod: register the UID of a pod the device assumed in a batch (batch-ahead)."""
         self._check(lib().kgpu_adopt_pod(self.h, int(slot), int(uid)))
@@ -301,12 +307,14 @@ class Engine:
         return int(out[0]), int(out[1])
 
     def counters(self):
-        """kgpu_debug_counters: {coop_retries, persistent_launches, coop_launches}."""
+        """kgpu_debug_counters: {coop_retries, persistent_launches, coop_launches, class_inits,
+        pod_table_full_uploads}."""
         out = np.zeros(8, np.int64)
         n = lib().kgpu_debug_counters(self.h, out.ctypes.data, len(out))
         if n < 0:
             self._check(n)
-        return dict(zip(["coop_retries", "persistent_launches", "coop_launches"], [int(x) for x in out[:n]]))
+        return dict(zip(["coop_retries", "persistent_launches", "coop_launches", "class_inits", "pod_table_full_uploads"],
+                        [int(x) for x in out[:n]]))
 
     def broken_linear(self, points, utilizations):
         """kgpu_debug_broken_linear: the device's broken-linear shape function (the one
