@@ -11,7 +11,6 @@
 * PreferNoSchedule taints on one shard only: the OR-exchanged union equals the cluster's, so the
   normalize decision is the same on every rank."""
 import os
-import socket
 
 import numpy as np
 import pytest
@@ -24,12 +23,10 @@ from kgpu.framework import GpuFramework
 COLS = ("alloc_cpu", "alloc_mem", "alloc_eph", "alloc_pods", "req_cpu", "req_mem", "nz_cpu", "nz_mem", "num_pods")
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+def _rendezvous_file():
+    """A fresh path for torch.distributed's FileStore (the file must not exist yet)."""
+    import tempfile
+    return os.path.join(tempfile.mkdtemp(prefix="kgpu_rdv_"), "store")
 
 
 def _workload(name):
@@ -59,8 +56,8 @@ def _rank_main(rank, world, port, name, out):
     n_total_nodes), scored by the C restatement; the ranks exchange their PreferNoSchedule unions,
     normalize maxima and best keys over gloo exactly as kgpu_comm_init / k_shard_pack /
     ncclAllGather do, and the combined winner must be the unsharded scheduleOne's, pod by pod."""
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # a rendezvous file, not a port: a free-port probe can race another process for the port
+    dist.init_process_group("gloo", init_method="file://" + port, rank=rank, world_size=world)
     try:
         import copy
         from kgpu import abi
@@ -142,7 +139,7 @@ def test_shard_combine_gloo_world2(name):
     world = 2
     ctx = mp.get_context("spawn")
     out = ctx.Queue()
-    port = _free_port()
+    port = _rendezvous_file()
     procs = [ctx.Process(target=_rank_main, args=(r, world, port, name, out)) for r in range(world)]
     for p in procs:
         p.start()

@@ -26,7 +26,6 @@ for the world-4 runs, the C restatement (oracle/c) over the whole cluster as wel
 the device's parity anchor, so the combine rule is pinned against both restatements."""
 import copy
 import os
-import socket
 
 import pytest
 import torch.distributed as dist
@@ -35,12 +34,10 @@ import torch.multiprocessing as mp
 from kgpu import cluster
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+def _rendezvous_file():
+    """A fresh path for torch.distributed's FileStore (the file must not exist yet)."""
+    import tempfile
+    return os.path.join(tempfile.mkdtemp(prefix="kgpu_rdv_"), "store")
 
 
 def _workload(name):
@@ -91,8 +88,8 @@ def _sum_maps(parts):
 
 
 def _rank_main(rank, world, port, name, out):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # a rendezvous file, not a port: a free-port probe can race another process for the port
+    dist.init_process_group("gloo", init_method="file://" + port, rank=rank, world_size=world)
     try:
         from oracle.refsched import framework as F
         from oracle.refsched import nodeinfo as NI
@@ -317,7 +314,7 @@ def _rank_main(rank, world, port, name, out):
 def _run(name, world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
+    port = _rendezvous_file()
     procs = [ctx.Process(target=_rank_main, args=(r, world, port, name, q)) for r in range(world)]
     for p in procs:
         p.start()

@@ -5,7 +5,6 @@ fabric differs).  Each rank holds one contiguous shard of Snapshot.List(); the h
 gloo.  Every rank must return the unsharded engine's placements, feasible counts and scores pod
 after pod, and its shard's node rows must equal the unsharded rows after the batches."""
 import os
-import socket
 
 import numpy as np
 import pytest
@@ -18,12 +17,10 @@ from kgpu.framework import GpuFramework
 COLS = ("req_cpu", "req_mem", "req_eph", "nz_cpu", "nz_mem", "num_pods")
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+def _rendezvous_file():
+    """A fresh path for torch.distributed's FileStore (the file must not exist yet)."""
+    import tempfile
+    return os.path.join(tempfile.mkdtemp(prefix="kgpu_rdv_"), "store")
 
 
 def _workload(name):
@@ -52,9 +49,8 @@ def _run(fw, pods, batches):
 
 
 def _rank_main(rank, world, port, name, out):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # a rendezvous file, not a port: a free-port probe can race another process for the port
+    dist.init_process_group("gloo", init_method="file://" + port, rank=rank, world_size=world)
     try:
         nodes, existing, pods, prof = _workload(name)
         fw = GpuFramework(prof, nodes, existing, pods_hint=pods[:16], device=0, shard=(rank, world))
@@ -77,14 +73,20 @@ def test_xgmi_mailbox_two_ranks_one_gpu(name, tmp_path):
     nodes, existing, pods, prof = _workload(name)
     world = 2
     ctx = mp.get_context("spawn")
-    port = _free_port()
+    port = _rendezvous_file()
     outs = [str(tmp_path / ("r%d.npz" % r)) for r in range(world)]
     procs = [ctx.Process(target=_rank_main, args=(r, world, port, name, outs[r])) for r in range(world)]
     for p in procs:
         p.start()
-    for p in procs:
-        p.join(180)
-        assert p.exitcode == 0, "rank exited with %r" % p.exitcode
+    try:
+        for p in procs:
+            p.join(180)
+            assert p.exitcode == 0, "rank exited with %r" % p.exitcode
+    finally:
+        for p in procs:  # a rank left waiting for a dead peer must not outlive the test
+            if p.is_alive():
+                p.kill()
+                p.join(10)
     fw = GpuFramework(prof, nodes, existing, pods_hint=pods[:16], device=0)
     want, rows = _run(fw, pods, 3)
     fw.engine.close()

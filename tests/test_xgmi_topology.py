@@ -12,7 +12,6 @@ equal the unsharded rows of its shard.  The cross-shard semantics under test are
 cluster-wide maps: TpPairToMatchNum / criticalPaths (podtopologyspread/filtering.go:246-270) and the
 inter-pod (anti-)affinity maps (interpodaffinity/filtering.go:166-271) built from every shard."""
 import os
-import socket
 
 import numpy as np
 import pytest
@@ -26,12 +25,10 @@ E_NODES = 20000  # config (e) over two ranks: 10k-node shards (each rank compile
 COLS = ("req_cpu", "req_mem", "req_eph", "nz_cpu", "nz_mem", "num_pods")
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+def _rendezvous_file():
+    """A fresh path for torch.distributed's FileStore (the file must not exist yet)."""
+    import tempfile
+    return os.path.join(tempfile.mkdtemp(prefix="kgpu_rdv_"), "store")
 
 
 def _workload(name):
@@ -60,9 +57,8 @@ def _run(fw, pods, batches):
 
 
 def _rank_main(rank, world, port, name, out):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # a rendezvous file, not a port: a free-port probe can race another process for the port
+    dist.init_process_group("gloo", init_method="file://" + port, rank=rank, world_size=world)
     try:
         if name == "sharded_e":
             # the columnar generator, sliced to this rank's shard, as bench.py runs config (e); the
@@ -94,14 +90,20 @@ def test_xgmi_topology_two_ranks_one_gpu(name, tmp_path):
     nodes, existing, pods, prof = _workload(name)
     world = 2
     ctx = mp.get_context("spawn")
-    port = _free_port()
+    port = _rendezvous_file()
     outs = [str(tmp_path / ("r%d.npz" % r)) for r in range(world)]
     procs = [ctx.Process(target=_rank_main, args=(r, world, port, name, outs[r])) for r in range(world)]
     for p in procs:
         p.start()
-    for p in procs:
-        p.join(240)
-        assert p.exitcode == 0, "rank exited with %r" % p.exitcode
+    try:
+        for p in procs:
+            p.join(240)
+            assert p.exitcode == 0, "rank exited with %r" % p.exitcode
+    finally:
+        for p in procs:  # a rank left waiting for a dead peer must not outlive the test
+            if p.is_alive():
+                p.kill()
+                p.join(10)
     fw = GpuFramework(prof, nodes, existing, pods_hint=pods[:16], device=0)
     q, pc, _, _ = fw.compile_pods(pods)
     ref = RefEngine(fw.config, fw.snap, threads=4).schedule(q, pc)
