@@ -221,7 +221,7 @@ struct kgpu_ctx {
   // KGPU_HOST_TRACE=1 (diagnostics): host time of a short cycle's steps, summed over cycles and printed
   // to stderr by kgpu_destroy (stamp k closes step k)
   bool htrace = false;
-  static constexpr int kHt = 12;
+  static constexpr int kHt = 18;
   int64_t ht_last = 0, ht_cur[kHt] = {}, ht_n = 0;
   int ht_seen = 0;
   std::vector<std::array<int64_t, kHt>> ht_cycles;  // per short cycle: ns of each step (p50 / p99 at destroy)
@@ -413,6 +413,13 @@ int ensure(kgpu_ctx* c, DevBuf& b, size_t bytes) {
   return KGPU_OK;
 }
 
+// ensure() for buffers a cycle sizes from its own pods (plans, scratch, class tables): grown with headroom,
+// so a run of pods that each need a little more does not pay a free + malloc on one cycle after another.
+int ensure_grow(kgpu_ctx* c, DevBuf& b, size_t bytes) {
+  if (b.bytes >= bytes) return KGPU_OK;
+  return ensure(c, b, std::max<size_t>({bytes, 2 * b.bytes, (size_t)64 << 10}));
+}
+
 // ---- short-cycle arena.  A short cycle (kgpu_schedule_one, small batches) stages what it must send
 // -- changed query pools, topology plans, DevState + queries, a one-pod persistent topology run's
 // tables and zeroed words -- in the pinned block c->cyc_host, at the offsets they take in the device
@@ -512,7 +519,7 @@ struct ArenaScope {
 
 template <class T>
 int upload_pool(kgpu_ctx* c, DevBuf& b, const T* src, int32_t n, const T** dst) {
-  int rc = ensure(c, b, sizeof(T) * (size_t)std::max(n, 1));
+  int rc = ensure_grow(c, b, sizeof(T) * (size_t)std::max(n, 1));
   if (rc) return rc;
   const size_t bytes = sizeof(T) * (size_t)std::max(n, 0);
   // A caller that passes the same pools every cycle (the batch's pools, one pod at a time) pays
@@ -584,7 +591,7 @@ int upload_pools(kgpu_ctx* c, const kgpu_pools* p, bool zero_copy = false) {
   put(o_sc, p->scalars, nb(p->n_scalars, sizeof(kgpu_scalar_req)));
   put(o_po, p->ports, nb(p->n_ports, sizeof(kgpu_port)));
   int rc;
-  if ((rc = ensure(c, c->pool_blk, total))) return rc;
+  if ((rc = ensure_grow(c, c->pool_blk, total))) return rc;
   const bool current = c->pool_blk.shadow_p == c->pool_blk.p && c->pool_blk.shadow.size() == total &&
                        std::memcmp(c->pool_blk.shadow.data(), h, total) == 0;
   const char* d = static_cast<const char*>(c->pool_blk.p);
@@ -1079,7 +1086,7 @@ int upload_vec(kgpu_ctx* c, DevBuf& b, const std::vector<T>& v, const T** dst) {
       *dst = static_cast<const T*>(a);
       return KGPU_OK;
     }
-  int rc = ensure(c, b, sizeof(T) * std::max<size_t>(v.size(), 1));
+  int rc = ensure_grow(c, b, sizeof(T) * std::max<size_t>(v.size(), 1));
   if (rc) return rc;
   if (!v.empty()) HIP_OK(c, hipMemcpyAsync(b.p, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice, c->stream));
   *dst = static_cast<const T*>(b.p);
@@ -1944,6 +1951,7 @@ int sync_classes(kgpu_ctx* c) {
   int rc;
   if ((rc = grow_columns(c, &c->st.mcnt, &c->Ccap, (int)c->classes.size()))) return rc;
   if ((rc = grow_columns(c, &c->st.tcnt, &c->TCcap, (int)c->tclasses.size()))) return rc;
+  ht(c, 15);
   const kgpu::ClassRec* dcl;
   const kgpu::ClassItem* dci;
   const kgpu::TermClassRec* dtc;
@@ -1960,6 +1968,7 @@ int sync_classes(kgpu_ctx* c) {
   c->st.tclasses = dtc;
   c->st.creqs = dcr;
   c->st.cints = dcint;
+  ht(c, 16);
   if (c->classes_init < (int)c->classes.size()) {
     // fresh mcnt columns: counted on the device over the pod table (snapshot + assumed pods)
     c->tc.valid = false;
@@ -1979,6 +1988,7 @@ int sync_classes(kgpu_ctx* c) {
     SYNC_OK(c);
     c->classes_init = (int)c->classes.size();
   }
+  ht(c, 17);
   return KGPU_OK;
 }
 
@@ -2000,7 +2010,9 @@ int stage_topology(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_
   if (sg.topo_on) {
     kgpu_pools empty{};
     if ((rc = build_plans(c, qs, n, pools ? pools : &empty, plans, aux, aux_terms, &max_scratch))) return rc;
+    ht(c, 12);  // (host trace: topology staging split into 12, 13, 14 and the rest in 1)
     if ((rc = sync_classes(c))) return rc;
+    ht(c, 13);
     const kgpu::QPlan* dpl;
     const int32_t* dax;
     const kgpu::TTerm* dat;
@@ -2010,7 +2022,8 @@ int stage_topology(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_
     c->st.plans = dpl;
     c->st.aux = dax;
     c->st.aux_terms = dat;
-    if ((rc = ensure(c, c->scratch, sizeof(int64_t) * (size_t)std::max<int64_t>(max_scratch, 1)))) return rc;
+    ht(c, 14);
+    if ((rc = ensure_grow(c, c->scratch, sizeof(int64_t) * (size_t)std::max<int64_t>(max_scratch, 1)))) return rc;
     c->st.scratch = static_cast<int64_t*>(c->scratch.p);
   } else {
     c->st.plans = nullptr;
@@ -3661,7 +3674,9 @@ int kgpu_destroy(kgpu_ctx* c) try {
   if (c->htrace) {
     static const char* names[kgpu_ctx::kHt] = {"", "topology staging", "ports+pools", "state staged+geometry",
                                                "tables planned", "tables staged+key", "copy API", "launch API",
-                                               "to end of issue", "synchronize", "records+bookkeeping", "record landed"};
+                                               "to end of issue", "synchronize", "records+bookkeeping", "record landed",
+                                               "  topo: plans built", "  topo: classes synced", "  topo: plans staged",
+                                               "    classes: columns", "    classes: tables", "    classes: counted"};
     // p50 and p99 of each step, and of the whole call, over the short cycles and over the longer calls
     auto pct = [](std::vector<int64_t> v, double q) {
       const size_t i = std::min(v.size() - 1, (size_t)(q * (double)(v.size() - 1) + 0.5));
@@ -4625,6 +4640,9 @@ int kgpu_prepare_pods(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kg
   int rc = build_plans(c, qs, n, pools ? pools : &empty, plans, aux, aux_terms, &scratch);
   if (rc == KGPU_E_UNSUPPORTED) return KGPU_OK;  // such a pod's own cycle reports it
   if (rc) return rc;
+  // the device scratch their plans need, allocated now rather than on a cycle
+  if ((rc = ensure_grow(c, c->scratch, sizeof(int64_t) * (size_t)std::max<int64_t>(scratch, 1)))) return rc;
+  c->st.scratch = static_cast<int64_t*>(c->scratch.p);
   return sync_classes(c);
 } catch (...) {
   return on_exception(c, false);
