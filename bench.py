@@ -96,7 +96,7 @@ def _object_workload(cfg, n_nodes, n_pods):
 def pmc_traffic(cfg, n_local, launch_pods, kname):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3 --pmc passes of this
     exact workload (the newest profiles/r*_pmc_traffic.json holding it; tools/pmc_summary.py), or None."""
-    for fname in ("r05_pmc_traffic.json", "r04_pmc_traffic.json", "r03_pmc_traffic.json", "r02_pmc_traffic.json", "r01_pmc_traffic.json"):
+    for fname in ("r06_pmc_traffic.json", "r05_pmc_traffic.json", "r04_pmc_traffic.json", "r03_pmc_traffic.json", "r02_pmc_traffic.json", "r01_pmc_traffic.json"):
         try:
             with open(os.path.join(ROOT, "profiles", fname)) as fh:
                 pmc = json.load(fh).get("%s:%d:%d" % (cfg, n_local, launch_pods))
