@@ -878,12 +878,14 @@ __device__ __forceinline__ void resolve_tail(const DevState& st, const PodArgs& 
   if (a.done_out) __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
   if (threadIdx.x == 0) {
-    __threadfence();
+    // release: this workgroup's partial (and rows) written back before its ticket -- no invalidate here
+    // (a full __threadfence() adds a buffer_inv whose wait every workgroup paid before its ticket)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     last = atomicAdd(st.ticket, 1) == (int)gridDim.x - 1;
   }
   __syncthreads();
   if (last) {
-    __threadfence();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // every other workgroup's partial
     PodArgs r{};
     r.prev = a.pod;
     r.prev_blocks = (int32_t)gridDim.x;
@@ -905,10 +907,8 @@ __device__ __forceinline__ void resolve_tail(const DevState& st, const PodArgs& 
     if (a.done_out) {
       __builtin_amdgcn_s_waitcnt(0);  // the record, the assume and the last workgroup's rows in L2 ...
       __syncthreads();
-      if (threadIdx.x == 0) {
-        __threadfence();  // ... written back, then the completion word
+      if (threadIdx.x == 0)  // ... written back by the store's own system-scope release, then the word
         __hip_atomic_store(a.done_out, 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-      }
     }
   }
 }
@@ -3256,11 +3256,12 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
       __syncthreads();
     }
     if (ta.abort_out && tid == 0) {
-      __threadfence();
-      if (atomicAdd(ta.done, 1) == G - 1) {
-        __threadfence();
-        __hip_atomic_store(ta.abort_out, load_sc1(ta.abort), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      }
+      // release only (a full __threadfence() adds an L1 invalidate whose wait every workgroup paid): the last
+      // workgroup reads nothing the others wrote but the abort word (an sc1 load), and its completion store
+      // carries its own system-scope release
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      if (atomicAdd(ta.done, 1) == G - 1)
+        __hip_atomic_store(ta.abort_out, load_sc1(ta.abort), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   };
   if (g == ta.hold) {  // KGPU_OPT_HOLD_GROUP: a workgroup that never became resident
