@@ -19,6 +19,7 @@ package gpueval
 
 /*
 #include "kgpu.h"
+#include "kgpu_compile.h"
 */
 import "C"
 

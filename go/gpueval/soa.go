@@ -13,6 +13,7 @@ package gpueval
 
 /*
 #include "kgpu.h"
+#include "kgpu_compile.h"
 */
 import "C"
 
