@@ -226,3 +226,86 @@ def test_no_duplicate_package_level_declarations():
                 dup.append("%s (%s, %s)" % (".".join(k for k in key if k), seen[key], f))
             seen.setdefault(key, f)
     assert not dup, dup
+
+
+@pytest.mark.parametrize("fname", _go_files())
+def test_every_import_is_used(fname):
+    """An imported package no code of the file names is a Go compile error."""
+    src = _strip_go(open(os.path.join(GO, fname)).read())
+    imports = []
+    for block in re.findall(r"^import\s*\((.*?)\)", src, flags=re.M | re.S):
+        imports += re.findall(r"^\s*(\w+\s+)?\"([^\"]+)\"", block, flags=re.M)
+    imports += re.findall(r"^import\s+(\w+\s+)?\"([^\"]+)\"", src, flags=re.M)
+    body = re.sub(r"^import\s*\(.*?\)", "", src, flags=re.M | re.S)
+    body = re.sub(r"^import\s+[^\n]*", "", body, flags=re.M)
+    unused = []
+    for alias, path in imports:
+        name = alias.strip() if alias else path.rsplit("/", 1)[-1]
+        if path == "C" or name in ("_", "."):
+            continue
+        if not re.search(r"\b%s\." % re.escape(name), body):
+            unused.append(path)
+    assert not unused, "%s imports packages it never names: %s" % (fname, unused)
+
+
+GO_BUILTINS = {"len", "cap", "append", "make", "new", "copy", "delete", "panic", "recover", "print", "println",
+               "close", "complex", "real", "imag"}  # go 1.13: no min / max / clear
+
+
+def _package_names():
+    funcs, methods, fields, types = set(), set(), set(), set()
+    for f in _go_files():
+        src = _strip_go(open(os.path.join(GO, f)).read())
+        for m in re.finditer(r"^func\s+(\(\s*\w*\s*\*?\s*\w+\s*\)\s*)?(\w+)\s*\(", src, flags=re.M):
+            (methods if m.group(1) else funcs).add(m.group(2))
+        types |= set(re.findall(r"^type\s+(\w+)\s", src, flags=re.M))
+        for body in re.findall(r"\bstruct\s*\{(.*?)^\}", src, flags=re.M | re.S):
+            fields |= set(re.findall(r"^\s*(\w+)\s+func\b", body, flags=re.M))
+    return funcs, methods, fields, types
+
+
+def test_unexported_calls_resolve_in_the_package():
+    """A call of an unexported name -- x.name(...) or name(...) -- must resolve to this package's methods,
+    functions or func-typed fields, a local closure, or a go 1.13 builtin (no min / max)."""
+    funcs, methods, fields, types = _package_names()
+    bad = []
+    for f in _go_files():
+        src = _strip_go(open(os.path.join(GO, f)).read())
+        src = re.sub(r'"(\\.|[^"\\])*"|`[^`]*`', '""', src)
+        # local closures and func-typed variables / parameters: name := func / name = func / name func(
+        local = set(re.findall(r"\b(\w+)\s*:?=\s*func\b", src)) | set(re.findall(r"\b(\w+)\s+func\s*\(", src))
+        for m in re.finditer(r"(\bC\.|\.)?\b([a-z]\w*)\s*\(", src):
+            sel, name = m.group(1), m.group(2)
+            if sel == "C.":
+                continue  # cgo: checked against the headers above
+            if name in ("func", "if", "for", "switch", "return", "go", "defer", "range", "select", "case", "interface",
+                        "struct", "map", "chan", "type", "var", "const", "import"):
+                continue
+            if sel:
+                if name not in methods and name not in fields and name not in local:
+                    bad.append("%s: .%s(" % (f, name))
+            else:
+                pre = src[max(0, m.start() - 6):m.start()]
+                if re.search(r"func\s*$", pre) or re.search(r"\)\s*$", pre):
+                    continue  # a declaration, or a method value / type conversion context
+                if name not in GO_BUILTINS and name not in funcs and name not in local and name not in types \
+                        and name not in methods and not re.match(r"^(u?int(8|16|32|64)?|float(32|64)|byte|rune|string|"
+                                                                 r"bool|uintptr|error)$", name):
+                    bad.append("%s: %s(" % (f, name))
+    assert not bad, sorted(set(bad))
+
+
+# APIs newer than the reference module's go 1.13 (go.mod `go 1.13`)
+POST_113 = [r"\bunsafe\.(Slice|String|StringData|SliceData|Add)\b", r"\bany\b", r"\bstrings\.(Cut|Clone|CutPrefix)\b",
+            r"\bbytes\.Cut\b", r"\bos\.(ReadFile|WriteFile|ReadDir)\b", r"\bio\.(ReadAll|Discard|NopCloser)\b",
+            r"\bmath\.(MaxInt|MinInt|MaxUint)\b", r"\batomic\.(Int32|Int64|Uint32|Uint64|Bool|Pointer|Value)\b\s*[{)]",
+            r"\bfunc\s+\w+\s*\[", r"\btype\s+\w+\s*\[\s*\w+\s+(any|comparable|interface)", r"\bslices\.", r"\bmaps\.",
+            r"\berrors\.Join\b", r"\bcontext\.(WithoutCancel|AfterFunc|Cause)\b", r"\bsync\.OnceValue"]
+
+
+@pytest.mark.parametrize("fname", _go_files())
+def test_go_113_only(fname):
+    src = _strip_go(open(os.path.join(GO, fname)).read())
+    src = re.sub(r'"(\\.|[^"\\])*"|`[^`]*`', '""', src)
+    hits = [p for p in POST_113 if re.search(p, src)]
+    assert not hits, "%s uses APIs newer than go 1.13: %s" % (fname, hits)
