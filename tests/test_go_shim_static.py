@@ -309,3 +309,46 @@ def test_go_113_only(fname):
     src = re.sub(r'"(\\.|[^"\\])*"|`[^`]*`', '""', src)
     hits = [p for p in POST_113 if re.search(p, src)]
     assert not hits, "%s uses APIs newer than go 1.13: %s" % (fname, hits)
+
+
+# The v1alpha1 plugin interfaces the shim implements (framework/v1alpha1/interface.go:209-367), as
+# (parameter types, result types) with the package qualifier the shim imports the framework under.
+PLUGIN_API = {
+    "Name": ([], "string"),                                                                     # :209
+    "PreFilter": (["context.Context", "*framework.CycleState", "*v1.Pod"], "*framework.Status"),  # :242
+    "PreFilterExtensions": ([], "framework.PreFilterExtensions"),                               # :249
+    "Filter": (["context.Context", "*framework.CycleState", "*v1.Pod", "*framework.NodeInfo"],
+               "*framework.Status"),                                                            # :273
+    "Score": (["context.Context", "*framework.CycleState", "*v1.Pod", "string"],
+              "(int64, *framework.Status)"),                                                    # :320
+    "ScoreExtensions": ([], "framework.ScoreExtensions"),                                       # :323
+    "Reserve": (["context.Context", "*framework.CycleState", "*v1.Pod", "string"], "*framework.Status"),  # :336
+    "Unreserve": (["context.Context", "*framework.CycleState", "*v1.Pod", "string"], ""),         # :367
+}
+
+
+def _method_sigs(recv):
+    out = {}
+    for f in _go_files():
+        src = _strip_go(open(os.path.join(GO, f)).read())
+        for m in re.finditer(r"^func\s+\(\s*\w+\s+\*%s\s*\)\s*(\w+)\s*\(([^)]*)\)\s*([^{]*)\{" % recv, src, flags=re.M):
+            params = []
+            for part in [p.strip() for p in m.group(2).split(",") if p.strip()]:
+                toks = part.split()
+                params.append(toks[-1])
+            # "a, b int" style groups: a bare name takes the next typed parameter's type
+            typed = [p if p[0] in "*[" or "." in p or p in ("string", "int64", "int32", "int", "bool") else None
+                     for p in params]
+            for i in range(len(typed) - 1, -1, -1):
+                if typed[i] is None:
+                    typed[i] = typed[i + 1]
+            out[m.group(1)] = (typed, " ".join(m.group(3).split()))
+    return out
+
+
+@pytest.mark.parametrize("recv,methods", [("GpuEval", list(PLUGIN_API)), ("GpuScore", ["Name", "Score", "ScoreExtensions"])])
+def test_plugin_methods_match_the_v1alpha1_interfaces(recv, methods):
+    sigs = _method_sigs(recv)
+    for name in methods:
+        assert name in sigs, "%s lacks %s" % (recv, name)
+        assert sigs[name] == (PLUGIN_API[name][0], PLUGIN_API[name][1]), (recv, name, sigs[name])
