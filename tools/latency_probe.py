@@ -1,4 +1,5 @@
-"""Per-call latency of kgpu_schedule_one (the drop-in plugin's per-cycle call) on configs (b), (c), (d).
+"""Per-call latency of kgpu_schedule_one (the drop-in plugin's per-cycle call) on configs (b), (c), (d), and
+"t" = (c) without its spread constraints (tolerations and node-affinity terms in the pools, one k_eval launch).
 
 Run under `rocprofv3 --hip-trace --kernel-trace --stats` to see where a call's time goes
 (API calls, copies, launches, synchronisation)."""
@@ -22,11 +23,15 @@ def main():
     ap.add_argument("--prepare", type=int, default=1,
                     help="1: kgpu_prepare_pods over the measured pods first (the drop-in registers its queue's pod "
                          "classes at upload); 0: each class is met on its first cycle")
+    ap.add_argument("--per-pod-pools", type=int, default=0,
+                    help="1: every pod compiled on its own, with its own pools block (the Go shim's shape)")
     args = ap.parse_args()
     from kgpu import cluster
     from kgpu.framework import GpuFramework
     if args.config == "b":
         nodes, existing, pods, prof = cluster.fit_least_balanced(n_nodes=args.nodes, n_pods=args.pods)
+    elif args.config == "t":  # (c) without the spread constraints: taints, tolerations, node affinity (k_eval)
+        nodes, existing, pods, prof = cluster.taints_affinity_spread(n_nodes=args.nodes, n_pods=args.pods, spread=False)
     elif args.config == "c":
         nodes, existing, pods, prof = cluster.taints_affinity_spread(n_nodes=args.nodes, n_pods=args.pods)
     else:
@@ -43,13 +48,16 @@ def main():
     if args.prepare:
         eng.prepare_pods(q, pc)
     lat = []
+    own = [fw.compile_pods([p])[:2] for p in pods] if args.per_pod_pools else None
     for i in range(len(q)):
+        qi, pci = (own[i][0][0], own[i][1]) if own else (q[i], pc)
         t = time.perf_counter()
-        eng.schedule_one(q[i], pc, seq=i, assume=True)
+        eng.schedule_one(qi, pci, seq=i, assume=True)
         lat.append((time.perf_counter() - t) * 1e6)
     la = np.array(lat)
-    print("kgpu_schedule_one config %s %d nodes%s: p50 %.1f us, p99 %.1f us, mean %.1f us"
-          % (args.config, args.nodes, " (classes prepared)" if args.prepare else "", np.percentile(la, 50),
+    print("kgpu_schedule_one config %s %d nodes%s%s: p50 %.1f us, p99 %.1f us, mean %.1f us"
+          % (args.config, args.nodes, " (classes prepared)" if args.prepare else "",
+             " (per-pod pools)" if args.per_pod_pools else "", np.percentile(la, 50),
              np.percentile(la, 99), la.mean()))
     eng.close()
 
