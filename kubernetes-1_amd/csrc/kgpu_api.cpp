@@ -2125,9 +2125,9 @@ int run_batch_once(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_
     if ((rc = stage_h2d(c, c->queries.p, qs, sizeof(kgpu_pod_query) * (size_t)n))) return rc;
     if ((rc = ensure(c, c->results, sizeof(kgpu_result) * (size_t)n))) return rc;
   }
-  if (!c->ticket.p) {
-    if ((rc = ensure(c, c->ticket, 64))) return rc;
-    HIP_OK(c, hipMemset(c->ticket.p, 0, 64));
+  if (!c->ticket.p) {  // resolve_tail's counters: the top one and 8 group counters, a 64-byte line each
+    if ((rc = ensure(c, c->ticket, 9 * 64))) return rc;
+    HIP_OK(c, hipMemset(c->ticket.p, 0, 9 * 64));
   }
   DevState st = c->st;
   st.ticket = static_cast<int32_t*>(c->ticket.p);
@@ -3324,9 +3324,9 @@ int pipe_submit(kgpu_ctx* c, const kgpu_pod_query* qs, int32_t n, const kgpu_poo
   if (kidx < 0) return fail(c, KGPU_E_UNSUPPORTED, "no persistent geometry for this node count");
   // the pools ride on the stream like every other copy (ordered after the batch in flight)
   if ((rc = upload_pools(c, pools))) return rc;
-  if (!c->ticket.p) {
-    if ((rc = ensure(c, c->ticket, 64))) return rc;
-    HIP_OK(c, hipMemset(c->ticket.p, 0, 64));
+  if (!c->ticket.p) {  // resolve_tail's counters: the top one and 8 group counters, a 64-byte line each
+    if ((rc = ensure(c, c->ticket, 9 * 64))) return rc;
+    HIP_OK(c, hipMemset(c->ticket.p, 0, 9 * 64));
   }
   const int s = c->pipe_next;
   c->pipe_next ^= 1;

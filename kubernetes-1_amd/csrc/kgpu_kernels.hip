@@ -870,6 +870,8 @@ __device__ __forceinline__ void chunk_of(int N, int& lo, int& hi) {
 // the assume -- in place of a k_resolve launch (PodArgs.resolve_self: the end of a short cycle, after
 // k_final, or after k_eval when the pod needs no normalize pass).  Release / acquire fences around the
 // ticket make every workgroup's partial visible to it across XCDs.
+constexpr int kTicketSplit = 128;  // grids this large count their tickets in 8 groups (resolve_tail)
+constexpr int kTicketLine = 16;    // int32 words between ticket counters (64-byte lines; 9 counters)
 __device__ __forceinline__ void resolve_tail(const DevState& st, const PodArgs& a) {
   __shared__ int last;
   // a cycle the host completes on done_out: every wave's stores (the diagnostic rows included) reach L2
@@ -881,7 +883,24 @@ __device__ __forceinline__ void resolve_tail(const DevState& st, const PodArgs& 
     // release: this workgroup's partial (and rows) written back before its ticket -- no invalidate here
     // (a full __threadfence() adds a buffer_inv whose wait every workgroup paid before its ticket)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    last = atomicAdd(st.ticket, 1) == (int)gridDim.x - 1;
+    const int G = (int)gridDim.x;
+    if (G < kTicketSplit) {
+      last = atomicAdd(st.ticket, 1) == G - 1;
+    } else {
+      // many workgroups finish together: arrivals on one device-scope counter serialize (~12 ns each,
+      // MI355X_MICROARCH.md fanin), so they count on 8 group counters (blockIdx mod 8, one line each) and
+      // each group's last arriver carries the group on to the top counter -- acquire its members' partials,
+      // release them with its own ticket
+      const int grp = (int)blockIdx.x & 7;
+      int32_t* sub = st.ticket + kTicketLine * (grp + 1);
+      last = 0;
+      if (atomicAdd(sub, 1) == ((G - grp + 7) >> 3) - 1) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        __hip_atomic_store(sub, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // for the next cycle
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        last = atomicAdd(st.ticket, 1) == 7;
+      }
+    }
   }
   __syncthreads();
   if (last) {

@@ -17,6 +17,8 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GO = os.path.join(ROOT, "go", "gpueval")
 INC = os.path.join(ROOT, "include")
+if not os.path.isdir(GO):  # the GPU box's copy of the tree leaves go/ out (.gpurunignore): CPU-only checks
+    pytest.skip("go/gpueval is not in this copy of the tree", allow_module_level=True)
 
 CGO_BUILTINS = {"CString", "GoString", "GoStringN", "GoBytes", "CBytes"}
 C_SCALARS = {"char", "schar", "uchar", "short", "ushort", "int", "uint", "long", "ulong", "longlong", "ulonglong",
