@@ -170,11 +170,24 @@ class Engine:
         return int(lib().kgpu_pipelined(self.h))
 
     def schedule_one(self, query, pools, seq=0, assume=True):
-        q = np.ascontiguousarray(np.atleast_1d(query), dtype=abi.QUERY)
+        # the per-cycle call: a record taken from a query array (np.void) is copied as bytes into a buffer
+        # whose address is known (an array's .ctypes.data costs microseconds per access); libkgpu copies
+        # the query before it returns, so the buffer is reused
+        one = self.__dict__.get("_one")
+        if one is None:
+            q1 = np.zeros(1, abi.QUERY)
+            slot = C.c_int32(-1)
+            one = self._one = (q1, q1.ctypes.data, slot, C.byref(slot))
+        q1, qp, slot, slotp = one
+        if isinstance(query, np.void) and query.dtype == abi.QUERY:
+            C.memmove(qp, query.tobytes(), abi.QUERY.itemsize)
+        else:
+            q = np.ascontiguousarray(np.atleast_1d(query), dtype=abi.QUERY)
+            C.memmove(qp, q.ctypes.data, abi.QUERY.itemsize)
         res = np.zeros(1, abi.RESULT)
-        slot = C.c_int32(-1)
-        self._check(lib().kgpu_schedule_one(self.h, q.ctypes.data, C.byref(pools), seq, 1 if assume else 0,
-                                            res.ctypes.data, C.byref(slot)))
+        slot.value = -1
+        self._check(lib().kgpu_schedule_one(self.h, qp, C.byref(pools), seq, 1 if assume else 0,
+                                            res.ctypes.data, slotp))
         return res[0], slot.value
 
     def filter_words(self, n):
