@@ -1529,7 +1529,10 @@ bool t_add(TRun& tr, const kgpu_ctx* c, const kgpu_pod_query& q, const kgpu::QPl
 }
 
 // Histogram deltas of every planned pod (the run's histograms over the columns it increments),
-// then the distinct plans: pods of one template share one plan record.
+// then the distinct plans: pods of one template share one plan record.  One delta per occurrence of the
+// column in the pod's list: the assume increments the column once per entry (a pod whose affinity terms
+// repeat one term counts it once per term, as processExistingPod does), and the run's histogram must move
+// by as much (round 6: one delta per column left the in-run histogram 1 short after such a pod).
 void t_finish(TRun& tr) {
   std::map<std::string, int> ids;
   std::vector<kgpu::TPlan> uniq;
@@ -1549,7 +1552,6 @@ void t_finish(TRun& tr) {
           d.key = hh.key;
           d.sig = hh.sig;
           ds.push_back(d);
-          break;
         }
     }
     tp.deltas = tr.deltas.add(ds);

@@ -3907,8 +3907,9 @@ __global__ __launch_bounds__(B) void k_tbatch(const DevState* __restrict__ stp, 
         const TDelta dl = cp(ta.deltas)[tp.deltas.begin + d];
         if (dl.sig >= 0 && !M.welig[dl.sig]) continue;
         const int v = dl.key >= 0 ? M.wlab[dl.key] : -1;
-        if (dl.off >= 0) H[dl.off + (v >= 0 ? v : dl.D)] += 1;
-        if (v >= 0) TOT[dl.hist] += 1;
+        // LDS atomics: a pod whose terms repeat one term carries one delta per term, on the same words
+        if (dl.off >= 0) atomicAdd(&H[dl.off + (v >= 0 ? v : dl.D)], 1);
+        if (v >= 0) atomicAdd(&TOT[dl.hist], 1);
       }
       if (M.wg == g) {
         const int local = wl - lo;

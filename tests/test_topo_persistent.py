@@ -141,3 +141,15 @@ def test_rank40_inverse_constants():
         x = (x * I1) & M
         x ^= k & M
         assert x == idx
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ahead", [0, 1])
+def test_gpu_tbatch_repeated_affinity_terms(ahead):
+    """A pod with two identical required podAffinity terms (seed 20359's pod 18) is assumed inside the run; a
+    later pod (24) that the terms match scores them once per term (processExistingPod).  The run's histogram
+    delta used to be applied once per column, so pod 24's InterPodAffinity score came out 1 high
+    (tools/stress_parity.py found it; 1000701 against oracle/c's 1000700)."""
+    fw, w, got, rw, rg = _run(gen_random.topo_cluster(20359, n_nodes=16, n_existing=24, n_pods=30), tfast=1,
+                              ahead=ahead)
+    _check(w, got, rw, rg)

@@ -89,13 +89,15 @@ def main():
         ("generic 20 nodes", lambda s: gen_random.cluster(s, n_nodes=20, n_existing=15, n_pods=30)),
         ("generic 700 nodes", lambda s: gen_random.cluster(s, n_nodes=700, n_existing=400, n_pods=60)),
         ("generic 5000 nodes", lambda s: gen_random.cluster(s, n_nodes=5000, n_existing=2000, n_pods=40)),
+        # 141 one-pod workgroups: resolve_tail's grouped tickets (uneven groups)
+        ("generic 9000 nodes", lambda s: gen_random.cluster(s, n_nodes=9000, n_existing=3000, n_pods=30)),
         ("topology 16 nodes", lambda s: gen_random.topo_cluster(s, n_nodes=16, n_existing=24, n_pods=30)),
         ("topology 1500 nodes", lambda s: gen_random.topo_cluster(s, n_nodes=1500, n_existing=600, n_pods=60)),
         ("topology 6000 nodes", lambda s: gen_random.topo_cluster(s, n_nodes=6000, n_existing=3000, n_pods=40)),
     ]
     out = []
     for tag, make in fams:
-        n = len(seeds) if "5000" not in tag and "6000" not in tag else max(4, len(seeds) // 5)
+        n = len(seeds) if not any(k in tag for k in ("5000", "6000", "9000")) else max(4, len(seeds) // 5)
         out.append(run_family(tag, make, seeds[:n], a.one_pod_every))
     print(json.dumps({"stress_parity": "ok", "families": out}))
 
