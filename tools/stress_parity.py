@@ -36,8 +36,24 @@ def _compare(tag, seed, want, got, rows_w=None, rows_g=None):
                 raise AssertionError("%s seed %d: node rows %s differ" % (tag, seed, k))
 
 
-def run_family(tag, make, seeds, one_pod_every):
-    from kgpu.compile import Cluster, Profile
+def make_profile(variant):
+    """The scheduler profile a sweep runs under (--variant): the default, or one setting changed."""
+    from kgpu.compile import Profile
+    if variant == "pct":  # percentageOfNodesToScore: numFeasibleNodesToFind and nextStartNodeIndex (k_cut)
+        return Profile(percentage_of_nodes_to_score=40)
+    if variant == "hpaw":  # InterPodAffinity's hardPodAffinityWeight
+        return Profile(hard_pod_affinity_weight=5)
+    if variant == "tie1":  # the first-max tie-break mode
+        return Profile(tie_break_mode=1)
+    if variant == "most":  # MostAllocated, RequestedToCapacityRatio and ResourceLimits in the score set
+        scores = [s for s in Profile.DEFAULT_SCORES if s[0] != "NodeResourcesLeastAllocated"]
+        return Profile(scores=scores + [("NodeResourcesMostAllocated", 1), ("RequestedToCapacityRatio", 2),
+                                        ("NodeResourceLimits", 1)])
+    return Profile()
+
+
+def run_family(tag, make, seeds, one_pod_every, variant="default"):
+    from kgpu.compile import Cluster
     from kgpu.framework import GpuFramework
     from oracle.cref import RefEngine
     pods_total = 0
@@ -48,7 +64,7 @@ def run_family(tag, make, seeds, one_pod_every):
         cl = Cluster(services=spec[3], rss=spec[4]) if len(spec) > 3 else None
         kw = {"cluster": cl} if cl is not None else {}
         # batch path
-        fw = GpuFramework(Profile(), nodes, ex, pods_hint=pods, **kw)
+        fw = GpuFramework(make_profile(variant), nodes, ex, pods_hint=pods, **kw)
         q, pc, _, errs = fw.compile_pods(pods)
         assert not errs, errs
         ref = RefEngine(fw.config, fw.snap, threads=8)
@@ -59,7 +75,7 @@ def run_family(tag, make, seeds, one_pod_every):
         pods_total += len(pods)
         # drop-in path: one kgpu_schedule_one per pod, each with its own pools (the Go shim's shape)
         if one_pod_every and s % one_pod_every == 0:
-            fw = GpuFramework(Profile(), nodes, ex, pods_hint=pods, **kw)
+            fw = GpuFramework(make_profile(variant), nodes, ex, pods_hint=pods, **kw)
             got1 = {f: [] for f in FIELDS}
             for i, pod in enumerate(pods):
                 qi, pci, _, errs = fw.compile_pods([pod])
@@ -72,7 +88,8 @@ def run_family(tag, make, seeds, one_pod_every):
         if hasattr(ref, "close"):
             ref.close()
         print("  %s seed %d: %d pods ok" % (tag, s, len(pods)), flush=True)  # progress (the box's silence limit)
-    line = {"family": tag, "clusters": len(seeds), "pods": pods_total, "seconds": round(time.time() - t0, 1)}
+    line = {"family": tag, "variant": variant, "clusters": len(seeds), "pods": pods_total,
+            "seconds": round(time.time() - t0, 1)}
     print(json.dumps(line), flush=True)
     return line
 
@@ -82,6 +99,8 @@ def main():
     ap.add_argument("--seeds", type=int, default=40)
     ap.add_argument("--start", type=int, default=1000, help="first seed (the test suite uses small seeds)")
     ap.add_argument("--one-pod-every", type=int, default=4, help="also run every k-th cluster one pod at a time")
+    ap.add_argument("--variant", default="default", choices=["default", "pct", "hpaw", "tie1", "most"],
+                    help="the profile setting the sweep changes (make_profile)")
     a = ap.parse_args()
     import gen_random
     seeds = list(range(a.start, a.start + a.seeds))
@@ -98,7 +117,7 @@ def main():
     out = []
     for tag, make in fams:
         n = len(seeds) if not any(k in tag for k in ("5000", "6000", "9000")) else max(4, len(seeds) // 5)
-        out.append(run_family(tag, make, seeds[:n], a.one_pod_every))
+        out.append(run_family(tag, make, seeds[:n], a.one_pod_every, a.variant))
     print(json.dumps({"stress_parity": "ok", "families": out}))
 
 
