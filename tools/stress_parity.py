@@ -101,6 +101,7 @@ def main():
     ap.add_argument("--one-pod-every", type=int, default=4, help="also run every k-th cluster one pod at a time")
     ap.add_argument("--variant", default="default", choices=["default", "pct", "hpaw", "tie1", "most"],
                     help="the profile setting the sweep changes (make_profile)")
+    ap.add_argument("--long-runs", action="store_true", help="two families of long topology runs instead")
     a = ap.parse_args()
     import gen_random
     seeds = list(range(a.start, a.start + a.seeds))
@@ -114,6 +115,11 @@ def main():
         ("topology 1500 nodes", lambda s: gen_random.topo_cluster(s, n_nodes=1500, n_existing=600, n_pods=60)),
         ("topology 6000 nodes", lambda s: gen_random.topo_cluster(s, n_nodes=6000, n_existing=3000, n_pods=40)),
     ]
+    if a.long_runs:  # long k_tbatch runs: more in-run assumes between a pod and the pods it affects
+        fams = [("topology 200 nodes, 200 pods", lambda s: gen_random.topo_cluster(s, n_nodes=200, n_existing=150,
+                                                                                  n_pods=200)),
+                ("topology 1500 nodes, 300 pods", lambda s: gen_random.topo_cluster(s, n_nodes=1500, n_existing=900,
+                                                                                   n_pods=300))]
     out = []
     for tag, make in fams:
         n = len(seeds) if not any(k in tag for k in ("5000", "6000", "9000")) else max(4, len(seeds) // 5)
