@@ -49,6 +49,9 @@ def make_profile(variant):
         scores = [s for s in Profile.DEFAULT_SCORES if s[0] != "NodeResourcesLeastAllocated"]
         return Profile(scores=scores + [("NodeResourcesMostAllocated", 1), ("RequestedToCapacityRatio", 2),
                                         ("NodeResourceLimits", 1)])
+    if variant == "fit":  # config (b)'s profile: k_batch's helper-wave instantiation on random pods
+        return Profile(filters=["NodeResourcesFit"], scores=[("NodeResourcesLeastAllocated", 1),
+                                                             ("NodeResourcesBalancedAllocation", 1)])
     return Profile()
 
 
@@ -99,9 +102,10 @@ def main():
     ap.add_argument("--seeds", type=int, default=40)
     ap.add_argument("--start", type=int, default=1000, help="first seed (the test suite uses small seeds)")
     ap.add_argument("--one-pod-every", type=int, default=4, help="also run every k-th cluster one pod at a time")
-    ap.add_argument("--variant", default="default", choices=["default", "pct", "hpaw", "tie1", "most"],
+    ap.add_argument("--variant", default="default", choices=["default", "pct", "hpaw", "tie1", "most", "fit"],
                     help="the profile setting the sweep changes (make_profile)")
     ap.add_argument("--long-runs", action="store_true", help="two families of long topology runs instead")
+    ap.add_argument("--long-generic", action="store_true", help="two families of long generic batches instead")
     a = ap.parse_args()
     import gen_random
     seeds = list(range(a.start, a.start + a.seeds))
@@ -115,6 +119,11 @@ def main():
         ("topology 1500 nodes", lambda s: gen_random.topo_cluster(s, n_nodes=1500, n_existing=600, n_pods=60)),
         ("topology 6000 nodes", lambda s: gen_random.topo_cluster(s, n_nodes=6000, n_existing=3000, n_pods=40)),
     ]
+    if a.long_generic:  # batches longer than a short cycle: the persistent k_batch
+        fams = [("generic 700 nodes, 400 pods", lambda s: gen_random.cluster(s, n_nodes=700, n_existing=400,
+                                                                            n_pods=400)),
+                ("generic 5000 nodes, 300 pods", lambda s: gen_random.cluster(s, n_nodes=5000, n_existing=2000,
+                                                                             n_pods=300))]
     if a.long_runs:  # long k_tbatch runs: more in-run assumes between a pod and the pods it affects
         fams = [("topology 200 nodes, 200 pods", lambda s: gen_random.topo_cluster(s, n_nodes=200, n_existing=150,
                                                                                   n_pods=200)),
